@@ -1,0 +1,242 @@
+/*
+ * o3dx.h — C-ABI of libo3dx.so, the MI355X (gfx950) point-cloud hot path behind
+ * the open3dpypro drop-in (qinhy/Open3D-py-extension).
+ *
+ * The reference is pure Python; every hot-path call in it falls through to
+ * Open3D 0.19's C++ CPU kernels via pybind11.  Each entry point below replaces
+ * one of those calls; the replaced reference call site is cited per function.
+ * The Python binding (ctypes) lives in open3dpypro/_native.py; INTEGRATION.md
+ * shows the binding a maintainer would add.
+ *
+ * Conventions (all functions):
+ *   - Plain pointers and sizes only.  "dev" = device (HBM) pointer, "host" =
+ *     host pointer.  Points are (n,3) float32, row-major (AoS, 12 B / point).
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *     Work is enqueued on it; functions that return a host value (counts,
+ *     bounds, transforms) synchronise that stream before returning.
+ *   - The caller owns every buffer, including the scratch workspace
+ *     (`ws`, `ws_bytes`, from the matching *_workspace_bytes query, 256-B
+ *     aligned).  The library never allocates device memory, never frees
+ *     caller memory and keeps no pointer after return.
+ *   - Return 0 on success, a negative errno on failure:
+ *       O3DX_EINVAL  bad argument (mirrors Open3D's LogError -> RuntimeError)
+ *       O3DX_ENOMEM  workspace too small
+ *       O3DX_EIO     HIP runtime error
+ *       O3DX_ENOTSUP configuration outside this implementation's range
+ *     o3dx_last_error() returns the thread-local message of the last failure.
+ *   - Indices are int32 (Open3D uses int for point ids; n < 2^31).
+ */
+#ifndef O3DX_H
+#define O3DX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define O3DX_ABI_VERSION 1
+
+#define O3DX_OK 0
+#define O3DX_EIO (-5)
+#define O3DX_ENOMEM (-12)
+#define O3DX_EINVAL (-22)
+#define O3DX_ENOTSUP (-95)
+
+/* search modes of estimate_normals / knn search
+ * (KDTreeSearchParamKNN / Radius / Hybrid, reference PointCloud.py:68, test_mesh.py:18) */
+#define O3DX_SEARCH_KNN 0
+#define O3DX_SEARCH_RADIUS 1
+#define O3DX_SEARCH_HYBRID 2
+
+/* largest k served by the register top-k path (KNN k, HYBRID max_nn) */
+#define O3DX_MAX_KNN 64
+
+/* ICP reduction vector layout (o3dx_icp_accumulate):
+ *   [0..20]  JTJ upper triangle, row-major (6x6)
+ *   [21..26] JTr
+ *   [27]     sum r^2         (point-to-plane residuals)
+ *   [28]     correspondence count
+ *   [29]     sum d^2         (squared correspondence distances, for inlier_rmse)
+ *   [30..31] reserved (0) */
+#define O3DX_ICP_NSUMS 32
+
+/* ---------------------------------------------------------------- misc */
+int o3dx_abi_version(void);
+const char* o3dx_last_error(void);
+
+/* ---------------------------------------------------------------- AABB
+ * Replaces o3d.geometry.PointCloud.get_min_bound()/get_max_bound()
+ * (reference PointCloud.py:145-146, :340).
+ * minmax_host = {minx, miny, minz, maxx, maxy, maxz}; n == 0 gives zeros
+ * (Open3D returns a zero vector for an empty cloud).  Synchronises. */
+size_t o3dx_aabb_workspace_bytes(int64_t n);
+int o3dx_aabb(const float* xyz_dev, int64_t n, double* minmax_host,
+              void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- voxel
+ * Replaces o3d PointCloud.voxel_down_sample_and_trace(voxel_size, min_bound,
+ * max_bound, approximate_class=False) + idxmat.max(1) + _select_by_idx
+ * (reference PointCloud.py:338-341, :361-362, :185-204; processors.py:427-430).
+ *
+ * key(p) = floor((p - min_bound) / voxel_size) per axis, computed in float64
+ * exactly as Open3D does.  The representative of a voxel is the largest
+ * original index in it (= idxmat.max(1)).  Output is in ascending original
+ * index order (= _select_by_idx order):
+ *   rep_idx_dev[0..m)          representative indices, ascending     (cap n)
+ *   rep_xyz_dev[0..3m)         their coordinates (nullable)          (cap 3n)
+ *   voxel_of_point_dev[0..n)   output row of each input point (nullable)
+ *   cubic_id_dev[0..8m)        Open3D's (M,8) cubic-id matrix, -1 filled,
+ *                              row r = voxel of rep_idx[r] (nullable, cap 8n)
+ * min_bound_host / max_bound_host: NULL -> the cloud's AABB (device pass).
+ * Errors (RuntimeError in Python, as Open3D): voxel_size <= 0;
+ * voxel_size * INT_MAX < max extent ("voxel_size is too small.").
+ * Synchronises (m is returned on the host). */
+size_t o3dx_voxel_workspace_bytes(int64_t n);
+int o3dx_voxel_down_sample(const float* xyz_dev, int64_t n,
+                           const double* min_bound_host,
+                           const double* max_bound_host, double voxel_size,
+                           int32_t* rep_idx_dev, float* rep_xyz_dev,
+                           int64_t* m_host, int32_t* voxel_of_point_dev,
+                           int32_t* cubic_id_dev, void* ws, size_t ws_bytes,
+                           void* stream);
+
+/* ---------------------------------------------------------------- normals
+ * Replaces o3d PointCloud.estimate_normals(search_param,
+ * fast_normal_computation=True) (reference PointCloud.py:68-73, used by
+ * processors.py:243-249 CPUNormals): per point the neighbour set of
+ * KDTreeFlann::Search (KNN k incl. the point itself / RADIUS d^2 < r^2 /
+ * HYBRID nearest <= max_nn with d^2 < r^2), Open3D's raw-moment float64
+ * covariance (identity if < 3 neighbours), FastEigen3x3 smallest eigenvector,
+ * (0,0,1) if it is zero; if prior_normals_dev is given the result is flipped
+ * to agree with it (Open3D's has_normal branch).
+ * normals_out_dev: (n,3) float32.  KNN/HYBRID require k <= O3DX_MAX_KNN. */
+size_t o3dx_normals_workspace_bytes(int64_t n);
+int o3dx_estimate_normals(const float* xyz_dev, int64_t n, int mode, int knn,
+                          double radius, const float* prior_normals_dev,
+                          float* normals_out_dev, void* ws, size_t ws_bytes,
+                          void* stream);
+
+/* ---------------------------------------------------------------- kNN search
+ * Batched form of KDTreeFlann.search_knn_vector_3d / search_hybrid_vector_3d
+ * (reference PointCloud.py:148-163).  For each query q: up to K = knn (KNN)
+ * or max_nn (HYBRID) nearest points of `xyz`, sorted by squared distance
+ * (float64, computed as nanoflann does).  Outputs, row-major (nq, K):
+ *   idx_out_dev (-1 padded), d2_out_dev (nullable, +inf padded),
+ *   count_out_dev (nq). */
+size_t o3dx_knn_workspace_bytes(int64_t n);
+int o3dx_knn_search(const float* xyz_dev, int64_t n, const float* queries_dev,
+                    int64_t nq, int mode, int knn, double radius,
+                    int32_t* idx_out_dev, double* d2_out_dev,
+                    int32_t* count_out_dev, void* ws, size_t ws_bytes,
+                    void* stream);
+
+/* ---------------------------------------------------------------- RANSAC
+ * Replaces o3d PointCloud.segment_plane(distance_threshold, ransac_n,
+ * num_iterations, probability=0.99999999) (reference PointCloud.py:75-77,
+ * processors.py:637-638, seg_planes PointCloud.py:941-985).
+ *
+ * o3dx_ransac_samples: Open3D's RandomSampler — per iteration `ransac_n`
+ *   distinct indices, each mt19937(seed)() % n, duplicates re-drawn.  Host only.
+ * o3dx_segment_plane: hypotheses from `samples_host` (iters x ransac_n),
+ *   ComputeTrianglePlane (n==3) / GetPlaneFromPoints, exact inlier counts
+ *   (|n.p+d| < thr in float64), Open3D's sequential selection rule (fitness,
+ *   then Sigma|d|/sqrt(cnt), early break at log(1-p)/log(1-fitness^n)),
+ *   final inlier scan with the winning hypothesis and the least-squares refit.
+ *   inliers_out_dev: ascending indices (cap n); plane_host: {a,b,c,d}.
+ * Errors: probability not in (0,1], ransac_n < 3, n < ransac_n. */
+int o3dx_ransac_samples(int64_t n, int ransac_n, int num_iterations,
+                        uint64_t seed, int32_t* samples_host);
+size_t o3dx_segment_plane_workspace_bytes(int64_t n, int num_iterations);
+int o3dx_segment_plane(const float* xyz_dev, int64_t n,
+                       double distance_threshold, int ransac_n,
+                       int num_iterations, double probability,
+                       const int32_t* samples_host, double* plane_host,
+                       int32_t* inliers_out_dev, int64_t* n_inliers_host,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* Building blocks of o3dx_segment_plane, exposed for point-sharded multi-GPU
+ * use (counts/sums are all-reduced between the calls).
+ * o3dx_plane_from_points: host-only plane fit of `k` points (ComputeTrianglePlane
+ *   for k==3 else GetPlaneFromPoints); zero plane if degenerate.
+ * o3dx_plane_count: exact inlier count of each hypothesis (counts_host[h]).
+ * o3dx_plane_abs_sum: Sigma |n.p+d| over inliers for the hypotheses listed in
+ *   which_host (sums_host[j] for which_host[j]).
+ * o3dx_ransac_select: Open3D's sequential selection replay on host; returns the
+ *   winning hypothesis index (or -1). needs sums for count ties (NaN else).
+ * o3dx_plane_inliers: ascending indices with |n.p+d| < thr (float64).
+ * o3dx_plane_moments: sums over idx of {x,y,z} (pass 1, centroid NULL) or of
+ *   centred {xx,xy,xz,yy,yz,zz} (pass 2), float64, for GetPlaneFromPoints.
+ * o3dx_plane_from_moments: host-only GetPlaneFromPoints from those sums. */
+int o3dx_plane_from_points(const double* pts_host, int k, double* plane_host);
+size_t o3dx_plane_count_workspace_bytes(int64_t n, int num_hypotheses);
+int o3dx_plane_count(const float* xyz_dev, int64_t n, const double* planes_host,
+                     int num_hypotheses, double distance_threshold,
+                     int64_t* counts_host, void* ws, size_t ws_bytes,
+                     void* stream);
+int o3dx_plane_abs_sum(const float* xyz_dev, int64_t n,
+                       const double* planes_host, const int32_t* which_host,
+                       int num_which, double distance_threshold,
+                       double* sums_host, void* ws, size_t ws_bytes,
+                       void* stream);
+int o3dx_ransac_select(const int64_t* counts_host, const double* sums_host,
+                       const double* planes_host, int num_hypotheses,
+                       int64_t n, int ransac_n, double probability);
+int o3dx_plane_inliers(const float* xyz_dev, int64_t n, const double* plane_host,
+                       double distance_threshold, int32_t* idx_out_dev,
+                       int64_t* count_host, void* ws, size_t ws_bytes,
+                       void* stream);
+int o3dx_plane_moments(const float* xyz_dev, const int32_t* idx_dev,
+                       int64_t count, const double* centroid_host,
+                       double* sums_host, void* ws, size_t ws_bytes,
+                       void* stream);
+int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
+                            const double* centred_host, double* plane_host);
+
+/* ---------------------------------------------------------------- ICP
+ * Point-to-plane ICP (north-star op; absent from the reference — attached as
+ * PointCloud.registration_icp / Processors.ICP).  Semantics of Open3D's
+ * registration_icp + TransformationEstimationPointToPlane: correspondences =
+ * target nearest neighbour of T*src within max_correspondence_distance
+ * (d^2 < r^2), r = (vs - vt).nt, J = [vs x nt ; nt], solve JTJ x = -JTr,
+ * update = Rz(x2) Ry(x1) Rx(x0) | x[3..5], T <- update * T.
+ *
+ * o3dx_icp_target_build: builds the persistent target structure (spatial grid
+ *   of target points + normals) inside `target_ws`; desc_host (16 doubles)
+ *   receives its descriptor, to be passed back to o3dx_icp_accumulate.
+ * o3dx_icp_accumulate: one fused pass over the source: transform by T_host
+ *   (row-major 4x4, float64), 1-NN, residual/Jacobian, fixed-order float64
+ *   reduction into sums_host[O3DX_ICP_NSUMS].  corr_out_dev (nullable, 2*ns
+ *   int32 pairs (i,j)) + ncorr_host receive the correspondence set.
+ * o3dx_icp_solve_point_to_plane: host-only 6x6 LDLT solve of the summed
+ *   system -> update_host (4x4 row-major); returns 1 if solved, 0 if singular
+ *   (identity update, as Open3D).
+ * o3dx_registration_icp_point_to_plane: the whole Open3D loop on one device.
+ */
+size_t o3dx_icp_target_workspace_bytes(int64_t nt);
+int o3dx_icp_target_build(const float* tgt_dev, const float* tgt_normals_dev,
+                          int64_t nt, double max_correspondence_distance,
+                          void* target_ws, size_t target_ws_bytes,
+                          double* desc_host, void* stream);
+size_t o3dx_icp_accumulate_workspace_bytes(int64_t ns);
+int o3dx_icp_accumulate(const float* src_dev, int64_t ns,
+                        const void* target_ws, const double* desc_host,
+                        const double* T_host, double max_correspondence_distance,
+                        double* sums_host, int32_t* corr_out_dev,
+                        int64_t* ncorr_host, void* ws, size_t ws_bytes,
+                        void* stream);
+int o3dx_icp_solve_point_to_plane(const double* sums_host, double* update_host);
+int o3dx_registration_icp_point_to_plane(
+    const float* src_dev, int64_t ns, const float* tgt_dev,
+    const float* tgt_normals_dev, int64_t nt,
+    double max_correspondence_distance, const double* init_host,
+    int max_iteration, double relative_fitness, double relative_rmse,
+    double* T_out_host, double* fitness_host, double* inlier_rmse_host,
+    int32_t* corr_out_dev, int64_t* ncorr_host, void* target_ws,
+    size_t target_ws_bytes, void* ws, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* O3DX_H */

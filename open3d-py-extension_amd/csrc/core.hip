@@ -1,0 +1,268 @@
+// core.hip — error state, scans / flag compaction, AABB reduction.
+//
+// AABB replaces o3d PointCloud.get_min_bound/get_max_bound
+// (reference open3dpypro/PointCloud.py:145-146, :340).  HBM-bound: 12 B/point.
+#include <cstdarg>
+
+#include "common.hpp"
+
+namespace o3dx {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+// ------------------------------------------------------------------ scans
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kBlock * kScanItems;  // 4096
+
+__global__ void __launch_bounds__(kBlock) k_tile_sums_i32(const int32_t* __restrict__ in, int64_t n,
+                                                          int32_t* __restrict__ part) {
+  __shared__ int sh[kBlock / 64 + 1];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = base + j;
+    s += (i < n) ? in[i] : 0;
+  }
+  int tot;
+  block_excl_scan<kBlock>(s, sh, &tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kBlock) k_tile_sums_u8(const uint8_t* __restrict__ f, int64_t n,
+                                                         int32_t* __restrict__ part) {
+  __shared__ int sh[kBlock / 64 + 1];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int s = 0;
+  if (base + kScanItems <= n) {
+    uint4 v = *reinterpret_cast<const uint4*>(f + base);
+    s = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // flags are 0/1 bytes
+  } else {
+    for (int j = 0; j < kScanItems; ++j) {
+      int64_t i = base + j;
+      s += (i < n) ? (f[i] != 0) : 0;
+    }
+  }
+  int tot;
+  block_excl_scan<kBlock>(s, sh, &tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// Single-block exclusive scan of the tile partials (in place); total -> *total.
+__global__ void __launch_bounds__(1024) k_scan_partials(int32_t* part, int64_t m, int32_t* total_i32,
+                                                        int64_t* total_i64) {
+  __shared__ int sh[1024 / 64 + 1];
+  int carry = 0;
+  for (int64_t b = 0; b < m; b += 1024) {
+    int64_t i = b + threadIdx.x;
+    int v = (i < m) ? part[i] : 0;
+    int tot;
+    int ex = block_excl_scan<1024>(v, sh, &tot);
+    if (i < m) part[i] = ex + carry;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    if (total_i32) *total_i32 = carry;
+    if (total_i64) *total_i64 = carry;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_tile_scan_i32(const int32_t* __restrict__ in, int64_t n,
+                                                          const int32_t* __restrict__ part,
+                                                          int32_t* __restrict__ out) {
+  __shared__ int sh[kBlock / 64 + 1];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int v[kScanItems];
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = base + j;
+    v[j] = (i < n) ? in[i] : 0;
+    s += v[j];
+  }
+  int tot;
+  int ex = block_excl_scan<kBlock>(s, sh, &tot) + part[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = base + j;
+    if (i < n) out[i] = ex;
+    ex += v[j];
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_tile_compact_u8(const uint8_t* __restrict__ f, int64_t n,
+                                                            const int32_t* __restrict__ part,
+                                                            int32_t* __restrict__ idx_out,
+                                                            int32_t* __restrict__ pos_out) {
+  __shared__ int sh[kBlock / 64 + 1];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  uint8_t v[kScanItems];
+  if (base + kScanItems <= n) {
+    uint4 q = *reinterpret_cast<const uint4*>(f + base);
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(&q);
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) v[j] = b[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      int64_t i = base + j;
+      v[j] = (i < n) ? f[i] : 0;
+    }
+  }
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) s += v[j] != 0;
+  int tot;
+  int ex = block_excl_scan<kBlock>(s, sh, &tot) + part[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = base + j;
+    if (i < n) {
+      if (pos_out) pos_out[i] = ex;
+      if (v[j]) idx_out[ex++] = (int32_t)i;
+    }
+  }
+}
+
+size_t scan_workspace_ints(int64_t n) { return (size_t)((n + kScanTile - 1) / kScanTile) + 64; }
+
+int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp, hipStream_t s) {
+  int64_t tiles = (n + kScanTile - 1) / kScanTile;
+  if (tiles == 0) {
+    O3DX_HIP(hipMemsetAsync(out, 0, sizeof(int32_t), s));
+    return 0;
+  }
+  hipLaunchKernelGGL(k_tile_sums_i32, dim3((unsigned)tiles), dim3(kBlock), 0, s, in, n, tmp);
+  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, tmp, tiles, out + n, (int64_t*)nullptr);
+  hipLaunchKernelGGL(k_tile_scan_i32, dim3((unsigned)tiles), dim3(kBlock), 0, s, in, n, tmp, out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+size_t compact_workspace_ints(int64_t n) { return scan_workspace_ints(n); }
+
+int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* pos_out,
+                  int64_t* count_dev, int32_t* tmp, hipStream_t s) {
+  int64_t tiles = (n + kScanTile - 1) / kScanTile;
+  if (tiles == 0) {
+    O3DX_HIP(hipMemsetAsync(count_dev, 0, sizeof(int64_t), s));
+    return 0;
+  }
+  hipLaunchKernelGGL(k_tile_sums_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp);
+  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, tmp, tiles, (int32_t*)nullptr, count_dev);
+  hipLaunchKernelGGL(k_tile_compact_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp, idx_out,
+                     pos_out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------- AABB
+constexpr int kAabbBlocks = 1024;
+
+struct P3 {
+  float x, y, z;
+};
+
+__global__ void __launch_bounds__(kBlock) k_aabb_partial(const float* __restrict__ xyz, int64_t n,
+                                                         float* __restrict__ part) {
+  float mn[3] = {INFINITY, INFINITY, INFINITY};
+  float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    P3 q = p[i];
+    mn[0] = fminf(mn[0], q.x);
+    mn[1] = fminf(mn[1], q.y);
+    mn[2] = fminf(mn[2], q.z);
+    mx[0] = fmaxf(mx[0], q.x);
+    mx[1] = fmaxf(mx[1], q.y);
+    mx[2] = fmaxf(mx[2], q.z);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+    }
+  __shared__ float sh[kBlock / 64][6];
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0)
+    for (int a = 0; a < 3; ++a) {
+      sh[w][a] = mn[a];
+      sh[w][3 + a] = mx[a];
+    }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float r = sh[0][threadIdx.x];
+    for (int k = 1; k < kBlock / 64; ++k)
+      r = threadIdx.x < 3 ? fminf(r, sh[k][threadIdx.x]) : fmaxf(r, sh[k][threadIdx.x]);
+    part[blockIdx.x * 6 + threadIdx.x] = r;
+  }
+}
+
+__global__ void k_aabb_final(const float* __restrict__ part, int nb, int64_t n, double* __restrict__ mm) {
+  int a = threadIdx.x;
+  if (a >= 6) return;
+  if (n == 0) {
+    mm[a] = 0.0;
+    return;
+  }
+  float r = part[a];
+  for (int b = 1; b < nb; ++b) r = a < 3 ? fminf(r, part[b * 6 + a]) : fmaxf(r, part[b * 6 + a]);
+  mm[a] = (double)r;
+}
+
+size_t aabb_ws_bytes(int64_t) { return Arena::align(kAabbBlocks * 6 * sizeof(float)) + 256; }
+
+int aabb_device(const float* xyz, int64_t n, double* mm_dev, void* ws, hipStream_t s) {
+  float* part = reinterpret_cast<float*>(ws);
+  int nb = (int)std::min<int64_t>(kAabbBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL(k_aabb_partial, dim3(nb), dim3(kBlock), 0, s, xyz, n, part);
+  hipLaunchKernelGGL(k_aabb_final, dim3(1), dim3(64), 0, s, part, nb, n, mm_dev);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace o3dx
+
+using namespace o3dx;
+
+extern "C" int o3dx_abi_version(void) { return O3DX_ABI_VERSION; }
+
+extern "C" const char* o3dx_last_error(void) { return g_err.c_str(); }
+
+extern "C" size_t o3dx_aabb_workspace_bytes(int64_t n) { return aabb_ws_bytes(n) + 256; }
+
+extern "C" int o3dx_aabb(const float* xyz, int64_t n, double* minmax_host, void* ws, size_t ws_bytes,
+                         void* stream) {
+  if (n < 0 || (n > 0 && !xyz) || !minmax_host) return fail(O3DX_EINVAL, "o3dx_aabb: bad arguments");
+  if (!ws || ws_bytes < o3dx_aabb_workspace_bytes(n))
+    return fail(O3DX_ENOMEM, "o3dx_aabb: workspace too small");
+  hipStream_t s = as_stream(stream);
+  char* w = (char*)ws;
+  double* mm = reinterpret_cast<double*>(w + aabb_ws_bytes(n));
+  O3DX_TRY(aabb_device(xyz, n, mm, w, s));
+  O3DX_HIP(hipMemcpyAsync(minmax_host, mm, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  return 0;
+}

@@ -1,0 +1,370 @@
+// icp.hip — point-to-plane ICP (north-star op; no symbol in the reference,
+// attached as PointCloud.registration_icp / Processors.ICP).
+//
+// Semantics restated from Open3D pipelines/registration/Registration.cpp
+// (RegistrationICP, GetRegistrationResultAndCorrespondences with
+// SearchHybrid(p, max_corr, 1)), TransformationEstimation.cpp
+// (PointToPlane::ComputeTransformation), utility/Eigen.cpp (ComputeJTJandJTr,
+// SolveJacobianSystemAndObtainExtrinsicMatrix, TransformVector6dToMatrix4d).
+//
+// One fused pass per iteration: transform the float32 source by the float64
+// cumulative T, nearest target within max_corr (target grid), residual
+// r = (vs - vt).nt, J = [vs x nt ; nt], and a fixed-order float64 reduction
+// of the 29 moments (21 JTJ + 6 JTr + r^2 + count, plus sum d^2) — per-lane,
+// wave xor-tree, block, then block partials in block order.  The 6x6 solve
+// and the loop stay on the host (float64 LDLT with diagonal pivoting).
+#include <vector>
+
+#include "grid.hpp"
+
+namespace o3dx {
+
+constexpr int kIcpBlocks = 1024;
+constexpr int kNS = O3DX_ICP_NSUMS;
+
+struct Mat4 {
+  double m[16];
+};
+
+__global__ void __launch_bounds__(kBlock) k_icp_accumulate(const float* __restrict__ src, int64_t ns, GridView g,
+                                                           const float4* __restrict__ tnorm, Mat4 T, double radius,
+                                                           double* __restrict__ partial, int32_t* __restrict__ cj) {
+  __shared__ double sh[kBlock / 64];
+  double acc[30];
+#pragma unroll
+  for (int k = 0; k < 30; ++k) acc[k] = 0.0;
+  const double* t = T.m;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
+    const double x = src[3 * i], y = src[3 * i + 1], z = src[3 * i + 2];
+    // Eigen 4x4 * (x,y,z,1): ((T0 x + T1 y) + T2 z) + T3 per row
+    const double px = ((t[0] * x + t[1] * y) + t[2] * z) + t[3];
+    const double py = ((t[4] * x + t[5] * y) + t[6] * z) + t[7];
+    const double pz = ((t[8] * x + t[9] * y) + t[10] * z) + t[11];
+    double d2;
+    int pos;
+    const int j = nn_search_dev(g, px, py, pz, radius, &d2, &pos);
+    if (cj) cj[i] = j;
+    if (j < 0) continue;
+    const float4 vt = g.pts[pos];
+    const float4 nt = tnorm[pos];
+    const double nx = nt.x, ny = nt.y, nz = nt.z;
+    const double r = ((px - (double)vt.x) * nx + (py - (double)vt.y) * ny) + (pz - (double)vt.z) * nz;
+    double J[6];
+    J[0] = py * nz - pz * ny;
+    J[1] = pz * nx - px * nz;
+    J[2] = px * ny - py * nx;
+    J[3] = nx;
+    J[4] = ny;
+    J[5] = nz;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = a; b < 6; ++b) acc[k++] += J[a] * J[b];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
+    acc[27] += r * r;
+    acc[28] += 1.0;
+    acc[29] += d2;
+  }
+#pragma unroll
+  for (int k = 0; k < 30; ++k) {
+    double v = block_sum_f64<kBlock>(acc[k], sh);
+    if (threadIdx.x == 0) partial[(int64_t)blockIdx.x * kNS + k] = v;
+  }
+  if (threadIdx.x < kNS - 30) partial[(int64_t)blockIdx.x * kNS + 30 + threadIdx.x] = 0.0;
+}
+
+__global__ void k_icp_final(const double* __restrict__ partial, int nb, double* __restrict__ out) {
+  int k = threadIdx.x;
+  if (k >= kNS) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * kNS + k];
+  out[k] = s;
+}
+
+__global__ void __launch_bounds__(kBlock) k_corr_flags(const int32_t* __restrict__ cj, int64_t ns,
+                                                       uint8_t* __restrict__ flags) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x)
+    flags[i] = cj[i] >= 0 ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_corr_pairs(const int32_t* __restrict__ cj, const int32_t* __restrict__ src_idx,
+                                                       int64_t m, int32_t* __restrict__ corr) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+    int32_t i = src_idx[k];
+    corr[2 * k] = i;
+    corr[2 * k + 1] = cj[i];
+  }
+}
+
+// ------------------------------------------------------------ host linear algebra
+static bool ldlt_solve6(const double A_in[36], const double b_in[6], double x[6]) {
+  double A[36];
+  std::memcpy(A, A_in, sizeof(A));
+  int perm[6] = {0, 1, 2, 3, 4, 5};
+  const int n = 6;
+  for (int k = 0; k < n; ++k) {
+    int piv = k;
+    double best = std::fabs(A[k * n + k]);
+    for (int i = k + 1; i < n; ++i)
+      if (std::fabs(A[i * n + i]) > best) {
+        best = std::fabs(A[i * n + i]);
+        piv = i;
+      }
+    if (piv != k) {
+      for (int j = 0; j < n; ++j) std::swap(A[k * n + j], A[piv * n + j]);
+      for (int i = 0; i < n; ++i) std::swap(A[i * n + k], A[i * n + piv]);
+      std::swap(perm[k], perm[piv]);
+    }
+    const double dk = A[k * n + k];
+    double col[6];
+    for (int i = k + 1; i < n; ++i) col[i] = A[i * n + k];
+    for (int i = k + 1; i < n; ++i)
+      for (int j = k + 1; j < n; ++j) A[i * n + j] -= dk != 0 ? col[i] * col[j] / dk : 0.0;
+    for (int i = k + 1; i < n; ++i) A[i * n + k] = dk != 0 ? col[i] / dk : 0.0;
+  }
+  double y[6];
+  for (int i = 0; i < n; ++i) y[i] = b_in[perm[i]];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < i; ++j) y[i] -= A[i * n + j] * y[j];
+  const double tiny = std::numeric_limits<double>::min();
+  for (int i = 0; i < n; ++i) y[i] = std::fabs(A[i * n + i]) > tiny ? y[i] / A[i * n + i] : 0.0;
+  for (int i = n - 1; i >= 0; --i)
+    for (int j = i + 1; j < n; ++j) y[i] -= A[j * n + i] * y[j];
+  for (int i = 0; i < n; ++i) x[perm[i]] = y[i];
+  for (int i = 0; i < n; ++i)
+    if (!std::isfinite(x[i])) return false;
+  return true;
+}
+
+// TransformVector6dToMatrix4d: R = Rz(x2) Ry(x1) Rx(x0), t = x[3..5]
+static void vec6_to_mat4(const double x[6], double T[16]) {
+  const double ca = std::cos(x[0]), sa = std::sin(x[0]);
+  const double cb = std::cos(x[1]), sb = std::sin(x[1]);
+  const double cg = std::cos(x[2]), sg = std::sin(x[2]);
+  const double Rz[9] = {cg, -sg, 0, sg, cg, 0, 0, 0, 1};
+  const double Ry[9] = {cb, 0, sb, 0, 1, 0, -sb, 0, cb};
+  const double Rx[9] = {1, 0, 0, 0, ca, -sa, 0, sa, ca};
+  double A[9], R[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      A[i * 3 + j] = (Rz[i * 3] * Ry[j] + Rz[i * 3 + 1] * Ry[3 + j]) + Rz[i * 3 + 2] * Ry[6 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[i * 3 + j] = (A[i * 3] * Rx[j] + A[i * 3 + 1] * Rx[3 + j]) + A[i * 3 + 2] * Rx[6 + j];
+  for (int i = 0; i < 16; ++i) T[i] = 0;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) T[i * 4 + j] = R[i * 3 + j];
+    T[i * 4 + 3] = x[3 + i];
+  }
+  T[15] = 1;
+}
+
+static void mat4_mul(const double* A, const double* B, double* C) {
+  double t[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      t[i * 4 + j] =
+          ((A[i * 4] * B[j] + A[i * 4 + 1] * B[4 + j]) + A[i * 4 + 2] * B[8 + j]) + A[i * 4 + 3] * B[12 + j];
+  std::memcpy(C, t, sizeof(t));
+}
+
+static int solve_update(const double* sums, double* upd) {
+  double JTJ[36], mb[6], x[6];
+  int t = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int b = a; b < 6; ++b) {
+      JTJ[a * 6 + b] = sums[t];
+      JTJ[b * 6 + a] = sums[t];
+      ++t;
+    }
+  for (int a = 0; a < 6; ++a) mb[a] = -sums[21 + a];
+  if (sums[28] <= 0.0 || !ldlt_solve6(JTJ, mb, x)) {
+    for (int a = 0; a < 16; ++a) upd[a] = (a % 5 == 0) ? 1.0 : 0.0;
+    return 0;
+  }
+  vec6_to_mat4(x, upd);
+  return 1;
+}
+
+// ------------------------------------------------------------ descriptors
+constexpr double kDescMagic = 4242.0;
+
+static void desc_pack(const GridBuild& G, const void* base, const float4* normals, double* d) {
+  const GridView& g = G.view;
+  d[0] = g.ox; d[1] = g.oy; d[2] = g.oz; d[3] = g.h; d[4] = g.inv_h; d[5] = g.slack;
+  d[6] = g.nx; d[7] = g.ny; d[8] = g.nz; d[9] = (double)g.n;
+  d[10] = (double)((const char*)G.pts - (const char*)base);
+  d[11] = (double)((const char*)G.start - (const char*)base);
+  d[12] = (double)((const char*)normals - (const char*)base);
+  d[13] = kDescMagic;
+  d[14] = d[15] = 0;
+}
+
+static bool desc_unpack(const double* d, const void* base, GridView* g, const float4** normals) {
+  if (!d || d[13] != kDescMagic) return false;
+  g->ox = (float)d[0]; g->oy = (float)d[1]; g->oz = (float)d[2]; g->h = (float)d[3]; g->inv_h = (float)d[4];
+  g->slack = (float)d[5];
+  g->nx = (int)d[6]; g->ny = (int)d[7]; g->nz = (int)d[8]; g->n = (int64_t)d[9];
+  g->pts = (const float4*)((const char*)base + (int64_t)d[10]);
+  g->start = (const int32_t*)((const char*)base + (int64_t)d[11]);
+  *normals = (const float4*)((const char*)base + (int64_t)d[12]);
+  return true;
+}
+
+struct AccWs {
+  double* partial;
+  double* sums;
+  int32_t* cj;
+  uint8_t* flags;
+  int32_t* src_idx;
+  int32_t* scan_tmp;
+  int64_t* cnt;
+};
+
+static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
+  w->partial = ar.take<double>((size_t)kIcpBlocks * kNS);
+  w->sums = ar.take<double>(kNS);
+  w->cj = ar.take<int32_t>(ns);
+  w->flags = ar.take<uint8_t>(ns + 16);
+  w->src_idx = ar.take<int32_t>(ns);
+  w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(ns));
+  w->cnt = ar.take<int64_t>(2);
+  return ar.used;
+}
+
+static int accumulate(const float* src, int64_t ns, const GridView& g, const float4* tn, const double* T, double radius,
+                      AccWs& w, hipStream_t s, double* sums_host, int32_t* corr_out, int64_t* ncorr) {
+  Mat4 M;
+  std::memcpy(M.m, T, sizeof(M.m));
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kIcpBlocks, (ns + kBlock - 1) / kBlock));
+  const bool want_corr = corr_out != nullptr;
+  if (ns > 0)
+    hipLaunchKernelGGL(k_icp_accumulate, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, radius, w.partial,
+                       want_corr ? w.cj : (int32_t*)nullptr);
+  else
+    O3DX_HIP(hipMemsetAsync(w.partial, 0, kNS * sizeof(double), s));
+  hipLaunchKernelGGL(k_icp_final, dim3(1), dim3(64), 0, s, w.partial, ns > 0 ? nb : 1, w.sums);
+  O3DX_HIP(hipMemcpyAsync(sums_host, w.sums, kNS * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (want_corr && ns > 0) {
+    hipLaunchKernelGGL(k_corr_flags, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, ns, w.flags);
+    O3DX_TRY(compact_flags(w.flags, ns, w.src_idx, nullptr, w.cnt, w.scan_tmp, s));
+    int64_t m = 0;
+    O3DX_HIP(hipMemcpyAsync(&m, w.cnt, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    O3DX_HIP(hipStreamSynchronize(s));
+    if (m > 0)
+      hipLaunchKernelGGL(k_corr_pairs, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, w.src_idx, m,
+                         corr_out);
+    if (ncorr) *ncorr = m;
+  } else if (ncorr) {
+    *ncorr = -1;
+  }
+  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_HIP(hipGetLastError());
+  if (ncorr && !want_corr) *ncorr = (int64_t)sums_host[28];
+  return 0;
+}
+
+// grid occupancy / minimum cell for the 1-NN-within-radius search
+static double icp_min_h(double max_corr) { return max_corr / 8.0; }
+
+}  // namespace o3dx
+
+using namespace o3dx;
+
+extern "C" size_t o3dx_icp_target_workspace_bytes(int64_t nt) { return grid_ws_bytes(nt) + 1024; }
+
+extern "C" int o3dx_icp_target_build(const float* tgt, const float* tgt_normals, int64_t nt, double max_corr,
+                                     void* target_ws, size_t target_ws_bytes, double* desc, void* stream) {
+  if (nt < 0 || (nt > 0 && (!tgt || !tgt_normals)) || !desc) return fail(O3DX_EINVAL, "o3dx_icp_target_build: bad args");
+  if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  if (!target_ws || target_ws_bytes < o3dx_icp_target_workspace_bytes(nt))
+    return fail(O3DX_ENOMEM, "icp target workspace too small");
+  GridBuild G;
+  O3DX_TRY(grid_build(tgt, nt, 2.0, icp_min_h(max_corr), target_ws, target_ws_bytes, as_stream(stream), &G, nullptr,
+                      tgt_normals));
+  desc_pack(G, target_ws, G.extra, desc);
+  return 0;
+}
+
+extern "C" size_t o3dx_icp_accumulate_workspace_bytes(int64_t ns) {
+  Arena ar(nullptr, 0);
+  AccWs w;
+  return acc_carve(ar, std::max<int64_t>(ns, 1), &w) + 1024;
+}
+
+extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, const void* target_ws, const double* desc,
+                                   const double* T, double max_corr, double* sums, int32_t* corr_out, int64_t* ncorr,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  if (ns < 0 || (ns > 0 && !src) || !target_ws || !T || !sums) return fail(O3DX_EINVAL, "o3dx_icp_accumulate: bad args");
+  GridView g;
+  const float4* tn;
+  if (!desc_unpack(desc, target_ws, &g, &tn)) return fail(O3DX_EINVAL, "invalid ICP target descriptor");
+  if (!ws || ws_bytes < o3dx_icp_accumulate_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
+  Arena ar(ws, ws_bytes);
+  AccWs w;
+  acc_carve(ar, std::max<int64_t>(ns, 1), &w);
+  return accumulate(src, ns, g, tn, T, max_corr, w, as_stream(stream), sums, corr_out, ncorr);
+}
+
+extern "C" int o3dx_icp_solve_point_to_plane(const double* sums, double* upd) {
+  if (!sums || !upd) return fail(O3DX_EINVAL, "o3dx_icp_solve_point_to_plane: bad args");
+  return solve_update(sums, upd);
+}
+
+extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns, const float* tgt,
+                                                    const float* tgt_normals, int64_t nt, double max_corr,
+                                                    const double* init, int max_iteration, double rel_fit,
+                                                    double rel_rmse, double* T_out, double* fitness, double* rmse,
+                                                    int32_t* corr_out, int64_t* ncorr, void* target_ws,
+                                                    size_t target_ws_bytes, void* ws, size_t ws_bytes, void* stream) {
+  if (!T_out || !fitness || !rmse) return fail(O3DX_EINVAL, "registration_icp: bad args");
+  if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  hipStream_t s = as_stream(stream);
+  double desc[16];
+  O3DX_TRY(o3dx_icp_target_build(tgt, tgt_normals, nt, max_corr, target_ws, target_ws_bytes, desc, stream));
+  GridView g;
+  const float4* tn;
+  desc_unpack(desc, target_ws, &g, &tn);
+  if (!ws || ws_bytes < o3dx_icp_accumulate_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
+  Arena ar(ws, ws_bytes);
+  AccWs w;
+  acc_carve(ar, std::max<int64_t>(ns, 1), &w);
+  double T[16];
+  if (init) std::memcpy(T, init, sizeof(T));
+  else
+    for (int a = 0; a < 16; ++a) T[a] = (a % 5 == 0) ? 1.0 : 0.0;
+  double sums[kNS];
+  auto metrics = [&](const double* sm, double& fit, double& rm) {
+    double c = sm[28];
+    if (c <= 0 || ns == 0) {
+      fit = 0;
+      rm = 0;
+    } else {
+      fit = c / (double)ns;
+      rm = std::sqrt(sm[29] / c);
+    }
+  };
+  O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, nullptr, nullptr));
+  double fit, rm;
+  metrics(sums, fit, rm);
+  for (int it = 0; it < max_iteration; ++it) {
+    double upd[16];
+    solve_update(sums, upd);
+    mat4_mul(upd, T, T);
+    const double pf = fit, pr = rm;
+    const bool last = (it + 1 == max_iteration);
+    O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, last ? corr_out : nullptr, last ? ncorr : nullptr));
+    metrics(sums, fit, rm);
+    if (std::fabs(pf - fit) < rel_fit && std::fabs(pr - rm) < rel_rmse) {
+      if (!last && corr_out) O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
+      break;
+    }
+  }
+  if (max_iteration <= 0 && corr_out) O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
+  std::memcpy(T_out, T, sizeof(T));
+  *fitness = fit;
+  *rmse = rm;
+  if (!corr_out && ncorr) *ncorr = (int64_t)sums[28];
+  return 0;
+}

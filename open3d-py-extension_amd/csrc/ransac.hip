@@ -1,0 +1,628 @@
+// ransac.hip — segment_plane (RANSAC) with Open3D semantics.
+//
+// Replaces o3d PointCloud.segment_plane(distance_threshold, ransac_n,
+// num_iterations, probability) (reference open3dpypro/PointCloud.py:75-77,
+// processors.py:637-638 PlaneDetection.cpu_model, seg_planes :941-985).
+// Restated from Open3D geometry/PointCloudSegmentation.cpp (SegmentPlane,
+// EvaluateRANSACBasedOnDistance, GetPlaneFromPoints, RandomSampler) and
+// TriangleMesh::ComputeTrianglePlane.
+//
+// GPU design: every hypothesis is scored against every point in ONE sweep
+// (hypotheses are independent; Open3D's sequential selection with early break
+// is replayed on the host afterwards, which cannot change any score).  Each
+// lane holds 4 points in registers; plane coefficients are wave-uniform
+// (scalar loads); a float32 FMA distance with a per-hypothesis error band
+// decides almost every point, lanes inside the band are re-decided in float64
+// exactly as Open3D evaluates |(a x + c z) + (b y + d)| < thr; inlier counts
+// are ballot-popcounts into LDS.  Sigma|d| (only needed to break fitness ties)
+// is computed exactly in float64 for the tied hypotheses only.
+#include <random>
+#include <vector>
+
+#include "common.hpp"
+
+namespace o3dx {
+
+constexpr int kPts = 4;
+constexpr int kHChunk = 1024;
+constexpr int kCountBlocksMax = 1024;
+
+struct P3 {
+  float x, y, z;
+};
+
+__device__ __forceinline__ double plane_dist64(const double* pl, double x, double y, double z) {
+  // Eigen Vector4d dot packet order: (a*x + c*z) + (b*y + d*1)
+  double ax = pl[0] * x, by = pl[1] * y, cz = pl[2] * z, dw = pl[3] * 1.0;
+  return fabs((ax + cz) + (by + dw));
+}
+
+__global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict__ xyz, int64_t n,
+                                                        const float4* __restrict__ pl32,
+                                                        const float2* __restrict__ band,
+                                                        const double* __restrict__ pl64, int H, int h0, int hc,
+                                                        double thr, int32_t* __restrict__ partial) {
+  __shared__ int cnt[kHChunk];
+  for (int h = threadIdx.x; h < hc; h += kBlock) cnt[h] = 0;
+  __syncthreads();
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  const int64_t tile = (int64_t)kBlock * kPts;
+  for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {
+    float px[kPts], py[kPts], pz[kPts];
+    bool ok[kPts];
+#pragma unroll
+    for (int j = 0; j < kPts; ++j) {
+      int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+      ok[j] = i < n;
+      P3 q = ok[j] ? p[i] : P3{0.f, 0.f, 0.f};
+      px[j] = q.x;
+      py[j] = q.y;
+      pz[j] = q.z;
+    }
+    for (int h = 0; h < hc; ++h) {
+      const float4 P = pl32[h0 + h];
+      const float2 B = band[h0 + h];
+      int wc = 0;
+#pragma unroll
+      for (int j = 0; j < kPts; ++j) {
+        const float d = fabsf(fmaf(P.x, px[j], fmaf(P.y, py[j], fmaf(P.z, pz[j], P.w))));
+        const bool in = ok[j] && d < B.x;
+        const bool amb = ok[j] && !in && d < B.y;
+        wc += __popcll(__ballot(in));
+        if (__ballot(amb)) {
+          bool ex = false;
+          if (amb) ex = plane_dist64(pl64 + 4 * (h0 + h), px[j], py[j], pz[j]) < thr;
+          wc += __popcll(__ballot(ex));
+        }
+      }
+      if (lane_id() == 0 && wc) atomicAdd(&cnt[h], wc);
+    }
+  }
+  __syncthreads();
+  for (int h = threadIdx.x; h < hc; h += kBlock) partial[(int64_t)blockIdx.x * H + h0 + h] = cnt[h];
+}
+
+__global__ void k_plane_count_reduce(const int32_t* __restrict__ partial, int nb, int H,
+                                     const uint8_t* __restrict__ degenerate, int64_t* __restrict__ counts) {
+  int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  int64_t s = 0;
+  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * H + h];
+  counts[h] = degenerate[h] ? -1 : s;
+}
+
+constexpr int kSumBlocksX = 64;
+
+__global__ void __launch_bounds__(kBlock) k_plane_abs_sum(const float* __restrict__ xyz, int64_t n,
+                                                          const double* __restrict__ pl64, double thr,
+                                                          double* __restrict__ partial) {
+  __shared__ double sh[kBlock / 64];
+  const double* pl = pl64 + 4 * blockIdx.y;
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    P3 q = p[i];
+    double d = plane_dist64(pl, q.x, q.y, q.z);
+    if (d < thr) acc += d;
+  }
+  double r = block_sum_f64<kBlock>(acc, sh);
+  if (threadIdx.x == 0) partial[blockIdx.y * gridDim.x + blockIdx.x] = r;
+}
+
+__global__ void __launch_bounds__(kBlock) k_plane_flags(const float* __restrict__ xyz, int64_t n, double a, double b,
+                                                        double c, double d, double thr, uint8_t* __restrict__ flags) {
+  const double pl[4] = {a, b, c, d};
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    P3 q = p[i];
+    flags[i] = plane_dist64(pl, q.x, q.y, q.z) < thr ? 1 : 0;
+  }
+}
+
+constexpr int kMomBlocks = 256;
+
+// pass 1 (centroid == nullptr): {x, y, z}; pass 2: centred {xx, xy, xz, yy, yz, zz}
+__global__ void __launch_bounds__(kBlock) k_plane_moments(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
+                                                          int64_t m, double cx, double cy, double cz, int pass2,
+                                                          double* __restrict__ partial) {
+  __shared__ double sh[kBlock / 64];
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    int64_t i = idx ? idx[j] : j;
+    double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    if (!pass2) {
+      acc[0] += x;
+      acc[1] += y;
+      acc[2] += z;
+    } else {
+      double r0 = x - cx, r1 = y - cy, r2 = z - cz;
+      acc[0] += r0 * r0;
+      acc[1] += r0 * r1;
+      acc[2] += r0 * r2;
+      acc[3] += r1 * r1;
+      acc[4] += r1 * r2;
+      acc[5] += r2 * r2;
+    }
+  }
+  for (int k = 0; k < 6; ++k) {
+    double r = block_sum_f64<kBlock>(acc[k], sh);
+    if (threadIdx.x == 0) partial[blockIdx.x * 6 + k] = r;
+  }
+}
+
+__global__ void k_sum_partials(const double* __restrict__ partial, int nb, int width, double* __restrict__ out) {
+  int k = threadIdx.x;
+  if (k >= width) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += partial[b * width + k];
+  out[k] = s;
+}
+
+__global__ void k_gather_samples(const float* __restrict__ xyz, const int32_t* __restrict__ idx, int64_t m,
+                                 float* __restrict__ out) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  int64_t i = idx[j];
+  out[3 * j] = xyz[3 * i];
+  out[3 * j + 1] = xyz[3 * i + 1];
+  out[3 * j + 2] = xyz[3 * i + 2];
+}
+
+// --------------------------------------------------------------- host math
+static inline void hcross(const double u[3], const double v[3], double o[3]) {
+  o[0] = u[1] * v[2] - u[2] * v[1];
+  o[1] = u[2] * v[0] - u[0] * v[2];
+  o[2] = u[0] * v[1] - u[1] * v[0];
+}
+static inline double hdot(const double u[3], const double v[3]) { return (u[0] * v[0] + u[1] * v[1]) + u[2] * v[2]; }
+
+static void plane_from_centred(const double c[3], const double mo[6], double pl[4]) {
+  const double xx = mo[0], xy = mo[1], xz = mo[2], yy = mo[3], yz = mo[4], zz = mo[5];
+  double det_x = yy * zz - yz * yz, det_y = xx * zz - xz * xz, det_z = xx * yy - xy * xy;
+  double abc[3];
+  if (det_x > det_y && det_x > det_z) {
+    abc[0] = det_x; abc[1] = xz * yz - xy * zz; abc[2] = xy * yz - xz * yy;
+  } else if (det_y > det_z) {
+    abc[0] = xz * yz - xy * zz; abc[1] = det_y; abc[2] = xy * xz - yz * xx;
+  } else {
+    abc[0] = xy * yz - xz * yy; abc[1] = xy * xz - yz * xx; abc[2] = det_z;
+  }
+  double norm = std::sqrt(hdot(abc, abc));
+  if (norm == 0) {
+    pl[0] = pl[1] = pl[2] = pl[3] = 0;
+    return;
+  }
+  for (int a = 0; a < 3; ++a) abc[a] /= norm;
+  pl[0] = abc[0]; pl[1] = abc[1]; pl[2] = abc[2];
+  pl[3] = -hdot(abc, c);
+}
+
+// ComputeTrianglePlane (k == 3) / GetPlaneFromPoints (k > 3), host float64
+static void plane_from_pts(const double* P, int k, double pl[4]) {
+  if (k == 3) {
+    double e0[3] = {P[3] - P[0], P[4] - P[1], P[5] - P[2]};
+    double e1[3] = {P[6] - P[0], P[7] - P[1], P[8] - P[2]};
+    double abc[3];
+    hcross(e0, e1, abc);
+    double norm = std::sqrt(hdot(abc, abc));
+    if (norm == 0) {
+      pl[0] = pl[1] = pl[2] = pl[3] = 0;
+      return;
+    }
+    for (int a = 0; a < 3; ++a) abc[a] /= norm;
+    pl[0] = abc[0]; pl[1] = abc[1]; pl[2] = abc[2];
+    pl[3] = -hdot(abc, P);
+    return;
+  }
+  double c[3] = {0, 0, 0};
+  for (int j = 0; j < k; ++j)
+    for (int a = 0; a < 3; ++a) c[a] += P[3 * j + a];
+  for (int a = 0; a < 3; ++a) c[a] /= (double)k;
+  double mo[6] = {0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < k; ++j) {
+    double r0 = P[3 * j] - c[0], r1 = P[3 * j + 1] - c[1], r2 = P[3 * j + 2] - c[2];
+    mo[0] += r0 * r0; mo[1] += r0 * r1; mo[2] += r0 * r2;
+    mo[3] += r1 * r1; mo[4] += r1 * r2; mo[5] += r2 * r2;
+  }
+  plane_from_centred(c, mo, pl);
+}
+
+static bool plane_is_zero(const double* pl) { return pl[0] == 0 && pl[1] == 0 && pl[2] == 0 && pl[3] == 0; }
+
+// ------------------------------------------------------------ workspaces
+static int count_blocks(int64_t n) {
+  int64_t tiles = (n + (int64_t)kBlock * kPts - 1) / ((int64_t)kBlock * kPts);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kCountBlocksMax, tiles));
+}
+
+struct CountWs {
+  float4* pl32;
+  float2* band;
+  double* pl64;
+  uint8_t* degen;
+  int32_t* partial;
+  int64_t* counts;
+  double* sum_partial;
+  double* sums;
+};
+
+static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
+  H = std::max(H, 1);
+  w->pl32 = ar.take<float4>(H);
+  w->band = ar.take<float2>(H);
+  w->pl64 = ar.take<double>(4 * (size_t)H);
+  w->degen = ar.take<uint8_t>(H);
+  w->partial = ar.take<int32_t>((size_t)count_blocks(n) * H);
+  w->counts = ar.take<int64_t>(H);
+  w->sum_partial = ar.take<double>((size_t)kSumBlocksX * H);
+  w->sums = ar.take<double>(H);
+  return ar.used;
+}
+
+// scale of |a x| + |b y| + |c z| + |d| over the cloud, for the float32 band
+static void upload_planes(const double* planes, int H, const double absmax[3], double thr, CountWs& w,
+                          std::vector<float4>& p32, std::vector<float2>& bnd, std::vector<uint8_t>& dg,
+                          hipStream_t s, int* rc) {
+  p32.resize(H);
+  bnd.resize(H);
+  dg.resize(H);
+  for (int h = 0; h < H; ++h) {
+    const double* pl = planes + 4 * h;
+    dg[h] = plane_is_zero(pl) ? 1 : 0;
+    p32[h] = make_float4((float)pl[0], (float)pl[1], (float)pl[2], (float)pl[3]);
+    double S = std::fabs(pl[0]) * absmax[0] + std::fabs(pl[1]) * absmax[1] + std::fabs(pl[2]) * absmax[2] +
+               std::fabs(pl[3]);
+    double g = 16.0 * std::ldexp(1.0, -24) * S + std::ldexp(1.0, -20) * thr;
+    float lo = (float)(thr - g), hi = (float)(thr + g);
+    if (dg[h]) {
+      lo = -1.0f;  // never an inlier
+      hi = -1.0f;
+    }
+    bnd[h] = make_float2(lo, hi);
+  }
+  *rc = 0;
+  if (hipMemcpyAsync(w.pl32, p32.data(), H * sizeof(float4), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(w.band, bnd.data(), H * sizeof(float2), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(w.pl64, planes, 4 * H * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(w.degen, dg.data(), H, hipMemcpyHostToDevice, s) != hipSuccess)
+    *rc = fail(O3DX_EIO, "plane upload failed");
+}
+
+static int absmax_of(const float* xyz, int64_t n, void* aabb_ws, double* mm_dev, hipStream_t s, double out[3]) {
+  double mm[6];
+  O3DX_TRY(aabb_device(xyz, n, mm_dev, aabb_ws, s));
+  O3DX_HIP(hipMemcpyAsync(mm, mm_dev, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  for (int a = 0; a < 3; ++a) out[a] = std::max(std::fabs(mm[a]), std::fabs(mm[3 + a]));
+  return 0;
+}
+
+static int run_count(const float* xyz, int64_t n, const double* planes, int H, double thr, CountWs& w, void* aabb_ws,
+                     double* mm_dev, hipStream_t s, std::vector<int64_t>& counts) {
+  double absmax[3];
+  O3DX_TRY(absmax_of(xyz, n, aabb_ws, mm_dev, s, absmax));
+  std::vector<float4> p32;
+  std::vector<float2> bnd;
+  std::vector<uint8_t> dg;
+  int rc;
+  upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, s, &rc);
+  if (rc) return rc;
+  const int nb = count_blocks(n);
+  for (int h0 = 0; h0 < H; h0 += kHChunk) {
+    int hc = std::min(kHChunk, H - h0);
+    hipLaunchKernelGGL(k_plane_count, dim3(nb), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, h0, hc, thr,
+                       w.partial);
+  }
+  hipLaunchKernelGGL(k_plane_count_reduce, dim3((H + 255) / 256), dim3(256), 0, s, w.partial, nb, H, w.degen, w.counts);
+  counts.resize(H);
+  O3DX_HIP(hipMemcpyAsync(counts.data(), w.counts, H * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+static int run_abs_sum(const float* xyz, int64_t n, const double* planes, const int32_t* which, int L, double thr,
+                       CountWs& w, hipStream_t s, double* sums_host) {
+  if (L == 0) return 0;
+  std::vector<double> sel((size_t)4 * L);
+  for (int j = 0; j < L; ++j)
+    for (int a = 0; a < 4; ++a) sel[4 * j + a] = planes[4 * which[j] + a];
+  O3DX_HIP(hipMemcpyAsync(w.pl64, sel.data(), sel.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_plane_abs_sum, dim3(kSumBlocksX, L), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, w.sum_partial);
+  // fixed-order final sums on the host
+  std::vector<double> part((size_t)kSumBlocksX * L);
+  O3DX_HIP(hipMemcpyAsync(part.data(), w.sum_partial, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_HIP(hipGetLastError());
+  for (int j = 0; j < L; ++j) {
+    double t = 0.0;
+    for (int b = 0; b < kSumBlocksX; ++b) t += part[(size_t)j * kSumBlocksX + b];
+    sums_host[j] = t;
+  }
+  return 0;
+}
+
+static int select_best(const int64_t* counts, const double* sums, const double* planes, int H, int64_t n, int ransac_n,
+                       double probability) {
+  double best_fit = 0, best_rmse = 0;
+  int best = -1;
+  size_t break_iteration = std::numeric_limits<size_t>::max();
+  int iteration_count = 0;
+  for (int it = 0; it < H; ++it) {
+    if ((size_t)iteration_count > break_iteration) continue;
+    if (counts[it] < 0 || (planes && plane_is_zero(planes + 4 * it))) continue;
+    double fit = counts[it] == 0 ? 0.0 : (double)counts[it] / (double)n;
+    double rmse = counts[it] == 0 ? 0.0 : sums[it] / std::sqrt((double)counts[it]);
+    if (fit > best_fit || (fit == best_fit && rmse < best_rmse)) {
+      best_fit = fit;
+      best_rmse = rmse;
+      best = it;
+      if (best_fit < 1.0) {
+        double bi = std::min(std::log(1 - probability) / std::log(1 - std::pow(best_fit, ransac_n)), (double)H);
+        break_iteration = (size_t)bi;
+      } else {
+        break_iteration = 0;
+      }
+    }
+    iteration_count++;
+  }
+  return best;
+}
+
+// hypotheses whose count equals another non-degenerate hypothesis' count
+static std::vector<int32_t> tied_hypotheses(const std::vector<int64_t>& counts) {
+  std::vector<std::pair<int64_t, int32_t>> v;
+  for (int h = 0; h < (int)counts.size(); ++h)
+    if (counts[h] > 0) v.emplace_back(counts[h], h);
+  std::sort(v.begin(), v.end());
+  std::vector<int32_t> out;
+  for (size_t i = 0; i < v.size(); ++i) {
+    bool t = (i > 0 && v[i].first == v[i - 1].first) || (i + 1 < v.size() && v[i].first == v[i + 1].first);
+    if (t) out.push_back(v[i].second);
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+static int run_moments(const float* xyz, const int32_t* idx, int64_t m, const double* centroid, double* part,
+                       double* out_dev, hipStream_t s, double out[6]) {
+  if (m == 0) {
+    for (int k = 0; k < 6; ++k) out[k] = 0;
+    return 0;
+  }
+  const int nb = (int)std::min<int64_t>(kMomBlocks, (m + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_plane_moments, dim3(nb), dim3(kBlock), 0, s, xyz, idx, m, centroid ? centroid[0] : 0.0,
+                     centroid ? centroid[1] : 0.0, centroid ? centroid[2] : 0.0, centroid ? 1 : 0, part);
+  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, s, part, nb, 6, out_dev);
+  O3DX_HIP(hipMemcpyAsync(out, out_dev, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+struct SegWs {
+  CountWs cw;
+  int32_t* sidx;
+  float* scoord;
+  uint8_t* flags;
+  int32_t* scan_tmp;
+  char* aabb;
+  double* mm;
+  int64_t* cnt;
+  double* mom_part;
+  double* mom_out;
+};
+
+static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
+  count_carve(ar, n, H, &w->cw);
+  w->sidx = ar.take<int32_t>((size_t)H * rn);
+  w->scoord = ar.take<float>((size_t)H * rn * 3);
+  w->flags = ar.take<uint8_t>(n + 16);
+  w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(n));
+  w->aabb = ar.take<char>(aabb_ws_bytes(n));
+  w->mm = ar.take<double>(8);
+  w->cnt = ar.take<int64_t>(4);
+  w->mom_part = ar.take<double>(kMomBlocks * 6);
+  w->mom_out = ar.take<double>(8);
+  return ar.used;
+}
+
+}  // namespace o3dx
+
+using namespace o3dx;
+
+extern "C" int o3dx_ransac_samples(int64_t n, int ransac_n, int iters, uint64_t seed, int32_t* out) {
+  if (n <= 0 || ransac_n <= 0 || iters < 0 || !out || n < ransac_n)
+    return fail(O3DX_EINVAL, "o3dx_ransac_samples: need n >= ransac_n > 0");
+  // Open3D RandomSampler: RandUint32() % total_size, redraw duplicates
+  std::mt19937 eng((uint32_t)seed);
+  for (int it = 0; it < iters; ++it) {
+    int got = 0;
+    while (got < ransac_n) {
+      int32_t idx = (int32_t)((uint64_t)eng() % (uint64_t)n);
+      bool dup = false;
+      for (int j = 0; j < got; ++j) dup |= out[(int64_t)it * ransac_n + j] == idx;
+      if (!dup) out[(int64_t)it * ransac_n + got++] = idx;
+    }
+  }
+  return 0;
+}
+
+extern "C" int o3dx_plane_from_points(const double* pts, int k, double* plane) {
+  if (!pts || !plane || k < 3) return fail(O3DX_EINVAL, "o3dx_plane_from_points: need k >= 3");
+  plane_from_pts(pts, k, plane);
+  return 0;
+}
+
+extern "C" int o3dx_plane_from_moments(const double* sum_xyz, int64_t count, const double* centred, double* plane) {
+  if (!sum_xyz || !centred || !plane) return fail(O3DX_EINVAL, "o3dx_plane_from_moments: bad arguments");
+  double c[3];
+  for (int a = 0; a < 3; ++a) c[a] = sum_xyz[a] / (double)count;
+  plane_from_centred(c, centred, plane);
+  return 0;
+}
+
+extern "C" size_t o3dx_plane_count_workspace_bytes(int64_t n, int H) {
+  Arena ar(nullptr, 0);
+  CountWs w;
+  count_carve(ar, std::max<int64_t>(n, 1), H, &w);
+  return ar.used + Arena::align(aabb_ws_bytes(n)) + 1024;
+}
+
+extern "C" int o3dx_plane_count(const float* xyz, int64_t n, const double* planes, int H, double thr, int64_t* counts,
+                                void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || H < 0 || (n > 0 && !xyz) || (H > 0 && (!planes || !counts)))
+    return fail(O3DX_EINVAL, "o3dx_plane_count: bad arguments");
+  if (!ws || ws_bytes < o3dx_plane_count_workspace_bytes(n, H)) return fail(O3DX_ENOMEM, "plane_count workspace too small");
+  if (H == 0) return 0;
+  if (n == 0) {
+    for (int h = 0; h < H; ++h) counts[h] = plane_is_zero(planes + 4 * h) ? -1 : 0;
+    return 0;
+  }
+  hipStream_t s = as_stream(stream);
+  Arena ar(ws, ws_bytes);
+  CountWs w;
+  count_carve(ar, n, H, &w);
+  char* aabb = ar.take<char>(aabb_ws_bytes(n));
+  double* mm = ar.take<double>(8);
+  O3DX_ARENA_CHECK(ar);
+  std::vector<int64_t> c;
+  O3DX_TRY(run_count(xyz, n, planes, H, thr, w, aabb, mm, s, c));
+  std::memcpy(counts, c.data(), H * sizeof(int64_t));
+  return 0;
+}
+
+extern "C" int o3dx_plane_abs_sum(const float* xyz, int64_t n, const double* planes, const int32_t* which, int L,
+                                  double thr, double* sums, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || L < 0 || (L > 0 && (!planes || !which || !sums))) return fail(O3DX_EINVAL, "o3dx_plane_abs_sum: bad args");
+  if (!ws || ws_bytes < o3dx_plane_count_workspace_bytes(n, L)) return fail(O3DX_ENOMEM, "abs_sum workspace too small");
+  if (L == 0) return 0;
+  if (n == 0) {
+    for (int j = 0; j < L; ++j) sums[j] = 0;
+    return 0;
+  }
+  Arena ar(ws, ws_bytes);
+  CountWs w;
+  count_carve(ar, n, L, &w);
+  O3DX_ARENA_CHECK(ar);
+  return run_abs_sum(xyz, n, planes, which, L, thr, w, as_stream(stream), sums);
+}
+
+extern "C" int o3dx_ransac_select(const int64_t* counts, const double* sums, const double* planes, int H, int64_t n,
+                                  int ransac_n, double probability) {
+  if (!counts || !sums || H < 0 || n <= 0) return -1;
+  return select_best(counts, sums, planes, H, n, ransac_n, probability);
+}
+
+extern "C" int o3dx_plane_inliers(const float* xyz, int64_t n, const double* plane, double thr, int32_t* idx_out,
+                                  int64_t* count_host, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || !plane || !count_host || (n > 0 && (!xyz || !idx_out))) return fail(O3DX_EINVAL, "o3dx_plane_inliers: bad args");
+  size_t need = Arena::align(n + 17) + Arena::align(compact_workspace_ints(n) * 4 + 1) + 512;
+  if (!ws || ws_bytes < need) return fail(O3DX_ENOMEM, "plane_inliers workspace too small");
+  if (n == 0 || plane_is_zero(plane)) {
+    *count_host = 0;
+    return 0;
+  }
+  hipStream_t s = as_stream(stream);
+  Arena ar(ws, ws_bytes);
+  uint8_t* flags = ar.take<uint8_t>(n + 16);
+  int32_t* tmp = ar.take<int32_t>(compact_workspace_ints(n));
+  int64_t* cnt = ar.take<int64_t>(2);
+  hipLaunchKernelGGL(k_plane_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1],
+                     plane[2], plane[3], thr, flags);
+  O3DX_TRY(compact_flags(flags, n, idx_out, nullptr, cnt, tmp, s));
+  O3DX_HIP(hipMemcpyAsync(count_host, cnt, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int o3dx_plane_moments(const float* xyz, const int32_t* idx, int64_t count, const double* centroid,
+                                  double* sums, void* ws, size_t ws_bytes, void* stream) {
+  if (count < 0 || !sums || (count > 0 && !xyz)) return fail(O3DX_EINVAL, "o3dx_plane_moments: bad args");
+  if (!ws || ws_bytes < 8192 + kMomBlocks * 6 * sizeof(double)) return fail(O3DX_ENOMEM, "moments workspace too small");
+  Arena ar(ws, ws_bytes);
+  double* part = ar.take<double>(kMomBlocks * 6);
+  double* outd = ar.take<double>(8);
+  double tmp[6];
+  O3DX_TRY(run_moments(xyz, idx, count, centroid, part, outd, as_stream(stream), tmp));
+  std::memcpy(sums, tmp, (centroid ? 6 : 3) * sizeof(double));
+  return 0;
+}
+
+extern "C" size_t o3dx_segment_plane_workspace_bytes(int64_t n, int iters) {
+  Arena ar(nullptr, 0);
+  SegWs w;
+  // ransac_n up to 16 sample points per hypothesis in the sample buffers
+  seg_carve(ar, std::max<int64_t>(n, 1), std::max(iters, 1), 16, &w);
+  return ar.used + 1024;
+}
+
+extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int ransac_n, int iters, double probability,
+                                  const int32_t* samples_host, double* plane_host, int32_t* inliers_out,
+                                  int64_t* n_inliers_host, void* ws, size_t ws_bytes, void* stream) {
+  if (!(probability > 0.0 && probability <= 1.0)) return fail(O3DX_EINVAL, "Probability must be > 0 or <= 1.0");
+  if (ransac_n < 3) return fail(O3DX_EINVAL, "ransac_n should be set to higher than or equal to 3.");
+  if (n < ransac_n) return fail(O3DX_EINVAL, "There must be at least 'ransac_n' points.");
+  if (ransac_n > 16) return fail(O3DX_ENOTSUP, "ransac_n > 16 not supported");
+  if (iters < 0 || !plane_host || !n_inliers_host || !inliers_out || !xyz || (iters > 0 && !samples_host))
+    return fail(O3DX_EINVAL, "o3dx_segment_plane: bad arguments");
+  if (!ws || ws_bytes < o3dx_segment_plane_workspace_bytes(n, iters))
+    return fail(O3DX_ENOMEM, "segment_plane workspace too small");
+  hipStream_t s = as_stream(stream);
+  Arena ar(ws, ws_bytes);
+  SegWs w;
+  seg_carve(ar, n, std::max(iters, 1), 16, &w);
+  const int H = iters;
+  // hypotheses (host float64, from the sampled points' coordinates)
+  std::vector<double> planes((size_t)4 * std::max(H, 1), 0.0);
+  if (H > 0) {
+    const int64_t ns = (int64_t)H * ransac_n;
+    for (int64_t j = 0; j < ns; ++j)
+      if (samples_host[j] < 0 || samples_host[j] >= n) return fail(O3DX_EINVAL, "sample index out of range");
+    O3DX_HIP(hipMemcpyAsync(w.sidx, samples_host, ns * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_gather_samples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, xyz, w.sidx, ns, w.scoord);
+    std::vector<float> sc((size_t)ns * 3);
+    O3DX_HIP(hipMemcpyAsync(sc.data(), w.scoord, sc.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    O3DX_HIP(hipStreamSynchronize(s));
+    std::vector<double> P((size_t)ransac_n * 3);
+    for (int h = 0; h < H; ++h) {
+      for (int j = 0; j < ransac_n * 3; ++j) P[j] = (double)sc[(size_t)h * ransac_n * 3 + j];
+      plane_from_pts(P.data(), ransac_n, &planes[(size_t)4 * h]);
+    }
+  }
+  int best = -1;
+  if (H > 0) {
+    std::vector<int64_t> counts;
+    O3DX_TRY(run_count(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts));
+    std::vector<int32_t> tied = tied_hypotheses(counts);
+    std::vector<double> sums(H, std::numeric_limits<double>::quiet_NaN());
+    if (!tied.empty()) {
+      std::vector<double> ts(tied.size());
+      O3DX_TRY(run_abs_sum(xyz, n, planes.data(), tied.data(), (int)tied.size(), thr, w.cw, s, ts.data()));
+      for (size_t j = 0; j < tied.size(); ++j) sums[tied[j]] = ts[j];
+    }
+    best = select_best(counts.data(), sums.data(), planes.data(), H, n, ransac_n, probability);
+  }
+  double bp[4] = {0, 0, 0, 0};
+  if (best >= 0) std::memcpy(bp, &planes[(size_t)4 * best], sizeof(bp));
+  int64_t k = 0;
+  if (!plane_is_zero(bp)) {
+    hipLaunchKernelGGL(k_plane_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, bp[0], bp[1], bp[2],
+                       bp[3], thr, w.flags);
+    O3DX_TRY(compact_flags(w.flags, n, inliers_out, nullptr, w.cnt, w.scan_tmp, s));
+    O3DX_HIP(hipMemcpyAsync(&k, w.cnt, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    O3DX_HIP(hipStreamSynchronize(s));
+  }
+  *n_inliers_host = k;
+  // GetPlaneFromPoints over the final inliers (zero plane when there are none)
+  if (k == 0) {
+    for (int a = 0; a < 4; ++a) plane_host[a] = 0;
+    return 0;
+  }
+  double s1[6], s2[6], c[3];
+  O3DX_TRY(run_moments(xyz, inliers_out, k, nullptr, w.mom_part, w.mom_out, s, s1));
+  for (int a = 0; a < 3; ++a) c[a] = s1[a] / (double)k;
+  O3DX_TRY(run_moments(xyz, inliers_out, k, c, w.mom_part, w.mom_out, s, s2));
+  plane_from_centred(c, s2, plane_host);
+  return 0;
+}

@@ -1,0 +1,133 @@
+"""ctypes binding of libo3dx.so (include/o3dx.h) — the only path to the kernels.
+
+There is deliberately no CPU fallback: if the library or a GPU is missing,
+every compute call raises RuntimeError (the exception type Open3D's pybind11
+layer raises, which reference callers catch generically, e.g.
+/root/reference/open3dpypro/PointCloud.py:964-968).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libo3dx.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "o3dx.h")
+
+SEARCH_KNN, SEARCH_RADIUS, SEARCH_HYBRID = 0, 1, 2
+MAX_KNN = 64
+ICP_NSUMS = 32
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int
+_D = ctypes.c_double
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "o3dx_abi_version": (_I32, []),
+    "o3dx_last_error": (ctypes.c_char_p, []),
+    "o3dx_aabb_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_aabb": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
+    "o3dx_voxel_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_voxel_down_sample": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_normals_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_estimate_normals": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _SZ, _P]),
+    "o3dx_knn_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_knn_search": (_I32, [_P, _I64, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_ransac_samples": (_I32, [_I64, _I32, _I32, ctypes.c_uint64, _P]),
+    "o3dx_segment_plane_workspace_bytes": (_SZ, [_I64, _I32]),
+    "o3dx_segment_plane": (_I32, [_P, _I64, _D, _I32, _I32, _D, _P, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_plane_from_points": (_I32, [_P, _I32, _P]),
+    "o3dx_plane_count_workspace_bytes": (_SZ, [_I64, _I32]),
+    "o3dx_plane_count": (_I32, [_P, _I64, _P, _I32, _D, _P, _P, _SZ, _P]),
+    "o3dx_plane_abs_sum": (_I32, [_P, _I64, _P, _P, _I32, _D, _P, _P, _SZ, _P]),
+    "o3dx_ransac_select": (_I32, [_P, _P, _P, _I32, _I64, _I32, _D]),
+    "o3dx_plane_inliers": (_I32, [_P, _I64, _P, _D, _P, _P, _P, _SZ, _P]),
+    "o3dx_plane_moments": (_I32, [_P, _P, _I64, _P, _P, _P, _SZ, _P]),
+    "o3dx_plane_from_moments": (_I32, [_P, _I64, _P, _P]),
+    "o3dx_icp_target_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_icp_target_build": (_I32, [_P, _P, _I64, _D, _P, _SZ, _P, _P]),
+    "o3dx_icp_accumulate_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_icp_accumulate": (_I32, [_P, _I64, _P, _P, _P, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_icp_solve_point_to_plane": (_I32, [_P, _P]),
+    "o3dx_registration_icp_point_to_plane": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,
+                                                     _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def declared_symbols():
+    """Every function name declared in include/o3dx.h."""
+    return list(_SIGS)
+
+
+def load():
+    """Load libo3dx.so (raises RuntimeError when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"libo3dx.so not found at {LIB_PATH}; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = load().o3dx_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg}" if what else msg)
+
+
+def require_device(t: torch.Tensor, what: str = "input"):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise RuntimeError(f"{what} must be a torch tensor on a ROCm GPU (got "
+                           f"{getattr(t, 'device', type(t))}); no CPU path exists")
+
+
+def default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("no ROCm GPU visible: the open3dpypro-mi355x kernels need an MI355X")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# per (device, stream) scratch buffers, grown on demand
+_ws = {}
+
+
+def workspace(nbytes: int, device: torch.device, slot: str = "main") -> torch.Tensor:
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream, slot)
+    buf = _ws.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws[key] = buf
+    return buf
+
+
+def release_workspaces():
+    _ws.clear()

@@ -1,0 +1,288 @@
+"""Tensor-level hot-path ops: torch-ROCm tensors in, torch tensors out.
+
+Each op is a thin call into libo3dx.so (include/o3dx.h); the tensor is only
+the device array container.  Inputs: (N,3) float32 contiguous on a ROCm GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+def _xyz(t: torch.Tensor, what="points") -> torch.Tensor:
+    N.require_device(t, what)
+    if t.ndim != 2 or t.shape[1] != 3:
+        raise RuntimeError(f"{what} must have shape (n, 3), got {tuple(t.shape)}")
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def aabb(xyz: torch.Tensor):
+    """(min_bound, max_bound) as float64 numpy — get_min_bound/get_max_bound."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    ws = N.workspace(L.o3dx_aabb_workspace_bytes(n), x.device)
+    out = np.zeros(6, np.float64)
+    N.check(L.o3dx_aabb(N.ptr(x), n, _np_ptr(out), N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "aabb")
+    return out[:3].copy(), out[3:].copy()
+
+
+def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_bound=None,
+                      with_xyz: bool = True, trace: bool = False):
+    """Open3D VoxelDownSampleAndTrace + idxmat.max(1) + _select_by_idx.
+
+    Returns dict: rep_idx (M,) int32 ascending; rep_xyz (M,3) (if with_xyz);
+    voxel_of_point (N,) int32 and cubic_id (M,8) int32 (if trace)."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    ws = N.workspace(L.o3dx_voxel_workspace_bytes(n), dev)
+    rep = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    rxyz = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev) if with_xyz else None
+    vop = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if trace else None
+    cub = torch.empty(max(8 * n, 8), dtype=torch.int32, device=dev) if trace else None
+    mnb = None if min_bound is None else _c(min_bound, np.float64)
+    mxb = None if max_bound is None else _c(max_bound, np.float64)
+    m = np.zeros(1, np.int64)
+    rc = L.o3dx_voxel_down_sample(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), N.ptr(rep),
+                                  N.ptr(rxyz), _np_ptr(m), N.ptr(vop), N.ptr(cub), N.ptr(ws), ws.numel(),
+                                  N.stream_ptr(dev))
+    N.check(rc, "voxel_down_sample")
+    M = int(m[0])
+    out = {"rep_idx": rep[:M]}
+    if with_xyz:
+        out["rep_xyz"] = rxyz[:M]
+    if trace:
+        out["voxel_of_point"] = vop[:n]
+        out["cubic_id"] = cub[: 8 * M].view(M, 8)
+    return out
+
+
+def estimate_normals(xyz: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30, radius: float = 0.0,
+                     prior: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Open3D EstimateNormals(search_param, fast_normal_computation=True) -> (N,3) float32."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    out = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev)
+    pr = None if prior is None else _xyz(prior.to(dev), "prior normals")
+    ws = N.workspace(L.o3dx_normals_workspace_bytes(n), dev)
+    rc = L.o3dx_estimate_normals(N.ptr(x), n, int(mode), int(knn), float(radius), N.ptr(pr), N.ptr(out), N.ptr(ws),
+                                 ws.numel(), N.stream_ptr(dev))
+    N.check(rc, "estimate_normals")
+    return out[:n]
+
+
+def knn_search(xyz: torch.Tensor, queries: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30,
+               radius: float = 0.0):
+    """Batched KDTreeFlann search: (idx (nq,K) int32, d2 (nq,K) float64, count (nq,) int32)."""
+    x = _xyz(xyz)
+    q = _xyz(queries.to(x.device), "queries")
+    L = N.load()
+    n, nq = x.shape[0], q.shape[0]
+    dev = x.device
+    K = int(knn)
+    idx = torch.empty((max(nq, 1), K), dtype=torch.int32, device=dev)
+    d2 = torch.empty((max(nq, 1), K), dtype=torch.float64, device=dev)
+    cnt = torch.empty(max(nq, 1), dtype=torch.int32, device=dev)
+    ws = N.workspace(L.o3dx_knn_workspace_bytes(n), dev)
+    rc = L.o3dx_knn_search(N.ptr(x), n, N.ptr(q), nq, int(mode), K, float(radius), N.ptr(idx), N.ptr(d2), N.ptr(cnt),
+                           N.ptr(ws), ws.numel(), N.stream_ptr(dev))
+    N.check(rc, "knn_search")
+    return idx[:nq], d2[:nq], cnt[:nq]
+
+
+def ransac_samples(n: int, ransac_n: int, num_iterations: int, seed: int) -> np.ndarray:
+    """Open3D RandomSampler over mt19937(seed): (iters, ransac_n) int32."""
+    out = np.empty((max(num_iterations, 1), ransac_n), np.int32)
+    N.check(N.load().o3dx_ransac_samples(int(n), int(ransac_n), int(num_iterations), int(seed) & (2**64 - 1),
+                                         _np_ptr(out)), "ransac_samples")
+    return out[:num_iterations]
+
+
+def segment_plane(xyz: torch.Tensor, distance_threshold: float, ransac_n: int, num_iterations: int,
+                  probability: float = 0.99999999, samples: Optional[np.ndarray] = None, seed: int = 0):
+    """Open3D SegmentPlane -> (plane float64[4], inliers (k,) int32 ascending on device)."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    if not (0.0 < probability <= 1.0):
+        raise RuntimeError("Probability must be > 0 or <= 1.0")
+    if ransac_n < 3:
+        raise RuntimeError("ransac_n should be set to higher than or equal to 3.")
+    if n < ransac_n:
+        raise RuntimeError("There must be at least 'ransac_n' points.")
+    if samples is None:
+        samples = ransac_samples(n, ransac_n, num_iterations, seed)
+    s = _c(samples, np.int32).reshape(num_iterations, ransac_n)
+    plane = np.zeros(4, np.float64)
+    inl = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    k = np.zeros(1, np.int64)
+    ws = N.workspace(L.o3dx_segment_plane_workspace_bytes(n, num_iterations), dev)
+    rc = L.o3dx_segment_plane(N.ptr(x), n, float(distance_threshold), int(ransac_n), int(num_iterations),
+                              float(probability), _np_ptr(s), _np_ptr(plane), N.ptr(inl), _np_ptr(k), N.ptr(ws),
+                              ws.numel(), N.stream_ptr(dev))
+    N.check(rc, "segment_plane")
+    return plane, inl[: int(k[0])]
+
+
+def plane_count(xyz: torch.Tensor, planes: np.ndarray, distance_threshold: float) -> np.ndarray:
+    """Exact per-hypothesis inlier counts (-1 for degenerate planes)."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    P = _c(planes, np.float64).reshape(-1, 4)
+    H = P.shape[0]
+    counts = np.zeros(max(H, 1), np.int64)
+    ws = N.workspace(L.o3dx_plane_count_workspace_bytes(n, H), x.device)
+    N.check(L.o3dx_plane_count(N.ptr(x), n, _np_ptr(P), H, float(distance_threshold), _np_ptr(counts), N.ptr(ws),
+                               ws.numel(), N.stream_ptr(x.device)), "plane_count")
+    return counts[:H]
+
+
+def plane_abs_sum(xyz: torch.Tensor, planes: np.ndarray, which, distance_threshold: float) -> np.ndarray:
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    P = _c(planes, np.float64).reshape(-1, 4)
+    w = _c(which, np.int32)
+    sums = np.zeros(max(len(w), 1), np.float64)
+    ws = N.workspace(L.o3dx_plane_count_workspace_bytes(n, max(len(w), 1)), x.device)
+    N.check(L.o3dx_plane_abs_sum(N.ptr(x), n, _np_ptr(P), _np_ptr(w), len(w), float(distance_threshold),
+                                 _np_ptr(sums), N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "plane_abs_sum")
+    return sums[: len(w)]
+
+
+def plane_from_points(pts: np.ndarray) -> np.ndarray:
+    p = _c(pts, np.float64).reshape(-1, 3)
+    out = np.zeros(4, np.float64)
+    N.check(N.load().o3dx_plane_from_points(_np_ptr(p), len(p), _np_ptr(out)), "plane_from_points")
+    return out
+
+
+def ransac_select(counts, sums, planes, n, ransac_n, probability=0.99999999) -> int:
+    c = _c(counts, np.int64)
+    s = _c(sums, np.float64)
+    P = _c(planes, np.float64).reshape(-1, 4)
+    return int(N.load().o3dx_ransac_select(_np_ptr(c), _np_ptr(s), _np_ptr(P), len(c), int(n), int(ransac_n),
+                                           float(probability)))
+
+
+def plane_inliers(xyz: torch.Tensor, plane, distance_threshold: float) -> torch.Tensor:
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    pl = _c(plane, np.float64)
+    idx = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
+    k = np.zeros(1, np.int64)
+    ws = N.workspace(2 * n + 65536, x.device)
+    N.check(L.o3dx_plane_inliers(N.ptr(x), n, _np_ptr(pl), float(distance_threshold), N.ptr(idx), _np_ptr(k),
+                                 N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "plane_inliers")
+    return idx[: int(k[0])]
+
+
+def plane_moments(xyz: torch.Tensor, idx: Optional[torch.Tensor], centroid=None) -> np.ndarray:
+    x = _xyz(xyz)
+    L = N.load()
+    count = x.shape[0] if idx is None else idx.numel()
+    c = None if centroid is None else _c(centroid, np.float64)
+    out = np.zeros(6, np.float64)
+    ws = N.workspace(65536, x.device, "moments")
+    ii = None if idx is None else idx.to(torch.int32).contiguous()
+    N.check(L.o3dx_plane_moments(N.ptr(x), N.ptr(ii), count, _np_ptr(c), _np_ptr(out), N.ptr(ws), ws.numel(),
+                                 N.stream_ptr(x.device)), "plane_moments")
+    return out if centroid is not None else out[:3]
+
+
+def plane_from_moments(sum_xyz, count, centred) -> np.ndarray:
+    out = np.zeros(4, np.float64)
+    N.check(N.load().o3dx_plane_from_moments(_np_ptr(_c(sum_xyz, np.float64)), int(count),
+                                             _np_ptr(_c(centred, np.float64)), _np_ptr(out)), "plane_from_moments")
+    return out
+
+
+class ICPTarget:
+    """Persistent target structure (grid of target points + normals) for ICP."""
+
+    def __init__(self, tgt: torch.Tensor, tgt_normals: torch.Tensor, max_correspondence_distance: float):
+        self.xyz = _xyz(tgt, "target points")
+        self.normals = _xyz(tgt_normals.to(self.xyz.device), "target normals")
+        if self.normals.shape[0] != self.xyz.shape[0]:
+            raise RuntimeError("target normals must match target points")
+        L = N.load()
+        nt = self.xyz.shape[0]
+        self.max_corr = float(max_correspondence_distance)
+        self.ws = torch.empty(L.o3dx_icp_target_workspace_bytes(nt), dtype=torch.uint8, device=self.xyz.device)
+        self.desc = np.zeros(16, np.float64)
+        N.check(L.o3dx_icp_target_build(N.ptr(self.xyz), N.ptr(self.normals), nt, self.max_corr, N.ptr(self.ws),
+                                        self.ws.numel(), _np_ptr(self.desc), N.stream_ptr(self.xyz.device)),
+                "icp_target_build")
+
+    def accumulate(self, src: torch.Tensor, T: np.ndarray, want_corr: bool = False):
+        """Fused transform + 1-NN + point-to-plane moments: (sums[32], corr or None)."""
+        s = _xyz(src.to(self.xyz.device), "source points")
+        L = N.load()
+        ns = s.shape[0]
+        TT = _c(T, np.float64).reshape(4, 4)
+        sums = np.zeros(N.ICP_NSUMS, np.float64)
+        corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if want_corr else None
+        nc = np.zeros(1, np.int64)
+        ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp")
+        N.check(L.o3dx_icp_accumulate(N.ptr(s), ns, N.ptr(self.ws), _np_ptr(self.desc), _np_ptr(TT), self.max_corr,
+                                      _np_ptr(sums), N.ptr(corr), _np_ptr(nc), N.ptr(ws), ws.numel(),
+                                      N.stream_ptr(s.device)), "icp_accumulate")
+        return sums, (corr[: int(nc[0])] if want_corr else None)
+
+
+def icp_solve(sums) -> np.ndarray:
+    upd = np.zeros((4, 4), np.float64)
+    N.load().o3dx_icp_solve_point_to_plane(_np_ptr(_c(sums, np.float64)), _np_ptr(upd))
+    return upd
+
+
+def registration_icp(src: torch.Tensor, tgt: torch.Tensor, tgt_normals: torch.Tensor,
+                     max_correspondence_distance: float, init=None, max_iteration: int = 30,
+                     relative_fitness: float = 1e-6, relative_rmse: float = 1e-6, return_corr: bool = True):
+    """Open3D registration_icp + TransformationEstimationPointToPlane on one device."""
+    s = _xyz(src, "source points")
+    t = _xyz(tgt.to(s.device), "target points")
+    tn = _xyz(tgt_normals.to(s.device), "target normals")
+    L = N.load()
+    ns, nt = s.shape[0], t.shape[0]
+    T0 = np.eye(4) if init is None else _c(init, np.float64).reshape(4, 4)
+    T0 = _c(T0, np.float64)
+    T = np.zeros((4, 4), np.float64)
+    fit = np.zeros(1)
+    rm = np.zeros(1)
+    corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if return_corr else None
+    nc = np.zeros(1, np.int64)
+    tws = N.workspace(L.o3dx_icp_target_workspace_bytes(nt), s.device, "icp_target")
+    ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp")
+    rc = L.o3dx_registration_icp_point_to_plane(N.ptr(s), ns, N.ptr(t), N.ptr(tn), nt,
+                                                float(max_correspondence_distance), _np_ptr(T0), int(max_iteration),
+                                                float(relative_fitness), float(relative_rmse), _np_ptr(T),
+                                                _np_ptr(fit), _np_ptr(rm), N.ptr(corr), _np_ptr(nc), N.ptr(tws),
+                                                tws.numel(), N.ptr(ws), ws.numel(), N.stream_ptr(s.device))
+    N.check(rc, "registration_icp")
+    out = {"transformation": T, "fitness": float(fit[0]), "inlier_rmse": float(rm[0])}
+    if return_corr:
+        out["correspondence_set"] = corr[: int(nc[0])]
+    return out

@@ -1,0 +1,106 @@
+"""oracle/np_restate.py — small-N numpy restatement of the same Open3D algorithms.
+
+TEST INFRASTRUCTURE ONLY (see oracle/oracle.py).  A second, independent
+transcription used to cross-check the C++ restatement on small inputs; it is
+written with numpy vector ops / brute force so that the two share no code.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+def voxel_down_sample(xyz, voxel_size, min_bound=None):
+    """Open3D VoxelDownSampleAndTrace + idxmat.max(1) + _select_by_idx
+    (reference PointCloud.py:338-341, :185-204): representative = largest
+    index per voxel, keys floor((p - min_bound)/vs) in float64; returns the
+    ascending representative indices."""
+    p = np.asarray(xyz, np.float32).astype(np.float64).reshape(-1, 3)
+    if len(p) == 0:
+        return np.zeros(0, np.int64)
+    mn = p.min(0) if min_bound is None else np.asarray(min_bound, np.float64)
+    keys = np.floor((p - mn) / voxel_size).astype(np.int64)
+    # lexicographic group id; representative = max index in group
+    _, inv = np.unique(keys, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    rep = np.full(inv.max() + 1, -1, np.int64)
+    np.maximum.at(rep, inv, np.arange(len(p)))
+    return np.sort(rep)
+
+
+def nanoflann_d2(q, pts):
+    d = pts - q
+    r = d[:, 0] * d[:, 0]
+    r = r + d[:, 1] * d[:, 1]
+    r = r + d[:, 2] * d[:, 2]
+    return r
+
+
+def neighbours(pts, q, mode, knn, radius):
+    """KDTreeFlann::Search by brute force; (d2, idx) lexicographic order."""
+    d2 = nanoflann_d2(q, pts)
+    order = np.lexsort((np.arange(len(pts)), d2))
+    if mode == 1:  # radius
+        order = order[d2[order] < radius * radius]
+        return order
+    order = order[:knn]
+    if mode == 2:  # hybrid
+        order = order[d2[order] < radius * radius]
+    return order
+
+
+def covariance(pts, idx):
+    if len(idx) == 0:
+        return np.eye(3)
+    m = np.zeros(9)
+    for i in idx:
+        x, y, z = pts[i]
+        m += [x, y, z, x * x, x * y, x * z, y * y, y * z, z * z]
+    m /= len(idx)
+    c = np.empty((3, 3))
+    c[0, 0] = m[3] - m[0] * m[0]
+    c[1, 1] = m[6] - m[1] * m[1]
+    c[2, 2] = m[8] - m[2] * m[2]
+    c[0, 1] = c[1, 0] = m[4] - m[0] * m[1]
+    c[0, 2] = c[2, 0] = m[5] - m[0] * m[2]
+    c[1, 2] = c[2, 1] = m[7] - m[1] * m[2]
+    return c
+
+
+def smallest_eigvec(c):
+    """Reference answer up to sign (numpy eigh)."""
+    w, v = np.linalg.eigh(c)
+    return v[:, 0], w
+
+
+def plane_dist(plane, pts):
+    a, b, c, d = plane
+    return np.abs((a * pts[:, 0] + c * pts[:, 2]) + (b * pts[:, 1] + d))
+
+
+def triangle_plane(p0, p1, p2):
+    e0 = p1 - p0
+    e1 = p2 - p0
+    abc = np.array([e0[1] * e1[2] - e0[2] * e1[1],
+                    e0[2] * e1[0] - e0[0] * e1[2],
+                    e0[0] * e1[1] - e0[1] * e1[0]])
+    nrm = math.sqrt((abc[0] * abc[0] + abc[1] * abc[1]) + abc[2] * abc[2])
+    if nrm == 0:
+        return np.zeros(4)
+    abc = abc / nrm
+    d = -((abc[0] * p0[0] + abc[1] * p0[1]) + abc[2] * p0[2])
+    return np.array([abc[0], abc[1], abc[2], d])
+
+
+def segment_plane_counts(xyz, thr, samples):
+    """Per-hypothesis exact inlier counts (ransac_n == 3) — EvaluateRANSACBasedOnDistance."""
+    p = np.asarray(xyz, np.float32).astype(np.float64).reshape(-1, 3)
+    out = []
+    for s in np.asarray(samples).reshape(-1, 3):
+        pl = triangle_plane(p[s[0]], p[s[1]], p[s[2]])
+        if not pl.any():
+            out.append(-1)
+            continue
+        out.append(int((plane_dist(pl, p) < thr).sum()))
+    return np.array(out, np.int64)

@@ -1,0 +1,248 @@
+"""GPU parity of the C-ABI kernels against the CPU oracle (tests-only checker).
+
+Bar: bit-exact for integer/index results (voxel representatives, trace,
+kNN index sets, RANSAC counts and inlier sets); normals and ICP transforms
+within 1e-5 (float64 math on both sides; normals compared up to sign only
+where Open3D's eigen-solver sign itself is ill-conditioned)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from oracle import np_restate as NPR
+from open3dpypro import ops, synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _normal_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b).max(1), np.minimum(np.abs(a - b).max(1), np.abs(a + b).max(1))
+
+
+# ------------------------------------------------------------------ AABB
+def test_aabb(dev, bunny):
+    mn, mx = ops.aabb(torch.from_numpy(bunny).to(dev))
+    rmn, rmx = O.aabb(bunny)
+    assert np.array_equal(mn, rmn) and np.array_equal(mx, rmx)
+
+
+def test_aabb_empty(dev):
+    mn, mx = ops.aabb(torch.zeros((0, 3), device=dev))
+    assert not mn.any() and not mx.any()
+
+
+# ----------------------------------------------------------------- voxel
+@pytest.mark.parametrize("vs,expect_m", [(0.005, 3017), (0.01, 751)])
+def test_voxel_bunny(dev, bunny, vs, expect_m):
+    out = ops.voxel_down_sample(torch.from_numpy(bunny).to(dev), vs, trace=True)
+    rep = out["rep_idx"].cpu().numpy()
+    ref, vop, cub = O.voxel_down_sample(bunny, vs, trace=True)
+    assert len(rep) == expect_m
+    assert np.array_equal(rep, ref)
+    assert np.array_equal(out["voxel_of_point"].cpu().numpy(), vop)
+    assert np.array_equal(out["cubic_id"].cpu().numpy(), cub)
+    assert np.array_equal(out["rep_xyz"].cpu().numpy(), bunny[ref])
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (7, 1), (100_000, 2), (1_000_003, 3)])
+def test_voxel_uniform(dev, n, seed):
+    pts = S.uniform_cube(n, seed)
+    vs = S.voxel_size_for(max(n, 8))
+    rep = ops.voxel_down_sample(pts.to(dev), vs)["rep_idx"].cpu().numpy()
+    assert np.array_equal(rep, O.voxel_down_sample(pts.numpy(), vs))
+    if n <= 100_000:
+        assert np.array_equal(rep, NPR.voxel_down_sample(pts.numpy(), vs))
+
+
+def test_voxel_hash_path_and_bounds(dev):
+    # sparse clusters far apart -> grid box >> 2n cells -> hash table path
+    rng = np.random.default_rng(5)
+    c = rng.uniform(-1000, 1000, (50, 3))
+    pts = (c[rng.integers(0, 50, 20000)] + rng.normal(0, 0.05, (20000, 3))).astype(np.float32)
+    vs = 0.01
+    rep = ops.voxel_down_sample(torch.from_numpy(pts).to(dev), vs)["rep_idx"].cpu().numpy()
+    assert np.array_equal(rep, O.voxel_down_sample(pts, vs))
+    # explicit bounds that do not contain every point (dense path must fall back)
+    mnb = pts.min(0).astype(np.float64) + 100.0
+    mxb = mnb + 10.0
+    rep = ops.voxel_down_sample(torch.from_numpy(pts).to(dev), 0.5, mnb, mxb)["rep_idx"].cpu().numpy()
+    assert np.array_equal(rep, O.voxel_down_sample(pts, 0.5, mnb, mxb))
+
+
+def test_voxel_duplicates_negative(dev):
+    rng = np.random.default_rng(9)
+    base = rng.uniform(-3, -1, (3000, 3)).astype(np.float32)
+    pts = np.concatenate([base, base[::3], base[::7]])
+    rep = ops.voxel_down_sample(torch.from_numpy(pts).to(dev), 0.05, trace=True)
+    ref, vop, cub = O.voxel_down_sample(pts, 0.05, trace=True)
+    assert np.array_equal(rep["rep_idx"].cpu().numpy(), ref)
+    assert np.array_equal(rep["cubic_id"].cpu().numpy(), cub)
+
+
+def test_voxel_errors(dev):
+    x = torch.rand(100, 3, device=dev)
+    with pytest.raises(RuntimeError, match="voxel_size <= 0"):
+        ops.voxel_down_sample(x, 0.0)
+    with pytest.raises(RuntimeError, match="too small"):
+        ops.voxel_down_sample(x * 1e3, 1e-9)
+
+
+def test_voxel_empty(dev):
+    out = ops.voxel_down_sample(torch.zeros((0, 3), device=dev), 0.1)
+    assert out["rep_idx"].numel() == 0
+
+
+# --------------------------------------------------------------- normals
+def test_normals_knn30_bunny_reps(dev, bunny):
+    ref_idx = O.voxel_down_sample(bunny, 0.005)
+    reps = bunny[ref_idx]
+    got = ops.estimate_normals(torch.from_numpy(reps).to(dev), knn=30).cpu().numpy()
+    exp = O.estimate_normals(reps, O.KNN, 30)
+    e_signed, e_any = _normal_err(got, exp)
+    assert e_any.max() < 1e-5
+    assert np.mean(e_signed < 1e-5) > 0.999
+
+
+@pytest.mark.parametrize("k", [3, 8, 16, 30, 64])
+def test_normals_knn_uniform(dev, k):
+    pts = S.uniform_cube(50_000, 11).numpy()
+    got = ops.estimate_normals(torch.from_numpy(pts).to(dev), knn=k).cpu().numpy()
+    exp = O.estimate_normals(pts, O.KNN, k)
+    e_signed, e_any = _normal_err(got, exp)
+    # near-isotropic neighbourhoods make a few eigenvectors ill-conditioned
+    assert np.mean(e_any < 1e-5) > 0.999
+    assert np.mean(e_signed < 1e-5) > 0.995
+
+
+def test_normals_hybrid_radius(dev, bunny):
+    x = torch.from_numpy(bunny).to(dev)
+    for mode, k, r in [(O.HYBRID, 30, 0.01), (O.HYBRID, 8, 0.003), (O.RADIUS, 0, 0.004)]:
+        got = ops.estimate_normals(x, mode=mode, knn=k, radius=r).cpu().numpy()
+        exp = O.estimate_normals(bunny, mode, k, r)
+        e_signed, e_any = _normal_err(got, exp)
+        assert np.mean(e_any < 1e-5) > 0.999, (mode, k, r, e_any.max())
+
+
+def test_normals_prior_orientation(dev, bunny):
+    prior = np.tile(np.array([[0.0, 0.0, 1.0]]), (len(bunny), 1))
+    got = ops.estimate_normals(torch.from_numpy(bunny).to(dev), knn=20,
+                               prior=torch.from_numpy(prior.astype(np.float32)).to(dev)).cpu().numpy()
+    exp = O.estimate_normals(bunny, O.KNN, 20, prior=prior)
+    assert np.mean(np.abs(got - exp).max(1) < 1e-5) > 0.999
+    assert (got[:, 2] >= -1e-7).all()
+
+
+def test_normals_degenerate(dev):
+    # fewer than 3 neighbours / identical points -> (0,0,1)
+    pts = np.zeros((5, 3), np.float32)
+    got = ops.estimate_normals(torch.from_numpy(pts).to(dev), knn=30).cpu().numpy()
+    assert np.allclose(got, [[0, 0, 1]] * 5)
+    two = np.array([[0, 0, 0], [1, 0, 0]], np.float32)
+    got = ops.estimate_normals(torch.from_numpy(two).to(dev), knn=30).cpu().numpy()
+    assert np.allclose(got, O.estimate_normals(two, O.KNN, 30))
+
+
+# ------------------------------------------------------------- kNN search
+def test_knn_search_sets(dev, bunny):
+    q = bunny[::37]
+    idx, d2, cnt = ops.knn_search(torch.from_numpy(bunny).to(dev), torch.from_numpy(q).to(dev), knn=30)
+    ridx, rd2, rcnt = O.knn_search(bunny, q, O.KNN, 30)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    assert np.array_equal(d2.cpu().numpy(), rd2)
+    idx, d2, cnt = ops.knn_search(torch.from_numpy(bunny).to(dev), torch.from_numpy(q).to(dev),
+                                  mode=O.HYBRID, knn=16, radius=0.004)
+    ridx, rd2, rcnt = O.knn_search(bunny, q, O.HYBRID, 16, 0.004)
+    assert np.array_equal(cnt.cpu().numpy(), rcnt)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+
+
+def test_knn_search_outside_queries(dev):
+    pts = S.uniform_cube(20000, 4).numpy()
+    q = (np.random.default_rng(1).uniform(-1, 2, (500, 3))).astype(np.float32)
+    idx, d2, cnt = ops.knn_search(torch.from_numpy(pts).to(dev), torch.from_numpy(q).to(dev), knn=8)
+    ridx, rd2, _ = O.knn_search(pts, q, O.KNN, 8)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+
+
+# ----------------------------------------------------------------- RANSAC
+def test_ransac_sampler_matches_oracle():
+    a = ops.ransac_samples(12345, 3, 500, 7)
+    b = O.ransac_samples(12345, 3, 500, 7)
+    assert np.array_equal(a, b)
+    assert all(len(set(r)) == 3 for r in a)
+
+
+@pytest.mark.parametrize("n,iters", [(5000, 100), (300_000, 256)])
+def test_ransac_counts_exact(dev, n, iters):
+    pts = S.planted_plane(n, 21).numpy()
+    samples = O.ransac_samples(n, 3, iters, 5)
+    _, _, counts, sums, _ = O.segment_plane(pts, 0.01, 3, iters, samples)
+    planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
+    got = ops.plane_count(torch.from_numpy(pts).to(dev), planes, 0.01)
+    assert np.array_equal(got, counts)
+    ok = counts > 0
+    gs = ops.plane_abs_sum(torch.from_numpy(pts).to(dev), planes, np.nonzero(ok)[0], 0.01)
+    np.testing.assert_allclose(gs, sums[ok], rtol=1e-12)
+
+
+@pytest.mark.parametrize("n,iters,ransac_n", [(30_000, 450, 3), (200_000, 1000, 3), (20_000, 100, 5)])
+def test_segment_plane_parity(dev, n, iters, ransac_n):
+    pts = S.planted_plane(n, 33).numpy()
+    samples = O.ransac_samples(n, ransac_n, iters, 9)
+    plane, inl = ops.segment_plane(torch.from_numpy(pts).to(dev), 0.01, ransac_n, iters, samples=samples)
+    rplane, rinl, _, _, _ = O.segment_plane(pts, 0.01, ransac_n, iters, samples)
+    assert np.array_equal(inl.cpu().numpy().astype(np.int64), rinl)
+    np.testing.assert_allclose(plane, rplane, rtol=0, atol=1e-9)
+
+
+def test_segment_plane_ties_small(dev):
+    # tiny cloud: many hypotheses tie in count -> rmse tie-break path
+    pts = S.planted_plane(60, 3).numpy()
+    samples = O.ransac_samples(60, 3, 200, 1)
+    plane, inl = ops.segment_plane(torch.from_numpy(pts).to(dev), 0.05, 3, 200, samples=samples)
+    rplane, rinl, _, _, _ = O.segment_plane(pts, 0.05, 3, 200, samples)
+    assert np.array_equal(inl.cpu().numpy().astype(np.int64), rinl)
+    np.testing.assert_allclose(plane, rplane, atol=1e-9)
+
+
+def test_segment_plane_errors(dev):
+    x = torch.rand(2, 3, device=dev)
+    with pytest.raises(RuntimeError, match="ransac_n"):
+        ops.segment_plane(x, 0.01, 3, 10)
+    with pytest.raises(RuntimeError, match="Probability"):
+        ops.segment_plane(torch.rand(10, 3, device=dev), 0.01, 3, 10, probability=0.0)
+
+
+# -------------------------------------------------------------------- ICP
+def _icp_case(n, seed=1):
+    tgt = S.box_surface(n, seed)
+    src = S.apply_transform(S.box_surface(n, seed + 1), S.rigid_transform())
+    return src.numpy(), tgt.numpy()
+
+
+def test_icp_accumulate_matches_oracle(dev):
+    src, tgt = _icp_case(20000)
+    tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
+    T = S.rigid_transform(0.3, (0, 0, 1), (0.001, 0, 0))
+    target = ops.ICPTarget(torch.from_numpy(tgt).to(dev), torch.from_numpy(tn).to(dev), 0.02)
+    sums, corr = target.accumulate(torch.from_numpy(src).to(dev), T, want_corr=True)
+    ref = O.icp_accumulate(src, tgt, tn, 0.02, T)
+    assert sums[28] == ref[28]
+    np.testing.assert_allclose(sums[:30], ref[:30], rtol=1e-9, atol=1e-9)
+
+
+def test_registration_icp_parity(dev):
+    src, tgt = _icp_case(30000)
+    tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
+    res = ops.registration_icp(torch.from_numpy(src).to(dev), torch.from_numpy(tgt).to(dev),
+                               torch.from_numpy(tn).to(dev), 0.02, max_iteration=30,
+                               relative_fitness=0.0, relative_rmse=0.0)
+    T, fit, rmse, corr = O.registration_icp(src, tgt, tn, 0.02, max_iteration=30, relative_fitness=0.0,
+                                            relative_rmse=0.0)
+    np.testing.assert_allclose(res["transformation"], T, atol=1e-5)
+    assert abs(res["fitness"] - fit) < 1e-6
+    assert abs(res["inlier_rmse"] - rmse) < 1e-6
+    Tgt_inv = np.linalg.inv(S.rigid_transform())
+    assert np.abs(res["transformation"] - Tgt_inv).max() < 2e-3
