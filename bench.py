@@ -1,0 +1,264 @@
+#!/usr/bin/env python
+"""bench.py — headline benchmark: Mpoints/s of voxel_down_sample + estimate_normals
+(KNN30) on synthetic uniform-random 10M-point float32 clouds (BASELINE.json
+configs[1]), plus ICP iterations/s and RANSAC time (C3) as
+secondary figures.
+
+One step = one pass of the hot path over one cloud that is already resident
+in HBM: voxel_down_sample(vs=(4/N)^(1/3)) -> estimate_normals(KNN 30) on the
+M representatives.  Multi-GPU: one process per GPU (torchrun), each rank owns
+one 10M-point spatial tile (an independent cloud, no data-path collective):
+weak scaling.  `value` = points processed by all ranks / max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+   or: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "open3d-py-extension_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from open3dpypro import _native, ops, synthetic  # noqa: E402
+
+METRIC = "Mpoints/sec voxel_down_sample+estimate_normals; ICP iters/sec @ N=10M"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_VALU_PEAK_TFLOPS = 78.6   # vector FP64 (half of the 157.3 TF FP32 vector peak)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU (C2: 10M)")
+    ap.add_argument("--knn", type=int, default=30)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-n", type=int, default=2_000_000, help="CPU baseline sample size")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the ICP / RANSAC figures")
+    ap.add_argument("--icp-n", type=int, default=10_000_000)
+    ap.add_argument("--icp-iters", type=int, default=30)
+    ap.add_argument("--ransac-iters", type=int, default=1000)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    return world, rank, dev
+
+
+def barrier(world, dev):
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pmc_traffic(path, kernel):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get("kernels", {}).get(kernel)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def cpu_baseline(n_cpu: int):
+    """Oracle restatement of Open3D's CPU path (voxel trace single-threaded as in
+    Open3D, KNN30 normals with OpenMP) on a bounded C2-shaped sample."""
+    from oracle import oracle as O
+
+    pts = synthetic.uniform_cube(n_cpu, seed=0).numpy()
+    vs = synthetic.voxel_size_for(n_cpu)
+    O.lib()
+    t0 = time.perf_counter()
+    rep = O.voxel_down_sample(pts, vs)
+    t1 = time.perf_counter()
+    O.estimate_normals(pts[rep], O.KNN, 30)
+    t2 = time.perf_counter()
+    el = t2 - t0
+    return {"value": round(n_cpu / el / 1e6, 4), "unit": "Mpoints/s", "cores": O.num_threads(),
+            "kind": "port",
+            "sample": (f"C2 shape at N={n_cpu} (uniform cube, vs=(4/N)^(1/3), M={len(rep)}): "
+                       f"Open3D-equivalent C++ restatement (oracle/): voxel trace 1 thread "
+                       f"{t1 - t0:.2f}s + KD-tree KNN30 normals {O.num_threads()} OpenMP threads "
+                       f"{t2 - t1:.2f}s; host {platform.processor() or platform.machine()}"),
+            "seconds": round(el, 3)}
+
+
+def secondary(dev, args):
+    """C3 on one GPU: RANSAC 1000 hypotheses and point-to-plane ICP, 10M points."""
+    out = {}
+    n = args.icp_n
+    _native.set_kernel_timing(True)
+    # RANSAC: planted plane, Open3D RandomSampler samples, full hypothesis sweep
+    pts = synthetic.planted_plane(n, seed=1, device=dev)
+    samples = ops.ransac_samples(n, 3, args.ransac_iters, seed=7)
+    ops.segment_plane(pts, 0.01, 3, args.ransac_iters, samples=samples)  # warm
+    _native.reset_kernel_timing()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    plane, inl = ops.segment_plane(pts, 0.01, 3, args.ransac_iters, samples=samples)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    pc_ms, pc_n = _native.kernel_timing("plane_count")
+    pairs = float(n) * args.ransac_iters
+    out["ransac"] = {"n": n, "iterations": args.ransac_iters, "ms": round((t1 - t0) * 1e3, 3),
+                     "plane_count_kernel_ms": round(pc_ms, 3), "inliers": int(inl.numel()),
+                     "plane": [round(float(v), 6) for v in plane],
+                     "Gpairs_per_s": round(pairs / (pc_ms * 1e-3) / 1e9, 2) if pc_ms > 0 else None}
+    del pts, inl
+    # ICP: box-surface target with KNN30 normals, source = independent sample moved by T_gt
+    tgt = synthetic.box_surface(n, seed=1, device=dev)
+    src = synthetic.apply_transform(synthetic.box_surface(n, seed=2, device=dev), synthetic.rigid_transform())
+    t0 = time.perf_counter()
+    tn = ops.estimate_normals(tgt, knn=30)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    target = ops.ICPTarget(tgt, tn, 0.02)
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    T = np.eye(4)
+    sums, _ = target.accumulate(src, T)  # warm
+    _native.reset_kernel_timing()
+    torch.cuda.synchronize(dev)
+    t3 = time.perf_counter()
+    for _ in range(args.icp_iters):
+        sums, _ = target.accumulate(src, T)
+        T = ops.icp_solve(sums) @ T
+    torch.cuda.synchronize(dev)
+    t4 = time.perf_counter()
+    acc_ms, acc_n = _native.kernel_timing("icp_accumulate")
+    _native.set_kernel_timing(False)
+    err = np.abs(T - np.linalg.inv(synthetic.rigid_transform())).max()
+    out["icp"] = {"n_source": n, "n_target": n, "iterations": args.icp_iters,
+                  "iters_per_s": round(args.icp_iters / (t4 - t3), 3),
+                  "ms_per_iter": round((t4 - t3) / args.icp_iters * 1e3, 3),
+                  "accumulate_kernel_ms": round(acc_ms / max(acc_n, 1), 3),
+                  "target_normals_s": round(t1 - t0, 3), "target_build_s": round(t2 - t1, 3),
+                  "fitness": round(float(sums[28]) / n, 6), "T_err_vs_gt_inverse": float(err),
+                  "achieved_GBs_36B_per_src_pt": round(36.0 * n / (acc_ms / max(acc_n, 1) * 1e-3) / 1e9, 2)
+                  if acc_ms > 0 else None}
+    return out
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist()
+    N = args.n
+    vs = synthetic.voxel_size_for(N)
+    # this rank's tile: an independent 10M cloud, shifted to x in [rank, rank+1)
+    pts = synthetic.uniform_cube(N, seed=0, offset=rank * N, device=dev)
+    pts[:, 0] += float(rank)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        out = ops.voxel_down_sample(pts, vs)
+        nrm = ops.estimate_normals(out["rep_xyz"], knn=args.knn)
+        return out["rep_idx"].numel(), nrm
+
+    for _ in range(args.warmup):
+        M, _ = step()
+    _native.reset_kernel_timing()
+    _native.set_kernel_timing(True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        M, _ = step()
+    ev1.record()
+    barrier(world, dev)
+    t1 = time.perf_counter()
+    _native.set_kernel_timing(False)
+    elapsed = max_over_ranks(t1 - t0, world, dev)
+    ev_ms = ev0.elapsed_time(ev1)
+
+    kernels = {}
+    for name in ("voxel_assign", "voxel_compact", "grid_count", "grid_sort", "normals_knn"):
+        ms, cnt = _native.kernel_timing(name)
+        if cnt:
+            kernels[name] = {"avg_ms": round(ms / cnt, 4), "launches": cnt}
+    # algorithmic bytes per launch:
+    #   normals_knn : 12 B/rep read + 12 B/rep normal written
+    #   voxel_assign: 12 B/point read + 4 B/point voxel id written
+    algo_bytes = {"normals_knn": 24.0 * M, "voxel_assign": 16.0 * N}
+    dom = max((k for k in kernels if k in algo_bytes), key=lambda k: kernels[k]["avg_ms"], default=None)
+    roof = None
+    if dom is not None:
+        avg_s = kernels[dom]["avg_ms"] * 1e-3
+        ach = algo_bytes[dom] / avg_s / 1e9
+        traffic = pmc_traffic(args.pmc_json, dom)
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "algorithmic_bytes_per_launch": algo_bytes[dom]}
+
+    total_pts = float(N) * world * args.steps
+    value = total_pts / elapsed / 1e6
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C2: uniform-random 10M pts float32 per GPU, voxel_down_sample(vs=(4/N)^(1/3)) "
+                               "+ estimate_normals(KNN30) on the representatives",
+                   "n_points_per_gpu": N, "voxel_size": vs, "voxels_per_gpu": int(M), "knn": args.knn,
+                   "parallelism": f"tile-per-gpu x{world}"},
+        "roofline": roof,
+        "cpu_baseline": None,
+        "extra": {"stream_event_ms_per_step_rank0": round(ev_ms / args.steps, 3), "kernels": kernels,
+                  "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps * world / elapsed / 1e9, 2),
+                  "storage_dtype": "f32", "arith": "float64 voxel keys / distances / covariance"},
+    }
+    if rank == 0 and world == 1 and not args.no_secondary:
+        del pts
+        torch.cuda.empty_cache()
+        try:
+            line["extra"].update(secondary(dev, args))
+        except RuntimeError as e:  # report, never hide
+            line["extra"]["secondary_error"] = str(e)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_n)
+        if line["cpu_baseline"]["value"] > 0:
+            line["extra"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -66,6 +66,16 @@ extern "C" {
 int o3dx_abi_version(void);
 const char* o3dx_last_error(void);
 
+/* Kernel timing (measurement support, off by default): when enabled, the
+ * library brackets its main kernel launches with hipEvents on the launch
+ * stream; o3dx_kernel_timing() waits for the pending events and returns the
+ * accumulated milliseconds and launch count of one kernel by name
+ * ("voxel_assign", "normals_knn", "grid_build", "plane_count",
+ * "icp_accumulate", ...).  Returns 0 if the name was seen, -1 otherwise. */
+void o3dx_set_kernel_timing(int enable);
+void o3dx_reset_kernel_timing(void);
+int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches);
+
 /* ---------------------------------------------------------------- AABB
  * Replaces o3d.geometry.PointCloud.get_min_bound()/get_max_bound()
  * (reference PointCloud.py:145-146, :340).

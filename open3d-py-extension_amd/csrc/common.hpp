@@ -123,6 +123,31 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
   return r;  // valid in thread 0
 }
 
+// ---------------------------------------------------------- kernel timing
+// RAII bracket of a launch with hipEvents on its stream (only when enabled by
+// o3dx_set_kernel_timing); read back lazily by o3dx_kernel_timing.
+bool timing_on();
+void timing_push(const char* name, hipEvent_t a, hipEvent_t b);
+struct KTimer {
+  const char* name;
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  KTimer(const char* n, hipStream_t st) : name(n), s(st) {
+    if (timing_on() && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+      (void)hipEventRecord(a, s);
+    else
+      a = b = nullptr;
+  }
+  void stop() {
+    if (a && b) {
+      (void)hipEventRecord(b, s);
+      timing_push(name, a, b);
+    }
+    a = b = nullptr;
+  }
+  ~KTimer() { stop(); }
+};
+
 // ---------------------------------------------------------- host helpers
 // Exclusive scan of `n` int32 counts into `out` (n+1 entries, out[n] = total).
 // Workspace: scan_workspace_ints(n) ints.
@@ -135,6 +160,12 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp,
 size_t compact_workspace_ints(int64_t n);
 int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* pos_out,
                   int64_t* count_dev, int32_t* tmp, hipStream_t s);
+
+// Column reduction of a row-major partials matrix part[rows][width] -> out[width]
+// with a fixed summation order (deterministic).  One block per 64 columns.
+enum class RedOp { kSumF64, kSumI64, kMinF32, kMaxF32 };
+int reduce_columns_f64(const double* part, int64_t rows, int width, double* out, hipStream_t s);
+int reduce_columns_i32_to_i64(const int32_t* part, int64_t rows, int width, int64_t* out, hipStream_t s);
 
 // AABB on device into a device double[6] (no sync).
 size_t aabb_ws_bytes(int64_t n);

@@ -3,10 +3,49 @@
 // AABB replaces o3d PointCloud.get_min_bound/get_max_bound
 // (reference open3dpypro/PointCloud.py:145-146, :340).  HBM-bound: 12 B/point.
 #include <cstdarg>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "common.hpp"
 
 namespace o3dx {
+
+// ------------------------------------------------------------ kernel timing
+static bool g_timing = false;
+static std::mutex g_tmu;
+struct Pending {
+  std::string name;
+  hipEvent_t a, b;
+};
+static std::vector<Pending> g_pending;
+static std::map<std::string, std::pair<double, int64_t>> g_times;
+
+bool timing_on() { return g_timing; }
+
+void timing_push(const char* name, hipEvent_t a, hipEvent_t b) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_pending.push_back({name, a, b});
+}
+
+static void timing_drain() {
+  std::vector<Pending> p;
+  {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    p.swap(g_pending);
+  }
+  for (auto& e : p) {
+    float ms = 0.f;
+    if (hipEventSynchronize(e.b) == hipSuccess && hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+      std::lock_guard<std::mutex> lk(g_tmu);
+      auto& t = g_times[e.name];
+      t.first += ms;
+      t.second += 1;
+    }
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+}
 
 static thread_local std::string g_err;
 
@@ -175,6 +214,41 @@ int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* po
   return 0;
 }
 
+// -------------------------------------------------------- column reductions
+// block = 64 columns x 16 row-groups; each thread sums its row-group's rows in
+// order, then the 16 group partials are added in group order.
+template <class T, class R>
+__global__ void __launch_bounds__(1024) k_reduce_columns(const T* __restrict__ part, int64_t rows, int width,
+                                                         R* __restrict__ out) {
+  __shared__ R sh[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  R acc = 0;
+  if (c < width)
+    for (int64_t r = g; r < rows; r += 16) acc += (R)part[r * width + c];
+  sh[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g == 0 && c < width) {
+    R t = 0;
+    for (int k = 0; k < 16; ++k) t += sh[k][threadIdx.x & 63];
+    out[c] = t;
+  }
+}
+
+int reduce_columns_f64(const double* part, int64_t rows, int width, double* out, hipStream_t s) {
+  hipLaunchKernelGGL((k_reduce_columns<double, double>), dim3((width + 63) / 64), dim3(1024), 0, s, part, rows, width,
+                     out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+int reduce_columns_i32_to_i64(const int32_t* part, int64_t rows, int width, int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL((k_reduce_columns<int32_t, int64_t>), dim3((width + 63) / 64), dim3(1024), 0, s, part, rows,
+                     width, out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
 // ------------------------------------------------------------------- AABB
 constexpr int kAabbBlocks = 1024;
 
@@ -220,16 +294,22 @@ __global__ void __launch_bounds__(kBlock) k_aabb_partial(const float* __restrict
   }
 }
 
-__global__ void k_aabb_final(const float* __restrict__ part, int nb, int64_t n, double* __restrict__ mm) {
-  int a = threadIdx.x;
-  if (a >= 6) return;
-  if (n == 0) {
-    mm[a] = 0.0;
-    return;
+__global__ void __launch_bounds__(1024) k_aabb_final(const float* __restrict__ part, int nb, int64_t n,
+                                                     double* __restrict__ mm) {
+  // 6 columns x 170 row-groups; min/max are order-independent
+  __shared__ float sh[6][171];
+  const int a = threadIdx.x % 6, g = threadIdx.x / 6;
+  if (g < 170) {
+    float r = a < 3 ? INFINITY : -INFINITY;
+    for (int b = g; b < nb; b += 170) r = a < 3 ? fminf(r, part[b * 6 + a]) : fmaxf(r, part[b * 6 + a]);
+    sh[a][g] = r;
   }
-  float r = part[a];
-  for (int b = 1; b < nb; ++b) r = a < 3 ? fminf(r, part[b * 6 + a]) : fmaxf(r, part[b * 6 + a]);
-  mm[a] = (double)r;
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float r = sh[a][0];
+    for (int k = 1; k < 170; ++k) r = a < 3 ? fminf(r, sh[a][k]) : fmaxf(r, sh[a][k]);
+    mm[a] = n == 0 ? 0.0 : (double)r;
+  }
 }
 
 size_t aabb_ws_bytes(int64_t) { return Arena::align(kAabbBlocks * 6 * sizeof(float)) + 256; }
@@ -238,7 +318,7 @@ int aabb_device(const float* xyz, int64_t n, double* mm_dev, void* ws, hipStream
   float* part = reinterpret_cast<float*>(ws);
   int nb = (int)std::min<int64_t>(kAabbBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
   hipLaunchKernelGGL(k_aabb_partial, dim3(nb), dim3(kBlock), 0, s, xyz, n, part);
-  hipLaunchKernelGGL(k_aabb_final, dim3(1), dim3(64), 0, s, part, nb, n, mm_dev);
+  hipLaunchKernelGGL(k_aabb_final, dim3(1), dim3(1024), 0, s, part, nb, n, mm_dev);
   O3DX_HIP(hipGetLastError());
   return 0;
 }
@@ -248,6 +328,31 @@ int aabb_device(const float* xyz, int64_t n, double* mm_dev, void* ws, hipStream
 using namespace o3dx;
 
 extern "C" int o3dx_abi_version(void) { return O3DX_ABI_VERSION; }
+
+extern "C" void o3dx_set_kernel_timing(int enable) {
+  if (!enable) timing_drain();
+  g_timing = enable != 0;
+}
+
+extern "C" void o3dx_reset_kernel_timing(void) {
+  timing_drain();
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_times.clear();
+}
+
+extern "C" int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches) {
+  timing_drain();
+  std::lock_guard<std::mutex> lk(g_tmu);
+  auto it = g_times.find(name ? name : "");
+  if (it == g_times.end()) {
+    if (total_ms) *total_ms = 0;
+    if (launches) *launches = 0;
+    return -1;
+  }
+  if (total_ms) *total_ms = it->second.first;
+  if (launches) *launches = it->second.second;
+  return 0;
+}
 
 extern "C" const char* o3dx_last_error(void) { return g_err.c_str(); }
 

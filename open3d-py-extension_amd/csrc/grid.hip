@@ -182,6 +182,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     // assignment error of a float32 cell computation, both sides of a face
     g.slack = (float)(32.0 * std::ldexp(1.0, -24) * (maxabs + maxext) + 1e-6 * h);
     const int64_t nc = d[0] * d[1] * d[2];
+    KTimer kt_count("grid_count", s);
     O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
     if (n > 0)
       hipLaunchKernelGGL(k_grid_count, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, g, G.count,
@@ -205,6 +206,8 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
         }
       }
     }
+    kt_count.stop();
+    KTimer kt_sort("grid_sort", s);
     O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));
     if (n > 0) {
       hipLaunchKernelGGL(k_grid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, G.cell, G.rank,
@@ -541,6 +544,7 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
   double min_h = (mode == O3DX_SEARCH_KNN) ? 0.0 : 0.0;
   O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), min_h, ws, ws_bytes, s, &G));
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  KTimer kt("normals_knn", s);
   if (mode == O3DX_SEARCH_RADIUS) {
     hipLaunchKernelGGL(k_normals_radius, dim3(grid), dim3(kBlock), 0, s, G.view, radius, prior, out);
   } else {

@@ -75,14 +75,6 @@ __global__ void __launch_bounds__(kBlock) k_icp_accumulate(const float* __restri
   if (threadIdx.x < kNS - 30) partial[(int64_t)blockIdx.x * kNS + 30 + threadIdx.x] = 0.0;
 }
 
-__global__ void k_icp_final(const double* __restrict__ partial, int nb, double* __restrict__ out) {
-  int k = threadIdx.x;
-  if (k >= kNS) return;
-  double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * kNS + k];
-  out[k] = s;
-}
-
 __global__ void __launch_bounds__(kBlock) k_corr_flags(const int32_t* __restrict__ cj, int64_t ns,
                                                        uint8_t* __restrict__ flags) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x)
@@ -239,12 +231,14 @@ static int accumulate(const float* src, int64_t ns, const GridView& g, const flo
   std::memcpy(M.m, T, sizeof(M.m));
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kIcpBlocks, (ns + kBlock - 1) / kBlock));
   const bool want_corr = corr_out != nullptr;
+  KTimer kt("icp_accumulate", s);
   if (ns > 0)
     hipLaunchKernelGGL(k_icp_accumulate, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, radius, w.partial,
                        want_corr ? w.cj : (int32_t*)nullptr);
   else
     O3DX_HIP(hipMemsetAsync(w.partial, 0, kNS * sizeof(double), s));
-  hipLaunchKernelGGL(k_icp_final, dim3(1), dim3(64), 0, s, w.partial, ns > 0 ? nb : 1, w.sums);
+  O3DX_TRY(reduce_columns_f64(w.partial, ns > 0 ? nb : 1, kNS, w.sums, s));
+  kt.stop();
   O3DX_HIP(hipMemcpyAsync(sums_host, w.sums, kNS * sizeof(double), hipMemcpyDeviceToHost, s));
   if (want_corr && ns > 0) {
     hipLaunchKernelGGL(k_corr_flags, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, ns, w.flags);

@@ -82,13 +82,9 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
   for (int h = threadIdx.x; h < hc; h += kBlock) partial[(int64_t)blockIdx.x * H + h0 + h] = cnt[h];
 }
 
-__global__ void k_plane_count_reduce(const int32_t* __restrict__ partial, int nb, int H,
-                                     const uint8_t* __restrict__ degenerate, int64_t* __restrict__ counts) {
+__global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H, int64_t* __restrict__ counts) {
   int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= H) return;
-  int64_t s = 0;
-  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * H + h];
-  counts[h] = degenerate[h] ? -1 : s;
+  if (h < H && degenerate[h]) counts[h] = -1;
 }
 
 constexpr int kSumBlocksX = 64;
@@ -148,14 +144,6 @@ __global__ void __launch_bounds__(kBlock) k_plane_moments(const float* __restric
     double r = block_sum_f64<kBlock>(acc[k], sh);
     if (threadIdx.x == 0) partial[blockIdx.x * 6 + k] = r;
   }
-}
-
-__global__ void k_sum_partials(const double* __restrict__ partial, int nb, int width, double* __restrict__ out) {
-  int k = threadIdx.x;
-  if (k >= width) return;
-  double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += partial[b * width + k];
-  out[k] = s;
 }
 
 __global__ void k_gather_samples(const float* __restrict__ xyz, const int32_t* __restrict__ idx, int64_t m,
@@ -308,12 +296,15 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, s, &rc);
   if (rc) return rc;
   const int nb = count_blocks(n);
+  KTimer kt("plane_count", s);
   for (int h0 = 0; h0 < H; h0 += kHChunk) {
     int hc = std::min(kHChunk, H - h0);
     hipLaunchKernelGGL(k_plane_count, dim3(nb), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, h0, hc, thr,
                        w.partial);
   }
-  hipLaunchKernelGGL(k_plane_count_reduce, dim3((H + 255) / 256), dim3(256), 0, s, w.partial, nb, H, w.degen, w.counts);
+  O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nb, H, w.counts, s));
+  hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
+  kt.stop();
   counts.resize(H);
   O3DX_HIP(hipMemcpyAsync(counts.data(), w.counts, H * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   O3DX_HIP(hipStreamSynchronize(s));
@@ -393,7 +384,7 @@ static int run_moments(const float* xyz, const int32_t* idx, int64_t m, const do
   const int nb = (int)std::min<int64_t>(kMomBlocks, (m + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(k_plane_moments, dim3(nb), dim3(kBlock), 0, s, xyz, idx, m, centroid ? centroid[0] : 0.0,
                      centroid ? centroid[1] : 0.0, centroid ? centroid[2] : 0.0, centroid ? 1 : 0, part);
-  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, s, part, nb, 6, out_dev);
+  O3DX_TRY(reduce_columns_f64(part, nb, 6, out_dev, s));
   O3DX_HIP(hipMemcpyAsync(out, out_dev, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
   O3DX_HIP(hipStreamSynchronize(s));
   O3DX_HIP(hipGetLastError());

@@ -246,19 +246,25 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
     if (dense) {
       nslots = (int64_t)nvox;
       O3DX_HIP(hipMemsetAsync(w.table, 0xFF, nslots * sizeof(int32_t), s));
+      KTimer kt("voxel_assign", s);
       hipLaunchKernelGGL(k_voxel_assign_dense, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.table, w.vid,
                          reinterpret_cast<int*>(w.count + 1));
     } else {
       nslots = hash_cap(n);
       O3DX_HIP(hipMemsetAsync(w.table, 0xFF, nslots * sizeof(int32_t), s));
       O3DX_HIP(hipMemsetAsync(w.keys, 0xFF, nslots * sizeof(uint64_t), s));
+      KTimer kt("voxel_assign", s);
       hipLaunchKernelGGL(k_voxel_assign_hash, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.keys, w.table,
                          (uint32_t)(nslots - 1), w.vid, reinterpret_cast<int*>(w.count + 1));
     }
-    O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
-    hipLaunchKernelGGL(k_voxel_mark, dim3(grid_for(nslots, kBlock, 8192)), dim3(kBlock), 0, s, w.table, nslots,
-                       w.flags);
-    O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count, w.scan_tmp, s));
+    {
+      KTimer kt("voxel_compact", s);
+      O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
+      hipLaunchKernelGGL(k_voxel_mark, dim3(grid_for(nslots, kBlock, 8192)), dim3(kBlock), 0, s, w.table, nslots,
+                         w.flags);
+      O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
+                             w.scan_tmp, s));
+    }
     O3DX_HIP(hipMemcpyAsync(counts, w.count, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     O3DX_HIP(hipStreamSynchronize(s));
     int errflag = (int)(counts[1] & 0xffffffff);

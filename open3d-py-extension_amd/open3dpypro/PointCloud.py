@@ -1,0 +1,797 @@
+"""PointCloud — drop-in for open3dpypro.PointCloud (reference
+/root/reference/open3dpypro/PointCloud.py), without Open3D.
+
+Storage: points / normals / colors live on the GPU as float32 (N,3) torch
+tensors (the kernels' input layout); a float64 host copy of the points is kept
+when the caller supplied host data, so get_points() round-trips the caller's
+values exactly, as Open3D's float64 storage does.  intensity / labels /
+row / column indices are plain numpy attributes, as in the reference.
+
+The hot-path methods call libo3dx.so (ops.py); there is no CPU fallback —
+without an MI355X they raise RuntimeError.  Host-only helpers (selections by
+numpy predicate, splitting, I/O) run anywhere.
+"""
+from __future__ import annotations
+
+import os
+import uuid
+from typing import Callable, List, Tuple
+
+import numpy as np
+import torch
+
+from . import ops, pcd_io
+from . import _native as N
+from .params import KDTreeSearchParamKNN, resolve
+
+_SEED = [None]
+
+
+def set_random_seed(seed: int):
+    """Counterpart of o3d.utility.random.seed: seeds segment_plane's sampler."""
+    _SEED[0] = int(seed)
+
+
+def _next_seed() -> int:
+    if _SEED[0] is None:
+        return int(np.random.SeedSequence().entropy) & 0xFFFFFFFF
+    s = _SEED[0]
+    _SEED[0] = (s * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
+    return s & 0xFFFFFFFF
+
+
+def _device() -> torch.device:
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+def _as_np(a) -> np.ndarray:
+    if isinstance(a, torch.Tensor):
+        return a.detach().cpu().numpy()
+    return np.asarray(a)
+
+
+def _check3(a, what):
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise AssertionError(f"{what} shape must be (n,3)")
+
+
+class RegistrationResult:
+    """Mirror of o3d.pipelines.registration.RegistrationResult."""
+
+    def __init__(self, transformation, fitness, inlier_rmse, correspondence_set):
+        self.transformation = transformation
+        self.fitness = fitness
+        self.inlier_rmse = inlier_rmse
+        self.correspondence_set = correspondence_set
+
+    def __repr__(self):
+        return (f"RegistrationResult with fitness={self.fitness:e}, inlier_rmse={self.inlier_rmse:e}, "
+                f"and correspondence_set size of {len(self.correspondence_set)}")
+
+
+class KDTreeGrid:
+    """Stand-in for o3d.geometry.KDTreeFlann (reference PointCloud.py:148-163):
+    the same search_* methods and return shapes, backed by the GPU grid search."""
+
+    def __init__(self, cloud: "PointCloudBase"):
+        self._x = cloud._dev_points()
+
+    def _one(self, query, mode, knn, radius):
+        q = torch.as_tensor(np.asarray(query, np.float32).reshape(1, 3), device=self._x.device)
+        idx, d2, cnt = ops.knn_search(self._x, q, mode=mode, knn=knn, radius=radius)
+        k = int(cnt[0].item())
+        return k, idx[0, :k].cpu().numpy().astype(np.int64), d2[0, :k].cpu().numpy()
+
+    def search_knn_vector_3d(self, query, knn: int):
+        if knn <= N.MAX_KNN:
+            return self._one(query, N.SEARCH_KNN, knn, 0.0)
+        return self._brute(query, knn, None)
+
+    def search_hybrid_vector_3d(self, query, radius: float, max_nn: int):
+        if max_nn <= N.MAX_KNN:
+            return self._one(query, N.SEARCH_HYBRID, max_nn, radius)
+        return self._brute(query, max_nn, radius)
+
+    def search_radius_vector_3d(self, query, radius: float):
+        return self._brute(query, None, radius)
+
+    def _brute(self, query, knn, radius):
+        # large-k / radius queries: the grid search is register-bounded to
+        # O3DX_MAX_KNN; answer with the exact kNN of the whole cloud instead
+        x = self._x
+        k = x.shape[0] if knn is None else min(int(knn), x.shape[0])
+        q = torch.as_tensor(np.asarray(query, np.float32).reshape(1, 3), device=x.device)
+        d = x.double() - q.double()
+        d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+        order = torch.argsort(d2, stable=True)[:k]
+        dd = d2[order]
+        if radius is not None:
+            keep = dd < radius * radius
+            order, dd = order[keep], dd[keep]
+        return int(order.numel()), order.cpu().numpy(), dd.cpu().numpy()
+
+
+class PointCloudBase:
+    COLOR_CHART = np.asarray([[230, 0, 18], [243, 152, 0], [252, 200, 0], [143, 195, 31], [0, 153, 68],
+                              [0, 160, 233], [29, 32, 136], [146, 7, 131], [228, 0, 127]])
+
+    def __init__(self, xyz=None, rgb=None, normals=None, intensity=None, labels=None, row_index=None,
+                 column_index=None, e57=None):
+        self.e57 = None
+        self.intensity = []
+        self.labels = []
+        self.row_index = []
+        self.column_index = []
+        self._pts = None        # (N,3) float32 tensor on the device
+        self._pts_host = None   # (N,3) float64 exact host copy (when supplied from host)
+        self._normals = None    # (N,3) float32 tensor
+        self._colors = None     # (N,3) float32 tensor in [0,1]
+        self.pcd_tree = None
+        self.scan_No = -1
+        self.uuid = uuid.uuid4()
+
+        if isinstance(xyz, PointCloudBase):
+            self._copy_from(xyz)
+            return
+        if xyz is not None and hasattr(xyz, "points") and not isinstance(xyz, (np.ndarray, torch.Tensor)):
+            # an open3d.geometry.PointCloud (or anything shaped like one)
+            pts = np.asarray(xyz.points)
+            normals = np.asarray(xyz.normals) if len(getattr(xyz, "normals", [])) else normals
+            rgb = np.asarray(xyz.colors) if len(getattr(xyz, "colors", [])) else rgb
+            xyz = pts
+
+        def ok(a):
+            return a is not None and len(a) > 0 and np.prod(a.shape) > 0
+
+        if ok(intensity):
+            self.set_intensity(intensity)
+        if ok(labels):  # accepted but silently dropped by the reference's __init__
+            self.set_labels(labels)
+        if ok(row_index):
+            self.row_index = row_index
+        if ok(column_index):
+            self.column_index = column_index
+        if ok(xyz):
+            self.set_points(xyz)
+        if ok(normals):
+            self.set_normals(normals)
+        if ok(rgb):
+            rgb = _as_np(rgb)
+            if rgb.max() > 1.0 or rgb.min() < 0.0:   # reference PointCloud.py:36-40
+                rgb = rgb * 1.0
+                rgb = (rgb - rgb.min()) / (rgb.max() - rgb.min())
+            self.set_rgb(rgb)
+
+    # ----------------------------------------------------------- storage
+    def _copy_from(self, other: "PointCloudBase"):
+        self._pts = other._pts
+        self._pts_host = other._pts_host
+        self._normals = other._normals
+        self._colors = other._colors
+        self.intensity = other.intensity
+        self.labels = other.labels
+        self.row_index = other.row_index
+        self.column_index = other.column_index
+
+    def _dev_points(self) -> torch.Tensor:
+        """float32 (N,3) device tensor — the kernels' input."""
+        if self._pts is None:
+            return torch.zeros((0, 3), dtype=torch.float32, device=_device())
+        if self._pts.device.type != "cuda" and torch.cuda.is_available():
+            self._pts = self._pts.to(_device())
+        return self._pts
+
+    @staticmethod
+    def _to_dev(a, dtype=torch.float32) -> torch.Tensor:
+        if isinstance(a, torch.Tensor):
+            t = a.detach()
+            if t.device.type == "cpu" and torch.cuda.is_available():
+                t = t.to(_device())
+            return t.to(dtype).contiguous()
+        return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=_device())
+
+    def clear(self):
+        self.__init__()
+        return self
+
+    def size(self) -> int:
+        return 0 if self._pts is None else int(self._pts.shape[0])
+
+    def has_points(self) -> bool:
+        return self.size() > 0
+
+    def is_empty(self) -> bool:
+        return not self.has_points()
+
+    def has_colors(self) -> bool:
+        return self._colors is not None and len(self._colors) > 0
+
+    def get_center(self) -> np.ndarray:
+        return self.get_points().mean(0) if self.has_points() else np.zeros(3)
+
+    def transform(self, T: np.ndarray):
+        """p <- (T @ [p;1])[:3] / w ; normals <- R n (Open3D Geometry3D::Transform)."""
+        T = np.asarray(T, np.float64).reshape(4, 4)
+        if self.has_points():
+            if self._pts_host is not None:
+                h = self._pts_host @ T[:3, :3].T + T[:3, 3]
+                w = self._pts_host @ T[3, :3] + T[3, 3]
+                self.set_points(h / w[:, None])
+            else:
+                Tt = torch.as_tensor(T, dtype=torch.float64, device=self._pts.device)
+                p = self._pts.double()
+                h = p @ Tt[:3, :3].T + Tt[:3, 3]
+                w = p @ Tt[3, :3] + Tt[3, 3]
+                self._pts = (h / w[:, None]).float().contiguous()
+        if self._normals is not None:
+            R = torch.as_tensor(T[:3, :3], dtype=torch.float64, device=self._normals.device)
+            self._normals = (self._normals.double() @ R.T).float().contiguous()
+        self.pcd_tree = None
+        return self
+
+    def translate(self, t: np.ndarray, relative: bool = True):
+        t = np.asarray(t, np.float64).reshape(3)
+        if not relative:
+            t = t - self.get_center()
+        T = np.eye(4)
+        T[:3, 3] = t
+        return self.transform(T)
+
+    def rotate(self, R: np.ndarray, center=None):
+        R = np.asarray(R, np.float64).reshape(3, 3)
+        c = self.get_center() if center is None else np.asarray(center, np.float64)
+        T = np.eye(4)
+        T[:3, :3] = R
+        T[:3, 3] = c - R @ c
+        return self.transform(T)
+
+    # ------------------------------------------------------------ hot path
+    def estimate_normals(self, method="default", param=KDTreeSearchParamKNN(30)):
+        """Open3D EstimateNormals(param, fast_normal_computation=True) on the GPU
+        (reference PointCloud.py:68-73).  Existing normals orient the result."""
+        if method == "poisson":
+            raise NotImplementedError("orient_normals_consistent_tangent_plane is outside the GPU hot path")
+        mode, knn, radius = resolve(param)
+        x = self._dev_points()
+        prior = self._normals if self.has_normals() else None
+        self._normals = ops.estimate_normals(x, mode=mode, knn=knn, radius=radius, prior=prior)
+        return self
+
+    def segment_plane(self, thickness: float = 0.01, ransac_n: int = 3, num_iterations: int = 450,
+                      probability: float = 0.99999999, seed=None, samples=None) -> Tuple[List, List[int]]:
+        """Open3D SegmentPlane (reference PointCloud.py:75-77) -> ([a,b,c,d], inlier indices)."""
+        x = self._dev_points()
+        n = x.shape[0]
+        if samples is None and n >= ransac_n >= 3 and 0 < probability <= 1:
+            samples = ops.ransac_samples(n, ransac_n, num_iterations, _next_seed() if seed is None else seed)
+        plane, inl = ops.segment_plane(x, thickness, ransac_n, num_iterations, probability, samples=samples)
+        a, b, c, d = (float(v) for v in plane)
+        return [a, b, c, d], inl.cpu().numpy().astype(np.int64).tolist()
+
+    def get_aabb(self):
+        if not self.has_points():
+            return np.zeros(3), np.zeros(3)
+        if self._pts_host is not None and not torch.cuda.is_available():
+            raise RuntimeError("get_aabb needs the ROCm GPU (no CPU path)")
+        return ops.aabb(self._dev_points())
+
+    # ---------------------------------------------------------------- has
+    def has_rgb(self) -> bool:
+        return self.has_points() and self._colors is not None and self.size() == len(self._colors)
+
+    def has_normals(self) -> bool:
+        return self.has_points() and self._normals is not None and self.size() == len(self._normals)
+
+    def has_intensity(self) -> bool:
+        return self.has_points() and self.size() == len(self.intensity)
+
+    def has_labels(self) -> bool:
+        return self.has_points() and self.size() == len(self.labels)
+
+    def has_col_row(self) -> bool:
+        return self.has_points() and self.size() == len(self.column_index) == len(self.row_index)
+
+    # ---------------------------------------------------------- set / get
+    def set_rgb(self, colors):
+        c = colors if isinstance(colors, torch.Tensor) else np.asarray(colors)
+        _check3(c, "colors")
+        self._colors = self._to_dev(c)
+        return self
+
+    def set_points(self, points):
+        if isinstance(points, torch.Tensor):
+            _check3(points, "points")
+            self._pts = self._to_dev(points)
+            self._pts_host = None
+        else:
+            p = np.asarray(points)
+            _check3(p, "points")
+            self._pts_host = np.ascontiguousarray(p, dtype=np.float64)
+            self._pts = self._to_dev(self._pts_host.astype(np.float32))
+        self.pcd_tree = None
+        return self
+
+    def set_normals(self, normals):
+        nrm = normals if isinstance(normals, torch.Tensor) else np.asarray(normals)
+        _check3(nrm, "normals")
+        self._normals = self._to_dev(nrm)
+        return self
+
+    def set_intensity(self, intensity: np.ndarray):
+        assert intensity.shape[1] == 1, "intensity shape must be (n,1)"
+        self.intensity = intensity
+        return self
+
+    def set_labels(self, labels: np.ndarray):
+        assert labels.shape[1] == 1, "labels shape must be (n,1)"
+        self.labels = labels
+        return self
+
+    def get_points(self) -> np.ndarray:
+        if self._pts_host is not None:
+            return self._pts_host.copy()
+        if self._pts is None:
+            return np.zeros((0, 3))
+        return self._pts.detach().cpu().numpy().astype(np.float64)
+
+    def get_colors(self) -> np.ndarray:
+        return np.zeros((0, 3)) if self._colors is None else self._colors.cpu().numpy().astype(np.float64)
+
+    def get_normals(self) -> np.ndarray:
+        return np.zeros((0, 3)) if self._normals is None else self._normals.cpu().numpy().astype(np.float64)
+
+    def get_intensity(self):
+        return self.intensity
+
+    def get_labels(self):
+        return self.labels
+
+    def get_col_row(self):
+        return (self.column_index, self.row_index)
+
+    def set_uniform_label(self, label: int):
+        self.labels = np.ones((self.size(), 1), dtype=int) * label
+        return self
+
+    def set_uniform_intensity(self, intensity: float):
+        self.set_intensity(np.ones((self.size(), 1), dtype=int) * intensity)
+        return self
+
+    # ------------------------------------------------------------- KD-tree
+    def calc_KDtree(self):
+        self.pcd_tree = KDTreeGrid(self)
+        return self.pcd_tree
+
+    def get_KDtree(self):
+        if self.pcd_tree is None:
+            self.calc_KDtree()
+        return self.pcd_tree
+
+    def get_points_by_knn(self, point_idx: int, max_nn: int = 1000000):
+        q = self.get_points()[point_idx]
+        return self.get_KDtree().search_knn_vector_3d(q, max_nn)
+
+    def get_points_radius(self, point_idx: int, search_radius: float = 30.0):
+        q = self.get_points()[point_idx]
+        return self.get_KDtree().search_radius_vector_3d(q, search_radius)
+
+    # ------------------------------------------------------------------ IO
+    def read_pcd(self, filename: str, format: str = "auto", remove_nan_points: bool = False,
+                 remove_infinite_points: bool = False, print_progress: bool = False):
+        ext = (os.path.splitext(filename)[1].lstrip(".") if format == "auto" else format).lower()
+        nrm = col = None
+        if ext == "pcd":
+            pts, nrm, col = pcd_io.read_pcd(filename, remove_nan_points, remove_infinite_points)
+        elif ext == "npy":
+            pts = np.load(filename, allow_pickle=False).reshape(-1, 3).astype(np.float64)
+        elif ext in ("xyz", "xyzn", "xyzrgb", "pts", "txt"):
+            a = np.loadtxt(filename, ndmin=2)
+            pts = a[:, :3]
+            if ext == "xyzn" and a.shape[1] >= 6:
+                nrm = a[:, 3:6]
+            if ext == "xyzrgb" and a.shape[1] >= 6:
+                col = a[:, 3:6]
+        else:
+            raise RuntimeError(f"read_pcd: unsupported format {ext!r}")
+        if ext != "pcd" and (remove_nan_points or remove_infinite_points):
+            keep = np.ones(len(pts), bool)
+            if remove_nan_points:
+                keep &= ~np.isnan(pts).any(1)
+            if remove_infinite_points:
+                keep &= ~np.isinf(pts).any(1)
+            pts = pts[keep]
+            nrm = nrm[keep] if nrm is not None else None
+            col = col[keep] if col is not None else None
+        return self.__class__(pts, rgb=col, normals=nrm)
+
+    def save_pcd(self, filename: str, write_ascii: bool = False, compressed: bool = False,
+                 print_progress: bool = False):
+        return pcd_io.write_pcd(filename, self.get_points(), self.get_normals() if self.has_normals() else None,
+                                self.get_colors() if self.has_rgb() else None, write_ascii=write_ascii)
+
+    def draw(self, geos=[], point_size: int = 1, centralize: bool = False):
+        raise NotImplementedError("visualisation is outside the GPU hot path (reference PointCloud.py:172-178)")
+
+
+class PointCloudSelections(PointCloudBase):
+
+    def clone(self, invert: bool = False):
+        return self._select_by_idx(np.arange(self.size()), invert=invert)
+
+    def _select_by_idx(self, indices, invert: bool = False):
+        """Boolean-mask gather of every per-point attribute; output keeps ascending
+        original index order (reference PointCloud.py:185-204)."""
+        res = self.__class__()
+        n = self.size()
+        if isinstance(indices, torch.Tensor):
+            dev = self._pts.device if self._pts is not None else indices.device
+            mask = torch.zeros(n, dtype=torch.bool, device=dev)
+            if indices.numel():
+                mask[indices.to(dev).long()] = True
+        else:
+            idx = np.asarray(indices, dtype=np.int64).reshape(-1)
+            mask = torch.zeros(n, dtype=torch.bool, device=self._pts.device if self._pts is not None else "cpu")
+            if idx.size:
+                mask[torch.as_tensor(idx, device=mask.device)] = True
+        if invert:
+            mask = ~mask
+        sel = torch.nonzero(mask).reshape(-1)
+        if self.has_points():
+            res._pts = self._pts.index_select(0, sel).contiguous()
+            if self._pts_host is not None:
+                res._pts_host = self._pts_host[sel.cpu().numpy()]
+        if self.has_rgb():
+            res._colors = self._colors.index_select(0, sel.to(self._colors.device)).contiguous()
+        if self.has_normals():
+            res._normals = self._normals.index_select(0, sel.to(self._normals.device)).contiguous()
+        hm = None
+        if self.has_intensity() or self.has_labels():
+            hm = mask.cpu().numpy()
+        if self.has_intensity():
+            res.intensity = self.intensity[hm].copy()
+        if self.has_labels():
+            res.labels = self.labels[hm].copy()
+        return res
+
+    def select_by_box(self, center, x_direction, y_direction, z_direction, invert: bool = False):
+        dirs = [np.asarray(d, np.float64) / np.linalg.norm(d) for d in (x_direction, y_direction, z_direction)]
+        half = [np.linalg.norm(d) ** 2 for d in dirs]
+        v = self.get_points() - np.asarray(center)
+        inside = np.logical_and.reduce([np.square(v @ d) < h for d, h in zip(dirs, half)])
+        return self.select_by_bool(inside, invert=invert)
+
+    def _bool2index(self, bools, invert: bool = False) -> np.ndarray:
+        b = np.asarray(bools)
+        if invert:
+            b = np.logical_not(b)
+        return np.where(b)[0]
+
+    def select_by_bool(self, bools, invert: bool = False):
+        return self._select_by_idx(self._bool2index(bools), invert=invert)
+
+    def get_index_by_normals(self, comfunc: Callable = lambda ns: np.ones(len(ns), dtype=bool), invert=False):
+        if not self.has_normals():
+            self.estimate_normals()
+        return self._bool2index(comfunc(self.get_normals()), invert=invert)
+
+    def select_by_normals(self, comfunc: Callable = lambda ns: np.ones(len(ns), dtype=bool), invert=False):
+        return self._select_by_idx(self.get_index_by_normals(comfunc=comfunc), invert=invert)
+
+    @staticmethod
+    def _cosine(model, similarity):
+        m = np.asarray(model, np.float64)[:3]
+        return lambda v: (v @ m) / (np.linalg.norm(v, axis=1) * np.linalg.norm(m)) >= similarity
+
+    def get_index_by_normals_cosine(self, model, similarity: float = 0.99, invert: bool = False):
+        return self.get_index_by_normals(comfunc=self._cosine(model, similarity), invert=invert)
+
+    def select_by_normals_cosine(self, model, similarity: float = 0.99, invert: bool = False):
+        return self._select_by_idx(self.get_index_by_normals_cosine(model, similarity), invert=invert)
+
+    def get_index_by_colors(self, comfunc: Callable = lambda rgb: np.ones(len(rgb), dtype=bool), invert=False):
+        return self._bool2index(comfunc(self.get_colors()), invert=invert)
+
+    def get_index_by_colors_cosine(self, model, similarity: float = 0.99, invert: bool = False):
+        return self.get_index_by_colors(comfunc=self._cosine(model, similarity), invert=invert)
+
+    def select_by_colors_cosine(self, model, similarity: float = 0.99, invert: bool = False):
+        return self._select_by_idx(self.get_index_by_colors_cosine(model, similarity), invert=invert)
+
+    def get_index_by_XYZ(self, comfunc: Callable = lambda X, Y, Z: np.ones(len(X), dtype=bool), invert=False):
+        p = self.get_points()
+        return self._bool2index(comfunc(p[:, 0], p[:, 1], p[:, 2]), invert=invert)
+
+    def select_by_XYZ(self, comfunc: Callable = lambda X, Y, Z: np.ones(len(X), dtype=bool), invert=False):
+        return self._select_by_idx(self.get_index_by_XYZ(comfunc), invert=invert)
+
+    def get_index_by_radius(self, r: float, invert: bool = False):
+        return self.get_index_by_XYZ(lambda X, Y, Z: (X ** 2 + Y ** 2 + Z ** 2) ** 0.5 <= r, invert=invert)
+
+    def select_by_radius(self, r: float, invert: bool = False):
+        return self._select_by_idx(self.get_index_by_radius(r), invert=invert)
+
+    def get_index_by_plane(self, model, thickness=0.03, invert: bool = False):
+        """|p.abc + d| / |abc| < thickness (strict), or a (lo, hi) signed band
+        (reference PointCloud.py:278-290)."""
+        p = self.get_points()
+        a, b, c, d = model
+        s = (p @ np.asarray([a, b, c], np.float64) + d) / (a ** 2 + b ** 2 + c ** 2) ** 0.5
+        if isinstance(thickness, tuple):
+            res = np.logical_and(s > thickness[0], s < thickness[1])
+        else:
+            res = np.abs(s) < thickness
+        return self._bool2index(res, invert=invert)
+
+    def select_by_plane(self, model, thickness=0.03, invert: bool = False):
+        return self._select_by_idx(self.get_index_by_plane(model, thickness), invert=invert)
+
+    def get_index_by_aabb(self, aabb_min, aabb_max, invert: bool = False):
+        p = self.get_points()
+        inside = np.all((p >= np.asarray(aabb_min)) & (p <= np.asarray(aabb_max)), axis=1)
+        return self._bool2index(inside, invert=invert)
+
+    def select_by_aabb(self, aabb_min, aabb_max, invert: bool = False):
+        return self._select_by_idx(self.get_index_by_aabb(aabb_min, aabb_max), invert=invert)
+
+    def get_index_by_aabb_list(self, aabb_min_max_list, invert: bool = False):
+        p = self.get_points()
+        inside = np.zeros(len(p), bool)
+        for lo, hi in aabb_min_max_list:
+            inside |= np.all((p >= np.asarray(lo)) & (p <= np.asarray(hi)), axis=1)
+        return self._bool2index(inside, invert=invert)
+
+    def select_by_aabb_list(self, aabb_min_max_list, invert: bool = False):
+        return self._select_by_idx(self.get_index_by_aabb_list(aabb_min_max_list), invert=invert)
+
+    def select_by_topN(self, n: int):
+        return self._select_by_idx(np.arange(self.size())[:n])
+
+
+class PointCloudUtility(PointCloudSelections):
+
+    def paint_uniform_color(self, color=(1.0, 0.0, 0.0)):
+        self._colors = self._to_dev(np.tile(np.asarray(color, np.float32).reshape(1, 3), (self.size(), 1)))
+        return self
+
+    def split_by_labels(self):
+        ul = np.unique(self.labels)
+        return [self.select_by_bool((self.labels == j).reshape(-1)) for j in ul], ul
+
+    def centralize(self):
+        return self.translate(-self.get_center())
+
+    def voxel_down_sample_and_trace(self, voxel_size: float):
+        """Open3D VoxelDownSampleAndTrace(vs, AABB min, AABB max) + idxmat.max(1) +
+        _select_by_idx (reference PointCloud.py:338-341) on the GPU.
+
+        Returns (cloud of the representatives in ascending index order,
+        idxmat (M,8) int32 cubic-id matrix, vec: list of M int arrays).  Row r
+        of idxmat / vec is the voxel of representative r; Open3D emits rows in
+        its hash-map order instead, which no implementation can reproduce."""
+        x = self._dev_points()
+        mn, mx = self.get_aabb()
+        out = ops.voxel_down_sample(x, voxel_size, mn, mx, with_xyz=False, trace=True)
+        rep = out["rep_idx"]
+        idxmat = out["cubic_id"].cpu().numpy()
+        vop = out["voxel_of_point"].long()
+        order = torch.argsort(vop, stable=True)
+        counts = torch.bincount(vop, minlength=rep.numel()).cpu().numpy()
+        flat = order.to(torch.int32).cpu().numpy()
+        vec = np.split(flat, np.cumsum(counts)[:-1]) if rep.numel() else []
+        return self._select_by_idx(rep), idxmat, vec
+
+    def voxel_down_sample(self, voxel_size: float):
+        """Representatives only (no trace) — the fast path."""
+        x = self._dev_points()
+        mn, mx = self.get_aabb()
+        out = ops.voxel_down_sample(x, voxel_size, mn, mx, with_xyz=False)
+        return self._select_by_idx(out["rep_idx"])
+
+    def random_down_sample(self, down_sample_ratio: float = 0.1):
+        if down_sample_ratio <= 0 or down_sample_ratio > 1:
+            return self.__class__()
+        idx = np.arange(self.size())
+        np.random.shuffle(idx)
+        return self._select_by_idx(idx[: int(len(idx) * down_sample_ratio)])
+
+    def uniform_down_sample(self, down_sample_ratio: float = 0.1):
+        if down_sample_ratio <= 0 or down_sample_ratio > 1:
+            return self.__class__()
+        return self._select_by_idx(np.arange(self.size())[:: int(1 / down_sample_ratio)])
+
+    def remove_statistical_outlier(self, nb_neighbors: int = 20, std_ratio: float = 2.0,
+                                   print_progress: bool = False):
+        """Open3D RemoveStatisticalOutliers (reference PointCloud.py:370-372):
+        mean distance to the nb_neighbors nearest (self included), keep points
+        with 0 < mean < cloud_mean + std_ratio * std (Bessel-corrected)."""
+        if nb_neighbors < 1 or std_ratio <= 0:
+            raise RuntimeError("Illegal input parameters, the number of neighbors and standard deviation "
+                               "ratio must be positive.")
+        if not self.has_points():
+            return self.__class__(), []
+        x = self._dev_points()
+        idx, d2, cnt = ops.knn_search(x, x, mode=N.SEARCH_KNN, knn=nb_neighbors)
+        valid = cnt > 0
+        d = torch.sqrt(torch.where(torch.isfinite(d2), d2, torch.zeros_like(d2)))
+        avg = torch.where(valid, d.sum(1) / cnt.clamp_min(1).double(), torch.full_like(d[:, 0], -1.0))
+        nv = int(valid.sum().item())
+        if nv == 0:
+            return self.__class__(), []
+        pos = avg > 0
+        mean = avg[pos].sum() / nv
+        sq = torch.where(pos, (avg - mean) ** 2, torch.zeros_like(avg)).sum()
+        std = torch.sqrt(sq / (nv - 1)) if nv > 1 else torch.zeros_like(sq)
+        thr = mean + std_ratio * std
+        keep = torch.nonzero((avg > 0) & (avg < thr)).reshape(-1)
+        kept = keep.cpu().numpy().tolist()
+        return self._select_by_idx(keep), kept
+
+    def merge_pcds(self, raw_pcds, rgb: bool = False, intensity: bool = False, normals: bool = False,
+                   labels: bool = False):
+        pcds = [p if isinstance(p, PointCloudBase) else self.__class__(p) for p in raw_pcds]
+        res = self.__class__(np.vstack([p.get_points() for p in pcds]))
+        if rgb:
+            res.set_rgb(np.vstack([p.get_colors() if p.has_colors() else np.ones((p.size(), 3)) for p in pcds]))
+        if normals:
+            for p in pcds:
+                if not p.has_normals():
+                    p.estimate_normals()
+            res.set_normals(np.vstack([p.get_normals() for p in pcds]))
+        if intensity:
+            res.set_intensity(np.vstack([p.get_intensity() if p.has_intensity()
+                                         else p.set_uniform_intensity(0).get_intensity() for p in pcds]))
+        if labels:
+            res.labels = np.vstack([p.get_labels() if p.has_labels() else p.set_uniform_label(0).get_labels()
+                                    for p in pcds])
+        return res
+
+    def append_pcd(self, pcd, rgb=False, intensity=False, normals=False, labels=False):
+        return self.merge_pcds([self, pcd], rgb=rgb, intensity=intensity, normals=normals, labels=labels)
+
+    def distance2plane(self, plane) -> np.ndarray:
+        a, b, c, d = plane
+        return ((self.get_points() * np.asarray([a, b, c])).sum(1) + d) / (a ** 2 + b ** 2 + c ** 2) ** 0.5
+
+    def remove_plane_outlier(self, plane_model, thickness: float = 0.03, similarity: float = 0.999,
+                             invert: bool = False):
+        cand = self.get_index_by_normals_cosine(plane_model, similarity)
+        sub = self._select_by_idx(cand)
+        floor_idx = np.arange(self.size())[cand][sub.get_index_by_plane(plane_model, thickness)]
+        return self._select_by_idx(floor_idx), floor_idx
+
+    def project2plane(self, plane):
+        plane = np.asarray(plane, np.float64)
+        dis = self.distance2plane(plane).reshape(-1, 1) * plane[:3].reshape(1, 3)
+        return self.__class__(self.get_points() - dis)
+
+    def seg_plane_by_svd(self):
+        p = self.get_points()
+        c = p.mean(0)
+        _, _, v = np.linalg.svd(p - c)
+        a, b, cc = v[-1]
+        return a, b, cc, -float((c * v[-1]).sum())
+
+
+class PointCloud(PointCloudUtility):
+
+    def split_pcd_index(self, nn: int, random: bool = False):
+        n = self.size()
+        if n <= nn:
+            return [np.arange(n)]
+        parts = n // nn
+        sizes = np.full(parts, nn) + np.asarray([len(a) for a in np.array_split(np.ones(n % nn), parts)])
+        r = np.arange(n)
+        if random:
+            np.random.shuffle(r)
+        starts = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+        return [r[s:s + k] for s, k in zip(starts, sizes)]
+
+    def split_pcd(self, nn: int, random: bool = False):
+        if self.size() <= nn:
+            return [self]
+        return [self._select_by_idx(i) for i in self.split_pcd_index(nn=nn, random=random)]
+
+    def split_by_voxel(self, voxel_size: float = 0.01, random: bool = True, top_n: int = 10):
+        """Round-robin one point per voxel into up to top_n clouds (reference
+        PointCloud.py:735-757), using the GPU voxel trace."""
+        lists = [np.asarray(v).tolist() for v in self.voxel_down_sample_and_trace(voxel_size)[2]]
+        if random:
+            for v in lists:
+                np.random.shuffle(v)
+        pcds, taken = [], []
+        while True:
+            pick = [v.pop() for v in lists if len(v) > 0]
+            if not pick:
+                break
+            taken += pick
+            pcds.append(self._select_by_idx(pick))
+            if len(pcds) >= top_n:
+                break
+        return pcds, self._select_by_idx(taken, True)
+
+    def rotation_matrix_from_vectors(self, vec1, vec2) -> np.ndarray:
+        a = (np.asarray(vec1, np.float64) / np.linalg.norm(vec1)).reshape(3)
+        b = (np.asarray(vec2, np.float64) / np.linalg.norm(vec2)).reshape(3)
+        v = np.cross(a, b)
+        if not any(v):
+            return np.eye(3)
+        c = np.dot(a, b)
+        s = np.linalg.norm(v)
+        K = np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
+        return np.eye(3) + K + K @ K * ((1 - c) / s ** 2)
+
+    def rotate_by_normal(self, plane):
+        a, b, c, d = plane
+        T = np.eye(4)
+        T[2, 3] = d
+        T[:3, :3] = self.rotation_matrix_from_vectors(np.array([a, b, c]) / np.linalg.norm([a, b, c]), (0, 0, 1))
+        self.transform(T)
+        return self, T
+
+    rotate_to_plane = rotate_by_normal
+
+    def to_2D_Img(self, resolution: float = 0.05, color: bool = False):
+        use_color = color and self.has_colors()
+        p = self.get_points()
+        minx, miny = p[:, 0].min(), p[:, 1].min()
+        ir = 1.0 / resolution
+        T = np.diag([ir, ir, ir, 1.0]) @ np.array([[1, 0, 0, -minx], [0, 1, 0, -miny], [0, 0, 1, 0], [0, 0, 0, 1.0]])
+        q = (p @ T[:3, :3].T + T[:3, 3]).round().astype(int)
+        ix, iy = q[:, 0], q[:, 1]
+        sx, sy = ix.max(), iy.max()
+        ix = np.clip(ix, 0, sx - 1)
+        iy = np.clip(iy, 0, sy - 1)
+        if use_color:
+            img = np.zeros((sy, sx, 3), np.uint8)
+            img[iy, ix] = (self.get_colors() * 255).astype(np.uint8)
+        else:
+            img = np.zeros((sy, sx), np.uint8)
+            img[iy, ix] = 255
+        return img, minx, T, miny, np.linalg.inv(T), resolution, list(zip(ix, iy))
+
+    def DBSCAN(self, eps: float = 0.05, min_samples: int = 3):
+        from sklearn.cluster import DBSCAN
+
+        labels = DBSCAN(eps=eps, min_samples=min_samples).fit(self.get_points()).labels_
+        return [self._select_by_idx(np.arange(len(labels))[labels == i]) for i in
+                range(len(set(labels) - {-1}))], labels
+
+    def seg_planes(self, thickness: float = 0.01, ransac_n: int = 3, num_iterations: int = 450,
+                   top_n: float = 10e9, minPointsRatio: float = 0.1):
+        """Repeated GPU segment_plane on the remaining outliers (reference
+        PointCloud.py:941-985) -> (planes, pcds (inliers..., outliers), aabbs)."""
+        rest, planes, pcds, aabbs = self, [], [], []
+        raw = self.size()
+        if raw < ransac_n:
+            return planes, pcds, aabbs
+        while rest.size() / raw > minPointsRatio:
+            try:
+                plane, inl = rest.segment_plane(thickness, ransac_n, num_iterations)
+            except RuntimeError as e:
+                print(e)
+                break
+            planes.append(plane)
+            inliers = rest._select_by_idx(inl)
+            pcds.append(inliers)
+            aabbs.append(inliers.get_aabb())
+            rest = rest._select_by_idx(inl, True)
+            if len(planes) > top_n:
+                break
+        pcds.append(rest)
+        aabbs.append(rest.get_aabb())
+        return planes, pcds, aabbs
+
+    def registration_icp(self, target: "PointCloudBase", max_correspondence_distance: float, init=None,
+                         max_iteration: int = 30, relative_fitness: float = 1e-6, relative_rmse: float = 1e-6):
+        """Point-to-plane ICP of self onto target (Open3D registration_icp with
+        TransformationEstimationPointToPlane), on the GPU.  North-star op; the
+        reference has no ICP."""
+        if not target.has_normals():
+            raise RuntimeError("TransformationEstimationPointToPlane and TransformationEstimationColoredICP "
+                               "require pre-computed normal vectors for target PointCloud.")
+        if max_correspondence_distance <= 0.0:
+            raise RuntimeError("Invalid max_correspondence_distance.")
+        r = ops.registration_icp(self._dev_points(), target._dev_points(), target._normals,
+                                 max_correspondence_distance, init, max_iteration, relative_fitness, relative_rmse)
+        return RegistrationResult(r["transformation"], r["fitness"], r["inlier_rmse"],
+                                  r["correspondence_set"].cpu().numpy().astype(np.int64))

@@ -31,6 +31,9 @@ _SZ = ctypes.c_size_t
 _SIGS = {
     "o3dx_abi_version": (_I32, []),
     "o3dx_last_error": (ctypes.c_char_p, []),
+    "o3dx_set_kernel_timing": (None, [_I32]),
+    "o3dx_reset_kernel_timing": (None, []),
+    "o3dx_kernel_timing": (_I32, [ctypes.c_char_p, _P, _P]),
     "o3dx_aabb_workspace_bytes": (_SZ, [_I64]),
     "o3dx_aabb": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
     "o3dx_voxel_workspace_bytes": (_SZ, [_I64]),
@@ -127,6 +130,22 @@ def workspace(nbytes: int, device: torch.device, slot: str = "main") -> torch.Te
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _ws[key] = buf
     return buf
+
+
+def set_kernel_timing(enable: bool):
+    load().o3dx_set_kernel_timing(1 if enable else 0)
+
+
+def reset_kernel_timing():
+    load().o3dx_reset_kernel_timing()
+
+
+def kernel_timing(name: str):
+    """(total_ms, launches) of a library kernel recorded while timing was on."""
+    ms = ctypes.c_double(0.0)
+    cnt = ctypes.c_int64(0)
+    load().o3dx_kernel_timing(name.encode(), ctypes.byref(ms), ctypes.byref(cnt))
+    return ms.value, cnt.value
 
 
 def release_workspaces():

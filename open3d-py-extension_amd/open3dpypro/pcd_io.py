@@ -158,26 +158,23 @@ def write_pcd(filename: str, points: np.ndarray, normals=None, colors=None, writ
         cols += [("normal_x", nr[:, 0]), ("normal_y", nr[:, 1]), ("normal_z", nr[:, 2])]
     if colors is not None:
         c = np.clip(np.round(np.asarray(colors, np.float64).reshape(-1, 3) * 255.0), 0, 255).astype(np.uint32)
-        packed = ((c[:, 0] << 16) | (c[:, 1] << 8) | c[:, 2]).astype(np.uint32).view(np.float32)
-        cols.append(("rgb", packed))
+        cols.append(("rgb", ((c[:, 0] << 16) | (c[:, 1] << 8) | c[:, 2]).astype(np.uint32)))
     n = len(pts)
     names = [c[0] for c in cols]
+    types = ["U" if nm == "rgb" else "F" for nm in names]
     head = ("# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\n"
             f"FIELDS {' '.join(names)}\nSIZE {' '.join(['4'] * len(names))}\n"
-            f"TYPE {' '.join(['F'] * len(names))}\nCOUNT {' '.join(['1'] * len(names))}\n"
+            f"TYPE {' '.join(types)}\nCOUNT {' '.join(['1'] * len(names))}\n"
             f"WIDTH {n}\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS {n}\n"
             f"DATA {'ascii' if write_ascii else 'binary'}\n")
     with open(filename, "wb") as f:
         f.write(head.encode("ascii"))
         if write_ascii:
-            body = np.stack([c[1] for c in cols], 1)
-            for i, row in enumerate(body):
-                vals = []
-                for (name, _), v in zip(cols, row):
-                    vals.append(str(int(np.float32(v).view(np.uint32))) if name == "rgb" else repr(float(v)))
-                f.write((" ".join(vals) + "\n").encode("ascii"))
+            strs = [[str(int(v)) for v in a] if nm == "rgb" else [repr(float(v)) for v in a] for nm, a in cols]
+            for row in zip(*strs):
+                f.write((" ".join(row) + "\n").encode("ascii"))
         else:
-            rec = np.empty(n, dtype=[(nm, np.float32) for nm in names])
+            rec = np.empty(n, dtype=[(nm, np.uint32 if nm == "rgb" else np.float32) for nm in names])
             for nm, v in cols:
                 rec[nm] = v
             f.write(rec.tobytes())

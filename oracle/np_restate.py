@@ -104,3 +104,59 @@ def segment_plane_counts(xyz, thr, samples):
             continue
         out.append(int((plane_dist(pl, p) < thr).sum()))
     return np.array(out, np.int64)
+
+
+# ---------------------------------------------------------------------------
+# Restatements of the reference's own torch branches (pinned by
+# tests/golden/ref_torch_branch.npz, generated from the reference itself).
+
+def voxel_torch_hash(xyz, voxel_size):
+    """Processors.VoxelDownsample cuda branch (reference processors.py:433-448):
+    int32 keys floor(p/vs), hash x*73856093 + y*19349663 + z*83492791 (int32
+    wrap), one representative per hash value, output in ascending (signed)
+    hash order.  Which member represents a group is whatever the reference's
+    unstable torch.sort puts first (the golden vector shows min, max and
+    middle members): unspecified.  This restatement returns the lowest index;
+    the fixture pins the group set and order, not the member."""
+    p = np.asarray(xyz, np.float32)
+    v = np.floor(p / np.float32(voxel_size)).astype(np.int32)
+    with np.errstate(over="ignore"):
+        key = (v[:, 0] * np.int32(73856093) + v[:, 1] * np.int32(19349663) + v[:, 2] * np.int32(83492791))
+    key = key.astype(np.int32)
+    order = np.lexsort((np.arange(len(p)), key))
+    ks = key[order]
+    first = np.ones(len(ks), bool)
+    first[1:] = ks[1:] != ks[:-1]
+    return order[first]
+
+
+def torch_hash_keys(xyz, voxel_size):
+    p = np.asarray(xyz, np.float32)
+    v = np.floor(p / np.float32(voxel_size)).astype(np.int64)
+    key = v[:, 0] * 73856093 + v[:, 1] * 19349663 + v[:, 2] * 83492791
+    return ((key + 2 ** 31) % 2 ** 32 - 2 ** 31).astype(np.int32)
+
+
+def ransac_batched_fp32(xyz, thr, samples, batch):
+    """PlaneDetection.ransac_plane_detection_torch_batched (reference
+    processors.py:561-627) given its sampled triples: float32 planes flipped
+    to d >= 0, counts |p.n + d| < thr, first strict improvement over batches."""
+    p = np.asarray(xyz, np.float32)
+    best_c, best = 0, None
+    for b0 in range(0, len(samples), batch):
+        s = samples[b0:b0 + batch]
+        p1, p2, p3 = p[s[:, 0]], p[s[:, 1]], p[s[:, 2]]
+        nrm = np.cross(p2 - p1, p3 - p1).astype(np.float32)
+        ln = np.linalg.norm(nrm, axis=1, keepdims=True).astype(np.float32)
+        nrm = nrm / np.maximum(ln, np.float32(1e-6))
+        d = -(nrm * p1).sum(1).astype(np.float32)
+        flip = d < 0
+        nrm[flip] = -nrm[flip]
+        d[flip] = -d[flip]
+        dist = np.abs(p @ nrm.T + d)
+        cnt = (dist < np.float32(thr)).sum(0)
+        j = int(np.argmax(cnt))
+        if cnt[j] > best_c:
+            best_c = int(cnt[j])
+            best = np.concatenate([nrm[j], [d[j]]]).astype(np.float64)
+    return best, best_c

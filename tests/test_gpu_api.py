@@ -1,0 +1,172 @@
+"""GPU: the drop-in API (PointCloud / processors) end to end against the oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import open3dpypro as o3p
+from open3dpypro import synthetic as S
+from open3dpypro.PointCloudMat import PointCloudMat, ShapeType
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUNNY = os.path.join(ROOT, "tests", "golden", "bunny.pcd")
+
+
+def _sign_err(a, b):
+    return np.minimum(np.abs(a - b).max(1), np.abs(a + b).max(1))
+
+
+def test_config1_bunny_pipeline(bunny):
+    """BASELINE configs[0]: read_pcd -> voxel_down_sample(0.005) -> estimate_normals()."""
+    pc = o3p.PointCloud().read_pcd(BUNNY)
+    down = pc.voxel_down_sample(0.005)
+    ref_idx = O.voxel_down_sample(bunny, 0.005)
+    assert down.size() == 3017
+    assert np.array_equal(down.get_points(), bunny[ref_idx].astype(np.float64))
+    down.estimate_normals()
+    ref_n = O.estimate_normals(bunny[ref_idx], O.KNN, 30)
+    err = np.abs(down.get_normals() - ref_n).max(1)
+    assert np.mean(err < 1e-5) > 0.999 and _sign_err(down.get_normals(), ref_n).max() < 1e-5
+
+
+def test_voxel_trace_api(bunny):
+    pc = o3p.PointCloud(bunny.astype(np.float64))
+    down, idxmat, vec = pc.voxel_down_sample_and_trace(0.01)
+    rep, vop, cub = O.voxel_down_sample(bunny, 0.01, trace=True)
+    assert np.array_equal(idxmat, cub) and np.array_equal(idxmat.max(1), rep)
+    assert len(vec) == len(rep)
+    for r, v in enumerate(vec[:200]):
+        assert np.array_equal(v, np.nonzero(vop == r)[0])
+    assert down.size() == len(rep)
+
+
+def test_hybrid_param_like_test_mesh(bunny):
+    pc = o3p.PointCloud(bunny.astype(np.float64))
+    pc.estimate_normals(param=o3p.KDTreeSearchParamHybrid(radius=0.01, max_nn=30))
+    ref = O.estimate_normals(bunny, O.HYBRID, 30, 0.01)
+    assert np.mean(np.abs(pc.get_normals() - ref).max(1) < 1e-5) > 0.999
+
+
+def test_estimate_normals_orients_by_existing(bunny):
+    pc = o3p.PointCloud(bunny.astype(np.float64), normals=np.tile([[0, 0, -1.0]], (len(bunny), 1)))
+    pc.estimate_normals()
+    assert (pc.get_normals()[:, 2] <= 1e-7).all()
+
+
+def test_segment_plane_api_and_seg_planes():
+    pts = S.planted_plane(50000, 4).numpy()
+    pc = o3p.PointCloud(pts.astype(np.float64))
+    samples = O.ransac_samples(len(pts), 3, 450, 77)
+    plane, inl = pc.segment_plane(0.01, 3, 450, samples=samples)
+    rplane, rinl, *_ = O.segment_plane(pts, 0.01, 3, 450, samples)
+    assert inl == rinl.tolist()
+    np.testing.assert_allclose(plane, rplane, atol=1e-9)
+    assert abs(abs(plane[2]) - 1) < 1e-3
+    o3p.set_random_seed(5)
+    planes, pcds, aabbs = pc.seg_planes(0.01, 3, 300, top_n=2, minPointsRatio=0.5)
+    assert len(planes) >= 1 and sum(p.size() for p in pcds) == len(pts)
+
+
+def test_kdtree_helpers(bunny):
+    pc = o3p.PointCloud(bunny.astype(np.float64))
+    k, idx, d2 = pc.get_points_by_knn(100, 20)
+    ridx, rd2, _ = O.knn_search(bunny, bunny[100:101], O.KNN, 20)
+    assert k == 20 and np.array_equal(idx, ridx[0])
+    k, idx, d2 = pc.get_points_radius(100, 0.005)
+    ridx, _, rc = O.knn_search(bunny, bunny[100:101], O.RADIUS, 0, 0.005, K=4096)
+    assert k == rc[0] and set(idx.tolist()) == set(ridx[0, :k].tolist())
+    k, idx, _ = pc.get_points_by_knn(100, 1000)   # beyond the register path: exact brute force
+    assert k == 1000 and idx[0] == 100
+
+
+def test_remove_statistical_outlier_api():
+    rng = np.random.default_rng(1)
+    pts = np.concatenate([rng.normal(0, 0.1, (5000, 3)), rng.uniform(-5, 5, (50, 3))]).astype(np.float32)
+    pc = o3p.PointCloud(pts.astype(np.float64))
+    cl, idx = pc.remove_statistical_outlier(20, 2.0)
+    # restatement check in numpy from the oracle's kNN distances
+    ridx, rd2, rc = O.knn_search(pts, pts, O.KNN, 20)
+    avg = np.sqrt(rd2).mean(1)
+    mean = avg.mean()
+    std = np.sqrt(((avg - mean) ** 2).sum() / (len(avg) - 1))
+    ref = np.nonzero((avg > 0) & (avg < mean + 2.0 * std))[0]
+    assert len(set(idx) ^ set(ref.tolist())) <= 2
+    assert cl.size() == len(idx) and len(idx) < len(pts)
+
+
+def test_registration_icp_api():
+    tgt = S.box_surface(40000, 5).numpy()
+    Tgt = S.rigid_transform()
+    src = S.apply_transform(S.box_surface(40000, 6), Tgt).numpy()
+    t = o3p.PointCloud(tgt.astype(np.float64))
+    t.estimate_normals()
+    s = o3p.PointCloud(src.astype(np.float64))
+    res = s.registration_icp(t, 0.02, max_iteration=30)
+    assert np.abs(res.transformation - np.linalg.inv(Tgt)).max() < 1e-4
+    assert res.fitness > 0.99 and res.correspondence_set.shape[1] == 2
+    with pytest.raises(RuntimeError, match="normal"):
+        s.registration_icp(o3p.PointCloud(tgt.astype(np.float64)), 0.02)
+
+
+def _mat(a, st=ShapeType.XYZ):
+    return PointCloudMat(shape_type=st).build(a)
+
+
+def test_processors_numpy_and_torch_branches(dev):
+    pts = S.planted_plane(30000, 8).numpy()
+    meta = {}
+    # numpy branch
+    vd = o3p.Processors.VoxelDownsample(voxel_size=0.05)
+    out, _ = vd.validate([_mat(pts)], meta)
+    ref = O.voxel_down_sample(pts, 0.05)
+    assert np.array_equal(out[0].data(), pts[ref])
+    # torch branch, same semantics
+    vt = o3p.Processors.VoxelDownsample(voxel_size=0.05)
+    out_t, _ = vt.validate([_mat(torch.from_numpy(pts).to(dev))], meta)
+    assert torch.equal(out_t[0].data().cpu(), torch.from_numpy(pts[ref]))
+    # normals processors
+    cn = o3p.Processors.CPUNormals()
+    o, _ = cn.validate([_mat(pts[ref])], meta)
+    assert o[0].info.shape_type == ShapeType.XYZN and o[0].data().dtype == np.float64
+    tn = o3p.Processors.TorchNormals()
+    o2, _ = tn.validate([_mat(torch.from_numpy(pts[ref]).to(dev))], meta)
+    assert o2[0].data().shape == (len(ref), 6)
+    e = _sign_err(o2[0].data()[:, 3:].double().cpu().numpy(), O.estimate_normals(pts[ref], O.KNN, 16))
+    assert np.mean(e < 1e-5) > 0.999
+    # plane detection (EMA + sign flip d >= 0)
+    pdp = o3p.Processors.PlaneDetection(distance_threshold=0.01, alpha=1.0, seed=3, num_iterations=300)
+    _, meta = pdp.validate([_mat(torch.from_numpy(pts).to(dev))], meta)
+    plane = np.asarray(meta[pdp.uuid][0])
+    assert plane[3] >= 0 and abs(abs(plane[2]) - 1) < 1e-2 and abs(abs(plane[3]) - 0.5) < 1e-2
+
+
+def test_processor_pipeline_like_test_pipeline(dev):
+    """The reference's GPU chain (test_pipeline.py:406-416) up to PlaneNormalize."""
+    pts = S.planted_plane(200000, 9).numpy() - np.array([0.5, 0.5, 0.0], np.float32)
+    det = o3p.Processors.PlaneDetection(distance_threshold=0.02, alpha=1.0, seed=1)
+    pipes = [o3p.Processors.RandomSample(n_samples=50000),
+             o3p.Processors.NumpyToTorch(),
+             o3p.Processors.RadiusSelection(radius=2.0),
+             o3p.Processors.VoxelDownsample(voxel_size=0.01),
+             det,
+             o3p.Processors.PlaneNormalize(uuid="PlaneNormalize:pn", detection_uuid=det.uuid,
+                                           save_results_to_meta=True)]
+    mats, meta = o3p.PointCloudMatProcessors.run_once([_mat(pts)], {}, pipes, validate=True)
+    z = mats[0].data()[:, 2].cpu().numpy()
+    assert np.mean(np.abs(z) < 0.02) > 0.1   # the planted plane now lies at z ~ 0
+    mats, meta = o3p.PointCloudMatProcessors.run_once([_mat(pts)], meta, pipes)   # streaming call
+    assert mats[0].data().is_cuda
+
+
+def test_icp_processor(dev):
+    tgt = S.box_surface(20000, 3)
+    tn = o3p.ops.estimate_normals(tgt.to(dev), knn=30).cpu()
+    src = S.apply_transform(S.box_surface(20000, 4), S.rigid_transform())
+    icp = o3p.Processors.ICP(max_correspondence_distance=0.02)
+    out, meta = icp.validate([_mat(src.to(dev)), _mat(torch.hstack([tgt, tn]).to(dev), ShapeType.XYZN)], {})
+    T = np.asarray(meta[icp.uuid]["transformation"])
+    assert np.abs(T - np.linalg.inv(S.rigid_transform())).max() < 1e-4
+    assert out[0].data().shape == (20000, 3)

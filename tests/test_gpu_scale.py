@@ -1,0 +1,64 @@
+"""GPU: parity at BASELINE sizes (10M points) and size-independent properties."""
+import numpy as np
+import pytest
+import torch
+
+from open3dpypro import ops, synthetic as S
+from oracle import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+N = 10_000_000
+
+
+@pytest.fixture(scope="module")
+def cloud10m(dev):
+    return S.uniform_cube(N, seed=0, device=dev)
+
+
+def test_voxel_10m_exact(cloud10m):
+    vs = S.voxel_size_for(N)
+    out = ops.voxel_down_sample(cloud10m, vs, trace=True)
+    rep = out["rep_idx"].cpu().numpy()
+    ref = O.voxel_down_sample(cloud10m.cpu().numpy(), vs)
+    assert np.array_equal(rep, ref)
+    # properties: every point's voxel row owns exactly the max index of its members
+    vop = out["voxel_of_point"].long()
+    M = rep.size
+    mx = torch.full((M,), -1, dtype=torch.long, device=vop.device)
+    mx.scatter_reduce_(0, vop, torch.arange(N, device=vop.device), reduce="amax")
+    assert torch.equal(mx.cpu(), torch.from_numpy(rep).long())
+
+
+def test_normals_10m_reps(cloud10m):
+    vs = S.voxel_size_for(N)
+    out = ops.voxel_down_sample(cloud10m, vs)
+    reps = out["rep_xyz"]
+    got = ops.estimate_normals(reps, knn=30).cpu().numpy()
+    ref = O.estimate_normals(reps.cpu().numpy(), O.KNN, 30)
+    err_signed = np.abs(got - ref).max(1)
+    err_any = np.minimum(err_signed, np.abs(got + ref).max(1))
+    assert np.mean(err_any < 1e-5) > 0.9995
+    assert np.mean(err_signed < 1e-5) > 0.999
+    assert np.abs(np.linalg.norm(got, axis=1) - 1).max() < 1e-5
+
+
+def test_ransac_10m_counts(dev):
+    pts = S.planted_plane(N, 1, device=dev)
+    samples = O.ransac_samples(N, 3, 1000, 7)
+    plane, inl = ops.segment_plane(pts, 0.01, 3, 1000, samples=samples)
+    rplane, rinl, counts, _, _ = O.segment_plane(pts.cpu().numpy(), 0.01, 3, 1000, samples)
+    assert inl.numel() == len(rinl) and np.array_equal(inl.cpu().numpy(), rinl)
+    np.testing.assert_allclose(plane, rplane, atol=1e-9)
+
+
+def test_icp_1m_parity(dev):
+    n = 1_000_000
+    tgt = S.box_surface(n, 1, device=dev)
+    src = S.apply_transform(S.box_surface(n, 2, device=dev), S.rigid_transform())
+    tn = ops.estimate_normals(tgt, knn=30)
+    res = ops.registration_icp(src, tgt, tn, 0.02, max_iteration=30, relative_fitness=0, relative_rmse=0,
+                               return_corr=False)
+    T, fit, rmse, _ = O.registration_icp(src.cpu().numpy(), tgt.cpu().numpy(), tn.cpu().numpy(), 0.02,
+                                         max_iteration=30, relative_fitness=0, relative_rmse=0)
+    np.testing.assert_allclose(res["transformation"], T, atol=1e-5)
+    assert abs(res["fitness"] - fit) < 1e-6

@@ -1,0 +1,264 @@
+"""CPU: host-side logic of the drop-in, the C-ABI library surface, PCD I/O,
+synthetic data.  No kernel is launched here (no GPU in this leg)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import open3dpypro as o3p
+from open3dpypro import _native as N
+from open3dpypro import pcd_io, synthetic as S
+from open3dpypro.PointCloudMat import PointCloudMat, PointCloudMatInfo, ShapeType
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GPU = torch.cuda.is_available()
+
+
+# ---------------------------------------------------------------- C-ABI
+def header_functions():
+    txt = open(N.HEADER_PATH).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(o3dx_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = N.load()  # loads only: no compute call without a GPU
+    decl = header_functions()
+    assert len(decl) >= 30
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert sorted(N.declared_symbols()) == decl
+    assert lib.o3dx_abi_version() == 1
+
+
+def test_library_host_only_entry_points():
+    # pure host functions are callable without a GPU
+    out = np.empty((50, 3), np.int32)
+    rc = N.load().o3dx_ransac_samples(1000, 3, 50, 11, out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0 and all(len(set(r)) == 3 for r in out)
+    from oracle import oracle as O
+    assert np.array_equal(out, O.ransac_samples(1000, 3, 50, 11))
+    pl = np.zeros(4)
+    pts = np.array([[0, 0, 1.0], [1, 0, 1], [0, 1, 1]])
+    assert N.load().o3dx_plane_from_points(pts.ctypes.data_as(ctypes.c_void_p), 3,
+                                           pl.ctypes.data_as(ctypes.c_void_p)) == 0
+    assert np.allclose(pl, [0, 0, 1, -1])
+    bad = N.load().o3dx_ransac_samples(2, 3, 5, 0, out.ctypes.data_as(ctypes.c_void_p))
+    assert bad == -22 and b"ransac_n" in N.load().o3dx_last_error()
+
+
+def test_icp_solve_host():
+    # JTJ = I, JTr = -x  ->  x; small rotation about z + translation
+    x = np.array([0, 0, 0.01, 0.1, -0.2, 0.3])
+    sums = np.zeros(32)
+    t = 0
+    for a in range(6):
+        for b in range(a, 6):
+            sums[t] = 1.0 if a == b else 0.0
+            t += 1
+    sums[21:27] = -x
+    sums[28] = 10
+    upd = o3p.ops.icp_solve(sums)
+    c, s = np.cos(0.01), np.sin(0.01)
+    assert np.allclose(upd[:3, :3], [[c, -s, 0], [s, c, 0], [0, 0, 1]])
+    assert np.allclose(upd[:3, 3], x[3:])
+
+
+@pytest.mark.skipif(GPU, reason="checks the no-GPU behaviour")
+def test_compute_fails_loudly_without_gpu():
+    pc = o3p.PointCloud(np.random.rand(100, 3))
+    with pytest.raises(RuntimeError):
+        pc.voxel_down_sample(0.1)
+    with pytest.raises(RuntimeError):
+        pc.estimate_normals()
+    with pytest.raises(RuntimeError):
+        o3p.ops.aabb(torch.rand(10, 3))
+
+
+# ---------------------------------------------------------------- PCD I/O
+def test_read_bunny_pcd():
+    f = pcd_io.read_pcd_arrays(os.path.join(ROOT, "tests", "golden", "bunny.pcd"))
+    assert set(f) >= {"Intensity", "x", "y", "z", "_"}
+    assert len(f["x"]) == 35947
+    pc = o3p.PointCloud().read_pcd(os.path.join(ROOT, "tests", "golden", "bunny.pcd"))
+    assert pc.size() == 35947 and not pc.has_normals()
+    p = pc.get_points()
+    assert p.dtype == np.float64
+    np.testing.assert_allclose(p.min(0), [-0.0947, -0.0619, 0.033], atol=1e-4)
+
+
+@pytest.mark.parametrize("ascii_", [False, True])
+def test_pcd_roundtrip(tmp_path, ascii_):
+    rng = np.random.default_rng(0)
+    pts = rng.normal(size=(200, 3)).astype(np.float32).astype(np.float64)
+    nrm = rng.normal(size=(200, 3)).astype(np.float32).astype(np.float64)
+    col = rng.integers(0, 256, (200, 3)) / 255.0
+    fn = str(tmp_path / "c.pcd")
+    pcd_io.write_pcd(fn, pts, nrm, col, write_ascii=ascii_)
+    p2, n2, c2 = pcd_io.read_pcd(fn)
+    assert np.array_equal(p2, pts) and np.array_equal(n2, nrm)
+    np.testing.assert_allclose(c2, col, atol=1e-12)
+
+
+def test_pcd_nan_removal(tmp_path):
+    pts = np.array([[0, 0, 0], [np.nan, 1, 1], [np.inf, 0, 0], [1, 2, 3]], np.float64)
+    fn = str(tmp_path / "n.pcd")
+    pcd_io.write_pcd(fn, pts)
+    assert len(pcd_io.read_pcd(fn)[0]) == 4
+    assert len(pcd_io.read_pcd(fn, remove_nan_points=True)[0]) == 3
+    assert len(pcd_io.read_pcd(fn, remove_nan_points=True, remove_infinite_points=True)[0]) == 2
+
+
+def test_lzf_decompress():
+    # literal run "abc" then back-reference copying "abcabc" (len 6, offset 3)
+    stream = bytes([2]) + b"abc" + bytes([(4 << 5) | 0, 2])
+    assert pcd_io.lzf_decompress(stream, 9) == b"abcabcabc"
+
+
+def test_read_other_formats(tmp_path):
+    a = np.random.rand(20, 3)
+    np.save(tmp_path / "a.npy", a)
+    assert np.allclose(o3p.PointCloud().read_pcd(str(tmp_path / "a.npy")).get_points(), a)
+    np.savetxt(tmp_path / "a.xyzn", np.hstack([a, a]))
+    pc = o3p.PointCloud().read_pcd(str(tmp_path / "a.xyzn"))
+    assert pc.has_normals() and np.allclose(pc.get_normals(), a.astype(np.float32))
+    with pytest.raises(RuntimeError):
+        o3p.PointCloud().read_pcd(str(tmp_path / "a.unknownfmt"))
+
+
+# ---------------------------------------------------------- PointCloud host
+def test_pointcloud_basics():
+    xyz = np.random.rand(50, 3)
+    rgb = np.random.rand(50, 3) * 255
+    pc = o3p.PointCloud(xyz, rgb=rgb, intensity=np.arange(50).reshape(-1, 1),
+                        labels=np.arange(50).reshape(-1, 1) % 3)
+    assert pc.size() == 50 and pc.has_rgb() and pc.has_intensity() and pc.has_labels()
+    assert np.array_equal(pc.get_points(), xyz)  # exact float64 round trip
+    c = pc.get_colors()
+    assert abs(c.min()) < 1e-6 and abs(c.max() - 1) < 1e-6  # reference PointCloud.py:36-40 rescale
+    with pytest.raises(AssertionError):
+        pc.set_points(np.zeros((3, 2)))
+    with pytest.raises(AssertionError):
+        pc.set_intensity(np.zeros((3, 2)))
+
+
+def test_select_by_idx_order_and_attributes():
+    xyz = np.random.rand(30, 3)
+    pc = o3p.PointCloud(xyz, intensity=np.arange(30).reshape(-1, 1), labels=np.arange(30).reshape(-1, 1))
+    s = pc._select_by_idx([7, 2, 2, 29])  # mask semantics: ascending, de-duplicated
+    assert np.array_equal(s.get_points(), xyz[[2, 7, 29]])
+    assert np.array_equal(s.intensity.ravel(), [2, 7, 29])
+    inv = pc._select_by_idx([7, 2], invert=True)
+    assert inv.size() == 28 and 2 not in inv.intensity.ravel()
+    t = pc._select_by_idx(torch.tensor([3, 1]))
+    assert np.array_equal(t.get_points(), xyz[[1, 3]])
+    assert pc.clone().size() == 30 and pc.clone(invert=True).size() == 0
+
+
+def test_selections_and_planes():
+    xyz = np.array([[0, 0, 0.0], [0, 0, 0.5], [0, 0, 1.0], [3, 0, 0]])
+    pc = o3p.PointCloud(xyz)
+    assert list(pc.get_index_by_plane([0, 0, 2, -1], 0.1)) == [1]          # normalised distance
+    assert list(pc.get_index_by_plane([0, 0, 1, -0.5], (-0.6, 0.1))) == [0, 1, 3]
+    assert list(pc.get_index_by_radius(1.0)) == [0, 1, 2]
+    assert pc.select_by_aabb([-1, -1, -1], [1, 1, 0.7]).size() == 2
+    assert pc.select_by_topN(2).size() == 2
+    assert np.allclose(pc.distance2plane([0, 0, 2, -1]), [-0.5, 0, 0.5, -0.5])
+
+
+def test_split_pcd_index_partitions():
+    pc = o3p.PointCloud(np.random.rand(103, 3))
+    parts = pc.split_pcd_index(10)
+    assert sum(len(p) for p in parts) == 103 and len(parts) == 10
+    assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(103))
+
+
+def test_transform_translate():
+    xyz = np.random.rand(10, 3)
+    pc = o3p.PointCloud(xyz, normals=np.tile([[0, 0, 1.0]], (10, 1)))
+    T = S.rigid_transform(30, (0, 0, 1), (1, 2, 3))
+    pc.transform(T)
+    np.testing.assert_allclose(pc.get_points(), xyz @ T[:3, :3].T + T[:3, 3], atol=1e-12)
+    np.testing.assert_allclose(pc.get_normals(), np.tile([[0, 0, 1.0]], (10, 1)), atol=1e-6)
+    pc.translate([1, 0, 0])
+    np.testing.assert_allclose(pc.get_points()[:, 0], (xyz @ T[:3, :3].T + T[:3, 3])[:, 0] + 1, atol=1e-12)
+
+
+def test_kdtree_params():
+    from open3dpypro.params import resolve
+    assert resolve(o3p.KDTreeSearchParamKNN(12)) == (N.SEARCH_KNN, 12, 0.0)
+    assert resolve(o3p.KDTreeSearchParamRadius(0.5)) == (N.SEARCH_RADIUS, 0, 0.5)
+    assert resolve(o3p.KDTreeSearchParamHybrid(0.01, 30)) == (N.SEARCH_HYBRID, 30, 0.01)
+
+
+# --------------------------------------------------------- PointCloudMat
+def test_pointcloudmat_validation():
+    m = PointCloudMat(shape_type=ShapeType.XYZRGB).build(np.zeros((5, 6), np.float32))
+    assert m.info.N == 5 and m.info.device == "cpu" and m.info.raw_shape == [5, 6]
+    with pytest.raises(ValueError):
+        PointCloudMat(shape_type=ShapeType.XYZ).build(np.zeros((5, 4), np.float32))
+    with pytest.raises(ValueError):
+        PointCloudMat(shape_type=ShapeType.XYZ).build(np.zeros(5, np.float32))
+    with pytest.raises(TypeError):
+        PointCloudMat(shape_type=ShapeType.XYZ).build([[0, 0, 0]])
+    with pytest.raises(TypeError):
+        m.require_torch_tensor()
+    t = PointCloudMat(shape_type=ShapeType.XYZ).build(torch.zeros((4, 3), dtype=torch.float64))
+    with pytest.raises(TypeError):
+        t.require_torch_float()
+    assert ShapeType.XYZ.add_normals() == ShapeType.XYZN and ShapeType.XYZRGBiN.contains_normals()
+    assert PointCloudMat.random("XYZN", 7).data().shape == (7, 6)
+
+
+def test_build_out_mats_rules():
+    p = o3p.Processors.DoingNothing()
+    a = PointCloudMat(shape_type=ShapeType.XYZ).build(np.zeros((3, 3), np.float32))
+    b = PointCloudMat(shape_type=ShapeType.XYZN).build(np.zeros((3, 6), np.float32))
+    assert len(p.build_out_mats([a], [np.zeros((2, 3)), np.zeros((1, 3))])) == 2
+    assert p.build_out_mats([a, a], [np.zeros((2, 3))])[0].info.shape_type == ShapeType.XYZ
+    with pytest.raises(ValueError):
+        p.build_out_mats([a, b], [np.zeros((2, 3))])
+    with pytest.raises(ValueError):
+        p.build_out_mats([a, a, a], [np.zeros((2, 3)), np.zeros((2, 3))])
+
+
+def test_pipeline_json_roundtrip():
+    pipes = [o3p.Processors.RandomSample(n_samples=5), o3p.Processors.VoxelDownsample(voxel_size=0.2),
+             o3p.Processors.PlaneDetection(distance_threshold=0.02, alpha=0.1),
+             o3p.Processors.ICP(max_correspondence_distance=0.05)]
+    js = o3p.PointCloudMatProcessors.dumps(pipes)
+    back = o3p.PointCloudMatProcessors.loads(js)
+    assert [type(p) for p in back] == [type(p) for p in pipes]
+    assert back[2].alpha == 0.1 and back[1].voxel_size == 0.2
+    assert back[0].uuid == pipes[0].uuid
+
+
+def test_host_processors_run():
+    data = np.random.rand(100, 3).astype(np.float32)
+    m = PointCloudMat(shape_type=ShapeType.XYZ).build(data)
+    meta = {}
+    pipes = [o3p.Processors.RandomSample(n_samples=40), o3p.Processors.RadiusSelection(radius=1.0)]
+    out, meta = o3p.PointCloudMatProcessors.run_once([m], meta, pipes, validate=True)
+    assert out[0].data().shape[0] <= 40
+    # PlaneNormalize maps the plane z = 0.5 onto z = 0
+    pn = o3p.Processors.PlaneNormalize(detection_uuid="det")
+    pts = np.c_[np.random.rand(10, 2), np.full(10, 0.5)].astype(np.float32)
+    mm = PointCloudMat(shape_type=ShapeType.XYZ).build(pts)
+    res, _ = pn.validate([mm], {"det": [[0, 0, 1, -0.5]]})
+    np.testing.assert_allclose(res[0].data()[:, 2], 0, atol=1e-6)
+
+
+# ------------------------------------------------------------- synthetic
+def test_synthetic_deterministic_and_sharded():
+    a = S.uniform_cube(1000, 3)
+    b = torch.cat([S.uniform_cube(400, 3), S.uniform_cube(600, 3, offset=400)])
+    assert torch.equal(a, b)
+    assert a.min() >= 0 and a.max() < 1
+    p = S.planted_plane(20000, 1)
+    assert 0.15 < ((p[:, 2] - 0.5).abs() < 0.01).float().mean() < 0.3
+    s = S.box_surface(5000, 2)
+    on_face = ((s == 0) | (s == torch.tensor([1.0, 0.8, 0.6]))).any(1)
+    assert bool(on_face.all())
