@@ -76,6 +76,14 @@ void o3dx_set_kernel_timing(int enable);
 void o3dx_reset_kernel_timing(void);
 int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches);
 
+/* Debug-only neighbour-search statistics: when enabled, every grid search
+ * (normals, kNN, ICP) adds {queries, cells visited, candidate points, shells}
+ * into device counters read by o3dx_search_stats (synchronises the device).
+ * Enabling allocates a 64-byte device buffer — the only device allocation the
+ * library ever makes; off by default. */
+int o3dx_set_search_stats(int enable);
+int o3dx_search_stats(int64_t* out4_host);
+
 /* ---------------------------------------------------------------- AABB
  * Replaces o3d.geometry.PointCloud.get_min_bound()/get_max_bound()
  * (reference PointCloud.py:145-146, :340).
@@ -215,6 +223,10 @@ int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
  * o3dx_icp_target_build: builds the persistent target structure (spatial grid
  *   of target points + normals) inside `target_ws`; desc_host (16 doubles)
  *   receives its descriptor, to be passed back to o3dx_icp_accumulate.
+ * o3dx_spatial_sort: (n,4) float32 copy of a cloud ordered by spatial grid
+ *   cell, w = bits of the original int32 index.  ICP sources are passed in
+ *   this layout (src_sorted4 = 1) so that the 64 queries of a wave probe
+ *   neighbouring target cells; results are reported by original index.
  * o3dx_icp_accumulate: one fused pass over the source: transform by T_host
  *   (row-major 4x4, float64), 1-NN, residual/Jacobian, fixed-order float64
  *   reduction into sums_host[O3DX_ICP_NSUMS].  corr_out_dev (nullable, 2*ns
@@ -222,7 +234,8 @@ int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
  * o3dx_icp_solve_point_to_plane: host-only 6x6 LDLT solve of the summed
  *   system -> update_host (4x4 row-major); returns 1 if solved, 0 if singular
  *   (identity update, as Open3D).
- * o3dx_registration_icp_point_to_plane: the whole Open3D loop on one device.
+ * o3dx_registration_icp_point_to_plane: the whole Open3D loop on one device
+ *   (ws sized by o3dx_registration_icp_workspace_bytes; sorts the source once).
  */
 size_t o3dx_icp_target_workspace_bytes(int64_t nt);
 int o3dx_icp_target_build(const float* tgt_dev, const float* tgt_normals_dev,
@@ -230,13 +243,18 @@ int o3dx_icp_target_build(const float* tgt_dev, const float* tgt_normals_dev,
                           void* target_ws, size_t target_ws_bytes,
                           double* desc_host, void* stream);
 size_t o3dx_icp_accumulate_workspace_bytes(int64_t ns);
-int o3dx_icp_accumulate(const float* src_dev, int64_t ns,
+int o3dx_icp_accumulate(const float* src_dev, int64_t ns, int src_sorted4,
                         const void* target_ws, const double* desc_host,
                         const double* T_host, double max_correspondence_distance,
                         double* sums_host, int32_t* corr_out_dev,
                         int64_t* ncorr_host, void* ws, size_t ws_bytes,
                         void* stream);
 int o3dx_icp_solve_point_to_plane(const double* sums_host, double* update_host);
+size_t o3dx_spatial_sort_workspace_bytes(int64_t n);
+int o3dx_spatial_sort(const float* xyz_dev, int64_t n, double target_occ,
+                      float* sorted4_dev, void* ws, size_t ws_bytes,
+                      void* stream);
+size_t o3dx_registration_icp_workspace_bytes(int64_t ns);
 int o3dx_registration_icp_point_to_plane(
     const float* src_dev, int64_t ns, const float* tgt_dev,
     const float* tgt_normals_dev, int64_t nt,

@@ -100,6 +100,12 @@ static GridLayout grid_layout(int64_t n) {
 
 size_t grid_ws_bytes(int64_t n) { return grid_layout(n).total; }
 
+// Debug-only search statistics (o3dx_search_stats): the one place the library
+// allocates device memory, and only after o3dx_set_search_stats(1).
+static unsigned long long* g_stats = nullptr;
+static bool g_stats_on = false;
+unsigned long long* search_stats_ptr() { return g_stats_on ? g_stats : nullptr; }
+
 static void dims_for(const double mn[3], const double mx[3], double h, int64_t d[3]) {
   for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor(std::max(0.0, mx[a] - mn[a]) / h) + 1;
 }
@@ -179,6 +185,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     g.ny = (int)d[1];
     g.nz = (int)d[2];
     g.n = n;
+    g.stats = search_stats_ptr();
     // assignment error of a float32 cell computation, both sides of a face
     g.slack = (float)(32.0 * std::ldexp(1.0, -24) * (maxabs + maxext) + 1e-6 * h);
     const int64_t nc = d[0] * d[1] * d[2];
@@ -218,6 +225,86 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     O3DX_HIP(hipGetLastError());
     break;
   }
+  return 0;
+}
+
+
+// ------------------------------------------------------------- chunk plan
+__device__ __forceinline__ int query_row(const GridView& g, float4 v, const Mat4d& T, int useT) {
+  float x = v.x, y = v.y, z = v.z;
+  if (useT) {
+    const double* t = T.m;
+    const double X = v.x, Y = v.y, Z = v.z;
+    x = (float)(((t[0] * X + t[1] * Y) + t[2] * Z) + t[3]);
+    y = (float)(((t[4] * X + t[5] * Y) + t[6] * Z) + t[7]);
+    z = (float)(((t[8] * X + t[9] * Y) + t[10] * Z) + t[11]);
+  }
+  int cx, cy, cz;
+  grid_cell(g, x, y, z, cx, cy, cz);
+  return cy + g.ny * cz;
+}
+
+__global__ void __launch_bounds__(kBlock) k_row_flags(const float4* __restrict__ q, int64_t n, GridView g, Mat4d T,
+                                                      int useT, uint8_t* __restrict__ flags) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = query_row(g, q[i], T, useT);
+    flags[i] = (i == 0 || r != query_row(g, q[i - 1], T, useT)) ? 1 : 0;
+  }
+}
+
+__global__ void k_run_nchunks(const int32_t* __restrict__ run_start, int64_t R, int64_t n, int qcap,
+                              int32_t* __restrict__ nch) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= R) return;
+  const int64_t a = run_start[k], b = (k + 1 < R) ? run_start[k + 1] : n;
+  nch[k] = (int32_t)((b - a + qcap - 1) / qcap);
+}
+
+__global__ void k_emit_chunks(const int32_t* __restrict__ run_start, int64_t R, int64_t n, int qcap,
+                              const int32_t* __restrict__ offs, int32_t* __restrict__ chunk_starts) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= R) return;
+  const int64_t a = run_start[k], b = (k + 1 < R) ? run_start[k + 1] : n;
+  int32_t o = offs[k];
+  for (int64_t p = a; p < b; p += qcap) chunk_starts[o++] = (int32_t)p;
+  if (k == R - 1) chunk_starts[offs[R]] = (int32_t)n;
+}
+
+size_t chunk_plan_ws_bytes(int64_t n) {
+  n = std::max<int64_t>(n, 1);
+  return Arena::align(n + 17) + 3 * Arena::align((n + 2) * 4) + Arena::align(scan_workspace_ints(n + 1) * 4 + 1) + 1024;
+}
+
+int chunk_plan(const float4* q, int64_t n, const GridView& g, const double* T, int qcap, int32_t* chunk_starts,
+               int64_t* nchunks, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (ws_bytes < chunk_plan_ws_bytes(n)) return fail(O3DX_ENOMEM, "chunk plan workspace too small");
+  if (n == 0) {
+    *nchunks = 0;
+    return 0;
+  }
+  Arena ar(ws, ws_bytes);
+  uint8_t* flags = ar.take<uint8_t>(n + 16);
+  int32_t* runs = ar.take<int32_t>(n + 1);
+  int32_t* nch = ar.take<int32_t>(n + 1);
+  int32_t* offs = ar.take<int32_t>(n + 1);
+  int32_t* tmp = ar.take<int32_t>(scan_workspace_ints(n + 1));
+  int64_t* cnt = ar.take<int64_t>(2);
+  Mat4d M;
+  for (int i = 0; i < 16; ++i) M.m[i] = T ? T[i] : ((i % 5 == 0) ? 1.0 : 0.0);
+  hipLaunchKernelGGL(k_row_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, q, n, g, M, T ? 1 : 0, flags);
+  O3DX_TRY(compact_flags(flags, n, runs, nullptr, cnt, tmp, s));
+  int64_t R = 0;
+  O3DX_HIP(hipMemcpyAsync(&R, cnt, sizeof(R), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  hipLaunchKernelGGL(k_run_nchunks, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, runs, R, n, qcap, nch);
+  O3DX_TRY(exclusive_scan_i32(nch, offs, R, tmp, s));
+  hipLaunchKernelGGL(k_emit_chunks, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, runs, R, n, qcap, offs,
+                     chunk_starts);
+  int32_t total = 0;
+  O3DX_HIP(hipMemcpyAsync(&total, offs + R, sizeof(total), hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_HIP(hipGetLastError());
+  *nchunks = total;
   return 0;
 }
 
@@ -431,9 +518,11 @@ __device__ __forceinline__ void finish_normal(int cnt, const MomAcc& acc, const 
 template <int K>
 __global__ void __launch_bounds__(kBlock) k_normals_knn(GridView g, const float* __restrict__ xyz, int kneed,
                                                         int hybrid, double radius, const float* __restrict__ prior,
-                                                        float* __restrict__ out) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= g.n) return;
+                                                        float* __restrict__ out, const int32_t* __restrict__ list,
+                                                        const int32_t* __restrict__ list_len) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (list ? t >= *list_len : t >= g.n) return;
+  const int64_t s = list ? list[t] : t;
   const float4 q = g.pts[s];
   const int oi = __float_as_int(q.w);
   double bd[K];
@@ -448,6 +537,274 @@ __global__ void __launch_bounds__(kBlock) k_normals_knn(GridView g, const float*
       acc.add((double)xyz[3 * id], (double)xyz[3 * id + 1], (double)xyz[3 * id + 2]);
     }
   finish_normal(cnt, acc, prior, oi, out);
+}
+
+
+// ---------------------------------------------------------------------------
+// KNN normals, histogram-select form (the default KNN path).
+//
+// Per query (one lane), with R = the radius inside which every point has been
+// scanned after shells 0..S (R = S h + m - slack):
+//   pass 1  float32 d^2 of every candidate in shells 0..S; the ones inside R
+//           are counted into NB bins uniform in d^2 (LDS, 16-bit counters);
+//           grow S until >= k lie inside R;
+//   locate  the bin b* holding the k-th distance -> [L, U);
+//   pass 2  rescan: d^2 < L(1-2e) is certainly among the k nearest (appended to
+//           an LDS list), d^2 in the band [L(1-2e), U(1+2e)) is a boundary
+//           candidate (LDS list), the rest is certainly out — e = 2^-20 bounds
+//           the float32 distance error relative to float64;
+//   pass 3  the (k - #certain) nearest boundary candidates by exact float64
+//           (d^2, index), i.e. the same set as the oracle / nanoflann;
+//   pass 4  Open3D's float64 raw moments over the k selected, FastEigen3x3.
+// No per-candidate sorted insertion: cost is ~2 scans of the 27-cell
+// neighbourhood in float32 plus O(k) float64 work.  Queries the form cannot
+// settle (the shell reaches the grid edge, a boundary list overflows) go to a
+// list served by the exact register top-k kernel above.
+constexpr int kHistBins = 16;
+constexpr int kBndCap = 16;
+constexpr float kRelEps = 9.5367431640625e-07f;  // 2^-20
+
+__device__ __forceinline__ float dist2_f32(const float4 q, const float4 p) {
+  const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+  return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+}
+
+template <int KMAX>
+__global__ void __launch_bounds__(64) k_normals_knn_hist(GridView g, int kneed, const float* __restrict__ prior,
+                                                         float* __restrict__ out, const int32_t* __restrict__ in_list,
+                                                         const int32_t* __restrict__ in_len,
+                                                         int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len) {
+  __shared__ uint32_t hist[kHistBins / 2][64];
+  __shared__ int32_t sel[KMAX][64];
+  __shared__ int32_t bnd[kBndCap][64];
+  const int lane = threadIdx.x;
+  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
+  if (in_list ? t >= *in_len : t >= g.n) return;
+  const int64_t s = in_list ? in_list[t] : t;
+  const float4 q = g.pts[s];
+  const int oi = __float_as_int(q.w);
+  int cx, cy, cz;
+  grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
+  const double m = cell_margin(g, q.x, q.y, q.z, cx, cy, cz);
+  const int rmax = shell_rmax(g, cx, cy, cz);
+  bool fb = false;
+  int S = 1;
+  float R2 = 0.f;
+  for (;; ++S) {
+    if (S >= rmax) {  // shells would cover the whole grid: leave it to the exact path
+      fb = true;
+      break;
+    }
+    const double R = (double)S * g.h + m - g.slack;
+    if (R <= 0.0) continue;
+#pragma unroll
+    for (int b = 0; b < kHistBins / 2; ++b) hist[b][lane] = 0u;
+    R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
+    const float scale = (float)kHistBins / R2;
+    int total = 0;
+    for_cube_rows(g, cx, cy, cz, S, [&](int p0, int p1) {
+      for_points4(g, p0, p1, [&](int, const float4 v) {
+        const float d2 = dist2_f32(q, v);
+        if (d2 < R2) {
+          const int b = min((int)(d2 * scale), kHistBins - 1);
+          hist[b >> 1][lane] += (b & 1) ? 0x10000u : 1u;
+          ++total;
+        }
+      });
+    });
+    if (total >= kneed) break;
+  }
+  if (!fb) {
+    int bstar = -1, cum = 0;
+#pragma unroll
+    for (int b = 0; b < kHistBins; ++b) {
+      const uint32_t w = hist[b >> 1][lane];
+      const int c = (b & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
+      if (bstar < 0 && cum + c >= kneed) bstar = b;
+      cum += c;
+    }
+    const float bw = R2 / (float)kHistBins;
+    const float Lm = (float)bstar * bw * (1.0f - 2.0f * kRelEps);
+    const float Up = (bstar == kHistBins - 1 ? R2 : (float)(bstar + 1) * bw) * (1.0f + 2.0f * kRelEps);
+    int nsel = 0, nb = 0;
+    for_cube_rows(g, cx, cy, cz, S, [&](int p0, int p1) {
+      for_points4(g, p0, p1, [&](int p, const float4 v) {
+        const float d2 = dist2_f32(q, v);
+        if (d2 < Lm) {
+          if (nsel < KMAX) sel[nsel][lane] = p;
+          ++nsel;
+        } else if (d2 < Up) {
+          if (nb < kBndCap) bnd[nb][lane] = p;
+          ++nb;
+        }
+      });
+    });
+    if (nsel > kneed || nb > kBndCap || nsel + nb < kneed) fb = true;
+    if (!fb) {
+      // exact tail: the (kneed - nsel) nearest boundary candidates by (d2_f64, index)
+      const double qx = q.x, qy = q.y, qz = q.z;
+      for (int t = nsel; t < kneed; ++t) {
+        int bj = -1, bidx = 0x7fffffff;
+        double bdd = INFINITY;
+        for (int j = 0; j < nb; ++j) {
+          const int p = bnd[j][lane];
+          if (p < 0) continue;
+          const float4 v = g.pts[p];
+          const double d = dist2_f64(qx, qy, qz, v);
+          const int id = __float_as_int(v.w);
+          if (lex_less(d, id, bdd, bidx)) {
+            bdd = d;
+            bidx = id;
+            bj = j;
+          }
+        }
+        sel[t][lane] = bnd[bj][lane];
+        bnd[bj][lane] = -1;
+      }
+      MomAcc acc;
+      acc.zero();
+      for (int j = 0; j < kneed; ++j) {
+        const float4 v = g.pts[sel[j][lane]];
+        acc.add((double)v.x, (double)v.y, (double)v.z);
+      }
+      finish_normal(kneed, acc, prior, oi, out);
+    }
+  }
+  if (fb) {
+    const int at = atomicAdd(fb_len, 1);
+    fb_list[at] = (int32_t)s;
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// KNN normals, LDS-tile form (first level of the default KNN path).
+// One block = one chunk of <= kTileQ queries in one grid row; the 9-row
+// neighbour box is staged into LDS (coalesced), then every query runs the
+// histogram-select passes of k_normals_knn_hist over LDS-resident candidates
+// (shells 0..1 only).  Queries the tile cannot settle (fewer than k points
+// within the shell-1 radius, or the box overflows LDS) are appended to
+// fb_list for the global-memory form.
+constexpr int kTileQ = 128;
+constexpr int kTilePts = 1536;
+constexpr int kTileCs = 640;
+
+template <int KMAX>
+__global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
+                                                             int kneed, const float* __restrict__ prior,
+                                                             float* __restrict__ out, int32_t* __restrict__ fb_list,
+                                                             int32_t* __restrict__ fb_len) {
+  __shared__ float4 tp[kTilePts];
+  __shared__ int32_t ccs[kTileCs];
+  __shared__ int32_t rows[kMaxTileRows + 1];
+  __shared__ int32_t rst[kMaxTileRows];
+  __shared__ uint32_t hist[kHistBins / 2][kTileQ];
+  __shared__ uint16_t sel[KMAX][kTileQ];
+  __shared__ uint16_t bnd[kBndCap][kTileQ];
+  const int tid = threadIdx.x;
+  const int q0 = chunk_starts[blockIdx.x], q1 = chunk_starts[blockIdx.x + 1];
+  const int64_t s = (int64_t)q0 + tid;
+  const bool active = s < q1;
+  // the chunk lies in one (y,z) row and is sorted by x: first/last give the box
+  int ax, ay, az, bx, by, bz;
+  {
+    const float4 f = g.pts[q0], l = g.pts[q1 - 1];
+    grid_cell(g, f.x, f.y, f.z, ax, ay, az);
+    grid_cell(g, l.x, l.y, l.z, bx, by, bz);
+  }
+  TileBox box;
+  box.x0 = max(min(ax, bx) - 1, 0);
+  box.x1 = min(max(ax, bx) + 1, g.nx - 1);
+  box.y0 = max(ay - 1, 0);
+  box.y1 = min(ay + 1, g.ny - 1);
+  box.z0 = max(az - 1, 0);
+  box.z1 = min(az + 1, g.nz - 1);
+  box.nxr = box.x1 - box.x0 + 1;
+  box.nyr = box.y1 - box.y0 + 1;
+  const int staged = stage_tile<kTileQ>(g, box, tp, kTilePts, ccs, kTileCs, rows, rst);
+  if (!active) return;  // no barrier below this point
+  const float4 q = g.pts[s];
+  int cx, cy, cz;
+  grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
+  bool fb = staged < 0 || cy != ay || cz != az;
+  if (!fb) {
+    const double R = (double)g.h + cell_margin(g, q.x, q.y, q.z, cx, cy, cz) - g.slack;
+    const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
+    const float scale = (float)kHistBins / fmaxf(R2, 1e-30f);
+#pragma unroll
+    for (int b = 0; b < kHistBins / 2; ++b) hist[b][tid] = 0u;
+    int total = 0;
+    for_tile_rows(box, ccs, cx, cy, cz, [&](int a, int e) {
+      for (int p = a; p < e; ++p) {
+        const float d2 = dist2_f32(q, tp[p]);
+        if (d2 < R2) {
+          const int b = min((int)(d2 * scale), kHistBins - 1);
+          hist[b >> 1][tid] += (b & 1) ? 0x10000u : 1u;
+          ++total;
+        }
+      }
+    });
+    fb = total < kneed;
+    if (!fb) {
+      int bstar = -1, cum = 0;
+#pragma unroll
+      for (int b = 0; b < kHistBins; ++b) {
+        const uint32_t w = hist[b >> 1][tid];
+        const int c = (b & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
+        if (bstar < 0 && cum + c >= kneed) bstar = b;
+        cum += c;
+      }
+      const float bw = R2 / (float)kHistBins;
+      const float Lm = (float)bstar * bw * (1.0f - 2.0f * kRelEps);
+      const float Up = (bstar == kHistBins - 1 ? R2 : (float)(bstar + 1) * bw) * (1.0f + 2.0f * kRelEps);
+      int nsel = 0, nb = 0;
+      for_tile_rows(box, ccs, cx, cy, cz, [&](int a, int e) {
+        for (int p = a; p < e; ++p) {
+          const float d2 = dist2_f32(q, tp[p]);
+          if (d2 < Lm) {
+            if (nsel < KMAX) sel[nsel][tid] = (uint16_t)p;
+            ++nsel;
+          } else if (d2 < Up) {
+            if (nb < kBndCap) bnd[nb][tid] = (uint16_t)p;
+            ++nb;
+          }
+        }
+      });
+      fb = nsel > kneed || nb > kBndCap || nsel + nb < kneed;
+      if (!fb) {
+        const double qx = q.x, qy = q.y, qz = q.z;
+        for (int t = nsel; t < kneed; ++t) {
+          int bj = 0, bidx = 0x7fffffff;
+          double bdd = INFINITY;
+          for (int j = 0; j < nb; ++j) {
+            const int p = bnd[j][tid];
+            if (p == 0xffff) continue;
+            const float4 v = tp[p];
+            const double d = dist2_f64(qx, qy, qz, v);
+            const int id = __float_as_int(v.w);
+            if (lex_less(d, id, bdd, bidx)) {
+              bdd = d;
+              bidx = id;
+              bj = j;
+            }
+          }
+          sel[t][tid] = bnd[bj][tid];
+          bnd[bj][tid] = 0xffff;
+        }
+        MomAcc acc;
+        acc.zero();
+        for (int j = 0; j < kneed; ++j) {
+          const float4 v = tp[sel[j][tid]];
+          acc.add((double)v.x, (double)v.y, (double)v.z);
+        }
+        finish_normal(kneed, acc, prior, __float_as_int(q.w), out);
+      }
+    }
+  }
+  if (fb) {
+    const int at = atomicAdd(fb_len, 1);
+    fb_list[at] = (int32_t)s;
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_normals_radius(GridView g, double radius, const float* __restrict__ prior,
@@ -519,7 +876,9 @@ static int pick_k(int k) {
 // grid occupancy target per search mode: ~k/4 points per cell keeps the
 // 27-cell first shell close to 2-3 k candidates
 static double occ_for(int mode, int k) {
+  if (const char* e = getenv("O3DX_GRID_OCC")) return atof(e);  // tuning override
   if (mode == O3DX_SEARCH_RADIUS) return 4.0;
+  if (mode == O3DX_SEARCH_KNN) return std::max(4.0, k / 3.0);  // histogram path: shells 0..1 hold k
   return std::max(2.0, k / 4.0);
 }
 
@@ -527,7 +886,32 @@ static double occ_for(int mode, int k) {
 
 using namespace o3dx;
 
-extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) { return grid_ws_bytes(n) + 1024; }
+extern "C" int o3dx_set_search_stats(int enable) {
+  if (enable && !g_stats) {
+    if (hipMalloc(&g_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {
+      g_stats = nullptr;
+      return fail(O3DX_EIO, "stats buffer allocation failed");
+    }
+  }
+  g_stats_on = enable != 0;
+  if (g_stats && hipMemset(g_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess)
+    return fail(O3DX_EIO, "stats reset failed");
+  return 0;
+}
+
+extern "C" int o3dx_search_stats(int64_t* out) {
+  if (!out) return fail(O3DX_EINVAL, "o3dx_search_stats: null output");
+  unsigned long long v[4] = {0, 0, 0, 0};
+  if (g_stats && hipDeviceSynchronize() == hipSuccess)
+    (void)hipMemcpy(v, g_stats, sizeof(v), hipMemcpyDeviceToHost);
+  for (int i = 0; i < 4; ++i) out[i] = (int64_t)v[i];
+  return 0;
+}
+
+extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
+  n = std::max<int64_t>(n, 1);
+  return grid_ws_bytes(n) + 4 * Arena::align((n + 3) * 4) + chunk_plan_ws_bytes(n) + 4096;
+}
 
 extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,
                                      const float* prior, float* out, void* ws, size_t ws_bytes, void* stream) {
@@ -545,12 +929,54 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
   O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), min_h, ws, ws_bytes, s, &G));
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
   KTimer kt("normals_knn", s);
+  const int kneed = (int)std::min<int64_t>(knn, n);
   if (mode == O3DX_SEARCH_RADIUS) {
     hipLaunchKernelGGL(k_normals_radius, dim3(grid), dim3(kBlock), 0, s, G.view, radius, prior, out);
+  } else if (mode == O3DX_SEARCH_KNN && kneed >= 1 && !getenv("O3DX_NORMALS_TOPK")) {
+    // LDS tiles -> global histogram-select -> exact register top-k, each level
+    // serving the queries the previous one could not settle
+    Arena ar((char*)ws + grid_ws_bytes(n), ws_bytes - grid_ws_bytes(n));
+    int32_t* lens = ar.take<int32_t>(4);
+    int32_t* list1 = ar.take<int32_t>(n);
+    int32_t* list2 = ar.take<int32_t>(n);
+    int32_t* chunks = ar.take<int32_t>(n + 2);
+    void* pws = ar.take<char>(chunk_plan_ws_bytes(n));
+    O3DX_ARENA_CHECK(ar);
+    O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
+    const unsigned g64 = (unsigned)((n + 63) / 64);
+    const bool tiles = !getenv("O3DX_NORMALS_NO_TILES");
+    if (tiles) {
+      int64_t nchunks = 0;
+      kt.stop();
+      O3DX_TRY(chunk_plan(G.view.pts, n, G.view, nullptr, kTileQ, chunks, &nchunks, pws,
+                          chunk_plan_ws_bytes(n), s));
+      KTimer kt2("normals_knn", s);
+      if (kneed <= 32)
+        hipLaunchKernelGGL(k_normals_knn_tile<32>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
+                           kneed, prior, out, list1, lens);
+      else
+        hipLaunchKernelGGL(k_normals_knn_tile<64>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
+                           kneed, prior, out, list1, lens);
+      if (kneed <= 32)
+        hipLaunchKernelGGL(k_normals_knn_hist<32>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out, list1, lens,
+                           list2, lens + 1);
+      else
+        hipLaunchKernelGGL(k_normals_knn_hist<64>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out, list1, lens,
+                           list2, lens + 1);
+    } else {
+      if (kneed <= 32)
+        hipLaunchKernelGGL(k_normals_knn_hist<32>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out,
+                           (const int32_t*)nullptr, (const int32_t*)nullptr, list2, lens + 1);
+      else
+        hipLaunchKernelGGL(k_normals_knn_hist<64>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out,
+                           (const int32_t*)nullptr, (const int32_t*)nullptr, list2, lens + 1);
+    }
+    O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, 0, radius, prior,
+                    out, list2, lens + 1);
   } else {
-    const int kneed = (int)std::min<int64_t>(knn, n);
     O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed,
-                    mode == O3DX_SEARCH_HYBRID ? 1 : 0, radius, prior, out);
+                    mode == O3DX_SEARCH_HYBRID ? 1 : 0, radius, prior, out, (const int32_t*)nullptr,
+                    (const int32_t*)nullptr);
   }
   O3DX_HIP(hipGetLastError());
   return 0;

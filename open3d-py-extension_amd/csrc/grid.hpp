@@ -12,6 +12,10 @@
 
 namespace o3dx {
 
+struct Mat4d {
+  double m[16];
+};
+
 struct GridView {
   const float4* __restrict__ pts;      // sorted by cell: (x, y, z, bits(original index))
   const int32_t* __restrict__ start;   // ncells + 1
@@ -19,7 +23,17 @@ struct GridView {
   float slack;                         // conservative rounding margin for the stop test
   int nx, ny, nz;
   int64_t n;
+  unsigned long long* stats;  // debug: {queries, cells visited, candidates, shells}; null = off
 };
+
+__device__ __forceinline__ void search_stats(const GridView& g, int cells, int cands, int shells) {
+  if (g.stats) {
+    atomicAdd(&g.stats[0], 1ull);
+    atomicAdd(&g.stats[1], (unsigned long long)cells);
+    atomicAdd(&g.stats[2], (unsigned long long)cands);
+    atomicAdd(&g.stats[3], (unsigned long long)shells);
+  }
+}
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
@@ -71,6 +85,39 @@ __device__ __forceinline__ void for_shell(const GridView& g, int cx, int cy, int
   }
 }
 
+// Visit the cube of cells within Chebyshev distance S of (cx,cy,cz) as
+// (2S+1)^2 row ranges: the cells of one (y,z) row are adjacent in the
+// cell-sorted array, so each row of the cube is ONE contiguous point range
+// [start[first], start[last+1]).  f(p0, p1) per row.
+template <class F>
+__device__ __forceinline__ void for_cube_rows(const GridView& g, int cx, int cy, int cz, int S, F&& f) {
+  const int x0 = max(cx - S, 0), x1 = min(cx + S, g.nx - 1);
+  for (int dz = -S; dz <= S; ++dz) {
+    const int z = cz + dz;
+    if (z < 0 || z >= g.nz) continue;
+    for (int dy = -S; dy <= S; ++dy) {
+      const int y = cy + dy;
+      if (y < 0 || y >= g.ny) continue;
+      const int rb = g.nx * (y + g.ny * z);
+      f(g.start[rb + x0], g.start[rb + x1 + 1]);
+    }
+  }
+}
+
+// f(p, point) over [p0, p1) with four loads in flight per step
+template <class F>
+__device__ __forceinline__ void for_points4(const GridView& g, int p0, int p1, F&& f) {
+  int p = p0;
+  for (; p + 4 <= p1; p += 4) {
+    const float4 a = g.pts[p], b = g.pts[p + 1], c = g.pts[p + 2], d = g.pts[p + 3];
+    f(p, a);
+    f(p + 1, b);
+    f(p + 2, c);
+    f(p + 3, d);
+  }
+  for (; p < p1; ++p) f(p, g.pts[p]);
+}
+
 __device__ __forceinline__ int shell_rmax(const GridView& g, int cx, int cy, int cz) {
   return max(max(max(cx, g.nx - 1 - cx), max(cy, g.ny - 1 - cy)), max(cz, g.nz - 1 - cz));
 }
@@ -101,9 +148,14 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
   double wd = INFINITY;
   int wi = 0x7fffffff;
   int cnt = 0;
-  for (int r = 0; r <= rmax; ++r) {
+  int st_cells = 0, st_cands = 0, r = 0;
+  for (r = 0; r <= rmax; ++r) {
     for_shell(g, cx, cy, cz, r, [&](int c) {
       const int s1 = g.start[c + 1];
+      if (g.stats) {
+        ++st_cells;
+        st_cands += s1 - g.start[c];
+      }
       for (int p = g.start[c]; p < s1; ++p) {
         const float4 v = g.pts[p];
         const double d = dist2_f64(dqx, dqy, dqz, v);
@@ -138,6 +190,7 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
     if (cnt >= kneed && B > 0.0 && wd < B * B) break;
     if (hybrid && B >= radius) break;
   }
+  search_stats(g, st_cells, st_cands, r + 1);
   return cnt;
 }
 
@@ -162,28 +215,122 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   // outside the query's cell (clamped): m < 0 shrinks the bound, still valid
   const int rmax = shell_rmax(g, cx, cy, cz);
   const double r2lim = radius * radius;
-  for (int r = 0; r <= rmax; ++r) {
-    for_shell(g, cx, cy, cz, r, [&](int c) {
-      const int s1 = g.start[c + 1];
-      for (int p = g.start[c]; p < s1; ++p) {
-        const float4 v = g.pts[p];
-        const double d = dist2_f64(qx, qy, qz, v);
-        const int oi = __float_as_int(v.w);
-        if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
-          bd = d;
-          bi = oi;
-          bp = p;
-        }
-      }
-    });
+  int st_cells = 0, st_cands = 0, r = 1;
+  auto visit = [&](int p, const float4 v) {
+    const double d = dist2_f64(qx, qy, qz, v);
+    const int oi = __float_as_int(v.w);
+    if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
+      bd = d;
+      bi = oi;
+      bp = p;
+    }
+  };
+  // shells 0 and 1 together: 9 contiguous row ranges
+  for_cube_rows(g, cx, cy, cz, 1, [&](int p0, int p1) {
+    if (g.stats) {
+      st_cells += 3;
+      st_cands += p1 - p0;
+    }
+    for_points4(g, p0, p1, visit);
+  });
+  for (;; ++r) {
     const double B = (double)r * g.h + m - g.slack;
-    if (B >= radius) break;
+    if (B >= radius || r >= rmax) break;
     if (bi >= 0 && B > 0.0 && bd < B * B) break;
+    for_shell(g, cx, cy, cz, r + 1, [&](int c) {
+      const int s1 = g.start[c + 1];
+      if (g.stats) {
+        ++st_cells;
+        st_cands += s1 - g.start[c];
+      }
+      for_points4(g, g.start[c], s1, visit);
+    });
   }
+  search_stats(g, st_cells, st_cands, r + 1);
   *best_d2 = bd;
   *best_pos = bp;
   return bi;
 }
+
+// ------------------------------------------------------------- LDS tiles
+// A chunk = <= Q consecutive queries (spatially sorted).  Its neighbour region
+// = bounding box of the queries' cells +-1, staged row by row into LDS: each
+// (y,z) row of the box is one contiguous range of the cell-sorted array, so
+// the staging loads are coalesced.  ccs[k*(nxr+1) + i] is the LDS offset of
+// the first point of cell (x0+i) in box row k (i = nxr: end of the row).
+struct TileBox {
+  int x0, x1, y0, y1, z0, z1;
+  int nxr;  // x1 - x0 + 1
+  int nyr;  // y1 - y0 + 1
+};
+
+// Stage the box into LDS.  Every thread of the block must call it.  Returns
+// the number of staged points, or -1 if the box does not fit (pts_cap points
+// / cs_cap cell-start slots / kMaxTileRows rows).  `rows` needs kMaxTileRows+1 ints.
+constexpr int kMaxTileRows = 36;
+
+template <int BLOCK>
+__device__ int stage_tile(const GridView& g, const TileBox& b, float4* __restrict__ pts, int pts_cap,
+                          int32_t* __restrict__ ccs, int cs_cap, int32_t* __restrict__ rows,
+                          int32_t* __restrict__ rstart) {
+  const int nrows = b.nyr * (b.z1 - b.z0 + 1);
+  const int w = b.nxr + 1;
+  if (nrows > kMaxTileRows || nrows * w > cs_cap) return -1;  // uniform across the block
+  for (int t = threadIdx.x; t < nrows * w; t += BLOCK) {
+    const int k = t / w, i = t - k * w;
+    const int y = b.y0 + k % b.nyr, z = b.z0 + k / b.nyr;
+    ccs[t] = g.start[(b.x0 + i) + g.nx * (y + g.ny * z)];  // global position for now
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int k = 0; k < nrows; ++k) {
+      rows[k] = acc;
+      rstart[k] = ccs[k * w];
+      acc += ccs[k * w + b.nxr] - ccs[k * w];
+    }
+    rows[nrows] = acc;
+  }
+  __syncthreads();
+  const int total = rows[nrows];
+  if (total > pts_cap) return -1;
+  for (int t = threadIdx.x; t < nrows * w; t += BLOCK) {
+    const int k = t / w;
+    ccs[t] = rows[k] + (ccs[t] - rstart[k]);
+  }
+  int k = 0;  // f only grows, so the row index is carried along
+  for (int f = threadIdx.x; f < total; f += BLOCK) {
+    while (rows[k + 1] <= f) ++k;
+    pts[f] = g.pts[rstart[k] + (f - rows[k])];
+  }
+  __syncthreads();
+  return total;
+}
+
+// Cube S=1 around (cx,cy,cz) inside a staged box: f(lds_p0, lds_p1) per row.
+template <class F>
+__device__ __forceinline__ void for_tile_rows(const TileBox& b, const int32_t* ccs, int cx, int cy, int cz, F&& f) {
+  const int w = b.nxr + 1;
+  const int xa = max(cx - 1, b.x0) - b.x0, xb = min(cx + 1, b.x1) - b.x0;
+  for (int dz = -1; dz <= 1; ++dz) {
+    const int z = cz + dz;
+    if (z < b.z0 || z > b.z1) continue;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int y = cy + dy;
+      if (y < b.y0 || y > b.y1) continue;
+      const int k = (y - b.y0) + b.nyr * (z - b.z0);
+      f(ccs[k * w + xa], ccs[k * w + xb + 1]);
+    }
+  }
+}
+
+// Chunk plan: split a spatially sorted query list into chunks of <= qcap
+// consecutive queries whose cells share one (y,z) row of grid g (cells of the
+// queries after transform T when `T` is non-null).  chunk_starts gets
+// nchunks+1 entries (last = n).  Synchronises (the chunk count sizes launches).
+size_t chunk_plan_ws_bytes(int64_t n);
+int chunk_plan(const float4* q, int64_t n, const GridView& g, const double* T, int qcap, int32_t* chunk_starts,
+               int64_t* nchunks, void* ws, size_t ws_bytes, hipStream_t s);
 
 // ---------------------------------------------------------------- build
 struct GridBuild {
@@ -203,6 +350,7 @@ struct GridBuild {
 };
 
 size_t grid_ws_bytes(int64_t n);
+unsigned long long* search_stats_ptr();  // device counters when stats are enabled, else null
 // target_occ: desired mean points per occupied cell.  min_h: lower bound on h
 // (0 = none).  Synchronises the stream (cell size is chosen on the host).
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,

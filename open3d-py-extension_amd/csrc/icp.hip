@@ -26,6 +26,10 @@ struct Mat4 {
   double m[16];
 };
 
+// SORTED: src is float4 (x, y, z, bits(original index)) in spatial (grid-cell)
+// order, so the 64 queries of a wave probe neighbouring target cells; else
+// plain (n,3) float32 in caller order.
+template <bool SORTED>
 __global__ void __launch_bounds__(kBlock) k_icp_accumulate(const float* __restrict__ src, int64_t ns, GridView g,
                                                            const float4* __restrict__ tnorm, Mat4 T, double radius,
                                                            double* __restrict__ partial, int32_t* __restrict__ cj) {
@@ -34,17 +38,30 @@ __global__ void __launch_bounds__(kBlock) k_icp_accumulate(const float* __restri
 #pragma unroll
   for (int k = 0; k < 30; ++k) acc[k] = 0.0;
   const double* t = T.m;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
-    const double x = src[3 * i], y = src[3 * i + 1], z = src[3 * i + 2];
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += (int64_t)gridDim.x * blockDim.x) {
+    double x, y, z;
+    int64_t i;
+    if (SORTED) {
+      const float4 v = reinterpret_cast<const float4*>(src)[j];
+      x = v.x;
+      y = v.y;
+      z = v.z;
+      i = __float_as_int(v.w);
+    } else {
+      i = j;
+      x = src[3 * i];
+      y = src[3 * i + 1];
+      z = src[3 * i + 2];
+    }
     // Eigen 4x4 * (x,y,z,1): ((T0 x + T1 y) + T2 z) + T3 per row
     const double px = ((t[0] * x + t[1] * y) + t[2] * z) + t[3];
     const double py = ((t[4] * x + t[5] * y) + t[6] * z) + t[7];
     const double pz = ((t[8] * x + t[9] * y) + t[10] * z) + t[11];
     double d2;
     int pos;
-    const int j = nn_search_dev(g, px, py, pz, radius, &d2, &pos);
-    if (cj) cj[i] = j;
-    if (j < 0) continue;
+    const int tj = nn_search_dev(g, px, py, pz, radius, &d2, &pos);
+    if (cj) cj[i] = tj;
+    if (tj < 0) continue;
     const float4 vt = g.pts[pos];
     const float4 nt = tnorm[pos];
     const double nx = nt.x, ny = nt.y, nz = nt.z;
@@ -198,6 +215,7 @@ static bool desc_unpack(const double* d, const void* base, GridView* g, const fl
   g->ox = (float)d[0]; g->oy = (float)d[1]; g->oz = (float)d[2]; g->h = (float)d[3]; g->inv_h = (float)d[4];
   g->slack = (float)d[5];
   g->nx = (int)d[6]; g->ny = (int)d[7]; g->nz = (int)d[8]; g->n = (int64_t)d[9];
+  g->stats = search_stats_ptr();
   g->pts = (const float4*)((const char*)base + (int64_t)d[10]);
   g->start = (const int32_t*)((const char*)base + (int64_t)d[11]);
   *normals = (const float4*)((const char*)base + (int64_t)d[12]);
@@ -225,15 +243,18 @@ static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
   return ar.used;
 }
 
-static int accumulate(const float* src, int64_t ns, const GridView& g, const float4* tn, const double* T, double radius,
-                      AccWs& w, hipStream_t s, double* sums_host, int32_t* corr_out, int64_t* ncorr) {
+static int accumulate(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, const double* T,
+                      double radius, AccWs& w, hipStream_t s, double* sums_host, int32_t* corr_out, int64_t* ncorr) {
   Mat4 M;
   std::memcpy(M.m, T, sizeof(M.m));
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kIcpBlocks, (ns + kBlock - 1) / kBlock));
   const bool want_corr = corr_out != nullptr;
   KTimer kt("icp_accumulate", s);
-  if (ns > 0)
-    hipLaunchKernelGGL(k_icp_accumulate, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, radius, w.partial,
+  if (ns > 0 && sorted)
+    hipLaunchKernelGGL(k_icp_accumulate<true>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, radius, w.partial,
+                       want_corr ? w.cj : (int32_t*)nullptr);
+  else if (ns > 0)
+    hipLaunchKernelGGL(k_icp_accumulate<false>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, radius, w.partial,
                        want_corr ? w.cj : (int32_t*)nullptr);
   else
     O3DX_HIP(hipMemsetAsync(w.partial, 0, kNS * sizeof(double), s));
@@ -260,7 +281,14 @@ static int accumulate(const float* src, int64_t ns, const GridView& g, const flo
 }
 
 // grid occupancy / minimum cell for the 1-NN-within-radius search
-static double icp_min_h(double max_corr) { return max_corr / 8.0; }
+static double icp_min_h(double max_corr) {
+  if (const char* e = getenv("O3DX_ICP_MINH_DIV")) return max_corr / atof(e);  // tuning override
+  return max_corr / 8.0;
+}
+static double icp_occ() {
+  if (const char* e = getenv("O3DX_ICP_OCC")) return atof(e);
+  return 2.0;
+}
 
 }  // namespace o3dx
 
@@ -275,7 +303,7 @@ extern "C" int o3dx_icp_target_build(const float* tgt, const float* tgt_normals,
   if (!target_ws || target_ws_bytes < o3dx_icp_target_workspace_bytes(nt))
     return fail(O3DX_ENOMEM, "icp target workspace too small");
   GridBuild G;
-  O3DX_TRY(grid_build(tgt, nt, 2.0, icp_min_h(max_corr), target_ws, target_ws_bytes, as_stream(stream), &G, nullptr,
+  O3DX_TRY(grid_build(tgt, nt, icp_occ(), icp_min_h(max_corr), target_ws, target_ws_bytes, as_stream(stream), &G, nullptr,
                       tgt_normals));
   desc_pack(G, target_ws, G.extra, desc);
   return 0;
@@ -287,9 +315,9 @@ extern "C" size_t o3dx_icp_accumulate_workspace_bytes(int64_t ns) {
   return acc_carve(ar, std::max<int64_t>(ns, 1), &w) + 1024;
 }
 
-extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, const void* target_ws, const double* desc,
-                                   const double* T, double max_corr, double* sums, int32_t* corr_out, int64_t* ncorr,
-                                   void* ws, size_t ws_bytes, void* stream) {
+extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, int src_sorted4, const void* target_ws,
+                                   const double* desc, const double* T, double max_corr, double* sums,
+                                   int32_t* corr_out, int64_t* ncorr, void* ws, size_t ws_bytes, void* stream) {
   if (ns < 0 || (ns > 0 && !src) || !target_ws || !T || !sums) return fail(O3DX_EINVAL, "o3dx_icp_accumulate: bad args");
   GridView g;
   const float4* tn;
@@ -298,12 +326,32 @@ extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, const void* tar
   Arena ar(ws, ws_bytes);
   AccWs w;
   acc_carve(ar, std::max<int64_t>(ns, 1), &w);
-  return accumulate(src, ns, g, tn, T, max_corr, w, as_stream(stream), sums, corr_out, ncorr);
+  return accumulate(src, ns, src_sorted4 != 0, g, tn, T, max_corr, w, as_stream(stream), sums, corr_out, ncorr);
+}
+
+extern "C" size_t o3dx_spatial_sort_workspace_bytes(int64_t n) { return grid_ws_bytes(n) + 1024; }
+
+extern "C" int o3dx_spatial_sort(const float* xyz, int64_t n, double target_occ, float* sorted4, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  if (n < 0 || (n > 0 && (!xyz || !sorted4))) return fail(O3DX_EINVAL, "o3dx_spatial_sort: bad args");
+  if (!ws || ws_bytes < o3dx_spatial_sort_workspace_bytes(n)) return fail(O3DX_ENOMEM, "spatial_sort workspace too small");
+  if (n == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  GridBuild G;
+  O3DX_TRY(grid_build(xyz, n, target_occ > 0 ? target_occ : 8.0, 0.0, ws, ws_bytes, s, &G));
+  O3DX_HIP(hipMemcpyAsync(sorted4, G.pts, (size_t)n * sizeof(float4), hipMemcpyDeviceToDevice, s));
+  return 0;
 }
 
 extern "C" int o3dx_icp_solve_point_to_plane(const double* sums, double* upd) {
   if (!sums || !upd) return fail(O3DX_EINVAL, "o3dx_icp_solve_point_to_plane: bad args");
   return solve_update(sums, upd);
+}
+
+extern "C" size_t o3dx_registration_icp_workspace_bytes(int64_t ns) {
+  ns = std::max<int64_t>(ns, 1);
+  return Arena::align((size_t)ns * sizeof(float4) + 1) +
+         std::max(o3dx_icp_accumulate_workspace_bytes(ns), o3dx_spatial_sort_workspace_bytes(ns)) + 1024;
 }
 
 extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns, const float* tgt,
@@ -320,8 +368,13 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
   GridView g;
   const float4* tn;
   desc_unpack(desc, target_ws, &g, &tn);
-  if (!ws || ws_bytes < o3dx_icp_accumulate_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
-  Arena ar(ws, ws_bytes);
+  if (!ws || ws_bytes < o3dx_registration_icp_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
+  // [sorted source float4][accumulate arena | sort scratch]
+  float* src4 = (float*)ws;
+  char* rest = (char*)ws + Arena::align((size_t)std::max<int64_t>(ns, 1) * sizeof(float4) + 1);
+  size_t rest_bytes = ws_bytes - (size_t)(rest - (char*)ws);
+  if (ns > 0) O3DX_TRY(o3dx_spatial_sort(src, ns, 8.0, src4, rest, rest_bytes, stream));
+  Arena ar(rest, rest_bytes);
   AccWs w;
   acc_carve(ar, std::max<int64_t>(ns, 1), &w);
   double T[16];
@@ -339,7 +392,7 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
       rm = std::sqrt(sm[29] / c);
     }
   };
-  O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, nullptr, nullptr));
+  O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, nullptr, nullptr));
   double fit, rm;
   metrics(sums, fit, rm);
   for (int it = 0; it < max_iteration; ++it) {
@@ -348,14 +401,14 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
     mat4_mul(upd, T, T);
     const double pf = fit, pr = rm;
     const bool last = (it + 1 == max_iteration);
-    O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, last ? corr_out : nullptr, last ? ncorr : nullptr));
+    O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, last ? corr_out : nullptr, last ? ncorr : nullptr));
     metrics(sums, fit, rm);
     if (std::fabs(pf - fit) < rel_fit && std::fabs(pr - rm) < rel_rmse) {
-      if (!last && corr_out) O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
+      if (!last && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
       break;
     }
   }
-  if (max_iteration <= 0 && corr_out) O3DX_TRY(accumulate(src, ns, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
+  if (max_iteration <= 0 && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
   std::memcpy(T_out, T, sizeof(T));
   *fitness = fit;
   *rmse = rm;

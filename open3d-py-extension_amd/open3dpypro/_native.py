@@ -34,6 +34,8 @@ _SIGS = {
     "o3dx_set_kernel_timing": (None, [_I32]),
     "o3dx_reset_kernel_timing": (None, []),
     "o3dx_kernel_timing": (_I32, [ctypes.c_char_p, _P, _P]),
+    "o3dx_set_search_stats": (_I32, [_I32]),
+    "o3dx_search_stats": (_I32, [_P]),
     "o3dx_aabb_workspace_bytes": (_SZ, [_I64]),
     "o3dx_aabb": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
     "o3dx_voxel_workspace_bytes": (_SZ, [_I64]),
@@ -56,7 +58,10 @@ _SIGS = {
     "o3dx_icp_target_workspace_bytes": (_SZ, [_I64]),
     "o3dx_icp_target_build": (_I32, [_P, _P, _I64, _D, _P, _SZ, _P, _P]),
     "o3dx_icp_accumulate_workspace_bytes": (_SZ, [_I64]),
-    "o3dx_icp_accumulate": (_I32, [_P, _I64, _P, _P, _P, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_icp_accumulate": (_I32, [_P, _I64, _I32, _P, _P, _P, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_spatial_sort_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_spatial_sort": (_I32, [_P, _I64, _D, _P, _P, _SZ, _P]),
+    "o3dx_registration_icp_workspace_bytes": (_SZ, [_I64]),
     "o3dx_icp_solve_point_to_plane": (_I32, [_P, _P]),
     "o3dx_registration_icp_point_to_plane": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,
                                                      _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
@@ -146,6 +151,21 @@ def kernel_timing(name: str):
     cnt = ctypes.c_int64(0)
     load().o3dx_kernel_timing(name.encode(), ctypes.byref(ms), ctypes.byref(cnt))
     return ms.value, cnt.value
+
+
+def search_stats(enable=None):
+    """Debug: enable/disable neighbour-search counters, or read
+    {queries, cells, candidates, shells} when called without arguments."""
+    import numpy as _np
+
+    if enable is not None:
+        check(load().o3dx_set_search_stats(1 if enable else 0), "search_stats")
+        return None
+    out = _np.zeros(4, _np.int64)
+    check(load().o3dx_search_stats(out.ctypes.data_as(ctypes.c_void_p)), "search_stats")
+    q = max(int(out[0]), 1)
+    return {"queries": int(out[0]), "cells_per_query": out[1] / q, "cands_per_query": out[2] / q,
+            "shells_per_query": out[3] / q}
 
 
 def release_workspaces():

@@ -237,19 +237,39 @@ class ICPTarget:
                 "icp_target_build")
 
     def accumulate(self, src: torch.Tensor, T: np.ndarray, want_corr: bool = False):
-        """Fused transform + 1-NN + point-to-plane moments: (sums[32], corr or None)."""
-        s = _xyz(src.to(self.xyz.device), "source points")
+        """Fused transform + 1-NN + point-to-plane moments: (sums[32], corr or None).
+        `src` is (n,3) float32, or the (n,4) output of spatial_sort (faster)."""
+        sorted4 = src.ndim == 2 and src.shape[1] == 4
+        if sorted4:
+            N.require_device(src, "source points")
+            s = src.float().contiguous()
+        else:
+            s = _xyz(src.to(self.xyz.device), "source points")
         L = N.load()
         ns = s.shape[0]
         TT = _c(T, np.float64).reshape(4, 4)
         sums = np.zeros(N.ICP_NSUMS, np.float64)
         corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if want_corr else None
         nc = np.zeros(1, np.int64)
-        ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp")
-        N.check(L.o3dx_icp_accumulate(N.ptr(s), ns, N.ptr(self.ws), _np_ptr(self.desc), _np_ptr(TT), self.max_corr,
+        ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp_acc")
+        N.check(L.o3dx_icp_accumulate(N.ptr(s), ns, 1 if sorted4 else 0, N.ptr(self.ws), _np_ptr(self.desc),
+                                      _np_ptr(TT), self.max_corr,
                                       _np_ptr(sums), N.ptr(corr), _np_ptr(nc), N.ptr(ws), ws.numel(),
                                       N.stream_ptr(s.device)), "icp_accumulate")
         return sums, (corr[: int(nc[0])] if want_corr else None)
+
+
+def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
+    """(n,4) float32 copy of the cloud ordered by grid cell; column 3 holds the
+    original int32 index bits (o3dx_spatial_sort)."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    out = torch.empty((max(n, 1), 4), dtype=torch.float32, device=x.device)
+    ws = N.workspace(L.o3dx_spatial_sort_workspace_bytes(n), x.device, "sort")
+    N.check(L.o3dx_spatial_sort(N.ptr(x), n, float(target_occ), N.ptr(out), N.ptr(ws), ws.numel(),
+                                N.stream_ptr(x.device)), "spatial_sort")
+    return out[:n]
 
 
 def icp_solve(sums) -> np.ndarray:
@@ -275,7 +295,7 @@ def registration_icp(src: torch.Tensor, tgt: torch.Tensor, tgt_normals: torch.Te
     corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if return_corr else None
     nc = np.zeros(1, np.int64)
     tws = N.workspace(L.o3dx_icp_target_workspace_bytes(nt), s.device, "icp_target")
-    ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp")
+    ws = N.workspace(L.o3dx_registration_icp_workspace_bytes(ns), s.device, "icp")
     rc = L.o3dx_registration_icp_point_to_plane(N.ptr(s), ns, N.ptr(t), N.ptr(tn), nt,
                                                 float(max_correspondence_distance), _np_ptr(T0), int(max_iteration),
                                                 float(relative_fitness), float(relative_rmse), _np_ptr(T),

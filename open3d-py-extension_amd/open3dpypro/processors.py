@@ -368,7 +368,6 @@ class Processors:
         relative_fitness: float = 1e-6
         relative_rmse: float = 1e-6
         init: Optional[List[List[float]]] = None
-        save_results_to_meta: bool = True
         result: dict = {}
 
         def validate_pcd(self, pcd_idx, pcd):

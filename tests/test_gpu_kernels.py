@@ -246,3 +246,36 @@ def test_registration_icp_parity(dev):
     assert abs(res["inlier_rmse"] - rmse) < 1e-6
     Tgt_inv = np.linalg.inv(S.rigid_transform())
     assert np.abs(res["transformation"] - Tgt_inv).max() < 2e-3
+
+
+def test_icp_accumulate_sorted_source_layout(dev):
+    src, tgt = _icp_case(30000, seed=4)
+    tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
+    T = S.rigid_transform(0.2, (1, 0, 0), (0, 0.002, 0))
+    target = ops.ICPTarget(torch.from_numpy(tgt).to(dev), torch.from_numpy(tn).to(dev), 0.02)
+    s = torch.from_numpy(src).to(dev)
+    s4 = ops.spatial_sort(s)
+    assert torch.equal(torch.sort(s4[:, 3].contiguous().view(torch.int32).long())[0],
+                       torch.arange(len(src), device=dev))
+    a, ca = target.accumulate(s, T, want_corr=True)
+    b, cb = target.accumulate(s4, T, want_corr=True)
+    assert a[28] == b[28]
+    np.testing.assert_allclose(a[:30], b[:30], rtol=1e-10, atol=1e-12)
+    assert torch.equal(ca, cb)
+    ref = O.icp_accumulate(src, tgt, tn, 0.02, T)
+    np.testing.assert_allclose(b[:30], ref[:30], rtol=1e-9, atol=1e-9)
+
+
+def test_normals_knn_paths_agree(dev):
+    """histogram-select path vs the exact register top-k path (fallback form)."""
+    import os
+    pts = S.uniform_cube(200_000, 12)
+    x = pts.to(dev)
+    a = ops.estimate_normals(x, knn=30).cpu().numpy()
+    os.environ["O3DX_NORMALS_TOPK"] = "1"
+    try:
+        b = ops.estimate_normals(x, knn=30).cpu().numpy()
+    finally:
+        del os.environ["O3DX_NORMALS_TOPK"]
+    e = np.abs(a - b).max(1)
+    assert np.mean(e < 1e-6) > 0.9999, e.max()

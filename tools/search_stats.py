@@ -1,0 +1,67 @@
+"""Diagnostics: neighbour-search work per query (cells / candidates / shells)
+and kernel times for the normals and ICP paths, across grid-occupancy settings.
+Usage (GPU box): python tools/search_stats.py"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "open3d-py-extension_amd"))
+
+
+def run_one():
+    import numpy as np
+    import torch
+    from open3dpypro import _native, ops, synthetic as S
+
+    dev = torch.device("cuda:0")
+    N = int(os.environ.get("N", "10000000"))
+    pts = S.uniform_cube(N, 0, device=dev)
+    reps = ops.voxel_down_sample(pts, S.voxel_size_for(N))["rep_xyz"]
+    out = {"env": {k: v for k, v in os.environ.items() if k.startswith("O3DX_")}}
+    ops.estimate_normals(reps, knn=30)
+    _native.search_stats(True)
+    _native.set_kernel_timing(True)
+    _native.reset_kernel_timing()
+    ops.estimate_normals(reps, knn=30)
+    out["normals_stats"] = _native.search_stats()
+    _native.search_stats(False)
+    _native.reset_kernel_timing()
+    for _ in range(3):
+        ops.estimate_normals(reps, knn=30)
+    ms, c = _native.kernel_timing("normals_knn")
+    out["normals_ms"] = ms / c
+    del pts, reps
+    tgt = S.box_surface(N, 1, device=dev)
+    src = S.apply_transform(S.box_surface(N, 2, device=dev), S.rigid_transform())
+    tn = ops.estimate_normals(tgt, knn=30)
+    target = ops.ICPTarget(tgt, tn, 0.02)
+    src = ops.spatial_sort(src)
+    T = np.eye(4)
+    for it in range(3):
+        sums, _ = target.accumulate(src, T)
+        T = ops.icp_solve(sums) @ T
+    _native.search_stats(True)
+    _native.reset_kernel_timing()
+    sums, _ = target.accumulate(src, T)
+    out["icp_stats_converged"] = _native.search_stats()
+    ms, c = _native.kernel_timing("icp_accumulate")
+    out["icp_ms_converged"] = ms / c
+    _native.search_stats(False)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "one":
+        run_one()
+        sys.exit(0)
+    grid = [{}, {"O3DX_GRID_OCC": "8"}, {"O3DX_GRID_OCC": "12"}, {"O3DX_GRID_OCC": "16"},
+            {"O3DX_ICP_MINH_DIV": "16", "O3DX_ICP_OCC": "1"}, {"O3DX_ICP_MINH_DIV": "16", "O3DX_ICP_OCC": "4"},
+            {"O3DX_ICP_MINH_DIV": "32", "O3DX_ICP_OCC": "2"}]
+    for extra in grid:
+        env = dict(os.environ, **extra)
+        r = subprocess.run([sys.executable, __file__, "one"], env=env, capture_output=True, text=True, timeout=300)
+        print(r.stdout.strip() or r.stderr[-2000:], flush=True)
+        if r.returncode != 0:
+            sys.exit(r.returncode)
