@@ -78,11 +78,13 @@ int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches);
 
 /* Debug-only neighbour-search statistics: when enabled, every grid search
  * (normals, kNN, ICP) adds {queries, cells visited, candidate points, shells}
- * into device counters read by o3dx_search_stats (synchronises the device).
+ * into device counters, and the KNN-normals levels count the queries they
+ * hand on {tile -> global histogram, global histogram -> register top-k};
+ * o3dx_search_stats copies those six counters out (synchronises the device).
  * Enabling allocates a 64-byte device buffer — the only device allocation the
  * library ever makes; off by default. */
 int o3dx_set_search_stats(int enable);
-int o3dx_search_stats(int64_t* out4_host);
+int o3dx_search_stats(int64_t* out6_host);
 
 /* ---------------------------------------------------------------- AABB
  * Replaces o3d.geometry.PointCloud.get_min_bound()/get_max_bound()

@@ -145,6 +145,11 @@ struct KTimer {
     }
     a = b = nullptr;
   }
+  void cancel() {  // drop without recording (a later KTimer of the same name takes over)
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    a = b = nullptr;
+  }
   ~KTimer() { stop(); }
 };
 

@@ -516,13 +516,22 @@ __device__ __forceinline__ void finish_normal(int cnt, const MomAcc& acc, const 
 }
 
 template <int K>
+__device__ __forceinline__ void knn_normal_query(const GridView& g, const float* __restrict__ xyz, int kneed, int hybrid,
+                                 double radius, const float* __restrict__ prior, float* __restrict__ out, int64_t s);
+
+template <int K>
 __global__ void __launch_bounds__(kBlock) k_normals_knn(GridView g, const float* __restrict__ xyz, int kneed,
                                                         int hybrid, double radius, const float* __restrict__ prior,
                                                         float* __restrict__ out, const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ list_len) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (list ? t >= *list_len : t >= g.n) return;
-  const int64_t s = list ? list[t] : t;
+  const int64_t lim = list ? (int64_t)*list_len : g.n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < lim; t += (int64_t)gridDim.x * blockDim.x)
+    knn_normal_query<K>(g, xyz, kneed, hybrid, radius, prior, out, list ? list[t] : t);
+}
+
+template <int K>
+__device__ __forceinline__ void knn_normal_query(const GridView& g, const float* __restrict__ xyz, int kneed, int hybrid,
+                                 double radius, const float* __restrict__ prior, float* __restrict__ out, int64_t s) {
   const float4 q = g.pts[s];
   const int oi = __float_as_int(q.w);
   double bd[K];
@@ -543,167 +552,267 @@ __global__ void __launch_bounds__(kBlock) k_normals_knn(GridView g, const float*
 // ---------------------------------------------------------------------------
 // KNN normals, histogram-select form (the default KNN path).
 //
-// Per query (one lane), with R = the radius inside which every point has been
-// scanned after shells 0..S (R = S h + m - slack):
-//   pass 1  float32 d^2 of every candidate in shells 0..S; the ones inside R
-//           are counted into NB bins uniform in d^2 (LDS, 16-bit counters);
-//           grow S until >= k lie inside R;
-//   locate  the bin b* holding the k-th distance -> [L, U);
-//   pass 2  rescan: d^2 < L(1-2e) is certainly among the k nearest (appended to
-//           an LDS list), d^2 in the band [L(1-2e), U(1+2e)) is a boundary
+// Per query, over the candidates of a neighbourhood inside which every point
+// closer than R has been scanned (R = S h + m - slack):
+//   count   float32 d^2 of every candidate; the ones inside R are counted
+//           into 16 bins uniform in d^2 (packed counters in registers); the
+//           wave form grows S until >= k lie inside R;
+//   locate  the bin b* holding the k-th distance -> [L, U); while b* holds
+//           more than kRefineAt points, re-bin [L, U) into 16 sub-bins
+//           (another scan, at most kMaxRefine times);
+//   select  rescan: d^2 < L(1-2e) is certainly among the k nearest (appended
+//           to an LDS list), d^2 in the band [L(1-2e), U(1+2e)) is a boundary
 //           candidate (LDS list), the rest is certainly out — e = 2^-20 bounds
 //           the float32 distance error relative to float64;
-//   pass 3  the (k - #certain) nearest boundary candidates by exact float64
-//           (d^2, index), i.e. the same set as the oracle / nanoflann;
-//   pass 4  Open3D's float64 raw moments over the k selected, FastEigen3x3.
-// No per-candidate sorted insertion: cost is ~2 scans of the 27-cell
-// neighbourhood in float32 plus O(k) float64 work.  Queries the form cannot
-// settle (the shell reaches the grid edge, a boundary list overflows) go to a
-// list served by the exact register top-k kernel above.
+//   finish  (finish_selection) the (k - #certain) nearest band candidates by
+//           exact float64 (d^2, original index) — the oracle's / nanoflann's
+//           order — then a check that every certain member precedes every
+//           unselected band member in that order, then Open3D's float64 raw
+//           moments over the k selected and FastEigen3x3.
+// No per-candidate sorted insertion: cost is ~2 scans of the neighbourhood in
+// float32 plus O(k) float64 work.  Queries a form cannot settle are appended
+// to a list for the next form (LDS tile, lane per query -> wave per query ->
+// register top-k).
 constexpr int kHistBins = 16;
 constexpr int kBndCap = 16;
+constexpr int kRefineAt = kBndCap - 2;  // tiles: refine only where the band would overflow
+constexpr int kMaxRefine = 2;
 constexpr float kRelEps = 9.5367431640625e-07f;  // 2^-20
 
-__device__ __forceinline__ float dist2_f32(const float4 q, const float4 p) {
-  const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+template <bool W8>
+struct RegHist {
+  static constexpr int kWords = W8 ? 4 : 8;
+  static constexpr int kPer = W8 ? 4 : 2;  // bins per word
+  static constexpr int kBits = W8 ? 8 : 16;
+  static constexpr int kMaxTotal = W8 ? 255 : 65535;
+  uint32_t h[kWords];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < kWords; ++i) h[i] = 0u;
+  }
+  __device__ __forceinline__ void add(int b) {
+    const uint32_t inc = 1u << ((b % kPer) * kBits);
+    const int w = b / kPer;
+#pragma unroll
+    for (int i = 0; i < kWords; ++i) h[i] += (w == i) ? inc : 0u;
+  }
+  __device__ __forceinline__ int count(int b) const {  // b a compile-time constant after unrolling
+    return (int)((h[b / kPer] >> ((b % kPer) * kBits)) & ((1u << kBits) - 1u));
+  }
+};
+
+__device__ __forceinline__ float dist2_f32(const float4 q, float x, float y, float z) {
+  const float dx = q.x - x, dy = q.y - y, dz = q.z - z;
   return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
 }
 
-template <int KMAX>
-__global__ void __launch_bounds__(64) k_normals_knn_hist(GridView g, int kneed, const float* __restrict__ prior,
-                                                         float* __restrict__ out, const int32_t* __restrict__ in_list,
-                                                         const int32_t* __restrict__ in_len,
-                                                         int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len) {
-  __shared__ uint32_t hist[kHistBins / 2][64];
-  __shared__ int32_t sel[KMAX][64];
-  __shared__ int32_t bnd[kBndCap][64];
-  const int lane = threadIdx.x;
-  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
-  if (in_list ? t >= *in_len : t >= g.n) return;
-  const int64_t s = in_list ? in_list[t] : t;
-  const float4 q = g.pts[s];
-  const int oi = __float_as_int(q.w);
-  int cx, cy, cz;
-  grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
-  const double m = cell_margin(g, q.x, q.y, q.z, cx, cy, cz);
-  const int rmax = shell_rmax(g, cx, cy, cz);
-  bool fb = false;
-  int S = 1;
-  float R2 = 0.f;
-  for (;; ++S) {
-    if (S >= rmax) {  // shells would cover the whole grid: leave it to the exact path
-      fb = true;
-      break;
-    }
-    const double R = (double)S * g.h + m - g.slack;
-    if (R <= 0.0) continue;
+// Locate the bin of the k-th distance in a histogram over [lo, hi) with
+// `below` points known below lo.  -> bin edges [*L, *U), *cum = points in the
+// bins before it, *cb = points in it; false when no bin reaches k.
+template <bool W8>
+__device__ __forceinline__ bool hist_locate(const RegHist<W8>& hist, int kneed, int below, float lo, float hi,
+                                            float* L, float* U, int* cum, int* cb) {
+  const float bw = (hi - lo) / (float)kHistBins;
+  int bstar = -1, c0 = 0, cn = 0;
 #pragma unroll
-    for (int b = 0; b < kHistBins / 2; ++b) hist[b][lane] = 0u;
-    R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
-    const float scale = (float)kHistBins / R2;
-    int total = 0;
-    for_cube_rows(g, cx, cy, cz, S, [&](int p0, int p1) {
-      for_points4(g, p0, p1, [&](int, const float4 v) {
-        const float d2 = dist2_f32(q, v);
-        if (d2 < R2) {
-          const int b = min((int)(d2 * scale), kHistBins - 1);
-          hist[b >> 1][lane] += (b & 1) ? 0x10000u : 1u;
-          ++total;
-        }
-      });
-    });
-    if (total >= kneed) break;
-  }
-  if (!fb) {
-    int bstar = -1, cum = 0;
-#pragma unroll
-    for (int b = 0; b < kHistBins; ++b) {
-      const uint32_t w = hist[b >> 1][lane];
-      const int c = (b & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
-      if (bstar < 0 && cum + c >= kneed) bstar = b;
-      cum += c;
-    }
-    const float bw = R2 / (float)kHistBins;
-    const float Lm = (float)bstar * bw * (1.0f - 2.0f * kRelEps);
-    const float Up = (bstar == kHistBins - 1 ? R2 : (float)(bstar + 1) * bw) * (1.0f + 2.0f * kRelEps);
-    int nsel = 0, nb = 0;
-    for_cube_rows(g, cx, cy, cz, S, [&](int p0, int p1) {
-      for_points4(g, p0, p1, [&](int p, const float4 v) {
-        const float d2 = dist2_f32(q, v);
-        if (d2 < Lm) {
-          if (nsel < KMAX) sel[nsel][lane] = p;
-          ++nsel;
-        } else if (d2 < Up) {
-          if (nb < kBndCap) bnd[nb][lane] = p;
-          ++nb;
-        }
-      });
-    });
-    if (nsel > kneed || nb > kBndCap || nsel + nb < kneed) fb = true;
-    if (!fb) {
-      // exact tail: the (kneed - nsel) nearest boundary candidates by (d2_f64, index)
-      const double qx = q.x, qy = q.y, qz = q.z;
-      for (int t = nsel; t < kneed; ++t) {
-        int bj = -1, bidx = 0x7fffffff;
-        double bdd = INFINITY;
-        for (int j = 0; j < nb; ++j) {
-          const int p = bnd[j][lane];
-          if (p < 0) continue;
-          const float4 v = g.pts[p];
-          const double d = dist2_f64(qx, qy, qz, v);
-          const int id = __float_as_int(v.w);
-          if (lex_less(d, id, bdd, bidx)) {
-            bdd = d;
-            bidx = id;
-            bj = j;
-          }
-        }
-        sel[t][lane] = bnd[bj][lane];
-        bnd[bj][lane] = -1;
+  for (int b = 0; b < kHistBins; ++b) {
+    const int c = hist.count(b);
+    if (bstar < 0) {
+      if (below + c0 + c >= kneed) {
+        bstar = b;
+        cn = c;
+      } else {
+        c0 += c;
       }
-      MomAcc acc;
-      acc.zero();
-      for (int j = 0; j < kneed; ++j) {
-        const float4 v = g.pts[sel[j][lane]];
-        acc.add((double)v.x, (double)v.y, (double)v.z);
-      }
-      finish_normal(kneed, acc, prior, oi, out);
     }
   }
-  if (fb) {
-    const int at = atomicAdd(fb_len, 1);
-    fb_list[at] = (int32_t)s;
-  }
+  *cum = c0;
+  *cb = cn;
+  *L = lo + (float)bstar * bw;
+  *U = (bstar == kHistBins - 1) ? hi : lo + (float)(bstar + 1) * bw;
+  return bstar >= 0;
 }
 
+// Lexicographic (d2_f64, original index) order; the index is fetched only on
+// an exact distance tie.
+template <class Id>
+__device__ __forceinline__ bool key_less(double da, int pa, double db, int pb, Id&& id) {
+  if (da != db) return da < db;
+  if (pb < 0) return pa >= 0;
+  if (pa < 0) return false;
+  return id(pa) < id(pb);
+}
+
+// Exact completion of a histogram selection (see above).  sel[0..nsel) hold
+// the certain members, bnd[0..nb) the band (positions understood by fetch /
+// id).  On success writes the normal of original point `oi` and returns true.
+template <int KMAX, class T, class Fetch, class Id>
+__device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int nsel, int nb, T (*sel)[64],
+                                                 T (*bnd)[64], int lane, Fetch&& fetch, Id&& id,
+                                                 const float* __restrict__ prior, int oi, float* __restrict__ out) {
+  const double qx = q.x, qy = q.y, qz = q.z;
+  double bd[kBndCap];
+  int bp[kBndCap];
+#pragma unroll
+  for (int j = 0; j < kBndCap; ++j) {
+    bp[j] = -1;
+    bd[j] = INFINITY;
+    if (j < nb) {
+      bp[j] = (int)bnd[j][lane];
+      bd[j] = dist2_f64(qx, qy, qz, fetch(bp[j]));
+    }
+  }
+  uint32_t used = 0u;
+  for (int t = nsel; t < kneed; ++t) {
+    int bj = -1, bpp = -1;
+    double bdd = INFINITY;
+#pragma unroll
+    for (int j = 0; j < kBndCap; ++j) {
+      if (j < nb && !((used >> j) & 1u) && key_less(bd[j], bp[j], bdd, bpp, id)) {
+        bdd = bd[j];
+        bpp = bp[j];
+        bj = j;
+      }
+    }
+    used |= 1u << bj;
+    sel[t][lane] = (T)bpp;
+  }
+  // the smallest unselected band key
+  int up = -1;
+  double ud = INFINITY;
+#pragma unroll
+  for (int j = 0; j < kBndCap; ++j)
+    if (j < nb && !((used >> j) & 1u) && key_less(bd[j], bp[j], ud, up, id)) {
+      ud = bd[j];
+      up = bp[j];
+    }
+  MomAcc acc;
+  acc.zero();
+  int cp = -1;
+  double cd = -1.0;
+  for (int j = 0; j < kneed; ++j) {
+    const int p = (int)sel[j][lane];
+    const float4 v = fetch(p);
+    if (j < nsel) {
+      const double d = dist2_f64(qx, qy, qz, v);
+      if (cp < 0 || key_less(cd, cp, d, p, id)) {
+        cd = d;
+        cp = p;
+      }
+    }
+    acc.add((double)v.x, (double)v.y, (double)v.z);
+  }
+  if (up >= 0 && cp >= 0 && !key_less(cd, cp, ud, up, id)) return false;  // rounding swapped the order
+  finish_normal(kneed, acc, prior, oi, out);
+  return true;
+}
+
+// The locate / refine / select steps over a candidate scan SCAN(BODY) in which
+// BODY sees `pp` (candidate position) and `d2` (float32 distance).  Expects
+// hist (filled over [0, R2)), kneed, R2, sel, bnd, lane; sets fb, nsel, nb.
+#define O3DX_HIST_SELECT(SCAN)                                                                        \
+  {                                                                                                   \
+    float lo = 0.f, hi = R2, L = 0.f, U = 0.f;                                                        \
+    int below = 0;                                                                                    \
+    for (int lvl = 0; !fb; ++lvl) {                                                                   \
+      int cum, cb;                                                                                    \
+      if (!hist_locate(hist, kneed, below, lo, hi, &L, &U, &cum, &cb)) {                             \
+        fb = true;                                                                                    \
+        break;                                                                                        \
+      }                                                                                               \
+      if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;                                    \
+      below += cum;                                                                                   \
+      lo = L;                                                                                         \
+      hi = U;                                                                                         \
+      const float sc = (float)kHistBins / (hi - lo);                                                  \
+      hist.zero();                                                                                    \
+      SCAN(if (d2 >= lo && d2 < hi) hist.add(min((int)((d2 - lo) * sc), kHistBins - 1));)            \
+    }                                                                                                 \
+    if (!fb) {                                                                                        \
+      const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);                 \
+      SCAN(if (d2 < Lm) {                                                                             \
+        if (nsel < KMAX) sel[nsel][lane] = pp;                                                        \
+        ++nsel;                                                                                       \
+      } else if (d2 < Up) {                                                                           \
+        if (nb < kBndCap) bnd[nb][lane] = pp;                                                         \
+        ++nb;                                                                                         \
+      })                                                                                              \
+      fb = nsel > kneed || nb > kBndCap || nsel + nb < kneed;                                         \
+    }                                                                                                 \
+  }
 
 // ---------------------------------------------------------------------------
 // KNN normals, LDS-tile form (first level of the default KNN path).
-// One block = one chunk of <= kTileQ queries in one grid row; the 9-row
-// neighbour box is staged into LDS (coalesced), then every query runs the
-// histogram-select passes of k_normals_knn_hist over LDS-resident candidates
-// (shells 0..1 only).  Queries the tile cannot settle (fewer than k points
-// within the shell-1 radius, or the box overflows LDS) are appended to
-// fb_list for the global-memory form.
-constexpr int kTileQ = 128;
-constexpr int kTilePts = 1536;
-constexpr int kTileCs = 640;
+// One block = one wave = one chunk of <= 64 consecutive queries in one grid
+// row; the 9-row neighbour box is staged into LDS (coalesced, SoA f32), then
+// every lane runs the histogram-select steps over LDS-resident candidates
+// (shells 0..1 only) with packed 8-bit (k <= 32) or 16-bit counters.
+// Queries the tile cannot settle (fewer than k points within the shell-1
+// radius, a counter could overflow, the band overflows, or the box does not
+// fit in LDS) are appended to fb_list for the global form.
+constexpr int kTileQ = 64;
+constexpr int kTilePts = 960;
+constexpr int kTileCs = 384;
+
+// Row r (0..8) of the 3x3 (y,z) rows around (cy,cz), clipped to the box and
+// to x in [cx-1, cx+1]: LDS slots [*a, *e) (empty when outside the box).
+__device__ __forceinline__ void tile_row(const TileBox& b, const int32_t* ccs, int cx, int cy, int cz, int r, int* a,
+                                         int* e) {
+  const int z = cz + r / 3 - 1, y = cy + r % 3 - 1;
+  if (z < b.z0 || z > b.z1 || y < b.y0 || y > b.y1) {
+    *a = *e = 0;
+    return;
+  }
+  const int w = b.nxr + 1;
+  const int k = (y - b.y0) + b.nyr * (z - b.z0);
+  *a = ccs[k * w + max(cx - 1, b.x0) - b.x0];
+  *e = ccs[k * w + min(cx + 1, b.x1) - b.x0 + 1];
+}
+
+// Candidates of the query's 27-cell cube from the LDS tile, four at a time
+// (LDS loads issued before use).
+#define O3DX_TILE_SCAN(BODY)                                \
+  for (int r_ = 0; r_ < 9; ++r_) {                          \
+    int a_, e_;                                             \
+    tile_row(box, ccs, cx, cy, cz, r_, &a_, &e_);           \
+    int p_ = a_;                                            \
+    for (; p_ + 4 <= e_; p_ += 4) {                         \
+      float xs_[4], ys_[4], zs_[4];                         \
+      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {    \
+        xs_[u_] = tx[p_ + u_];                              \
+        ys_[u_] = ty[p_ + u_];                              \
+        zs_[u_] = tz[p_ + u_];                              \
+      }                                                     \
+      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {    \
+        const int pp = p_ + u_;                             \
+        (void)pp;                                           \
+        const float d2 = dist2_f32(q, xs_[u_], ys_[u_], zs_[u_]); \
+        BODY                                                \
+      }                                                     \
+    }                                                       \
+    for (; p_ < e_; ++p_) {                                 \
+      const int pp = p_;                                    \
+      (void)pp;                                             \
+      const float d2 = dist2_f32(q, tx[p_], ty[p_], tz[p_]); \
+      BODY                                                  \
+    }                                                       \
+  }
 
 template <int KMAX>
 __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
                                                              int kneed, const float* __restrict__ prior,
                                                              float* __restrict__ out, int32_t* __restrict__ fb_list,
                                                              int32_t* __restrict__ fb_len) {
-  __shared__ float4 tp[kTilePts];
+  static_assert(kTileQ == 64, "one wave per tile");
+  __shared__ float tx[kTilePts], ty[kTilePts], tz[kTilePts];
   __shared__ int32_t ccs[kTileCs];
   __shared__ int32_t rows[kMaxTileRows + 1];
   __shared__ int32_t rst[kMaxTileRows];
-  __shared__ uint32_t hist[kHistBins / 2][kTileQ];
   __shared__ uint16_t sel[KMAX][kTileQ];
   __shared__ uint16_t bnd[kBndCap][kTileQ];
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   const int q0 = chunk_starts[blockIdx.x], q1 = chunk_starts[blockIdx.x + 1];
-  const int64_t s = (int64_t)q0 + tid;
+  const int64_t s = (int64_t)q0 + lane;
   const bool active = s < q1;
   // the chunk lies in one (y,z) row and is sorted by x: first/last give the box
   int ax, ay, az, bx, by, bz;
@@ -721,89 +830,250 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   box.z1 = min(az + 1, g.nz - 1);
   box.nxr = box.x1 - box.x0 + 1;
   box.nyr = box.y1 - box.y0 + 1;
-  const int staged = stage_tile<kTileQ>(g, box, tp, kTilePts, ccs, kTileCs, rows, rst);
+  const int staged = stage_tile<kTileQ, kTilePts>(g, box, tx, ty, tz, ccs, kTileCs, rows, rst);
   if (!active) return;  // no barrier below this point
   const float4 q = g.pts[s];
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
   bool fb = staged < 0 || cy != ay || cz != az;
+  int nsel = 0, nb = 0;
   if (!fb) {
     const double R = (double)g.h + cell_margin(g, q.x, q.y, q.z, cx, cy, cz) - g.slack;
     const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
     const float scale = (float)kHistBins / fmaxf(R2, 1e-30f);
-#pragma unroll
-    for (int b = 0; b < kHistBins / 2; ++b) hist[b][tid] = 0u;
+    RegHist<(KMAX <= 32)> hist;
+    hist.zero();
     int total = 0;
-    for_tile_rows(box, ccs, cx, cy, cz, [&](int a, int e) {
-      for (int p = a; p < e; ++p) {
-        const float d2 = dist2_f32(q, tp[p]);
-        if (d2 < R2) {
-          const int b = min((int)(d2 * scale), kHistBins - 1);
-          hist[b >> 1][tid] += (b & 1) ? 0x10000u : 1u;
-          ++total;
-        }
-      }
-    });
-    fb = total < kneed;
-    if (!fb) {
-      int bstar = -1, cum = 0;
-#pragma unroll
-      for (int b = 0; b < kHistBins; ++b) {
-        const uint32_t w = hist[b >> 1][tid];
-        const int c = (b & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
-        if (bstar < 0 && cum + c >= kneed) bstar = b;
-        cum += c;
-      }
-      const float bw = R2 / (float)kHistBins;
-      const float Lm = (float)bstar * bw * (1.0f - 2.0f * kRelEps);
-      const float Up = (bstar == kHistBins - 1 ? R2 : (float)(bstar + 1) * bw) * (1.0f + 2.0f * kRelEps);
-      int nsel = 0, nb = 0;
-      for_tile_rows(box, ccs, cx, cy, cz, [&](int a, int e) {
-        for (int p = a; p < e; ++p) {
-          const float d2 = dist2_f32(q, tp[p]);
-          if (d2 < Lm) {
-            if (nsel < KMAX) sel[nsel][tid] = (uint16_t)p;
-            ++nsel;
-          } else if (d2 < Up) {
-            if (nb < kBndCap) bnd[nb][tid] = (uint16_t)p;
-            ++nb;
-          }
-        }
-      });
-      fb = nsel > kneed || nb > kBndCap || nsel + nb < kneed;
-      if (!fb) {
-        const double qx = q.x, qy = q.y, qz = q.z;
-        for (int t = nsel; t < kneed; ++t) {
-          int bj = 0, bidx = 0x7fffffff;
-          double bdd = INFINITY;
-          for (int j = 0; j < nb; ++j) {
-            const int p = bnd[j][tid];
-            if (p == 0xffff) continue;
-            const float4 v = tp[p];
-            const double d = dist2_f64(qx, qy, qz, v);
-            const int id = __float_as_int(v.w);
-            if (lex_less(d, id, bdd, bidx)) {
-              bdd = d;
-              bidx = id;
-              bj = j;
-            }
-          }
-          sel[t][tid] = bnd[bj][tid];
-          bnd[bj][tid] = 0xffff;
-        }
-        MomAcc acc;
-        acc.zero();
-        for (int j = 0; j < kneed; ++j) {
-          const float4 v = tp[sel[j][tid]];
-          acc.add((double)v.x, (double)v.y, (double)v.z);
-        }
-        finish_normal(kneed, acc, prior, __float_as_int(q.w), out);
-      }
-    }
+    O3DX_TILE_SCAN(if (d2 < R2) {
+      hist.add(min((int)(d2 * scale), kHistBins - 1));
+      ++total;
+    })
+    fb = total < kneed || total > hist.kMaxTotal;
+    O3DX_HIST_SELECT(O3DX_TILE_SCAN)
+    if (!fb)
+      fb = !finish_selection<KMAX>(
+          q, kneed, nsel, nb, sel, bnd, lane,
+          [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
+          [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, prior,
+          __float_as_int(q.w), out);
   }
   if (fb) {
+    if (g.stats) atomicAdd(&g.stats[4], 1ull);
     const int at = atomicAdd(fb_len, 1);
     fb_list[at] = (int32_t)s;
+  }
+}
+#undef O3DX_TILE_SCAN
+#undef O3DX_HIST_SELECT
+
+
+// ---------------------------------------------------------------------------
+// KNN normals, wave-per-query form (second level: the queries the tiles hand
+// on, or every query when tiles are off).  One wave scans one query's cube
+// rows — contiguous ranges of the cell-sorted array, so lanes read coalesced
+// — growing S until >= k points lie inside R; per-lane packed 16-bit bin
+// counters are summed across the wave; the certain / band lists are built
+// with ballot + mbcnt into LDS; the exact tail ranks the band (<= 64, one per
+// lane) by (d2_f64, original index); the moments are float64 wave sums.
+constexpr int kWaveBnd = 64;
+constexpr int kWaveRefineAt = 32;
+constexpr int kWavesPerBlock = 4;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Rows of the (2S+1)^3 cube; each row range is walked 64 candidates at a time
+// (uniform trip count: `valid` marks the lanes past the row end).
+#define O3DX_WAVE_SCAN(S, BODY)                                              \
+  {                                                                          \
+    const int x0_ = max(cx - (S), 0), x1_ = min(cx + (S), g.nx - 1);         \
+    for (int dz_ = -(S); dz_ <= (S); ++dz_) {                                \
+      const int z_ = cz + dz_;                                               \
+      if (z_ < 0 || z_ >= g.nz) continue;                                    \
+      for (int dy_ = -(S); dy_ <= (S); ++dy_) {                              \
+        const int y_ = cy + dy_;                                             \
+        if (y_ < 0 || y_ >= g.ny) continue;                                  \
+        const int rb_ = g.nx * (y_ + g.ny * z_);                             \
+        const int a_ = g.start[rb_ + x0_], e_ = g.start[rb_ + x1_ + 1];      \
+        for (int b_ = a_; b_ < e_; b_ += 64) {                               \
+          const int pp = b_ + lane;                                          \
+          const bool valid = pp < e_;                                        \
+          const float4 v_ = g.pts[valid ? pp : a_];                          \
+          const float d2 = dist2_f32(q, v_.x, v_.y, v_.z);                   \
+          BODY                                                               \
+        }                                                                    \
+      }                                                                      \
+    }                                                                        \
+  }
+
+template <int KMAX>
+__device__ __forceinline__ void wave_query(const GridView& g, int kneed, const float* __restrict__ prior,
+                                           float* __restrict__ out, int64_t s, int lane, int32_t* sel, int32_t* bnd,
+                                           int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len) {
+  const float4 q = g.pts[s];
+  int cx, cy, cz;
+  grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
+  const double m = cell_margin(g, q.x, q.y, q.z, cx, cy, cz);
+  const int rmax = shell_rmax(g, cx, cy, cz);
+  bool fb = false;
+  int S = 1;
+  float R2 = 0.f;
+  RegHist<false> hist;
+  for (;; ++S) {
+    if (S >= rmax) {  // shells would cover the whole grid: leave it to the exact path
+      fb = true;
+      break;
+    }
+    const double R = (double)S * g.h + m - g.slack;
+    if (R <= 0.0) continue;
+    R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
+    const float scale = (float)kHistBins / R2;
+    hist.zero();
+    int tot = 0;
+    O3DX_WAVE_SCAN(S, if (valid && d2 < R2) {
+      hist.add(min((int)(d2 * scale), kHistBins - 1));
+      ++tot;
+    })
+    tot = wave_sum(tot);
+    if (tot > hist.kMaxTotal) {  // packed wave sums could carry
+      fb = true;
+      break;
+    }
+    if (tot >= kneed) break;
+  }
+  float lo = 0.f, hi = R2, L = 0.f, U = 0.f;
+  int below = 0;
+  for (int lvl = 0; !fb; ++lvl) {
+#pragma unroll
+    for (int i = 0; i < hist.kWords; ++i) hist.h[i] = wave_sum(hist.h[i]);
+    int cum, cb;
+    if (!hist_locate(hist, kneed, below, lo, hi, &L, &U, &cum, &cb)) {
+      fb = true;
+      break;
+    }
+    if (cb <= kWaveRefineAt || lvl == kMaxRefine || !(U > L)) break;
+    below += cum;
+    lo = L;
+    hi = U;
+    const float sc = (float)kHistBins / (hi - lo);
+    hist.zero();
+    O3DX_WAVE_SCAN(S, if (valid && d2 >= lo && d2 < hi) hist.add(min((int)((d2 - lo) * sc), kHistBins - 1));)
+  }
+  int nsel = 0, nb = 0;
+  if (!fb) {
+    const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
+    O3DX_WAVE_SCAN(S, {
+      const bool c1 = valid && d2 < Lm;
+      const bool c2 = valid && !(d2 < Lm) && d2 < Up;
+      const uint64_t m1 = __ballot(c1);
+      const uint64_t m2 = __ballot(c2);
+      if (c1) {
+        const int at = nsel + lanes_below(m1);
+        if (at < KMAX) sel[at] = pp;
+      }
+      if (c2) {
+        const int at = nb + lanes_below(m2);
+        if (at < kWaveBnd) bnd[at] = pp;
+      }
+      nsel += __popcll(m1);
+      nb += __popcll(m2);
+    })
+    fb = nsel > kneed || nb > kWaveBnd || nsel + nb < kneed;
+  }
+  if (!fb) {
+    wave_sync();
+    const int need = kneed - nsel;
+    const double qx = q.x, qy = q.y, qz = q.z;
+    // exact keys of the band, one per lane, and their ranks
+    double bd = INFINITY;
+    int bid = 0x7fffffff, bpos = -1;
+    if (lane < nb) {
+      bpos = bnd[lane];
+      const float4 v = g.pts[bpos];
+      bd = dist2_f64(qx, qy, qz, v);
+      bid = __float_as_int(v.w);
+    }
+    int rank = 0;
+    for (int i = 0; i < nb; ++i) {
+      const double di = __shfl(bd, i, 64);
+      const int ii = __shfl(bid, i, 64);
+      rank += (di < bd || (di == bd && ii < bid)) ? 1 : 0;
+    }
+    // largest certain key must precede the smallest unselected band key (rank == need)
+    double cd = -1.0;
+    int cid = -1;
+    if (lane < nsel) {
+      const float4 v = g.pts[sel[lane]];
+      cd = dist2_f64(qx, qy, qz, v);
+      cid = __float_as_int(v.w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double od = __shfl_xor(cd, o, 64);
+      const int oid = __shfl_xor(cid, o, 64);
+      if (od > cd || (od == cd && oid > cid)) {
+        cd = od;
+        cid = oid;
+      }
+    }
+    if (need < nb && nsel > 0) {
+      const uint64_t mk = __ballot(lane < nb && rank == need);
+      const int l = __ffsll((unsigned long long)mk) - 1;
+      const double ud = __shfl(bd, l, 64);
+      const int uid = __shfl(bid, l, 64);
+      fb = !(cd < ud || (cd == ud && cid < uid));
+    }
+    if (!fb) {
+      if (lane < nb && rank < need) sel[nsel + rank] = bpos;
+      wave_sync();
+      double x = 0.0, y = 0.0, z = 0.0;
+      if (lane < kneed) {
+        const float4 v = g.pts[sel[lane]];
+        x = v.x;
+        y = v.y;
+        z = v.z;
+      }
+      MomAcc acc;
+      acc.m[0] = wave_sum(x);
+      acc.m[1] = wave_sum(y);
+      acc.m[2] = wave_sum(z);
+      acc.m[3] = wave_sum(x * x);
+      acc.m[4] = wave_sum(x * y);
+      acc.m[5] = wave_sum(x * z);
+      acc.m[6] = wave_sum(y * y);
+      acc.m[7] = wave_sum(y * z);
+      acc.m[8] = wave_sum(z * z);
+      if (lane == 0) finish_normal(kneed, acc, prior, __float_as_int(q.w), out);
+    }
+  }
+  wave_sync();  // the lists are reused by the wave's next query
+  if (fb && lane == 0) {
+    if (g.stats) atomicAdd(&g.stats[5], 1ull);
+    const int at = atomicAdd(fb_len, 1);
+    fb_list[at] = (int32_t)s;
+  }
+}
+#undef O3DX_WAVE_SCAN
+
+template <int KMAX>
+__global__ void __launch_bounds__(64 * kWavesPerBlock) k_normals_knn_wave(
+    GridView g, int kneed, const float* __restrict__ prior, float* __restrict__ out,
+    const int32_t* __restrict__ in_list, const int32_t* __restrict__ in_len, int32_t* __restrict__ fb_list,
+    int32_t* __restrict__ fb_len) {
+  __shared__ int32_t sel[kWavesPerBlock][KMAX];
+  __shared__ int32_t bnd[kWavesPerBlock][kWaveBnd];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t lim = in_list ? (int64_t)*in_len : g.n;
+  for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wv; t < lim; t += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t s = in_list ? (int64_t)__builtin_amdgcn_readfirstlane(in_list[t]) : t;
+    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], fb_list, fb_len);
   }
 }
 
@@ -901,10 +1171,10 @@ extern "C" int o3dx_set_search_stats(int enable) {
 
 extern "C" int o3dx_search_stats(int64_t* out) {
   if (!out) return fail(O3DX_EINVAL, "o3dx_search_stats: null output");
-  unsigned long long v[4] = {0, 0, 0, 0};
+  unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
   if (g_stats && hipDeviceSynchronize() == hipSuccess)
     (void)hipMemcpy(v, g_stats, sizeof(v), hipMemcpyDeviceToHost);
-  for (int i = 0; i < 4; ++i) out[i] = (int64_t)v[i];
+  for (int i = 0; i < 6; ++i) out[i] = (int64_t)v[i];
   return 0;
 }
 
@@ -928,13 +1198,10 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
   double min_h = (mode == O3DX_SEARCH_KNN) ? 0.0 : 0.0;
   O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), min_h, ws, ws_bytes, s, &G));
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
-  KTimer kt("normals_knn", s);
   const int kneed = (int)std::min<int64_t>(knn, n);
-  if (mode == O3DX_SEARCH_RADIUS) {
-    hipLaunchKernelGGL(k_normals_radius, dim3(grid), dim3(kBlock), 0, s, G.view, radius, prior, out);
-  } else if (mode == O3DX_SEARCH_KNN && kneed >= 1 && !getenv("O3DX_NORMALS_TOPK")) {
-    // LDS tiles -> global histogram-select -> exact register top-k, each level
-    // serving the queries the previous one could not settle
+  if (mode == O3DX_SEARCH_KNN && kneed >= 1 && !getenv("O3DX_NORMALS_TOPK")) {
+    // LDS tiles (lane per query) -> wave per query -> exact register top-k,
+    // each level serving the queries the previous one could not settle
     Arena ar((char*)ws + grid_ws_bytes(n), ws_bytes - grid_ws_bytes(n));
     int32_t* lens = ar.take<int32_t>(4);
     int32_t* list1 = ar.take<int32_t>(n);
@@ -943,40 +1210,38 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
     void* pws = ar.take<char>(chunk_plan_ws_bytes(n));
     O3DX_ARENA_CHECK(ar);
     O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
-    const unsigned g64 = (unsigned)((n + 63) / 64);
     const bool tiles = !getenv("O3DX_NORMALS_NO_TILES");
-    if (tiles) {
-      int64_t nchunks = 0;
-      kt.stop();
-      O3DX_TRY(chunk_plan(G.view.pts, n, G.view, nullptr, kTileQ, chunks, &nchunks, pws,
-                          chunk_plan_ws_bytes(n), s));
-      KTimer kt2("normals_knn", s);
-      if (kneed <= 32)
+    int64_t nchunks = 0;
+    if (tiles)
+      O3DX_TRY(chunk_plan(G.view.pts, n, G.view, nullptr, kTileQ, chunks, &nchunks, pws, chunk_plan_ws_bytes(n), s));
+    KTimer kt("normals_knn", s);
+    const int32_t* wl = tiles ? list1 : nullptr;
+    const int32_t* wlen = tiles ? lens : nullptr;
+    // the wave form grid-strides over its list (at most n queries)
+    const unsigned gw = (unsigned)std::min<int64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 8192);
+    if (kneed <= 32) {
+      if (tiles)
         hipLaunchKernelGGL(k_normals_knn_tile<32>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
                            kneed, prior, out, list1, lens);
-      else
+      hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
+                         out, wl, wlen, list2, lens + 1);
+    } else {
+      if (tiles)
         hipLaunchKernelGGL(k_normals_knn_tile<64>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
                            kneed, prior, out, list1, lens);
-      if (kneed <= 32)
-        hipLaunchKernelGGL(k_normals_knn_hist<32>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out, list1, lens,
-                           list2, lens + 1);
-      else
-        hipLaunchKernelGGL(k_normals_knn_hist<64>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out, list1, lens,
-                           list2, lens + 1);
-    } else {
-      if (kneed <= 32)
-        hipLaunchKernelGGL(k_normals_knn_hist<32>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out,
-                           (const int32_t*)nullptr, (const int32_t*)nullptr, list2, lens + 1);
-      else
-        hipLaunchKernelGGL(k_normals_knn_hist<64>, dim3(g64), dim3(64), 0, s, G.view, kneed, prior, out,
-                           (const int32_t*)nullptr, (const int32_t*)nullptr, list2, lens + 1);
+      hipLaunchKernelGGL(k_normals_knn_wave<64>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
+                         out, wl, wlen, list2, lens + 1);
     }
-    O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, 0, radius, prior,
-                    out, list2, lens + 1);
+    O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed, 0,
+                    radius, prior, out, list2, lens + 1);
   } else {
-    O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed,
-                    mode == O3DX_SEARCH_HYBRID ? 1 : 0, radius, prior, out, (const int32_t*)nullptr,
-                    (const int32_t*)nullptr);
+    KTimer kt("normals_knn", s);
+    if (mode == O3DX_SEARCH_RADIUS)
+      hipLaunchKernelGGL(k_normals_radius, dim3(grid), dim3(kBlock), 0, s, G.view, radius, prior, out);
+    else
+      O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed,
+                      mode == O3DX_SEARCH_HYBRID ? 1 : 0, radius, prior, out, (const int32_t*)nullptr,
+                      (const int32_t*)nullptr);
   }
   O3DX_HIP(hipGetLastError());
   return 0;

@@ -264,15 +264,20 @@ struct TileBox {
   int nyr;  // y1 - y0 + 1
 };
 
-// Stage the box into LDS.  Every thread of the block must call it.  Returns
-// the number of staged points, or -1 if the box does not fit (pts_cap points
-// / cs_cap cell-start slots / kMaxTileRows rows).  `rows` needs kMaxTileRows+1 ints.
+// Stage the box into LDS as three float arrays (x, y, z; the original index
+// is not staged: the rare exact-tie test fetches it with tile_global_pos).
+// Every thread of the block must call it.  Returns the number of staged
+// points, or -1 if the box does not fit (PTS points / cs_cap cell-start slots
+// / kMaxTileRows rows).  `rows` needs kMaxTileRows+1 ints, `rstart` kMaxTileRows.
+// The row prefix is one wave scan; each thread issues all of its (at most
+// PTS/BLOCK) global loads before the first LDS store.
 constexpr int kMaxTileRows = 36;
 
-template <int BLOCK>
-__device__ int stage_tile(const GridView& g, const TileBox& b, float4* __restrict__ pts, int pts_cap,
-                          int32_t* __restrict__ ccs, int cs_cap, int32_t* __restrict__ rows,
+template <int BLOCK, int PTS>
+__device__ int stage_tile(const GridView& g, const TileBox& b, float* __restrict__ tx, float* __restrict__ ty,
+                          float* __restrict__ tz, int32_t* __restrict__ ccs, int cs_cap, int32_t* __restrict__ rows,
                           int32_t* __restrict__ rstart) {
+  static_assert(BLOCK >= kMaxTileRows, "row scan needs one lane per row");
   const int nrows = b.nyr * (b.z1 - b.z0 + 1);
   const int w = b.nxr + 1;
   if (nrows > kMaxTileRows || nrows * w > cs_cap) return -1;  // uniform across the block
@@ -282,29 +287,53 @@ __device__ int stage_tile(const GridView& g, const TileBox& b, float4* __restric
     ccs[t] = g.start[(b.x0 + i) + g.nx * (y + g.ny * z)];  // global position for now
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int k = 0; k < nrows; ++k) {
-      rows[k] = acc;
-      rstart[k] = ccs[k * w];
-      acc += ccs[k * w + b.nxr] - ccs[k * w];
+  if (threadIdx.x < 64) {
+    const int k = threadIdx.x;
+    const int r0 = k < nrows ? ccs[k * w] : 0;
+    const int len = k < nrows ? ccs[k * w + b.nxr] - r0 : 0;
+    const int inc = wave_incl_scan(len);
+    if (k < nrows) {
+      rows[k + 1] = inc;
+      rstart[k] = r0;
     }
-    rows[nrows] = acc;
+    if (k == 0) rows[0] = 0;
   }
   __syncthreads();
   const int total = rows[nrows];
-  if (total > pts_cap) return -1;
+  if (total > PTS) return -1;
   for (int t = threadIdx.x; t < nrows * w; t += BLOCK) {
     const int k = t / w;
     ccs[t] = rows[k] + (ccs[t] - rstart[k]);
   }
+  constexpr int J = (PTS + BLOCK - 1) / BLOCK;
+  float4 buf[J];
   int k = 0;  // f only grows, so the row index is carried along
-  for (int f = threadIdx.x; f < total; f += BLOCK) {
-    while (rows[k + 1] <= f) ++k;
-    pts[f] = g.pts[rstart[k] + (f - rows[k])];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int f = threadIdx.x + j * BLOCK;
+    if (f < total) {
+      while (rows[k + 1] <= f) ++k;
+      buf[j] = g.pts[rstart[k] + (f - rows[k])];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int f = threadIdx.x + j * BLOCK;
+    if (f < total) {
+      tx[f] = buf[j].x;
+      ty[f] = buf[j].y;
+      tz[f] = buf[j].z;
+    }
   }
   __syncthreads();
   return total;
+}
+
+// Global (cell-sorted) position of LDS tile slot f.
+__device__ __forceinline__ int tile_global_pos(const int32_t* rows, const int32_t* rstart, int f) {
+  int k = 0;
+  while (rows[k + 1] <= f) ++k;
+  return rstart[k] + (f - rows[k]);
 }
 
 // Cube S=1 around (cx,cy,cz) inside a staged box: f(lds_p0, lds_p1) per row.

@@ -155,17 +155,18 @@ def kernel_timing(name: str):
 
 def search_stats(enable=None):
     """Debug: enable/disable neighbour-search counters, or read
-    {queries, cells, candidates, shells} when called without arguments."""
+    {queries, cells, candidates, shells, tile/hist hand-offs} when called
+    without arguments."""
     import numpy as _np
 
     if enable is not None:
         check(load().o3dx_set_search_stats(1 if enable else 0), "search_stats")
         return None
-    out = _np.zeros(4, _np.int64)
+    out = _np.zeros(6, _np.int64)
     check(load().o3dx_search_stats(out.ctypes.data_as(ctypes.c_void_p)), "search_stats")
     q = max(int(out[0]), 1)
     return {"queries": int(out[0]), "cells_per_query": out[1] / q, "cands_per_query": out[2] / q,
-            "shells_per_query": out[3] / q}
+            "shells_per_query": out[3] / q, "tile_fallbacks": int(out[4]), "hist_fallbacks": int(out[5])}
 
 
 def release_workspaces():

@@ -266,16 +266,48 @@ def test_icp_accumulate_sorted_source_layout(dev):
     np.testing.assert_allclose(b[:30], ref[:30], rtol=1e-9, atol=1e-9)
 
 
-def test_normals_knn_paths_agree(dev):
-    """histogram-select path vs the exact register top-k path (fallback form)."""
+@pytest.mark.parametrize("k", [5, 30, 64])
+@pytest.mark.parametrize("shape", ["cube", "surface", "dups"])
+def test_normals_knn_paths_agree(dev, k, shape):
+    """The three KNN-normals forms (LDS tile -> wave per query -> register
+    top-k) agree: default chain vs wave form over every query vs exact top-k."""
     import os
-    pts = S.uniform_cube(200_000, 12)
+    if shape == "cube":
+        pts = S.uniform_cube(200_000, 12)
+    elif shape == "surface":
+        pts = S.box_surface(200_000, 13)
+    else:  # exact duplicates: ties at d2 = 0 (pairs / triples keep the covariance well posed)
+        base = S.uniform_cube(20_000, 14)
+        pts = torch.cat([base, base[:5000], base[:5000]])
     x = pts.to(dev)
-    a = ops.estimate_normals(x, knn=30).cpu().numpy()
-    os.environ["O3DX_NORMALS_TOPK"] = "1"
-    try:
-        b = ops.estimate_normals(x, knn=30).cpu().numpy()
-    finally:
-        del os.environ["O3DX_NORMALS_TOPK"]
-    e = np.abs(a - b).max(1)
-    assert np.mean(e < 1e-6) > 0.9999, e.max()
+    outs = {}
+    for mode, env in (("chain", None), ("wave", "O3DX_NORMALS_NO_TILES"), ("topk", "O3DX_NORMALS_TOPK")):
+        if env:
+            os.environ[env] = "1"
+        try:
+            outs[mode] = ops.estimate_normals(x, knn=k).cpu().numpy()
+        finally:
+            if env:
+                del os.environ[env]
+    for mode in ("chain", "wave"):
+        e = np.abs(outs[mode] - outs["topk"]).max(1)
+        assert np.mean(e < 1e-6) > 0.9999, (mode, e.max())
+
+
+def test_normals_knn_degenerate_clusters(dev):
+    """40 copies of each of 300 points (neighbourhoods of identical points,
+    counters near their packing limits): every form returns finite unit normals
+    and the (0, 0, 1) default where the covariance is exactly zero."""
+    import os
+    base = S.uniform_cube(20_000, 15)
+    pts = torch.cat([base, base[:300].repeat(40, 1)]).to(dev)
+    for env in (None, "O3DX_NORMALS_NO_TILES", "O3DX_NORMALS_TOPK"):
+        if env:
+            os.environ[env] = "1"
+        try:
+            nrm = ops.estimate_normals(pts, knn=30).cpu().numpy()
+        finally:
+            if env:
+                del os.environ[env]
+        assert np.isfinite(nrm).all()
+        assert np.allclose(np.linalg.norm(nrm, axis=1), 1.0, atol=1e-5)
