@@ -212,14 +212,15 @@ def main():
     ev_ms = ev0.elapsed_time(ev1)
 
     kernels = {}
-    for name in ("voxel_assign", "voxel_compact", "grid_count", "grid_sort", "normals_knn"):
+    for name in ("voxel_assign", "voxel_compact", "grid_count", "grid_sort", "normals_tile", "normals_wave",
+                 "normals_knn"):
         ms, cnt = _native.kernel_timing(name)
         if cnt:
             kernels[name] = {"avg_ms": round(ms / cnt, 4), "launches": cnt}
     # algorithmic bytes per launch:
-    #   normals_knn : 12 B/rep read + 12 B/rep normal written
-    #   voxel_assign: 12 B/point read + 4 B/point voxel id written
-    algo_bytes = {"normals_knn": 24.0 * M, "voxel_assign": 16.0 * N}
+    #   normals_tile: M queries x (12 B xyz read + 12 B normal written)
+    #   voxel_assign: N points x (12 B xyz read + 4 B voxel id written)
+    algo_bytes = {"normals_tile": 24.0 * M, "voxel_assign": 16.0 * N}
     dom = max((k for k in kernels if k in algo_bytes), key=lambda k: kernels[k]["avg_ms"], default=None)
     roof = None
     if dom is not None:
@@ -228,7 +229,8 @@ def main():
         traffic = pmc_traffic(args.pmc_json, dom)
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "algorithmic_bytes_per_launch": algo_bytes[dom]}
+                "algorithmic_bytes_per_launch": algo_bytes[dom],
+                "note": "kNN selection is VALU/LDS-issue bound, not HBM bound: see DESIGN.md (Roofline)"}
 
     total_pts = float(N) * world * args.steps
     value = total_pts / elapsed / 1e6

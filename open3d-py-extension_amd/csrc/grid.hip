@@ -609,8 +609,8 @@ __device__ __forceinline__ float dist2_f32(const float4 q, float x, float y, flo
 // Locate the bin of the k-th distance in a histogram over [lo, hi) with
 // `below` points known below lo.  -> bin edges [*L, *U), *cum = points in the
 // bins before it, *cb = points in it; false when no bin reaches k.
-template <bool W8>
-__device__ __forceinline__ bool hist_locate(const RegHist<W8>& hist, int kneed, int below, float lo, float hi,
+template <class H>
+__device__ __forceinline__ bool hist_locate(const H& hist, int kneed, int below, float lo, float hi,
                                             float* L, float* U, int* cum, int* cb) {
   const float bw = (hi - lo) / (float)kHistBins;
   int bstar = -1, c0 = 0, cn = 0;
@@ -707,52 +707,38 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
   return true;
 }
 
-// The locate / refine / select steps over a candidate scan SCAN(BODY) in which
-// BODY sees `pp` (candidate position) and `d2` (float32 distance).  Expects
-// hist (filled over [0, R2)), kneed, R2, sel, bnd, lane; sets fb, nsel, nb.
-#define O3DX_HIST_SELECT(SCAN)                                                                        \
-  {                                                                                                   \
-    float lo = 0.f, hi = R2, L = 0.f, U = 0.f;                                                        \
-    int below = 0;                                                                                    \
-    for (int lvl = 0; !fb; ++lvl) {                                                                   \
-      int cum, cb;                                                                                    \
-      if (!hist_locate(hist, kneed, below, lo, hi, &L, &U, &cum, &cb)) {                             \
-        fb = true;                                                                                    \
-        break;                                                                                        \
-      }                                                                                               \
-      if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;                                    \
-      below += cum;                                                                                   \
-      lo = L;                                                                                         \
-      hi = U;                                                                                         \
-      const float sc = (float)kHistBins / (hi - lo);                                                  \
-      hist.zero();                                                                                    \
-      SCAN(if (d2 >= lo && d2 < hi) hist.add(min((int)((d2 - lo) * sc), kHistBins - 1));)            \
-    }                                                                                                 \
-    if (!fb) {                                                                                        \
-      const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);                 \
-      SCAN(if (d2 < Lm) {                                                                             \
-        if (nsel < KMAX) sel[nsel][lane] = pp;                                                        \
-        ++nsel;                                                                                       \
-      } else if (d2 < Up) {                                                                           \
-        if (nb < kBndCap) bnd[nb][lane] = pp;                                                         \
-        ++nb;                                                                                         \
-      })                                                                                              \
-      fb = nsel > kneed || nb > kBndCap || nsel + nb < kneed;                                         \
-    }                                                                                                 \
-  }
-
 // ---------------------------------------------------------------------------
 // KNN normals, LDS-tile form (first level of the default KNN path).
 // One block = one wave = one chunk of <= 64 consecutive queries in one grid
 // row; the 9-row neighbour box is staged into LDS (coalesced, SoA f32), then
 // every lane runs the histogram-select steps over LDS-resident candidates
-// (shells 0..1 only) with packed 8-bit (k <= 32) or 16-bit counters.
-// Queries the tile cannot settle (fewer than k points within the shell-1
-// radius, a counter could overflow, the band overflows, or the box does not
-// fit in LDS) are appended to fb_list for the global form.
+// (shells 0..1 only).  The histogram lives in LDS (in the selection list's
+// space, unused until the select scan): 18 packed 16-bit slots per lane —
+// 0 below the range, 1..16 the bins, 17 at or above it — word-major [9][64]
+// so each lane owns a bank column, updated with ds_add (no dependency on
+// the previous update).  Queries the tile cannot settle (fewer than k points
+// within the shell-1 radius, the band overflows, the order check fails, or
+// a single cell's box does not fit in LDS) are appended to fb_list for the
+// wave form.  A chunk whose box does not fit is processed in x-halves.
 constexpr int kTileQ = 64;
 constexpr int kTilePts = 960;
 constexpr int kTileCs = 384;
+
+// Blocks are dealt round-robin over the 8 XCDs (b and b+8 share one, each XCD
+// has its own L2): give each XCD a contiguous run of chunks, so the rows a
+// chunk stages were mostly staged just before by its neighbours on the same
+// XCD.  A bijection on [0, nb).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int x = b & 7, i = b >> 3, q = nb >> 3, r = nb & 7;
+  return x * q + min(x, r) + i;
+}
+
+struct TileHist {
+  uint32_t h[9];
+  __device__ __forceinline__ int count(int b) const {  // b in -1..16; compile-time after unrolling
+    return (int)((h[(b + 1) >> 1] >> (((b + 1) & 1) * 16)) & 0xffffu);
+  }
+};
 
 // Row r (0..8) of the 3x3 (y,z) rows around (cy,cz), clipped to the box and
 // to x in [cx-1, cx+1]: LDS slots [*a, *e) (empty when outside the box).
@@ -798,6 +784,18 @@ __device__ __forceinline__ void tile_row(const TileBox& b, const int32_t* ccs, i
     }                                                       \
   }
 
+// Histogram of the cube's candidates over [LO, LO + 16/SC) into the LDS slots
+// `hw`, then into registers `th`.
+#define O3DX_TILE_HIST(LO, SC)                                                              \
+  {                                                                                         \
+    _Pragma("unroll") for (int i_ = 0; i_ < 9; ++i_) hw[i_ * 64 + lane] = 0u;              \
+    O3DX_TILE_SCAN({                                                                        \
+      const int ix_ = (int)fminf(fmaxf((d2 - (LO)) * (SC), -1.0f), 16.0f) + 1;              \
+      atomicAdd(&hw[(ix_ >> 1) * 64 + lane], 1u << ((ix_ & 1) << 4));                      \
+    })                                                                                      \
+    _Pragma("unroll") for (int i_ = 0; i_ < 9; ++i_) th.h[i_] = hw[i_ * 64 + lane];        \
+  }
+
 template <int KMAX>
 __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
                                                              int kneed, const float* __restrict__ prior,
@@ -811,51 +809,94 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   __shared__ uint16_t sel[KMAX][kTileQ];
   __shared__ uint16_t bnd[kBndCap][kTileQ];
   const int lane = threadIdx.x;
-  const int q0 = chunk_starts[blockIdx.x], q1 = chunk_starts[blockIdx.x + 1];
+  const int c = xcd_block(blockIdx.x, gridDim.x);
+  const int q0 = chunk_starts[c], q1 = chunk_starts[c + 1];
   const int64_t s = (int64_t)q0 + lane;
   const bool active = s < q1;
-  // the chunk lies in one (y,z) row and is sorted by x: first/last give the box
+  // the chunk lies in one (y,z) row and is sorted by x: first/last give its cells
   int ax, ay, az, bx, by, bz;
   {
     const float4 f = g.pts[q0], l = g.pts[q1 - 1];
     grid_cell(g, f.x, f.y, f.z, ax, ay, az);
     grid_cell(g, l.x, l.y, l.z, bx, by, bz);
   }
-  TileBox box;
-  box.x0 = max(min(ax, bx) - 1, 0);
-  box.x1 = min(max(ax, bx) + 1, g.nx - 1);
-  box.y0 = max(ay - 1, 0);
-  box.y1 = min(ay + 1, g.ny - 1);
-  box.z0 = max(az - 1, 0);
-  box.z1 = min(az + 1, g.nz - 1);
-  box.nxr = box.x1 - box.x0 + 1;
-  box.nyr = box.y1 - box.y0 + 1;
-  const int staged = stage_tile<kTileQ, kTilePts>(g, box, tx, ty, tz, ccs, kTileCs, rows, rst);
-  if (!active) return;  // no barrier below this point
-  const float4 q = g.pts[s];
+  const float4 q = g.pts[active ? s : (int64_t)q0];
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
-  bool fb = staged < 0 || cy != ay || cz != az;
-  int nsel = 0, nb = 0;
-  if (!fb) {
-    const double R = (double)g.h + cell_margin(g, q.x, q.y, q.z, cx, cy, cz) - g.slack;
-    const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
-    const float scale = (float)kHistBins / fmaxf(R2, 1e-30f);
-    RegHist<(KMAX <= 32)> hist;
-    hist.zero();
-    int total = 0;
-    O3DX_TILE_SCAN(if (d2 < R2) {
-      hist.add(min((int)(d2 * scale), kHistBins - 1));
-      ++total;
-    })
-    fb = total < kneed || total > hist.kMaxTotal;
-    O3DX_HIST_SELECT(O3DX_TILE_SCAN)
-    if (!fb)
-      fb = !finish_selection<KMAX>(
-          q, kneed, nsel, nb, sel, bnd, lane,
-          [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
-          [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, prior,
-          __float_as_int(q.w), out);
+  bool fb = active && (cy != ay || cz != az);
+  // Parts: x-cell ranges processed left to right.  A part whose box does not
+  // fit in LDS is halved (down to one cell) before it is staged.
+  for (int x_lo = ax; x_lo <= bx;) {
+    int x_hi = bx, staged;
+    TileBox box;
+    for (;;) {
+      box.x0 = max(x_lo - 1, 0);
+      box.x1 = min(x_hi + 1, g.nx - 1);
+      box.y0 = max(ay - 1, 0);
+      box.y1 = min(ay + 1, g.ny - 1);
+      box.z0 = max(az - 1, 0);
+      box.z1 = min(az + 1, g.nz - 1);
+      box.nxr = box.x1 - box.x0 + 1;
+      box.nyr = box.y1 - box.y0 + 1;
+      staged = stage_tile<kTileQ, kTilePts>(g, box, tx, ty, tz, ccs, kTileCs, rows, rst);
+      if (staged >= 0 || x_hi == x_lo) break;
+      __syncthreads();
+      x_hi = x_lo + (x_hi - x_lo) / 2;
+    }
+    if (active && !fb && cx >= x_lo && cx <= x_hi) {
+      fb = staged < 0;
+      if (fb && g.stats) atomicAdd(&g.stats[6], 1ull);
+      int nsel = 0, nb = 0;
+      if (!fb) {
+        const double R = (double)g.h + cell_margin(g, q.x, q.y, q.z, cx, cy, cz) - g.slack;
+        const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
+        static_assert(sizeof(sel) >= 9 * 64 * sizeof(uint32_t), "histogram reuses the selection list");
+        uint32_t* hw = reinterpret_cast<uint32_t*>(&sel[0][0]);
+        TileHist th;
+        O3DX_TILE_HIST(0.0f, (float)kHistBins / fmaxf(R2, 1e-30f))
+        int total = 0;
+#pragma unroll
+        for (int b = 0; b < kHistBins; ++b) total += th.count(b);
+        fb = total < kneed;
+        if (fb && g.stats) atomicAdd(&g.stats[7], 1ull);
+        float lo = 0.f, hi = R2, L = 0.f, U = 0.f;
+        for (int lvl = 0; !fb; ++lvl) {
+          int cum, cb;
+          if (!hist_locate(th, kneed, th.count(-1), lo, hi, &L, &U, &cum, &cb)) {
+            fb = true;
+            break;
+          }
+          if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
+          lo = L;
+          hi = U;
+          O3DX_TILE_HIST(lo, (float)kHistBins / (hi - lo))
+        }
+        if (!fb) {
+          const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
+          int nU = 0;
+          O3DX_TILE_SCAN({
+            nU += d2 < U ? 1 : 0;
+            if (d2 < Lm) {
+              if (nsel < KMAX) sel[nsel][lane] = (uint16_t)pp;
+              ++nsel;
+            } else if (d2 < Up) {
+              if (nb < kBndCap) bnd[nb][lane] = (uint16_t)pp;
+              ++nb;
+            }
+          })
+          // nU >= k: the k nearest lie clearly below Up, so nothing past the band can displace them
+          fb = nsel > kneed || nb > kBndCap || nsel + nb < kneed || nU < kneed;
+        }
+        if (!fb)
+          fb = !finish_selection<KMAX>(
+              q, kneed, nsel, nb, sel, bnd, lane,
+              [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
+              [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, prior,
+              __float_as_int(q.w), out);
+      }
+    }
+    x_lo = x_hi + 1;
+    __syncthreads();  // the next part restages the LDS tile
   }
   if (fb) {
     if (g.stats) atomicAdd(&g.stats[4], 1ull);
@@ -864,7 +905,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   }
 }
 #undef O3DX_TILE_SCAN
-#undef O3DX_HIST_SELECT
+#undef O3DX_TILE_HIST
 
 
 // ---------------------------------------------------------------------------
@@ -969,7 +1010,9 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   int nsel = 0, nb = 0;
   if (!fb) {
     const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
+    int nU = 0;
     O3DX_WAVE_SCAN(S, {
+      nU += __popcll(__ballot(valid && d2 < U));
       const bool c1 = valid && d2 < Lm;
       const bool c2 = valid && !(d2 < Lm) && d2 < Up;
       const uint64_t m1 = __ballot(c1);
@@ -985,7 +1028,7 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
       nsel += __popcll(m1);
       nb += __popcll(m2);
     })
-    fb = nsel > kneed || nb > kWaveBnd || nsel + nb < kneed;
+    fb = nsel > kneed || nb > kWaveBnd || nsel + nb < kneed || nU < kneed;
   }
   if (!fb) {
     wave_sync();
@@ -1171,10 +1214,10 @@ extern "C" int o3dx_set_search_stats(int enable) {
 
 extern "C" int o3dx_search_stats(int64_t* out) {
   if (!out) return fail(O3DX_EINVAL, "o3dx_search_stats: null output");
-  unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (g_stats && hipDeviceSynchronize() == hipSuccess)
     (void)hipMemcpy(v, g_stats, sizeof(v), hipMemcpyDeviceToHost);
-  for (int i = 0; i < 6; ++i) out[i] = (int64_t)v[i];
+  for (int i = 0; i < 8; ++i) out[i] = (int64_t)v[i];
   return 0;
 }
 
@@ -1219,18 +1262,23 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
     const int32_t* wlen = tiles ? lens : nullptr;
     // the wave form grid-strides over its list (at most n queries)
     const unsigned gw = (unsigned)std::min<int64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 8192);
-    if (kneed <= 32) {
-      if (tiles)
+    if (tiles) {
+      KTimer kt_tile("normals_tile", s);
+      if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_tile<32>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
                            kneed, prior, out, list1, lens);
-      hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
-                         out, wl, wlen, list2, lens + 1);
-    } else {
-      if (tiles)
+      else
         hipLaunchKernelGGL(k_normals_knn_tile<64>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
                            kneed, prior, out, list1, lens);
-      hipLaunchKernelGGL(k_normals_knn_wave<64>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
-                         out, wl, wlen, list2, lens + 1);
+    }
+    {
+      KTimer kt_wave("normals_wave", s);
+      if (kneed <= 32)
+        hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
+                           out, wl, wlen, list2, lens + 1);
+      else
+        hipLaunchKernelGGL(k_normals_knn_wave<64>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
+                           out, wl, wlen, list2, lens + 1);
     }
     O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed, 0,
                     radius, prior, out, list2, lens + 1);

@@ -162,11 +162,12 @@ def search_stats(enable=None):
     if enable is not None:
         check(load().o3dx_set_search_stats(1 if enable else 0), "search_stats")
         return None
-    out = _np.zeros(6, _np.int64)
+    out = _np.zeros(8, _np.int64)
     check(load().o3dx_search_stats(out.ctypes.data_as(ctypes.c_void_p)), "search_stats")
     q = max(int(out[0]), 1)
     return {"queries": int(out[0]), "cells_per_query": out[1] / q, "cands_per_query": out[2] / q,
-            "shells_per_query": out[3] / q, "tile_fallbacks": int(out[4]), "hist_fallbacks": int(out[5])}
+            "shells_per_query": out[3] / q, "tile_fallbacks": int(out[4]), "wave_fallbacks": int(out[5]),
+            "tile_box_overflow": int(out[6]), "tile_short_radius": int(out[7])}
 
 
 def release_workspaces():

@@ -56,9 +56,14 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         run_one()
         sys.exit(0)
-    grid = [{}, {"O3DX_GRID_OCC": "8"}, {"O3DX_GRID_OCC": "12"}, {"O3DX_GRID_OCC": "16"},
-            {"O3DX_ICP_MINH_DIV": "16", "O3DX_ICP_OCC": "1"}, {"O3DX_ICP_MINH_DIV": "16", "O3DX_ICP_OCC": "4"},
-            {"O3DX_ICP_MINH_DIV": "32", "O3DX_ICP_OCC": "2"}]
+    sweep = os.environ.get("SWEEP", "")
+    if sweep:  # e.g. SWEEP=O3DX_GRID_OCC=8,10,12
+        key, vals = sweep.split("=")
+        grid = [{key: v} for v in vals.split(",")]
+    else:
+        grid = [{}, {"O3DX_GRID_OCC": "8"}, {"O3DX_GRID_OCC": "12"}, {"O3DX_GRID_OCC": "16"},
+                {"O3DX_ICP_MINH_DIV": "16", "O3DX_ICP_OCC": "1"}, {"O3DX_ICP_MINH_DIV": "16", "O3DX_ICP_OCC": "4"},
+                {"O3DX_ICP_MINH_DIV": "32", "O3DX_ICP_OCC": "2"}]
     for extra in grid:
         env = dict(os.environ, **extra)
         r = subprocess.run([sys.executable, __file__, "one"], env=env, capture_output=True, text=True, timeout=300)
