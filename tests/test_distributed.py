@@ -1,0 +1,157 @@
+"""CPU: the multi-GPU path's collectives with torch.distributed `gloo`,
+world size 2 (one process per rank, rendezvous on 127.0.0.1).  The per-rank
+compute is the oracle (test infrastructure) so these run without a GPU; the
+GPU box runs the same helpers over RCCL with the HIP kernels as `accumulate`.
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import np_restate as NPR
+from oracle import oracle as O
+from open3dpypro import distributed as D
+from open3dpypro import synthetic as S
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(rank, world, port, fn, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # surface the failure in the parent
+        q.put((rank, e))
+    finally:
+        dist.destroy_process_group()
+
+
+def spawn(fn, world=WORLD):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_run, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, v = q.get(timeout=300)
+        out[r] = v
+    for p in ps:
+        p.join(timeout=60)
+    for r, v in out.items():
+        if isinstance(v, Exception):
+            raise v
+    return [out[r] for r in range(world)]
+
+
+# ---------------------------------------------------------------- AABB
+def _aabb_rank(rank, world):
+    pts = S.uniform_cube(5000, 3 + rank).numpy() * (rank + 1) - rank
+    mn, mx = O.aabb(pts)
+    return D.global_aabb(mn, mx)
+
+
+def test_global_aabb_two_ranks():
+    res = spawn(_aabb_rank)
+    allp = np.concatenate([S.uniform_cube(5000, 3 + r).numpy() * (r + 1) - r for r in range(WORLD)])
+    mn, mx = O.aabb(allp)
+    for gmn, gmx in res:
+        assert np.array_equal(gmn, mn) and np.array_equal(gmx, mx)
+
+
+# ---------------------------------------------------------------- voxel slabs
+def test_voxel_slabs_partition_reps():
+    """x-slabs aligned to the global voxel grid: per-slab voxel reps (with the
+    global min/max bound) are exactly the single-GPU reps, split by owner."""
+    pts = S.uniform_cube(40_000, 21).numpy()
+    vs = 0.05
+    mn, mx = O.aabb(pts)
+    full = O.voxel_down_sample(pts, vs, mn, mx)
+    for world in (2, 3, 4):
+        keys = D.slab_bounds(mn, mx, vs, world)
+        kx = np.floor((pts[:, 0].astype(np.float64) - mn[0]) / vs).astype(np.int64)
+        owner = D.slab_of(kx, keys)
+        got = []
+        for r in range(world):
+            idx = np.nonzero(owner == r)[0]
+            rep = O.voxel_down_sample(pts[idx], vs, mn, mx)
+            got.append(idx[rep])
+        got = np.sort(np.concatenate(got))
+        assert np.array_equal(got, np.sort(full))
+
+
+# ---------------------------------------------------------------- RANSAC counts
+def _ransac_rank(rank, world):
+    pts = S.planted_plane(20_000, 5).numpy()
+    samples = O.ransac_samples(len(pts), 3, 64, 11)
+    a, b = D.shard_range(len(pts), world, rank)
+    # planes come from the replicated sample list; each rank counts its shard
+    p64 = pts.astype(np.float64)
+    counts = []
+    for s in samples:
+        pl = NPR.triangle_plane(p64[s[0]], p64[s[1]], p64[s[2]])
+        counts.append(-1 if not pl.any() else int((NPR.plane_dist(pl, p64[a:b]) < 0.01).sum()))
+    return D.allreduce_counts(np.array(counts, np.int64))
+
+
+def test_ransac_counts_allreduce_exact():
+    res = spawn(_ransac_rank)
+    pts = S.planted_plane(20_000, 5).numpy()
+    samples = O.ransac_samples(len(pts), 3, 64, 11)
+    ref = NPR.segment_plane_counts(pts, 0.01, samples)
+    for got in res:
+        assert np.array_equal(got, ref)
+
+
+# ---------------------------------------------------------------- ICP
+def _icp_clouds():
+    tgt = S.box_surface(20_000, 1).numpy()
+    src = S.box_surface(20_000, 2).numpy()
+    Tgt = S.rigid_transform()
+    src = (src.astype(np.float64) @ Tgt[:3, :3].T + Tgt[:3, 3]).astype(np.float32)
+    tn = O.estimate_normals(tgt, O.KNN, 30)
+    return src, tgt, tn
+
+
+def _icp_rank(rank, world):
+    src, tgt, tn = _icp_clouds()
+    a, b = D.shard_range(len(src), world, rank)
+    shard = src[a:b]
+    return D.registration_icp_point_to_plane(lambda T: O.icp_accumulate(shard, tgt, tn, 0.05, T),
+                                             len(src), max_iteration=15)
+
+
+def test_icp_sharded_matches_single():
+    res = spawn(_icp_rank)
+    src, tgt, tn = _icp_clouds()
+    T1, f1, r1 = D.registration_icp_point_to_plane(lambda T: O.icp_accumulate(src, tgt, tn, 0.05, T),
+                                                   len(src), max_iteration=15)
+    (Ta, fa, ra), (Tb, fb, rb) = res
+    assert np.array_equal(Ta, Tb) and fa == fb and ra == rb  # every rank solved the same bits
+    assert np.abs(Ta - T1).max() < 1e-9
+    assert abs(fa - f1) < 1e-12 and abs(ra - r1) < 1e-9
+    # and the loop is the oracle's registration_icp
+    To, fo, ro = O.registration_icp(src, tgt, tn, 0.05, max_iteration=15)[:3]
+    assert np.abs(T1 - To).max() < 1e-9 and abs(f1 - fo) < 1e-12
+
+
+def test_shard_range_covers():
+    for n in (0, 1, 7, 1000, 1001):
+        for world in (1, 2, 3, 8):
+            parts = [D.shard_range(n, world, r, align=4) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))

@@ -1,0 +1,44 @@
+"""GPU: the sharded ICP driver with the HIP accumulate kernel as each rank's
+`accumulate` — two ranks (gloo rendezvous on 127.0.0.1) sharing the one GPU of
+the test box, against the single-process device loop and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from open3dpypro import distributed as D
+from open3dpypro import ops, synthetic as S
+
+from test_distributed import spawn
+
+pytestmark = pytest.mark.gpu
+
+
+def _clouds():
+    tgt = S.box_surface(200_000, 1).numpy()
+    src = S.box_surface(200_000, 2).numpy()
+    Tg = S.rigid_transform()
+    src = (src.astype(np.float64) @ Tg[:3, :3].T + Tg[:3, 3]).astype(np.float32)
+    return src, tgt
+
+
+def _rank(rank, world):
+    dev = torch.device("cuda:0")
+    src, tgt = _clouds()
+    t = torch.from_numpy(tgt).to(dev)
+    tn = ops.estimate_normals(t, knn=30)
+    target = ops.ICPTarget(t, tn, 0.02)
+    a, b = D.shard_range(len(src), world, rank)
+    shard = ops.spatial_sort(torch.from_numpy(src[a:b]).to(dev))
+    return D.registration_icp_point_to_plane(lambda T: target.accumulate(shard, T)[0], len(src), max_iteration=20)
+
+
+def test_sharded_icp_on_device_matches_single():
+    (Ta, fa, ra), (Tb, fb, rb) = spawn(_rank)
+    assert np.array_equal(Ta, Tb) and fa == fb and ra == rb
+    T1, f1, r1 = _rank(0, 1)
+    assert np.abs(Ta - T1).max() < 1e-9 and abs(fa - f1) < 1e-12
+    src, tgt = _clouds()
+    tn = O.estimate_normals(tgt, O.KNN, 30)
+    To, fo, ro = O.registration_icp(src, tgt, tn, 0.02, max_iteration=20)[:3]
+    assert np.abs(T1 - To).max() < 1e-5 and abs(f1 - fo) < 1e-5
