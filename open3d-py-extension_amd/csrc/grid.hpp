@@ -215,36 +215,57 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   // outside the query's cell (clamped): m < 0 shrinks the bound, still valid
   const int rmax = shell_rmax(g, cx, cy, cz);
   const double r2lim = radius * radius;
-  int st_cells = 0, st_cands = 0, r = 1;
-  auto visit = [&](int p, const float4 v) {
-    const double d = dist2_f64(qx, qy, qz, v);
-    const int oi = __float_as_int(v.w);
-    if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
-      bd = d;
-      bi = oi;
-      bp = p;
-    }
-  };
-  // shells 0 and 1 together: 9 contiguous row ranges
-  for_cube_rows(g, cx, cy, cz, 1, [&](int p0, int p1) {
+  int st_cells = 0, st_cands = 0, r = 0;
+  // Cells are visited shell by shell, each only if its box (shrunk by the
+  // rounding slack) can hold a point that beats the current best (or lies
+  // inside the radius while there is none): a lower bound, so the result is
+  // the exact lexicographic (d^2, index) minimum.
+  auto visit_cell = [&](int x, int y, int z) {
+    const double bx0 = (double)g.ox + (double)x * g.h, by0 = (double)g.oy + (double)y * g.h,
+                 bz0 = (double)g.oz + (double)z * g.h;
+    const double ex = fmax(fmax(bx0 - qx, qx - (bx0 + g.h)) - g.slack, 0.0);
+    const double ey = fmax(fmax(by0 - qy, qy - (by0 + g.h)) - g.slack, 0.0);
+    const double ez = fmax(fmax(bz0 - qz, qz - (bz0 + g.h)) - g.slack, 0.0);
+    const double lb = (ex * ex + ey * ey) + ez * ez;
+    if (lb > (bi >= 0 ? bd : r2lim)) return;
+    const int c = x + g.nx * (y + g.ny * z);
+    const int p0 = g.start[c], p1 = g.start[c + 1];
     if (g.stats) {
-      st_cells += 3;
+      ++st_cells;
       st_cands += p1 - p0;
     }
-    for_points4(g, p0, p1, visit);
-  });
+    for_points4(g, p0, p1, [&](int p, const float4 v) {
+      const double d = dist2_f64(qx, qy, qz, v);
+      const int oi = __float_as_int(v.w);
+      if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
+        bd = d;
+        bi = oi;
+        bp = p;
+      }
+    });
+  };
+  visit_cell(cx, cy, cz);
   for (;; ++r) {
+    // every point within B of q has been visited (or pruned by the bound)
     const double B = (double)r * g.h + m - g.slack;
     if (B >= radius || r >= rmax) break;
     if (bi >= 0 && B > 0.0 && bd < B * B) break;
-    for_shell(g, cx, cy, cz, r + 1, [&](int c) {
-      const int s1 = g.start[c + 1];
-      if (g.stats) {
-        ++st_cells;
-        st_cands += s1 - g.start[c];
+    const int rr = r + 1;
+    for (int dz = -rr; dz <= rr; ++dz) {
+      const int z = cz + dz;
+      if (z < 0 || z >= g.nz) continue;
+      const bool zf = (dz == -rr) || (dz == rr);
+      for (int dy = -rr; dy <= rr; ++dy) {
+        const int y = cy + dy;
+        if (y < 0 || y >= g.ny) continue;
+        const int step = (zf || dy == -rr || dy == rr) ? 1 : 2 * rr;
+        for (int dx = -rr; dx <= rr; dx += step) {
+          const int x = cx + dx;
+          if (x < 0 || x >= g.nx) continue;
+          visit_cell(x, y, z);
+        }
       }
-      for_points4(g, g.start[c], s1, visit);
-    });
+    }
   }
   search_stats(g, st_cells, st_cands, r + 1);
   *best_d2 = bd;

@@ -283,7 +283,7 @@ static int accumulate(const float* src, int64_t ns, bool sorted, const GridView&
 // grid occupancy / minimum cell for the 1-NN-within-radius search
 static double icp_min_h(double max_corr) {
   if (const char* e = getenv("O3DX_ICP_MINH_DIV")) return max_corr / atof(e);  // tuning override
-  return max_corr / 8.0;
+  return max_corr / 16.0;
 }
 static double icp_occ() {
   if (const char* e = getenv("O3DX_ICP_OCC")) return atof(e);

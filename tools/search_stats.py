@@ -39,6 +39,16 @@ def run_one():
     target = ops.ICPTarget(tgt, tn, 0.02)
     src = ops.spatial_sort(src)
     T = np.eye(4)
+    target.accumulate(src, T)
+    _native.search_stats(True)
+    _native.reset_kernel_timing()
+    target.accumulate(src, T)
+    out["icp_stats_first"] = _native.search_stats()
+    _native.search_stats(False)
+    _native.reset_kernel_timing()
+    target.accumulate(src, T)
+    ms, c = _native.kernel_timing("icp_accumulate")
+    out["icp_ms_first"] = ms / c
     for it in range(3):
         sums, _ = target.accumulate(src, T)
         T = ops.icp_solve(sums) @ T
@@ -46,9 +56,11 @@ def run_one():
     _native.reset_kernel_timing()
     sums, _ = target.accumulate(src, T)
     out["icp_stats_converged"] = _native.search_stats()
+    _native.search_stats(False)
+    _native.reset_kernel_timing()
+    sums, _ = target.accumulate(src, T)
     ms, c = _native.kernel_timing("icp_accumulate")
     out["icp_ms_converged"] = ms / c
-    _native.search_stats(False)
     print(json.dumps(out), flush=True)
 
 
