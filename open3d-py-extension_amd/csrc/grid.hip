@@ -733,68 +733,97 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
   return x * q + min(x, r) + i;
 }
 
+constexpr int kTileSlots = kHistBins + 2;  // below the range, the bins, at or above it
+
 struct TileHist {
-  uint32_t h[9];
-  __device__ __forceinline__ int count(int b) const {  // b in -1..16; compile-time after unrolling
-    return (int)((h[(b + 1) >> 1] >> (((b + 1) & 1) * 16)) & 0xffffu);
-  }
+  uint32_t h[kTileSlots];
+  __device__ __forceinline__ int count(int b) const { return (int)h[b + 1]; }  // b in -1..16
 };
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// f32 d^2 of two candidates with packed math (v_pk_add / v_pk_mul / v_pk_fma):
+// the same operations and roundings as dist2_f32, two lanes of work per op.
+__device__ __forceinline__ f32x2 dist2_pair(const float4 q, f32x2 x, f32x2 y, f32x2 z) {
+  const f32x2 dx = (f32x2){q.x, q.x} - x, dy = (f32x2){q.y, q.y} - y, dz = (f32x2){q.z, q.z} - z;
+  return __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+}
+
 // Row r (0..8) of the 3x3 (y,z) rows around (cy,cz), clipped to the box and
-// to x in [cx-1, cx+1]: LDS slots [*a, *e) (empty when outside the box).
-__device__ __forceinline__ void tile_row(const TileBox& b, const int32_t* ccs, int cx, int cy, int cz, int r, int* a,
-                                         int* e) {
+// to x in [cx-1, cx+1], then trimmed to the cells whose box (grown by the
+// rounding slack) comes closer to q than sqrt(bound): LDS slots [*a, *e).
+// A trimmed cell holds no point with f32 d^2 below bound, so no scan that
+// only counts / selects d^2 < bound can miss anything.
+__device__ __forceinline__ void tile_row(const GridView& g, const TileBox& b, const int32_t* ccs, const float4 q,
+                                         int cx, int cy, int cz, int r, float bound, int* a, int* e) {
   const int z = cz + r / 3 - 1, y = cy + r % 3 - 1;
-  if (z < b.z0 || z > b.z1 || y < b.y0 || y > b.y1) {
-    *a = *e = 0;
-    return;
+  *a = *e = 0;
+  if (z < b.z0 || z > b.z1 || y < b.y0 || y > b.y1) return;
+  const float lim = bound * (1.0f + 1e-5f);
+  const float y0 = g.oy + (float)y * g.h, z0 = g.oz + (float)z * g.h;
+  const float gy = fmaxf(fmaxf(y0 - q.y, q.y - (y0 + g.h)) - g.slack, 0.0f);
+  const float gz = fmaxf(fmaxf(z0 - q.z, q.z - (z0 + g.h)) - g.slack, 0.0f);
+  const float dyz = gy * gy + gz * gz;
+  if (dyz > lim) return;
+  int xa = max(cx - 1, b.x0), xb = min(cx + 1, b.x1);
+  if (xa < cx) {
+    const float gx = fmaxf(q.x - (g.ox + (float)cx * g.h) - g.slack, 0.0f);
+    if (dyz + gx * gx > lim) xa = cx;
+  }
+  if (xb > cx) {
+    const float gx = fmaxf((g.ox + (float)(cx + 1) * g.h) - q.x - g.slack, 0.0f);
+    if (dyz + gx * gx > lim) xb = cx;
   }
   const int w = b.nxr + 1;
   const int k = (y - b.y0) + b.nyr * (z - b.z0);
-  *a = ccs[k * w + max(cx - 1, b.x0) - b.x0];
-  *e = ccs[k * w + min(cx + 1, b.x1) - b.x0 + 1];
+  *a = ccs[k * w + xa - b.x0];
+  *e = ccs[k * w + xb - b.x0 + 1];
 }
 
 // Candidates of the query's 27-cell cube from the LDS tile, four at a time
-// (LDS loads issued before use).
-#define O3DX_TILE_SCAN(BODY)                                \
-  for (int r_ = 0; r_ < 9; ++r_) {                          \
-    int a_, e_;                                             \
-    tile_row(box, ccs, cx, cy, cz, r_, &a_, &e_);           \
-    int p_ = a_;                                            \
-    for (; p_ + 4 <= e_; p_ += 4) {                         \
-      float xs_[4], ys_[4], zs_[4];                         \
-      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {    \
-        xs_[u_] = tx[p_ + u_];                              \
-        ys_[u_] = ty[p_ + u_];                              \
-        zs_[u_] = tz[p_ + u_];                              \
-      }                                                     \
-      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {    \
-        const int pp = p_ + u_;                             \
-        (void)pp;                                           \
-        const float d2 = dist2_f32(q, xs_[u_], ys_[u_], zs_[u_]); \
-        BODY                                                \
-      }                                                     \
-    }                                                       \
-    for (; p_ < e_; ++p_) {                                 \
-      const int pp = p_;                                    \
-      (void)pp;                                             \
-      const float d2 = dist2_f32(q, tx[p_], ty[p_], tz[p_]); \
-      BODY                                                  \
-    }                                                       \
+// (LDS loads issued before use, distances two at a time in packed f32).
+#define O3DX_TILE_SCAN(BOUND, BODY)                                        \
+  for (int r_ = 0; r_ < 9; ++r_) {                                         \
+    int a_, e_;                                                            \
+    tile_row(g, box, ccs, q, cx, cy, cz, r_, (BOUND), &a_, &e_);           \
+    int p_ = a_;                                                           \
+    for (; p_ + 4 <= e_; p_ += 4) {                                        \
+      const f32x2 xa_ = {tx[p_], tx[p_ + 1]}, xb_ = {tx[p_ + 2], tx[p_ + 3]}; \
+      const f32x2 ya_ = {ty[p_], ty[p_ + 1]}, yb_ = {ty[p_ + 2], ty[p_ + 3]}; \
+      const f32x2 za_ = {tz[p_], tz[p_ + 1]}, zb_ = {tz[p_ + 2], tz[p_ + 3]}; \
+      const f32x2 da_ = dist2_pair(q, xa_, ya_, za_);                      \
+      const f32x2 db_ = dist2_pair(q, xb_, yb_, zb_);                      \
+      const float ds_[4] = {da_.x, da_.y, db_.x, db_.y};                   \
+      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                   \
+        const int pp = p_ + u_;                                            \
+        (void)pp;                                                          \
+        const float d2 = ds_[u_];                                          \
+        BODY                                                               \
+      }                                                                    \
+    }                                                                      \
+    for (; p_ < e_; ++p_) {                                                \
+      const int pp = p_;                                                   \
+      (void)pp;                                                            \
+      const float d2 = dist2_f32(q, tx[p_], ty[p_], tz[p_]);               \
+      BODY                                                                 \
+    }                                                                      \
   }
 
-// Histogram of the cube's candidates over [LO, LO + 16/SC) into the LDS slots
-// `hw`, then into registers `th`.
-#define O3DX_TILE_HIST(LO, SC)                                                              \
+// Histogram of the cube's candidates over [LO, HI = LO + 16/SC) into the LDS
+// counters `hw` (slot-major [18][64]: each lane owns a bank column; ds_add,
+// no return), then into registers `th`; cells entirely beyond HI skipped.
+#define O3DX_TILE_HIST(LO, SC, HI)                                                          \
   {                                                                                         \
-    _Pragma("unroll") for (int i_ = 0; i_ < 9; ++i_) hw[i_ * 64 + lane] = 0u;              \
-    O3DX_TILE_SCAN({                                                                        \
-      const int ix_ = (int)fminf(fmaxf((d2 - (LO)) * (SC), -1.0f), 16.0f) + 1;              \
-      atomicAdd(&hw[(ix_ >> 1) * 64 + lane], 1u << ((ix_ & 1) << 4));                      \
-    })                                                                                      \
-    _Pragma("unroll") for (int i_ = 0; i_ < 9; ++i_) th.h[i_] = hw[i_ * 64 + lane];        \
+    _Pragma("unroll") for (int i_ = 0; i_ < kTileSlots; ++i_) hw[i_ * 64 + lane] = 0u;     \
+    const float off_ = -(LO) * (SC);                                                        \
+    O3DX_TILE_HIST_SCAN((HI), (SC), off_)                                                   \
+    _Pragma("unroll") for (int i_ = 0; i_ < kTileSlots; ++i_) th.h[i_] = hw[i_ * 64 + lane]; \
   }
+#define O3DX_TILE_HIST_SCAN(HI, SC, OFF)                                                    \
+  O3DX_TILE_SCAN(HI, {                                                                      \
+    const int ix_ = (int)fminf(fmaxf(fmaf(d2, (SC), (OFF)), -1.0f), 16.0f);                 \
+    atomicAdd(&hw[(ix_ + 1) * 64 + lane], 1u);                                              \
+  })
 
 template <int KMAX>
 __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
@@ -806,7 +835,12 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   __shared__ int32_t ccs[kTileCs];
   __shared__ int32_t rows[kMaxTileRows + 1];
   __shared__ int32_t rst[kMaxTileRows];
-  __shared__ uint16_t sel[KMAX][kTileQ];
+  // the selection list (u16 [KMAX][64]) and the histogram counters (u32
+  // [18][64]) share one LDS buffer: the histogram is dead before selection
+  constexpr int kSelWords = (KMAX * kTileQ * 2 + 3) / 4;
+  constexpr int kHistWords = kTileSlots * kTileQ;
+  __shared__ uint32_t selbuf[kSelWords > kHistWords ? kSelWords : kHistWords];
+  uint16_t(*sel)[kTileQ] = reinterpret_cast<uint16_t(*)[kTileQ]>(selbuf);
   __shared__ uint16_t bnd[kBndCap][kTileQ];
   const int lane = threadIdx.x;
   const int c = xcd_block(blockIdx.x, gridDim.x);
@@ -850,10 +884,9 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
       if (!fb) {
         const double R = (double)g.h + cell_margin(g, q.x, q.y, q.z, cx, cy, cz) - g.slack;
         const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
-        static_assert(sizeof(sel) >= 9 * 64 * sizeof(uint32_t), "histogram reuses the selection list");
-        uint32_t* hw = reinterpret_cast<uint32_t*>(&sel[0][0]);
+        uint32_t* hw = selbuf;
         TileHist th;
-        O3DX_TILE_HIST(0.0f, (float)kHistBins / fmaxf(R2, 1e-30f))
+        O3DX_TILE_HIST(0.0f, (float)kHistBins / fmaxf(R2, 1e-30f), R2)
         int total = 0;
 #pragma unroll
         for (int b = 0; b < kHistBins; ++b) total += th.count(b);
@@ -869,20 +902,20 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
           if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
           lo = L;
           hi = U;
-          O3DX_TILE_HIST(lo, (float)kHistBins / (hi - lo))
+          O3DX_TILE_HIST(lo, (float)kHistBins / (hi - lo), hi)
         }
         if (!fb) {
           const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
           int nU = 0;
-          O3DX_TILE_SCAN({
+          // branch-free appends: every candidate is written to the next free
+          // slot of both lists and kept only where the count advances
+          O3DX_TILE_SCAN(Up, {
             nU += d2 < U ? 1 : 0;
-            if (d2 < Lm) {
-              if (nsel < KMAX) sel[nsel][lane] = (uint16_t)pp;
-              ++nsel;
-            } else if (d2 < Up) {
-              if (nb < kBndCap) bnd[nb][lane] = (uint16_t)pp;
-              ++nb;
-            }
+            sel[min(nsel, KMAX - 1)][lane] = (uint16_t)pp;
+            bnd[min(nb, kBndCap - 1)][lane] = (uint16_t)pp;
+            const bool in_ = d2 < Lm;
+            nsel += in_ ? 1 : 0;
+            nb += (!in_ && d2 < Up) ? 1 : 0;
           })
           // nU >= k: the k nearest lie clearly below Up, so nothing past the band can displace them
           fb = nsel > kneed || nb > kBndCap || nsel + nb < kneed || nU < kneed;
@@ -906,6 +939,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
 }
 #undef O3DX_TILE_SCAN
 #undef O3DX_TILE_HIST
+#undef O3DX_TILE_HIST_SCAN
 
 
 // ---------------------------------------------------------------------------
