@@ -643,66 +643,79 @@ __device__ __forceinline__ bool key_less(double da, int pa, double db, int pb, I
   return id(pa) < id(pb);
 }
 
-// Exact completion of a histogram selection (see above).  sel[0..nsel) hold
-// the certain members, bnd[0..nb) the band (positions understood by fetch /
-// id).  On success writes the normal of original point `oi` and returns true.
+// Exact completion of a tile selection (see above).  lst[0..n) holds every
+// candidate with f32 d^2 < Up (LDS slots understood by `fetch` / `id`).
+//   1. partition in place: certain (d^2 < Lm) to the front, accumulating
+//      their moments on the way; the rest is the band;
+//   2. move the (k - #certain) nearest band entries by (d2_f64, original
+//      index) to the front of the band, adding their moments;
+//   3. order check: the largest certain key precedes the smallest unselected
+//      band key (exactly only when the f32 bound cannot decide it).
+// Writes the normal of original point `oi`; false = hand the query on.
 template <int KMAX, class T, class Fetch, class Id>
-__device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int nsel, int nb, T (*sel)[64],
-                                                 T (*bnd)[64], int lane, Fetch&& fetch, Id&& id,
-                                                 const float* __restrict__ prior, int oi, float* __restrict__ out) {
+__device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int n, float Lm, float U, T (*lst)[64],
+                                                 int lane, Fetch&& fetch, Id&& id, const float* __restrict__ prior,
+                                                 int oi, float* __restrict__ out, bool skip_eigen = false) {
   const double qx = q.x, qy = q.y, qz = q.z;
-  double bd[kBndCap];
-  int bp[kBndCap];
-#pragma unroll
-  for (int j = 0; j < kBndCap; ++j) {
-    bp[j] = -1;
-    bd[j] = INFINITY;
-    if (j < nb) {
-      bp[j] = (int)bnd[j][lane];
-      bd[j] = dist2_f64(qx, qy, qz, fetch(bp[j]));
+  MomAcc acc;
+  acc.zero();
+  int nsel = 0, nU = 0;
+  for (int j = 0; j < n; ++j) {
+    const int p = (int)lst[j][lane];
+    const float4 v = fetch(p);
+    const float d2f = dist2_f32(q, v.x, v.y, v.z);  // the scan's value, bit for bit
+    nU += d2f < U ? 1 : 0;
+    if (d2f < Lm) {
+      if (nsel != j) {
+        lst[j][lane] = lst[nsel][lane];
+        lst[nsel][lane] = (T)p;
+      }
+      ++nsel;
+      acc.add((double)v.x, (double)v.y, (double)v.z);
     }
   }
-  uint32_t used = 0u;
+  // nU >= k: the k nearest lie clearly below Up, so nothing past the band can displace them
+  if (nsel > kneed || n - nsel > kBndCap || n < kneed || nU < kneed) return false;
   for (int t = nsel; t < kneed; ++t) {
-    int bj = -1, bpp = -1;
-    double bdd = INFINITY;
-#pragma unroll
-    for (int j = 0; j < kBndCap; ++j) {
-      if (j < nb && !((used >> j) & 1u) && key_less(bd[j], bp[j], bdd, bpp, id)) {
-        bdd = bd[j];
-        bpp = bp[j];
+    int bj = t, bp = (int)lst[t][lane];
+    double bd = dist2_f64(qx, qy, qz, fetch(bp));
+    for (int j = t + 1; j < n; ++j) {
+      const int p = (int)lst[j][lane];
+      const double d = dist2_f64(qx, qy, qz, fetch(p));
+      if (key_less(d, p, bd, bp, id)) {
+        bd = d;
+        bp = p;
         bj = j;
       }
     }
-    used |= 1u << bj;
-    sel[t][lane] = (T)bpp;
-  }
-  // the smallest unselected band key
-  int up = -1;
-  double ud = INFINITY;
-#pragma unroll
-  for (int j = 0; j < kBndCap; ++j)
-    if (j < nb && !((used >> j) & 1u) && key_less(bd[j], bp[j], ud, up, id)) {
-      ud = bd[j];
-      up = bp[j];
-    }
-  MomAcc acc;
-  acc.zero();
-  int cp = -1;
-  double cd = -1.0;
-  for (int j = 0; j < kneed; ++j) {
-    const int p = (int)sel[j][lane];
-    const float4 v = fetch(p);
-    if (j < nsel) {
-      const double d = dist2_f64(qx, qy, qz, v);
-      if (cp < 0 || key_less(cd, cp, d, p, id)) {
-        cd = d;
-        cp = p;
-      }
-    }
+    lst[bj][lane] = lst[t][lane];
+    lst[t][lane] = (T)bp;
+    const float4 v = fetch(bp);
     acc.add((double)v.x, (double)v.y, (double)v.z);
   }
-  if (up >= 0 && cp >= 0 && !key_less(cd, cp, ud, up, id)) return false;  // rounding swapped the order
+  if (n > kneed && nsel > 0) {
+    int up = -1;
+    double ud = INFINITY;
+    for (int j = kneed; j < n; ++j) {
+      const int p = (int)lst[j][lane];
+      const double d = dist2_f64(qx, qy, qz, fetch(p));
+      if (key_less(d, p, ud, up, id)) {
+        ud = d;
+        up = p;
+      }
+    }
+    // certain keys are < Lm (1 + 2^-22) exactly; compare one by one only when that does not settle it
+    if (!(ud > (double)Lm * (1.0 + 1e-6))) {
+      for (int j = 0; j < nsel; ++j) {
+        const int p = (int)lst[j][lane];
+        if (!key_less(dist2_f64(qx, qy, qz, fetch(p)), p, ud, up, id)) return false;  // rounding swapped the order
+      }
+    }
+  }
+  if (skip_eigen) {  // profiling only (O3DX_TILE_DEBUG=4)
+    out[3 * oi] = (float)(acc.m[3] + acc.m[5] + acc.m[8]);
+    return true;
+  }
   finish_normal(kneed, acc, prior, oi, out);
   return true;
 }
@@ -829,19 +842,19 @@ template <int KMAX>
 __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
                                                              int kneed, const float* __restrict__ prior,
                                                              float* __restrict__ out, int32_t* __restrict__ fb_list,
-                                                             int32_t* __restrict__ fb_len) {
+                                                             int32_t* __restrict__ fb_len, int dbg) {
   static_assert(kTileQ == 64, "one wave per tile");
   __shared__ float tx[kTilePts], ty[kTilePts], tz[kTilePts];
   __shared__ int32_t ccs[kTileCs];
   __shared__ int32_t rows[kMaxTileRows + 1];
   __shared__ int32_t rst[kMaxTileRows];
-  // the selection list (u16 [KMAX][64]) and the histogram counters (u32
-  // [18][64]) share one LDS buffer: the histogram is dead before selection
-  constexpr int kSelWords = (KMAX * kTileQ * 2 + 3) / 4;
+  // the candidate list (u16 [KMAX + band + 1][64]) and the histogram counters
+  // (u32 [18][64]) share one LDS buffer: the histogram is dead before the list
+  constexpr int kListCap = KMAX + kBndCap + 1;  // last slot: write sink
+  constexpr int kListWords = (kListCap * kTileQ * 2 + 3) / 4;
   constexpr int kHistWords = kTileSlots * kTileQ;
-  __shared__ uint32_t selbuf[kSelWords > kHistWords ? kSelWords : kHistWords];
-  uint16_t(*sel)[kTileQ] = reinterpret_cast<uint16_t(*)[kTileQ]>(selbuf);
-  __shared__ uint16_t bnd[kBndCap][kTileQ];
+  __shared__ uint32_t selbuf[kListWords > kHistWords ? kListWords : kHistWords];
+  uint16_t(*lst)[kTileQ] = reinterpret_cast<uint16_t(*)[kTileQ]>(selbuf);
   const int lane = threadIdx.x;
   const int c = xcd_block(blockIdx.x, gridDim.x);
   const int q0 = chunk_starts[c], q1 = chunk_starts[c + 1];
@@ -877,12 +890,12 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
       __syncthreads();
       x_hi = x_lo + (x_hi - x_lo) / 2;
     }
-    if (active && !fb && cx >= x_lo && cx <= x_hi) {
+    if (active && !fb && cx >= x_lo && cx <= x_hi && dbg != 1) {
       fb = staged < 0;
       if (fb && g.stats) atomicAdd(&g.stats[6], 1ull);
-      int nsel = 0, nb = 0;
       if (!fb) {
-        const double R = (double)g.h + cell_margin(g, q.x, q.y, q.z, cx, cy, cz) - g.slack;
+        const double reach = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, 1);
+        const double R = (reach == INFINITY) ? (double)(g.nx + g.ny + g.nz) * g.h : reach - g.slack;
         const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
         uint32_t* hw = selbuf;
         TileHist th;
@@ -904,28 +917,24 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
           hi = U;
           O3DX_TILE_HIST(lo, (float)kHistBins / (hi - lo), hi)
         }
-        if (!fb) {
+        if (!fb && dbg != 2) {
           const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
-          int nU = 0;
-          // branch-free appends: every candidate is written to the next free
-          // slot of both lists and kept only where the count advances
+          // branch-free append of every candidate below Up: written to the
+          // next free slot, kept where the count advances
+          int n = 0;
           O3DX_TILE_SCAN(Up, {
-            nU += d2 < U ? 1 : 0;
-            sel[min(nsel, KMAX - 1)][lane] = (uint16_t)pp;
-            bnd[min(nb, kBndCap - 1)][lane] = (uint16_t)pp;
-            const bool in_ = d2 < Lm;
-            nsel += in_ ? 1 : 0;
-            nb += (!in_ && d2 < Up) ? 1 : 0;
+            lst[min(n, kListCap - 1)][lane] = (uint16_t)pp;
+            n += d2 < Up ? 1 : 0;
           })
-          // nU >= k: the k nearest lie clearly below Up, so nothing past the band can displace them
-          fb = nsel > kneed || nb > kBndCap || nsel + nb < kneed || nU < kneed;
+          if (dbg == 3) {
+            if (n == 12345) out[0] = 0.f;  // keep the scan alive
+          } else
+          fb = n >= kListCap ||
+               !finish_selection<KMAX>(
+                   q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
+                   [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, prior,
+                   __float_as_int(q.w), out, dbg == 4);
         }
-        if (!fb)
-          fb = !finish_selection<KMAX>(
-              q, kneed, nsel, nb, sel, bnd, lane,
-              [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
-              [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, prior,
-              __float_as_int(q.w), out);
       }
     }
     x_lo = x_hi + 1;
@@ -995,7 +1004,6 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   const float4 q = g.pts[s];
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
-  const double m = cell_margin(g, q.x, q.y, q.z, cx, cy, cz);
   const int rmax = shell_rmax(g, cx, cy, cz);
   bool fb = false;
   int S = 1;
@@ -1006,7 +1014,7 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
       fb = true;
       break;
     }
-    const double R = (double)S * g.h + m - g.slack;
+    const double R = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, S) - g.slack;
     if (R <= 0.0) continue;
     R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
     const float scale = (float)kHistBins / R2;
@@ -1162,7 +1170,6 @@ __global__ void __launch_bounds__(kBlock) k_normals_radius(GridView g, double ra
   const int oi = __float_as_int(q.w);
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
-  const double m = cell_margin(g, q.x, q.y, q.z, cx, cy, cz);
   const int rmax = shell_rmax(g, cx, cy, cz);
   const double r2 = radius * radius, qx = q.x, qy = q.y, qz = q.z;
   MomAcc acc;
@@ -1179,7 +1186,7 @@ __global__ void __launch_bounds__(kBlock) k_normals_radius(GridView g, double ra
         }
       }
     });
-    if ((double)r * g.h + m - g.slack >= radius) break;
+    if (cube_reach(g, qx, qy, qz, cx, cy, cz, r) - g.slack >= radius) break;
   }
   finish_normal(cnt, acc, prior, oi, out);
 }
@@ -1297,13 +1304,16 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
     // the wave form grid-strides over its list (at most n queries)
     const unsigned gw = (unsigned)std::min<int64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 8192);
     if (tiles) {
+      // O3DX_TILE_DEBUG=1/2/3: stop after staging / histogram / list scan (profiling only; wrong normals)
+      const char* dbg_env = getenv("O3DX_TILE_DEBUG");
+      const int dbg = dbg_env ? atoi(dbg_env) : 0;
       KTimer kt_tile("normals_tile", s);
       if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_tile<32>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
-                           kneed, prior, out, list1, lens);
+                           kneed, prior, out, list1, lens, dbg);
       else
         hipLaunchKernelGGL(k_normals_knn_tile<64>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
-                           kneed, prior, out, list1, lens);
+                           kneed, prior, out, list1, lens, dbg);
     }
     {
       KTimer kt_wave("normals_wave", s);

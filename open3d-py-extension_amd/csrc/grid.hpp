@@ -44,17 +44,6 @@ __device__ __forceinline__ void grid_cell(const GridView& g, float x, float y, f
   cz = clampi((int)floorf((z - g.oz) * g.inv_h), 0, g.nz - 1);
 }
 
-// signed distance from q to the faces of its (clamped) cell; negative when q
-// lies outside the grid box, which only makes the stop bound more conservative
-__device__ __forceinline__ double cell_margin(const GridView& g, float x, float y, float z, int cx, int cy,
-                                              int cz) {
-  double lx = (double)g.ox + (double)cx * g.h, ly = (double)g.oy + (double)cy * g.h,
-         lz = (double)g.oz + (double)cz * g.h;
-  double m = fmin(fmin((double)x - lx, lx + g.h - (double)x),
-                  fmin(fmin((double)y - ly, ly + g.h - (double)y), fmin((double)z - lz, lz + g.h - (double)z)));
-  return m;
-}
-
 // nanoflann L2_Adaptor::evalMetric (dim 3): ((dx*dx) + dy*dy) + dz*dz, double.
 __device__ __forceinline__ double dist2_f64(double qx, double qy, double qz, float4 p) {
   double dx = qx - (double)p.x, dy = qy - (double)p.y, dz = qz - (double)p.z;
@@ -118,6 +107,23 @@ __device__ __forceinline__ void for_points4(const GridView& g, int p0, int p1, F
   for (; p < p1; ++p) f(p, g.pts[p]);
 }
 
+// Completeness radius of the (2S+1)^3 cube around cell (cx,cy,cz): the
+// distance from q to the nearest cube face that has grid cells beyond it
+// (faces on the grid boundary have no points beyond them: the grid covers
+// every point, clamped).  Every point closer to q than this (minus the
+// rounding slack) lies in the cube.  +inf when the cube covers the grid.
+__device__ __forceinline__ double cube_reach(const GridView& g, double x, double y, double z, int cx, int cy, int cz,
+                                             int S) {
+  double r = INFINITY;
+  if (cx - S > 0) r = fmin(r, x - ((double)g.ox + (double)(cx - S) * g.h));
+  if (cx + S < g.nx - 1) r = fmin(r, ((double)g.ox + (double)(cx + S + 1) * g.h) - x);
+  if (cy - S > 0) r = fmin(r, y - ((double)g.oy + (double)(cy - S) * g.h));
+  if (cy + S < g.ny - 1) r = fmin(r, ((double)g.oy + (double)(cy + S + 1) * g.h) - y);
+  if (cz - S > 0) r = fmin(r, z - ((double)g.oz + (double)(cz - S) * g.h));
+  if (cz + S < g.nz - 1) r = fmin(r, ((double)g.oz + (double)(cz + S + 1) * g.h) - z);
+  return r;
+}
+
 __device__ __forceinline__ int shell_rmax(const GridView& g, int cx, int cy, int cz) {
   return max(max(max(cx, g.nx - 1 - cx), max(cy, g.ny - 1 - cy)), max(cz, g.nz - 1 - cz));
 }
@@ -141,7 +147,6 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
   if (g.n == 0 || kneed <= 0) return 0;
   int cx, cy, cz;
   grid_cell(g, qx, qy, qz, cx, cy, cz);
-  const double m = cell_margin(g, qx, qy, qz, cx, cy, cz);
   const int rmax = shell_rmax(g, cx, cy, cz);
   const double dqx = qx, dqy = qy, dqz = qz;
   const double r2lim = hybrid ? radius * radius : INFINITY;
@@ -186,7 +191,7 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
         }
       }
     });
-    const double B = (double)r * g.h + m - g.slack;
+    const double B = cube_reach(g, dqx, dqy, dqz, cx, cy, cz, r) - g.slack;
     if (cnt >= kneed && B > 0.0 && wd < B * B) break;
     if (hybrid && B >= radius) break;
   }
@@ -207,12 +212,9 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   }
   const float fx = (float)qx, fy = (float)qy, fz = (float)qz;
   int cx, cy, cz;
-  // queries may lie outside the grid box: clamp, and account for the overshoot
+  // queries may lie outside the grid box: clamped to the nearest cell (cube_reach
+  // only counts faces with cells beyond them, so the bound stays valid)
   grid_cell(g, fx, fy, fz, cx, cy, cz);
-  const double lx = (double)g.ox + (double)cx * g.h, ly = (double)g.oy + (double)cy * g.h,
-               lz = (double)g.oz + (double)cz * g.h;
-  double m = fmin(fmin(qx - lx, lx + g.h - qx), fmin(fmin(qy - ly, ly + g.h - qy), fmin(qz - lz, lz + g.h - qz)));
-  // outside the query's cell (clamped): m < 0 shrinks the bound, still valid
   const int rmax = shell_rmax(g, cx, cy, cz);
   const double r2lim = radius * radius;
   int st_cells = 0, st_cands = 0, r = 0;
@@ -247,7 +249,7 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   visit_cell(cx, cy, cz);
   for (;; ++r) {
     // every point within B of q has been visited (or pruned by the bound)
-    const double B = (double)r * g.h + m - g.slack;
+    const double B = cube_reach(g, qx, qy, qz, cx, cy, cz, r) - g.slack;
     if (B >= radius || r >= rmax) break;
     if (bi >= 0 && B > 0.0 && bd < B * B) break;
     const int rr = r + 1;
