@@ -973,40 +973,53 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Rows of the (2S+1)^3 cube; each row range is walked 64 candidates at a time
-// (uniform trip count: `valid` marks the lanes past the row end).
-#define O3DX_WAVE_SCAN(S, BODY)                                              \
-  {                                                                          \
-    const int x0_ = max(cx - (S), 0), x1_ = min(cx + (S), g.nx - 1);         \
-    for (int dz_ = -(S); dz_ <= (S); ++dz_) {                                \
-      const int z_ = cz + dz_;                                               \
-      if (z_ < 0 || z_ >= g.nz) continue;                                    \
-      for (int dy_ = -(S); dy_ <= (S); ++dy_) {                              \
-        const int y_ = cy + dy_;                                             \
-        if (y_ < 0 || y_ >= g.ny) continue;                                  \
-        const int rb_ = g.nx * (y_ + g.ny * z_);                             \
-        const int a_ = g.start[rb_ + x0_], e_ = g.start[rb_ + x1_ + 1];      \
-        for (int b_ = a_; b_ < e_; b_ += 64) {                               \
-          const int pp = b_ + lane;                                          \
-          const bool valid = pp < e_;                                        \
-          const float4 v_ = g.pts[valid ? pp : a_];                          \
-          const float d2 = dist2_f32(q, v_.x, v_.y, v_.z);                   \
-          BODY                                                               \
-        }                                                                    \
-      }                                                                      \
-    }                                                                        \
+// Rows of the (2S+1)^3 cube, four rows at a time: each lane loads one
+// candidate of each of the four rows (four independent loads in flight),
+// 64 candidates per row per step; `valid` marks lanes past a row's end.
+#define O3DX_WAVE_SCAN(S, BODY)                                                  \
+  {                                                                              \
+    const int x0_ = max(cx - (S), 0), x1_ = min(cx + (S), g.nx - 1);             \
+    const int side_ = 2 * (S) + 1;                                               \
+    for (int r0_ = 0; r0_ < side_ * side_; r0_ += 4) {                           \
+      int a_[4], e_[4];                                                          \
+      int len_ = 0;                                                              \
+      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+        const int r_ = r0_ + u_;                                                 \
+        const int z_ = cz + r_ / side_ - (S), y_ = cy + r_ % side_ - (S);        \
+        a_[u_] = e_[u_] = 0;                                                     \
+        if (r_ < side_ * side_ && z_ >= 0 && z_ < g.nz && y_ >= 0 && y_ < g.ny) { \
+          const int rb_ = g.nx * (y_ + g.ny * z_);                               \
+          a_[u_] = g.start[rb_ + x0_];                                           \
+          e_[u_] = g.start[rb_ + x1_ + 1];                                       \
+        }                                                                        \
+        len_ = max(len_, e_[u_] - a_[u_]);                                       \
+      }                                                                          \
+      for (int b_ = 0; b_ < len_; b_ += 64) {                                    \
+        float4 v_[4];                                                            \
+        _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                       \
+          const int p_ = a_[u_] + b_ + lane;                                     \
+          v_[u_] = g.pts[p_ < e_[u_] ? p_ : 0];                                  \
+        }                                                                        \
+        _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                       \
+          const int pp = a_[u_] + b_ + lane;                                     \
+          const bool valid = pp < e_[u_];                                        \
+          const float d2 = dist2_f32(q, v_[u_].x, v_[u_].y, v_[u_].z);           \
+          BODY                                                                   \
+        }                                                                        \
+      }                                                                          \
+    }                                                                            \
   }
 
 template <int KMAX>
 __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const float* __restrict__ prior,
                                            float* __restrict__ out, int64_t s, int lane, int32_t* sel, int32_t* bnd,
-                                           int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len) {
+                                           int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int s0) {
   const float4 q = g.pts[s];
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
   const int rmax = shell_rmax(g, cx, cy, cz);
   bool fb = false;
-  int S = 1;
+  int S = s0;
   float R2 = 0.f;
   RegHist<false> hist;
   for (;; ++S) {
@@ -1151,14 +1164,14 @@ template <int KMAX>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) k_normals_knn_wave(
     GridView g, int kneed, const float* __restrict__ prior, float* __restrict__ out,
     const int32_t* __restrict__ in_list, const int32_t* __restrict__ in_len, int32_t* __restrict__ fb_list,
-    int32_t* __restrict__ fb_len) {
+    int32_t* __restrict__ fb_len, int s0) {
   __shared__ int32_t sel[kWavesPerBlock][KMAX];
   __shared__ int32_t bnd[kWavesPerBlock][kWaveBnd];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t lim = in_list ? (int64_t)*in_len : g.n;
   for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wv; t < lim; t += (int64_t)gridDim.x * kWavesPerBlock) {
     const int64_t s = in_list ? (int64_t)__builtin_amdgcn_readfirstlane(in_list[t]) : t;
-    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], fb_list, fb_len);
+    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], fb_list, fb_len, s0);
   }
 }
 
@@ -1316,13 +1329,16 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
                            kneed, prior, out, list1, lens, dbg);
     }
     {
+      // the tiles hand on (almost only) queries whose k-th neighbour lies
+      // beyond the shell-1 radius: start those at shell 2
+      const int s0 = tiles ? 2 : 1;
       KTimer kt_wave("normals_wave", s);
       if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
-                           out, wl, wlen, list2, lens + 1);
+                           out, wl, wlen, list2, lens + 1, s0);
       else
         hipLaunchKernelGGL(k_normals_knn_wave<64>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
-                           out, wl, wlen, list2, lens + 1);
+                           out, wl, wlen, list2, lens + 1, s0);
     }
     O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed, 0,
                     radius, prior, out, list2, lens + 1);
