@@ -29,8 +29,15 @@ __global__ void __launch_bounds__(kBlock) k_count_nonzero(const int32_t* __restr
   int64_t local = 0;
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x)
     local += count[c] != 0;
+  __shared__ int64_t sh[kBlock / 64];
   local = wave_sum(local);
-  if (lane_id() == 0 && local) atomicAdd(out, (unsigned long long)local);
+  if (lane_id() == 0) sh[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += sh[w];
+    if (t) atomicAdd(out, (unsigned long long)t);
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_grid_scatter(const float* __restrict__ xyz, int64_t n,
@@ -198,7 +205,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
       // surface-like clouds: occupied cells are far denser than the box average
       unsigned long long occ = 0;
       O3DX_HIP(hipMemsetAsync(G.scratch, 0, sizeof(int64_t), s));
-      hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(nc, kBlock, 4096)), dim3(kBlock), 0, s, G.count, nc,
+      hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(nc, kBlock, 1024)), dim3(kBlock), 0, s, G.count, nc,
                          (unsigned long long*)G.scratch);
       O3DX_HIP(hipMemcpyAsync(&occ, G.scratch, sizeof(occ), hipMemcpyDeviceToHost, s));
       O3DX_HIP(hipStreamSynchronize(s));
@@ -230,81 +237,58 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
 
 
 // ------------------------------------------------------------- chunk plan
-__device__ __forceinline__ int query_row(const GridView& g, float4 v, const Mat4d& T, int useT) {
-  float x = v.x, y = v.y, z = v.z;
-  if (useT) {
-    const double* t = T.m;
-    const double X = v.x, Y = v.y, Z = v.z;
-    x = (float)(((t[0] * X + t[1] * Y) + t[2] * Z) + t[3]);
-    y = (float)(((t[4] * X + t[5] * Y) + t[6] * Z) + t[7]);
-    z = (float)(((t[8] * X + t[9] * Y) + t[10] * Z) + t[11]);
-  }
-  int cx, cy, cz;
-  grid_cell(g, x, y, z, cx, cy, cz);
-  return cy + g.ny * cz;
-}
-
-__global__ void __launch_bounds__(kBlock) k_row_flags(const float4* __restrict__ q, int64_t n, GridView g, Mat4d T,
-                                                      int useT, uint8_t* __restrict__ flags) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int r = query_row(g, q[i], T, useT);
-    flags[i] = (i == 0 || r != query_row(g, q[i - 1], T, useT)) ? 1 : 0;
-  }
-}
-
-__global__ void k_run_nchunks(const int32_t* __restrict__ run_start, int64_t R, int64_t n, int qcap,
+// Queries = the grid's own (cell-sorted) points, so the queries of grid row
+// k = (y, z) are the contiguous range [start[k nx], start[(k+1) nx]).  Each
+// row is cut into chunks of <= qcap queries; no host synchronisation: the
+// caller launches `upper` blocks, the slots past the real chunk count hold n
+// (empty chunks) and slot upper+1 holds the real count.
+__global__ void k_row_nchunks(const int32_t* __restrict__ start, int nx, int64_t rows, int qcap,
                               int32_t* __restrict__ nch) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= R) return;
-  const int64_t a = run_start[k], b = (k + 1 < R) ? run_start[k + 1] : n;
-  nch[k] = (int32_t)((b - a + qcap - 1) / qcap);
+  if (k >= rows) return;
+  const int32_t a = start[k * nx], b = start[(k + 1) * nx];
+  nch[k] = (b - a + qcap - 1) / qcap;
 }
 
-__global__ void k_emit_chunks(const int32_t* __restrict__ run_start, int64_t R, int64_t n, int qcap,
-                              const int32_t* __restrict__ offs, int32_t* __restrict__ chunk_starts) {
+__global__ void k_emit_chunks(const int32_t* __restrict__ start, int nx, int64_t rows, int qcap,
+                              const int32_t* __restrict__ offs, int64_t n, int64_t upper,
+                              int32_t* __restrict__ chunk_starts) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= R) return;
-  const int64_t a = run_start[k], b = (k + 1 < R) ? run_start[k + 1] : n;
-  int32_t o = offs[k];
-  for (int64_t p = a; p < b; p += qcap) chunk_starts[o++] = (int32_t)p;
-  if (k == R - 1) chunk_starts[offs[R]] = (int32_t)n;
-}
-
-size_t chunk_plan_ws_bytes(int64_t n) {
-  n = std::max<int64_t>(n, 1);
-  return Arena::align(n + 17) + 3 * Arena::align((n + 2) * 4) + Arena::align(scan_workspace_ints(n + 1) * 4 + 1) + 1024;
-}
-
-int chunk_plan(const float4* q, int64_t n, const GridView& g, const double* T, int qcap, int32_t* chunk_starts,
-               int64_t* nchunks, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (ws_bytes < chunk_plan_ws_bytes(n)) return fail(O3DX_ENOMEM, "chunk plan workspace too small");
-  if (n == 0) {
-    *nchunks = 0;
-    return 0;
+  if (k < rows) {
+    const int32_t a = start[k * nx], b = start[(k + 1) * nx];
+    int32_t o = offs[k];
+    for (int32_t p = a; p < b; p += qcap) chunk_starts[o++] = p;
   }
+  const int64_t total = offs[rows];
+  for (int64_t c = total + k; c <= upper; c += (int64_t)gridDim.x * blockDim.x) chunk_starts[c] = (int32_t)n;
+  if (k == 0) chunk_starts[upper + 1] = (int32_t)total;  // the real chunk count, for the launch
+}
+
+int64_t chunk_plan_upper(int64_t n, const GridView& g, int qcap) {
+  return (n + qcap - 1) / qcap + (int64_t)g.ny * g.nz;
+}
+
+size_t chunk_plan_ws_bytes(int64_t n, int64_t rows) {
+  rows = std::max<int64_t>(rows, 1);
+  (void)n;
+  return 2 * Arena::align((rows + 2) * 4) + Arena::align(scan_workspace_ints(rows + 1) * 4 + 1) + 1024;
+}
+
+int chunk_plan(int64_t n, const GridView& g, int qcap, int32_t* chunk_starts, void* ws, size_t ws_bytes,
+               hipStream_t s) {
+  const int64_t rows = (int64_t)g.ny * g.nz;
+  if (ws_bytes < chunk_plan_ws_bytes(n, rows)) return fail(O3DX_ENOMEM, "chunk plan workspace too small");
   Arena ar(ws, ws_bytes);
-  uint8_t* flags = ar.take<uint8_t>(n + 16);
-  int32_t* runs = ar.take<int32_t>(n + 1);
-  int32_t* nch = ar.take<int32_t>(n + 1);
-  int32_t* offs = ar.take<int32_t>(n + 1);
-  int32_t* tmp = ar.take<int32_t>(scan_workspace_ints(n + 1));
-  int64_t* cnt = ar.take<int64_t>(2);
-  Mat4d M;
-  for (int i = 0; i < 16; ++i) M.m[i] = T ? T[i] : ((i % 5 == 0) ? 1.0 : 0.0);
-  hipLaunchKernelGGL(k_row_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, q, n, g, M, T ? 1 : 0, flags);
-  O3DX_TRY(compact_flags(flags, n, runs, nullptr, cnt, tmp, s));
-  int64_t R = 0;
-  O3DX_HIP(hipMemcpyAsync(&R, cnt, sizeof(R), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
-  hipLaunchKernelGGL(k_run_nchunks, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, runs, R, n, qcap, nch);
-  O3DX_TRY(exclusive_scan_i32(nch, offs, R, tmp, s));
-  hipLaunchKernelGGL(k_emit_chunks, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, runs, R, n, qcap, offs,
+  int32_t* nch = ar.take<int32_t>(rows + 1);
+  int32_t* offs = ar.take<int32_t>(rows + 1);
+  int32_t* tmp = ar.take<int32_t>(scan_workspace_ints(rows + 1));
+  const int64_t upper = chunk_plan_upper(n, g, qcap);
+  const unsigned gr = (unsigned)((rows + 255) / 256);
+  hipLaunchKernelGGL(k_row_nchunks, dim3(gr), dim3(256), 0, s, g.start, g.nx, rows, qcap, nch);
+  O3DX_TRY(exclusive_scan_i32(nch, offs, rows, tmp, s));
+  hipLaunchKernelGGL(k_emit_chunks, dim3(gr), dim3(256), 0, s, g.start, g.nx, rows, qcap, offs, n, upper,
                      chunk_starts);
-  int32_t total = 0;
-  O3DX_HIP(hipMemcpyAsync(&total, offs + R, sizeof(total), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
   O3DX_HIP(hipGetLastError());
-  *nchunks = total;
   return 0;
 }
 
@@ -856,7 +840,11 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   __shared__ uint32_t selbuf[kListWords > kHistWords ? kListWords : kHistWords];
   uint16_t(*lst)[kTileQ] = reinterpret_cast<uint16_t(*)[kTileQ]>(selbuf);
   const int lane = threadIdx.x;
-  const int c = xcd_block(blockIdx.x, gridDim.x);
+  // the launch covers an upper bound of the chunk count; the real count sits
+  // after the list, and the XCD-contiguous mapping spans the real chunks only
+  const int nreal = chunk_starts[gridDim.x + 1];
+  if ((int)blockIdx.x >= nreal) return;
+  const int c = xcd_block(blockIdx.x, nreal);
   const int q0 = chunk_starts[c], q1 = chunk_starts[c + 1];
   const int64_t s = (int64_t)q0 + lane;
   const bool active = s < q1;
@@ -1277,7 +1265,10 @@ extern "C" int o3dx_search_stats(int64_t* out) {
 
 extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
   n = std::max<int64_t>(n, 1);
-  return grid_ws_bytes(n) + 4 * Arena::align((n + 3) * 4) + chunk_plan_ws_bytes(n) + 4096;
+  // grid rows (ny * nz) are bounded by the cell cap
+  const int64_t rows = cap_cells(n);
+  return grid_ws_bytes(n) + 3 * Arena::align((n + 3) * 4) + Arena::align((n / 64 + rows + 4) * 4) +
+         chunk_plan_ws_bytes(n, rows) + 4096;
 }
 
 extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,
@@ -1303,14 +1294,15 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
     int32_t* lens = ar.take<int32_t>(4);
     int32_t* list1 = ar.take<int32_t>(n);
     int32_t* list2 = ar.take<int32_t>(n);
-    int32_t* chunks = ar.take<int32_t>(n + 2);
-    void* pws = ar.take<char>(chunk_plan_ws_bytes(n));
+    const int64_t upper = chunk_plan_upper(n, G.view, kTileQ);
+    int32_t* chunks = ar.take<int32_t>(upper + 2);
+    const size_t pws_bytes = chunk_plan_ws_bytes(n, (int64_t)G.view.ny * G.view.nz);
+    void* pws = ar.take<char>(pws_bytes);
     O3DX_ARENA_CHECK(ar);
     O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
     const bool tiles = !getenv("O3DX_NORMALS_NO_TILES");
-    int64_t nchunks = 0;
-    if (tiles)
-      O3DX_TRY(chunk_plan(G.view.pts, n, G.view, nullptr, kTileQ, chunks, &nchunks, pws, chunk_plan_ws_bytes(n), s));
+    if (tiles) O3DX_TRY(chunk_plan(n, G.view, kTileQ, chunks, pws, pws_bytes, s));
+    const int64_t nchunks = upper;
     KTimer kt("normals_knn", s);
     const int32_t* wl = tiles ? list1 : nullptr;
     const int32_t* wlen = tiles ? lens : nullptr;

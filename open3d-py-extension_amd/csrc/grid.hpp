@@ -376,13 +376,14 @@ __device__ __forceinline__ void for_tile_rows(const TileBox& b, const int32_t* c
   }
 }
 
-// Chunk plan: split a spatially sorted query list into chunks of <= qcap
-// consecutive queries whose cells share one (y,z) row of grid g (cells of the
-// queries after transform T when `T` is non-null).  chunk_starts gets
-// nchunks+1 entries (last = n).  Synchronises (the chunk count sizes launches).
-size_t chunk_plan_ws_bytes(int64_t n);
-int chunk_plan(const float4* q, int64_t n, const GridView& g, const double* T, int qcap, int32_t* chunk_starts,
-               int64_t* nchunks, void* ws, size_t ws_bytes, hipStream_t s);
+// Chunk plan (normals tiles): the grid's own points, row by row, in chunks of
+// <= qcap consecutive queries of one (y,z) row.  chunk_starts needs
+// chunk_plan_upper()+2 entries; slots past the real count hold n.  Enqueues
+// only (no host synchronisation).
+int64_t chunk_plan_upper(int64_t n, const GridView& g, int qcap);
+size_t chunk_plan_ws_bytes(int64_t n, int64_t rows);
+int chunk_plan(int64_t n, const GridView& g, int qcap, int32_t* chunk_starts, void* ws, size_t ws_bytes,
+               hipStream_t s);
 
 // ---------------------------------------------------------------- build
 struct GridBuild {
