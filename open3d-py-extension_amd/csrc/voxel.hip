@@ -60,12 +60,24 @@ __global__ void __launch_bounds__(kBlock) k_voxel_assign_dense(const float* __re
     voxel_ref(p[i], g, r, v);
     if (v[0] < 0 || v[0] >= g.nx || v[1] < 0 || v[1] >= g.ny || v[2] < 0 || v[2] >= g.nz) {
       *err = 1;
-      vid[i] = 0;
+      vid[i] = -1;
       continue;
     }
     int32_t id = v[0] + g.nx * (v[1] + g.ny * v[2]);
     vid[i] = id;
-    atomicMax(&rep[id], (int32_t)i);
+    rep[id] = (int32_t)i;  // plain store: some index of the voxel wins (k_voxel_settle makes it the max)
+  }
+}
+
+// Second half of the dense assignment: the racy plain stores above left one of
+// each voxel's indices in the table; only points with a larger index need the
+// (device-scope, slow) atomicMax.  Grid-stride rounds run in index order, so
+// the last writer usually is already the maximum and few atomics remain.
+__global__ void __launch_bounds__(kBlock) k_voxel_settle(const int32_t* __restrict__ vid, int64_t n,
+                                                         int32_t* __restrict__ rep) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t id = vid[i];
+    if (id >= 0 && rep[id] < (int32_t)i) atomicMax(&rep[id], (int32_t)i);
   }
 }
 
@@ -249,6 +261,7 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
       KTimer kt("voxel_assign", s);
       hipLaunchKernelGGL(k_voxel_assign_dense, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.table, w.vid,
                          reinterpret_cast<int*>(w.count + 1));
+      hipLaunchKernelGGL(k_voxel_settle, dim3(grid), dim3(kBlock), 0, s, w.vid, n, w.table);
     } else {
       nslots = hash_cap(n);
       O3DX_HIP(hipMemsetAsync(w.table, 0xFF, nslots * sizeof(int32_t), s));
