@@ -53,12 +53,39 @@ __global__ void __launch_bounds__(kBlock) k_grid_scatter(const float* __restrict
   }
 }
 
-// deterministic in-cell order: ascending original index (atomic ranks are not)
+// Deterministic in-cell order (ascending original index; atomic ranks are
+// not): every point counts the points of its cell with a smaller index and
+// moves there — thread per point, O(cell size) reads each, all L2-local.
+// Cells above kRankCell points are copied as they are and sorted by
+// k_grid_cell_sort (serial insertion, only such cells).
+constexpr int kRankCell = 256;
+
+__global__ void __launch_bounds__(kBlock) k_grid_rank_fix(const float4* __restrict__ tmp,
+                                                          const float4* __restrict__ tmp_extra, int64_t n,
+                                                          const int32_t* __restrict__ cell,
+                                                          const int32_t* __restrict__ start, float4* __restrict__ pts,
+                                                          float4* __restrict__ extra) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = tmp[p];
+    const int i = __float_as_int(v.w);
+    const int c = cell[i];
+    const int s0 = start[c], s1 = start[c + 1];
+    int dst = (int)p;
+    if (s1 - s0 <= kRankCell) {
+      int r = 0;
+      for (int q = s0; q < s1; ++q) r += __float_as_int(tmp[q].w) < i ? 1 : 0;
+      dst = s0 + r;
+    }
+    pts[dst] = v;
+    if (extra) extra[dst] = tmp_extra[p];
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_grid_cell_sort(const int32_t* __restrict__ start, int64_t nc,
                                                            float4* __restrict__ pts, float4* __restrict__ extra) {
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
     int s0 = start[c], s1 = start[c + 1];
-    if (s1 - s0 < 2) continue;
+    if (s1 - s0 <= kRankCell) continue;
     for (int i = s0 + 1; i < s1; ++i) {
       float4 v = pts[i];
       float4 e = extra ? extra[i] : make_float4(0, 0, 0, 0);
@@ -78,7 +105,7 @@ __global__ void __launch_bounds__(kBlock) k_grid_cell_sort(const int32_t* __rest
 static int64_t cap_cells(int64_t n) { return std::max<int64_t>(4 * n, 4096); }
 
 struct GridLayout {
-  size_t pts, extra, count, start, cell, rank, scan, aabb, mm, scratch, total;
+  size_t pts, extra, tmp, tmp_extra, count, start, cell, rank, scan, aabb, mm, scratch, total;
 };
 
 static GridLayout grid_layout(int64_t n) {
@@ -93,6 +120,8 @@ static GridLayout grid_layout(int64_t n) {
   int64_t cc = cap_cells(n);
   L.pts = put(n * sizeof(float4));
   L.extra = put(n * sizeof(float4));
+  L.tmp = put(n * sizeof(float4));
+  L.tmp_extra = put(n * sizeof(float4));
   L.count = put((cc + 1) * sizeof(int32_t));
   L.start = put((cc + 1) * sizeof(int32_t));
   L.cell = put(n * sizeof(int32_t));
@@ -224,8 +253,12 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     KTimer kt_sort("grid_sort", s);
     O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));
     if (n > 0) {
+      float4* tmp = (float4*)(w + L.tmp);
+      float4* tmp_extra = extra_sorted ? (float4*)(w + L.tmp_extra) : nullptr;
       hipLaunchKernelGGL(k_grid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, G.cell, G.rank,
-                         G.start, G.pts, extra_src, extra_sorted);
+                         G.start, tmp, extra_src, tmp_extra);
+      hipLaunchKernelGGL(k_grid_rank_fix, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, tmp, tmp_extra, n,
+                         G.cell, G.start, G.pts, extra_sorted);
       hipLaunchKernelGGL(k_grid_cell_sort, dim3(grid_for(nc, kBlock, 8192)), dim3(kBlock), 0, s, G.start, nc, G.pts,
                          extra_sorted);
     }
