@@ -23,7 +23,7 @@
 
 namespace o3dx {
 
-constexpr int kPts = 4;
+constexpr int kPts = 8;
 constexpr int kHChunk = 1024;
 constexpr int kCountBlocksMax = 1024;
 
@@ -37,45 +37,72 @@ __device__ __forceinline__ double plane_dist64(const double* pl, double x, doubl
   return fabs((ax + cz) + (by + dw));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// One block sweeps tiles of kBlock * kPts points against hypotheses
+// [h0, h0 + hc).  Points past n are NaN (every comparison false, no masks).
+// The next hypothesis' coefficients are loaded while the current one is
+// evaluated; distances of two points per packed FMA.
 __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict__ xyz, int64_t n,
                                                         const float4* __restrict__ pl32,
                                                         const float2* __restrict__ band,
                                                         const double* __restrict__ pl64, int H, int h0, int hc,
                                                         double thr, int32_t* __restrict__ partial) {
+  static_assert(kPts % 2 == 0, "points are processed in pairs");
+  constexpr int kPairs = kPts / 2;
   __shared__ int cnt[kHChunk];
   for (int h = threadIdx.x; h < hc; h += kBlock) cnt[h] = 0;
   __syncthreads();
   const P3* p = reinterpret_cast<const P3*>(xyz);
   const int64_t tile = (int64_t)kBlock * kPts;
+  const float qnan = __int_as_float(0x7fc00000);
   for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {
-    float px[kPts], py[kPts], pz[kPts];
-    bool ok[kPts];
+    f32x2 X[kPairs], Y[kPairs], Z[kPairs];
 #pragma unroll
-    for (int j = 0; j < kPts; ++j) {
-      int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
-      ok[j] = i < n;
-      P3 q = ok[j] ? p[i] : P3{0.f, 0.f, 0.f};
-      px[j] = q.x;
-      py[j] = q.y;
-      pz[j] = q.z;
+    for (int k = 0; k < kPairs; ++k) {
+      const int64_t i0 = base + (int64_t)(2 * k) * kBlock + threadIdx.x, i1 = i0 + kBlock;
+      const P3 a = i0 < n ? p[i0] : P3{qnan, qnan, qnan};
+      const P3 b = i1 < n ? p[i1] : P3{qnan, qnan, qnan};
+      X[k] = (f32x2){a.x, b.x};
+      Y[k] = (f32x2){a.y, b.y};
+      Z[k] = (f32x2){a.z, b.z};
     }
+    float4 P = pl32[h0];
+    float2 B = band[h0];
     for (int h = 0; h < hc; ++h) {
-      const float4 P = pl32[h0 + h];
-      const float2 B = band[h0 + h];
+      const int hn = (h + 1 < hc) ? h + 1 : h;
+      const float4 Pn = pl32[h0 + hn];
+      const float2 Bn = band[h0 + hn];
       int wc = 0;
+      uint64_t ambw = 0ull;  // wave-level: some lane has a point inside the ambiguity band
 #pragma unroll
-      for (int j = 0; j < kPts; ++j) {
-        const float d = fabsf(fmaf(P.x, px[j], fmaf(P.y, py[j], fmaf(P.z, pz[j], P.w))));
-        const bool in = ok[j] && d < B.x;
-        const bool amb = ok[j] && !in && d < B.y;
-        wc += __popcll(__ballot(in));
-        if (__ballot(amb)) {
-          bool ex = false;
-          if (amb) ex = plane_dist64(pl64 + 4 * (h0 + h), px[j], py[j], pz[j]) < thr;
-          wc += __popcll(__ballot(ex));
+      for (int k = 0; k < kPairs; ++k) {
+        const f32x2 d = __builtin_elementwise_fma(
+            (f32x2){P.x, P.x}, X[k],
+            __builtin_elementwise_fma((f32x2){P.y, P.y}, Y[k],
+                                      __builtin_elementwise_fma((f32x2){P.z, P.z}, Z[k], (f32x2){P.w, P.w})));
+        const float e0 = fabsf(d.x), e1 = fabsf(d.y);
+        const uint64_t l0 = __ballot(e0 < B.x), l1 = __ballot(e1 < B.x);
+        wc += __popcll(l0) + __popcll(l1);
+        ambw |= (__ballot(e0 < B.y) & ~l0) | (__ballot(e1 < B.y) & ~l1);
+      }
+      if (ambw) {  // rare: re-decide band points in float64, Open3D's order
+        const double* pl = pl64 + 4 * (h0 + h);
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+          const f32x2 d = __builtin_elementwise_fma(
+              (f32x2){P.x, P.x}, X[k],
+              __builtin_elementwise_fma((f32x2){P.y, P.y}, Y[k],
+                                        __builtin_elementwise_fma((f32x2){P.z, P.z}, Z[k], (f32x2){P.w, P.w})));
+          const float e0 = fabsf(d.x), e1 = fabsf(d.y);
+          const bool x0 = !(e0 < B.x) && e0 < B.y && plane_dist64(pl, X[k].x, Y[k].x, Z[k].x) < thr;
+          const bool x1 = !(e1 < B.x) && e1 < B.y && plane_dist64(pl, X[k].y, Y[k].y, Z[k].y) < thr;
+          wc += __popcll(__ballot(x0)) + __popcll(__ballot(x1));
         }
       }
       if (lane_id() == 0 && wc) atomicAdd(&cnt[h], wc);
+      P = Pn;
+      B = Bn;
     }
   }
   __syncthreads();
