@@ -55,16 +55,18 @@ def parse():
     ap.add_argument("--icp-iters", type=int, default=30)
     ap.add_argument("--ransac-iters", type=int, default=1000)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--dist-icp", action="store_true",
+                    help="also run the sharded-ICP leg (RCCL) when world == 1 (under torchrun)")
     return ap.parse_args()
 
 
-def setup_dist():
+def setup_dist(force=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or (force and "MASTER_PORT" in os.environ):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     return world, rank, dev
@@ -84,15 +86,15 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def pmc_traffic(path, kernel):
-    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary."""
+def pmc_entry(path, kernel):
+    """Per-launch PMC figures of `kernel` from the committed rocprofv3 summary
+    (tools/pmc.sh + tools/pmc_summary.py): HBM bytes, VALU-issue floor."""
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get("kernels", {}).get(kernel)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError, TypeError):
-        return None
+        return d.get("kernels", {}).get(kernel) or {}
+    except (OSError, ValueError, TypeError):
+        return {}
 
 
 def cpu_baseline(n_cpu: int):
@@ -178,9 +180,37 @@ def secondary(dev, args):
     return out
 
 
+def secondary_sharded_icp(dev, args, world, rank):
+    """C3/C5-style ICP with the source sharded over the ranks (strong scaling of
+    one 10M source) and the target replicated; the 29 float64 moments are
+    all-gathered over RCCL once per iteration (open3dpypro.distributed)."""
+    from open3dpypro import distributed as D
+
+    n = args.icp_n
+    tgt = synthetic.box_surface(n, seed=1, device=dev)
+    src = synthetic.apply_transform(synthetic.box_surface(n, seed=2, device=dev), synthetic.rigid_transform())
+    target = ops.ICPTarget(tgt, ops.estimate_normals(tgt, knn=30), 0.02)
+    a, b = D.shard_range(n, world, rank)
+    shard = ops.spatial_sort(src[a:b].contiguous())
+    del src
+    acc = lambda T: target.accumulate(shard, T)[0]  # noqa: E731
+    D.registration_icp_point_to_plane(acc, n, max_iteration=1)  # warm
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    T, fit, rm = D.registration_icp_point_to_plane(acc, n, max_iteration=args.icp_iters, relative_fitness=0.0,
+                                                   relative_rmse=0.0)
+    barrier(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    err = float(np.abs(T - np.linalg.inv(synthetic.rigid_transform())).max())
+    return {"icp_sharded": {"n_source": n, "n_target": n, "ranks": world, "iterations": args.icp_iters,
+                            "iters_per_s": round(args.icp_iters / el, 3), "fitness": round(fit, 6),
+                            "T_err_vs_gt_inverse": err,
+                            "collective": "all_gather of 32 float64 per iteration (RCCL), summed in rank order"}}
+
+
 def main():
     args = parse()
-    world, rank, dev = setup_dist()
+    world, rank, dev = setup_dist(args.dist_icp)
     N = args.n
     vs = synthetic.voxel_size_for(N)
     # this rank's tile: an independent 10M cloud, shifted to x in [rank, rank+1)
@@ -226,11 +256,16 @@ def main():
     if dom is not None:
         avg_s = kernels[dom]["avg_ms"] * 1e-3
         ach = algo_bytes[dom] / avg_s / 1e9
-        traffic = pmc_traffic(args.pmc_json, dom)
+        pmc = pmc_entry(args.pmc_json, dom)
+        traffic = pmc.get("hbm_bytes_per_launch")
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "algorithmic_bytes_per_launch": algo_bytes[dom],
                 "note": "kNN selection is VALU/LDS-issue bound, not HBM bound: see DESIGN.md (Roofline)"}
+        if pmc.get("valu_issue_floor_ms"):
+            # the bound that actually applies: VALU issue (PMC SQ_INSTS_VALU x 4 cycles / 1024 SIMDs @ 2.4 GHz)
+            roof["valu_issue_floor_ms"] = round(pmc["valu_issue_floor_ms"], 4)
+            roof["valu_issue_frac"] = round(pmc["valu_issue_floor_ms"] / kernels[dom]["avg_ms"], 4)
 
     total_pts = float(N) * world * args.steps
     value = total_pts / elapsed / 1e6
@@ -248,11 +283,16 @@ def main():
                   "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps * world / elapsed / 1e9, 2),
                   "storage_dtype": "f32", "arith": "float64 voxel keys / distances / covariance"},
     }
+    del pts
+    torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_secondary:
-        del pts
-        torch.cuda.empty_cache()
         try:
             line["extra"].update(secondary(dev, args))
+        except RuntimeError as e:  # report, never hide
+            line["extra"]["secondary_error"] = str(e)
+    if (world > 1 or args.dist_icp) and not args.no_secondary:
+        try:
+            line["extra"].update(secondary_sharded_icp(dev, args, world, rank))
         except RuntimeError as e:  # report, never hide
             line["extra"]["secondary_error"] = str(e)
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -261,7 +301,7 @@ def main():
             line["extra"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

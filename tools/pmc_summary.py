@@ -39,6 +39,13 @@ def main(src, out):
         e = {c: sum(v) / len(v) for c, v in d.items()}
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
             e["hbm_bytes_per_launch"] = 2.0 * e["FETCH_SIZE"] * 1024 + e["WRITE_SIZE"] * 1024
+        if "SQ_INSTS_VALU" in e and "SQ_WAVES" in e:
+            # VALU-issue floor: one wave64 VALU instruction per SIMD per 4 cycles,
+            # 1024 SIMDs (256 CUs x 4) at the 2.4 GHz peak engine clock
+            e["valu_insts_per_wave"] = e["SQ_INSTS_VALU"] / e["SQ_WAVES"]
+            e["valu_issue_floor_ms"] = e["SQ_INSTS_VALU"] * 4.0 / (1024 * 2.4e9) * 1e3
+        if "SQ_ACTIVE_INST_VALU" in e and "SQ_WAVE_CYCLES" in e:
+            e["valu_active_frac_of_wave_cycles"] = e["SQ_ACTIVE_INST_VALU"] / e["SQ_WAVE_CYCLES"]
         e["launches_sampled"] = max(len(v) for v in d.values())
         res["kernels"][k] = e
     with open(out, "w") as f:
