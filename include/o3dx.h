@@ -79,12 +79,13 @@ int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches);
 /* Debug-only neighbour-search statistics: when enabled, every grid search
  * (normals, kNN, ICP) adds {queries, cells visited, candidate points, shells}
  * into device counters, and the KNN-normals levels count the queries they
- * hand on {tile -> global histogram, global histogram -> register top-k};
- * o3dx_search_stats copies those six counters out (synchronises the device).
+ * hand on {tile -> wave form, wave form -> register top-k} and why the tile
+ * gave up {box over LDS capacity, too few points within the shell-1 radius};
+ * o3dx_search_stats copies those eight counters out (synchronises the device).
  * Enabling allocates a 64-byte device buffer — the only device allocation the
  * library ever makes; off by default. */
 int o3dx_set_search_stats(int enable);
-int o3dx_search_stats(int64_t* out6_host);
+int o3dx_search_stats(int64_t* out8_host);
 
 /* ---------------------------------------------------------------- AABB
  * Replaces o3d.geometry.PointCloud.get_min_bound()/get_max_bound()
@@ -225,10 +226,12 @@ int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
  * o3dx_icp_target_build: builds the persistent target structure (spatial grid
  *   of target points + normals) inside `target_ws`; desc_host (16 doubles)
  *   receives its descriptor, to be passed back to o3dx_icp_accumulate.
- * o3dx_spatial_sort: (n,4) float32 copy of a cloud ordered by spatial grid
- *   cell, w = bits of the original int32 index.  ICP sources are passed in
- *   this layout (src_sorted4 = 1) so that the 64 queries of a wave probe
- *   neighbouring target cells; results are reported by original index.
+ * o3dx_spatial_sort: (n,4) float32 copy of a cloud in a compact spatial order
+ *   (grid cells of ~target_occ points, 8x8x8 blocks of cells, Morton order
+ *   inside a block), w = bits of the original int32 index.  ICP sources are
+ *   passed in this layout (src_sorted4 = 1) so that 64 consecutive queries
+ *   form a compact patch (one LDS tile of target points); results are
+ *   reported by original index.
  * o3dx_icp_accumulate: one fused pass over the source: transform by T_host
  *   (row-major 4x4, float64), 1-NN, residual/Jacobian, fixed-order float64
  *   reduction into sums_host[O3DX_ICP_NSUMS].  corr_out_dev (nullable, 2*ns

@@ -18,7 +18,7 @@ __global__ void __launch_bounds__(kBlock) k_grid_count(const float* __restrict__
     float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
     int cx, cy, cz;
     grid_cell(g, x, y, z, cx, cy, cz);
-    int c = cx + g.nx * (cy + g.ny * cz);
+    const int c = cell_index(g, cx, cy, cz);
     cell[i] = c;
     rank[i] = atomicAdd(&count[c], 1);
   }
@@ -146,8 +146,14 @@ static void dims_for(const double mn[3], const double mx[3], double h, int64_t d
   for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor(std::max(0.0, mx[a] - mn[a]) / h) + 1;
 }
 
+// size of the cell index space for dims d
+static int64_t cell_space(const int64_t d[3], bool blocked) {
+  if (!blocked) return d[0] * d[1] * d[2];
+  return ((d[0] + 7) / 8) * ((d[1] + 7) / 8) * ((d[2] + 7) / 8) * 512;
+}
+
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
-               hipStream_t s, GridBuild* out, float4* extra_sorted, const float* extra_src) {
+               hipStream_t s, GridBuild* out, float4* extra_sorted, const float* extra_src, bool blocked) {
   GridLayout L = grid_layout(n);
   if (ws_bytes < L.total) return fail(O3DX_ENOMEM, "grid workspace too small (need %zu)", L.total);
   char* w = (char*)ws;
@@ -198,7 +204,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     int64_t d[3];
     for (int guard = 0; guard < 64; ++guard) {
       dims_for(mn, mx, hh, d);
-      double cells = (double)d[0] * d[1] * d[2];
+      double cells = (double)cell_space(d, blocked);
       if (cells <= (double)G.cap_cells) break;
       hh *= std::cbrt(cells / (double)G.cap_cells) * 1.01;
     }
@@ -224,7 +230,10 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     g.stats = search_stats_ptr();
     // assignment error of a float32 cell computation, both sides of a face
     g.slack = (float)(32.0 * std::ldexp(1.0, -24) * (maxabs + maxext) + 1e-6 * h);
-    const int64_t nc = d[0] * d[1] * d[2];
+    g.blocked = blocked ? 1 : 0;
+    g.bnx = (int)((d[0] + 7) / 8);
+    g.bny = (int)((d[1] + 7) / 8);
+    const int64_t nc = cell_space(d, blocked);
     KTimer kt_count("grid_count", s);
     O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
     if (n > 0)
@@ -618,10 +627,6 @@ struct RegHist {
   }
 };
 
-__device__ __forceinline__ float dist2_f32(const float4 q, float x, float y, float z) {
-  const float dx = q.x - x, dy = q.y - y, dz = q.z - z;
-  return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-}
 
 // Locate the bin of the k-th distance in a histogram over [lo, hi) with
 // `below` points known below lo.  -> bin edges [*L, *U), *cum = points in the

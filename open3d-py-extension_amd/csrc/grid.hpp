@@ -24,7 +24,22 @@ struct GridView {
   int nx, ny, nz;
   int64_t n;
   unsigned long long* stats;  // debug: {queries, cells visited, candidates, shells}; null = off
+  int blocked;                // cell order: 0 = row-major (x fastest; searchable), 1 = 8^3 blocks
+  int bnx, bny;               // blocked order: number of blocks along x, y
 };
+
+// Cell index.  Row-major (x fastest) keeps every (y,z) row contiguous, which
+// the searches rely on.  The blocked order (spatial_sort only) lists 8x8x8
+// blocks row-major and the cells of a block in Morton order, so consecutive
+// points form compact 3-D patches on any surface.
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 3 bits -> every third bit
+  return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4);
+}
+__device__ __forceinline__ int cell_index(const GridView& g, int cx, int cy, int cz) {
+  if (!g.blocked) return cx + g.nx * (cy + g.ny * cz);
+  const int b = (cx >> 3) + g.bnx * ((cy >> 3) + g.bny * (cz >> 3));
+  return (b << 9) | (int)(spread3(cx & 7) | (spread3(cy & 7) << 1) | (spread3(cz & 7) << 2));
+}
 
 __device__ __forceinline__ void search_stats(const GridView& g, int cells, int cands, int shells) {
   if (g.stats) {
@@ -42,6 +57,12 @@ __device__ __forceinline__ void grid_cell(const GridView& g, float x, float y, f
   cx = clampi((int)floorf((x - g.ox) * g.inv_h), 0, g.nx - 1);
   cy = clampi((int)floorf((y - g.oy) * g.inv_h), 0, g.ny - 1);
   cz = clampi((int)floorf((z - g.oz) * g.inv_h), 0, g.nz - 1);
+}
+
+// float32 squared distance (filtering only; decisions are made in float64)
+__device__ __forceinline__ float dist2_f32(const float4 q, float x, float y, float z) {
+  const float dx = q.x - x, dy = q.y - y, dz = q.z - z;
+  return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
 }
 
 // nanoflann L2_Adaptor::evalMetric (dim 3): ((dx*dx) + dy*dy) + dz*dz, double.
@@ -218,18 +239,25 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   const int rmax = shell_rmax(g, cx, cy, cz);
   const double r2lim = radius * radius;
   int st_cells = 0, st_cands = 0, r = 0;
-  // Cells are visited shell by shell, each only if its box (shrunk by the
-  // rounding slack) can hold a point that beats the current best (or lies
-  // inside the radius while there is none): a lower bound, so the result is
-  // the exact lexicographic (d^2, index) minimum.
+  // Cells are visited shell by shell.  Everything is filtered in float32
+  // against thr, a float32 bound that every point beating the current best
+  // (or lying inside the radius while there is none) stays below: the float32
+  // distance of a point is within delta = slack of its exact distance, so
+  // thr = (sqrt(best) + 2 delta)^2.  Only candidates below thr are compared
+  // in float64 — the exact lexicographic (d^2, index) minimum is kept.  A
+  // cell is skipped when the float32 lower bound of its box (shrunk by 3
+  // delta per axis) reaches thr.
+  const float4 qf = make_float4(fx, fy, fz, 0.f);
+  const double dl = 2.0 * (double)g.slack;
+  auto bound_of = [&](double dist) { return (float)((dist + dl) * (dist + dl) * (1.0 + 1e-6)); };
+  float thr = bound_of(radius);
+  const float sl3 = 3.0f * g.slack;
   auto visit_cell = [&](int x, int y, int z) {
-    const double bx0 = (double)g.ox + (double)x * g.h, by0 = (double)g.oy + (double)y * g.h,
-                 bz0 = (double)g.oz + (double)z * g.h;
-    const double ex = fmax(fmax(bx0 - qx, qx - (bx0 + g.h)) - g.slack, 0.0);
-    const double ey = fmax(fmax(by0 - qy, qy - (by0 + g.h)) - g.slack, 0.0);
-    const double ez = fmax(fmax(bz0 - qz, qz - (bz0 + g.h)) - g.slack, 0.0);
-    const double lb = (ex * ex + ey * ey) + ez * ez;
-    if (lb > (bi >= 0 ? bd : r2lim)) return;
+    const float bx0 = g.ox + (float)x * g.h, by0 = g.oy + (float)y * g.h, bz0 = g.oz + (float)z * g.h;
+    const float ex = fmaxf(fmaxf(bx0 - fx, fx - (bx0 + g.h)) - sl3, 0.0f);
+    const float ey = fmaxf(fmaxf(by0 - fy, fy - (by0 + g.h)) - sl3, 0.0f);
+    const float ez = fmaxf(fmaxf(bz0 - fz, fz - (bz0 + g.h)) - sl3, 0.0f);
+    if (fmaf(ez, ez, fmaf(ey, ey, ex * ex)) >= thr) return;
     const int c = x + g.nx * (y + g.ny * z);
     const int p0 = g.start[c], p1 = g.start[c + 1];
     if (g.stats) {
@@ -237,12 +265,15 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
       st_cands += p1 - p0;
     }
     for_points4(g, p0, p1, [&](int p, const float4 v) {
-      const double d = dist2_f64(qx, qy, qz, v);
-      const int oi = __float_as_int(v.w);
-      if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
-        bd = d;
-        bi = oi;
-        bp = p;
+      if (dist2_f32(qf, v.x, v.y, v.z) < thr) {
+        const double d = dist2_f64(qx, qy, qz, v);
+        const int oi = __float_as_int(v.w);
+        if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
+          bd = d;
+          bi = oi;
+          bp = p;
+          thr = bound_of(sqrt(d));
+        }
       }
     });
   };
@@ -407,6 +438,7 @@ unsigned long long* search_stats_ptr();  // device counters when stats are enabl
 // target_occ: desired mean points per occupied cell.  min_h: lower bound on h
 // (0 = none).  Synchronises the stream (cell size is chosen on the host).
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
-               hipStream_t s, GridBuild* out, float4* extra_sorted = nullptr, const float* extra_src = nullptr);
+               hipStream_t s, GridBuild* out, float4* extra_sorted = nullptr, const float* extra_src = nullptr,
+               bool blocked = false);
 
 }  // namespace o3dx

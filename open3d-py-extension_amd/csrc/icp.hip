@@ -26,9 +26,34 @@ struct Mat4 {
   double m[16];
 };
 
-// SORTED: src is float4 (x, y, z, bits(original index)) in spatial (grid-cell)
-// order, so the 64 queries of a wave probe neighbouring target cells; else
-// plain (n,3) float32 in caller order.
+// One correspondence into the 30 float64 moments: r = (vs - vt).nt,
+// J = [vs x nt ; nt] (Open3D ComputeJTJandJTr order), plus count and d^2.
+__device__ __forceinline__ void icp_add(double acc[30], double px, double py, double pz, const float4 vt,
+                                        const float4 nt, double d2) {
+  const double nx = nt.x, ny = nt.y, nz = nt.z;
+  const double r = ((px - (double)vt.x) * nx + (py - (double)vt.y) * ny) + (pz - (double)vt.z) * nz;
+  double J[6];
+  J[0] = py * nz - pz * ny;
+  J[1] = pz * nx - px * nz;
+  J[2] = px * ny - py * nx;
+  J[3] = nx;
+  J[4] = ny;
+  J[5] = nz;
+  int k = 0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = a; b < 6; ++b) acc[k++] += J[a] * J[b];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
+  acc[27] += r * r;
+  acc[28] += 1.0;
+  acc[29] += d2;
+}
+
+// SORTED: src is float4 (x, y, z, bits(original index)) in the compact spatial
+// order of o3dx_spatial_sort, so the 64 queries of a wave probe neighbouring
+// target cells; else plain (n,3) float32 in caller order.
 template <bool SORTED>
 __global__ void __launch_bounds__(kBlock) k_icp_accumulate(const float* __restrict__ src, int64_t ns, GridView g,
                                                            const float4* __restrict__ tnorm, Mat4 T, double radius,
@@ -62,27 +87,7 @@ __global__ void __launch_bounds__(kBlock) k_icp_accumulate(const float* __restri
     const int tj = nn_search_dev(g, px, py, pz, radius, &d2, &pos);
     if (cj) cj[i] = tj;
     if (tj < 0) continue;
-    const float4 vt = g.pts[pos];
-    const float4 nt = tnorm[pos];
-    const double nx = nt.x, ny = nt.y, nz = nt.z;
-    const double r = ((px - (double)vt.x) * nx + (py - (double)vt.y) * ny) + (pz - (double)vt.z) * nz;
-    double J[6];
-    J[0] = py * nz - pz * ny;
-    J[1] = pz * nx - px * nz;
-    J[2] = px * ny - py * nx;
-    J[3] = nx;
-    J[4] = ny;
-    J[5] = nz;
-    int k = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-      for (int b = a; b < 6; ++b) acc[k++] += J[a] * J[b];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
-    acc[27] += r * r;
-    acc[28] += 1.0;
-    acc[29] += d2;
+    icp_add(acc, px, py, pz, g.pts[pos], tnorm[pos], d2);
   }
 #pragma unroll
   for (int k = 0; k < 30; ++k) {
@@ -216,6 +221,8 @@ static bool desc_unpack(const double* d, const void* base, GridView* g, const fl
   g->slack = (float)d[5];
   g->nx = (int)d[6]; g->ny = (int)d[7]; g->nz = (int)d[8]; g->n = (int64_t)d[9];
   g->stats = search_stats_ptr();
+  g->blocked = 0;
+  g->bnx = g->bny = 0;
   g->pts = (const float4*)((const char*)base + (int64_t)d[10]);
   g->start = (const int32_t*)((const char*)base + (int64_t)d[11]);
   *normals = (const float4*)((const char*)base + (int64_t)d[12]);
@@ -338,7 +345,8 @@ extern "C" int o3dx_spatial_sort(const float* xyz, int64_t n, double target_occ,
   if (n == 0) return 0;
   hipStream_t s = as_stream(stream);
   GridBuild G;
-  O3DX_TRY(grid_build(xyz, n, target_occ > 0 ? target_occ : 8.0, 0.0, ws, ws_bytes, s, &G));
+  O3DX_TRY(grid_build(xyz, n, target_occ > 0 ? target_occ : 8.0, 0.0, ws, ws_bytes, s, &G, nullptr, nullptr,
+                      /*blocked=*/true));
   O3DX_HIP(hipMemcpyAsync(sorted4, G.pts, (size_t)n * sizeof(float4), hipMemcpyDeviceToDevice, s));
   return 0;
 }

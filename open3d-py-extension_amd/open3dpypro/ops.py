@@ -260,8 +260,9 @@ class ICPTarget:
 
 
 def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
-    """(n,4) float32 copy of the cloud ordered by grid cell; column 3 holds the
-    original int32 index bits (o3dx_spatial_sort)."""
+    """(n,4) float32 copy of the cloud in a compact spatial order (8^3 blocks of
+    grid cells, Morton order inside a block); column 3 holds the original
+    int32 index bits (o3dx_spatial_sort)."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
