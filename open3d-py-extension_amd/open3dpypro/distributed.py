@@ -11,7 +11,10 @@ algorithm itself exchanges:
   * RANSAC: per-hypothesis integer counts, summed exactly (`allreduce_counts`);
   * ICP: the 29 float64 moments per iteration, all-gathered and summed in
     rank order, so every rank solves the same 6x6 system to the same bits
-    (`allreduce_icp_sums`, `registration_icp_point_to_plane`).
+    (`allreduce_icp_sums`, `registration_icp_point_to_plane`);
+  * voxel + normals of one cloud over x-slabs (C4): points to their slab
+    owner, then one halo exchange of the representatives near each slab face
+    (`voxel_normals_slabs`).
 
 Every function takes an optional process group; with no initialised process
 group they degrade to the single-process identity.
@@ -133,6 +136,114 @@ def registration_icp_point_to_plane(accumulate: Callable[[np.ndarray], np.ndarra
     return T, fit, rm
 
 
+def _exchange(dest: torch.Tensor, world: int, group, *tensors):
+    """all_to_all of the rows of each tensor to rank dest[i] (rows keep their
+    relative order per source rank; sources are concatenated in rank order)."""
+    cd = _comm_device(group)
+    order = torch.argsort(dest, stable=True)
+    send = torch.bincount(dest, minlength=world).to(torch.int64).to(cd)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    ss, rs = send.tolist(), recv.tolist()
+    out = []
+    for t in tensors:
+        src = t[order].contiguous().to(cd)
+        dst = torch.empty((sum(rs),) + tuple(t.shape[1:]), dtype=t.dtype, device=cd)
+        dist.all_to_all_single(dst, src, output_split_sizes=rs, input_split_sizes=ss, group=group)
+        out.append(dst.to(t.device))
+    return out
+
+
+def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float, knn: int = 30, group=None,
+                        voxel_fn=None, normals_fn=None, kdist_fn=None, halo: Optional[float] = None):
+    """C4: voxel_down_sample + estimate_normals(KNN) of one cloud spread over
+    the ranks, decomposed into x-slabs aligned to the global voxel grid.
+
+    `xyz` (n,3) float32 and `gidx` (n,) int64 global point indices are this
+    rank's (arbitrary) share of the cloud.  Steps: global AABB (all-reduce);
+    points to their slab owner (all-to-all); local voxel reps with the GLOBAL
+    bounds, rows kept in global-index order so the max-index rep and every
+    index tie-break equal the single-GPU ones; reps within `halo` of a slab
+    face to the neighbour rank (all-to-all: the one exchange of this path);
+    normals on own + halo reps.  The halo is verified (every own rep's k-th
+    neighbour distance minus its distance to the face stays below the halo)
+    and doubled until it holds.  Returns (rep global indices ascending, rep
+    xyz, normals) of this rank's slab; the union over ranks is the single-GPU
+    result.  Compute defaults to the HIP kernels (ops); tests inject the
+    oracle."""
+    from . import ops
+
+    world, rank = _world(group)
+    if voxel_fn is None:
+        def voxel_fn(p, vs, mn, mx):
+            return ops.voxel_down_sample(p, vs, mn, mx, with_xyz=False)["rep_idx"].long()
+    if normals_fn is None:
+        def normals_fn(p, k):
+            return ops.estimate_normals(p, knn=k)
+    if kdist_fn is None:
+        def kdist_fn(p, q, k):
+            return ops.knn_search(p, q, knn=k)[1][:, k - 1]
+    # 1. global bounds (a rank with no points contributes nothing)
+    if xyz.shape[0] > 0:
+        lmn = xyz.double().min(0).values.cpu().numpy()
+        lmx = xyz.double().max(0).values.cpu().numpy()
+    else:
+        lmn, lmx = np.full(3, np.inf), np.full(3, -np.inf)
+    mn, mx = global_aabb(lmn, lmx, group)
+    # 2. points to their slab owner, then into global-index order
+    keys = slab_bounds(mn, mx, voxel_size, world)
+    kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / voxel_size).to(torch.int64)
+    inner = torch.tensor(keys[1:-1], dtype=torch.int64, device=xyz.device)
+    owner = torch.searchsorted(inner, kx, right=True)
+    if world > 1:
+        xyz, gidx = _exchange(owner, world, group, xyz, gidx)
+    o = torch.argsort(gidx)
+    xyz, gidx = xyz[o].contiguous(), gidx[o].contiguous()
+    # 3. local reps with the global bounds
+    rep = voxel_fn(xyz, voxel_size, mn, mx)
+    rxyz, rg = xyz[rep].contiguous(), gidx[rep].contiguous()
+    x_lo = float(mn[0]) + keys[rank] * voxel_size
+    x_hi = float(mn[0]) + keys[rank + 1] * voxel_size
+    t_lo = rxyz[:, 0].double() - x_lo  # distance to the slab faces
+    t_hi = x_hi - rxyz[:, 0].double()
+    H = float(halo) if halo else 3.0 * voxel_size
+    min_width = min(keys[r + 1] - keys[r] for r in range(world)) * voxel_size
+    while True:
+        if world > 1 and H >= min_width:
+            raise RuntimeError("voxel_normals_slabs: the kNN halo is wider than a slab; use fewer ranks")
+        # 4. halo exchange with the neighbour slabs
+        if world > 1:
+            send_lo = (t_lo < H) & (rank > 0)
+            send_hi = (t_hi < H) & (rank < world - 1)
+            dest = torch.cat([torch.full((int(send_lo.sum()),), rank - 1, dtype=torch.int64, device=rxyz.device),
+                              torch.full((int(send_hi.sum()),), rank + 1, dtype=torch.int64, device=rxyz.device)])
+            hx, hg = _exchange(dest, world, group, torch.cat([rxyz[send_lo], rxyz[send_hi]]),
+                               torch.cat([rg[send_lo], rg[send_hi]]))
+        else:
+            hx, hg = rxyz[:0], rg[:0]
+        ux, ug = torch.cat([rxyz, hx]), torch.cat([rg, hg])
+        o = torch.argsort(ug)
+        ux, ug = ux[o].contiguous(), ug[o].contiguous()
+        own = torch.searchsorted(ug, rg)  # positions of the own reps in the union
+        # 5. verify: reps near a face must have their k-th neighbour inside the halo
+        inf = torch.full_like(t_lo, np.inf)
+        t = torch.minimum(t_lo if rank > 0 else inf, t_hi if rank < world - 1 else inf)
+        near = torch.nonzero(t < H).flatten()
+        ok = 1.0
+        if near.numel() and world > 1:
+            dk = torch.sqrt(kdist_fn(ux, ux[own[near]], knn).double())
+            ok = 1.0 if bool((dk - t[near] < H).all()) else 0.0
+        flag = torch.tensor([ok], dtype=torch.float64, device=_comm_device(group))
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if flag.item() == 1.0:
+            break
+        H *= 2.0
+    # 6. normals on own + halo reps, kept for the own reps
+    nrm = normals_fn(ux, knn)[own]
+    return rg, rxyz, nrm
+
+
 def shard_range(n: int, world: int, rank: int, align: int = 1) -> Tuple[int, int]:
     """Contiguous [a, b) share of n items for `rank` (boundaries multiples of `align`)."""
     per = -(-n // world)
@@ -142,4 +253,4 @@ def shard_range(n: int, world: int, rank: int, align: int = 1) -> Tuple[int, int
 
 
 __all__ = ["global_aabb", "slab_bounds", "slab_of", "allreduce_counts", "allreduce_icp_sums",
-           "registration_icp_point_to_plane", "shard_range"]
+           "registration_icp_point_to_plane", "voxel_normals_slabs", "shard_range"]

@@ -155,3 +155,49 @@ def test_shard_range_covers():
             parts = [D.shard_range(n, world, r, align=4) for r in range(world)]
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+
+
+# ---------------------------------------------------------------- C4 slabs
+def _o3_voxel(p, vs, mn, mx):
+    return torch.from_numpy(O.voxel_down_sample(p.numpy(), vs, mn, mx).astype(np.int64))
+
+
+def _o3_normals(p, k):
+    return torch.from_numpy(O.estimate_normals(p.numpy(), O.KNN, k))
+
+
+def _o3_kdist(p, q, k):
+    return torch.from_numpy(O.knn_search(p.numpy(), q.numpy(), O.KNN, k)[1][:, k - 1].copy())
+
+
+def _c4_cloud():
+    return S.uniform_cube(60_000, 31)
+
+
+def _c4_rank(rank, world):
+    pts = _c4_cloud()
+    n = pts.shape[0]
+    # an arbitrary (non-spatial) initial share: every world-th point
+    g = torch.arange(rank, n, world, dtype=torch.int64)
+    return D.voxel_normals_slabs(pts[g], g, 0.05, knn=30, voxel_fn=_o3_voxel, normals_fn=_o3_normals,
+                                 kdist_fn=_o3_kdist)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_slabs_match_single(world):
+    """Voxel reps and KNN30 normals of a cloud split over x-slabs (with the
+    halo exchange) equal the single-process result: same reps, same normals
+    bit for bit (the oracle sums each neighbourhood in the same order)."""
+    res = spawn(_c4_rank, world=world)
+    pts = _c4_cloud().numpy()
+    mn, mx = O.aabb(pts)
+    rep = O.voxel_down_sample(pts, 0.05, mn, mx)
+    nrm = O.estimate_normals(pts[rep], O.KNN, 30)
+    g = np.concatenate([r[0].numpy() for r in res])
+    nn = np.concatenate([r[2].numpy() for r in res])
+    o = np.argsort(g)
+    assert np.array_equal(g[o], rep.astype(np.int64))
+    assert np.array_equal(nn[o], nrm)
+    for r in res:  # each slab's reps are ascending and their xyz are the input points
+        assert np.all(np.diff(r[0].numpy()) > 0)
+        assert np.array_equal(r[1].numpy(), pts[r[0].numpy()])
