@@ -27,12 +27,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _plain(v):
+    """torch tensors -> numpy (tensors in a queue would be shared through a
+    socket that dies with the child process)."""
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu().numpy()
+    if isinstance(v, (tuple, list)):
+        return type(v)(_plain(x) for x in v)
+    return v
+
+
 def _run(rank, world, port, fn, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, fn(rank, world)))
+        q.put((rank, _plain(fn(rank, world))))
     except Exception as e:  # surface the failure in the parent
         q.put((rank, e))
     finally:
@@ -193,11 +203,11 @@ def test_c4_slabs_match_single(world):
     mn, mx = O.aabb(pts)
     rep = O.voxel_down_sample(pts, 0.05, mn, mx)
     nrm = O.estimate_normals(pts[rep], O.KNN, 30)
-    g = np.concatenate([r[0].numpy() for r in res])
-    nn = np.concatenate([r[2].numpy() for r in res])
+    g = np.concatenate([r[0] for r in res])
+    nn = np.concatenate([r[2] for r in res])
     o = np.argsort(g)
     assert np.array_equal(g[o], rep.astype(np.int64))
     assert np.array_equal(nn[o], nrm)
     for r in res:  # each slab's reps are ascending and their xyz are the input points
-        assert np.all(np.diff(r[0].numpy()) > 0)
-        assert np.array_equal(r[1].numpy(), pts[r[0].numpy()])
+        assert np.all(np.diff(r[0]) > 0)
+        assert np.array_equal(r[1], pts[r[0]])

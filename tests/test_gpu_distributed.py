@@ -49,7 +49,7 @@ def _c4_rank(rank, world):
     pts = S.uniform_cube(400_000, 33)
     g = torch.arange(rank, pts.shape[0], world, dtype=torch.int64)
     rg, rx, nrm = D.voxel_normals_slabs(pts[g].to(dev), g.to(dev), 0.02, knn=30)
-    return rg.cpu(), nrm.cpu()
+    return rg, nrm
 
 
 def test_c4_slabs_on_device_match_single():
@@ -62,8 +62,8 @@ def test_c4_slabs_on_device_match_single():
     mn, mx = ops.aabb(pts)
     out = ops.voxel_down_sample(pts, 0.02, mn, mx)
     ref = ops.estimate_normals(out["rep_xyz"], knn=30).cpu().numpy()
-    g = np.concatenate([r[0].numpy() for r in res])
-    nn = np.concatenate([r[1].numpy() for r in res])
+    g = np.concatenate([r[0] for r in res])
+    nn = np.concatenate([r[1] for r in res])
     o = np.argsort(g)
     assert np.array_equal(g[o], out["rep_idx"].cpu().numpy().astype(np.int64))
     dots = np.abs((nn[o] * ref).sum(1))
