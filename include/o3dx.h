@@ -269,6 +269,33 @@ int o3dx_registration_icp_point_to_plane(
     int32_t* corr_out_dev, int64_t* ncorr_host, void* target_ws,
     size_t target_ws_bytes, void* ws, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- PCD IO
+ * o3dx_pcd_unpack: decode PCD fields on the device (replaces the host-side
+ * field decoding of o3d.io.read_point_cloud behind PointCloudBase.read_pcd,
+ * reference PointCloud.py:165-166).  data_dev holds the raw DATA bytes
+ * (binary: n records; binary_compressed: the decompressed column blocks).
+ * Field j (nfields <= 16) of point i is read at
+ *   data_dev + src_off_host[j] + i * src_stride_host[j]   (no alignment needed)
+ * as types_host[j], converted to float32 and stored at
+ *   dst_dev_host[j] + i * dst_stride_host[j]   (floats).
+ * O3DX_PCD_RGB reads a packed 0x00RRGGBB (F4 or U4 bits) and stores r, g, b
+ * (3 consecutive floats, each /255).  Enqueues only. */
+#define O3DX_PCD_F4 1
+#define O3DX_PCD_F8 2
+#define O3DX_PCD_U1 3
+#define O3DX_PCD_U2 4
+#define O3DX_PCD_U4 5
+#define O3DX_PCD_I1 6
+#define O3DX_PCD_I2 7
+#define O3DX_PCD_I4 8
+#define O3DX_PCD_RGB 9
+/* o3dx_lzf_decompress (host): liblzf stream -> dst_host; returns the
+ * decompressed length, or a negative error for a corrupt stream. */
+int64_t o3dx_lzf_decompress(const uint8_t* src_host, int64_t n, uint8_t* dst_host, int64_t dst_len);
+int o3dx_pcd_unpack(const uint8_t* data_dev, int64_t n, int nfields, const int32_t* types_host,
+                    const int64_t* src_off_host, const int64_t* src_stride_host,
+                    float* const* dst_dev_host, const int64_t* dst_stride_host, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

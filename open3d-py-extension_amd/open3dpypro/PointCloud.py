@@ -380,7 +380,10 @@ class PointCloudBase:
                  remove_infinite_points: bool = False, print_progress: bool = False):
         ext = (os.path.splitext(filename)[1].lstrip(".") if format == "auto" else format).lower()
         nrm = col = None
-        if ext == "pcd":
+        if ext == "pcd" and torch.cuda.is_available():
+            # decoded on the GPU into the device arrays the cloud keeps
+            pts, nrm, col = pcd_io.read_pcd_device(filename, _device(), remove_nan_points, remove_infinite_points)
+        elif ext == "pcd":
             pts, nrm, col = pcd_io.read_pcd(filename, remove_nan_points, remove_infinite_points)
         elif ext == "npy":
             pts = np.load(filename, allow_pickle=False).reshape(-1, 3).astype(np.float64)

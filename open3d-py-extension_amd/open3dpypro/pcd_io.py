@@ -7,6 +7,12 @@ x/y/z -> points, normal_x/normal_y/normal_z -> normals and rgb/rgba (packed
 0x00RRGGBB) -> colors in [0,1]; other fields are parsed and returned by
 read_pcd_arrays but not attached to the cloud.  DATA ascii, binary and
 binary_compressed (LZF) are supported.
+
+read_pcd_device is the hot-path reader: the header is
+parsed here, the raw DATA bytes go to HBM in one copy (binary_compressed is
+LZF-decompressed on the host by the library first), and o3dx_pcd_unpack
+decodes every field on the GPU straight into the device arrays the
+PointCloud keeps.
 """
 from __future__ import annotations
 
@@ -179,3 +185,93 @@ def write_pcd(filename: str, points: np.ndarray, normals=None, colors=None, writ
                 rec[nm] = v
             f.write(rec.tobytes())
     return True
+
+
+def read_pcd_device(filename: str, device, remove_nan_points: bool = False, remove_infinite_points: bool = False):
+    """-> (points (n,3) float32, normals or None, colors or None) as tensors on
+    `device`, decoded on the GPU (o3dx_pcd_unpack).  ascii DATA is parsed on
+    the host (text) and copied."""
+    import ctypes
+    import struct
+
+    import torch
+
+    from . import _native as N
+
+    dev = torch.device(device)
+    with open(filename, "rb") as f:
+        h = _parse_header(f)
+        mode = h["DATA"][0].lower()
+        if mode == "ascii":
+            f.close()
+            pts, nrm, col = read_pcd(filename, remove_nan_points, remove_infinite_points)
+            tt = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+            return tt(pts), tt(nrm), tt(col)
+        fields = h["FIELDS"]
+        sizes = [int(v) for v in h.get("SIZE", ["4"] * len(fields))]
+        types = [t.upper() for t in h.get("TYPE", ["F"] * len(fields))]
+        counts = [int(v) for v in h.get("COUNT", ["1"] * len(fields))]
+        npts = int(h["POINTS"][0]) if "POINTS" in h else int(h["WIDTH"][0]) * int(h.get("HEIGHT", ["1"])[0])
+        rec = sum(sz * c for sz, c in zip(sizes, counts))
+        if mode == "binary":
+            raw = np.fromfile(f, dtype=np.uint8, count=rec * npts)
+            if raw.size != rec * npts:
+                raise RuntimeError(f"{filename}: truncated PCD binary data")
+        elif mode == "binary_compressed":
+            csize, usize = struct.unpack("<II", f.read(8))
+            comp = np.frombuffer(f.read(csize), dtype=np.uint8)
+            raw = np.empty(usize, dtype=np.uint8)
+            got = N.load().o3dx_lzf_decompress(comp.ctypes.data_as(ctypes.c_void_p), comp.size,
+                                               raw.ctypes.data_as(ctypes.c_void_p), usize)
+            if got != usize:
+                N.check(-22 if got >= 0 else int(got), "read_pcd (LZF)")
+        else:
+            raise RuntimeError(f"unsupported PCD DATA mode {mode!r}")
+    if not all(k in fields for k in ("x", "y", "z")):
+        raise RuntimeError(f"{filename}: PCD has no x/y/z fields")
+    columnar = mode == "binary_compressed"
+    # byte offset of each field: inside a record, or of its column block
+    off, o = {}, 0
+    for name, sz, c in zip(fields, sizes, counts):
+        off[name] = (o, sz)
+        o += sz * c * (npts if columnar else 1)
+    buf = torch.from_numpy(raw).to(dev)
+    pts = torch.empty((npts, 3), dtype=torch.float32, device=dev)
+    has_n = all(k in fields for k in ("normal_x", "normal_y", "normal_z"))
+    nrm = torch.empty((npts, 3), dtype=torch.float32, device=dev) if has_n else None
+    ckey = next((k for k in ("rgb", "rgba") if k in fields), None)
+    col = torch.empty((npts, 3), dtype=torch.float32, device=dev) if ckey else None
+    plan = [(k, pts, a) for a, k in enumerate(("x", "y", "z"))]
+    if has_n:
+        plan += [(k, nrm, a) for a, k in enumerate(("normal_x", "normal_y", "normal_z"))]
+    tys, so, ss, dp, ds = [], [], [], [], []
+    for name, out, a in plan:
+        o, sz = off[name]
+        t = N.PCD_TYPES.get((types[fields.index(name)], sz))
+        if t is None:
+            raise RuntimeError(f"{filename}: unsupported PCD field type for {name!r}")
+        tys.append(t), so.append(o), ss.append(sz if columnar else rec), dp.append(out.data_ptr() + 4 * a), ds.append(3)
+    if ckey:
+        o, sz = off[ckey]
+        if sz != 4:
+            raise RuntimeError(f"{filename}: PCD colour field must be 4 bytes")
+        tys.append(N.PCD_RGB), so.append(o), ss.append(sz if columnar else rec), dp.append(col.data_ptr()), ds.append(3)
+    nf = len(tys)
+    arr = lambda v, ty: (ty * nf)(*v)  # noqa: E731
+    N.check(N.load().o3dx_pcd_unpack(ctypes.c_void_p(buf.data_ptr()), npts, nf, arr(tys, ctypes.c_int32),
+                                     arr(so, ctypes.c_int64), arr(ss, ctypes.c_int64),
+                                     arr(dp, ctypes.c_void_p), arr(ds, ctypes.c_int64), N.stream_ptr(dev)),
+            "read_pcd")
+    del buf
+    if remove_nan_points or remove_infinite_points:
+        keep = torch.ones(npts, dtype=torch.bool, device=dev)
+        for a in ([pts] + ([nrm] if nrm is not None else [])):
+            if remove_nan_points:
+                keep &= ~torch.isnan(a).any(1)
+            if remove_infinite_points:
+                keep &= ~torch.isinf(a).any(1)
+        if not bool(keep.all()):
+            pts = pts[keep]
+            nrm = nrm[keep] if nrm is not None else None
+            col = col[keep] if col is not None else None
+    return pts, nrm, col

@@ -170,3 +170,41 @@ def test_icp_processor(dev):
     T = np.asarray(meta[icp.uuid]["transformation"])
     assert np.abs(T - np.linalg.inv(S.rigid_transform())).max() < 1e-4
     assert out[0].data().shape == (20000, 3)
+
+
+@pytest.mark.parametrize("layout", ["bunny", "binary", "compressed", "ascii", "nan"])
+def test_read_pcd_device_matches_host(dev, tmp_path, layout):
+    """PCD fields decoded on the GPU (o3dx_pcd_unpack) equal the host reader's,
+    for the reference's own bunny.pcd (binary, Intensity x y z _ records) and
+    written binary / binary_compressed / ascii files with normals + rgb."""
+    from open3dpypro import pcd_io
+    from test_host import write_pcd_compressed
+
+    if layout == "bunny":
+        path = BUNNY
+    else:
+        rng = np.random.default_rng(9)
+        pts = rng.random((5000, 3)).astype(np.float32)
+        nrm = rng.standard_normal((5000, 3)).astype(np.float32)
+        rgb = rng.integers(0, 1 << 24, 5000).astype(np.uint32)
+        col = np.stack([(rgb >> 16) & 255, (rgb >> 8) & 255, rgb & 255], 1) / 255.0
+        if layout == "nan":
+            pts[::7, 1] = np.nan
+            pts[::11, 2] = np.inf
+        path = str(tmp_path / f"{layout}.pcd")
+        if layout == "compressed":
+            write_pcd_compressed(path, pts, nrm, rgb)
+        else:
+            pcd_io.write_pcd(path, pts, nrm, col, write_ascii=(layout == "ascii"))
+    for rm in (False, True):
+        hp, hn, hc = pcd_io.read_pcd(path, rm, rm)
+        dp, dn, dc = pcd_io.read_pcd_device(path, dev, rm, rm)
+        assert np.array_equal(dp.cpu().numpy().astype(np.float64), hp, equal_nan=True)
+        if hn is not None:
+            assert np.array_equal(dn.cpu().numpy().astype(np.float64), hn.astype(np.float32).astype(np.float64),
+                                  equal_nan=True)
+        if hc is not None:
+            assert np.allclose(dc.cpu().numpy(), hc, atol=1e-6)
+    # and through the drop-in API
+    pc = o3p.PointCloud().read_pcd(path)
+    assert pc.size() == len(pcd_io.read_pcd(path)[0])

@@ -262,3 +262,99 @@ def test_synthetic_deterministic_and_sharded():
     s = S.box_surface(5000, 2)
     on_face = ((s == 0) | (s == torch.tensor([1.0, 0.8, 0.6]))).any(1)
     assert bool(on_face.all())
+
+
+def _lzf_compress(data: bytes) -> bytes:
+    """Small greedy liblzf-format compressor (test helper): back references
+    (>= 3 bytes, offset <= 8192) found by a hash of 3-byte prefixes."""
+    out = bytearray()
+    lit = bytearray()
+    table = {}
+    i, n = 0, len(data)
+
+    def flush():
+        while lit:
+            chunk = lit[:32]
+            out.append(len(chunk) - 1)
+            out.extend(chunk)
+            del lit[:32]
+
+    while i < n:
+        ref = table.get(data[i:i + 3]) if i + 3 <= n else None
+        if i + 3 <= n:
+            table[data[i:i + 3]] = i
+        if ref is not None and 0 < i - ref <= 8192:
+            ln = 0
+            while i + ln < n and ln < 264 and data[ref + ln] == data[i + ln]:
+                ln += 1
+            if ln >= 3:
+                flush()
+                off = i - ref - 1
+                l2 = ln - 2
+                if l2 < 7:
+                    out.append((l2 << 5) | (off >> 8))
+                else:
+                    out.append((7 << 5) | (off >> 8))
+                    out.append(l2 - 7)
+                out.append(off & 0xFF)
+                i += ln
+                continue
+        lit.append(data[i])
+        i += 1
+    flush()
+    return bytes(out)
+
+
+def write_pcd_compressed(path, pts, normals=None, rgb_u32=None):
+    cols = [("x", pts[:, 0]), ("y", pts[:, 1]), ("z", pts[:, 2])]
+    if normals is not None:
+        cols += [("normal_x", normals[:, 0]), ("normal_y", normals[:, 1]), ("normal_z", normals[:, 2])]
+    if rgb_u32 is not None:
+        cols.append(("rgb", rgb_u32))
+    n = len(pts)
+    body = b"".join(np.ascontiguousarray(c, np.uint32 if k == "rgb" else np.float32).tobytes() for k, c in cols)
+    comp = _lzf_compress(body)
+    head = ("VERSION 0.7\nFIELDS " + " ".join(k for k, _ in cols) + "\nSIZE " + " ".join("4" for _ in cols) +
+            "\nTYPE " + " ".join("U" if k == "rgb" else "F" for k, _ in cols) + "\nCOUNT " +
+            " ".join("1" for _ in cols) + f"\nWIDTH {n}\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS {n}\n"
+            "DATA binary_compressed\n")
+    import struct
+    with open(path, "wb") as f:
+        f.write(head.encode() + struct.pack("<II", len(comp), len(body)) + comp)
+    return body
+
+
+def test_lzf_library_matches_python(tmp_path):
+    """o3dx_lzf_decompress (host code in libo3dx.so) vs the Python decoder,
+    on a stream with literal runs and overlapping back references."""
+    import ctypes
+
+    from open3dpypro import _native as N
+    from open3dpypro import pcd_io
+
+    rng = np.random.default_rng(3)
+    data = bytes(rng.integers(0, 4, 5000, dtype=np.uint8)) + b"abcabcabcabc" * 50 + bytes(range(256)) * 3
+    comp = _lzf_compress(data)
+    assert pcd_io.lzf_decompress(comp, len(data)) == data
+    src = np.frombuffer(comp, np.uint8)
+    dst = np.zeros(len(data), np.uint8)
+    got = N.load().o3dx_lzf_decompress(src.ctypes.data_as(ctypes.c_void_p), src.size,
+                                       dst.ctypes.data_as(ctypes.c_void_p), dst.size)
+    assert got == len(data) and dst.tobytes() == data
+    bad = N.load().o3dx_lzf_decompress(src.ctypes.data_as(ctypes.c_void_p), src.size,
+                                       dst.ctypes.data_as(ctypes.c_void_p), 10)
+    assert bad < 0
+
+
+def test_pcd_binary_compressed_host_reader(tmp_path):
+    from open3dpypro import pcd_io
+
+    rng = np.random.default_rng(4)
+    pts = rng.random((3000, 3)).astype(np.float32)
+    nrm = rng.standard_normal((3000, 3)).astype(np.float32)
+    rgb = rng.integers(0, 1 << 24, 3000).astype(np.uint32)
+    p = str(tmp_path / "c.pcd")
+    write_pcd_compressed(p, pts, nrm, rgb)
+    P, Nn, C = pcd_io.read_pcd(p)
+    assert np.array_equal(P, pts.astype(np.float64)) and np.array_equal(Nn, nrm.astype(np.float64))
+    assert np.allclose(C * 255.0, np.stack([(rgb >> 16) & 255, (rgb >> 8) & 255, rgb & 255], 1))
