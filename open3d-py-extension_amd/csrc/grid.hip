@@ -872,7 +872,8 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   __shared__ int32_t rst[kMaxTileRows];
   // the candidate list (u16 [KMAX + band + 1][64]) and the histogram counters
   // (u32 [18][64]) share one LDS buffer: the histogram is dead before the list
-  constexpr int kListCap = KMAX + kBndCap + 1;  // last slot: write sink
+  constexpr int kListMax = KMAX + kBndCap;      // more entries than this: hand the query on
+  constexpr int kListCap = kListMax + 4;        // room for one unconditional 4-candidate store
   constexpr int kListWords = (kListCap * kTileQ * 2 + 3) / 4;
   constexpr int kHistWords = kTileSlots * kTileQ;
   __shared__ uint32_t selbuf[kListWords > kHistWords ? kListWords : kHistWords];
@@ -945,17 +946,37 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
         }
         if (!fb && dbg != 2) {
           const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
-          // branch-free append of every candidate below Up: written to the
-          // next free slot, kept where the count advances
+          // branch-free append of every candidate below Up: candidate u of a
+          // group of four is written to slot n + (#accepted before u), so the
+          // accepted ones end up contiguous and a rejected one is overwritten
+          // by the next accepted (or by the next group); one clamp per group
           int n = 0;
-          O3DX_TILE_SCAN(Up, {
-            lst[min(n, kListCap - 1)][lane] = (uint16_t)pp;
-            n += d2 < Up ? 1 : 0;
-          })
+          for (int r_ = 0; r_ < 9; ++r_) {
+            int a_, e_;
+            tile_row(g, box, ccs, q, cx, cy, cz, r_, Up, &a_, &e_);
+            int p_ = a_;
+            for (; p_ + 4 <= e_; p_ += 4) {
+              const f32x2 da_ = dist2_pair(q, (f32x2){tx[p_], tx[p_ + 1]}, (f32x2){ty[p_], ty[p_ + 1]},
+                                           (f32x2){tz[p_], tz[p_ + 1]});
+              const f32x2 db_ = dist2_pair(q, (f32x2){tx[p_ + 2], tx[p_ + 3]}, (f32x2){ty[p_ + 2], ty[p_ + 3]},
+                                           (f32x2){tz[p_ + 2], tz[p_ + 3]});
+              const int a0 = da_.x < Up, a1 = da_.y < Up, a2 = db_.x < Up, a3 = db_.y < Up;
+              uint16_t* base = &lst[min(n, kListMax)][lane];
+              base[0] = (uint16_t)p_;
+              base[a0 * kTileQ] = (uint16_t)(p_ + 1);
+              base[(a0 + a1) * kTileQ] = (uint16_t)(p_ + 2);
+              base[(a0 + a1 + a2) * kTileQ] = (uint16_t)(p_ + 3);
+              n += a0 + a1 + a2 + a3;
+            }
+            for (; p_ < e_; ++p_) {
+              lst[min(n, kListMax)][lane] = (uint16_t)p_;
+              n += dist2_f32(q, tx[p_], ty[p_], tz[p_]) < Up ? 1 : 0;
+            }
+          }
           if (dbg == 3) {
             if (n == 12345) out[0] = 0.f;  // keep the scan alive
           } else
-          fb = n >= kListCap ||
+          fb = n > kListMax ||
                !finish_selection<KMAX>(
                    q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
                    [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, prior,
