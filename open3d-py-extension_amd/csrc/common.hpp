@@ -78,6 +78,18 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int l = lane_id();
 #pragma unroll

@@ -280,30 +280,56 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
 
 // ------------------------------------------------------------- chunk plan
 // Queries = the grid's own (cell-sorted) points, so the queries of grid row
-// k = (y, z) are the contiguous range [start[k nx], start[(k+1) nx]).  Each
-// row is cut into chunks of <= qcap queries; no host synchronisation: the
-// caller launches `upper` blocks, the slots past the real chunk count hold n
-// (empty chunks) and slot upper+1 holds the real count.
-__global__ void k_row_nchunks(const int32_t* __restrict__ start, int nx, int64_t rows, int qcap,
-                              int32_t* __restrict__ nch) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= rows) return;
-  const int32_t a = start[k * nx], b = start[(k + 1) * nx];
-  nch[k] = (b - a + qcap - 1) / qcap;
+// k = (y, z) are the contiguous range [start[k nx], start[(k+1) nx]).  Rows
+// of >= qcap queries are cut into chunks of qcap; shorter rows of one z slab
+// are merged with their successors in y (contiguous in memory) while the
+// chunk stays <= qcap queries and spans <= kChunkYSpan + 1 rows — on a surface
+// seen edge-on every row holds only a few points.  One thread per z slab;
+// no host synchronisation: the caller launches `upper` blocks, the slots past
+// the real chunk count hold n (empty chunks) and slot upper+1 holds the count.
+constexpr int kChunkYSpan = 9;  // box rows (span + 3) x 3 <= kMaxTileRows
+
+template <bool EMIT>
+__global__ void k_slab_chunks(const int32_t* __restrict__ start, int nx, int ny, int nz, int qcap,
+                              int32_t* __restrict__ cnt_or_off, int32_t* __restrict__ chunk_starts) {
+  const int z = blockIdx.x * blockDim.x + threadIdx.x;
+  if (z >= nz) return;
+  int cnt = 0, o = EMIT ? cnt_or_off[z] : 0;
+  int open_start = -1, open_len = 0, open_y0 = 0;
+  auto put = [&](int p) {
+    if (EMIT) chunk_starts[o++] = p;
+    ++cnt;
+  };
+  for (int y = 0; y < ny; ++y) {
+    const int64_t k = y + (int64_t)ny * z;
+    const int32_t a = start[k * nx], b = start[(k + 1) * nx], len = b - a;
+    if (len == 0) continue;
+    if (open_start >= 0 && (len >= qcap || open_len + len > qcap || y - open_y0 > kChunkYSpan)) {
+      put(open_start);
+      open_start = -1;
+      open_len = 0;
+    }
+    if (len >= qcap) {
+      for (int32_t p = a; p < b; p += qcap) put(p);
+      continue;
+    }
+    if (open_start < 0) {
+      open_start = a;
+      open_y0 = y;
+    }
+    open_len += len;
+  }
+  if (open_start >= 0) put(open_start);
+  if (!EMIT) cnt_or_off[z] = cnt;
 }
 
-__global__ void k_emit_chunks(const int32_t* __restrict__ start, int nx, int64_t rows, int qcap,
-                              const int32_t* __restrict__ offs, int64_t n, int64_t upper,
-                              int32_t* __restrict__ chunk_starts) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < rows) {
-    const int32_t a = start[k * nx], b = start[(k + 1) * nx];
-    int32_t o = offs[k];
-    for (int32_t p = a; p < b; p += qcap) chunk_starts[o++] = p;
-  }
-  const int64_t total = offs[rows];
-  for (int64_t c = total + k; c <= upper; c += (int64_t)gridDim.x * blockDim.x) chunk_starts[c] = (int32_t)n;
-  if (k == 0) chunk_starts[upper + 1] = (int32_t)total;  // the real chunk count, for the launch
+__global__ void k_chunk_tail(const int32_t* __restrict__ offs, int nz, int64_t n, int64_t upper,
+                             int32_t* __restrict__ chunk_starts) {
+  const int64_t total = offs[nz];
+  for (int64_t c = total + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c <= upper;
+       c += (int64_t)gridDim.x * blockDim.x)
+    chunk_starts[c] = (int32_t)n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) chunk_starts[upper + 1] = (int32_t)total;
 }
 
 int64_t chunk_plan_upper(int64_t n, const GridView& g, int qcap) {
@@ -311,7 +337,7 @@ int64_t chunk_plan_upper(int64_t n, const GridView& g, int qcap) {
 }
 
 size_t chunk_plan_ws_bytes(int64_t n, int64_t rows) {
-  rows = std::max<int64_t>(rows, 1);
+  rows = std::max<int64_t>(rows, 1);  // bounds the number of z slabs too
   (void)n;
   return 2 * Arena::align((rows + 2) * 4) + Arena::align(scan_workspace_ints(rows + 1) * 4 + 1) + 1024;
 }
@@ -321,15 +347,17 @@ int chunk_plan(int64_t n, const GridView& g, int qcap, int32_t* chunk_starts, vo
   const int64_t rows = (int64_t)g.ny * g.nz;
   if (ws_bytes < chunk_plan_ws_bytes(n, rows)) return fail(O3DX_ENOMEM, "chunk plan workspace too small");
   Arena ar(ws, ws_bytes);
-  int32_t* nch = ar.take<int32_t>(rows + 1);
-  int32_t* offs = ar.take<int32_t>(rows + 1);
-  int32_t* tmp = ar.take<int32_t>(scan_workspace_ints(rows + 1));
+  int32_t* cnt = ar.take<int32_t>(g.nz + 1);
+  int32_t* offs = ar.take<int32_t>(g.nz + 1);
+  int32_t* tmp = ar.take<int32_t>(scan_workspace_ints(g.nz + 1));
   const int64_t upper = chunk_plan_upper(n, g, qcap);
-  const unsigned gr = (unsigned)((rows + 255) / 256);
-  hipLaunchKernelGGL(k_row_nchunks, dim3(gr), dim3(256), 0, s, g.start, g.nx, rows, qcap, nch);
-  O3DX_TRY(exclusive_scan_i32(nch, offs, rows, tmp, s));
-  hipLaunchKernelGGL(k_emit_chunks, dim3(gr), dim3(256), 0, s, g.start, g.nx, rows, qcap, offs, n, upper,
+  const unsigned gz = (unsigned)((g.nz + 63) / 64);
+  hipLaunchKernelGGL(k_slab_chunks<false>, dim3(gz), dim3(64), 0, s, g.start, g.nx, g.ny, g.nz, qcap, cnt,
+                     (int32_t*)nullptr);
+  O3DX_TRY(exclusive_scan_i32(cnt, offs, g.nz, tmp, s));
+  hipLaunchKernelGGL(k_slab_chunks<true>, dim3(gz), dim3(64), 0, s, g.start, g.nx, g.ny, g.nz, qcap, offs,
                      chunk_starts);
+  hipLaunchKernelGGL(k_chunk_tail, dim3(256), dim3(256), 0, s, offs, g.nz, n, upper, chunk_starts);
   O3DX_HIP(hipGetLastError());
   return 0;
 }
@@ -887,27 +915,32 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   const int q0 = chunk_starts[c], q1 = chunk_starts[c + 1];
   const int64_t s = (int64_t)q0 + lane;
   const bool active = s < q1;
-  // the chunk lies in one (y,z) row and is sorted by x: first/last give its cells
-  int ax, ay, az, bx, by, bz;
-  {
-    const float4 f = g.pts[q0], l = g.pts[q1 - 1];
-    grid_cell(g, f.x, f.y, f.z, ax, ay, az);
-    grid_cell(g, l.x, l.y, l.z, bx, by, bz);
-  }
+  // the chunk lies in one z slab and spans a few y rows (each sorted by x)
   const float4 q = g.pts[active ? s : (int64_t)q0];
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
-  bool fb = active && (cy != ay || cz != az);
-  // Parts: x-cell ranges processed left to right.  A part whose box does not
-  // fit in LDS is halved (down to one cell) before it is staged.
-  for (int x_lo = ax; x_lo <= bx;) {
-    int x_hi = bx, staged;
+  int az;
+  {
+    const float4 f = g.pts[q0];
+    int fx, fy;
+    grid_cell(g, f.x, f.y, f.z, fx, fy, az);
+  }
+  const int ay0 = wave_min(active ? cy : INT_MAX), ay1 = wave_max(active ? cy : INT_MIN);
+  bool fb = active && cz != az;
+  bool todo = active && !fb;
+  // Parts: x-cell ranges [lowest unprocessed cx, highest cx] of the chunk's
+  // lanes, left to right.  A part whose box does not fit in LDS is halved
+  // (down to one cell) before it is staged.
+  for (;;) {
+    const int x_lo = wave_min(todo ? cx : INT_MAX);
+    if (x_lo == INT_MAX) break;
+    int x_hi = wave_max(todo ? cx : INT_MIN), staged;
     TileBox box;
     for (;;) {
       box.x0 = max(x_lo - 1, 0);
       box.x1 = min(x_hi + 1, g.nx - 1);
-      box.y0 = max(ay - 1, 0);
-      box.y1 = min(ay + 1, g.ny - 1);
+      box.y0 = max(ay0 - 1, 0);
+      box.y1 = min(ay1 + 1, g.ny - 1);
       box.z0 = max(az - 1, 0);
       box.z1 = min(az + 1, g.nz - 1);
       box.nxr = box.x1 - box.x0 + 1;
@@ -917,7 +950,9 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
       __syncthreads();
       x_hi = x_lo + (x_hi - x_lo) / 2;
     }
-    if (active && !fb && cx >= x_lo && cx <= x_hi && dbg != 1) {
+    const bool mine = todo && cx >= x_lo && cx <= x_hi;
+    if (mine) todo = false;
+    if (mine && dbg != 1) {
       fb = staged < 0;
       if (fb && g.stats) atomicAdd(&g.stats[6], 1ull);
       if (!fb) {
@@ -984,7 +1019,6 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
         }
       }
     }
-    x_lo = x_hi + 1;
     __syncthreads();  // the next part restages the LDS tile
   }
   if (fb) {

@@ -30,12 +30,23 @@ def run_one():
     _native.reset_kernel_timing()
     for _ in range(3):
         ops.estimate_normals(reps, knn=30)
-    ms, c = _native.kernel_timing("normals_knn")
-    out["normals_ms"] = ms / c
+    for name in ("normals_knn", "normals_tile", "normals_wave"):
+        ms, c = _native.kernel_timing(name)
+        out[name + "_ms"] = ms / max(c, 1)
     del pts, reps
     tgt = S.box_surface(N, 1, device=dev)
     src = S.apply_transform(S.box_surface(N, 2, device=dev), S.rigid_transform())
     tn = ops.estimate_normals(tgt, knn=30)
+    _native.search_stats(True)
+    ops.estimate_normals(tgt, knn=30)
+    out["surface_normals_stats"] = _native.search_stats()
+    _native.search_stats(False)
+    _native.reset_kernel_timing()
+    for _ in range(3):
+        tn = ops.estimate_normals(tgt, knn=30)
+    for name in ("normals_knn", "normals_tile", "normals_wave"):
+        ms, c = _native.kernel_timing(name)
+        out["surface_" + name + "_ms"] = ms / max(c, 1)
     target = ops.ICPTarget(tgt, tn, 0.02)
     src = ops.spatial_sort(src)
     T = np.eye(4)
