@@ -281,51 +281,58 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
 // ------------------------------------------------------------- chunk plan
 // Queries = the grid's own (cell-sorted) points, so the queries of grid row
 // k = (y, z) are the contiguous range [start[k nx], start[(k+1) nx]).  Rows
-// of >= qcap queries are cut into chunks of qcap; shorter rows of one z slab
-// are merged with their successors in y (contiguous in memory) while the
-// chunk stays <= qcap queries and spans <= kChunkYSpan + 1 rows — on a surface
-// seen edge-on every row holds only a few points.  One thread per z slab;
-// no host synchronisation: the caller launches `upper` blocks, the slots past
-// the real chunk count hold n (empty chunks) and slot upper+1 holds the count.
-constexpr int kChunkYSpan = 9;  // box rows (span + 3) x 3 <= kMaxTileRows
+// of >= qcap queries are cut into chunks of qcap; within a group of
+// kChunkRows consecutive rows of one z slab, shorter rows are merged with
+// their successors (contiguous in memory) while the chunk stays <= qcap
+// queries — on a surface seen edge-on every row holds only a few points.
+// One thread per group; no host synchronisation: the caller launches `upper`
+// blocks, the slots past the real chunk count hold n (empty chunks) and slot
+// upper+1 holds the count.
+constexpr int kChunkRows = 10;  // box rows (kChunkRows + 2) x 3 <= kMaxTileRows
 
 template <bool EMIT>
-__global__ void k_slab_chunks(const int32_t* __restrict__ start, int nx, int ny, int nz, int qcap,
-                              int32_t* __restrict__ cnt_or_off, int32_t* __restrict__ chunk_starts) {
-  const int z = blockIdx.x * blockDim.x + threadIdx.x;
-  if (z >= nz) return;
-  int cnt = 0, o = EMIT ? cnt_or_off[z] : 0;
-  int open_start = -1, open_len = 0, open_y0 = 0;
-  auto put = [&](int p) {
-    if (EMIT) chunk_starts[o++] = p;
-    ++cnt;
-  };
-  for (int y = 0; y < ny; ++y) {
-    const int64_t k = y + (int64_t)ny * z;
-    const int32_t a = start[k * nx], b = start[(k + 1) * nx], len = b - a;
+__global__ void k_group_chunks(const int32_t* __restrict__ start, int nx, int ny, int nz, int qcap,
+                               int32_t* __restrict__ cnt_or_off, int32_t* __restrict__ chunk_starts) {
+  const int gy = (ny + kChunkRows - 1) / kChunkRows;
+  const int64_t grp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (grp >= (int64_t)gy * nz) return;
+  const int z = (int)(grp / gy), y0 = (int)(grp % gy) * kChunkRows, y1 = min(y0 + kChunkRows, ny);
+  int32_t bnd[kChunkRows + 1];
+#pragma unroll
+  for (int j = 0; j <= kChunkRows; ++j)
+    bnd[j] = start[(int64_t)min(y0 + j, y1) * nx + (int64_t)ny * nx * z];
+  int cnt = 0, o = EMIT ? cnt_or_off[grp] : 0;
+  int open_start = -1, open_len = 0;
+#pragma unroll
+  for (int j = 0; j < kChunkRows; ++j) {
+    const int32_t a = bnd[j], len = bnd[j + 1] - a;
     if (len == 0) continue;
-    if (open_start >= 0 && (len >= qcap || open_len + len > qcap || y - open_y0 > kChunkYSpan)) {
-      put(open_start);
+    if (open_start >= 0 && (len >= qcap || open_len + len > qcap)) {
+      if (EMIT) chunk_starts[o++] = open_start;
+      ++cnt;
       open_start = -1;
       open_len = 0;
     }
     if (len >= qcap) {
-      for (int32_t p = a; p < b; p += qcap) put(p);
+      for (int32_t p = a; p < a + len; p += qcap) {
+        if (EMIT) chunk_starts[o++] = p;
+        ++cnt;
+      }
       continue;
     }
-    if (open_start < 0) {
-      open_start = a;
-      open_y0 = y;
-    }
+    if (open_start < 0) open_start = a;
     open_len += len;
   }
-  if (open_start >= 0) put(open_start);
-  if (!EMIT) cnt_or_off[z] = cnt;
+  if (open_start >= 0) {
+    if (EMIT) chunk_starts[o] = open_start;
+    ++cnt;
+  }
+  if (!EMIT) cnt_or_off[grp] = cnt;
 }
 
-__global__ void k_chunk_tail(const int32_t* __restrict__ offs, int nz, int64_t n, int64_t upper,
+__global__ void k_chunk_tail(const int32_t* __restrict__ offs, int64_t ngroups, int64_t n, int64_t upper,
                              int32_t* __restrict__ chunk_starts) {
-  const int64_t total = offs[nz];
+  const int64_t total = offs[ngroups];
   for (int64_t c = total + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c <= upper;
        c += (int64_t)gridDim.x * blockDim.x)
     chunk_starts[c] = (int32_t)n;
@@ -337,7 +344,7 @@ int64_t chunk_plan_upper(int64_t n, const GridView& g, int qcap) {
 }
 
 size_t chunk_plan_ws_bytes(int64_t n, int64_t rows) {
-  rows = std::max<int64_t>(rows, 1);  // bounds the number of z slabs too
+  rows = std::max<int64_t>(rows, 1);  // bounds the number of row groups too
   (void)n;
   return 2 * Arena::align((rows + 2) * 4) + Arena::align(scan_workspace_ints(rows + 1) * 4 + 1) + 1024;
 }
@@ -347,17 +354,18 @@ int chunk_plan(int64_t n, const GridView& g, int qcap, int32_t* chunk_starts, vo
   const int64_t rows = (int64_t)g.ny * g.nz;
   if (ws_bytes < chunk_plan_ws_bytes(n, rows)) return fail(O3DX_ENOMEM, "chunk plan workspace too small");
   Arena ar(ws, ws_bytes);
-  int32_t* cnt = ar.take<int32_t>(g.nz + 1);
-  int32_t* offs = ar.take<int32_t>(g.nz + 1);
-  int32_t* tmp = ar.take<int32_t>(scan_workspace_ints(g.nz + 1));
+  const int64_t ngroups = (int64_t)((g.ny + kChunkRows - 1) / kChunkRows) * g.nz;
+  int32_t* cnt = ar.take<int32_t>(ngroups + 1);
+  int32_t* offs = ar.take<int32_t>(ngroups + 1);
+  int32_t* tmp = ar.take<int32_t>(scan_workspace_ints(ngroups + 1));
   const int64_t upper = chunk_plan_upper(n, g, qcap);
-  const unsigned gz = (unsigned)((g.nz + 63) / 64);
-  hipLaunchKernelGGL(k_slab_chunks<false>, dim3(gz), dim3(64), 0, s, g.start, g.nx, g.ny, g.nz, qcap, cnt,
+  const unsigned gg = (unsigned)((ngroups + 255) / 256);
+  hipLaunchKernelGGL(k_group_chunks<false>, dim3(gg), dim3(256), 0, s, g.start, g.nx, g.ny, g.nz, qcap, cnt,
                      (int32_t*)nullptr);
-  O3DX_TRY(exclusive_scan_i32(cnt, offs, g.nz, tmp, s));
-  hipLaunchKernelGGL(k_slab_chunks<true>, dim3(gz), dim3(64), 0, s, g.start, g.nx, g.ny, g.nz, qcap, offs,
+  O3DX_TRY(exclusive_scan_i32(cnt, offs, ngroups, tmp, s));
+  hipLaunchKernelGGL(k_group_chunks<true>, dim3(gg), dim3(256), 0, s, g.start, g.nx, g.ny, g.nz, qcap, offs,
                      chunk_starts);
-  hipLaunchKernelGGL(k_chunk_tail, dim3(256), dim3(256), 0, s, offs, g.nz, n, upper, chunk_starts);
+  hipLaunchKernelGGL(k_chunk_tail, dim3(256), dim3(256), 0, s, offs, ngroups, n, upper, chunk_starts);
   O3DX_HIP(hipGetLastError());
   return 0;
 }

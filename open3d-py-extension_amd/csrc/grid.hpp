@@ -409,7 +409,7 @@ __device__ __forceinline__ void for_tile_rows(const TileBox& b, const int32_t* c
 
 // Chunk plan (normals tiles): the grid's own points in chunks of <= qcap
 // consecutive queries: long (y,z) rows cut in qcap pieces, short rows of one z
-// slab merged (span <= 10 rows).  chunk_starts needs
+// slab merged (within groups of 10 rows).  chunk_starts needs
 // chunk_plan_upper()+2 entries; slots past the real count hold n.  Enqueues
 // only (no host synchronisation).
 int64_t chunk_plan_upper(int64_t n, const GridView& g, int qcap);

@@ -9,7 +9,14 @@
 //   1. key per point in float64 exactly as Open3D: floor(((double)p - min)/vs).
 //   2. voxel table: dense int32 array over the grid box when it is small
 //      (<= 2n + 2^20 cells), else an open-addressing hash table on a packed
-//      63-bit key.  rep[voxel] = atomicMax(point index)  (= idxmat.max(1)).
+//      63-bit key.  rep[voxel] = max point index  (= idxmat.max(1)).
+//      Dense grids of <= kMaxBuckets buckets (bricks of 2^12..2^13 voxels) are
+//      reduced without global atomics: the points are binned by brick
+//      (block-local LDS histograms, one global atomic per block and brick to
+//      reserve a run), then one workgroup per brick takes the max in an LDS
+//      table and writes the brick's slice of the table plus the rep flags.
+//      Scattered 4-byte stores/atomics into a table larger than L2 were the
+//      cost of the plain dense path (k_voxel_assign_dense + k_voxel_settle).
 //   3. flags[rep] = 1, then a flag compaction gives the representatives in
 //      ascending index order (= _select_by_idx order) for free.
 //   4. trace (optional): voxel_of_point via the compaction prefix, Open3D's
@@ -79,6 +86,165 @@ __global__ void __launch_bounds__(kBlock) k_voxel_settle(const int32_t* __restri
     const int32_t id = vid[i];
     if (id >= 0 && rep[id] < (int32_t)i) atomicMax(&rep[id], (int32_t)i);
   }
+}
+
+// ------------------------------------------------------- brick-binned path
+constexpr int kBinBlock = 512;
+constexpr int kBinPer = 32;                    // points per thread in the binning passes
+constexpr int kBinChunk = kBinBlock * kBinPer; // points per binning block
+constexpr int kCtrPad = 32;                    // one 128-B line per brick counter / cursor
+constexpr int kMaxBuckets = 8192;              // LDS histogram (32 KB)
+constexpr int kMaxBrickBits = 13;              // LDS max table (32 KB)
+constexpr int kReduceBlock = 512;
+
+struct Bricks {
+  int sx, sy, sz;     // log2 brick extent per axis
+  int nbx, nby, nbz;  // bricks per axis
+  int nb;
+};
+
+__device__ __forceinline__ bool voxel_of(const P3& q, const VoxelGeom& g, int v[3]) {
+  double r[3];
+  voxel_ref(q, g, r, v);
+  return v[0] >= 0 && v[0] < g.nx && v[1] >= 0 && v[1] < g.ny && v[2] >= 0 && v[2] < g.nz;
+}
+
+// (brick << 16) | local voxel within the brick
+__device__ __forceinline__ uint32_t brick_code(const int v[3], const Bricks& b) {
+  const uint32_t bk = (uint32_t)((v[0] >> b.sx) + b.nbx * ((v[1] >> b.sy) + b.nby * (v[2] >> b.sz)));
+  const uint32_t lx = v[0] & ((1 << b.sx) - 1), ly = v[1] & ((1 << b.sy) - 1), lz = v[2] & ((1 << b.sz) - 1);
+  return (bk << 16) | lx | (ly << b.sx) | (lz << (b.sx + b.sy));
+}
+
+// Pass 1: brick counts (LDS histogram per block, one global add per touched
+// brick).  Also writes the voxel id per point when the trace needs it.
+__global__ void __launch_bounds__(kBinBlock) k_vbin_count(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+                                                       Bricks b, int32_t* __restrict__ bcount,
+                                                       int32_t* __restrict__ vid, int* __restrict__ err) {
+  __shared__ int32_t hist[kMaxBuckets];
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) hist[k] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kBinChunk;
+  bool bad = false;
+#pragma unroll 4
+  for (int j = 0; j < kBinPer; ++j) {
+    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    if (i >= n) break;
+    int v[3];
+    const bool in = voxel_of(p[i], g, v);
+    if (in) atomicAdd(&hist[brick_code(v, b) >> 16], 1);
+    bad |= !in;
+    if (vid) vid[i] = in ? v[0] + g.nx * (v[1] + g.ny * v[2]) : -1;
+  }
+  if (bad) *err = 1;
+  __syncthreads();
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock)
+    if (hist[k]) atomicAdd(&bcount[k * kCtrPad], hist[k]);
+}
+
+// Padded counters -> contiguous counts (for the scan), offsets -> padded cursors.
+__global__ void k_vbin_unpad(const int32_t* __restrict__ padded, int nb, int32_t* __restrict__ dense) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nb) dense[k] = padded[k * kCtrPad];
+}
+__global__ void k_vbin_pad(const int32_t* __restrict__ dense, int nb, int32_t* __restrict__ padded) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nb) padded[k * kCtrPad] = dense[k];
+}
+
+// Pass 2: reserve a run per touched brick, then scatter (local << 32 | index).
+__global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+                                                         Bricks b, int32_t* __restrict__ cursor,
+                                                         uint64_t* __restrict__ entries) {
+  __shared__ int32_t hist[kMaxBuckets];
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) hist[k] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kBinChunk;
+  uint32_t code[kBinPer];
+#pragma unroll
+  for (int j = 0; j < kBinPer; ++j) {
+    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    int v[3];
+    code[j] = ~0u;
+    if (i < n && voxel_of(p[i], g, v)) {
+      code[j] = brick_code(v, b);
+      atomicAdd(&hist[code[j] >> 16], 1);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock)
+    if (hist[k]) hist[k] = atomicAdd(&cursor[k * kCtrPad], hist[k]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kBinPer; ++j) {
+    if (code[j] == ~0u) continue;
+    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    const int32_t at = atomicAdd(&hist[code[j] >> 16], 1);
+    entries[at] = ((uint64_t)(code[j] & 0xffffu) << 32) | (uint32_t)i;
+  }
+}
+
+// Pass 3: one workgroup per brick: max index per voxel in LDS, then the
+// brick's slice of the dense table (-1 = empty) and flags[rep] = 1.
+__global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __restrict__ entries,
+                                                              const int32_t* __restrict__ boff, VoxelGeom g,
+                                                              Bricks b, int32_t* __restrict__ table,
+                                                              uint8_t* __restrict__ flags) {
+  __shared__ int32_t tab[1 << kMaxBrickBits];
+  const int nloc = 1 << (b.sx + b.sy + b.sz);
+  for (int k = threadIdx.x; k < nloc; k += kReduceBlock) tab[k] = -1;
+  __syncthreads();
+  const int bk = blockIdx.x;
+  const int32_t e0 = boff[bk], e1 = boff[bk + 1];
+  for (int32_t e = e0 + threadIdx.x; e < e1; e += kReduceBlock) {
+    const uint64_t w = entries[e];
+    atomicMax(&tab[(int)(w >> 32)], (int32_t)(uint32_t)w);
+  }
+  __syncthreads();
+  const int bx = bk % b.nbx, by = (bk / b.nbx) % b.nby, bz = bk / (b.nbx * b.nby);
+  for (int k = threadIdx.x; k < nloc; k += kReduceBlock) {
+    const int x = (bx << b.sx) + (k & ((1 << b.sx) - 1));
+    const int y = (by << b.sy) + ((k >> b.sx) & ((1 << b.sy) - 1));
+    const int z = (bz << b.sz) + (k >> (b.sx + b.sy));
+    if (x >= g.nx || y >= g.ny || z >= g.nz) continue;
+    const int32_t r = tab[k];
+    table[x + (int64_t)g.nx * (y + (int64_t)g.ny * z)] = r;
+    if (r >= 0) flags[r] = 1;
+  }
+}
+
+// Brick shape: 2^bits voxels, split over the axes by repeatedly doubling the
+// axis with the most bricks left; nb = 0 when the grid needs more than
+// kMaxBuckets bricks (the plain dense path handles it).
+static Bricks plan_bricks(int nx, int ny, int nz) {
+  Bricks b{};
+  for (int bits = 12; bits <= kMaxBrickBits; ++bits) {
+    int sh[3] = {0, 0, 0};
+    const int64_t d[3] = {nx, ny, nz};
+    for (int it = 0; it < bits; ++it) {
+      int best = -1;
+      int64_t left = 1;
+      for (int a = 0; a < 3; ++a) {
+        const int64_t l = (d[a] + (1ll << sh[a]) - 1) >> sh[a];
+        if (l > left) {
+          left = l;
+          best = a;
+        }
+      }
+      if (best < 0) break;
+      ++sh[best];
+    }
+    int64_t nb[3];
+    for (int a = 0; a < 3; ++a) nb[a] = (d[a] + (1ll << sh[a]) - 1) >> sh[a];
+    const int64_t total = nb[0] * nb[1] * nb[2];
+    if (total <= kMaxBuckets) {
+      b = Bricks{sh[0], sh[1], sh[2], (int)nb[0], (int)nb[1], (int)nb[2], (int)total};
+      return b;
+    }
+  }
+  return b;
 }
 
 __global__ void __launch_bounds__(kBlock) k_voxel_assign_hash(const float* __restrict__ xyz, int64_t n,
@@ -159,6 +325,10 @@ static int64_t hash_cap(int64_t n) {
 }
 
 struct VoxelWs {
+  uint64_t* entries;           // brick-binned (local, index) pairs
+  int32_t* bcount;             // brick counts and cursors (padded), offsets
+  int32_t* boff;
+  int32_t* bcur;
   int32_t* table;              // dense rep or hash rep
   unsigned long long* keys;    // hash keys
   int32_t* vid;
@@ -177,10 +347,14 @@ static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
   char* tb = ar.take<char>(table_bytes);
   w->table = reinterpret_cast<int32_t*>(tb);
   w->keys = tb ? reinterpret_cast<unsigned long long*>(tb + Arena::align(hc * sizeof(int32_t))) : nullptr;
+  w->entries = ar.take<uint64_t>(n);
+  w->bcount = ar.take<int32_t>((kMaxBuckets + 1) * kCtrPad);
+  w->boff = ar.take<int32_t>(kMaxBuckets + 1);
+  w->bcur = ar.take<int32_t>((kMaxBuckets + 1) * kCtrPad);
   w->vid = ar.take<int32_t>(n);
   w->flags = ar.take<uint8_t>(n + 16);
   w->pos = ar.take<int32_t>(n);
-  w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(n));
+  w->scan_tmp = ar.take<int32_t>(std::max<size_t>(compact_workspace_ints(n), scan_workspace_ints(kMaxBuckets + 1)));
   w->aabb = ar.take<char>(aabb_ws_bytes(n));
   w->mm = ar.take<double>(8);
   w->count = ar.take<int64_t>(4);
@@ -255,22 +429,43 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
   for (int attempt = 0; attempt < 2; ++attempt) {
     int64_t nslots;
     O3DX_HIP(hipMemsetAsync(w.count, 0, 4 * sizeof(int64_t), s));
-    if (dense) {
+    const Bricks bricks = dense ? plan_bricks(g.nx, g.ny, g.nz) : Bricks{};
+    if (dense && bricks.nb > 0 && !getenv("O3DX_VOXEL_PLAIN")) {
       nslots = (int64_t)nvox;
-      O3DX_HIP(hipMemsetAsync(w.table, 0xFF, nslots * sizeof(int32_t), s));
+      const unsigned nblk = (unsigned)((n + kBinChunk - 1) / kBinChunk);
       KTimer kt("voxel_assign", s);
-      hipLaunchKernelGGL(k_voxel_assign_dense, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.table, w.vid,
-                         reinterpret_cast<int*>(w.count + 1));
-      hipLaunchKernelGGL(k_voxel_settle, dim3(grid), dim3(kBlock), 0, s, w.vid, n, w.table);
+      O3DX_HIP(hipMemsetAsync(w.bcount, 0, (size_t)bricks.nb * kCtrPad * sizeof(int32_t), s));
+      O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
+      hipLaunchKernelGGL(k_vbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bcount,
+                         (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
+      const unsigned gb = (unsigned)((bricks.nb + 255) / 256);
+      hipLaunchKernelGGL(k_vbin_unpad, dim3(gb), dim3(256), 0, s, w.bcount, bricks.nb, w.bcur);
+      O3DX_TRY(exclusive_scan_i32(w.bcur, w.boff, bricks.nb, w.scan_tmp, s));
+      hipLaunchKernelGGL(k_vbin_pad, dim3(gb), dim3(256), 0, s, w.boff, bricks.nb, w.bcount);
+      hipLaunchKernelGGL(k_vbin_scatter, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bcount,
+                         w.entries);
+      hipLaunchKernelGGL(k_vbin_reduce, dim3(bricks.nb), dim3(kReduceBlock), 0, s, w.entries, w.boff, g, bricks,
+                         w.table, w.flags);
+      kt.stop();
+      KTimer kc("voxel_compact", s);
+      O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
+                             w.scan_tmp, s));
     } else {
-      nslots = hash_cap(n);
-      O3DX_HIP(hipMemsetAsync(w.table, 0xFF, nslots * sizeof(int32_t), s));
-      O3DX_HIP(hipMemsetAsync(w.keys, 0xFF, nslots * sizeof(uint64_t), s));
-      KTimer kt("voxel_assign", s);
-      hipLaunchKernelGGL(k_voxel_assign_hash, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.keys, w.table,
-                         (uint32_t)(nslots - 1), w.vid, reinterpret_cast<int*>(w.count + 1));
-    }
-    {
+      if (dense) {
+        nslots = (int64_t)nvox;
+        O3DX_HIP(hipMemsetAsync(w.table, 0xFF, nslots * sizeof(int32_t), s));
+        KTimer kt("voxel_assign", s);
+        hipLaunchKernelGGL(k_voxel_assign_dense, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.table, w.vid,
+                           reinterpret_cast<int*>(w.count + 1));
+        hipLaunchKernelGGL(k_voxel_settle, dim3(grid), dim3(kBlock), 0, s, w.vid, n, w.table);
+      } else {
+        nslots = hash_cap(n);
+        O3DX_HIP(hipMemsetAsync(w.table, 0xFF, nslots * sizeof(int32_t), s));
+        O3DX_HIP(hipMemsetAsync(w.keys, 0xFF, nslots * sizeof(uint64_t), s));
+        KTimer kt("voxel_assign", s);
+        hipLaunchKernelGGL(k_voxel_assign_hash, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.keys, w.table,
+                           (uint32_t)(nslots - 1), w.vid, reinterpret_cast<int*>(w.count + 1));
+      }
       KTimer kt("voxel_compact", s);
       O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
       hipLaunchKernelGGL(k_voxel_mark, dim3(grid_for(nslots, kBlock, 8192)), dim3(kBlock), 0, s, w.table, nslots,
