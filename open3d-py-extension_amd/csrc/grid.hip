@@ -1062,39 +1062,57 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Rows of the (2S+1)^3 cube, four rows at a time: each lane loads one
-// candidate of each of the four rows (four independent loads in flight),
-// 64 candidates per row per step; `valid` marks lanes past a row's end.
+// Rows of the (2S+1)^3 cube (S <= 3: one lane per row) into the wave's LDS
+// row table: ra = first cell-sorted position, rp = prefix of the row lengths.
+// Returns the cube's candidate count.  One round of loads, then every scan
+// walks the rows' points as one flat range.
+constexpr int kWaveMaxS = 3;
+
+__device__ __forceinline__ int wave_rows(const GridView& g, int cx, int cy, int cz, int S, int lane,
+                                         int32_t* __restrict__ ra, int32_t* __restrict__ rp) {
+  const int side = 2 * S + 1, nr = side * side;
+  int a = 0, len = 0;
+  if (lane < nr) {
+    const int z = cz + lane / side - S, y = cy + lane % side - S;
+    if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
+      const int rb = g.nx * (y + g.ny * z);
+      a = g.start[rb + max(cx - S, 0)];
+      len = g.start[rb + min(cx + S, g.nx - 1) + 1] - a;
+    }
+  }
+  const int inc = wave_incl_scan(len);
+  if (lane < nr) {
+    ra[lane] = a;
+    rp[lane + 1] = inc;
+  }
+  if (lane == 0) rp[0] = 0;
+  wave_sync();
+  return __shfl(inc, 63, 64);
+}
+
+// The cube's candidates as one flat range, 256 per step (four independent
+// loads in flight per lane); each lane's row cursor only moves forward.
+// `valid` marks lanes past the end; `pp` is the candidate's position.
 #define O3DX_WAVE_SCAN(S, BODY)                                                  \
   {                                                                              \
-    const int x0_ = max(cx - (S), 0), x1_ = min(cx + (S), g.nx - 1);             \
-    const int side_ = 2 * (S) + 1;                                               \
-    for (int r0_ = 0; r0_ < side_ * side_; r0_ += 4) {                           \
-      int a_[4], e_[4];                                                          \
-      int len_ = 0;                                                              \
+    int row_ = 0;                                                                \
+    for (int b_ = 0; b_ < ncand; b_ += 256) {                                    \
+      float4 v_[4];                                                              \
+      int p_[4];                                                                 \
       _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
-        const int r_ = r0_ + u_;                                                 \
-        const int z_ = cz + r_ / side_ - (S), y_ = cy + r_ % side_ - (S);        \
-        a_[u_] = e_[u_] = 0;                                                     \
-        if (r_ < side_ * side_ && z_ >= 0 && z_ < g.nz && y_ >= 0 && y_ < g.ny) { \
-          const int rb_ = g.nx * (y_ + g.ny * z_);                               \
-          a_[u_] = g.start[rb_ + x0_];                                           \
-          e_[u_] = g.start[rb_ + x1_ + 1];                                       \
+        const int f_ = b_ + u_ * 64 + lane;                                      \
+        p_[u_] = -1;                                                             \
+        if (f_ < ncand) {                                                        \
+          while (rp[row_ + 1] <= f_) ++row_;                                     \
+          p_[u_] = ra[row_] + (f_ - rp[row_]);                                   \
         }                                                                        \
-        len_ = max(len_, e_[u_] - a_[u_]);                                       \
+        v_[u_] = g.pts[p_[u_] >= 0 ? p_[u_] : 0];                                \
       }                                                                          \
-      for (int b_ = 0; b_ < len_; b_ += 64) {                                    \
-        float4 v_[4];                                                            \
-        _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                       \
-          const int p_ = a_[u_] + b_ + lane;                                     \
-          v_[u_] = g.pts[p_ < e_[u_] ? p_ : 0];                                  \
-        }                                                                        \
-        _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                       \
-          const int pp = a_[u_] + b_ + lane;                                     \
-          const bool valid = pp < e_[u_];                                        \
-          const float d2 = dist2_f32(q, v_[u_].x, v_[u_].y, v_[u_].z);           \
-          BODY                                                                   \
-        }                                                                        \
+      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+        const int pp = p_[u_];                                                   \
+        const bool valid = pp >= 0;                                              \
+        const float d2 = dist2_f32(q, v_[u_].x, v_[u_].y, v_[u_].z);             \
+        BODY                                                                     \
       }                                                                          \
     }                                                                            \
   }
@@ -1102,6 +1120,7 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
 template <int KMAX>
 __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const float* __restrict__ prior,
                                            float* __restrict__ out, int64_t s, int lane, int32_t* sel, int32_t* bnd,
+                                           int32_t* __restrict__ ra, int32_t* __restrict__ rp,
                                            int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int s0) {
   const float4 q = g.pts[s];
   int cx, cy, cz;
@@ -1111,13 +1130,16 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   int S = s0;
   float R2 = 0.f;
   RegHist<false> hist;
+  int ncand = 0;
   for (;; ++S) {
-    if (S >= rmax) {  // shells would cover the whole grid: leave it to the exact path
+    if (S >= rmax || S > kWaveMaxS) {  // beyond one lane per row, or the whole grid: the exact path
       fb = true;
       break;
     }
     const double R = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, S) - g.slack;
     if (R <= 0.0) continue;
+    wave_sync();  // the previous shell's row table is no longer read
+    ncand = wave_rows(g, cx, cy, cz, S, lane, ra, rp);
     R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
     const float scale = (float)kHistBins / R2;
     hist.zero();
@@ -1256,11 +1278,13 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) k_normals_knn_wave(
     int32_t* __restrict__ fb_len, int s0) {
   __shared__ int32_t sel[kWavesPerBlock][KMAX];
   __shared__ int32_t bnd[kWavesPerBlock][kWaveBnd];
+  __shared__ int32_t ra[kWavesPerBlock][64];
+  __shared__ int32_t rp[kWavesPerBlock][65];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t lim = in_list ? (int64_t)*in_len : g.n;
   for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wv; t < lim; t += (int64_t)gridDim.x * kWavesPerBlock) {
     const int64_t s = in_list ? (int64_t)__builtin_amdgcn_readfirstlane(in_list[t]) : t;
-    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], fb_list, fb_len, s0);
+    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], ra[wv], rp[wv], fb_list, fb_len, s0);
   }
 }
 
