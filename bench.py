@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU (C2: 10M)")
     ap.add_argument("--knn", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--sorted-grid", action="store_true",
+                    help="normals sort the representatives into their own grid (no voxel table hand-over)")
     ap.add_argument("--cpu-n", type=int, default=2_000_000, help="CPU baseline sample size")
     ap.add_argument("--no-secondary", action="store_true", help="skip the ICP / RANSAC figures")
     ap.add_argument("--icp-n", type=int, default=10_000_000)
@@ -218,9 +220,13 @@ def main():
     pts[:, 0] += float(rank)
     torch.cuda.synchronize(dev)
 
+    keep = not args.sorted_grid
+
     def step():
-        out = ops.voxel_down_sample(pts, vs)
-        nrm = ops.estimate_normals(out["rep_xyz"], knn=args.knn)
+        # PointCloud.voxel_down_sample(vs).estimate_normals(): the voxel table
+        # of the first call is the search grid of the second
+        out = ops.voxel_down_sample(pts, vs, keep_grid=keep)
+        nrm = ops.estimate_normals(out["rep_xyz"], knn=args.knn, voxel_grid=out.get("voxel_grid"))
         return out["rep_idx"].numel(), nrm
 
     for _ in range(args.warmup):

@@ -123,6 +123,29 @@ int o3dx_voxel_down_sample(const float* xyz_dev, int64_t n,
                            int32_t* cubic_id_dev, void* ws, size_t ws_bytes,
                            void* stream);
 
+/* Voxel down-sample that also keeps its voxel grid for a following
+ * estimate_normals on the representatives (the pipeline
+ * pcd.voxel_down_sample(vs).estimate_normals(), reference PointCloud.py:361,
+ * :68).  o3dx_voxel_grid_cells(n, min, max, vs): the number of voxels nvox of
+ * the dense voxel table for these bounds (host arithmetic), 0 when the grid
+ * is too sparse to keep.  o3dx_voxel_down_sample_grid: same outputs as
+ * o3dx_voxel_down_sample (explicit bounds required), plus
+ *   voxel_pts_dev[0..4 nvox)  per voxel (x, y, z, output row as int32 bits)
+ *                             of its representative, row -1 when empty
+ *   geom_host[12]             {min_bound xyz, voxel_size, nx, ny, nz, valid,
+ *                              occupied 2^3-voxel cells, 0, 0, nvox}
+ * valid = 0 when the table could not be kept (points outside the bounds). */
+int64_t o3dx_voxel_grid_cells(int64_t n, const double* min_bound_host,
+                              const double* max_bound_host, double voxel_size);
+int o3dx_voxel_down_sample_grid(const float* xyz_dev, int64_t n,
+                                const double* min_bound_host,
+                                const double* max_bound_host, double voxel_size,
+                                int32_t* rep_idx_dev, float* rep_xyz_dev,
+                                int64_t* m_host, int32_t* voxel_of_point_dev,
+                                int32_t* cubic_id_dev, float* voxel_pts_dev,
+                                int64_t voxel_cells, double* geom_host,
+                                void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- normals
  * Replaces o3d PointCloud.estimate_normals(search_param,
  * fast_normal_computation=True) (reference PointCloud.py:68-73, used by
@@ -138,6 +161,20 @@ int o3dx_estimate_normals(const float* xyz_dev, int64_t n, int mode, int knn,
                           double radius, const float* prior_normals_dev,
                           float* normals_out_dev, void* ws, size_t ws_bytes,
                           void* stream);
+
+/* estimate_normals of the m representatives of o3dx_voxel_down_sample_grid
+ * (rep_xyz_dev, voxel_pts_dev, geom_host from that call): the search grid is
+ * read off the voxel table (cells of b^3 voxels, b in 1..4 chosen from the
+ * occupied 2^3-cell count) instead of being rebuilt by sorting; same results as
+ * o3dx_estimate_normals(rep_xyz_dev, m, ...) up to float64 summation order.
+ * Workspace: o3dx_normals_workspace_bytes(m).  No host synchronisation. */
+int o3dx_estimate_normals_voxel(const double* geom_host,
+                                const float* voxel_pts_dev,
+                                const float* rep_xyz_dev, int64_t m, int mode,
+                                int knn, double radius,
+                                const float* prior_normals_dev,
+                                float* normals_out_dev, void* ws,
+                                size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- kNN search
  * Batched form of KDTreeFlann.search_knn_vector_3d / search_hybrid_vector_3d

@@ -1063,21 +1063,34 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
 }
 
 // Rows of the (2S+1)^3 cube (S <= 3: one lane per row) into the wave's LDS
-// row table: ra = first cell-sorted position, rp = prefix of the row lengths.
-// Returns the cube's candidate count.  One round of loads, then every scan
-// walks the rows' points as one flat range.
+// row table: ra = first cell-sorted position, rp = prefix of the row lengths;
+// each row is trimmed to the x-cells whose boxes (widened by 2 slack) come
+// closer to q than sqrt(r2), rows that do not are dropped.  Returns the
+// candidate count.  One round of loads, then every scan walks the rows'
+// points as one flat range.
 constexpr int kWaveMaxS = 3;
 
-__device__ __forceinline__ int wave_rows(const GridView& g, int cx, int cy, int cz, int S, int lane,
-                                         int32_t* __restrict__ ra, int32_t* __restrict__ rp) {
+__device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int cx, int cy, int cz, int S, float r2,
+                                         int lane, int32_t* __restrict__ ra, int32_t* __restrict__ rp) {
   const int side = 2 * S + 1, nr = side * side;
   int a = 0, len = 0;
   if (lane < nr) {
     const int z = cz + lane / side - S, y = cy + lane % side - S;
     if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
-      const int rb = g.nx * (y + g.ny * z);
-      a = g.start[rb + max(cx - S, 0)];
-      len = g.start[rb + min(cx + S, g.nx - 1) + 1] - a;
+      const float y0 = g.oy + (float)y * g.h, z0 = g.oz + (float)z * g.h, sl = 2.0f * g.slack;
+      const float dy = fmaxf(fmaxf(y0 - q.y, q.y - (y0 + g.h)) - sl, 0.0f);
+      const float dz = fmaxf(fmaxf(z0 - q.z, q.z - (z0 + g.h)) - sl, 0.0f);
+      const float rem = r2 - fmaf(dy, dy, dz * dz);
+      if (rem > 0.0f) {
+        const float rx = sqrtf(rem) + sl;
+        const int x0 = max(max(cx - S, 0), (int)floorf((q.x - rx - g.ox) * g.inv_h));
+        const int x1 = min(min(cx + S, g.nx - 1), (int)floorf((q.x + rx - g.ox) * g.inv_h));
+        if (x0 <= x1) {
+          const int rb = g.nx * (y + g.ny * z);
+          a = g.start[rb + x0];
+          len = g.start[rb + x1 + 1] - a;
+        }
+      }
     }
   }
   const int inc = wave_incl_scan(len);
@@ -1131,16 +1144,25 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   float R2 = 0.f;
   RegHist<false> hist;
   int ncand = 0;
-  for (;; ++S) {
+  // A query the tile handed on (s0 = 2) rarely needs more than the shell-1
+  // reach + h/2: that ball first (fewer rows and x-cells of the 5^3 cube),
+  // then the whole shell.
+  bool trial = s0 == 2;
+  for (;;) {
     if (S >= rmax || S > kWaveMaxS) {  // beyond one lane per row, or the whole grid: the exact path
       fb = true;
       break;
     }
-    const double R = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, S) - g.slack;
-    if (R <= 0.0) continue;
-    wave_sync();  // the previous shell's row table is no longer read
-    ncand = wave_rows(g, cx, cy, cz, S, lane, ra, rp);
+    double R = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, S) - g.slack;
+    if (trial) R = fmin(R, cube_reach(g, q.x, q.y, q.z, cx, cy, cz, S - 1) - g.slack + 0.5 * (double)g.h);
+    if (R <= 0.0) {
+      ++S;
+      trial = false;
+      continue;
+    }
     R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
+    wave_sync();  // the previous shell's row table is no longer read
+    ncand = wave_rows(g, q, cx, cy, cz, S, R2, lane, ra, rp);
     const float scale = (float)kHistBins / R2;
     hist.zero();
     int tot = 0;
@@ -1154,6 +1176,10 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
       break;
     }
     if (tot >= kneed) break;
+    if (trial)
+      trial = false;
+    else
+      ++S;
   }
   float lo = 0.f, hi = R2, L = 0.f, U = 0.f;
   int below = 0;
@@ -1362,54 +1388,141 @@ static double occ_for(int mode, int k) {
   return std::max(2.0, k / 4.0);
 }
 
-}  // namespace o3dx
+// ------------------------------------------------------ grid from voxels
+// Search grid read off a voxel table (o3dx_voxel_down_sample_grid): cell =
+// b^3 voxels, origin = the voxel grid's min_bound, each cell's points in voxel
+// order (x fastest) — a count and an emit pass over the table, no sort.  The
+// cell of a point is fixed by its float64 voxel key; the float32 cell test of
+// the search kernels sees the same faces up to rounding, covered by `slack`
+// exactly as for grid_build's own float32 assignment.
+template <int B>
+__global__ void __launch_bounds__(kBlock) k_vgrid_count(const float4* __restrict__ vox, int vnx, int vny, int vnz,
+                                                        GridView g, int32_t* __restrict__ count) {
+  const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+    const int cx = (int)(c % g.nx), cy = (int)((c / g.nx) % g.ny), cz = (int)(c / ((int64_t)g.nx * g.ny));
+    int k = 0;
+    for (int dz = 0; dz < B; ++dz)
+      for (int dy = 0; dy < B; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < B; ++dx) {
+          const int x = cx * B + dx, y = cy * B + dy, z = cz * B + dz;
+          if (x < vnx && y < vny && z < vnz)
+            k += __float_as_int(vox[x + (int64_t)vnx * (y + (int64_t)vny * z)].w) >= 0;
+        }
+    count[c] = k;
+  }
+}
 
-using namespace o3dx;
+template <int B>
+__global__ void __launch_bounds__(kBlock) k_vgrid_emit(const float4* __restrict__ vox, int vnx, int vny, int vnz,
+                                                       GridView g, float4* __restrict__ pts) {
+  const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+    const int cx = (int)(c % g.nx), cy = (int)((c / g.nx) % g.ny), cz = (int)(c / ((int64_t)g.nx * g.ny));
+    int p = g.start[c];
+    for (int dz = 0; dz < B; ++dz)
+      for (int dy = 0; dy < B; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < B; ++dx) {
+          const int x = cx * B + dx, y = cy * B + dy, z = cz * B + dz;
+          if (x >= vnx || y >= vny || z >= vnz) continue;
+          const float4 v = vox[x + (int64_t)vnx * (y + (int64_t)vny * z)];
+          if (__float_as_int(v.w) >= 0) pts[p++] = v;
+        }
+  }
+}
 
-extern "C" int o3dx_set_search_stats(int enable) {
-  if (enable && !g_stats) {
-    if (hipMalloc(&g_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {
-      g_stats = nullptr;
-      return fail(O3DX_EIO, "stats buffer allocation failed");
+// 0: built; 1: no usable voxel grid (caller sorts the points instead).
+static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, double target_occ, void* ws,
+                            size_t ws_bytes, hipStream_t s, GridBuild* out) {
+  if (!vox || geom[7] != 1.0 || getenv("O3DX_NO_VOXEL_GRID")) return 1;
+  const int vn[3] = {(int)geom[4], (int)geom[5], (int)geom[6]};
+  const double vs = geom[3];
+  GridLayout L = grid_layout(n);
+  if (ws_bytes < L.total) return fail(O3DX_ENOMEM, "grid workspace too small (need %zu)", L.total);
+  // b: mean points per occupied cell closest to the target.  One rep per
+  // occupied voxel and the occupied 2^3 cells give the cloud's local
+  // dimension D = log2(m / occ2); a cell of b^3 voxels then holds ~b^D reps.
+  const double occ2 = geom[8];
+  if (!(occ2 > 0.0)) return 1;
+  const double D = std::min(3.0, std::max(1.0, std::log2((double)n / occ2)));
+  int b = 0;
+  double best = 0.0;
+  for (int c = 1; c <= 4; ++c) {
+    int64_t cells = 1;
+    for (int a = 0; a < 3; ++a) cells *= (vn[a] + c - 1) / c;
+    if (cells > cap_cells(n)) continue;
+    const double err = std::fabs(D * std::log((double)c) - std::log(target_occ));
+    if (b == 0 || err < best) {
+      b = c;
+      best = err;
     }
   }
-  g_stats_on = enable != 0;
-  if (g_stats && hipMemset(g_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess)
-    return fail(O3DX_EIO, "stats reset failed");
+  if (const char* e = getenv("O3DX_VOXEL_GRID_B")) b = std::max(1, std::min(4, atoi(e)));  // tuning override
+  if (b == 0) return 1;
+  char* w = (char*)ws;
+  GridBuild& G = *out;
+  G.pts = (float4*)(w + L.pts);
+  G.start = (int32_t*)(w + L.start);
+  G.count = (int32_t*)(w + L.count);
+  G.cell = (int32_t*)(w + L.cell);
+  G.rank = (int32_t*)(w + L.rank);
+  G.scan_tmp = (int32_t*)(w + L.scan);
+  G.aabb_ws = w + L.aabb;
+  G.mm = (double*)(w + L.mm);
+  G.scratch = (int64_t*)(w + L.scratch);
+  G.cap_cells = cap_cells(n);
+  G.extra = nullptr;
+  GridView& g = G.view;
+  const double h = b * vs;
+  double maxabs = 0.0, maxext = 0.0;
+  for (int a = 0; a < 3; ++a) {
+    const double ext = vn[a] * vs;
+    maxabs = std::max(maxabs, std::max(std::fabs(geom[a]), std::fabs(geom[a] + ext)));
+    maxext = std::max(maxext, ext);
+  }
+  g.pts = G.pts;
+  g.start = G.start;
+  g.ox = (float)geom[0];
+  g.oy = (float)geom[1];
+  g.oz = (float)geom[2];
+  g.h = (float)h;
+  g.inv_h = (float)(1.0 / h);
+  g.nx = (vn[0] + b - 1) / b;
+  g.ny = (vn[1] + b - 1) / b;
+  g.nz = (vn[2] + b - 1) / b;
+  g.n = n;
+  g.stats = search_stats_ptr();
+  g.slack = (float)(32.0 * std::ldexp(1.0, -24) * (maxabs + maxext) + 1e-6 * h);
+  g.blocked = 0;
+  g.bnx = (g.nx + 7) / 8;
+  g.bny = (g.ny + 7) / 8;
+  const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
+  const unsigned gc = grid_for(nc, kBlock, 8192);
+  KTimer kt("grid_voxel", s);
+  switch (b) {
+#define O3DX_VGRID(BB)                                                                                          \
+  case BB:                                                                                                      \
+    hipLaunchKernelGGL(k_vgrid_count<BB>, dim3(gc), dim3(kBlock), 0, s, vox, vn[0], vn[1], vn[2], g, G.count);  \
+    O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));                                          \
+    hipLaunchKernelGGL(k_vgrid_emit<BB>, dim3(gc), dim3(kBlock), 0, s, vox, vn[0], vn[1], vn[2], g, G.pts);      \
+    break;
+    O3DX_VGRID(1)
+    O3DX_VGRID(2)
+    O3DX_VGRID(3)
+    O3DX_VGRID(4)
+#undef O3DX_VGRID
+  }
+  O3DX_HIP(hipGetLastError());
   return 0;
 }
 
-extern "C" int o3dx_search_stats(int64_t* out) {
-  if (!out) return fail(O3DX_EINVAL, "o3dx_search_stats: null output");
-  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (g_stats && hipDeviceSynchronize() == hipSuccess)
-    (void)hipMemcpy(v, g_stats, sizeof(v), hipMemcpyDeviceToHost);
-  for (int i = 0; i < 8; ++i) out[i] = (int64_t)v[i];
-  return 0;
-}
-
-extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
-  n = std::max<int64_t>(n, 1);
-  // grid rows (ny * nz) are bounded by the cell cap
-  const int64_t rows = cap_cells(n);
-  return grid_ws_bytes(n) + 3 * Arena::align((n + 3) * 4) + Arena::align((n / 64 + rows + 4) * 4) +
-         chunk_plan_ws_bytes(n, rows) + 4096;
-}
-
-extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,
-                                     const float* prior, float* out, void* ws, size_t ws_bytes, void* stream) {
-  if (n < 0 || (n > 0 && (!xyz || !out))) return fail(O3DX_EINVAL, "o3dx_estimate_normals: bad arguments");
-  if (mode != O3DX_SEARCH_KNN && mode != O3DX_SEARCH_RADIUS && mode != O3DX_SEARCH_HYBRID)
-    return fail(O3DX_EINVAL, "o3dx_estimate_normals: unknown search mode %d", mode);
-  if (mode != O3DX_SEARCH_RADIUS && (knn < 0 || knn > O3DX_MAX_KNN))
-    return fail(O3DX_ENOTSUP, "knn/max_nn %d outside [0, %d]", knn, O3DX_MAX_KNN);
-  if (mode != O3DX_SEARCH_KNN && !(radius > 0.0)) return fail(O3DX_EINVAL, "radius must be > 0");
-  if (!ws || ws_bytes < o3dx_normals_workspace_bytes(n)) return fail(O3DX_ENOMEM, "normals workspace too small");
-  if (n == 0) return 0;
-  hipStream_t s = as_stream(stream);
-  GridBuild G;
-  double min_h = (mode == O3DX_SEARCH_KNN) ? 0.0 : 0.0;
-  O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), min_h, ws, ws_bytes, s, &G));
+// The normals on a built grid: shared by o3dx_estimate_normals (grid sorted
+// from the points) and o3dx_estimate_normals_voxel (grid read off the voxel
+// table).  `xyz` is the caller's point array the grid's w fields index.
+static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, int knn, double radius,
+                           const float* prior, float* out, void* ws, size_t ws_bytes, hipStream_t s) {
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
   const int kneed = (int)std::min<int64_t>(knn, n);
   if (mode == O3DX_SEARCH_KNN && kneed >= 1 && !getenv("O3DX_NORMALS_TOPK")) {
@@ -1470,6 +1583,76 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
   }
   O3DX_HIP(hipGetLastError());
   return 0;
+}
+
+}  // namespace o3dx
+
+using namespace o3dx;
+
+extern "C" int o3dx_set_search_stats(int enable) {
+  if (enable && !g_stats) {
+    if (hipMalloc(&g_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {
+      g_stats = nullptr;
+      return fail(O3DX_EIO, "stats buffer allocation failed");
+    }
+  }
+  g_stats_on = enable != 0;
+  if (g_stats && hipMemset(g_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess)
+    return fail(O3DX_EIO, "stats reset failed");
+  return 0;
+}
+
+extern "C" int o3dx_search_stats(int64_t* out) {
+  if (!out) return fail(O3DX_EINVAL, "o3dx_search_stats: null output");
+  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g_stats && hipDeviceSynchronize() == hipSuccess)
+    (void)hipMemcpy(v, g_stats, sizeof(v), hipMemcpyDeviceToHost);
+  for (int i = 0; i < 8; ++i) out[i] = (int64_t)v[i];
+  return 0;
+}
+
+extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
+  n = std::max<int64_t>(n, 1);
+  // grid rows (ny * nz) are bounded by the cell cap
+  const int64_t rows = cap_cells(n);
+  return grid_ws_bytes(n) + 3 * Arena::align((n + 3) * 4) + Arena::align((n / 64 + rows + 4) * 4) +
+         chunk_plan_ws_bytes(n, rows) + 4096;
+}
+
+extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,
+                                     const float* prior, float* out, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || (n > 0 && (!xyz || !out))) return fail(O3DX_EINVAL, "o3dx_estimate_normals: bad arguments");
+  if (mode != O3DX_SEARCH_KNN && mode != O3DX_SEARCH_RADIUS && mode != O3DX_SEARCH_HYBRID)
+    return fail(O3DX_EINVAL, "o3dx_estimate_normals: unknown search mode %d", mode);
+  if (mode != O3DX_SEARCH_RADIUS && (knn < 0 || knn > O3DX_MAX_KNN))
+    return fail(O3DX_ENOTSUP, "knn/max_nn %d outside [0, %d]", knn, O3DX_MAX_KNN);
+  if (mode != O3DX_SEARCH_KNN && !(radius > 0.0)) return fail(O3DX_EINVAL, "radius must be > 0");
+  if (!ws || ws_bytes < o3dx_normals_workspace_bytes(n)) return fail(O3DX_ENOMEM, "normals workspace too small");
+  if (n == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  GridBuild G;
+  O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), 0.0, ws, ws_bytes, s, &G));
+  return normals_on_grid(G, xyz, n, mode, knn, radius, prior, out, ws, ws_bytes, s);
+}
+
+extern "C" int o3dx_estimate_normals_voxel(const double* geom, const float* voxel_pts, const float* xyz, int64_t n,
+                                           int mode, int knn, double radius, const float* prior, float* out,
+                                           void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || (n > 0 && (!xyz || !out || !geom))) return fail(O3DX_EINVAL, "o3dx_estimate_normals_voxel: bad arguments");
+  if (mode != O3DX_SEARCH_KNN && mode != O3DX_SEARCH_RADIUS && mode != O3DX_SEARCH_HYBRID)
+    return fail(O3DX_EINVAL, "o3dx_estimate_normals_voxel: unknown search mode %d", mode);
+  if (mode != O3DX_SEARCH_RADIUS && (knn < 0 || knn > O3DX_MAX_KNN))
+    return fail(O3DX_ENOTSUP, "knn/max_nn %d outside [0, %d]", knn, O3DX_MAX_KNN);
+  if (mode != O3DX_SEARCH_KNN && !(radius > 0.0)) return fail(O3DX_EINVAL, "radius must be > 0");
+  if (!ws || ws_bytes < o3dx_normals_workspace_bytes(n)) return fail(O3DX_ENOMEM, "normals workspace too small");
+  if (n == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  GridBuild G;
+  const int rc = grid_from_voxels(geom, reinterpret_cast<const float4*>(voxel_pts), n, occ_for(mode, knn), ws, ws_bytes,
+                                  s, &G);
+  if (rc == 1) O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), 0.0, ws, ws_bytes, s, &G));  // no usable voxel grid
+  else if (rc != 0) return rc;
+  return normals_on_grid(G, xyz, n, mode, knn, radius, prior, out, ws, ws_bytes, s);
 }
 
 extern "C" size_t o3dx_knn_workspace_bytes(int64_t n) { return grid_ws_bytes(n) + 1024; }

@@ -317,6 +317,53 @@ __global__ void __launch_bounds__(kBlock) k_voxel_trace(const float* __restrict_
   }
 }
 
+// Kept voxel grid: vox[v] = (x, y, z, output row as int bits) of voxel v's
+// representative, w = -1 for an empty voxel (the buffer is 0xFF-filled).
+// Thread per representative (its row is j): the gather of rep_xyz plus one
+// 16-byte scatter, so the normals later read the reps in voxel order.
+__global__ void __launch_bounds__(kBlock) k_gather_vox(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
+                                                       int64_t m, VoxelGeom g, float* __restrict__ rep_xyz,
+                                                       float4* __restrict__ vox) {
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const P3 q = p[idx[j]];
+    if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q;
+    double r[3];
+    int v[3];
+    voxel_ref(q, g, r, v);  // inside the grid: the dense path accepted every point
+    vox[v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2])] = make_float4(q.x, q.y, q.z, __int_as_float((int)j));
+  }
+}
+
+// Occupied cells of 2^3 voxels (thread per cell, one atomic per block): with
+// one rep per occupied voxel, m / occ2 gives the cloud's local dimension, from
+// which the normals size their search cell.
+__global__ void __launch_bounds__(kBlock) k_voxel_occ2(const int32_t* __restrict__ table, VoxelGeom g,
+                                                       unsigned long long* __restrict__ occ2) {
+  const int cx = (g.nx + 1) / 2, cy = (g.ny + 1) / 2, cz = (g.nz + 1) / 2;
+  const int64_t nc = (int64_t)cx * cy * cz;
+  unsigned long long c = 0;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nc; t += (int64_t)gridDim.x * blockDim.x) {
+    const int x0 = (int)(t % cx) * 2, y0 = (int)((t / cx) % cy) * 2, z0 = (int)(t / ((int64_t)cx * cy)) * 2;
+    bool any = false;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const int x = x0 + (d & 1), y = y0 + ((d >> 1) & 1), z = z0 + (d >> 2);
+      if (x < g.nx && y < g.ny && z < g.nz) any |= table[x + (int64_t)g.nx * (y + (int64_t)g.ny * z)] >= 0;
+    }
+    c += any;
+  }
+  __shared__ unsigned long long sh[kBlock / 64];
+  c = wave_sum(c);
+  if (lane_id() == 0) sh[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += sh[w];
+    if (t) atomicAdd(occ2, t);  // one per block: the grid is capped at 1024 blocks
+  }
+}
+
 static int64_t dense_cap(int64_t n) { return 2 * n + (1 << 20); }
 static int64_t hash_cap(int64_t n) {
   int64_t t = 1024;
@@ -337,7 +384,7 @@ struct VoxelWs {
   int32_t* scan_tmp;
   char* aabb;
   double* mm;
-  int64_t* count;  // [0] = m, [1] = err (as int)
+  int64_t* count;  // [0] = m, [1] = err (as int), [2] occupied 2^3 cells
 };
 
 static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
@@ -357,7 +404,7 @@ static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
   w->scan_tmp = ar.take<int32_t>(std::max<size_t>(compact_workspace_ints(n), scan_workspace_ints(kMaxBuckets + 1)));
   w->aabb = ar.take<char>(aabb_ws_bytes(n));
   w->mm = ar.take<double>(8);
-  w->count = ar.take<int64_t>(4);
+  w->count = ar.take<int64_t>(8);
   return ar.used;
 }
 
@@ -372,10 +419,27 @@ extern "C" size_t o3dx_voxel_workspace_bytes(int64_t n) {
   return carve(ar, std::max<int64_t>(n, 1), &w) + Arena::align(hash_cap(std::max<int64_t>(n, 1)) * 4) + 1024;
 }
 
-extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double* min_bound_host,
-                                      const double* max_bound_host, double voxel_size, int32_t* rep_idx,
-                                      float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point, int32_t* cubic_id,
-                                      void* ws, size_t ws_bytes, void* stream) {
+static void voxel_dims(const double mn[3], const double mx[3], double vs, double dims[3]) {
+  for (int a = 0; a < 3; ++a) dims[a] = std::floor(std::max(0.0, mx[a] - mn[a]) / vs) + 1.0;
+}
+
+extern "C" int64_t o3dx_voxel_grid_cells(int64_t n, const double* min_bound_host, const double* max_bound_host,
+                                         double voxel_size) {
+  if (!min_bound_host || !max_bound_host || !(voxel_size > 0.0) || n <= 0) return 0;
+  double dims[3];
+  voxel_dims(min_bound_host, max_bound_host, voxel_size, dims);
+  const double nvox = dims[0] * dims[1] * dims[2];
+  if (!(nvox <= (double)dense_cap(n))) return 0;
+  if (plan_bricks((int)dims[0], (int)dims[1], (int)dims[2]).nb == 0) return 0;
+  return (int64_t)nvox;
+}
+
+static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host, const double* max_bound_host,
+                      double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point,
+                      int32_t* cubic_id, float* vox, int64_t vox_cap, double* geom, void* ws, size_t ws_bytes,
+                      void* stream) {
+  if (geom)
+    for (int k = 0; k < 12; ++k) geom[k] = 0.0;
   if (n < 0 || (n > 0 && (!xyz || !rep_idx)) || !m_host)
     return fail(O3DX_EINVAL, "o3dx_voxel_down_sample: bad arguments");
   if (!(voxel_size > 0.0)) return fail(O3DX_EINVAL, "voxel_size <= 0.");
@@ -417,7 +481,7 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
   g.mnz = mn[2];
   g.vs = voxel_size;
   double dims[3];
-  for (int a = 0; a < 3; ++a) dims[a] = std::floor(std::max(0.0, mx[a] - mn[a]) / voxel_size) + 1.0;
+  voxel_dims(mn, mx, voxel_size, dims);
   double nvox = dims[0] * dims[1] * dims[2];
   bool dense = nvox <= (double)dense_cap(n);
   g.nx = (int)dims[0];
@@ -425,10 +489,12 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
   g.nz = (int)dims[2];
 
   const unsigned grid = grid_for(n, kBlock, 8192);
-  int64_t counts[2];
+  int64_t counts[3];
+  bool grid_kept = false;
   for (int attempt = 0; attempt < 2; ++attempt) {
+    grid_kept = false;
     int64_t nslots;
-    O3DX_HIP(hipMemsetAsync(w.count, 0, 4 * sizeof(int64_t), s));
+    O3DX_HIP(hipMemsetAsync(w.count, 0, 8 * sizeof(int64_t), s));
     const Bricks bricks = dense ? plan_bricks(g.nx, g.ny, g.nz) : Bricks{};
     if (dense && bricks.nb > 0 && !getenv("O3DX_VOXEL_PLAIN")) {
       nslots = (int64_t)nvox;
@@ -450,6 +516,13 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
       KTimer kc("voxel_compact", s);
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
                              w.scan_tmp, s));
+      if (vox && nslots == vox_cap) {
+        O3DX_HIP(hipMemsetAsync(vox, 0xFF, (size_t)nslots * 4 * sizeof(float), s));
+        const int64_t nc2 = (int64_t)((g.nx + 1) / 2) * ((g.ny + 1) / 2) * ((g.nz + 1) / 2);
+        hipLaunchKernelGGL(k_voxel_occ2, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table, g,
+                           reinterpret_cast<unsigned long long*>(w.count + 2));
+        grid_kept = true;
+      }
     } else {
       if (dense) {
         nslots = (int64_t)nvox;
@@ -473,7 +546,7 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
                              w.scan_tmp, s));
     }
-    O3DX_HIP(hipMemcpyAsync(counts, w.count, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    O3DX_HIP(hipMemcpyAsync(counts, w.count, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     O3DX_HIP(hipStreamSynchronize(s));
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
@@ -483,7 +556,15 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
   }
   const int64_t m = counts[0];
   *m_host = m;
-  if (rep_xyz && m > 0)
+  if (geom && grid_kept) {
+    const double gv[12] = {g.mnx, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny, (double)g.nz, 1.0,
+                           (double)counts[2], 0.0, 0.0, nvox};
+    for (int k = 0; k < 12; ++k) geom[k] = gv[k];
+  }
+  if (grid_kept && m > 0)
+    hipLaunchKernelGGL(k_gather_vox, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, xyz, rep_idx, m, g, rep_xyz,
+                       reinterpret_cast<float4*>(vox));
+  else if (rep_xyz && m > 0)
     hipLaunchKernelGGL(k_gather_xyz, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, xyz, rep_idx, m, rep_xyz);
   if ((voxel_of_point || cubic_id) && m > 0) {
     if (cubic_id) O3DX_HIP(hipMemsetAsync(cubic_id, 0xFF, (size_t)m * 8 * sizeof(int32_t), s));
@@ -492,4 +573,22 @@ extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double*
   }
   O3DX_HIP(hipGetLastError());
   return 0;
+}
+
+extern "C" int o3dx_voxel_down_sample(const float* xyz, int64_t n, const double* min_bound_host,
+                                      const double* max_bound_host, double voxel_size, int32_t* rep_idx,
+                                      float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point, int32_t* cubic_id,
+                                      void* ws, size_t ws_bytes, void* stream) {
+  return voxel_impl(xyz, n, min_bound_host, max_bound_host, voxel_size, rep_idx, rep_xyz, m_host, voxel_of_point,
+                    cubic_id, nullptr, 0, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int o3dx_voxel_down_sample_grid(const float* xyz, int64_t n, const double* min_bound_host,
+                                           const double* max_bound_host, double voxel_size, int32_t* rep_idx,
+                                           float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point,
+                                           int32_t* cubic_id, float* voxel_pts, int64_t voxel_cells,
+                                           double* geom_host, void* ws, size_t ws_bytes, void* stream) {
+  if (!voxel_pts || !geom_host) return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_grid: null voxel_pts / geom");
+  return voxel_impl(xyz, n, min_bound_host, max_bound_host, voxel_size, rep_idx, rep_xyz, m_host, voxel_of_point,
+                    cubic_id, voxel_pts, voxel_cells, geom_host, ws, ws_bytes, stream);
 }

@@ -254,8 +254,21 @@ class PointCloudBase:
         mode, knn, radius = resolve(param)
         x = self._dev_points()
         prior = self._normals if self.has_normals() else None
-        self._normals = ops.estimate_normals(x, mode=mode, knn=knn, radius=radius, prior=prior)
+        self._normals = ops.estimate_normals(x, mode=mode, knn=knn, radius=radius, prior=prior,
+                                             voxel_grid=self._kept_voxel_grid(x))
         return self
+
+    def _kept_voxel_grid(self, x):
+        """The voxel table of the voxel_down_sample that made this cloud, while
+        its points are unchanged (same tensor, no in-place writes)."""
+        kept = getattr(self, "_voxel_grid", None)
+        if kept is None:
+            return None
+        vg, pts, version = kept
+        if x is not pts or pts._version != version or vg.m != x.shape[0]:
+            self._voxel_grid = None
+            return None
+        return vg
 
     def segment_plane(self, thickness: float = 0.01, ransac_n: int = 3, num_iterations: int = 450,
                       probability: float = 0.99999999, seed=None, samples=None) -> Tuple[List, List[int]]:
@@ -587,8 +600,12 @@ class PointCloudUtility(PointCloudSelections):
         """Representatives only (no trace) — the fast path."""
         x = self._dev_points()
         mn, mx = self.get_aabb()
-        out = ops.voxel_down_sample(x, voxel_size, mn, mx, with_xyz=False)
-        return self._select_by_idx(out["rep_idx"])
+        out = ops.voxel_down_sample(x, voxel_size, mn, mx, with_xyz=False, keep_grid=True)
+        res = self._select_by_idx(out["rep_idx"])
+        if out["voxel_grid"] is not None and res._pts is not None:
+            # estimate_normals on the result reads its search grid off the voxel table
+            res._voxel_grid = (out["voxel_grid"], res._pts, res._pts._version)
+        return res
 
     def random_down_sample(self, down_sample_ratio: float = 0.1):
         if down_sample_ratio <= 0 or down_sample_ratio > 1:

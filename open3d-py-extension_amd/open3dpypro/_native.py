@@ -43,7 +43,10 @@ _SIGS = {
     "o3dx_aabb": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
     "o3dx_voxel_workspace_bytes": (_SZ, [_I64]),
     "o3dx_voxel_down_sample": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_voxel_grid_cells": (_I64, [_I64, _P, _P, _D]),
+    "o3dx_voxel_down_sample_grid": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P]),
     "o3dx_normals_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_estimate_normals_voxel": (_I32, [_P, _P, _P, _I64, _I32, _I32, _D, _P, _P, _P, _SZ, _P]),
     "o3dx_estimate_normals": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _SZ, _P]),
     "o3dx_knn_workspace_bytes": (_SZ, [_I64]),
     "o3dx_knn_search": (_I32, [_P, _I64, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),

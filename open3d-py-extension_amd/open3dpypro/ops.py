@@ -43,11 +43,14 @@ def aabb(xyz: torch.Tensor):
 
 
 def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_bound=None,
-                      with_xyz: bool = True, trace: bool = False):
+                      with_xyz: bool = True, trace: bool = False, keep_grid: bool = False):
     """Open3D VoxelDownSampleAndTrace + idxmat.max(1) + _select_by_idx.
 
     Returns dict: rep_idx (M,) int32 ascending; rep_xyz (M,3) (if with_xyz);
-    voxel_of_point (N,) int32 and cubic_id (M,8) int32 (if trace)."""
+    voxel_of_point (N,) int32 and cubic_id (M,8) int32 (if trace);
+    voxel_grid (if keep_grid): the voxel table for estimate_normals(...,
+    voxel_grid=) on the representatives' points (rep_xyz), or None when the
+    grid was too sparse to keep."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
@@ -60,9 +63,23 @@ def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_
     mnb = None if min_bound is None else _c(min_bound, np.float64)
     mxb = None if max_bound is None else _c(max_bound, np.float64)
     m = np.zeros(1, np.int64)
-    rc = L.o3dx_voxel_down_sample(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), N.ptr(rep),
-                                  N.ptr(rxyz), _np_ptr(m), N.ptr(vop), N.ptr(cub), N.ptr(ws), ws.numel(),
-                                  N.stream_ptr(dev))
+    cells = 0
+    if keep_grid and n > 0:
+        if mnb is None or mxb is None:
+            amn, amx = aabb(x)
+            mnb = _c(amn, np.float64) if mnb is None else mnb
+            mxb = _c(amx, np.float64) if mxb is None else mxb
+        cells = int(L.o3dx_voxel_grid_cells(n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size)))
+    geom = np.zeros(12, np.float64)
+    if cells > 0:
+        vox = torch.empty((cells, 4), dtype=torch.float32, device=dev)
+        rc = L.o3dx_voxel_down_sample_grid(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), N.ptr(rep),
+                                           N.ptr(rxyz), _np_ptr(m), N.ptr(vop), N.ptr(cub), N.ptr(vox), cells,
+                                           _np_ptr(geom), N.ptr(ws), ws.numel(), N.stream_ptr(dev))
+    else:
+        rc = L.o3dx_voxel_down_sample(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), N.ptr(rep),
+                                      N.ptr(rxyz), _np_ptr(m), N.ptr(vop), N.ptr(cub), N.ptr(ws), ws.numel(),
+                                      N.stream_ptr(dev))
     N.check(rc, "voxel_down_sample")
     M = int(m[0])
     out = {"rep_idx": rep[:M]}
@@ -71,12 +88,29 @@ def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_
     if trace:
         out["voxel_of_point"] = vop[:n]
         out["cubic_id"] = cub[: 8 * M].view(M, 8)
+    if keep_grid:
+        out["voxel_grid"] = VoxelGrid(geom, vox, M) if geom[7] == 1.0 else None
     return out
 
 
+class VoxelGrid:
+    """The voxel table of a voxel_down_sample(keep_grid=True): per voxel the
+    representative's (x, y, z, output row) (row -1 empty) + the grid geometry.
+    Lets estimate_normals on the M representatives skip sorting them into a
+    search grid (include/o3dx.h o3dx_estimate_normals_voxel)."""
+
+    def __init__(self, geom: np.ndarray, pts: torch.Tensor, m: int):
+        self.geom = np.ascontiguousarray(geom, np.float64)
+        self.pts = pts
+        self.m = int(m)
+
+
 def estimate_normals(xyz: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30, radius: float = 0.0,
-                     prior: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Open3D EstimateNormals(search_param, fast_normal_computation=True) -> (N,3) float32."""
+                     prior: Optional[torch.Tensor] = None, voxel_grid: Optional[VoxelGrid] = None) -> torch.Tensor:
+    """Open3D EstimateNormals(search_param, fast_normal_computation=True) -> (N,3) float32.
+
+    voxel_grid: the VoxelGrid of the voxel_down_sample that produced `xyz`
+    (its rep_xyz); the search grid is then read off the voxel table."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
@@ -84,8 +118,15 @@ def estimate_normals(xyz: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30,
     out = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev)
     pr = None if prior is None else _xyz(prior.to(dev), "prior normals")
     ws = N.workspace(L.o3dx_normals_workspace_bytes(n), dev)
-    rc = L.o3dx_estimate_normals(N.ptr(x), n, int(mode), int(knn), float(radius), N.ptr(pr), N.ptr(out), N.ptr(ws),
-                                 ws.numel(), N.stream_ptr(dev))
+    if voxel_grid is not None:
+        if voxel_grid.m != n or voxel_grid.pts.device != dev:
+            raise ValueError("voxel_grid does not belong to these points")
+        rc = L.o3dx_estimate_normals_voxel(_np_ptr(voxel_grid.geom), N.ptr(voxel_grid.pts), N.ptr(x), n, int(mode),
+                                           int(knn), float(radius), N.ptr(pr), N.ptr(out), N.ptr(ws), ws.numel(),
+                                           N.stream_ptr(dev))
+    else:
+        rc = L.o3dx_estimate_normals(N.ptr(x), n, int(mode), int(knn), float(radius), N.ptr(pr), N.ptr(out),
+                                     N.ptr(ws), ws.numel(), N.stream_ptr(dev))
     N.check(rc, "estimate_normals")
     return out[:n]
 

@@ -32,6 +32,24 @@ def test_config1_bunny_pipeline(bunny):
     assert np.mean(err < 1e-5) > 0.999 and _sign_err(down.get_normals(), ref_n).max() < 1e-5
 
 
+def test_voxel_grid_kept_until_points_change(bunny):
+    """voxel_down_sample keeps its voxel table on the result for
+    estimate_normals; an in-place edit or new points drop it."""
+    pc = o3p.PointCloud(bunny.astype(np.float64))
+    down = pc.voxel_down_sample(0.005)
+    assert down._kept_voxel_grid(down._dev_points()) is not None
+    ref_n = O.estimate_normals(bunny[O.voxel_down_sample(bunny, 0.005)], O.KNN, 30)
+    assert _sign_err(down.estimate_normals().get_normals(), ref_n).max() < 1e-5
+    down._pts[0, 0] += 1.0  # in place: the table no longer describes the points
+    assert down._kept_voxel_grid(down._dev_points()) is None
+    down2 = pc.voxel_down_sample(0.005)
+    down2.set_points(down2.get_points() + 1.0)
+    assert down2._kept_voxel_grid(down2._dev_points()) is None
+    shifted = bunny[O.voxel_down_sample(bunny, 0.005)].astype(np.float64) + 1.0
+    exp = O.estimate_normals(shifted.astype(np.float32), O.KNN, 30)
+    assert np.mean(_sign_err(down2.estimate_normals().get_normals(), exp) < 1e-5) > 0.999
+
+
 def test_voxel_trace_api(bunny):
     pc = o3p.PointCloud(bunny.astype(np.float64))
     down, idxmat, vec = pc.voxel_down_sample_and_trace(0.01)

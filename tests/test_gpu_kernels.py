@@ -311,3 +311,59 @@ def test_normals_knn_degenerate_clusters(dev):
                 del os.environ[env]
         assert np.isfinite(nrm).all()
         assert np.allclose(np.linalg.norm(nrm, axis=1), 1.0, atol=1e-5)
+
+
+# ------------------------------------------- voxel grid kept for the normals
+@pytest.mark.parametrize("shape", ["cube", "surface", "bunny"])
+@pytest.mark.parametrize("k", [5, 30])
+def test_normals_on_voxel_grid(dev, bunny, shape, k):
+    """voxel_down_sample(keep_grid) + estimate_normals(voxel_grid=): the
+    representatives are unchanged, the search grid is read off the voxel
+    table, and the normals agree with the sorted-grid path (to float64
+    summation order) and with the oracle."""
+    if shape == "cube":
+        pts, vs = S.uniform_cube(400_000, 21), S.voxel_size_for(400_000)
+    elif shape == "surface":
+        pts, vs = S.box_surface(400_000, 22), 0.01
+    else:
+        pts, vs = torch.from_numpy(bunny), 0.002
+    x = pts.to(dev)
+    a = ops.voxel_down_sample(x, vs, keep_grid=True)
+    b = ops.voxel_down_sample(x, vs)
+    assert torch.equal(a["rep_idx"], b["rep_idx"]) and torch.equal(a["rep_xyz"], b["rep_xyz"])
+    vg = a["voxel_grid"]
+    assert vg is not None and vg.m == a["rep_idx"].numel()
+    fused = ops.estimate_normals(a["rep_xyz"], knn=k, voxel_grid=vg).cpu().numpy()
+    plain = ops.estimate_normals(b["rep_xyz"], knn=k).cpu().numpy()
+    e = np.abs(fused - plain).max(1)
+    assert np.mean(e < 1e-6) > 0.9999, e.max()
+    if shape != "cube" or k == 30:
+        reps = pts.numpy()[a["rep_idx"].cpu().numpy()]
+        exp = O.estimate_normals(reps, O.KNN, k)
+        _, e_any = _normal_err(fused, exp)
+        assert np.mean(e_any < 1e-5) > 0.999
+
+
+def test_normals_on_voxel_grid_modes_and_prior(dev, bunny):
+    """Hybrid / radius search and prior orientation over the voxel grid."""
+    x = torch.from_numpy(bunny).to(dev)
+    a = ops.voxel_down_sample(x, 0.002, keep_grid=True)
+    reps, vg = a["rep_xyz"], a["voxel_grid"]
+    for mode, kk, r in ((O.HYBRID, 30, 0.01), (O.RADIUS, 0, 0.006)):
+        got = ops.estimate_normals(reps, mode=mode, knn=kk, radius=r, voxel_grid=vg).cpu().numpy()
+        ref = ops.estimate_normals(reps, mode=mode, knn=kk, radius=r).cpu().numpy()
+        assert np.mean(np.abs(got - ref).max(1) < 1e-6) > 0.9999
+    prior = -ops.estimate_normals(reps, knn=30)
+    got = ops.estimate_normals(reps, knn=30, prior=prior, voxel_grid=vg)
+    assert (torch.sum(got * prior, 1) >= 0).all()
+
+
+def test_voxel_grid_not_kept_when_sparse(dev):
+    """Points outside the given bounds force the hash table: no grid is kept
+    and estimate_normals takes the sorted-grid path."""
+    pts = S.uniform_cube(20_000, 23)
+    x = pts.to(dev)
+    out = ops.voxel_down_sample(x, 0.05, min_bound=[0.2, 0.2, 0.2], max_bound=[0.8, 0.8, 0.8], keep_grid=True)
+    assert out["voxel_grid"] is None
+    ref = ops.voxel_down_sample(x, 0.05, min_bound=[0.2, 0.2, 0.2], max_bound=[0.8, 0.8, 0.8])
+    assert torch.equal(out["rep_idx"], ref["rep_idx"])
