@@ -1051,6 +1051,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
 constexpr int kWaveBnd = 64;
 constexpr int kWaveRefineAt = 32;
 constexpr int kWavesPerBlock = 4;
+constexpr int kWaveCache = 512;  // candidates per wave kept in LDS (d2 + position)
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1124,16 +1125,36 @@ __device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int 
       _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
         const int pp = p_[u_];                                                   \
         const bool valid = pp >= 0;                                              \
+        const int fidx = b_ + u_ * 64 + lane;                                    \
         const float d2 = dist2_f32(q, v_[u_].x, v_[u_].y, v_[u_].z);             \
+        (void)fidx;                                                              \
         BODY                                                                     \
       }                                                                          \
     }                                                                            \
+  }
+
+// The same candidates from the wave's LDS cache (filled by the first scan of
+// the shell when they fit): no global loads in the refinement / list scans.
+#define O3DX_WAVE_SCAN_L(BODY)                                                   \
+  for (int b_ = 0; b_ < ncand; b_ += 64) {                                       \
+    const int f_ = b_ + lane;                                                    \
+    const bool valid = f_ < ncand;                                               \
+    const float d2 = valid ? cd2[f_] : 0.0f;                                     \
+    const int pp = valid ? cpos[f_] : -1;                                        \
+    BODY                                                                         \
+  }
+#define O3DX_WAVE_ANY(BODY)        \
+  if (cached) {                    \
+    O3DX_WAVE_SCAN_L(BODY)         \
+  } else {                         \
+    O3DX_WAVE_SCAN(S, BODY)        \
   }
 
 template <int KMAX>
 __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const float* __restrict__ prior,
                                            float* __restrict__ out, int64_t s, int lane, int32_t* sel, int32_t* bnd,
                                            int32_t* __restrict__ ra, int32_t* __restrict__ rp,
+                                           float* __restrict__ cd2, int32_t* __restrict__ cpos,
                                            int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int s0) {
   const float4 q = g.pts[s];
   int cx, cy, cz;
@@ -1144,6 +1165,7 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   float R2 = 0.f;
   RegHist<false> hist;
   int ncand = 0;
+  bool cached = false;
   // A query the tile handed on (s0 = 2) rarely needs more than the shell-1
   // reach + h/2: that ball first (fewer rows and x-cells of the 5^3 cube),
   // then the whole shell.
@@ -1163,12 +1185,19 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
     R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
     wave_sync();  // the previous shell's row table is no longer read
     ncand = wave_rows(g, q, cx, cy, cz, S, R2, lane, ra, rp);
+    cached = ncand <= kWaveCache;
     const float scale = (float)kHistBins / R2;
     hist.zero();
     int tot = 0;
-    O3DX_WAVE_SCAN(S, if (valid && d2 < R2) {
-      hist.add(min((int)(d2 * scale), kHistBins - 1));
-      ++tot;
+    O3DX_WAVE_SCAN(S, {
+      if (cached && valid) {
+        cd2[fidx] = d2;
+        cpos[fidx] = pp;
+      }
+      if (valid && d2 < R2) {
+        hist.add(min((int)(d2 * scale), kHistBins - 1));
+        ++tot;
+      }
     })
     tot = wave_sum(tot);
     if (tot > hist.kMaxTotal) {  // packed wave sums could carry
@@ -1181,6 +1210,7 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
     else
       ++S;
   }
+  wave_sync();  // the LDS cache is read by other lanes from here on
   float lo = 0.f, hi = R2, L = 0.f, U = 0.f;
   int below = 0;
   for (int lvl = 0; !fb; ++lvl) {
@@ -1197,13 +1227,13 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
     hi = U;
     const float sc = (float)kHistBins / (hi - lo);
     hist.zero();
-    O3DX_WAVE_SCAN(S, if (valid && d2 >= lo && d2 < hi) hist.add(min((int)((d2 - lo) * sc), kHistBins - 1));)
+    O3DX_WAVE_ANY(if (valid && d2 >= lo && d2 < hi) hist.add(min((int)((d2 - lo) * sc), kHistBins - 1));)
   }
   int nsel = 0, nb = 0;
   if (!fb) {
     const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
     int nU = 0;
-    O3DX_WAVE_SCAN(S, {
+    O3DX_WAVE_ANY({
       nU += __popcll(__ballot(valid && d2 < U));
       const bool c1 = valid && d2 < Lm;
       const bool c2 = valid && !(d2 < Lm) && d2 < Up;
@@ -1296,9 +1326,11 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   }
 }
 #undef O3DX_WAVE_SCAN
+#undef O3DX_WAVE_SCAN_L
+#undef O3DX_WAVE_ANY
 
 template <int KMAX>
-__global__ void __launch_bounds__(64 * kWavesPerBlock) k_normals_knn_wave(
+__global__ void __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4))) k_normals_knn_wave(
     GridView g, int kneed, const float* __restrict__ prior, float* __restrict__ out,
     const int32_t* __restrict__ in_list, const int32_t* __restrict__ in_len, int32_t* __restrict__ fb_list,
     int32_t* __restrict__ fb_len, int s0) {
@@ -1306,11 +1338,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) k_normals_knn_wave(
   __shared__ int32_t bnd[kWavesPerBlock][kWaveBnd];
   __shared__ int32_t ra[kWavesPerBlock][64];
   __shared__ int32_t rp[kWavesPerBlock][65];
+  __shared__ float cd2[kWavesPerBlock][kWaveCache];
+  __shared__ int32_t cpos[kWavesPerBlock][kWaveCache];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t lim = in_list ? (int64_t)*in_len : g.n;
   for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wv; t < lim; t += (int64_t)gridDim.x * kWavesPerBlock) {
     const int64_t s = in_list ? (int64_t)__builtin_amdgcn_readfirstlane(in_list[t]) : t;
-    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], ra[wv], rp[wv], fb_list, fb_len, s0);
+    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], ra[wv], rp[wv], cd2[wv], cpos[wv], fb_list,
+                     fb_len, s0);
   }
 }
 

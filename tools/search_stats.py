@@ -18,8 +18,22 @@ def run_one():
     dev = torch.device("cuda:0")
     N = int(os.environ.get("N", "10000000"))
     pts = S.uniform_cube(N, 0, device=dev)
-    reps = ops.voxel_down_sample(pts, S.voxel_size_for(N))["rep_xyz"]
     out = {"env": {k: v for k, v in os.environ.items() if k.startswith("O3DX_")}}
+    vd = ops.voxel_down_sample(pts, S.voxel_size_for(N), keep_grid=True)
+    reps, vg = vd["rep_xyz"], vd["voxel_grid"]
+    ops.estimate_normals(reps, knn=30, voxel_grid=vg)
+    _native.search_stats(True)
+    ops.estimate_normals(reps, knn=30, voxel_grid=vg)
+    out["voxel_grid_normals_stats"] = _native.search_stats()
+    _native.search_stats(False)
+    _native.set_kernel_timing(True)
+    _native.reset_kernel_timing()
+    for _ in range(3):
+        ops.estimate_normals(reps, knn=30, voxel_grid=vg)
+    for name in ("normals_knn", "normals_tile", "normals_wave", "grid_voxel"):
+        ms, c = _native.kernel_timing(name)
+        out["voxel_grid_" + name + "_ms"] = ms / max(c, 1)
+    del vd, vg
     ops.estimate_normals(reps, knn=30)
     _native.search_stats(True)
     _native.set_kernel_timing(True)
