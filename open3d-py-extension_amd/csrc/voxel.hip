@@ -92,8 +92,7 @@ __global__ void __launch_bounds__(kBlock) k_voxel_settle(const int32_t* __restri
 constexpr int kBinBlock = 512;
 constexpr int kBinPer = 32;                    // points per thread in the binning passes
 constexpr int kBinChunk = kBinBlock * kBinPer; // points per binning block
-constexpr int kCtrPad = 32;                    // one 128-B line per brick counter / cursor
-constexpr int kMaxBuckets = 8192;              // LDS histogram (32 KB)
+constexpr int kMaxBuckets = 4096;              // LDS histogram (16 KB); scatter LDS <= 64 KB
 constexpr int kMaxBrickBits = 13;              // LDS max table (32 KB)
 constexpr int kReduceBlock = 512;
 
@@ -116,10 +115,12 @@ __device__ __forceinline__ uint32_t brick_code(const int v[3], const Bricks& b) 
   return (bk << 16) | lx | (ly << b.sx) | (lz << (b.sx + b.sy));
 }
 
-// Pass 1: brick counts (LDS histogram per block, one global add per touched
-// brick).  Also writes the voxel id per point when the trace needs it.
+// Pass 1: brick counts per block (LDS histogram), stored brick-major —
+// hist[k * nblk + block] — so that one exclusive scan gives every block its
+// run in every brick (no global atomics).  Also writes the voxel id per
+// point when the trace needs it.
 __global__ void __launch_bounds__(kBinBlock) k_vbin_count(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                       Bricks b, int32_t* __restrict__ bcount,
+                                                       Bricks b, int32_t* __restrict__ bhist,
                                                        int32_t* __restrict__ vid, int* __restrict__ err) {
   __shared__ int32_t hist[kMaxBuckets];
   const P3* p = reinterpret_cast<const P3*>(xyz);
@@ -139,65 +140,92 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_count(const float* __restric
   }
   if (bad) *err = 1;
   __syncthreads();
-  for (int k = threadIdx.x; k < b.nb; k += kBinBlock)
-    if (hist[k]) atomicAdd(&bcount[k * kCtrPad], hist[k]);
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) bhist[(int64_t)k * gridDim.x + blockIdx.x] = hist[k];
 }
 
-// Padded counters -> contiguous counts (for the scan), offsets -> padded cursors.
-__global__ void k_vbin_unpad(const int32_t* __restrict__ padded, int nb, int32_t* __restrict__ dense) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < nb) dense[k] = padded[k * kCtrPad];
-}
-__global__ void k_vbin_pad(const int32_t* __restrict__ dense, int nb, int32_t* __restrict__ padded) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < nb) padded[k * kCtrPad] = dense[k];
-}
+// Pass 2: scatter (local << 32 | index) into the block's run of each brick
+// (boff = the scanned brick-major histogram).  The block's points go out in
+// rounds of kBinRound: sorted by brick in LDS first, so each brick's entries
+// leave as one contiguous run (coalesced stores instead of one line per lane).
+constexpr int kBinRound = 4096;
 
-// Pass 2: reserve a run per touched brick, then scatter (local << 32 | index).
+// dynamic LDS: stage[kBinRound] (u64), cur[nb], loc[nb]
+inline size_t scatter_lds_bytes(int nb) { return kBinRound * sizeof(uint64_t) + 2 * (size_t)nb * sizeof(int32_t); }
+
 __global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                         Bricks b, int32_t* __restrict__ cursor,
+                                                         Bricks b, const int32_t* __restrict__ boff,
                                                          uint64_t* __restrict__ entries) {
-  __shared__ int32_t hist[kMaxBuckets];
+  static_assert(kBinChunk % kBinRound == 0 && kBinRound % kBinBlock == 0, "round shape");
+  extern __shared__ uint64_t lds_u64[];
+  uint64_t* stage = lds_u64;
+  int32_t* cur = reinterpret_cast<int32_t*>(lds_u64 + kBinRound);  // global address of stage slot 0, per brick
+  int32_t* loc = cur + b.nb;                                         // round: count -> offset -> cursor
+  __shared__ int32_t wsum[kBinBlock / 64 + 1];
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) hist[k] = 0;
-  __syncthreads();
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) cur[k] = boff[(int64_t)k * gridDim.x + blockIdx.x];
   const int64_t base = (int64_t)blockIdx.x * kBinChunk;
-  uint32_t code[kBinPer];
+  constexpr int kPer = kBinRound / kBinBlock;           // points per thread per round
+  const int span = (b.nb + kBinBlock - 1) / kBinBlock;  // bricks per thread in the local scan
+  for (int r0 = 0; r0 < kBinChunk && base + r0 < n; r0 += kBinRound) {
+    for (int k = threadIdx.x; k < b.nb; k += kBinBlock) loc[k] = 0;
+    __syncthreads();
+    uint32_t code[kPer];
 #pragma unroll
-  for (int j = 0; j < kBinPer; ++j) {
-    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
-    int v[3];
-    code[j] = ~0u;
-    if (i < n && voxel_of(p[i], g, v)) {
-      code[j] = brick_code(v, b);
-      atomicAdd(&hist[code[j] >> 16], 1);
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = base + r0 + threadIdx.x + (int64_t)j * kBinBlock;
+      int v[3];
+      code[j] = ~0u;
+      if (i < n && voxel_of(p[i], g, v)) {
+        code[j] = brick_code(v, b);
+        atomicAdd(&loc[code[j] >> 16], 1);
+      }
     }
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < b.nb; k += kBinBlock)
-    if (hist[k]) hist[k] = atomicAdd(&cursor[k * kCtrPad], hist[k]);
-  __syncthreads();
+    __syncthreads();
+    // exclusive scan of the round's brick counts (each thread a span of bricks);
+    // cur[k] becomes the global address of stage slot 0 for brick k
+    const int k0 = threadIdx.x * span, k1 = min(k0 + span, b.nb);
+    int run = 0;
+    for (int k = k0; k < k1; ++k) run += loc[k];
+    int tot;
+    int ex = block_excl_scan<kBinBlock>(run, wsum, &tot);
+    for (int k = k0; k < k1; ++k) {
+      const int c = loc[k];
+      loc[k] = ex;
+      cur[k] -= ex;
+      ex += c;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kBinPer; ++j) {
-    if (code[j] == ~0u) continue;
-    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
-    const int32_t at = atomicAdd(&hist[code[j] >> 16], 1);
-    entries[at] = ((uint64_t)(code[j] & 0xffffu) << 32) | (uint32_t)i;
+    for (int j = 0; j < kPer; ++j) {
+      if (code[j] == ~0u) continue;
+      const int64_t i = base + r0 + threadIdx.x + (int64_t)j * kBinBlock;
+      const int at = atomicAdd(&loc[code[j] >> 16], 1);
+      stage[at] = ((uint64_t)(code[j] >> 16) << 48) | ((uint64_t)(code[j] & 0xffffu) << 32) | (uint32_t)i;
+    }
+    __syncthreads();
+    // consecutive stage slots of one brick -> consecutive addresses of its run
+    for (int t = threadIdx.x; t < tot; t += kBinBlock) {
+      const uint64_t e = stage[t];
+      entries[cur[(int)(e >> 48)] + t] = e & 0x0000ffffffffffffull;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < b.nb; k += kBinBlock) cur[k] += loc[k];  // loc[k] = end of brick k's slice
+    __syncthreads();
   }
 }
 
 // Pass 3: one workgroup per brick: max index per voxel in LDS, then the
 // brick's slice of the dense table (-1 = empty) and flags[rep] = 1.
 __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __restrict__ entries,
-                                                              const int32_t* __restrict__ boff, VoxelGeom g,
-                                                              Bricks b, int32_t* __restrict__ table,
+                                                              const int32_t* __restrict__ boff, int nblk,
+                                                              VoxelGeom g, Bricks b, int32_t* __restrict__ table,
                                                               uint8_t* __restrict__ flags) {
   __shared__ int32_t tab[1 << kMaxBrickBits];
   const int nloc = 1 << (b.sx + b.sy + b.sz);
   for (int k = threadIdx.x; k < nloc; k += kReduceBlock) tab[k] = -1;
   __syncthreads();
   const int bk = blockIdx.x;
-  const int32_t e0 = boff[bk], e1 = boff[bk + 1];
+  const int32_t e0 = boff[(int64_t)bk * nblk], e1 = boff[(int64_t)(bk + 1) * nblk];
   for (int32_t e = e0 + threadIdx.x; e < e1; e += kReduceBlock) {
     const uint64_t w = entries[e];
     atomicMax(&tab[(int)(w >> 32)], (int32_t)(uint32_t)w);
@@ -365,6 +393,8 @@ __global__ void __launch_bounds__(kBlock) k_voxel_occ2(const int32_t* __restrict
 }
 
 static int64_t dense_cap(int64_t n) { return 2 * n + (1 << 20); }
+static int64_t bin_blocks(int64_t n) { return (n + kBinChunk - 1) / kBinChunk; }
+static int64_t bin_hist_ints(int64_t n) { return bin_blocks(n) * kMaxBuckets; }
 static int64_t hash_cap(int64_t n) {
   int64_t t = 1024;
   while (t < 2 * n) t <<= 1;
@@ -373,9 +403,8 @@ static int64_t hash_cap(int64_t n) {
 
 struct VoxelWs {
   uint64_t* entries;           // brick-binned (local, index) pairs
-  int32_t* bcount;             // brick counts and cursors (padded), offsets
+  int32_t* bhist;              // per-block brick counts, brick-major, and their scan
   int32_t* boff;
-  int32_t* bcur;
   int32_t* table;              // dense rep or hash rep
   unsigned long long* keys;    // hash keys
   int32_t* vid;
@@ -395,13 +424,12 @@ static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
   w->table = reinterpret_cast<int32_t*>(tb);
   w->keys = tb ? reinterpret_cast<unsigned long long*>(tb + Arena::align(hc * sizeof(int32_t))) : nullptr;
   w->entries = ar.take<uint64_t>(n);
-  w->bcount = ar.take<int32_t>((kMaxBuckets + 1) * kCtrPad);
-  w->boff = ar.take<int32_t>(kMaxBuckets + 1);
-  w->bcur = ar.take<int32_t>((kMaxBuckets + 1) * kCtrPad);
+  w->bhist = ar.take<int32_t>(bin_hist_ints(n));
+  w->boff = ar.take<int32_t>(bin_hist_ints(n) + 1);
   w->vid = ar.take<int32_t>(n);
   w->flags = ar.take<uint8_t>(n + 16);
   w->pos = ar.take<int32_t>(n);
-  w->scan_tmp = ar.take<int32_t>(std::max<size_t>(compact_workspace_ints(n), scan_workspace_ints(kMaxBuckets + 1)));
+  w->scan_tmp = ar.take<int32_t>(std::max<size_t>(compact_workspace_ints(n), scan_workspace_ints(bin_hist_ints(n) + 1)));
   w->aabb = ar.take<char>(aabb_ws_bytes(n));
   w->mm = ar.take<double>(8);
   w->count = ar.take<int64_t>(8);
@@ -500,18 +528,14 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       nslots = (int64_t)nvox;
       const unsigned nblk = (unsigned)((n + kBinChunk - 1) / kBinChunk);
       KTimer kt("voxel_assign", s);
-      O3DX_HIP(hipMemsetAsync(w.bcount, 0, (size_t)bricks.nb * kCtrPad * sizeof(int32_t), s));
       O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
-      hipLaunchKernelGGL(k_vbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bcount,
+      hipLaunchKernelGGL(k_vbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bhist,
                          (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
-      const unsigned gb = (unsigned)((bricks.nb + 255) / 256);
-      hipLaunchKernelGGL(k_vbin_unpad, dim3(gb), dim3(256), 0, s, w.bcount, bricks.nb, w.bcur);
-      O3DX_TRY(exclusive_scan_i32(w.bcur, w.boff, bricks.nb, w.scan_tmp, s));
-      hipLaunchKernelGGL(k_vbin_pad, dim3(gb), dim3(256), 0, s, w.boff, bricks.nb, w.bcount);
-      hipLaunchKernelGGL(k_vbin_scatter, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bcount,
-                         w.entries);
-      hipLaunchKernelGGL(k_vbin_reduce, dim3(bricks.nb), dim3(kReduceBlock), 0, s, w.entries, w.boff, g, bricks,
-                         w.table, w.flags);
+      O3DX_TRY(exclusive_scan_i32(w.bhist, w.boff, (int64_t)bricks.nb * nblk, w.scan_tmp, s));
+      hipLaunchKernelGGL(k_vbin_scatter, dim3(nblk), dim3(kBinBlock), scatter_lds_bytes(bricks.nb), s, xyz, n, g,
+                         bricks, w.boff, w.entries);
+      hipLaunchKernelGGL(k_vbin_reduce, dim3(bricks.nb), dim3(kReduceBlock), 0, s, w.entries, w.boff, (int)nblk, g,
+                         bricks, w.table, w.flags);
       kt.stop();
       KTimer kc("voxel_compact", s);
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
