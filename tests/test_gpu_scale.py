@@ -42,6 +42,21 @@ def test_normals_10m_reps(cloud10m):
     assert np.abs(np.linalg.norm(got, axis=1) - 1).max() < 1e-5
 
 
+def test_normals_10m_voxel_table(cloud10m):
+    """The bench's exact step: voxel_down_sample(keep_grid) -> estimate_normals
+    on the dense voxel table, against the oracle on the same representatives."""
+    vs = S.voxel_size_for(N)
+    out = ops.voxel_down_sample(cloud10m, vs, keep_grid=True)
+    reps = out["rep_xyz"]
+    got = ops.estimate_normals(reps, knn=30, voxel_grid=out["voxel_grid"]).cpu().numpy()
+    ref = O.estimate_normals(reps.cpu().numpy(), O.KNN, 30)
+    err_signed = np.abs(got - ref).max(1)
+    err_any = np.minimum(err_signed, np.abs(got + ref).max(1))
+    assert np.mean(err_any < 1e-5) > 0.9995
+    assert np.mean(err_signed < 1e-5) > 0.999
+    assert np.abs(np.linalg.norm(got, axis=1) - 1).max() < 1e-5
+
+
 def test_ransac_10m_counts(dev):
     pts = S.planted_plane(N, 1, device=dev)
     samples = O.ransac_samples(N, 3, 1000, 7)

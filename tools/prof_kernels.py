@@ -16,11 +16,12 @@ N = int(os.environ.get("N", "10000000"))
 what = sys.argv[1] if len(sys.argv) > 1 else "all"
 if what in ("all", "normals"):
     pts = S.uniform_cube(N, 0, device=dev)
-    reps = ops.voxel_down_sample(pts, S.voxel_size_for(N))["rep_xyz"]
+    vd = ops.voxel_down_sample(pts, S.voxel_size_for(N), keep_grid=True)
+    reps, vg = vd["rep_xyz"], vd["voxel_grid"]
     for _ in range(3):
-        ops.estimate_normals(reps, knn=30)
+        ops.estimate_normals(reps, knn=30, voxel_grid=vg)
     torch.cuda.synchronize()
-    del pts, reps
+    del pts, reps, vd, vg
 if what in ("all", "icp"):
     tgt = S.box_surface(N, 1, device=dev)
     src = S.apply_transform(S.box_surface(N, 2, device=dev), S.rigid_transform())
