@@ -248,15 +248,15 @@ def main():
     ev_ms = ev0.elapsed_time(ev1)
 
     kernels = {}
-    for name in ("voxel_assign", "voxel_compact", "grid_count", "grid_sort", "normals_tile", "normals_wave",
-                 "normals_knn"):
+    for name in ("voxel_assign", "voxel_compact", "grid_count", "grid_sort", "normals_stile", "normals_tile",
+                 "normals_wave", "normals_knn"):
         ms, cnt = _native.kernel_timing(name)
         if cnt:
             kernels[name] = {"avg_ms": round(ms / cnt, 4), "launches": cnt}
     # algorithmic bytes per launch:
-    #   normals_tile: M queries x (12 B xyz read + 12 B normal written)
+    #   normals_stile / normals_tile: M queries x (12 B xyz read + 12 B normal written)
     #   voxel_assign: N points x (12 B xyz read + 4 B voxel id written)
-    algo_bytes = {"normals_tile": 24.0 * M, "voxel_assign": 16.0 * N}
+    algo_bytes = {"normals_stile": 24.0 * M, "normals_tile": 24.0 * M, "voxel_assign": 16.0 * N}
     dom = max((k for k in kernels if k in algo_bytes), key=lambda k: kernels[k]["avg_ms"], default=None)
     roof = None
     if dom is not None:

@@ -691,84 +691,95 @@ __device__ __forceinline__ bool hist_locate(const H& hist, int kneed, int below,
   return bstar >= 0;
 }
 
-// Lexicographic (d2_f64, original index) order; the index is fetched only on
-// an exact distance tie.
-template <class Id>
-__device__ __forceinline__ bool key_less(double da, int pa, double db, int pb, Id&& id) {
-  if (da != db) return da < db;
-  if (pb < 0) return pa >= 0;
-  if (pa < 0) return false;
-  return id(pa) < id(pb);
-}
-
 // Exact completion of a tile selection (see above).  lst[0..n) holds every
-// candidate with f32 d^2 < Up (LDS slots understood by `fetch` / `id`).
-//   1. partition in place: certain (d^2 < Lm) to the front, accumulating
-//      their moments on the way; the rest is the band;
-//   2. move the (k - #certain) nearest band entries by (d2_f64, original
-//      index) to the front of the band, adding their moments;
-//   3. order check: the largest certain key precedes the smallest unselected
-//      band key (exactly only when the f32 bound cannot decide it).
-// Writes the normal of original point `oi`; false = hand the query on.
-template <int KMAX, class T, class Fetch, class Id>
+// candidate with f32 d^2 < Up (LDS slots understood by `fetch`).
+//   1. one pass over the list, four entries per step with all their LDS loads
+//      issued first: certain entries (d^2 < Lm) go straight into the float64
+//      moments, band entries are compacted to the front of the list (the
+//      write position never passes the read position);
+//   2. the band (<= kBndCap entries) in registers with its float32 d^2: the
+//      (k - #certain) nearest are picked by repeated minimum and added;
+//   3. the picked and unpicked band keys, and the certain keys and the
+//      unpicked band keys, must be separated by more than the float32 error
+//      (2^-20 relative each side): then the float64 (d^2, index) order — the
+//      oracle's / nanoflann's — selects the same set.
+// A band that overflows or a separation within rounding (ties included)
+// hands the query on (false) to the exact wave form.  Writes the normal of
+// original point `oi`.
+template <int KMAX, class T, class Fetch>
 __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int n, float Lm, float U, T (*lst)[64],
-                                                 int lane, Fetch&& fetch, Id&& id, const float* __restrict__ prior,
-                                                 int oi, float* __restrict__ out, bool skip_eigen = false) {
-  const double qx = q.x, qy = q.y, qz = q.z;
+                                                 int lane, Fetch&& fetch, const float* __restrict__ prior, int oi,
+                                                 float* __restrict__ out, bool skip_eigen = false) {
   MomAcc acc;
   acc.zero();
-  int nsel = 0, nU = 0;
-  for (int j = 0; j < n; ++j) {
-    const int p = (int)lst[j][lane];
-    const float4 v = fetch(p);
-    const float d2f = dist2_f32(q, v.x, v.y, v.z);  // the scan's value, bit for bit
-    nU += d2f < U ? 1 : 0;
-    if (d2f < Lm) {
-      if (nsel != j) {
-        lst[j][lane] = lst[nsel][lane];
-        lst[nsel][lane] = (T)p;
+  int nsel = 0, nb = 0, nU = 0;
+  for (int j = 0; j < n; j += 4) {
+    int p[4];
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[u] = (int)lst[min(j + u, n - 1)][lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = fetch(p[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (j + u < n) {
+        const float d2f = dist2_f32(q, v[u].x, v[u].y, v[u].z);  // the scan's value, bit for bit
+        nU += d2f < U ? 1 : 0;
+        if (d2f < Lm) {
+          ++nsel;
+          acc.add((double)v[u].x, (double)v[u].y, (double)v[u].z);
+        } else {
+          lst[min(nb, kBndCap)][lane] = (T)p[u];
+          ++nb;
+        }
       }
-      ++nsel;
-      acc.add((double)v.x, (double)v.y, (double)v.z);
     }
   }
   // nU >= k: the k nearest lie clearly below Up, so nothing past the band can displace them
-  if (nsel > kneed || n - nsel > kBndCap || n < kneed || nU < kneed) return false;
-  for (int t = nsel; t < kneed; ++t) {
-    int bj = t, bp = (int)lst[t][lane];
-    double bd = dist2_f64(qx, qy, qz, fetch(bp));
-    for (int j = t + 1; j < n; ++j) {
-      const int p = (int)lst[j][lane];
-      const double d = dist2_f64(qx, qy, qz, fetch(p));
-      if (key_less(d, p, bd, bp, id)) {
-        bd = d;
-        bp = p;
-        bj = j;
-      }
+  if (nsel > kneed || nb > kBndCap || n < kneed || nU < kneed) return false;
+  const int need = kneed - nsel;
+  float bk[kBndCap];
+  int bs[kBndCap];
+#pragma unroll
+  for (int i = 0; i < kBndCap; ++i) {
+    bk[i] = INFINITY;
+    bs[i] = 0;
+    if (i < nb) {
+      bs[i] = (int)lst[i][lane];
+      const float4 v = fetch(bs[i]);
+      bk[i] = dist2_f32(q, v.x, v.y, v.z);
     }
-    lst[bj][lane] = lst[t][lane];
-    lst[t][lane] = (T)bp;
-    const float4 v = fetch(bp);
-    acc.add((double)v.x, (double)v.y, (double)v.z);
   }
-  if (n > kneed && nsel > 0) {
-    int up = -1;
-    double ud = INFINITY;
-    for (int j = kneed; j < n; ++j) {
-      const int p = (int)lst[j][lane];
-      const double d = dist2_f64(qx, qy, qz, fetch(p));
-      if (key_less(d, p, ud, up, id)) {
-        ud = d;
-        up = p;
+  uint32_t picked = 0;
+  float kmax = -1.0f;
+  for (int t = 0; t < need; ++t) {
+    float best = INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int i = 0; i < kBndCap; ++i)
+      if (!((picked >> i) & 1u) && bk[i] < best) {
+        best = bk[i];
+        bi = i;
+      }
+    picked |= 1u << bi;
+    kmax = best;
+  }
+  float umin = INFINITY;
+#pragma unroll
+  for (int i = 0; i < kBndCap; ++i) {
+    if (i < nb) {
+      if ((picked >> i) & 1u) {
+        const float4 v = fetch(bs[i]);
+        acc.add((double)v.x, (double)v.y, (double)v.z);
+      } else {
+        umin = fminf(umin, bk[i]);
       }
     }
-    // certain keys are < Lm (1 + 2^-22) exactly; compare one by one only when that does not settle it
-    if (!(ud > (double)Lm * (1.0 + 1e-6))) {
-      for (int j = 0; j < nsel; ++j) {
-        const int p = (int)lst[j][lane];
-        if (!key_less(dist2_f64(qx, qy, qz, fetch(p)), p, ud, up, id)) return false;  // rounding swapped the order
-      }
-    }
+  }
+  if (need < nb) {
+    const float sep = 1.0f - 4.0f * kRelEps;
+    if (need > 0 && !(kmax < umin * sep)) return false;
+    if (nsel > 0 && !(Lm < umin * sep)) return false;
   }
   if (skip_eigen) {  // profiling only (O3DX_TILE_DEBUG=4)
     out[3 * oi] = (float)(acc.m[3] + acc.m[5] + acc.m[8]);
@@ -1022,8 +1033,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
           fb = n > kListMax ||
                !finish_selection<KMAX>(
                    q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
-                   [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, prior,
-                   __float_as_int(q.w), out, dbg == 4);
+                   prior, __float_as_int(q.w), out, dbg == 4);
         }
       }
     }
@@ -1038,6 +1048,206 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
 #undef O3DX_TILE_SCAN
 #undef O3DX_TILE_HIST
 #undef O3DX_TILE_HIST_SCAN
+
+// ---------------------------------------------------------------------------
+// KNN normals straight off a dense voxel table (the voxel_down_sample ->
+// estimate_normals hand-over, o3dx_estimate_normals_voxel), used when the
+// representatives fill their voxels (<= 1 rep per voxel by construction; most
+// voxels occupied — any volumetric cloud after down-sampling).  No search
+// grid is built: the voxel table is the grid, at voxel granularity.
+//
+// One wave = one block of 4^3 voxels (lane = voxel, <= 64 queries).  The
+// block's box (the block + 3 voxels on every side, 10^3) is staged from the
+// table into LDS as dense SoA float32 slots (empty voxel: +inf, never inside
+// any bound).  Every lane scans a fixed ball-shaped stencil around its own
+// voxel: the 172 voxels (33 rows of 4-6) that can hold a point within 2.45
+// voxels of a query in the upper half of its voxel along each axis, mirrored
+// per axis to the half the lane's query is in.  Row offsets and lengths are
+// compile-time constants (one base, one sign per axis), so the lanes never
+// diverge in the scans, and every point closer than R = 2.45 voxels (minus
+// the rounding slack) has been seen: at one rep per voxel that ball holds ~60
+// points, k = 30 lie within ~1.94 voxels.  Steps as the LDS tile above: count
+// over [0, R), locate / refine, list pass, exact finish (finish_selection).
+// Queries whose k-th neighbour lies beyond R (cloud borders) go, by voxel
+// index, to the wave form (from shell 3) and the register top-k over the table
+// itself (a dense GridView).
+constexpr int kVB = 4;                     // block edge (voxels)
+constexpr int kVM = 3;                     // box margin (the stencil's reach in voxels)
+constexpr int kVE = kVB + 2 * kVM;         // box edge (10)
+constexpr int kSY = kVE, kSZ = kVE * kVE;  // LDS slot strides
+constexpr int kVSlots = kVE * kSZ;         // 1000
+constexpr double kStencilR = 2.45;         // completeness radius (voxels)
+
+// (dy, dz, x0, x1) in the oriented frame (query in [0.49, 1) of its voxel on
+// every axis): the voxels within kStencilR of any such query, generated by
+// tools/stencil_rows.py.
+#define O3DX_S25_ROWS(X)                                                                                     \
+  X(-2, -2, -1, 2) X(-1, -2, -2, 2) X(0, -2, -2, 2) X(1, -2, -2, 2) X(2, -2, -2, 2) X(-2, -1, -2, 2)         \
+  X(-1, -1, -2, 3) X(0, -1, -2, 3) X(1, -1, -2, 3) X(2, -1, -2, 3) X(3, -1, -1, 2) X(-2, 0, -2, 2)           \
+  X(-1, 0, -2, 3) X(0, 0, -2, 3) X(1, 0, -2, 3) X(2, 0, -2, 3) X(3, 0, -1, 2) X(-2, 1, -2, 2)                \
+  X(-1, 1, -2, 3) X(0, 1, -2, 3) X(1, 1, -2, 3) X(2, 1, -2, 3) X(3, 1, -1, 2) X(-2, 2, -2, 2)                \
+  X(-1, 2, -2, 3) X(0, 2, -2, 3) X(1, 2, -2, 3) X(2, 2, -2, 3) X(3, 2, -1, 2) X(-1, 3, -1, 2)                \
+  X(0, 3, -1, 2) X(1, 3, -1, 2) X(2, 3, -1, 2)
+
+struct DenseVox {
+  const float4* __restrict__ vox;  // (x, y, z, bits(row)), row -1 = empty (0xFF fill: NaN coordinates)
+  int nx, ny, nz;                  // voxel dims
+  int nbx, nby, nbz;               // 4^3 blocks
+  float ox, oy, oz, vs, inv_vs;
+  float rc2;                       // completeness radius^2 (world, float32, shrunk by the slack)
+  unsigned long long* stats;       // debug counters (o3dx_search_stats) or null
+};
+
+__device__ __forceinline__ float4 dvox_load(const DenseVox& d, int x, int y, int z) {
+  float4 v = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));
+  if (x >= 0 && y >= 0 && z >= 0 && x < d.nx && y < d.ny && z < d.nz) {
+    v = d.vox[x + (int64_t)d.nx * (y + (int64_t)d.ny * z)];
+    if (__float_as_int(v.w) < 0) v.x = v.y = v.z = INFINITY;
+  }
+  return v;
+}
+
+// f(slot, d2) over L consecutive slots from st: pairs in packed f32, one single.
+template <int L, class F>
+__device__ __forceinline__ void scan_run(const float* tx, const float* ty, const float* tz, int st, const float4 q,
+                                         F&& f) {
+#pragma unroll
+  for (int i = 0; i + 1 < L; i += 2) {
+    const f32x2 dd = dist2_pair(q, (f32x2){tx[st + i], tx[st + i + 1]}, (f32x2){ty[st + i], ty[st + i + 1]},
+                                (f32x2){tz[st + i], tz[st + i + 1]});
+    f(st + i, dd.x);
+    f(st + i + 1, dd.y);
+  }
+  if (L & 1) f(st + L - 1, dist2_f32(q, tx[st + L - 1], ty[st + L - 1], tz[st + L - 1]));
+}
+
+// The lane's stencil: qs = its own slot, SY / SZ = the y / z slot strides
+// signed by the orientation, xpos = x orientation.
+template <class F>
+__device__ __forceinline__ void stencil_scan(const float* tx, const float* ty, const float* tz, int qs, int SY, int SZ,
+                                             bool xpos, const float4 q, F&& f) {
+  // a scheduling fence per row keeps the unrolled stencil from hoisting every
+  // row's loads (register pressure; the other waves hide the LDS latency)
+#define O3DX_ROW(DY, DZ, XA, XB)                                                                   \
+  scan_run<(XB) - (XA) + 1>(tx, ty, tz, qs + (DY) * SY + (DZ) * SZ + (xpos ? (XA) : -(XB)), q, f); \
+  __builtin_amdgcn_sched_barrier(0);
+  O3DX_S25_ROWS(O3DX_ROW)
+#undef O3DX_ROW
+}
+
+template <int KMAX>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior,
+                                                      float* __restrict__ out, int32_t* __restrict__ fb_list,
+                                                      int32_t* __restrict__ fb_len, int force_fb, int dbg) {
+  __shared__ float tx[kVSlots], ty[kVSlots], tz[kVSlots];
+  constexpr int kListMax = KMAX + kBndCap;
+  constexpr int kListCap = kListMax + 4;
+  constexpr int kListWords = (kListCap * 64 * 2 + 3) / 4;
+  constexpr int kHistWords = kTileSlots * 64;
+  __shared__ uint32_t selbuf[kListWords > kHistWords ? kListWords : kHistWords];
+  uint16_t(*lst)[64] = reinterpret_cast<uint16_t(*)[64]>(selbuf);
+  uint32_t* hw = selbuf;
+  const int lane = threadIdx.x;
+  const int nb = d.nbx * d.nby * d.nbz;
+  const int b = xcd_block(blockIdx.x, nb);
+  const int bx = b % d.nbx, by = (b / d.nbx) % d.nby, bz = b / (d.nbx * d.nby);
+  const int gx0 = bx * kVB - kVM, gy0 = by * kVB - kVM, gz0 = bz * kVB - kVM;  // box origin (voxels)
+  {
+    constexpr int J = (kVSlots + 63) / 64;
+    float4 buf[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int t = lane + 64 * j;
+      if (t < kVSlots) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kSY) % kVE, gz0 + t / kSZ);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int t = lane + 64 * j;
+      if (t < kVSlots) {
+        tx[t] = buf[j].x;
+        ty[t] = buf[j].y;
+        tz[t] = buf[j].z;
+      }
+    }
+  }
+  __syncthreads();
+  const int lx = lane & 3, ly = (lane >> 2) & 3, lz = lane >> 4;
+  const int qs = (lx + kVM) + kSY * (ly + kVM) + kSZ * (lz + kVM);
+  const float4 q = make_float4(tx[qs], ty[qs], tz[qs], 0.0f);
+  if (!(q.x < INFINITY)) return;  // empty voxel or outside the grid: no query (no barrier follows)
+  const int vx = gx0 + kVM + lx, vy = gy0 + kVM + ly, vz = gz0 + kVM + lz;
+  const int64_t vq = vx + (int64_t)d.nx * (vy + (int64_t)d.ny * vz);
+  const int oi = __float_as_int(d.vox[vq].w);
+  // orientation: the half of its voxel the query lies in, per axis
+  const bool xpos = (q.x - (d.ox + (float)vx * d.vs)) * d.inv_vs >= 0.5f;
+  const bool ypos = (q.y - (d.oy + (float)vy * d.vs)) * d.inv_vs >= 0.5f;
+  const bool zpos = (q.z - (d.oz + (float)vz * d.vs)) * d.inv_vs >= 0.5f;
+  const int SY = ypos ? kSY : -kSY, SZ = zpos ? kSZ : -kSZ;
+  bool fb = force_fb != 0;  // force_fb: tests of the hand-off path
+  if (dbg == 1) {             // profiling only (O3DX_TILE_DEBUG): stop after staging
+    if (q.x == 12345.f) out[0] = 0.f;
+    return;
+  }
+  if (!fb) {
+    const float R2 = d.rc2;
+    TileHist th;
+    auto hist = [&](float lo_, float sc_) {
+#pragma unroll
+      for (int i = 0; i < kTileSlots; ++i) hw[i * 64 + lane] = 0u;
+      const float off_ = -lo_ * sc_;
+      stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int, float d2) {
+        const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f);
+        atomicAdd(&hw[(ix + 1) * 64 + lane], 1u);
+      });
+#pragma unroll
+      for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
+    };
+    hist(0.0f, (float)kHistBins / R2);
+    int total = 0;
+#pragma unroll
+    for (int i = 0; i < kHistBins; ++i) total += th.count(i);
+    fb = total < kneed;
+    if (fb && d.stats) atomicAdd(&d.stats[7], 1ull);
+    float lo = 0.f, hi = R2, L = 0.f, U = 0.f;
+    for (int lvl = 0; !fb; ++lvl) {
+      int cum, cb;
+      if (!hist_locate(th, kneed, th.count(-1), lo, hi, &L, &U, &cum, &cb)) {
+        fb = true;
+        break;
+      }
+      if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
+      lo = L;
+      hi = U;
+      hist(lo, (float)kHistBins / (hi - lo));
+    }
+    if (dbg == 2) {
+      if (L == 12345.f) out[0] = 0.f;
+      return;
+    }
+    if (!fb) {
+      const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
+      int n = 0;
+      stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
+        lst[min(n, kListMax)][lane] = (uint16_t)pp;
+        n += d2 < Up ? 1 : 0;
+      });
+      if (dbg == 3) {
+        if (n == 12345) out[0] = 0.f;
+        return;
+      }
+      if (n > kListMax && d.stats) atomicAdd(&d.stats[5], 1ull);
+      fb = n > kListMax ||
+           !finish_selection<KMAX>(
+               q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); }, prior,
+               oi, out, dbg == 4);
+    }
+  }
+  if (fb) {
+    if (d.stats) atomicAdd(&d.stats[4], 1ull);
+    const int at = atomicAdd(fb_len, 1);
+    fb_list[at] = (int32_t)vq;
+  }
+}
 
 
 // ---------------------------------------------------------------------------
@@ -1063,45 +1273,51 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Rows of the (2S+1)^3 cube (S <= 3: one lane per row) into the wave's LDS
+// Rows of the (2S+1)^3 cube (S <= 5: two rows per lane) into the wave's LDS
 // row table: ra = first cell-sorted position, rp = prefix of the row lengths;
 // each row is trimmed to the x-cells whose boxes (widened by 2 slack) come
 // closer to q than sqrt(r2), rows that do not are dropped.  Returns the
 // candidate count.  One round of loads, then every scan walks the rows'
 // points as one flat range.
-constexpr int kWaveMaxS = 3;
+constexpr int kWaveMaxS = 5;
+constexpr int kWaveRows = 128;  // >= (2 kWaveMaxS + 1)^2
 
 __device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int cx, int cy, int cz, int S, float r2,
                                          int lane, int32_t* __restrict__ ra, int32_t* __restrict__ rp) {
   const int side = 2 * S + 1, nr = side * side;
-  int a = 0, len = 0;
-  if (lane < nr) {
-    const int z = cz + lane / side - S, y = cy + lane % side - S;
-    if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
-      const float y0 = g.oy + (float)y * g.h, z0 = g.oz + (float)z * g.h, sl = 2.0f * g.slack;
-      const float dy = fmaxf(fmaxf(y0 - q.y, q.y - (y0 + g.h)) - sl, 0.0f);
-      const float dz = fmaxf(fmaxf(z0 - q.z, q.z - (z0 + g.h)) - sl, 0.0f);
-      const float rem = r2 - fmaf(dy, dy, dz * dz);
-      if (rem > 0.0f) {
-        const float rx = sqrtf(rem) + sl;
-        const int x0 = max(max(cx - S, 0), (int)floorf((q.x - rx - g.ox) * g.inv_h));
-        const int x1 = min(min(cx + S, g.nx - 1), (int)floorf((q.x + rx - g.ox) * g.inv_h));
-        if (x0 <= x1) {
-          const int rb = g.nx * (y + g.ny * z);
-          a = g.start[rb + x0];
-          len = g.start[rb + x1 + 1] - a;
+  int carry = 0;
+  if (lane == 0) rp[0] = 0;
+  for (int h = 0; h * 64 < nr; ++h) {
+    const int row = lane + 64 * h;
+    int a = 0, len = 0;
+    if (row < nr) {
+      const int z = cz + row / side - S, y = cy + row % side - S;
+      if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
+        const float y0 = g.oy + (float)y * g.h, z0 = g.oz + (float)z * g.h, sl = 2.0f * g.slack;
+        const float dy = fmaxf(fmaxf(y0 - q.y, q.y - (y0 + g.h)) - sl, 0.0f);
+        const float dz = fmaxf(fmaxf(z0 - q.z, q.z - (z0 + g.h)) - sl, 0.0f);
+        const float rem = r2 - fmaf(dy, dy, dz * dz);
+        if (rem > 0.0f) {
+          const float rx = sqrtf(rem) + sl;
+          const int x0 = max(max(cx - S, 0), (int)floorf((q.x - rx - g.ox) * g.inv_h));
+          const int x1 = min(min(cx + S, g.nx - 1), (int)floorf((q.x + rx - g.ox) * g.inv_h));
+          if (x0 <= x1) {
+            const int rb = g.nx * (y + g.ny * z);
+            a = cell_start(g, rb + x0);
+            len = cell_start(g, rb + x1 + 1) - a;
+          }
         }
       }
     }
+    const int inc = wave_incl_scan(len) + carry;
+    if (row < nr) {
+      ra[row] = a;
+      rp[row + 1] = inc;
+    }
+    carry = __shfl(inc, 63, 64);
   }
-  const int inc = wave_incl_scan(len);
-  if (lane < nr) {
-    ra[lane] = a;
-    rp[lane + 1] = inc;
-  }
-  if (lane == 0) rp[0] = 0;
   wave_sync();
-  return __shfl(inc, 63, 64);
+  return carry;
 }
 
 // The cube's candidates as one flat range, 256 per step (four independent
@@ -1169,9 +1385,9 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   // A query the tile handed on (s0 = 2) rarely needs more than the shell-1
   // reach + h/2: that ball first (fewer rows and x-cells of the 5^3 cube),
   // then the whole shell.
-  bool trial = s0 == 2;
+  bool trial = s0 >= 2;
   for (;;) {
-    if (S >= rmax || S > kWaveMaxS) {  // beyond one lane per row, or the whole grid: the exact path
+    if (S >= rmax || S > kWaveMaxS) {  // beyond the row table, or the whole grid: the exact path
       fb = true;
       break;
     }
@@ -1336,8 +1552,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_wav
     int32_t* __restrict__ fb_len, int s0) {
   __shared__ int32_t sel[kWavesPerBlock][KMAX];
   __shared__ int32_t bnd[kWavesPerBlock][kWaveBnd];
-  __shared__ int32_t ra[kWavesPerBlock][64];
-  __shared__ int32_t rp[kWavesPerBlock][65];
+  __shared__ int32_t ra[kWavesPerBlock][kWaveRows];
+  __shared__ int32_t rp[kWavesPerBlock][kWaveRows + 1];
   __shared__ float cd2[kWavesPerBlock][kWaveCache];
   __shared__ int32_t cpos[kWavesPerBlock][kWaveCache];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1553,6 +1769,87 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
   return 0;
 }
 
+// KNN normals straight off the dense voxel table (k_normals_stile; hand-offs
+// to the wave form and the register top-k over the table).  1: not applicable
+// (the caller builds a search grid instead).
+static int normals_dense_vox(const double* geom, const float4* vox, const float* xyz, int64_t n, int mode, int knn,
+                             const float* prior, float* out, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (!vox || geom[7] != 1.0 || mode != O3DX_SEARCH_KNN || getenv("O3DX_NO_STILE")) return 1;
+  const int kneed = (int)std::min<int64_t>(knn, n);
+  if (kneed < 1 || kneed > 32 || !(geom[8] > 0.0)) return 1;
+  // occupied fraction of the voxels inside occupied 2^3 cells: the 5^3
+  // stencil holds the k nearest only where the voxels are well filled
+  const double dens = (double)n / (8.0 * geom[8]);
+  const double kth = std::cbrt((double)kneed / (std::min(dens, 1.0) * 4.18879020478639098));  // voxels
+  if (dens < 0.7 || kth > 2.0) return 1;  // the stencil ball (2.45 voxels) holds k with a wide margin
+  DenseVox d;
+  d.vox = vox;
+  d.nx = (int)geom[4];
+  d.ny = (int)geom[5];
+  d.nz = (int)geom[6];
+  d.nbx = (d.nx + kVB - 1) / kVB;
+  d.nby = (d.ny + kVB - 1) / kVB;
+  d.nbz = (d.nz + kVB - 1) / kVB;
+  const int64_t nb = (int64_t)d.nbx * d.nby * d.nbz;
+  if (nb <= 0 || nb > INT32_MAX || (int64_t)d.nx * d.ny * d.nz > INT32_MAX) return 1;
+  d.ox = (float)geom[0];
+  d.oy = (float)geom[1];
+  d.oz = (float)geom[2];
+  d.vs = (float)geom[3];
+  d.inv_vs = (float)(1.0 / geom[3]);
+  double maxabs = 0.0, maxext = 0.0;
+  const int vn[3] = {d.nx, d.ny, d.nz};
+  for (int a = 0; a < 3; ++a) {
+    const double ext = vn[a] * geom[3];
+    maxabs = std::max(maxabs, std::max(std::fabs(geom[a]), std::fabs(geom[a] + ext)));
+    maxext = std::max(maxext, ext);
+  }
+  const double slack = 32.0 * std::ldexp(1.0, -24) * (maxabs + maxext) + 1e-6 * geom[3];
+  const double R = kStencilR * geom[3] - slack;
+  d.rc2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
+  d.stats = search_stats_ptr();
+  Arena ar((char*)ws, ws_bytes);
+  int32_t* lens = ar.take<int32_t>(4);
+  int32_t* list = ar.take<int32_t>(n);
+  int32_t* list2 = ar.take<int32_t>(n);
+  O3DX_ARENA_CHECK(ar);
+  O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
+  {
+    KTimer kt("normals_knn", s);
+    {
+      KTimer kt_tile("normals_stile", s);
+      // O3DX_TILE_DEBUG=1/2/3/4: stop after staging / histogram / list scan / moments (profiling only)
+      const char* dbg = getenv("O3DX_TILE_DEBUG");
+      hipLaunchKernelGGL(k_normals_stile<32>, dim3((unsigned)nb), dim3(64), 0, s, d, kneed, prior, out, list, lens,
+                         getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dbg ? atoi(dbg) : 0);
+    }
+    // the table as a dense GridView (identity cell starts, <= 1 point per cell)
+    GridView g{};
+    g.pts = vox;
+    g.start = nullptr;
+    g.dense = 1;
+    g.ox = (float)geom[0];
+    g.oy = (float)geom[1];
+    g.oz = (float)geom[2];
+    g.h = (float)geom[3];
+    g.inv_h = (float)(1.0 / geom[3]);
+    g.slack = (float)slack;
+    g.nx = d.nx;
+    g.ny = d.ny;
+    g.nz = d.nz;
+    g.n = (int64_t)d.nx * d.ny * d.nz;
+    g.stats = d.stats;
+    KTimer kt_wave("normals_wave", s);
+    hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(2048), dim3(64 * kWavesPerBlock), 0, s, g, kneed, prior, out,
+                       list, lens, list2, lens + 1, 3);
+    kt_wave.stop();
+    hipLaunchKernelGGL(k_normals_knn<32>, dim3(64), dim3(kBlock), 0, s, g, xyz, kneed, 0, 0.0, prior, out, list2,
+                       lens + 1);
+  }
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
 // The normals on a built grid: shared by o3dx_estimate_normals (grid sorted
 // from the points) and o3dx_estimate_normals_voxel (grid read off the voxel
 // table).  `xyz` is the caller's point array the grid's w fields index.
@@ -1682,6 +1979,9 @@ extern "C" int o3dx_estimate_normals_voxel(const double* geom, const float* voxe
   if (!ws || ws_bytes < o3dx_normals_workspace_bytes(n)) return fail(O3DX_ENOMEM, "normals workspace too small");
   if (n == 0) return 0;
   hipStream_t s = as_stream(stream);
+  const int rd = normals_dense_vox(geom, reinterpret_cast<const float4*>(voxel_pts), xyz, n, mode, knn, prior, out, ws,
+                                   ws_bytes, s);
+  if (rd != 1) return rd;
   GridBuild G;
   const int rc = grid_from_voxels(geom, reinterpret_cast<const float4*>(voxel_pts), n, occ_for(mode, knn), ws, ws_bytes,
                                   s, &G);

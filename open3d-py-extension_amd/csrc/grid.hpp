@@ -26,7 +26,12 @@ struct GridView {
   unsigned long long* stats;  // debug: {queries, cells visited, candidates, shells}; null = off
   int blocked;                // cell order: 0 = row-major (x fastest; searchable), 1 = 8^3 blocks
   int bnx, bny;               // blocked order: number of blocks along x, y
+  int dense = 0;              // 1: pts is a dense voxel table (<= 1 point per cell, empty = NaN
+                              // coordinates, w = -1) and start is the identity (start may be null)
 };
+
+// First sorted position of cell c (dense tables: the cell itself).
+__device__ __forceinline__ int cell_start(const GridView& g, int c) { return g.dense ? c : g.start[c]; }
 
 // Cell index.  Row-major (x fastest) keeps every (y,z) row contiguous, which
 // the searches rely on.  The blocked order (spatial_sort only) lists 8x8x8
@@ -109,7 +114,7 @@ __device__ __forceinline__ void for_cube_rows(const GridView& g, int cx, int cy,
       const int y = cy + dy;
       if (y < 0 || y >= g.ny) continue;
       const int rb = g.nx * (y + g.ny * z);
-      f(g.start[rb + x0], g.start[rb + x1 + 1]);
+      f(cell_start(g, rb + x0), cell_start(g, rb + x1 + 1));
     }
   }
 }
@@ -177,15 +182,15 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
   int st_cells = 0, st_cands = 0, r = 0;
   for (r = 0; r <= rmax; ++r) {
     for_shell(g, cx, cy, cz, r, [&](int c) {
-      const int s1 = g.start[c + 1];
+      const int s1 = cell_start(g, c + 1);
       if (g.stats) {
         ++st_cells;
-        st_cands += s1 - g.start[c];
+        st_cands += s1 - cell_start(g, c);
       }
-      for (int p = g.start[c]; p < s1; ++p) {
+      for (int p = cell_start(g, c); p < s1; ++p) {
         const float4 v = g.pts[p];
         const double d = dist2_f64(dqx, dqy, dqz, v);
-        if (!(d < r2lim)) continue;
+        if (!(d < r2lim)) continue;  // NaN (an empty dense cell) fails too
         const int oi = __float_as_int(v.w);
         if (lex_less(d, oi, wd, wi)) {
 #pragma unroll

@@ -367,3 +367,35 @@ def test_voxel_grid_not_kept_when_sparse(dev):
     assert out["voxel_grid"] is None
     ref = ops.voxel_down_sample(x, 0.05, min_bound=[0.2, 0.2, 0.2], max_bound=[0.8, 0.8, 0.8])
     assert torch.equal(out["rep_idx"], ref["rep_idx"])
+
+
+@pytest.mark.parametrize("env", [None, "O3DX_STILE_FORCE_FB", "O3DX_NO_STILE"])
+@pytest.mark.parametrize("k", [5, 30])
+def test_normals_dense_voxel_table(dev, env, k):
+    """Volumetric reps fill their voxels: estimate_normals(voxel_grid=) runs
+    straight off the dense voxel table (k_normals_stile; its hand-off path —
+    wave form and register top-k over the table — forced for every query by
+    O3DX_STILE_FORCE_FB): same normals as the sorted-grid path and the oracle.
+    Non-cubic box, dims not multiples of the 4^3 tile blocks."""
+    import os
+    n = 200_000
+    pts = S.uniform_cube(n, 33) * torch.tensor([1.0, 0.55, 0.3])
+    vs = float((0.165 * 4 / n) ** (1 / 3))
+    x = pts.to(dev)
+    a = ops.voxel_down_sample(x, vs, keep_grid=True)
+    vg = a["voxel_grid"]
+    assert vg is not None
+    if env:
+        os.environ[env] = "1"
+    try:
+        fused = ops.estimate_normals(a["rep_xyz"], knn=k, voxel_grid=vg).cpu().numpy()
+    finally:
+        if env:
+            del os.environ[env]
+    plain = ops.estimate_normals(a["rep_xyz"], knn=k).cpu().numpy()
+    e = np.abs(fused - plain).max(1)
+    assert np.mean(e < 1e-6) > 0.9999, e.max()
+    reps = pts.numpy()[a["rep_idx"].cpu().numpy()]
+    exp = O.estimate_normals(reps, O.KNN, k)
+    _, e_any = _normal_err(fused, exp)
+    assert np.mean(e_any < 1e-5) > 0.999
