@@ -168,12 +168,14 @@ def secondary(dev, args):
     torch.cuda.synchronize(dev)
     t4 = time.perf_counter()
     acc_ms, acc_n = _native.kernel_timing("icp_accumulate")
+    m_ms, m_n = _native.kernel_timing("icp_match")
     _native.set_kernel_timing(False)
     err = np.abs(T - np.linalg.inv(synthetic.rigid_transform())).max()
     out["icp"] = {"n_source": n, "n_target": n, "iterations": args.icp_iters,
                   "iters_per_s": round(args.icp_iters / (t4 - t3), 3),
                   "ms_per_iter": round((t4 - t3) / args.icp_iters * 1e3, 3),
                   "accumulate_kernel_ms": round(acc_ms / max(acc_n, 1), 3),
+                  "match_kernel_ms": round(m_ms / max(m_n, 1), 3),
                   "target_normals_s": round(t1 - t0, 3), "target_build_s": round(t2 - t1, 3),
                   "source_sort_s": round(t2b - t2, 3),
                   "fitness": round(float(sums[28]) / n, 6), "T_err_vs_gt_inverse": float(err),

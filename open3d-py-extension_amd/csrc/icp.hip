@@ -51,43 +51,75 @@ __device__ __forceinline__ void icp_add(double acc[30], double px, double py, do
   acc[29] += d2;
 }
 
-// SORTED: src is float4 (x, y, z, bits(original index)) in the compact spatial
-// order of o3dx_spatial_sort, so the 64 queries of a wave probe neighbouring
-// target cells; else plain (n,3) float32 in caller order.
+// Source point j -> (original index, float64 position under T).  SORTED: src
+// is float4 (x, y, z, bits(original index)) in the compact spatial order of
+// o3dx_spatial_sort, so the 64 queries of a wave probe neighbouring target
+// cells; else plain (n,3) float32 in caller order.
 template <bool SORTED>
-__global__ void __launch_bounds__(kBlock) k_icp_accumulate(const float* __restrict__ src, int64_t ns, GridView g,
-                                                           const float4* __restrict__ tnorm, Mat4 T, double radius,
-                                                           double* __restrict__ partial, int32_t* __restrict__ cj) {
+__device__ __forceinline__ int64_t icp_source(const float* __restrict__ src, int64_t j, const Mat4& T, double* px,
+                                              double* py, double* pz) {
+  double x, y, z;
+  int64_t i;
+  if (SORTED) {
+    const float4 v = reinterpret_cast<const float4*>(src)[j];
+    x = v.x;
+    y = v.y;
+    z = v.z;
+    i = __float_as_int(v.w);
+  } else {
+    i = j;
+    x = src[3 * i];
+    y = src[3 * i + 1];
+    z = src[3 * i + 2];
+  }
+  const double* t = T.m;
+  // Eigen 4x4 * (x,y,z,1): ((T0 x + T1 y) + T2 z) + T3 per row
+  *px = ((t[0] * x + t[1] * y) + t[2] * z) + t[3];
+  *py = ((t[4] * x + t[5] * y) + t[6] * z) + t[7];
+  *pz = ((t[8] * x + t[9] * y) + t[10] * z) + t[11];
+  return i;
+}
+
+// Pass 1 — correspondences: one thread per source point, the 1-NN within
+// max_correspondence_distance (nn_search_dev); writes the target's sorted
+// position (-1: none) and, when asked, the target's original index by source
+// index.  No accumulators live here, so the search runs at full occupancy
+// (the search is latency-bound: many waves hide the dependent cell loads).
+template <bool SORTED>
+__global__ void __launch_bounds__(kBlock) k_icp_match(const float* __restrict__ src, int64_t ns, GridView g, Mat4 T,
+                                                      double radius, int32_t* __restrict__ mpos,
+                                                      int32_t* __restrict__ cj) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ns) return;
+  double px, py, pz;
+  const int64_t i = icp_source<SORTED>(src, j, T, &px, &py, &pz);
+  double d2;
+  int pos;
+  const int tj = nn_search_dev(g, px, py, pz, radius, &d2, &pos);
+  mpos[j] = pos;
+  if (cj) cj[i] = tj;
+}
+
+// Pass 2 — moments: a streaming pass over the matched pairs (source point,
+// target point + normal gathered by sorted position), the 30 float64 sums per
+// lane, wave xor-tree, block, block partials (fixed order: bit-identical run
+// to run).  d^2 is recomputed exactly as the search computed it.
+template <bool SORTED>
+__global__ void __launch_bounds__(kBlock) k_icp_moments(const float* __restrict__ src, int64_t ns, GridView g,
+                                                        const float4* __restrict__ tnorm, Mat4 T,
+                                                        const int32_t* __restrict__ mpos,
+                                                        double* __restrict__ partial) {
   __shared__ double sh[kBlock / 64];
   double acc[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) acc[k] = 0.0;
-  const double* t = T.m;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += (int64_t)gridDim.x * blockDim.x) {
-    double x, y, z;
-    int64_t i;
-    if (SORTED) {
-      const float4 v = reinterpret_cast<const float4*>(src)[j];
-      x = v.x;
-      y = v.y;
-      z = v.z;
-      i = __float_as_int(v.w);
-    } else {
-      i = j;
-      x = src[3 * i];
-      y = src[3 * i + 1];
-      z = src[3 * i + 2];
-    }
-    // Eigen 4x4 * (x,y,z,1): ((T0 x + T1 y) + T2 z) + T3 per row
-    const double px = ((t[0] * x + t[1] * y) + t[2] * z) + t[3];
-    const double py = ((t[4] * x + t[5] * y) + t[6] * z) + t[7];
-    const double pz = ((t[8] * x + t[9] * y) + t[10] * z) + t[11];
-    double d2;
-    int pos;
-    const int tj = nn_search_dev(g, px, py, pz, radius, &d2, &pos);
-    if (cj) cj[i] = tj;
-    if (tj < 0) continue;
-    icp_add(acc, px, py, pz, g.pts[pos], tnorm[pos], d2);
+    const int pos = mpos[j];
+    if (pos < 0) continue;
+    double px, py, pz;
+    icp_source<SORTED>(src, j, T, &px, &py, &pz);
+    const float4 vt = g.pts[pos];
+    icp_add(acc, px, py, pz, vt, tnorm[pos], dist2_f64(px, py, pz, vt));
   }
 #pragma unroll
   for (int k = 0; k < 30; ++k) {
@@ -233,6 +265,7 @@ struct AccWs {
   double* partial;
   double* sums;
   int32_t* cj;
+  int32_t* mpos;
   uint8_t* flags;
   int32_t* src_idx;
   int32_t* scan_tmp;
@@ -243,6 +276,7 @@ static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
   w->partial = ar.take<double>((size_t)kIcpBlocks * kNS);
   w->sums = ar.take<double>(kNS);
   w->cj = ar.take<int32_t>(ns);
+  w->mpos = ar.take<int32_t>(ns);
   w->flags = ar.take<uint8_t>(ns + 16);
   w->src_idx = ar.take<int32_t>(ns);
   w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(ns));
@@ -257,14 +291,22 @@ static int accumulate(const float* src, int64_t ns, bool sorted, const GridView&
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kIcpBlocks, (ns + kBlock - 1) / kBlock));
   const bool want_corr = corr_out != nullptr;
   KTimer kt("icp_accumulate", s);
-  if (ns > 0 && sorted)
-    hipLaunchKernelGGL(k_icp_accumulate<true>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, radius, w.partial,
-                       want_corr ? w.cj : (int32_t*)nullptr);
-  else if (ns > 0)
-    hipLaunchKernelGGL(k_icp_accumulate<false>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, radius, w.partial,
-                       want_corr ? w.cj : (int32_t*)nullptr);
-  else
+  if (ns > 0) {
+    int32_t* cj = want_corr ? w.cj : (int32_t*)nullptr;
+    const unsigned nm = grid_for(ns, kBlock, 1 << 30);
+    KTimer km("icp_match", s);
+    if (sorted)
+      hipLaunchKernelGGL(k_icp_match<true>, dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
+    else
+      hipLaunchKernelGGL(k_icp_match<false>, dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
+    km.stop();
+    if (sorted)
+      hipLaunchKernelGGL(k_icp_moments<true>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, w.partial);
+    else
+      hipLaunchKernelGGL(k_icp_moments<false>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, w.partial);
+  } else {
     O3DX_HIP(hipMemsetAsync(w.partial, 0, kNS * sizeof(double), s));
+  }
   O3DX_TRY(reduce_columns_f64(w.partial, ns > 0 ? nb : 1, kNS, w.sums, s));
   kt.stop();
   O3DX_HIP(hipMemcpyAsync(sums_host, w.sums, kNS * sizeof(double), hipMemcpyDeviceToHost, s));
