@@ -128,15 +128,21 @@ int o3dx_voxel_down_sample(const float* xyz_dev, int64_t n,
  * pcd.voxel_down_sample(vs).estimate_normals(), reference PointCloud.py:361,
  * :68).  o3dx_voxel_grid_cells(n, min, max, vs): the number of voxels nvox of
  * the dense voxel table for these bounds (host arithmetic), 0 when the grid
- * is too sparse to keep.  o3dx_voxel_down_sample_grid: same outputs as
- * o3dx_voxel_down_sample (explicit bounds required), plus
+ * is too sparse to keep; o3dx_voxel_grid_capacity(n): the largest nvox any
+ * call on n points keeps (a table buffer of that many voxels fits whatever
+ * the bounds turn out to be).  o3dx_voxel_down_sample_grid: same outputs as
+ * o3dx_voxel_down_sample (null bounds: the AABB, computed on the device),
+ * plus, when nvox <= voxel_cells (the capacity of voxel_pts_dev),
  *   voxel_pts_dev[0..4 nvox)  per voxel (x, y, z, output row as int32 bits)
  *                             of its representative, row -1 when empty
  *   geom_host[12]             {min_bound xyz, voxel_size, nx, ny, nz, valid,
  *                              occupied 2^3-voxel cells, 0, 0, nvox}
- * valid = 0 when the table could not be kept (points outside the bounds). */
+ * valid = 0 when the table could not be kept (too sparse, larger than
+ * voxel_cells, or points outside the bounds).  One host synchronisation for
+ * m (two with null bounds). */
 int64_t o3dx_voxel_grid_cells(int64_t n, const double* min_bound_host,
                               const double* max_bound_host, double voxel_size);
+int64_t o3dx_voxel_grid_capacity(int64_t n);
 int o3dx_voxel_down_sample_grid(const float* xyz_dev, int64_t n,
                                 const double* min_bound_host,
                                 const double* max_bound_host, double voxel_size,

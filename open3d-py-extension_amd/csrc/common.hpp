@@ -140,15 +140,28 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 // o3dx_set_kernel_timing); read back lazily by o3dx_kernel_timing.
 bool timing_on();
 void timing_push(const char* name, hipEvent_t a, hipEvent_t b);
+hipEvent_t timing_event();           // from the recycled pool (or new)
+void timing_release(hipEvent_t e);   // back to the pool
+// Wait for the stream's work to finish (polling first; see core.hip).
+int host_wait(hipStream_t s);
+// Device -> host copy of a small result, then host_wait.
+int read_back(void* dst_host, const void* src_dev, size_t bytes, hipStream_t s);
 struct KTimer {
   const char* name;
   hipStream_t s;
   hipEvent_t a = nullptr, b = nullptr;
   KTimer(const char* n, hipStream_t st) : name(n), s(st) {
-    if (timing_on() && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
-      (void)hipEventRecord(a, s);
-    else
-      a = b = nullptr;
+    if (timing_on()) {
+      a = timing_event();
+      b = timing_event();
+      if (a && b) {
+        (void)hipEventRecord(a, s);
+      } else {
+        timing_release(a);
+        timing_release(b);
+        a = b = nullptr;
+      }
+    }
   }
   void stop() {
     if (a && b) {
@@ -158,8 +171,8 @@ struct KTimer {
     a = b = nullptr;
   }
   void cancel() {  // drop without recording (a later KTimer of the same name takes over)
-    if (a) (void)hipEventDestroy(a);
-    if (b) (void)hipEventDestroy(b);
+    timing_release(a);
+    timing_release(b);
     a = b = nullptr;
   }
   ~KTimer() { stop(); }

@@ -3,6 +3,7 @@
 // AABB replaces o3d PointCloud.get_min_bound/get_max_bound
 // (reference open3dpypro/PointCloud.py:145-146, :340).  HBM-bound: 12 B/point.
 #include <cstdarg>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -21,7 +22,59 @@ struct Pending {
 static std::vector<Pending> g_pending;
 static std::map<std::string, std::pair<double, int64_t>> g_times;
 
+static std::vector<hipEvent_t> g_free_events;  // recycled: no event creation on the launch path
+
 bool timing_on() { return g_timing; }
+
+hipEvent_t timing_event() {
+  {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if (!g_free_events.empty()) {
+      hipEvent_t e = g_free_events.back();
+      g_free_events.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+
+void timing_release(hipEvent_t e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_free_events.push_back(e);
+}
+
+int read_back(void* dst_host, const void* src_dev, size_t bytes, hipStream_t s) {
+  // small read-backs go through a per-thread pinned staging buffer (a direct
+  // DMA target; pageable destinations take the runtime's staged path)
+  constexpr size_t kCap = 64 << 10;
+  thread_local void* pin = nullptr;
+  if (bytes <= kCap) {
+    if (!pin && hipHostMalloc(&pin, kCap, hipHostMallocDefault) != hipSuccess) pin = nullptr;
+    if (pin) {
+      O3DX_HIP(hipMemcpyAsync(pin, src_dev, bytes, hipMemcpyDeviceToHost, s));
+      O3DX_TRY(host_wait(s));
+      std::memcpy(dst_host, pin, bytes);
+      return 0;
+    }
+  }
+  O3DX_HIP(hipMemcpyAsync(dst_host, src_dev, bytes, hipMemcpyDeviceToHost, s));
+  return host_wait(s);
+}
+
+int host_wait(hipStream_t s) {
+  // poll instead of a blocking wait: the short read-backs on the launch path
+  // (counts, bounds) return as soon as the copy lands, without an interrupt
+  // wake-up; falls back to the blocking wait after ~2 ms
+  for (int i = 0; i < 4096; ++i) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) break;
+  }
+  O3DX_HIP(hipStreamSynchronize(s));
+  return 0;
+}
 
 void timing_push(const char* name, hipEvent_t a, hipEvent_t b) {
   std::lock_guard<std::mutex> lk(g_tmu);
@@ -42,8 +95,8 @@ static void timing_drain() {
       t.first += ms;
       t.second += 1;
     }
-    (void)hipEventDestroy(e.a);
-    (void)hipEventDestroy(e.b);
+    timing_release(e.a);
+    timing_release(e.b);
   }
 }
 
@@ -367,7 +420,6 @@ extern "C" int o3dx_aabb(const float* xyz, int64_t n, double* minmax_host, void*
   char* w = (char*)ws;
   double* mm = reinterpret_cast<double*>(w + aabb_ws_bytes(n));
   O3DX_TRY(aabb_device(xyz, n, mm, w, s));
-  O3DX_HIP(hipMemcpyAsync(minmax_host, mm, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(minmax_host, mm, 6 * sizeof(double), s));
   return 0;
 }

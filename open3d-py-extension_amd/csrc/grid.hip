@@ -173,8 +173,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
 
   double mm[6];
   O3DX_TRY(aabb_device(xyz, n, G.mm, G.aabb_ws, s));
-  O3DX_HIP(hipMemcpyAsync(mm, G.mm, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(mm, G.mm, 6 * sizeof(double), s));
   const double mn[3] = {mm[0], mm[1], mm[2]}, mx[3] = {mm[3], mm[4], mm[5]};
   double ext[3], maxabs = 0, maxext = 0;
   for (int a = 0; a < 3; ++a) {
@@ -245,8 +244,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
       O3DX_HIP(hipMemsetAsync(G.scratch, 0, sizeof(int64_t), s));
       hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(nc, kBlock, 1024)), dim3(kBlock), 0, s, G.count, nc,
                          (unsigned long long*)G.scratch);
-      O3DX_HIP(hipMemcpyAsync(&occ, G.scratch, sizeof(occ), hipMemcpyDeviceToHost, s));
-      O3DX_HIP(hipStreamSynchronize(s));
+      O3DX_TRY(read_back(&occ, G.scratch, sizeof(occ), s));
       double mean_occ = occ ? nn / (double)occ : nn;
       if (mean_occ > 2.5 * target_occ) {
         double hn = h * std::sqrt(target_occ / mean_occ);

@@ -309,13 +309,11 @@ static int accumulate(const float* src, int64_t ns, bool sorted, const GridView&
   }
   O3DX_TRY(reduce_columns_f64(w.partial, ns > 0 ? nb : 1, kNS, w.sums, s));
   kt.stop();
-  O3DX_HIP(hipMemcpyAsync(sums_host, w.sums, kNS * sizeof(double), hipMemcpyDeviceToHost, s));
   if (want_corr && ns > 0) {
     hipLaunchKernelGGL(k_corr_flags, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, ns, w.flags);
     O3DX_TRY(compact_flags(w.flags, ns, w.src_idx, nullptr, w.cnt, w.scan_tmp, s));
     int64_t m = 0;
-    O3DX_HIP(hipMemcpyAsync(&m, w.cnt, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    O3DX_HIP(hipStreamSynchronize(s));
+    O3DX_TRY(read_back(&m, w.cnt, sizeof(int64_t), s));
     if (m > 0)
       hipLaunchKernelGGL(k_corr_pairs, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, w.src_idx, m,
                          corr_out);
@@ -323,7 +321,7 @@ static int accumulate(const float* src, int64_t ns, bool sorted, const GridView&
   } else if (ncorr) {
     *ncorr = -1;
   }
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(sums_host, w.sums, kNS * sizeof(double), s));
   O3DX_HIP(hipGetLastError());
   if (ncorr && !want_corr) *ncorr = (int64_t)sums_host[28];
   return 0;

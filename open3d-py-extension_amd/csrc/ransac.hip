@@ -306,8 +306,7 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
 static int absmax_of(const float* xyz, int64_t n, void* aabb_ws, double* mm_dev, hipStream_t s, double out[3]) {
   double mm[6];
   O3DX_TRY(aabb_device(xyz, n, mm_dev, aabb_ws, s));
-  O3DX_HIP(hipMemcpyAsync(mm, mm_dev, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(mm, mm_dev, 6 * sizeof(double), s));
   for (int a = 0; a < 3; ++a) out[a] = std::max(std::fabs(mm[a]), std::fabs(mm[3 + a]));
   return 0;
 }
@@ -333,8 +332,7 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
   kt.stop();
   counts.resize(H);
-  O3DX_HIP(hipMemcpyAsync(counts.data(), w.counts, H * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(counts.data(), w.counts, H * sizeof(int64_t), s));
   O3DX_HIP(hipGetLastError());
   return 0;
 }
@@ -349,8 +347,7 @@ static int run_abs_sum(const float* xyz, int64_t n, const double* planes, const 
   hipLaunchKernelGGL(k_plane_abs_sum, dim3(kSumBlocksX, L), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, w.sum_partial);
   // fixed-order final sums on the host
   std::vector<double> part((size_t)kSumBlocksX * L);
-  O3DX_HIP(hipMemcpyAsync(part.data(), w.sum_partial, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(part.data(), w.sum_partial, part.size() * sizeof(double), s));
   O3DX_HIP(hipGetLastError());
   for (int j = 0; j < L; ++j) {
     double t = 0.0;
@@ -412,8 +409,7 @@ static int run_moments(const float* xyz, const int32_t* idx, int64_t m, const do
   hipLaunchKernelGGL(k_plane_moments, dim3(nb), dim3(kBlock), 0, s, xyz, idx, m, centroid ? centroid[0] : 0.0,
                      centroid ? centroid[1] : 0.0, centroid ? centroid[2] : 0.0, centroid ? 1 : 0, part);
   O3DX_TRY(reduce_columns_f64(part, nb, 6, out_dev, s));
-  O3DX_HIP(hipMemcpyAsync(out, out_dev, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(out, out_dev, 6 * sizeof(double), s));
   O3DX_HIP(hipGetLastError());
   return 0;
 }
@@ -549,8 +545,7 @@ extern "C" int o3dx_plane_inliers(const float* xyz, int64_t n, const double* pla
   hipLaunchKernelGGL(k_plane_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1],
                      plane[2], plane[3], thr, flags);
   O3DX_TRY(compact_flags(flags, n, idx_out, nullptr, cnt, tmp, s));
-  O3DX_HIP(hipMemcpyAsync(count_host, cnt, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipStreamSynchronize(s));
+  O3DX_TRY(read_back(count_host, cnt, sizeof(int64_t), s));
   return 0;
 }
 
@@ -600,8 +595,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     O3DX_HIP(hipMemcpyAsync(w.sidx, samples_host, ns * sizeof(int32_t), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_gather_samples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, xyz, w.sidx, ns, w.scoord);
     std::vector<float> sc((size_t)ns * 3);
-    O3DX_HIP(hipMemcpyAsync(sc.data(), w.scoord, sc.size() * sizeof(float), hipMemcpyDeviceToHost, s));
-    O3DX_HIP(hipStreamSynchronize(s));
+    O3DX_TRY(read_back(sc.data(), w.scoord, sc.size() * sizeof(float), s));
     std::vector<double> P((size_t)ransac_n * 3);
     for (int h = 0; h < H; ++h) {
       for (int j = 0; j < ransac_n * 3; ++j) P[j] = (double)sc[(size_t)h * ransac_n * 3 + j];
@@ -628,8 +622,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     hipLaunchKernelGGL(k_plane_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, bp[0], bp[1], bp[2],
                        bp[3], thr, w.flags);
     O3DX_TRY(compact_flags(w.flags, n, inliers_out, nullptr, w.cnt, w.scan_tmp, s));
-    O3DX_HIP(hipMemcpyAsync(&k, w.cnt, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    O3DX_HIP(hipStreamSynchronize(s));
+    O3DX_TRY(read_back(&k, w.cnt, sizeof(int64_t), s));
   }
   *n_inliers_host = k;
   // GetPlaneFromPoints over the final inliers (zero plane when there are none)

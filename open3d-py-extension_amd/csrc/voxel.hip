@@ -316,8 +316,13 @@ __global__ void __launch_bounds__(kBlock) k_voxel_mark(const int32_t* __restrict
   }
 }
 
+// The representatives' count is read on the device (cnt[0] = m, cnt[1] =
+// error flag of the assign pass: nothing is gathered then), so the gathers
+// are queued before the host reads m back.
 __global__ void __launch_bounds__(kBlock) k_gather_xyz(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
-                                                       int64_t m, float* __restrict__ out) {
+                                                       const int64_t* __restrict__ cnt, float* __restrict__ out) {
+  if ((int)(cnt[1] & 0xffffffff) != 0) return;
+  const int64_t m = cnt[0];
   const P3* p = reinterpret_cast<const P3*>(xyz);
   P3* o = reinterpret_cast<P3*>(out);
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x)
@@ -350,8 +355,10 @@ __global__ void __launch_bounds__(kBlock) k_voxel_trace(const float* __restrict_
 // Thread per representative (its row is j): the gather of rep_xyz plus one
 // 16-byte scatter, so the normals later read the reps in voxel order.
 __global__ void __launch_bounds__(kBlock) k_gather_vox(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
-                                                       int64_t m, VoxelGeom g, float* __restrict__ rep_xyz,
-                                                       float4* __restrict__ vox) {
+                                                       const int64_t* __restrict__ cnt, VoxelGeom g,
+                                                       float* __restrict__ rep_xyz, float4* __restrict__ vox) {
+  if ((int)(cnt[1] & 0xffffffff) != 0) return;
+  const int64_t m = cnt[0];
   const P3* p = reinterpret_cast<const P3*>(xyz);
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     const P3 q = p[idx[j]];
@@ -451,6 +458,8 @@ static void voxel_dims(const double mn[3], const double mx[3], double vs, double
   for (int a = 0; a < 3; ++a) dims[a] = std::floor(std::max(0.0, mx[a] - mn[a]) / vs) + 1.0;
 }
 
+extern "C" int64_t o3dx_voxel_grid_capacity(int64_t n) { return n > 0 ? dense_cap(n) : 0; }
+
 extern "C" int64_t o3dx_voxel_grid_cells(int64_t n, const double* min_bound_host, const double* max_bound_host,
                                          double voxel_size) {
   if (!min_bound_host || !max_bound_host || !(voxel_size > 0.0) || n <= 0) return 0;
@@ -484,8 +493,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   if (!min_bound_host || !max_bound_host) {
     double mm[6];
     O3DX_TRY(aabb_device(xyz, n, w.mm, w.aabb, s));
-    O3DX_HIP(hipMemcpyAsync(mm, w.mm, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
-    O3DX_HIP(hipStreamSynchronize(s));
+    O3DX_TRY(read_back(mm, w.mm, 6 * sizeof(double), s));
     for (int a = 0; a < 3; ++a) {
       mn[a] = min_bound_host ? min_bound_host[a] : mm[a];
       mx[a] = max_bound_host ? max_bound_host[a] : mm[3 + a];
@@ -540,7 +548,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       KTimer kc("voxel_compact", s);
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
                              w.scan_tmp, s));
-      if (vox && nslots == vox_cap) {
+      if (vox && nslots <= vox_cap) {
         O3DX_HIP(hipMemsetAsync(vox, 0xFF, (size_t)nslots * 4 * sizeof(float), s));
         const int64_t nc2 = (int64_t)((g.nx + 1) / 2) * ((g.ny + 1) / 2) * ((g.nz + 1) / 2);
         hipLaunchKernelGGL(k_voxel_occ2, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table, g,
@@ -570,8 +578,15 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
                              w.scan_tmp, s));
     }
-    O3DX_HIP(hipMemcpyAsync(counts, w.count, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    O3DX_HIP(hipStreamSynchronize(s));
+    // gathers sized by the device-side count (at most n rows), queued ahead
+    // of the read-back so they overlap the host round trip
+    const unsigned gg = grid_for(n, kBlock, 8192);
+    if (grid_kept)
+      hipLaunchKernelGGL(k_gather_vox, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, g, rep_xyz,
+                         reinterpret_cast<float4*>(vox));
+    else if (rep_xyz)
+      hipLaunchKernelGGL(k_gather_xyz, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, rep_xyz);
+    O3DX_TRY(read_back(counts, w.count, 3 * sizeof(int64_t), s));
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
     if (errflag == 2 || !dense)
@@ -585,11 +600,6 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
                            (double)counts[2], 0.0, 0.0, nvox};
     for (int k = 0; k < 12; ++k) geom[k] = gv[k];
   }
-  if (grid_kept && m > 0)
-    hipLaunchKernelGGL(k_gather_vox, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, xyz, rep_idx, m, g, rep_xyz,
-                       reinterpret_cast<float4*>(vox));
-  else if (rep_xyz && m > 0)
-    hipLaunchKernelGGL(k_gather_xyz, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, xyz, rep_idx, m, rep_xyz);
   if ((voxel_of_point || cubic_id) && m > 0) {
     if (cubic_id) O3DX_HIP(hipMemsetAsync(cubic_id, 0xFF, (size_t)m * 8 * sizeof(int32_t), s));
     hipLaunchKernelGGL(k_voxel_trace, dim3(grid), dim3(kBlock), 0, s, xyz, n, g, w.vid, w.table, w.pos,

@@ -44,6 +44,7 @@ _SIGS = {
     "o3dx_voxel_workspace_bytes": (_SZ, [_I64]),
     "o3dx_voxel_down_sample": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_voxel_grid_cells": (_I64, [_I64, _P, _P, _D]),
+    "o3dx_voxel_grid_capacity": (_I64, [_I64]),
     "o3dx_voxel_down_sample_grid": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P]),
     "o3dx_normals_workspace_bytes": (_SZ, [_I64]),
     "o3dx_estimate_normals_voxel": (_I32, [_P, _P, _P, _I64, _I32, _I32, _D, _P, _P, _P, _SZ, _P]),
@@ -122,7 +123,13 @@ def default_device() -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device: torch.device) -> int:
+    # the raw handle without building a torch.cuda.Stream (launch-path cost)
+    if _raw_stream is not None and device.index is not None:
+        return _raw_stream(device.index)
     return torch.cuda.current_stream(device).cuda_stream
 
 
@@ -137,7 +144,7 @@ _ws = {}
 
 
 def workspace(nbytes: int, device: torch.device, slot: str = "main") -> torch.Tensor:
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream, slot)
+    key = (device.index, stream_ptr(device), slot)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

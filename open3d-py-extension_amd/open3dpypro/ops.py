@@ -65,11 +65,10 @@ def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_
     m = np.zeros(1, np.int64)
     cells = 0
     if keep_grid and n > 0:
-        if mnb is None or mxb is None:
-            amn, amx = aabb(x)
-            mnb = _c(amn, np.float64) if mnb is None else mnb
-            mxb = _c(amx, np.float64) if mxb is None else mxb
-        cells = int(L.o3dx_voxel_grid_cells(n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size)))
+        # a table buffer for the largest grid the library keeps: the bounds
+        # (and the AABB when they are not given) stay on the library's side,
+        # no extra host round trip
+        cells = int(L.o3dx_voxel_grid_capacity(n))
     geom = np.zeros(12, np.float64)
     if cells > 0:
         vox = torch.empty((cells, 4), dtype=torch.float32, device=dev)
