@@ -102,13 +102,15 @@ __global__ void __launch_bounds__(kBlock) k_grid_cell_sort(const int32_t* __rest
   }
 }
 
-static int64_t cap_cells(int64_t n) { return std::max<int64_t>(4 * n, 4096); }
+// cell-index capacity: cap_mult cells per point (the dense start table costs
+// 8 B per cell: count + start)
+static int64_t cap_cells(int64_t n, int cap_mult) { return std::max<int64_t>((int64_t)cap_mult * n, 4096); }
 
 struct GridLayout {
   size_t pts, extra, tmp, tmp_extra, count, start, cell, rank, scan, aabb, mm, scratch, total;
 };
 
-static GridLayout grid_layout(int64_t n) {
+static GridLayout grid_layout(int64_t n, int cap_mult) {
   n = std::max<int64_t>(n, 1);
   GridLayout L;
   size_t o = 0;
@@ -117,7 +119,7 @@ static GridLayout grid_layout(int64_t n) {
     o += Arena::align(bytes + 1);
     return at;
   };
-  int64_t cc = cap_cells(n);
+  int64_t cc = cap_cells(n, cap_mult);
   L.pts = put(n * sizeof(float4));
   L.extra = put(n * sizeof(float4));
   L.tmp = put(n * sizeof(float4));
@@ -134,7 +136,7 @@ static GridLayout grid_layout(int64_t n) {
   return L;
 }
 
-size_t grid_ws_bytes(int64_t n) { return grid_layout(n).total; }
+size_t grid_ws_bytes(int64_t n, int cap_mult) { return grid_layout(n, cap_mult).total; }
 
 // Debug-only search statistics (o3dx_search_stats): the one place the library
 // allocates device memory, and only after o3dx_set_search_stats(1).
@@ -153,8 +155,9 @@ static int64_t cell_space(const int64_t d[3], bool blocked) {
 }
 
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
-               hipStream_t s, GridBuild* out, float4* extra_sorted, const float* extra_src, bool blocked) {
-  GridLayout L = grid_layout(n);
+               hipStream_t s, GridBuild* out, float4* extra_sorted, const float* extra_src, bool blocked,
+               int cap_mult) {
+  GridLayout L = grid_layout(n, cap_mult);
   if (ws_bytes < L.total) return fail(O3DX_ENOMEM, "grid workspace too small (need %zu)", L.total);
   char* w = (char*)ws;
   GridBuild& G = *out;
@@ -167,7 +170,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
   G.aabb_ws = w + L.aabb;
   G.mm = (double*)(w + L.mm);
   G.scratch = (int64_t*)(w + L.scratch);
-  G.cap_cells = cap_cells(std::max<int64_t>(n, 1));
+  G.cap_cells = cap_cells(std::max<int64_t>(n, 1), cap_mult);
   if (!extra_sorted && extra_src) extra_sorted = (float4*)(w + L.extra);
   G.extra = extra_sorted;
 
@@ -1688,7 +1691,7 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
   if (!vox || geom[7] != 1.0 || getenv("O3DX_NO_VOXEL_GRID")) return 1;
   const int vn[3] = {(int)geom[4], (int)geom[5], (int)geom[6]};
   const double vs = geom[3];
-  GridLayout L = grid_layout(n);
+  GridLayout L = grid_layout(n, 4);
   if (ws_bytes < L.total) return fail(O3DX_ENOMEM, "grid workspace too small (need %zu)", L.total);
   // b: mean points per occupied cell closest to the target.  One rep per
   // occupied voxel and the occupied 2^3 cells give the cloud's local
@@ -1701,7 +1704,7 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
   for (int c = 1; c <= 4; ++c) {
     int64_t cells = 1;
     for (int a = 0; a < 3; ++a) cells *= (vn[a] + c - 1) / c;
-    if (cells > cap_cells(n)) continue;
+    if (cells > cap_cells(n, 4)) continue;
     const double err = std::fabs(D * std::log((double)c) - std::log(target_occ));
     if (b == 0 || err < best) {
       b = c;
@@ -1721,7 +1724,7 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
   G.aabb_ws = w + L.aabb;
   G.mm = (double*)(w + L.mm);
   G.scratch = (int64_t*)(w + L.scratch);
-  G.cap_cells = cap_cells(n);
+  G.cap_cells = cap_cells(n, 4);
   G.extra = nullptr;
   GridView& g = G.view;
   const double h = b * vs;
@@ -1944,7 +1947,7 @@ extern "C" int o3dx_search_stats(int64_t* out) {
 extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
   n = std::max<int64_t>(n, 1);
   // grid rows (ny * nz) are bounded by the cell cap
-  const int64_t rows = cap_cells(n);
+  const int64_t rows = cap_cells(n, 4);
   return grid_ws_bytes(n) + 3 * Arena::align((n + 3) * 4) + Arena::align((n / 64 + rows + 4) * 4) +
          chunk_plan_ws_bytes(n, rows) + 4096;
 }

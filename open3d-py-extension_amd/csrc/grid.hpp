@@ -283,6 +283,27 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
     });
   };
   visit_cell(cx, cy, cz);
+  if (bi >= 0) {
+    // A match in the own cell bounds the search: every better point lies in
+    // the ball of radius sqrt(thr) (+ the assignment slack), so only the
+    // cells that ball overlaps are visited (the bound only shrinks while they
+    // are scanned), instead of the full shells around the cell.
+    const float rb = sqrtf(thr) + sl3;
+    const int x0 = max(0, (int)floorf((fx - rb - g.ox) * g.inv_h)), x1 = min(g.nx - 1, (int)floorf((fx + rb - g.ox) * g.inv_h));
+    const int y0 = max(0, (int)floorf((fy - rb - g.oy) * g.inv_h)), y1 = min(g.ny - 1, (int)floorf((fy + rb - g.oy) * g.inv_h));
+    const int z0 = max(0, (int)floorf((fz - rb - g.oz) * g.inv_h)), z1 = min(g.nz - 1, (int)floorf((fz + rb - g.oz) * g.inv_h));
+    if ((x1 - x0) <= 2 && (y1 - y0) <= 2 && (z1 - z0) <= 2 && x0 <= cx && cx <= x1 && y0 <= cy && cy <= y1 &&
+        z0 <= cz && cz <= z1) {
+      for (int z = z0; z <= z1; ++z)
+        for (int y = y0; y <= y1; ++y)
+          for (int x = x0; x <= x1; ++x)
+            if (x != cx || y != cy || z != cz) visit_cell(x, y, z);
+      search_stats(g, st_cells, st_cands, 2);
+      *best_d2 = bd;
+      *best_pos = bp;
+      return bi;
+    }
+  }
   for (;; ++r) {
     // every point within B of q has been visited (or pruned by the bound)
     const double B = cube_reach(g, qx, qy, qz, cx, cy, cz, r) - g.slack;
@@ -439,12 +460,14 @@ struct GridBuild {
   GridView view;
 };
 
-size_t grid_ws_bytes(int64_t n);
+size_t grid_ws_bytes(int64_t n, int cap_mult = 4);
 unsigned long long* search_stats_ptr();  // device counters when stats are enabled, else null
 // target_occ: desired mean points per occupied cell.  min_h: lower bound on h
-// (0 = none).  Synchronises the stream (cell size is chosen on the host).
+// (0 = none).  cap_mult: cell capacity per point (the workspace must come
+// from grid_ws_bytes(n, cap_mult)).  Synchronises the stream (cell size is
+// chosen on the host).
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
                hipStream_t s, GridBuild* out, float4* extra_sorted = nullptr, const float* extra_src = nullptr,
-               bool blocked = false);
+               bool blocked = false, int cap_mult = 4);
 
 }  // namespace o3dx

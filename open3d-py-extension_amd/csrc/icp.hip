@@ -332,6 +332,13 @@ static double icp_min_h(double max_corr) {
   if (const char* e = getenv("O3DX_ICP_MINH_DIV")) return max_corr / atof(e);  // tuning override
   return max_corr / 16.0;
 }
+// target grid cell capacity per point: a surface occupies few of the box's
+// cells, so a finer grid than the volume default keeps the candidates per
+// query low (the dense start table costs 8 B per cell)
+static int icp_cap_mult() {
+  if (const char* e = getenv("O3DX_ICP_CAP")) return std::max(1, atoi(e));
+  return 12;
+}
 static double icp_occ() {
   if (const char* e = getenv("O3DX_ICP_OCC")) return atof(e);
   return 2.0;
@@ -341,7 +348,7 @@ static double icp_occ() {
 
 using namespace o3dx;
 
-extern "C" size_t o3dx_icp_target_workspace_bytes(int64_t nt) { return grid_ws_bytes(nt) + 1024; }
+extern "C" size_t o3dx_icp_target_workspace_bytes(int64_t nt) { return grid_ws_bytes(nt, icp_cap_mult()) + 1024; }
 
 extern "C" int o3dx_icp_target_build(const float* tgt, const float* tgt_normals, int64_t nt, double max_corr,
                                      void* target_ws, size_t target_ws_bytes, double* desc, void* stream) {
@@ -351,7 +358,7 @@ extern "C" int o3dx_icp_target_build(const float* tgt, const float* tgt_normals,
     return fail(O3DX_ENOMEM, "icp target workspace too small");
   GridBuild G;
   O3DX_TRY(grid_build(tgt, nt, icp_occ(), icp_min_h(max_corr), target_ws, target_ws_bytes, as_stream(stream), &G, nullptr,
-                      tgt_normals));
+                      tgt_normals, false, icp_cap_mult()));
   desc_pack(G, target_ws, G.extra, desc);
   return 0;
 }
