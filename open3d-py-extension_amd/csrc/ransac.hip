@@ -23,9 +23,9 @@
 
 namespace o3dx {
 
-constexpr int kPts = 8;
+constexpr int kPts = 16;
 constexpr int kHChunk = 1024;
-constexpr int kCountBlocksMax = 1024;
+constexpr int kCountBlocksMax = 4096;
 
 struct P3 {
   float x, y, z;
@@ -45,7 +45,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // evaluated; distances of two points per packed FMA.
 __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict__ xyz, int64_t n,
                                                         const float4* __restrict__ pl32,
-                                                        const float2* __restrict__ band,
+                                                        const float4* __restrict__ band,
                                                         const double* __restrict__ pl64, int H, int h0, int hc,
                                                         double thr, int32_t* __restrict__ partial) {
   static_assert(kPts % 2 == 0, "points are processed in pairs");
@@ -68,25 +68,33 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
       Z[k] = (f32x2){a.z, b.z};
     }
     float4 P = pl32[h0];
-    float2 B = band[h0];
+    float4 B = band[h0];
     for (int h = 0; h < hc; ++h) {
       const int hn = (h + 1 < hc) ? h + 1 : h;
       const float4 Pn = pl32[h0 + hn];
-      const float2 Bn = band[h0 + hn];
+      const float4 Bn = band[h0 + hn];
       int wc = 0;
-      uint64_t ambw = 0ull;  // wave-level: some lane has a point inside the ambiguity band
+      // ambiguity band [B.x, B.y) = mid B.z +- B.w (conservative): each lane
+      // keeps its closest |e - mid| (VALU), one ballot per hypothesis
+      float amb = INFINITY;
+      // all distances first (independent chains), then the tests
+      f32x2 D[kPairs];
 #pragma unroll
-      for (int k = 0; k < kPairs; ++k) {
-        const f32x2 d = __builtin_elementwise_fma(
+      for (int k = 0; k < kPairs; ++k)
+        D[k] = __builtin_elementwise_fma(
             (f32x2){P.x, P.x}, X[k],
             __builtin_elementwise_fma((f32x2){P.y, P.y}, Y[k],
                                       __builtin_elementwise_fma((f32x2){P.z, P.z}, Z[k], (f32x2){P.w, P.w})));
-        const float e0 = fabsf(d.x), e1 = fabsf(d.y);
-        const uint64_t l0 = __ballot(e0 < B.x), l1 = __ballot(e1 < B.x);
-        wc += __popcll(l0) + __popcll(l1);
-        ambw |= (__ballot(e0 < B.y) & ~l0) | (__ballot(e1 < B.y) & ~l1);
-      }
-      if (ambw) {  // rare: re-decide band points in float64, Open3D's order
+      __builtin_amdgcn_sched_barrier(0);
+      float am[kPairs];
+#pragma unroll
+      for (int k = 0; k < kPairs; ++k) am[k] = fminf(fabsf(fabsf(D[k].x) - B.z), fabsf(fabsf(D[k].y) - B.z));
+#pragma unroll
+      for (int k = 0; k < kPairs; ++k)
+        wc += __popcll(__ballot(fabsf(D[k].x) < B.x)) + __popcll(__ballot(fabsf(D[k].y) < B.x));
+#pragma unroll
+      for (int k = 0; k < kPairs; ++k) amb = fminf(amb, am[k]);
+      if (__ballot(amb <= B.w)) {  // rare: re-decide band points in float64, Open3D's order
         const double* pl = pl64 + 4 * (h0 + h);
 #pragma unroll
         for (int k = 0; k < kPairs; ++k) {
@@ -252,7 +260,7 @@ static int count_blocks(int64_t n) {
 
 struct CountWs {
   float4* pl32;
-  float2* band;
+  float4* band;
   double* pl64;
   uint8_t* degen;
   int32_t* partial;
@@ -264,7 +272,7 @@ struct CountWs {
 static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   H = std::max(H, 1);
   w->pl32 = ar.take<float4>(H);
-  w->band = ar.take<float2>(H);
+  w->band = ar.take<float4>(H);
   w->pl64 = ar.take<double>(4 * (size_t)H);
   w->degen = ar.take<uint8_t>(H);
   w->partial = ar.take<int32_t>((size_t)count_blocks(n) * H);
@@ -276,7 +284,7 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
 
 // scale of |a x| + |b y| + |c z| + |d| over the cloud, for the float32 band
 static void upload_planes(const double* planes, int H, const double absmax[3], double thr, CountWs& w,
-                          std::vector<float4>& p32, std::vector<float2>& bnd, std::vector<uint8_t>& dg,
+                          std::vector<float4>& p32, std::vector<float4>& bnd, std::vector<uint8_t>& dg,
                           hipStream_t s, int* rc) {
   p32.resize(H);
   bnd.resize(H);
@@ -293,11 +301,16 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
       lo = -1.0f;  // never an inlier
       hi = -1.0f;
     }
-    bnd[h] = make_float2(lo, hi);
+    // detection window mid +- half, covering [lo, hi) after float32 rounding
+    // of |e - mid| (half widened by 2^-18 relative)
+    const float mid = (float)(0.5 * ((double)lo + (double)hi));
+    float half = (float)(std::max((double)mid - (double)lo, (double)hi - (double)mid) * (1.0 + std::ldexp(1.0, -18)));
+    if (dg[h]) half = -1.0f;
+    bnd[h] = make_float4(lo, hi, mid, half);
   }
   *rc = 0;
   if (hipMemcpyAsync(w.pl32, p32.data(), H * sizeof(float4), hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(w.band, bnd.data(), H * sizeof(float2), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(w.band, bnd.data(), H * sizeof(float4), hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(w.pl64, planes, 4 * H * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(w.degen, dg.data(), H, hipMemcpyHostToDevice, s) != hipSuccess)
     *rc = fail(O3DX_EIO, "plane upload failed");
@@ -316,7 +329,7 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   double absmax[3];
   O3DX_TRY(absmax_of(xyz, n, aabb_ws, mm_dev, s, absmax));
   std::vector<float4> p32;
-  std::vector<float2> bnd;
+  std::vector<float4> bnd;
   std::vector<uint8_t> dg;
   int rc;
   upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, s, &rc);

@@ -32,4 +32,10 @@ if what in ("all", "icp"):
     for _ in range(3):
         sums, _ = target.accumulate(src4, T)
     torch.cuda.synchronize()
+if what in ("all", "ransac"):
+    pts = S.planted_plane(N, 3, device=dev)
+    samples = ops.ransac_samples(N, 3, 1000, seed=7)
+    for _ in range(2):
+        ops.segment_plane(pts, 0.01, 3, 1000, samples=samples)
+    torch.cuda.synchronize()
 print("done")
