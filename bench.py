@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--icp-iters", type=int, default=30)
     ap.add_argument("--ransac-iters", type=int, default=1000)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--c4-n", type=int, default=50_000_000, help="C4 cloud size (0: skip the C4 legs)")
     ap.add_argument("--dist-icp", action="store_true",
                     help="also run the sharded-ICP leg (RCCL) when world == 1 (under torchrun)")
     return ap.parse_args()
@@ -212,6 +213,61 @@ def secondary_sharded_icp(dev, args, world, rank):
                             "collective": "all_gather of 32 float64 per iteration (RCCL), summed in rank order"}}
 
 
+def c4_single_gpu(dev, args):
+    """C4's cloud size on one GPU (north star: voxel_down_sample +
+    estimate_normals at N=50M): the headline step on 50M uniform points."""
+    n = args.c4_n
+    pts = synthetic.uniform_cube(n, seed=0, device=dev)
+    vs = synthetic.voxel_size_for(n)
+
+    def step():
+        out = ops.voxel_down_sample(pts, vs, keep_grid=True)
+        ops.estimate_normals(out["rep_xyz"], knn=args.knn, voxel_grid=out.get("voxel_grid"))
+        return out["rep_idx"].numel()
+
+    step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        m = step()
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / 3
+    algo = 12.0 * n + 28.0 * m
+    del pts
+    torch.cuda.empty_cache()
+    return {"c4_single_gpu": {"n": n, "voxels": int(m), "ms": round(el * 1e3, 3),
+                              "Mpoints_per_s": round(n / el / 1e6, 2),
+                              "pipeline_algorithmic_GBs": round(algo / el / 1e9, 2),
+                              "frac_of_hbm_peak": round(algo / el / 1e9 / HBM_PEAK_GBS, 5),
+                              "algorithmic_bytes": "12 N + 28 M (SURVEY.md 8(d))"}}
+
+
+def c4_slabs(dev, args, world, rank):
+    """C4 across the ranks: ONE 50M cloud (this rank holds an index range of
+    it), voxel-aligned x-slabs, points to their slab owner and a verified halo
+    of representatives to the neighbours (all-to-all over RCCL), voxel reps +
+    KNN normals per slab (open3dpypro.distributed.voxel_normals_slabs)."""
+    from open3dpypro import distributed as D
+
+    n = args.c4_n
+    a, b = D.shard_range(n, world, rank)
+    pts = synthetic.uniform_cube(b - a, seed=0, offset=a, device=dev)
+    gidx = torch.arange(a, b, dtype=torch.int64, device=dev)
+    vs = synthetic.voxel_size_for(n)
+    D.voxel_normals_slabs(pts, gidx, vs, knn=args.knn)  # warm
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    rg, _, _ = D.voxel_normals_slabs(pts, gidx, vs, knn=args.knn)
+    barrier(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    m = torch.tensor([rg.numel()], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(m)
+    return {"c4_slabs": {"n": n, "ranks": world, "voxels": int(m.item()), "ms": round(el * 1e3, 3),
+                         "Mpoints_per_s": round(n / el / 1e6, 2), "scaling": "strong",
+                         "collectives": "all_reduce (AABB, halo check), all_to_all (points to slab owners, halo reps)"}}
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist(args.dist_icp)
@@ -303,6 +359,14 @@ def main():
             line["extra"].update(secondary_sharded_icp(dev, args, world, rank))
         except RuntimeError as e:  # report, never hide
             line["extra"]["secondary_error"] = str(e)
+    if args.c4_n > 0 and not args.no_secondary:
+        try:
+            if world == 1:
+                line["extra"].update(c4_single_gpu(dev, args))
+            else:
+                line["extra"].update(c4_slabs(dev, args, world, rank))
+        except RuntimeError as e:  # report, never hide
+            line["extra"]["c4_error"] = str(e)
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_n)
         if line["cpu_baseline"]["value"] > 0:

@@ -714,6 +714,7 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
   MomAcc acc;
   acc.zero();
   int nsel = 0, nb = 0, nU = 0;
+  const float Ub = U * (1.0f + 2.0f * kRelEps);  // the list's bound; entries past it (a wider list) are skipped
   for (int j = 0; j < n; j += 4) {
     int p[4];
     float4 v[4];
@@ -729,7 +730,7 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
         if (d2f < Lm) {
           ++nsel;
           acc.add((double)v[u].x, (double)v[u].y, (double)v[u].z);
-        } else {
+        } else if (d2f < Ub) {
           lst[min(nb, kBndCap)][lane] = (T)p[u];
           ++nb;
         }
@@ -1075,8 +1076,6 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
 constexpr int kVB = 4;                     // block edge (voxels)
 constexpr int kVM = 3;                     // box margin (the stencil's reach in voxels)
 constexpr int kVE = kVB + 2 * kVM;         // box edge (10)
-constexpr int kSY = kVE, kSZ = kVE * kVE;  // LDS slot strides
-constexpr int kVSlots = kVE * kSZ;         // 1000
 constexpr double kStencilR = 2.45;         // completeness radius (voxels)
 
 // (dy, dz, x0, x1) in the oriented frame (query in [0.49, 1) of its voxel on
@@ -1136,35 +1135,60 @@ __device__ __forceinline__ void stencil_scan(const float* tx, const float* ty, c
 #undef O3DX_ROW
 }
 
-template <int KMAX>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior,
-                                                      float* __restrict__ out, int32_t* __restrict__ fb_list,
-                                                      int32_t* __restrict__ fb_len, int force_fb, int dbg) {
-  __shared__ float tx[kVSlots], ty[kVSlots], tz[kVSlots];
+// Block shapes: WY x WZ waves, each wave a 4^3 voxel block; the block's box is
+// the union (4 x 4WY x 4WZ voxels + the 3-voxel margin), staged once for all
+// its waves — 2x2 waves stage 7.7 slots per query instead of 15.6 and fit
+// 3 blocks (12 waves) per CU in LDS instead of 8 single-wave blocks.
+template <int WY, int WZ>
+struct StileShape {
+  static constexpr int NW = WY * WZ;
+  static constexpr int EY = kVB * WY + 2 * kVM, EZ = kVB * WZ + 2 * kVM;
+  static constexpr int SY = kVE, SZ = kVE * EY, SLOTS = kVE * EY * EZ;
+};
+
+// MERGED: the histogram pass also appends every candidate below T2 = 3/4 R2 to
+// the list (at one rep per voxel the k = 30 band lies below it for all but
+// ~0.1 % of the queries, and <= 52 points do); the list pass then only runs
+// for lanes whose Up exceeds T2 or whose list overflowed.  Saves the second
+// stencil scan (3 LDS reads per candidate); the histogram gets its own LDS.
+constexpr int kMergedCap = 56;
+constexpr float kMergedFrac = 0.75f;
+
+// WPE: waves per SIMD to register-allocate for (LDS allows 2 for 1x1, 3 for 2x2)
+template <int KMAX, int WY, int WZ, int WPE, bool MERGED>
+__global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
+                int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
+  using Sh = StileShape<WY, WZ>;
+  constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::SLOTS;
+  __shared__ float tx[kSlots], ty[kSlots], tz[kSlots];
   constexpr int kListMax = KMAX + kBndCap;
-  constexpr int kListCap = kListMax + 4;
-  constexpr int kListWords = (kListCap * 64 * 2 + 3) / 4;
+  constexpr int kListRows = MERGED && kMergedCap > kListMax ? kMergedCap + 1 : kListMax + 4;
+  constexpr int kListWords = (kListRows * 64 * 2 + 3) / 4;
   constexpr int kHistWords = kTileSlots * 64;
-  __shared__ uint32_t selbuf[kListWords > kHistWords ? kListWords : kHistWords];
-  uint16_t(*lst)[64] = reinterpret_cast<uint16_t(*)[64]>(selbuf);
-  uint32_t* hw = selbuf;
-  const int lane = threadIdx.x;
+  constexpr int kSelWords = MERGED ? kListWords : (kListWords > kHistWords ? kListWords : kHistWords);
+  __shared__ uint32_t selbuf[Sh::NW][kSelWords];
+  __shared__ uint32_t histbuf[MERGED ? Sh::NW : 1][MERGED ? kHistWords : 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint16_t(*lst)[64] = reinterpret_cast<uint16_t(*)[64]>(selbuf[wv]);
+  uint32_t* hw = MERGED ? histbuf[MERGED ? wv : 0] : selbuf[wv];
   const int nb = d.nbx * d.nby * d.nbz;
   const int b = xcd_block(blockIdx.x, nb);
   const int bx = b % d.nbx, by = (b / d.nbx) % d.nby, bz = b / (d.nbx * d.nby);
-  const int gx0 = bx * kVB - kVM, gy0 = by * kVB - kVM, gz0 = bz * kVB - kVM;  // box origin (voxels)
+  const int gx0 = bx * kVB - kVM, gy0 = by * (kVB * WY) - kVM, gz0 = bz * (kVB * WZ) - kVM;  // box origin
   {
-    constexpr int J = (kVSlots + 63) / 64;
+    constexpr int kT = 64 * Sh::NW;
+    constexpr int J = (kSlots + kT - 1) / kT;
     float4 buf[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int t = lane + 64 * j;
-      if (t < kVSlots) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kSY) % kVE, gz0 + t / kSZ);
+      const int t = threadIdx.x + kT * j;
+      if (t < kSlots) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kSY) % Sh::EY, gz0 + t / kSZ);
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int t = lane + 64 * j;
-      if (t < kVSlots) {
+      const int t = threadIdx.x + kT * j;
+      if (t < kSlots) {
         tx[t] = buf[j].x;
         ty[t] = buf[j].y;
         tz[t] = buf[j].z;
@@ -1172,7 +1196,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
   }
   __syncthreads();
-  const int lx = lane & 3, ly = (lane >> 2) & 3, lz = lane >> 4;
+  const int lx = lane & 3, ly = ((lane >> 2) & 3) + kVB * (wv % WY), lz = (lane >> 4) + kVB * (wv / WY);
   const int qs = (lx + kVM) + kSY * (ly + kVM) + kSZ * (lz + kVM);
   const float4 q = make_float4(tx[qs], ty[qs], tz[qs], 0.0f);
   if (!(q.x < INFINITY)) return;  // empty voxel or outside the grid: no query (no barrier follows)
@@ -1191,19 +1215,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
   if (!fb) {
     const float R2 = d.rc2;
+    const float T2 = R2 * kMergedFrac;
+    int nl = 0;  // MERGED: candidates below T2 appended by the first pass
     TileHist th;
-    auto hist = [&](float lo_, float sc_) {
+    auto hist = [&](float lo_, float sc_, auto app) {
 #pragma unroll
       for (int i = 0; i < kTileSlots; ++i) hw[i * 64 + lane] = 0u;
       const float off_ = -lo_ * sc_;
-      stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int, float d2) {
+      stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
         const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f);
         atomicAdd(&hw[(ix + 1) * 64 + lane], 1u);
+        if constexpr (decltype(app)::value) {
+          lst[min(nl, kMergedCap)][lane] = (uint16_t)pp;
+          nl += d2 < T2 ? 1 : 0;
+        }
       });
 #pragma unroll
       for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
     };
-    hist(0.0f, (float)kHistBins / R2);
+    hist(0.0f, (float)kHistBins / R2, std::integral_constant<bool, MERGED>{});
     int total = 0;
 #pragma unroll
     for (int i = 0; i < kHistBins; ++i) total += th.count(i);
@@ -1219,7 +1249,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
       lo = L;
       hi = U;
-      hist(lo, (float)kHistBins / (hi - lo));
+      hist(lo, (float)kHistBins / (hi - lo), std::false_type{});
     }
     if (dbg == 2) {
       if (L == 12345.f) out[0] = 0.f;
@@ -1227,17 +1257,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     if (!fb) {
       const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
-      int n = 0;
-      stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
-        lst[min(n, kListMax)][lane] = (uint16_t)pp;
-        n += d2 < Up ? 1 : 0;
-      });
+      // the merged list holds every candidate below T2 >= Up (the rest of it,
+      // Up <= d2 < T2, is skipped by finish_selection)
+      const bool have = MERGED && Up <= T2 && nl <= kMergedCap;
+      int n = nl, cap = kMergedCap;
+      if (!have) {
+        n = 0;
+        cap = kListMax;
+        stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
+          lst[min(n, kListMax)][lane] = (uint16_t)pp;
+          n += d2 < Up ? 1 : 0;
+        });
+      }
       if (dbg == 3) {
         if (n == 12345) out[0] = 0.f;
         return;
       }
-      if (n > kListMax && d.stats) atomicAdd(&d.stats[5], 1ull);
-      fb = n > kListMax ||
+      if (n > cap && d.stats) atomicAdd(&d.stats[5], 1ull);
+      fb = n > cap ||
            !finish_selection<KMAX>(
                q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); }, prior,
                oi, out, dbg == 4);
@@ -1788,9 +1825,15 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   d.nx = (int)geom[4];
   d.ny = (int)geom[5];
   d.nz = (int)geom[6];
+  // block shape (O3DX_STILE_SHAPE): 3 (default) 2x2 waves sharing one box, allocated
+  // for 3 waves/SIMD (some VGPR spills, still the fastest: 0.78 vs 0.83 ms at 10M);
+  // 2: the same block at 2 waves/SIMD; 1: one wave per 4^3 block
+  const char* shape_env = getenv("O3DX_STILE_SHAPE");
+  const int shape = shape_env ? atoi(shape_env) : 3;
+  const int wyz = shape == 1 ? 1 : 2;
   d.nbx = (d.nx + kVB - 1) / kVB;
-  d.nby = (d.ny + kVB - 1) / kVB;
-  d.nbz = (d.nz + kVB - 1) / kVB;
+  d.nby = (d.ny + kVB * wyz - 1) / (kVB * wyz);
+  d.nbz = (d.nz + kVB * wyz - 1) / (kVB * wyz);
   const int64_t nb = (int64_t)d.nbx * d.nby * d.nbz;
   if (nb <= 0 || nb > INT32_MAX || (int64_t)d.nx * d.ny * d.nz > INT32_MAX) return 1;
   d.ox = (float)geom[0];
@@ -1821,8 +1864,25 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
       KTimer kt_tile("normals_stile", s);
       // O3DX_TILE_DEBUG=1/2/3/4: stop after staging / histogram / list scan / moments (profiling only)
       const char* dbg = getenv("O3DX_TILE_DEBUG");
-      hipLaunchKernelGGL(k_normals_stile<32>, dim3((unsigned)nb), dim3(64), 0, s, d, kneed, prior, out, list, lens,
-                         getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dbg ? atoi(dbg) : 0);
+      const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
+      const char* mg = getenv("O3DX_STILE_MERGED");
+      const bool merged = mg && atoi(mg) != 0;
+#define O3DX_STILE_LAUNCH(WYZ, WPE, MG)                                                                         \
+  hipLaunchKernelGGL((k_normals_stile<32, WYZ, WYZ, WPE, MG>), dim3((unsigned)nb), dim3(64 * WYZ * WYZ), 0, s, d, \
+                     kneed, prior, out, list, lens, ffb, dg)
+      if (merged) {
+        if (wyz == 1)
+          O3DX_STILE_LAUNCH(1, 2, true);
+        else
+          O3DX_STILE_LAUNCH(2, 2, true);
+      } else if (wyz == 1) {
+        O3DX_STILE_LAUNCH(1, 2, false);
+      } else if (shape == 3) {
+        O3DX_STILE_LAUNCH(2, 3, false);
+      } else {
+        O3DX_STILE_LAUNCH(2, 2, false);
+      }
+#undef O3DX_STILE_LAUNCH
     }
     // the table as a dense GridView (identity cell starts, <= 1 point per cell)
     GridView g{};

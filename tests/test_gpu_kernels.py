@@ -369,7 +369,7 @@ def test_voxel_grid_not_kept_when_sparse(dev):
     assert torch.equal(out["rep_idx"], ref["rep_idx"])
 
 
-@pytest.mark.parametrize("env", [None, "O3DX_STILE_FORCE_FB", "O3DX_NO_STILE"])
+@pytest.mark.parametrize("env", [None, "O3DX_STILE_FORCE_FB", "O3DX_NO_STILE", "O3DX_STILE_SHAPE"])
 @pytest.mark.parametrize("k", [5, 30])
 def test_normals_dense_voxel_table(dev, env, k):
     """Volumetric reps fill their voxels: estimate_normals(voxel_grid=) runs
