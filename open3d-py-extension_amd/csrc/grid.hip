@@ -1126,6 +1126,9 @@ __device__ __forceinline__ void scan_run(const float* tx, const float* ty, const
 template <class F>
 __device__ __forceinline__ void stencil_scan(const float* tx, const float* ty, const float* tz, int qs, int SY, int SZ,
                                              bool xpos, const float4 q, F&& f) {
+  // the row bases are recomputed per scan (laundered inputs): hoisted and
+  // shared across the kernel's scans they would stay live throughout
+  asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
   // a scheduling fence per row keeps the unrolled stencil from hoisting every
   // row's loads (register pressure; the other waves hide the LDS latency)
 #define O3DX_ROW(DY, DZ, XA, XB)                                                                   \
