@@ -1268,8 +1268,10 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
         n = 0;
         cap = kListMax;
         stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
-          lst[min(n, kListMax)][lane] = (uint16_t)pp;
-          n += d2 < Up ? 1 : 0;
+          if (d2 < Up) {  // masked store: only the accepted lanes take part in the LDS banking
+            lst[min(n, kListMax)][lane] = (uint16_t)pp;
+            ++n;
+          }
         });
       }
       if (dbg == 3) {
