@@ -1108,31 +1108,35 @@ __device__ __forceinline__ float4 dvox_load(const DenseVox& d, int x, int y, int
 }
 
 // f(slot, d2) over L consecutive slots from st: pairs in packed f32, one single.
+// x, y interleaved (one ds_read2_b64 per pair), z apart: two LDS reads per
+// pair instead of three, the same 12 bytes per slot.
 template <int L, class F>
-__device__ __forceinline__ void scan_run(const float* tx, const float* ty, const float* tz, int st, const float4 q,
-                                         F&& f) {
+__device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int st, const float4 q, F&& f) {
 #pragma unroll
   for (int i = 0; i + 1 < L; i += 2) {
-    const f32x2 dd = dist2_pair(q, (f32x2){tx[st + i], tx[st + i + 1]}, (f32x2){ty[st + i], ty[st + i + 1]},
-                                (f32x2){tz[st + i], tz[st + i + 1]});
+    const float2 a = txy[st + i], b = txy[st + i + 1];
+    const f32x2 dd = dist2_pair(q, (f32x2){a.x, b.x}, (f32x2){a.y, b.y}, (f32x2){tz[st + i], tz[st + i + 1]});
     f(st + i, dd.x);
     f(st + i + 1, dd.y);
   }
-  if (L & 1) f(st + L - 1, dist2_f32(q, tx[st + L - 1], ty[st + L - 1], tz[st + L - 1]));
+  if (L & 1) {
+    const float2 a = txy[st + L - 1];
+    f(st + L - 1, dist2_f32(q, a.x, a.y, tz[st + L - 1]));
+  }
 }
 
 // The lane's stencil: qs = its own slot, SY / SZ = the y / z slot strides
 // signed by the orientation, xpos = x orientation.
 template <class F>
-__device__ __forceinline__ void stencil_scan(const float* tx, const float* ty, const float* tz, int qs, int SY, int SZ,
-                                             bool xpos, const float4 q, F&& f) {
+__device__ __forceinline__ void stencil_scan(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
+                                             const float4 q, F&& f) {
   // the row bases are recomputed per scan (laundered inputs): hoisted and
   // shared across the kernel's scans they would stay live throughout
   asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
   // a scheduling fence per row keeps the unrolled stencil from hoisting every
   // row's loads (register pressure; the other waves hide the LDS latency)
 #define O3DX_ROW(DY, DZ, XA, XB)                                                                   \
-  scan_run<(XB) - (XA) + 1>(tx, ty, tz, qs + (DY) * SY + (DZ) * SZ + (xpos ? (XA) : -(XB)), q, f); \
+  scan_run<(XB) - (XA) + 1>(txy, tz, qs + (DY) * SY + (DZ) * SZ + (xpos ? (XA) : -(XB)), q, f); \
   __builtin_amdgcn_sched_barrier(0);
   O3DX_S25_ROWS(O3DX_ROW)
 #undef O3DX_ROW
@@ -1164,7 +1168,8 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
                 int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
   using Sh = StileShape<WY, WZ>;
   constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::SLOTS;
-  __shared__ float tx[kSlots], ty[kSlots], tz[kSlots];
+  __shared__ float2 txy[kSlots];
+  __shared__ float tz[kSlots];
   constexpr int kListMax = KMAX + kBndCap;
   constexpr int kListRows = MERGED && kMergedCap > kListMax ? kMergedCap + 1 : kListMax + 4;
   constexpr int kListWords = (kListRows * 64 * 2 + 3) / 4;
@@ -1192,8 +1197,7 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
     for (int j = 0; j < J; ++j) {
       const int t = threadIdx.x + kT * j;
       if (t < kSlots) {
-        tx[t] = buf[j].x;
-        ty[t] = buf[j].y;
+        txy[t] = make_float2(buf[j].x, buf[j].y);
         tz[t] = buf[j].z;
       }
     }
@@ -1201,7 +1205,7 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   __syncthreads();
   const int lx = lane & 3, ly = ((lane >> 2) & 3) + kVB * (wv % WY), lz = (lane >> 4) + kVB * (wv / WY);
   const int qs = (lx + kVM) + kSY * (ly + kVM) + kSZ * (lz + kVM);
-  const float4 q = make_float4(tx[qs], ty[qs], tz[qs], 0.0f);
+  const float4 q = make_float4(txy[qs].x, txy[qs].y, tz[qs], 0.0f);
   if (!(q.x < INFINITY)) return;  // empty voxel or outside the grid: no query (no barrier follows)
   const int vx = gx0 + kVM + lx, vy = gy0 + kVM + ly, vz = gz0 + kVM + lz;
   const int64_t vq = vx + (int64_t)d.nx * (vy + (int64_t)d.ny * vz);
@@ -1225,7 +1229,7 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
 #pragma unroll
       for (int i = 0; i < kTileSlots; ++i) hw[i * 64 + lane] = 0u;
       const float off_ = -lo_ * sc_;
-      stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
+      stencil_scan(txy, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
         const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f);
         atomicAdd(&hw[(ix + 1) * 64 + lane], 1u);
         if constexpr (decltype(app)::value) {
@@ -1267,7 +1271,7 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
       if (!have) {
         n = 0;
         cap = kListMax;
-        stencil_scan(tx, ty, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
+        stencil_scan(txy, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
           if (d2 < Up) {  // masked store: only the accepted lanes take part in the LDS banking
             lst[min(n, kListMax)][lane] = (uint16_t)pp;
             ++n;
@@ -1281,7 +1285,7 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
       if (n > cap && d.stats) atomicAdd(&d.stats[5], 1ull);
       fb = n > cap ||
            !finish_selection<KMAX>(
-               q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); }, prior,
+               q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(txy[p].x, txy[p].y, tz[p], 0.f); }, prior,
                oi, out, dbg == 4);
     }
   }
