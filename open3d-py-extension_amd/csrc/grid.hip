@@ -1110,19 +1110,24 @@ __device__ __forceinline__ float4 dvox_load(const DenseVox& d, int x, int y, int
 // f(slot, d2) over L consecutive slots from st: pairs in packed f32, one single.
 // x, y interleaved (one ds_read2_b64 per pair), z apart: two LDS reads per
 // pair instead of three, the same 12 bytes per slot.
+// The row's loads are all issued before its first f (whose LDS atomics /
+// stores the compiler cannot move reads across).
 template <int L, class F>
 __device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int st, const float4 q, F&& f) {
+  float2 a[L];
+  float c[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    a[i] = txy[st + i];
+    c[i] = tz[st + i];
+  }
 #pragma unroll
   for (int i = 0; i + 1 < L; i += 2) {
-    const float2 a = txy[st + i], b = txy[st + i + 1];
-    const f32x2 dd = dist2_pair(q, (f32x2){a.x, b.x}, (f32x2){a.y, b.y}, (f32x2){tz[st + i], tz[st + i + 1]});
+    const f32x2 dd = dist2_pair(q, (f32x2){a[i].x, a[i + 1].x}, (f32x2){a[i].y, a[i + 1].y}, (f32x2){c[i], c[i + 1]});
     f(st + i, dd.x);
     f(st + i + 1, dd.y);
   }
-  if (L & 1) {
-    const float2 a = txy[st + L - 1];
-    f(st + L - 1, dist2_f32(q, a.x, a.y, tz[st + L - 1]));
-  }
+  if (L & 1) f(st + L - 1, dist2_f32(q, a[L - 1].x, a[L - 1].y, c[L - 1]));
 }
 
 // The lane's stencil: qs = its own slot, SY / SZ = the y / z slot strides
