@@ -1840,14 +1840,14 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   d.ny = (int)geom[5];
   d.nz = (int)geom[6];
   // block shape (O3DX_STILE_SHAPE): 3 (default) 2x2 waves sharing one box, allocated
-  // for 3 waves/SIMD (some VGPR spills, still the fastest: 0.78 vs 0.83 ms at 10M);
-  // 2: the same block at 2 waves/SIMD; 1: one wave per 4^3 block
+  // for 3 waves/SIMD; 2: the same block at 2 waves/SIMD; 1: one wave per 4^3
+  // block; 4: 2x3 waves (a larger shared box, 2 workgroups = 12 waves per CU)
   const char* shape_env = getenv("O3DX_STILE_SHAPE");
   const int shape = shape_env ? atoi(shape_env) : 3;
-  const int wyz = shape == 1 ? 1 : 2;
+  const int wy = shape == 1 ? 1 : 2, wz = shape == 1 ? 1 : shape == 4 ? 3 : 2;
   d.nbx = (d.nx + kVB - 1) / kVB;
-  d.nby = (d.ny + kVB * wyz - 1) / (kVB * wyz);
-  d.nbz = (d.nz + kVB * wyz - 1) / (kVB * wyz);
+  d.nby = (d.ny + kVB * wy - 1) / (kVB * wy);
+  d.nbz = (d.nz + kVB * wz - 1) / (kVB * wz);
   const int64_t nb = (int64_t)d.nbx * d.nby * d.nbz;
   if (nb <= 0 || nb > INT32_MAX || (int64_t)d.nx * d.ny * d.nz > INT32_MAX) return 1;
   d.ox = (float)geom[0];
@@ -1881,22 +1881,26 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
       const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
       const char* mg = getenv("O3DX_STILE_MERGED");
       const bool merged = mg && atoi(mg) != 0;
-#define O3DX_STILE_LAUNCH(WYZ, WPE, MG)                                                                         \
-  hipLaunchKernelGGL((k_normals_stile<32, WYZ, WYZ, WPE, MG>), dim3((unsigned)nb), dim3(64 * WYZ * WYZ), 0, s, d, \
+#define O3DX_STILE_LAUNCH2(WY, WZ, WPE, MG)                                                                  \
+  hipLaunchKernelGGL((k_normals_stile<32, WY, WZ, WPE, MG>), dim3((unsigned)nb), dim3(64 * WY * WZ), 0, s, d, \
                      kneed, prior, out, list, lens, ffb, dg)
+#define O3DX_STILE_LAUNCH(WYZ, WPE, MG) O3DX_STILE_LAUNCH2(WYZ, WYZ, WPE, MG)
       if (merged) {
-        if (wyz == 1)
+        if (wy == 1)
           O3DX_STILE_LAUNCH(1, 2, true);
         else
           O3DX_STILE_LAUNCH(2, 2, true);
-      } else if (wyz == 1) {
+      } else if (wy == 1) {
         O3DX_STILE_LAUNCH(1, 2, false);
+      } else if (shape == 4) {
+        O3DX_STILE_LAUNCH2(2, 3, 3, false);
       } else if (shape == 3) {
         O3DX_STILE_LAUNCH(2, 3, false);
       } else {
         O3DX_STILE_LAUNCH(2, 2, false);
       }
 #undef O3DX_STILE_LAUNCH
+#undef O3DX_STILE_LAUNCH2
     }
     // the table as a dense GridView (identity cell starts, <= 1 point per cell)
     GridView g{};
