@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define O3DX_ABI_VERSION 1
+#define O3DX_ABI_VERSION 2
 
 #define O3DX_OK 0
 #define O3DX_EIO (-5)
@@ -86,6 +86,25 @@ int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches);
  * library ever makes; off by default. */
 int o3dx_set_search_stats(int enable);
 int o3dx_search_stats(int64_t* out8_host);
+
+/* Test hooks (parity evidence; no reference counterpart).
+ *
+ * o3dx_set_debug_neighbors: while buf_dev is non-null, every KNN-normals
+ * kernel (voxel-table blocks, LDS tiles, wave form, register top-k) writes the
+ * k neighbour ids it selected for output row r into buf_dev[r*k .. r*k+k) (in
+ * the order it summed them; ids = the caller's point rows).  Only calls whose
+ * k equals `k` and whose rows are < `rows` write.  NULL turns it off.  The
+ * buffer is caller-owned; the library keeps the pointer until it is reset.
+ *
+ * o3dx_fast_eigen3x3: the device FastEigen3x3 (the normals kernels' solver)
+ * on m covariances {xx,xy,xz,yy,yz,zz} (f64, dev) -> smallest-eigenvalue
+ * eigenvectors (m,3) f64 (dev).  Asynchronous.
+ *
+ * o3dx_libm_probe: the device double-precision function the normals use
+ * (fn 0 = acos, 1 = cos, 2 = sqrt) on n values (dev) -> out (dev). */
+int o3dx_set_debug_neighbors(int32_t* buf_dev, int64_t rows, int k);
+int o3dx_fast_eigen3x3(const double* cov_dev, int64_t m, double* out_dev, void* stream);
+int o3dx_libm_probe(const double* x_dev, int64_t n, int fn, double* out_dev, void* stream);
 
 /* ---------------------------------------------------------------- AABB
  * Replaces o3d.geometry.PointCloud.get_min_bound()/get_max_bound()
@@ -161,26 +180,32 @@ int o3dx_voxel_down_sample_grid(const float* xyz_dev, int64_t n,
  * covariance (identity if < 3 neighbours), FastEigen3x3 smallest eigenvector,
  * (0,0,1) if it is zero; if prior_normals_dev is given the result is flipped
  * to agree with it (Open3D's has_normal branch).
- * normals_out_dev: (n,3) float32.  KNN/HYBRID require k <= O3DX_MAX_KNN. */
+ * normals_out_dev: (n,3) float32.  KNN/HYBRID require k <= O3DX_MAX_KNN.
+ * kth_d2_dev (nullable, KNN only): (n,) float32, per point an upper bound of
+ * the squared distance of its k-th neighbour (>= the exact float64 value, to
+ * a few float32 ulps) — what a spatially sharded caller needs to prove a halo
+ * wide enough (open3dpypro.distributed.voxel_normals_slabs). */
 size_t o3dx_normals_workspace_bytes(int64_t n);
 int o3dx_estimate_normals(const float* xyz_dev, int64_t n, int mode, int knn,
                           double radius, const float* prior_normals_dev,
-                          float* normals_out_dev, void* ws, size_t ws_bytes,
-                          void* stream);
+                          float* normals_out_dev, float* kth_d2_dev, void* ws,
+                          size_t ws_bytes, void* stream);
 
 /* estimate_normals of the m representatives of o3dx_voxel_down_sample_grid
  * (rep_xyz_dev, voxel_pts_dev, geom_host from that call): the search grid is
  * read off the voxel table (cells of b^3 voxels, b in 1..4 chosen from the
- * occupied 2^3-cell count) instead of being rebuilt by sorting; same results as
- * o3dx_estimate_normals(rep_xyz_dev, m, ...) up to float64 summation order.
+ * occupied 2^3-cell count) — or, for volumetric clouds, the table itself is
+ * the search structure (4^3-voxel blocks staged in LDS) — instead of being
+ * rebuilt by sorting; same neighbour sets and results as
+ * o3dx_estimate_normals(rep_xyz_dev, m, ...).
  * Workspace: o3dx_normals_workspace_bytes(m).  No host synchronisation. */
 int o3dx_estimate_normals_voxel(const double* geom_host,
                                 const float* voxel_pts_dev,
                                 const float* rep_xyz_dev, int64_t m, int mode,
                                 int knn, double radius,
                                 const float* prior_normals_dev,
-                                float* normals_out_dev, void* ws,
-                                size_t ws_bytes, void* stream);
+                                float* normals_out_dev, float* kth_d2_dev,
+                                void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- kNN search
  * Batched form of KDTreeFlann.search_knn_vector_3d / search_hybrid_vector_3d

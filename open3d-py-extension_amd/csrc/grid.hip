@@ -144,6 +144,14 @@ static unsigned long long* g_stats = nullptr;
 static bool g_stats_on = false;
 unsigned long long* search_stats_ptr() { return g_stats_on ? g_stats : nullptr; }
 
+// Test hook (o3dx_set_debug_neighbors): caller-owned (rows, k) buffer.
+static int32_t* g_dbg_nbr = nullptr;
+static int64_t g_dbg_rows = 0;
+static int g_dbg_k = 0;
+static int32_t* debug_nbr(int kneed, int64_t rows) {
+  return (g_dbg_nbr && kneed == g_dbg_k && rows <= g_dbg_rows) ? g_dbg_nbr : nullptr;
+}
+
 static void dims_for(const double mn[3], const double mx[3], double h, int64_t d[3]) {
   for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor(std::max(0.0, mx[a] - mn[a]) / h) + 1;
 }
@@ -606,6 +614,8 @@ __device__ __forceinline__ void knn_normal_query(const GridView& g, const float*
   for (int j = 0; j < K; ++j)
     if (j < cnt) {
       const int id = bi[j];
+      if (g.nbr && j < kneed) g.nbr[(int64_t)oi * kneed + j] = id;
+      if (g.kd2 && j == cnt - 1) g.kd2[oi] = (float)(bd[j] * (1.0 + 1e-6));
       acc.add((double)xyz[3 * id], (double)xyz[3 * id + 1], (double)xyz[3 * id + 2]);
     }
   finish_normal(cnt, acc, prior, oi, out);
@@ -707,13 +717,16 @@ __device__ __forceinline__ bool hist_locate(const H& hist, int kneed, int below,
 // A band that overflows or a separation within rounding (ties included)
 // hands the query on (false) to the exact wave form.  Writes the normal of
 // original point `oi`.
-template <int KMAX, class T, class Fetch>
+template <int KMAX, class T, class Fetch, class Ident>
 __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int n, float Lm, float U, T (*lst)[64],
                                                  int lane, Fetch&& fetch, const float* __restrict__ prior, int oi,
-                                                 float* __restrict__ out, bool skip_eigen = false) {
+                                                 float* __restrict__ out, int32_t* __restrict__ nbr, Ident&& ident,
+                                                 float* __restrict__ kd2, bool skip_eigen = false) {
   MomAcc acc;
   acc.zero();
   int nsel = 0, nb = 0, nU = 0;
+  float cmax = 0.0f;  // largest certain key
+  int32_t* const nrow = nbr ? nbr + (int64_t)oi * kneed : nullptr;  // test hook
   const float Ub = U * (1.0f + 2.0f * kRelEps);  // the list's bound; entries past it (a wider list) are skipped
   for (int j = 0; j < n; j += 4) {
     int p[4];
@@ -728,6 +741,8 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
         const float d2f = dist2_f32(q, v[u].x, v[u].y, v[u].z);  // the scan's value, bit for bit
         nU += d2f < U ? 1 : 0;
         if (d2f < Lm) {
+          if (nrow && nsel < kneed) nrow[nsel] = ident(p[u]);
+          cmax = fmaxf(cmax, d2f);
           ++nsel;
           acc.add((double)v[u].x, (double)v[u].y, (double)v[u].z);
         } else if (d2f < Ub) {
@@ -767,11 +782,13 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
     kmax = best;
   }
   float umin = INFINITY;
+  int nput = nsel;
 #pragma unroll
   for (int i = 0; i < kBndCap; ++i) {
     if (i < nb) {
       if ((picked >> i) & 1u) {
         const float4 v = fetch(bs[i]);
+        if (nrow) nrow[nput++] = ident(bs[i]);
         acc.add((double)v.x, (double)v.y, (double)v.z);
       } else {
         umin = fminf(umin, bk[i]);
@@ -783,6 +800,7 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
     if (need > 0 && !(kmax < umin * sep)) return false;
     if (nsel > 0 && !(Lm < umin * sep)) return false;
   }
+  if (kd2) kd2[oi] = fmaxf(cmax, need > 0 ? kmax : 0.0f) * (1.0f + 4.0f * kRelEps);
   if (skip_eigen) {  // profiling only (O3DX_TILE_DEBUG=4)
     out[3 * oi] = (float)(acc.m[3] + acc.m[5] + acc.m[8]);
     return true;
@@ -1035,7 +1053,8 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
           fb = n > kListMax ||
                !finish_selection<KMAX>(
                    q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
-                   prior, __float_as_int(q.w), out, dbg == 4);
+                   prior, __float_as_int(q.w), out, g.nbr,
+                   [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, g.kd2, dbg == 4);
         }
       }
     }
@@ -1096,6 +1115,8 @@ struct DenseVox {
   float ox, oy, oz, vs, inv_vs;
   float rc2;                       // completeness radius^2 (world, float32, shrunk by the slack)
   unsigned long long* stats;       // debug counters (o3dx_search_stats) or null
+  int32_t* nbr;                    // test hook (o3dx_set_debug_neighbors) or null
+  float* kd2;                      // per row an upper bound of the k-th neighbour d^2, or null
 };
 
 __device__ __forceinline__ float4 dvox_load(const DenseVox& d, int x, int y, int z) {
@@ -1291,7 +1312,13 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
       fb = n > cap ||
            !finish_selection<KMAX>(
                q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(txy[p].x, txy[p].y, tz[p], 0.f); }, prior,
-               oi, out, dbg == 4);
+               oi, out, d.nbr,
+               [&](int p) {
+                 const int bx = p % kVE, by = (p / kSY) % Sh::EY, bz = p / kSZ;
+                 return __float_as_int(
+                     d.vox[(gx0 + bx) + (int64_t)d.nx * ((gy0 + by) + (int64_t)d.ny * (gz0 + bz))].w);
+               },
+               d.kd2, dbg == 4);
     }
   }
   if (fb) {
@@ -1572,6 +1599,13 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
         x = v.x;
         y = v.y;
         z = v.z;
+        if (g.nbr) g.nbr[(int64_t)__float_as_int(q.w) * kneed + lane] = __float_as_int(v.w);
+      }
+      if (g.kd2) {
+        double dk = lane < kneed ? dist2_f64(q.x, q.y, q.z, g.pts[sel[lane]]) : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) dk = fmax(dk, __shfl_xor(dk, o, 64));
+        if (lane == 0) g.kd2[__float_as_int(q.w)] = (float)(dk * (1.0 + 1e-6));
       }
       MomAcc acc;
       acc.m[0] = wave_sum(x);
@@ -1825,7 +1859,7 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
 // to the wave form and the register top-k over the table).  1: not applicable
 // (the caller builds a search grid instead).
 static int normals_dense_vox(const double* geom, const float4* vox, const float* xyz, int64_t n, int mode, int knn,
-                             const float* prior, float* out, void* ws, size_t ws_bytes, hipStream_t s) {
+                             const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes, hipStream_t s) {
   if (!vox || geom[7] != 1.0 || mode != O3DX_SEARCH_KNN || getenv("O3DX_NO_STILE")) return 1;
   const int kneed = (int)std::min<int64_t>(knn, n);
   if (kneed < 1 || kneed > 32 || !(geom[8] > 0.0)) return 1;
@@ -1866,6 +1900,8 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   const double R = kStencilR * geom[3] - slack;
   d.rc2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
   d.stats = search_stats_ptr();
+  d.nbr = debug_nbr(kneed, n);
+  d.kd2 = kd2;
   Arena ar((char*)ws, ws_bytes);
   int32_t* lens = ar.take<int32_t>(4);
   int32_t* list = ar.take<int32_t>(n);
@@ -1885,9 +1921,12 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   hipLaunchKernelGGL((k_normals_stile<32, WY, WZ, WPE, MG>), dim3((unsigned)nb), dim3(64 * WY * WZ), 0, s, d, \
                      kneed, prior, out, list, lens, ffb, dg)
 #define O3DX_STILE_LAUNCH(WYZ, WPE, MG) O3DX_STILE_LAUNCH2(WYZ, WYZ, WPE, MG)
+      // the launched variant must match the block grid (wy x wz waves) sized above
       if (merged) {
         if (wy == 1)
           O3DX_STILE_LAUNCH(1, 2, true);
+        else if (wz == 3)
+          O3DX_STILE_LAUNCH2(2, 3, 2, true);
         else
           O3DX_STILE_LAUNCH(2, 2, true);
       } else if (wy == 1) {
@@ -1918,6 +1957,8 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
     g.nz = d.nz;
     g.n = (int64_t)d.nx * d.ny * d.nz;
     g.stats = d.stats;
+    g.nbr = d.nbr;
+    g.kd2 = d.kd2;
     KTimer kt_wave("normals_wave", s);
     hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(2048), dim3(64 * kWavesPerBlock), 0, s, g, kneed, prior, out,
                        list, lens, list2, lens + 1, 3);
@@ -1933,9 +1974,11 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
 // from the points) and o3dx_estimate_normals_voxel (grid read off the voxel
 // table).  `xyz` is the caller's point array the grid's w fields index.
 static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, int knn, double radius,
-                           const float* prior, float* out, void* ws, size_t ws_bytes, hipStream_t s) {
+                           const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes, hipStream_t s) {
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
   const int kneed = (int)std::min<int64_t>(knn, n);
+  G.view.nbr = mode == O3DX_SEARCH_KNN ? debug_nbr(kneed, n) : nullptr;
+  G.view.kd2 = mode == O3DX_SEARCH_KNN ? kd2 : nullptr;
   if (mode == O3DX_SEARCH_KNN && kneed >= 1 && !getenv("O3DX_NORMALS_TOPK")) {
     // LDS tiles (lane per query) -> wave per query -> exact register top-k,
     // each level serving the queries the previous one could not settle
@@ -2022,6 +2065,50 @@ extern "C" int o3dx_search_stats(int64_t* out) {
   return 0;
 }
 
+extern "C" int o3dx_set_debug_neighbors(int32_t* buf, int64_t rows, int k) {
+  if (buf && (rows < 0 || k < 1 || k > O3DX_MAX_KNN)) return fail(O3DX_EINVAL, "o3dx_set_debug_neighbors: bad k/rows");
+  g_dbg_nbr = buf;
+  g_dbg_rows = buf ? rows : 0;
+  g_dbg_k = buf ? k : 0;
+  return 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_fast_eigen(const double* __restrict__ cov, int64_t m,
+                                                       double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  double c[6], v[3];
+  for (int j = 0; j < 6; ++j) c[j] = cov[6 * i + j];
+  fast_eigen3x3(c, v);
+  for (int j = 0; j < 3; ++j) out[3 * i + j] = v[j];
+}
+
+__global__ void __launch_bounds__(kBlock) k_libm_probe(const double* __restrict__ x, int64_t n, int fn,
+                                                       double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double v = x[i];
+  out[i] = fn == 0 ? acos(v) : fn == 1 ? cos(v) : sqrt(v);
+}
+
+extern "C" int o3dx_fast_eigen3x3(const double* cov, int64_t m, double* out, void* stream) {
+  if (m < 0 || (m > 0 && (!cov || !out))) return fail(O3DX_EINVAL, "o3dx_fast_eigen3x3: bad arguments");
+  if (m == 0) return 0;
+  hipLaunchKernelGGL(k_fast_eigen, dim3((unsigned)((m + kBlock - 1) / kBlock)), dim3(kBlock), 0, as_stream(stream),
+                     cov, m, out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int o3dx_libm_probe(const double* x, int64_t n, int fn, double* out, void* stream) {
+  if (n < 0 || fn < 0 || fn > 2 || (n > 0 && (!x || !out))) return fail(O3DX_EINVAL, "o3dx_libm_probe: bad arguments");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_libm_probe, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, as_stream(stream), x,
+                     n, fn, out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
 extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
   n = std::max<int64_t>(n, 1);
   // grid rows (ny * nz) are bounded by the cell cap
@@ -2031,7 +2118,8 @@ extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
 }
 
 extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,
-                                     const float* prior, float* out, void* ws, size_t ws_bytes, void* stream) {
+                                     const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes,
+                                     void* stream) {
   if (n < 0 || (n > 0 && (!xyz || !out))) return fail(O3DX_EINVAL, "o3dx_estimate_normals: bad arguments");
   if (mode != O3DX_SEARCH_KNN && mode != O3DX_SEARCH_RADIUS && mode != O3DX_SEARCH_HYBRID)
     return fail(O3DX_EINVAL, "o3dx_estimate_normals: unknown search mode %d", mode);
@@ -2043,12 +2131,12 @@ extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int 
   hipStream_t s = as_stream(stream);
   GridBuild G;
   O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), 0.0, ws, ws_bytes, s, &G));
-  return normals_on_grid(G, xyz, n, mode, knn, radius, prior, out, ws, ws_bytes, s);
+  return normals_on_grid(G, xyz, n, mode, knn, radius, prior, out, kd2, ws, ws_bytes, s);
 }
 
 extern "C" int o3dx_estimate_normals_voxel(const double* geom, const float* voxel_pts, const float* xyz, int64_t n,
                                            int mode, int knn, double radius, const float* prior, float* out,
-                                           void* ws, size_t ws_bytes, void* stream) {
+                                           float* kd2, void* ws, size_t ws_bytes, void* stream) {
   if (n < 0 || (n > 0 && (!xyz || !out || !geom))) return fail(O3DX_EINVAL, "o3dx_estimate_normals_voxel: bad arguments");
   if (mode != O3DX_SEARCH_KNN && mode != O3DX_SEARCH_RADIUS && mode != O3DX_SEARCH_HYBRID)
     return fail(O3DX_EINVAL, "o3dx_estimate_normals_voxel: unknown search mode %d", mode);
@@ -2058,15 +2146,15 @@ extern "C" int o3dx_estimate_normals_voxel(const double* geom, const float* voxe
   if (!ws || ws_bytes < o3dx_normals_workspace_bytes(n)) return fail(O3DX_ENOMEM, "normals workspace too small");
   if (n == 0) return 0;
   hipStream_t s = as_stream(stream);
-  const int rd = normals_dense_vox(geom, reinterpret_cast<const float4*>(voxel_pts), xyz, n, mode, knn, prior, out, ws,
-                                   ws_bytes, s);
+  const int rd = normals_dense_vox(geom, reinterpret_cast<const float4*>(voxel_pts), xyz, n, mode, knn, prior, out,
+                                   kd2, ws, ws_bytes, s);
   if (rd != 1) return rd;
   GridBuild G;
   const int rc = grid_from_voxels(geom, reinterpret_cast<const float4*>(voxel_pts), n, occ_for(mode, knn), ws, ws_bytes,
                                   s, &G);
   if (rc == 1) O3DX_TRY(grid_build(xyz, n, occ_for(mode, knn), 0.0, ws, ws_bytes, s, &G));  // no usable voxel grid
   else if (rc != 0) return rc;
-  return normals_on_grid(G, xyz, n, mode, knn, radius, prior, out, ws, ws_bytes, s);
+  return normals_on_grid(G, xyz, n, mode, knn, radius, prior, out, kd2, ws, ws_bytes, s);
 }
 
 extern "C" size_t o3dx_knn_workspace_bytes(int64_t n) { return grid_ws_bytes(n) + 1024; }

@@ -28,6 +28,8 @@ struct GridView {
   int bnx, bny;               // blocked order: number of blocks along x, y
   int dense = 0;              // 1: pts is a dense voxel table (<= 1 point per cell, empty = NaN
                               // coordinates, w = -1) and start is the identity (start may be null)
+  int32_t* nbr = nullptr;     // test hook (o3dx_set_debug_neighbors): k selected ids per output row
+  float* kd2 = nullptr;       // KNN normals: per output row an upper bound of the k-th neighbour d^2
 };
 
 // First sorted position of cell c (dense tables: the cell itself).

@@ -39,6 +39,9 @@ _SIGS = {
     "o3dx_kernel_timing": (_I32, [ctypes.c_char_p, _P, _P]),
     "o3dx_set_search_stats": (_I32, [_I32]),
     "o3dx_search_stats": (_I32, [_P]),
+    "o3dx_set_debug_neighbors": (_I32, [_P, _I64, _I32]),
+    "o3dx_fast_eigen3x3": (_I32, [_P, _I64, _P, _P]),
+    "o3dx_libm_probe": (_I32, [_P, _I64, _I32, _P, _P]),
     "o3dx_aabb_workspace_bytes": (_SZ, [_I64]),
     "o3dx_aabb": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
     "o3dx_voxel_workspace_bytes": (_SZ, [_I64]),
@@ -47,8 +50,8 @@ _SIGS = {
     "o3dx_voxel_grid_capacity": (_I64, [_I64]),
     "o3dx_voxel_down_sample_grid": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P]),
     "o3dx_normals_workspace_bytes": (_SZ, [_I64]),
-    "o3dx_estimate_normals_voxel": (_I32, [_P, _P, _P, _I64, _I32, _I32, _D, _P, _P, _P, _SZ, _P]),
-    "o3dx_estimate_normals": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _SZ, _P]),
+    "o3dx_estimate_normals_voxel": (_I32, [_P, _P, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_estimate_normals": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_knn_workspace_bytes": (_SZ, [_I64]),
     "o3dx_knn_search": (_I32, [_P, _I64, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_ransac_samples": (_I32, [_I64, _I32, _I32, ctypes.c_uint64, _P]),

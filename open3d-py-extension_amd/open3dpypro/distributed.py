@@ -155,7 +155,7 @@ def _exchange(dest: torch.Tensor, world: int, group, *tensors):
 
 
 def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float, knn: int = 30, group=None,
-                        voxel_fn=None, normals_fn=None, kdist_fn=None, halo: Optional[float] = None):
+                        voxel_fn=None, normals_fn=None, halo: Optional[float] = None):
     """C4: voxel_down_sample + estimate_normals(KNN) of one cloud spread over
     the ranks, decomposed into x-slabs aligned to the global voxel grid.
 
@@ -165,12 +165,19 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
     bounds, rows kept in global-index order so the max-index rep and every
     index tie-break equal the single-GPU ones; reps within `halo` of a slab
     face to the neighbour rank (all-to-all: the one exchange of this path);
-    normals on own + halo reps.  The halo is verified (every own rep's k-th
-    neighbour distance minus its distance to the face stays below the halo)
-    and doubled until it holds.  Returns (rep global indices ascending, rep
-    xyz, normals) of this rank's slab; the union over ranks is the single-GPU
-    result.  Compute defaults to the HIP kernels (ops); tests inject the
-    oracle."""
+    normals on own + halo reps.
+
+    Halo proof, for EVERY own rep (not only those near a face): a rep p at
+    distance t from its nearest interior slab face misses only points farther
+    than t + H (they lie more than H beyond that face, or beyond a farther
+    one), so its k nearest within own + halo are its true k nearest when its
+    k-th-neighbour distance in the union is below t + H.  The normals kernels
+    return an upper bound of that distance per row (o3dx estimate_normals
+    kth_d2), so the check costs no extra search; when any rep on any rank
+    fails it, H doubles and the exchange + normals repeat.  Returns (rep
+    global indices ascending, rep xyz, normals) of this rank's slab; the union
+    over ranks is the single-GPU result.  Compute defaults to the HIP kernels
+    (ops); tests inject the oracle (normals_fn(p, k) -> (normals, kth_d2))."""
     from . import ops
 
     world, rank = _world(group)
@@ -179,10 +186,7 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
             return ops.voxel_down_sample(p, vs, mn, mx, with_xyz=False)["rep_idx"].long()
     if normals_fn is None:
         def normals_fn(p, k):
-            return ops.estimate_normals(p, knn=k)
-    if kdist_fn is None:
-        def kdist_fn(p, q, k):
-            return ops.knn_search(p, q, knn=k)[1][:, k - 1]
+            return ops.estimate_normals(p, knn=k, return_kdist=True)
     # 1. global bounds (a rank with no points contributes nothing)
     if xyz.shape[0] > 0:
         lmn = xyz.double().min(0).values.cpu().numpy()
@@ -206,8 +210,11 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
     x_hi = float(mn[0]) + keys[rank + 1] * voxel_size
     t_lo = rxyz[:, 0].double() - x_lo  # distance to the slab faces
     t_hi = x_hi - rxyz[:, 0].double()
+    inf = torch.full_like(t_lo, np.inf)
+    t = torch.minimum(t_lo if rank > 0 else inf, t_hi if rank < world - 1 else inf)  # interior faces only
     H = float(halo) if halo else 3.0 * voxel_size
     min_width = min(keys[r + 1] - keys[r] for r in range(world)) * voxel_size
+    n_total = int(_allreduce_int(rg.numel(), group))
     while True:
         if world > 1 and H >= min_width:
             raise RuntimeError("voxel_normals_slabs: the kNN halo is wider than a slab; use fewer ranks")
@@ -225,23 +232,33 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
         o = torch.argsort(ug)
         ux, ug = ux[o].contiguous(), ug[o].contiguous()
         own = torch.searchsorted(ug, rg)  # positions of the own reps in the union
-        # 5. verify: reps near a face must have their k-th neighbour inside the halo
-        inf = torch.full_like(t_lo, np.inf)
-        t = torch.minimum(t_lo if rank > 0 else inf, t_hi if rank < world - 1 else inf)
-        near = torch.nonzero(t < H).flatten()
+        # 5. normals on own + halo reps, with each row's k-th-distance bound
+        nrm, kd2 = normals_fn(ux, knn)
+        # 6. verify every own rep (see above); fewer than k points in the
+        # union while the cloud holds more cannot be verified at all
         ok = 1.0
-        if near.numel() and world > 1:
-            dk = torch.sqrt(kdist_fn(ux, ux[own[near]], knn).double())
-            ok = 1.0 if bool((dk - t[near] < H).all()) else 0.0
+        if world > 1 and rg.numel():
+            if ux.shape[0] < min(knn, n_total):
+                ok = 0.0
+            else:
+                dk = torch.sqrt(kd2[own].double().to(t.device))
+                ok = 1.0 if bool((dk < (t + H) * (1.0 - 1e-9)).all()) else 0.0
         flag = torch.tensor([ok], dtype=torch.float64, device=_comm_device(group))
         if world > 1:
             dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
         if flag.item() == 1.0:
             break
         H *= 2.0
-    # 6. normals on own + halo reps, kept for the own reps
-    nrm = normals_fn(ux, knn)[own]
-    return rg, rxyz, nrm
+    return rg, rxyz, nrm[own]
+
+
+def _allreduce_int(v: int, group=None) -> int:
+    world, _ = _world(group)
+    if world == 1:
+        return int(v)
+    t = torch.tensor([int(v)], dtype=torch.int64, device=_comm_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return int(t.item())
 
 
 def shard_range(n: int, world: int, rank: int, align: int = 1) -> Tuple[int, int]:

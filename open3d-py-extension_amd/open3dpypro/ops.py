@@ -105,28 +105,36 @@ class VoxelGrid:
 
 
 def estimate_normals(xyz: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30, radius: float = 0.0,
-                     prior: Optional[torch.Tensor] = None, voxel_grid: Optional[VoxelGrid] = None) -> torch.Tensor:
+                     prior: Optional[torch.Tensor] = None, voxel_grid: Optional[VoxelGrid] = None,
+                     return_kdist: bool = False):
     """Open3D EstimateNormals(search_param, fast_normal_computation=True) -> (N,3) float32.
 
     voxel_grid: the VoxelGrid of the voxel_down_sample that produced `xyz`
-    (its rep_xyz); the search grid is then read off the voxel table."""
+    (its rep_xyz); the search grid is then read off the voxel table.
+    return_kdist (KNN only): also return (N,) float32 upper bounds of each
+    point's squared k-th-neighbour distance (for halo checks of sharded runs)."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
     dev = x.device
     out = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev)
+    if return_kdist and mode != N.SEARCH_KNN:
+        raise ValueError("return_kdist needs KNN search")
+    kd2 = torch.empty(max(n, 1), dtype=torch.float32, device=dev) if return_kdist else None
     pr = None if prior is None else _xyz(prior.to(dev), "prior normals")
     ws = N.workspace(L.o3dx_normals_workspace_bytes(n), dev)
     if voxel_grid is not None:
         if voxel_grid.m != n or voxel_grid.pts.device != dev:
             raise ValueError("voxel_grid does not belong to these points")
         rc = L.o3dx_estimate_normals_voxel(_np_ptr(voxel_grid.geom), N.ptr(voxel_grid.pts), N.ptr(x), n, int(mode),
-                                           int(knn), float(radius), N.ptr(pr), N.ptr(out), N.ptr(ws), ws.numel(),
-                                           N.stream_ptr(dev))
+                                           int(knn), float(radius), N.ptr(pr), N.ptr(out), N.ptr(kd2), N.ptr(ws),
+                                           ws.numel(), N.stream_ptr(dev))
     else:
         rc = L.o3dx_estimate_normals(N.ptr(x), n, int(mode), int(knn), float(radius), N.ptr(pr), N.ptr(out),
-                                     N.ptr(ws), ws.numel(), N.stream_ptr(dev))
+                                     N.ptr(kd2), N.ptr(ws), ws.numel(), N.stream_ptr(dev))
     N.check(rc, "estimate_normals")
+    if return_kdist:
+        return out[:n], kd2[:n]
     return out[:n]
 
 

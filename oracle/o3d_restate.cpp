@@ -349,7 +349,14 @@ void eigvec1(const M3& A, const double e0[3], double eval1, double out[3]) {
 
 // [upstream] geometry/EstimateNormals.cpp FastEigen3x3 (Eberly, robust 3x3
 // symmetric eigensolver) -> eigenvector of the smallest eigenvalue.
-void fast_eigen3x3(const double c[6], double out[3]) {
+// `nudge` (test certificates only; 0 = Open3D exactly): base-3 digits for the
+// acos, cos(angle) and cos(angle + 2pi/3) results — 0 as is, 1 one ulp up,
+// 2 one ulp down — the 1-ulp libm latitude between two correct platforms.
+static double nudged(double v, int d) {
+  return d == 1 ? std::nextafter(v, INFINITY) : d == 2 ? std::nextafter(v, -INFINITY) : v;
+}
+
+void fast_eigen3x3(const double c[6], double out[3], int nudge = 0) {
   M3 A;
   A.a[0][0] = c[0]; A.a[0][1] = c[1]; A.a[0][2] = c[2];
   A.a[1][0] = c[1]; A.a[1][1] = c[3]; A.a[1][2] = c[4];
@@ -374,10 +381,10 @@ void fast_eigen3x3(const double c[6], double out[3]) {
     double det = (b00 * c00 - A.a[0][1] * c01 + A.a[0][2] * c02) / (p * p * p);
     double half_det = det * 0.5;
     half_det = std::min(std::max(half_det, -1.0), 1.0);
-    double angle = std::acos(half_det) / (double)3;
+    double angle = nudged(std::acos(half_det), nudge % 3) / (double)3;
     const double two_thirds_pi = 2.09439510239319549;
-    double beta2 = std::cos(angle) * 2;
-    double beta0 = std::cos(angle + two_thirds_pi) * 2;
+    double beta2 = nudged(std::cos(angle), (nudge / 3) % 3) * 2;
+    double beta0 = nudged(std::cos(angle + two_thirds_pi), (nudge / 9) % 3) * 2;
     double beta1 = -(beta0 + beta2);
     double eval[3] = {q + p * beta0, q + p * beta1, q + p * beta2};
     double e0[3], e1[3], e2[3];
@@ -755,6 +762,14 @@ void oref_knn_search(const float* xyz, int64_t n, const float* q, int64_t nq, in
 // FastEigen3x3 on a batch of covariances {xx,xy,xz,yy,yz,zz} (unit tests).
 void oref_fast_eigen3x3(const double* cov, int64_t m, double* out) {
   for (int64_t i = 0; i < m; ++i) fast_eigen3x3(cov + 6 * i, out + 3 * i);
+}
+
+// FastEigen3x3 with the transcendental results nudged by one ulp (nudge in
+// [0, 27)): the conditioning certificate of the parity tests — a normal that
+// moves by more than the tolerance under a 1-ulp acos/cos change is decided
+// by the platform's libm, not by the algorithm.
+void oref_fast_eigen3x3_nudged(const double* cov, int64_t m, int nudge, double* out) {
+  for (int64_t i = 0; i < m; ++i) fast_eigen3x3(cov + 6 * i, out + 3 * i, nudge);
 }
 
 // [upstream] utility/Random.cpp + geometry/PointCloudSegmentation.cpp

@@ -46,6 +46,7 @@ def lib():
         L.oref_estimate_normals.argtypes = [_P, _I64, _I32, _I32, _D, _P, _P]
         L.oref_knn_search.argtypes = [_P, _I64, _P, _I64, _I32, _I32, _D, _I32, _P, _P, _P]
         L.oref_fast_eigen3x3.argtypes = [_P, _I64, _P]
+        L.oref_fast_eigen3x3_nudged.argtypes = [_P, _I64, _I32, _P]
         L.oref_ransac_samples.argtypes = [_I64, _I32, _I32, ctypes.c_uint64, _P]
         L.oref_segment_plane.argtypes = [_P, _I64, _D, _I32, _I32, _D, _P, _P, _P, _P, _P, _P, _P]
         L.oref_segment_plane.restype = _I32
@@ -129,6 +130,38 @@ def fast_eigen3x3(cov6):
     c = np.ascontiguousarray(cov6, np.float64).reshape(-1, 6)
     out = np.empty((len(c), 3), np.float64)
     lib().oref_fast_eigen3x3(_ptr(c), len(c), _ptr(out))
+    return out
+
+
+def fast_eigen3x3_nudged(cov6, nudge):
+    """FastEigen3x3 with acos / cos results moved by one ulp (nudge: base-3
+    digits, see o3d_restate.cpp) — the conditioning certificate."""
+    c = np.ascontiguousarray(cov6, np.float64).reshape(-1, 6)
+    out = np.empty((len(c), 3), np.float64)
+    lib().oref_fast_eigen3x3_nudged(_ptr(c), len(c), int(nudge), _ptr(out))
+    return out
+
+
+def covariance(xyz, idx, cnt=None):
+    """Open3D ComputeCovariance over neighbour rows idx (m,K) (first cnt[i]
+    entries, in the given order — the kNN result order): sequential float64
+    raw moments, {xx,xy,xz,yy,yz,zz}.  <3 neighbours -> identity."""
+    p = np.asarray(xyz, np.float32).reshape(-1, 3).astype(np.float64)
+    idx = np.asarray(idx).reshape(len(idx), -1)
+    cnt = np.full(len(idx), idx.shape[1]) if cnt is None else np.asarray(cnt)
+    out = np.zeros((len(idx), 6))
+    for r in range(len(idx)):
+        k = int(cnt[r])
+        if k < 3:
+            out[r] = [1, 0, 0, 1, 0, 1]
+            continue
+        m = np.zeros(9)
+        for j in range(k):
+            x, y, z = p[idx[r, j]]
+            m += [x, y, z, x * x, x * y, x * z, y * y, y * z, z * z]
+        u = m / k
+        out[r] = [u[3] - u[0] * u[0], u[4] - u[0] * u[1], u[5] - u[0] * u[2], u[6] - u[1] * u[1],
+                  u[7] - u[1] * u[2], u[8] - u[2] * u[2]]
     return out
 
 

@@ -173,11 +173,11 @@ def _o3_voxel(p, vs, mn, mx):
 
 
 def _o3_normals(p, k):
-    return torch.from_numpy(O.estimate_normals(p.numpy(), O.KNN, k))
-
-
-def _o3_kdist(p, q, k):
-    return torch.from_numpy(O.knn_search(p.numpy(), q.numpy(), O.KNN, k)[1][:, k - 1].copy())
+    """oracle normals + the exact squared k-th-neighbour distance per row"""
+    x = p.numpy()
+    kk = min(k, len(x))
+    kd2 = O.knn_search(x, x, O.KNN, kk)[1][:, kk - 1].copy() if len(x) else np.zeros(0)
+    return torch.from_numpy(O.estimate_normals(x, O.KNN, k)), torch.from_numpy(kd2)
 
 
 def _c4_cloud():
@@ -189,20 +189,13 @@ def _c4_rank(rank, world):
     n = pts.shape[0]
     # an arbitrary (non-spatial) initial share: every world-th point
     g = torch.arange(rank, n, world, dtype=torch.int64)
-    return D.voxel_normals_slabs(pts[g], g, 0.05, knn=30, voxel_fn=_o3_voxel, normals_fn=_o3_normals,
-                                 kdist_fn=_o3_kdist)
+    return D.voxel_normals_slabs(pts[g], g, 0.05, knn=30, voxel_fn=_o3_voxel, normals_fn=_o3_normals)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_c4_slabs_match_single(world):
-    """Voxel reps and KNN30 normals of a cloud split over x-slabs (with the
-    halo exchange) equal the single-process result: same reps, same normals
-    bit for bit (the oracle sums each neighbourhood in the same order)."""
-    res = spawn(_c4_rank, world=world)
-    pts = _c4_cloud().numpy()
+def _check_slabs(res, pts, vs, k=30):
     mn, mx = O.aabb(pts)
-    rep = O.voxel_down_sample(pts, 0.05, mn, mx)
-    nrm = O.estimate_normals(pts[rep], O.KNN, 30)
+    rep = O.voxel_down_sample(pts, vs, mn, mx)
+    nrm = O.estimate_normals(pts[rep], O.KNN, k)
     g = np.concatenate([r[0] for r in res])
     nn = np.concatenate([r[2] for r in res])
     o = np.argsort(g)
@@ -211,3 +204,59 @@ def test_c4_slabs_match_single(world):
     for r in res:  # each slab's reps are ascending and their xyz are the input points
         assert np.all(np.diff(r[0]) > 0)
         assert np.array_equal(r[1], pts[r[0]])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_slabs_match_single(world):
+    """Voxel reps and KNN30 normals of a cloud split over x-slabs (with the
+    halo exchange) equal the single-process result: same reps, same normals
+    bit for bit (the oracle sums each neighbourhood in the same order)."""
+    res = spawn(_c4_rank, world=world)
+    _check_slabs(res, _c4_cloud().numpy(), 0.05)
+
+
+# A clustered cloud that defeats a halo check limited to the reps near a face:
+# dense blobs sit on every interior slab face (their reps near the face have
+# tiny k-th-neighbour distances), the sparse background keeps a band of 0.04
+# clear around each face, so a background rep at 0.04 from a face (beyond the
+# initial 3-voxel halo of 0.015) has k-th neighbours ~0.12 away across it.
+CL_VS = 0.005
+
+
+def _clustered_cloud(world):
+    nkeys = int(np.floor(1.0 / CL_VS)) + 1
+    faces = [((nkeys * r) // world) * CL_VS for r in range(1, world)]
+    bg = S.uniform_cube(6000, 41).numpy().astype(np.float64)
+    keep = np.ones(len(bg), bool)
+    for f in faces:
+        keep &= np.abs(bg[:, 0] - f) >= 0.04
+    parts = [bg[keep], np.array([[0.0, 0.5, 0.5], [1.0, 0.5, 0.5]])]  # anchors: x bounds exactly [0, 1]
+    rng = np.random.default_rng(42)
+    for f in faces:
+        d = rng.normal(size=(20000, 3))
+        d *= (0.02 * rng.uniform(0, 1, (20000, 1)) ** (1 / 3)) / np.linalg.norm(d, axis=1, keepdims=True)
+        parts.append(np.array([f, 0.9, 0.9]) + d)
+    return np.concatenate(parts).astype(np.float32), faces
+
+
+def _clustered_rank(rank, world):
+    pts, _ = _clustered_cloud(world)
+    g = torch.arange(rank, len(pts), world, dtype=torch.int64)
+    return D.voxel_normals_slabs(torch.from_numpy(pts)[g], g, CL_VS, knn=30, voxel_fn=_o3_voxel,
+                                 normals_fn=_o3_normals)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_slabs_clustered_halo(world):
+    pts, faces = _clustered_cloud(world)
+    # the case really exercises the hole: some rep farther than the initial
+    # halo H from every face still has true neighbours beyond H across one
+    mn, mx = O.aabb(pts)
+    rep = O.voxel_down_sample(pts, CL_VS, mn, mx)
+    r = pts[rep]
+    dk = np.sqrt(O.knn_search(r, r, O.KNN, 30)[1][:, 29])
+    t = np.min(np.abs(r[:, :1].astype(np.float64) - np.array(faces)[None, :]), 1)
+    H0 = 3 * CL_VS
+    assert np.any((t >= H0) & (dk > t + H0))
+    res = spawn(_clustered_rank, world=world)
+    _check_slabs(res, pts, CL_VS)

@@ -5,6 +5,7 @@ import torch
 
 from open3dpypro import ops, synthetic as S
 from oracle import oracle as O
+from parity import DebugNeighbors, assert_neighbour_sets, assert_normals
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 N = 10_000_000
@@ -29,31 +30,35 @@ def test_voxel_10m_exact(cloud10m):
     assert torch.equal(mx.cpu(), torch.from_numpy(rep).long())
 
 
-def test_normals_10m_reps(cloud10m):
+def test_normals_10m_reps(cloud10m, dev):
+    """C2 representatives through the sorted-grid path (LDS tiles -> wave form
+    -> register top-k): every row within 1e-5 signed, sets bit-exact."""
     vs = S.voxel_size_for(N)
     out = ops.voxel_down_sample(cloud10m, vs)
     reps = out["rep_xyz"]
-    got = ops.estimate_normals(reps, knn=30).cpu().numpy()
-    ref = O.estimate_normals(reps.cpu().numpy(), O.KNN, 30)
-    err_signed = np.abs(got - ref).max(1)
-    err_any = np.minimum(err_signed, np.abs(got + ref).max(1))
-    assert np.mean(err_any < 1e-5) > 0.9995
-    assert np.mean(err_signed < 1e-5) > 0.999
+    with DebugNeighbors(reps.shape[0], 30, dev) as dn:
+        got = ops.estimate_normals(reps, knn=30).cpu().numpy()
+    r = reps.cpu().numpy()
+    ref = O.estimate_normals(r, O.KNN, 30)
+    assert_normals(got, ref, r, k=30, what="c2_sorted_grid")
+    assert_neighbour_sets(dn.ids(), r, 30, "c2_sorted_grid")
     assert np.abs(np.linalg.norm(got, axis=1) - 1).max() < 1e-5
 
 
-def test_normals_10m_voxel_table(cloud10m):
+def test_normals_10m_voxel_table(cloud10m, dev):
     """The bench's exact step: voxel_down_sample(keep_grid) -> estimate_normals
-    on the dense voxel table, against the oracle on the same representatives."""
+    on the dense voxel table (k_normals_stile, wave form, register top-k),
+    against the oracle on the same representatives: every row within 1e-5
+    signed, and every selected neighbour set bit-equal to the oracle's."""
     vs = S.voxel_size_for(N)
     out = ops.voxel_down_sample(cloud10m, vs, keep_grid=True)
     reps = out["rep_xyz"]
-    got = ops.estimate_normals(reps, knn=30, voxel_grid=out["voxel_grid"]).cpu().numpy()
-    ref = O.estimate_normals(reps.cpu().numpy(), O.KNN, 30)
-    err_signed = np.abs(got - ref).max(1)
-    err_any = np.minimum(err_signed, np.abs(got + ref).max(1))
-    assert np.mean(err_any < 1e-5) > 0.9995
-    assert np.mean(err_signed < 1e-5) > 0.999
+    with DebugNeighbors(reps.shape[0], 30, dev) as dn:
+        got = ops.estimate_normals(reps, knn=30, voxel_grid=out["voxel_grid"]).cpu().numpy()
+    r = reps.cpu().numpy()
+    ref = O.estimate_normals(r, O.KNN, 30)
+    assert_normals(got, ref, r, k=30, what="c2_voxel_table")
+    assert_neighbour_sets(dn.ids(), r, 30, "c2_voxel_table")
     assert np.abs(np.linalg.norm(got, axis=1) - 1).max() < 1e-5
 
 
