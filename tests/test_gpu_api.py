@@ -163,7 +163,11 @@ def test_processors_numpy_and_torch_branches(dev):
 
 def test_processor_pipeline_like_test_pipeline(dev):
     """The reference's GPU chain (test_pipeline.py:406-416) up to PlaneNormalize."""
-    pts = S.planted_plane(200000, 9).numpy() - np.array([0.5, 0.5, 0.0], np.float32)
+    # half the points on the plane: after RandomSample + voxel thinning the plane
+    # keeps ~30 % of the reps, so 512 hypotheses find it with certainty (at the
+    # default 20 % it keeps ~14 %, and 512 triples miss it ~25 % of the time)
+    np.random.seed(0)
+    pts = S.planted_plane(200000, 9, frac=0.5).numpy() - np.array([0.5, 0.5, 0.0], np.float32)
     det = o3p.Processors.PlaneDetection(distance_threshold=0.02, alpha=1.0, seed=1)
     pipes = [o3p.Processors.RandomSample(n_samples=50000),
              o3p.Processors.NumpyToTorch(),
