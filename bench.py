@@ -1,14 +1,22 @@
 #!/usr/bin/env python
-"""bench.py — headline benchmark: Mpoints/s of voxel_down_sample + estimate_normals
-(KNN30) on synthetic uniform-random 10M-point float32 clouds (BASELINE.json
-configs[1]), plus ICP iterations/s and RANSAC time (C3) as
-secondary figures.
+"""bench.py — headline benchmark (BASELINE.json metric): Mpoints/s of
+voxel_down_sample + estimate_normals (KNN30), plus ICP iterations/s.
 
-One step = one pass of the hot path over one cloud that is already resident
-in HBM: voxel_down_sample(vs=(4/N)^(1/3)) -> estimate_normals(KNN 30) on the
-M representatives.  Multi-GPU: one process per GPU (torchrun), each rank owns
-one 10M-point spatial tile (an independent cloud, no data-path collective):
-weak scaling.  `value` = points processed by all ranks / max-over-ranks time.
+N = 1 (default): C2 — one synthetic uniform-random 10M-point float32 cloud
+resident in HBM; one step = voxel_down_sample(vs=(4/N)^(1/3)) ->
+estimate_normals(KNN 30) on the M representatives.  Secondary figures on the
+same GPU: C3 (RANSAC 1000 hypotheses + point-to-plane ICP 30 iterations at
+10M), C4's size on one GPU (50M) and C5 (200M full pipeline incl. ICP), and
+the CPU baselines (the oracle, an Open3D-equivalent C++ restatement) of the
+voxel+normals step, RANSAC and ICP on the same inputs.
+
+N > 1 (torchrun, one process per GPU, RCCL): C4 — ONE 50M-point cloud tiled
+over the ranks as voxel-aligned x-slabs (each rank's points resident in its
+slab), one step = global AABB all-reduce, slab voxel reps, halo exchange of
+boundary representatives (all-to-all), normals off the slab's voxel table,
+halo proof all-reduce (open3dpypro.distributed.voxel_normals_slabs): strong
+scaling; plus the sharded ICP (RCCL moment all-gather per iteration).
+`value` = points of the whole job / max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
    or: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -51,7 +59,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--sorted-grid", action="store_true",
                     help="normals sort the representatives into their own grid (no voxel table hand-over)")
-    ap.add_argument("--cpu-n", type=int, default=2_000_000, help="CPU baseline sample size")
+    ap.add_argument("--cpu-n", type=int, default=10_000_000, help="CPU baseline size (C2 input: 10M)")
+    ap.add_argument("--cpu-icp-iters", type=int, default=2, help="ICP iterations of the CPU ICP leg (bounded sample)")
+    ap.add_argument("--c5-n", type=int, default=200_000_000, help="C5 cloud size (0: skip the C5 leg)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the ICP / RANSAC figures")
     ap.add_argument("--icp-n", type=int, default=10_000_000)
     ap.add_argument("--icp-iters", type=int, default=30)
@@ -67,12 +77,23 @@ def setup_dist(force=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-GPU path on a one-GPU box: every rank on cuda:0, gloo
+    shared = os.environ.get("O3DX_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or (force and "MASTER_PORT" in os.environ):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if shared:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     return world, rank, dev
+
+
+def comm_dev(dev):
+    return dev if dist.is_initialized() and dist.get_backend() == "nccl" else torch.device("cpu")
 
 
 def barrier(world, dev):
@@ -84,7 +105,7 @@ def barrier(world, dev):
 def max_over_ranks(x, world, dev):
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=comm_dev(dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -100,12 +121,27 @@ def pmc_entry(path, kernel):
         return {}
 
 
-def cpu_baseline(n_cpu: int):
-    """Oracle restatement of Open3D's CPU path (voxel trace single-threaded as in
-    Open3D, KNN30 normals with OpenMP) on a bounded C2-shaped sample."""
+def host_info():
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(n_cpu: int, pts_dev=None):
+    """The oracle (an Open3D-equivalent C++ restatement, oracle/) of the C2
+    step on the C2 input itself: voxel trace single-threaded as Open3D's,
+    KD-tree KNN30 normals with OpenMP."""
     from oracle import oracle as O
 
-    pts = synthetic.uniform_cube(n_cpu, seed=0).numpy()
+    pts = (pts_dev.cpu().numpy() if pts_dev is not None and pts_dev.shape[0] == n_cpu
+           else synthetic.uniform_cube(n_cpu, seed=0).numpy())
     vs = synthetic.voxel_size_for(n_cpu)
     O.lib()
     t0 = time.perf_counter()
@@ -116,11 +152,49 @@ def cpu_baseline(n_cpu: int):
     el = t2 - t0
     return {"value": round(n_cpu / el / 1e6, 4), "unit": "Mpoints/s", "cores": O.num_threads(),
             "kind": "port",
-            "sample": (f"C2 shape at N={n_cpu} (uniform cube, vs=(4/N)^(1/3), M={len(rep)}): "
-                       f"Open3D-equivalent C++ restatement (oracle/): voxel trace 1 thread "
-                       f"{t1 - t0:.2f}s + KD-tree KNN30 normals {O.num_threads()} OpenMP threads "
-                       f"{t2 - t1:.2f}s; host {platform.processor() or platform.machine()}"),
-            "seconds": round(el, 3)}
+            "sample": (f"the C2 input itself (N={n_cpu}, M={len(rep)}): Open3D-equivalent C++ restatement "
+                       f"(oracle/o3d_restate.cpp): voxel trace 1 thread {t1 - t0:.2f}s + KD-tree KNN30 normals "
+                       f"{O.num_threads()} OpenMP threads {t2 - t1:.2f}s"),
+            "seconds": round(el, 3), **host_info()}
+
+
+def cpu_secondary(dev, args, tn_dev=None):
+    """CPU legs of C3 through the oracle (labelled as the restatement):
+    segment_plane 1000 hypotheses on the 10M planted-plane cloud (OpenMP over
+    hypotheses, as Open3D), and point-to-plane ICP on the 10M box-surface
+    clouds — a bounded sample of iterations (KD-tree build + per-iteration
+    rate reported separately)."""
+    from oracle import oracle as O
+
+    out = {}
+    n = args.icp_n
+    pts = synthetic.planted_plane(n, seed=1).numpy()
+    samples = ops.ransac_samples(n, 3, args.ransac_iters, seed=7)
+    t0 = time.perf_counter()
+    O.segment_plane(pts, 0.01, 3, args.ransac_iters, samples)
+    el = time.perf_counter() - t0
+    out["cpu_ransac"] = {"n": n, "iterations": args.ransac_iters, "seconds": round(el, 3),
+                         "Gpairs_per_s": round(n * args.ransac_iters / el / 1e9, 3), "cores": O.num_threads(),
+                         "kind": "port (oracle segment_plane, OpenMP over hypotheses)"}
+    del pts
+    tgt = synthetic.box_surface(n, seed=1).numpy()
+    src = synthetic.apply_transform(synthetic.box_surface(n, seed=2), synthetic.rigid_transform()).numpy()
+    tn = tn_dev.cpu().numpy() if tn_dev is not None else O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
+    k = max(1, args.cpu_icp_iters)
+    t0 = time.perf_counter()
+    O.registration_icp(src, tgt, tn, 0.02, max_iteration=0)
+    t1 = time.perf_counter()
+    O.registration_icp(src, tgt, tn, 0.02, max_iteration=k, relative_fitness=0.0, relative_rmse=0.0)
+    t2 = time.perf_counter()
+    per_iter = max((t2 - t1) - (t1 - t0), 1e-9) / k  # build + first correspondence pass cancel out
+    out["cpu_icp"] = {"n_source": n, "n_target": n, "iterations_timed": k,
+                      "iters_per_s": round(1.0 / per_iter, 4), "setup_s": round(t1 - t0, 3),
+                      "cores": O.num_threads(),
+                      "kind": "port (oracle registration_icp: KD-tree build + hybrid 1-NN per iteration, OpenMP "
+                              "correspondences, sequential JTJ)",
+                      "sample": f"{k} iterations of C3's 10M/10M ICP; target normals = the GPU's (equal to the "
+                                f"oracle's within 1e-5)"}
+    return out
 
 
 def secondary(dev, args):
@@ -242,42 +316,148 @@ def c4_single_gpu(dev, args):
                               "algorithmic_bytes": "12 N + 28 M (SURVEY.md 8(d))"}}
 
 
-def c4_slabs(dev, args, world, rank):
-    """C4 across the ranks: ONE 50M cloud (this rank holds an index range of
-    it), voxel-aligned x-slabs, points to their slab owner and a verified halo
-    of representatives to the neighbours (all-to-all over RCCL), voxel reps +
-    KNN normals per slab (open3dpypro.distributed.voxel_normals_slabs)."""
+def c5_pipeline(dev, args):
+    """C5's full pipeline on one GPU (200M points fit one MI355X's HBM):
+    a 200M-point box-surface scene and an independent 200M-point sample of it
+    moved by T_gt -> voxel_down_sample both (vs 0.5 mm) -> KNN30 normals on the
+    target reps -> segment_plane (1000 hypotheses) on the target reps ->
+    point-to-plane ICP source reps -> target reps, 30 iterations from T = I."""
+    n = args.c5_n
+    vs = 0.0005
+    res = {"n": n, "voxel_size": vs}
+    stages = {}
+
+    def timed(name, fn):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize(dev)
+        stages[name] = round((time.perf_counter() - t0) * 1e3, 3)
+        return r
+
+    tgt = synthetic.box_surface(n, seed=1, device=dev)
+    src = synthetic.apply_transform(synthetic.box_surface(n, seed=2, device=dev), synthetic.rigid_transform())
+    torch.cuda.synchronize(dev)
+    t_all = time.perf_counter()
+    vt = timed("voxel_target", lambda: ops.voxel_down_sample(tgt, vs, keep_grid=True))
+    vsrc = timed("voxel_source", lambda: ops.voxel_down_sample(src, vs))
+    del tgt, src
+    treps, sreps = vt["rep_xyz"], vsrc["rep_xyz"]
+    tn = timed("normals_target", lambda: ops.estimate_normals(treps, knn=30, voxel_grid=vt.get("voxel_grid")))
+    samples = ops.ransac_samples(treps.shape[0], 3, args.ransac_iters, seed=7)
+    plane, inl = timed("segment_plane", lambda: ops.segment_plane(treps, 0.002, 3, args.ransac_iters,
+                                                                  samples=samples))
+
+    def icp():
+        target = ops.ICPTarget(treps, tn, 0.02)
+        s4 = ops.spatial_sort(sreps)
+        T = np.eye(4)
+        sums = None
+        for _ in range(args.icp_iters):
+            sums, _ = target.accumulate(s4, T)
+            T = ops.icp_solve(sums) @ T
+        return T, sums
+
+    T, sums = timed("icp_30", icp)
+    total = time.perf_counter() - t_all
+    res.update({"target_reps": int(treps.shape[0]), "source_reps": int(sreps.shape[0]), "stages_ms": stages,
+                "total_ms": round(total * 1e3, 3), "Mpoints_per_s_voxel_normals_target":
+                round(n / ((stages["voxel_target"] + stages["normals_target"]) * 1e-3) / 1e6, 2),
+                "icp_iters_per_s": round(args.icp_iters / (stages["icp_30"] * 1e-3), 2),
+                "plane": [round(float(v), 6) for v in plane], "plane_inliers": int(inl.numel()),
+                "icp_fitness": round(float(sums[28]) / max(int(sreps.shape[0]), 1), 6),
+                "T_err_vs_gt_inverse": float(np.abs(T - np.linalg.inv(synthetic.rigid_transform())).max())})
+    del vt, vsrc, treps, sreps, tn, inl
+    torch.cuda.empty_cache()
+    return {"c5_single_gpu": res}
+
+
+def c4_headline(dev, args, world, rank):
+    """N > 1 headline (C4): ONE 50M-point cloud, each rank's points resident in
+    its voxel-aligned x-slab (a spatially tiled dataset; placement untimed),
+    one step = open3dpypro.distributed.voxel_normals_slabs(presorted=True)."""
     from open3dpypro import distributed as D
 
     n = args.c4_n
-    a, b = D.shard_range(n, world, rank)
-    pts = synthetic.uniform_cube(b - a, seed=0, offset=a, device=dev)
-    gidx = torch.arange(a, b, dtype=torch.int64, device=dev)
     vs = synthetic.voxel_size_for(n)
-    D.voxel_normals_slabs(pts, gidx, vs, knn=args.knn)  # warm
+    full = synthetic.uniform_cube(n, seed=0, device=dev)
+    mn, mx = ops.aabb(full)
+    keys = D.slab_bounds(mn, mx, vs, world)
+    kx = torch.floor((full[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+    gidx = torch.nonzero((kx >= keys[rank]) & (kx < keys[rank + 1])).flatten()
+    pts = full[gidx].contiguous()
+    del full, kx
+    torch.cuda.empty_cache()
+
+    def step():
+        return D.voxel_normals_slabs(pts, gidx, vs, knn=args.knn, presorted=True)
+
+    for _ in range(args.warmup):
+        rg, _, _ = step()
+    _native.reset_kernel_timing()
+    _native.set_kernel_timing(True)
     barrier(world, dev)
     t0 = time.perf_counter()
-    rg, _, _ = D.voxel_normals_slabs(pts, gidx, vs, knn=args.knn)
+    for _ in range(args.steps):
+        rg, _, _ = step()
     barrier(world, dev)
-    el = max_over_ranks(time.perf_counter() - t0, world, dev)
-    m = torch.tensor([rg.numel()], dtype=torch.int64, device=dev)
-    if world > 1:
-        dist.all_reduce(m)
-    return {"c4_slabs": {"n": n, "ranks": world, "voxels": int(m.item()), "ms": round(el * 1e3, 3),
-                         "Mpoints_per_s": round(n / el / 1e6, 2), "scaling": "strong",
-                         "collectives": "all_reduce (AABB, halo check), all_to_all (points to slab owners, halo reps)"}}
+    t1 = time.perf_counter()
+    _native.set_kernel_timing(False)
+    elapsed = max_over_ranks(t1 - t0, world, dev)
+    m = torch.tensor([rg.numel()], dtype=torch.int64, device=comm_dev(dev))
+    dist.all_reduce(m)
+    return elapsed, int(m.item()), int(pts.shape[0])
+
+
+def kernel_table():
+    kernels = {}
+    for name in ("voxel_assign", "voxel_compact", "grid_count", "grid_sort", "normals_stile", "normals_tile",
+                 "normals_wave", "normals_knn"):
+        ms, cnt = _native.kernel_timing(name)
+        if cnt:
+            kernels[name] = {"avg_ms": round(ms / cnt, 4), "launches": cnt}
+    return kernels
+
+
+def roofline(kernels, M, N, pmc_json):
+    # algorithmic bytes per launch (DESIGN.md §4, SURVEY §8(d)):
+    #   normals_stile / normals_tile: M queries x (12 B xyz read + 12 B normal written)
+    #   voxel_assign: N points x (12 B xyz read + 4 B voxel id written)
+    algo_bytes = {"normals_stile": 24.0 * M, "normals_tile": 24.0 * M, "voxel_assign": 16.0 * N}
+    dom = max((k for k in kernels if k in algo_bytes), key=lambda k: kernels[k]["avg_ms"], default=None)
+    if dom is None:
+        return None
+    avg_s = kernels[dom]["avg_ms"] * 1e-3
+    ach = algo_bytes[dom] / avg_s / 1e9
+    pmc = pmc_entry(pmc_json, dom)
+    roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": pmc.get("hbm_bytes_per_launch"),
+            "algorithmic_bytes_per_launch": algo_bytes[dom],
+            "note": "exact kNN selection is LDS / VALU-issue work, not HBM streaming: DESIGN.md §4.1"}
+    if pmc.get("SQ_INSTS_VALU"):
+        # VALU-issue floor (MI355X_MICROARCH.md: a wave64 VALU instruction issues in 2 cycles on a SIMD
+        # holding >= 2 waves; float64 / transcendental ones take longer, so this is a lower bound)
+        floor_ms = pmc["SQ_INSTS_VALU"] * 2.0 / (1024 * 2.4e9) * 1e3
+        roof["valu_issue_floor_ms"] = round(floor_ms, 4)
+        roof["valu_issue_frac"] = round(floor_ms / kernels[dom]["avg_ms"], 4)
+    if pmc.get("SQ_LDS_IDX_ACTIVE") and pmc.get("GRBM_GUI_ACTIVE"):
+        # LDS busy share: SQ_LDS_IDX_ACTIVE (LDS-array cycles, summed over CUs) / (256 CUs x kernel cycles)
+        cyc = pmc["GRBM_GUI_ACTIVE"] / 8.0  # GRBM_GUI_ACTIVE sums the 8 XCDs
+        roof["lds_busy_frac"] = round(pmc["SQ_LDS_IDX_ACTIVE"] / (256.0 * cyc), 4)
+        if pmc.get("SQ_LDS_BANK_CONFLICT") is not None:
+            roof["lds_conflict_frac"] = round(pmc["SQ_LDS_BANK_CONFLICT"] / pmc["SQ_LDS_IDX_ACTIVE"], 4)
+    return roof
 
 
 def main():
     args = parse()
     world, rank, dev = setup_dist(args.dist_icp)
+    if world > 1:
+        return main_multi(args, world, rank, dev)
     N = args.n
     vs = synthetic.voxel_size_for(N)
-    # this rank's tile: an independent 10M cloud, shifted to x in [rank, rank+1)
-    pts = synthetic.uniform_cube(N, seed=0, offset=rank * N, device=dev)
-    pts[:, 0] += float(rank)
+    pts = synthetic.uniform_cube(N, seed=0, device=dev)
     torch.cuda.synchronize(dev)
-
     keep = not args.sorted_grid
 
     def step():
@@ -302,80 +482,87 @@ def main():
     barrier(world, dev)
     t1 = time.perf_counter()
     _native.set_kernel_timing(False)
-    elapsed = max_over_ranks(t1 - t0, world, dev)
+    elapsed = t1 - t0
     ev_ms = ev0.elapsed_time(ev1)
+    kernels = kernel_table()
+    value = float(N) * args.steps / elapsed / 1e6
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C2: uniform-random 10M pts float32, voxel_down_sample(vs=(4/N)^(1/3)) "
+                               "+ estimate_normals(KNN30) on the representatives",
+                   "n_points": N, "voxel_size": vs, "voxels": int(M), "knn": args.knn, "parallelism": "single"},
+        "roofline": roofline(kernels, M, N, args.pmc_json),
+        "cpu_baseline": None,
+        "extra": {"stream_event_ms_per_step": round(ev_ms / args.steps, 3), "kernels": kernels,
+                  "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps / elapsed / 1e9, 2),
+                  "storage_dtype": "f32", "arith": "float64 voxel keys / distances / covariance"},
+    }
+    if not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_n, pts)
+        if line["cpu_baseline"]["value"] > 0:
+            line["extra"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
+    del pts
+    torch.cuda.empty_cache()
+    if not args.no_secondary:
+        for name, fn in (("secondary", lambda: secondary(dev, args)),
+                         ("c4", lambda: c4_single_gpu(dev, args) if args.c4_n > 0 else {}),
+                         ("c5", lambda: c5_pipeline(dev, args) if args.c5_n > 0 else {})):
+            try:
+                line["extra"].update(fn())
+            except RuntimeError as e:  # report, never hide
+                line["extra"][f"{name}_error"] = str(e)
+            torch.cuda.empty_cache()
+        if args.dist_icp:
+            line["extra"].update(secondary_sharded_icp(dev, args, world, rank))
+        if not args.no_cpu:
+            try:
+                tn = ops.estimate_normals(synthetic.box_surface(args.icp_n, seed=1, device=dev), knn=30)
+                line["extra"].update(cpu_secondary(dev, args, tn))
+            except RuntimeError as e:
+                line["extra"]["cpu_secondary_error"] = str(e)
+            ex = line["extra"]
+            if "cpu_ransac" in ex and "ransac" in ex:
+                ex["cpu_ransac"]["gpu_over_cpu"] = round(ex["cpu_ransac"]["seconds"] * 1e3 / ex["ransac"]["ms"], 1)
+            if "cpu_icp" in ex and "icp" in ex:
+                ex["cpu_icp"]["gpu_over_cpu"] = round(ex["icp"]["iters_per_s"] / ex["cpu_icp"]["iters_per_s"], 1)
+    print(json.dumps(line), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
-    kernels = {}
-    for name in ("voxel_assign", "voxel_compact", "grid_count", "grid_sort", "normals_stile", "normals_tile",
-                 "normals_wave", "normals_knn"):
-        ms, cnt = _native.kernel_timing(name)
-        if cnt:
-            kernels[name] = {"avg_ms": round(ms / cnt, 4), "launches": cnt}
-    # algorithmic bytes per launch:
-    #   normals_stile / normals_tile: M queries x (12 B xyz read + 12 B normal written)
-    #   voxel_assign: N points x (12 B xyz read + 4 B voxel id written)
-    algo_bytes = {"normals_stile": 24.0 * M, "normals_tile": 24.0 * M, "voxel_assign": 16.0 * N}
-    dom = max((k for k in kernels if k in algo_bytes), key=lambda k: kernels[k]["avg_ms"], default=None)
-    roof = None
-    if dom is not None:
-        avg_s = kernels[dom]["avg_ms"] * 1e-3
-        ach = algo_bytes[dom] / avg_s / 1e9
-        pmc = pmc_entry(args.pmc_json, dom)
-        traffic = pmc.get("hbm_bytes_per_launch")
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "algorithmic_bytes_per_launch": algo_bytes[dom],
-                "note": "kNN selection is VALU/LDS-issue bound, not HBM bound: see DESIGN.md (Roofline)"}
-        if pmc.get("valu_issue_floor_ms"):
-            # the bound that actually applies: VALU issue (PMC SQ_INSTS_VALU x 4 cycles / 1024 SIMDs @ 2.4 GHz)
-            roof["valu_issue_floor_ms"] = round(pmc["valu_issue_floor_ms"], 4)
-            roof["valu_issue_frac"] = round(pmc["valu_issue_floor_ms"] / kernels[dom]["avg_ms"], 4)
 
-    total_pts = float(N) * world * args.steps
-    value = total_pts / elapsed / 1e6
+def main_multi(args, world, rank, dev):
+    """N > 1: the C4 headline (strong scaling of one 50M cloud over the ranks)."""
+    elapsed, M, n_local = c4_headline(dev, args, world, rank)
+    kernels = kernel_table()
+    N = args.c4_n
+    value = float(N) * args.steps / elapsed / 1e6
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": "C2: uniform-random 10M pts float32 per GPU, voxel_down_sample(vs=(4/N)^(1/3)) "
-                               "+ estimate_normals(KNN30) on the representatives",
-                   "n_points_per_gpu": N, "voxel_size": vs, "voxels_per_gpu": int(M), "knn": args.knn,
-                   "parallelism": f"tile-per-gpu x{world}"},
-        "roofline": roof,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"C4: one uniform-random {N // 1_000_000}M-pt float32 cloud tiled over {world} GPUs "
+                               "as voxel-aligned x-slabs, voxel_down_sample(vs=(4/N)^(1/3)) + estimate_normals(KNN30) "
+                               "with a verified halo exchange of boundary representatives over RCCL",
+                   "n_points": N, "voxel_size": synthetic.voxel_size_for(N), "voxels": M, "knn": args.knn,
+                   "parallelism": f"x-slab spatial tiling x{world}", "points_rank0": n_local},
+        "roofline": roofline(kernels, M / world, N / world, args.pmc_json),
         "cpu_baseline": None,
-        "extra": {"stream_event_ms_per_step_rank0": round(ev_ms / args.steps, 3), "kernels": kernels,
-                  "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps * world / elapsed / 1e9, 2),
-                  "storage_dtype": "f32", "arith": "float64 voxel keys / distances / covariance"},
+        "extra": {"kernels_rank0": kernels,
+                  "collectives": "all_reduce (AABB, halo proof), all_to_all (halo representatives)",
+                  "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps / elapsed / 1e9, 2)},
     }
-    del pts
     torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and not args.no_secondary:
-        try:
-            line["extra"].update(secondary(dev, args))
-        except RuntimeError as e:  # report, never hide
-            line["extra"]["secondary_error"] = str(e)
-    if (world > 1 or args.dist_icp) and not args.no_secondary:
+    if not args.no_secondary:
         try:
             line["extra"].update(secondary_sharded_icp(dev, args, world, rank))
         except RuntimeError as e:  # report, never hide
             line["extra"]["secondary_error"] = str(e)
-    if args.c4_n > 0 and not args.no_secondary:
-        try:
-            if world == 1:
-                line["extra"].update(c4_single_gpu(dev, args))
-            else:
-                line["extra"].update(c4_slabs(dev, args, world, rank))
-        except RuntimeError as e:  # report, never hide
-            line["extra"]["c4_error"] = str(e)
-    if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_n)
-        if line["cpu_baseline"]["value"] > 0:
-            line["extra"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist.is_initialized():
-        dist.barrier()
-        dist.destroy_process_group()
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -171,6 +171,34 @@ int o3dx_voxel_down_sample_grid(const float* xyz_dev, int64_t n,
                                 int64_t voxel_cells, double* geom_host,
                                 void* ws, size_t ws_bytes, void* stream);
 
+/* Slab form (C4: one cloud spread over GPUs as voxel-aligned x-slabs,
+ * open3dpypro.distributed.voxel_normals_slabs).  Keys are those of the GLOBAL
+ * min_bound (so every voxel and representative is the single-GPU one); only
+ * the x keys [kx0, kx1) are materialised.
+ * o3dx_voxel_down_sample_window: o3dx_voxel_down_sample_grid restricted to
+ * the window (every point must fall inside it; voxel_pts_dev nullable);
+ * geom_host[0] is then the window's x origin and geom_host[9] = kx0.
+ * o3dx_voxel_table_build: the voxel table (x, y, z, row) of n points holding
+ * at most one point per voxel — a slab's own + halo representatives in their
+ * global order — over the same window, plus geom_host, for
+ * o3dx_estimate_normals_voxel.  Errors: a point outside the window, two
+ * points in one voxel.  Synchronises. */
+int o3dx_voxel_down_sample_window(const float* xyz_dev, int64_t n,
+                                  const double* min_bound_host,
+                                  const double* max_bound_host, double voxel_size,
+                                  int64_t kx0, int64_t kx1, int32_t* rep_idx_dev,
+                                  float* rep_xyz_dev, int64_t* m_host,
+                                  float* voxel_pts_dev, int64_t voxel_cells,
+                                  double* geom_host, void* ws, size_t ws_bytes,
+                                  void* stream);
+size_t o3dx_voxel_table_workspace_bytes(void);
+int o3dx_voxel_table_build(const float* xyz_dev, int64_t n,
+                           const double* min_bound_host,
+                           const double* max_bound_host, double voxel_size,
+                           int64_t kx0, int64_t kx1, float* voxel_pts_dev,
+                           int64_t voxel_cells, double* geom_host, void* ws,
+                           size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- normals
  * Replaces o3d PointCloud.estimate_normals(search_param,
  * fast_normal_computation=True) (reference PointCloud.py:68-73, used by

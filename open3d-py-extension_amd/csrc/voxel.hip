@@ -32,6 +32,7 @@ constexpr int kHashOff = 1 << (kHashBits - 1);
 struct VoxelGeom {
   double mnx, mny, mnz, vs;
   int nx, ny, nz;
+  int kx0 = 0;  // x-key window [kx0, kx0 + nx) of a slab (keys stay those of min_bound)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t k) {
@@ -52,7 +53,7 @@ __device__ __forceinline__ void voxel_ref(const P3& q, const VoxelGeom& g, doubl
   r[0] = ((double)q.x - g.mnx) / g.vs;
   r[1] = ((double)q.y - g.mny) / g.vs;
   r[2] = ((double)q.z - g.mnz) / g.vs;
-  v[0] = (int)floor(r[0]);
+  v[0] = (int)floor(r[0]) - g.kx0;
   v[1] = (int)floor(r[1]);
   v[2] = (int)floor(r[2]);
 }
@@ -373,7 +374,11 @@ __global__ void __launch_bounds__(kBlock) k_gather_vox(const float* __restrict__
 // Occupied cells of 2^3 voxels (thread per cell, one atomic per block): with
 // one rep per occupied voxel, m / occ2 gives the cloud's local dimension, from
 // which the normals size their search cell.
-__global__ void __launch_bounds__(kBlock) k_voxel_occ2(const int32_t* __restrict__ table, VoxelGeom g,
+__device__ __forceinline__ bool voxel_full(const int32_t* t, int64_t i) { return t[i] >= 0; }
+__device__ __forceinline__ bool voxel_full(const float4* t, int64_t i) { return __float_as_int(t[i].w) >= 0; }
+
+template <class T>
+__global__ void __launch_bounds__(kBlock) k_voxel_occ2(const T* __restrict__ table, VoxelGeom g,
                                                        unsigned long long* __restrict__ occ2) {
   const int cx = (g.nx + 1) / 2, cy = (g.ny + 1) / 2, cz = (g.nz + 1) / 2;
   const int64_t nc = (int64_t)cx * cy * cz;
@@ -384,7 +389,7 @@ __global__ void __launch_bounds__(kBlock) k_voxel_occ2(const int32_t* __restrict
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
       const int x = x0 + (d & 1), y = y0 + ((d >> 1) & 1), z = z0 + (d >> 2);
-      if (x < g.nx && y < g.ny && z < g.nz) any |= table[x + (int64_t)g.nx * (y + (int64_t)g.ny * z)] >= 0;
+      if (x < g.nx && y < g.ny && z < g.nz) any |= voxel_full(table, x + (int64_t)g.nx * (y + (int64_t)g.ny * z));
     }
     c += any;
   }
@@ -474,7 +479,7 @@ extern "C" int64_t o3dx_voxel_grid_cells(int64_t n, const double* min_bound_host
 static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host, const double* max_bound_host,
                       double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point,
                       int32_t* cubic_id, float* vox, int64_t vox_cap, double* geom, void* ws, size_t ws_bytes,
-                      void* stream) {
+                      void* stream, const int64_t* xwin = nullptr) {
   if (geom)
     for (int k = 0; k < 12; ++k) geom[k] = 0.0;
   if (n < 0 || (n > 0 && (!xyz || !rep_idx)) || !m_host)
@@ -518,8 +523,15 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   g.vs = voxel_size;
   double dims[3];
   voxel_dims(mn, mx, voxel_size, dims);
+  if (xwin) {  // slab: only the x keys [xwin[0], xwin[1]) exist, every point must fall inside
+    if (xwin[0] < 0 || xwin[1] <= xwin[0] || (double)xwin[1] > dims[0])
+      return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_window: bad x-key window");
+    g.kx0 = (int)xwin[0];
+    dims[0] = (double)(xwin[1] - xwin[0]);
+  }
   double nvox = dims[0] * dims[1] * dims[2];
   bool dense = nvox <= (double)dense_cap(n);
+  if (xwin && !dense) return fail(O3DX_ENOTSUP, "o3dx_voxel_down_sample_window: slab grid too sparse for a table");
   g.nx = (int)dims[0];
   g.ny = (int)dims[1];
   g.nz = (int)dims[2];
@@ -551,7 +563,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       if (vox && nslots <= vox_cap) {
         O3DX_HIP(hipMemsetAsync(vox, 0xFF, (size_t)nslots * 4 * sizeof(float), s));
         const int64_t nc2 = (int64_t)((g.nx + 1) / 2) * ((g.ny + 1) / 2) * ((g.nz + 1) / 2);
-        hipLaunchKernelGGL(k_voxel_occ2, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table, g,
+        hipLaunchKernelGGL(k_voxel_occ2<int32_t>, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table, g,
                            reinterpret_cast<unsigned long long*>(w.count + 2));
         grid_kept = true;
       }
@@ -589,6 +601,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     O3DX_TRY(read_back(counts, w.count, 3 * sizeof(int64_t), s));
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
+    if (xwin) return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_window: points outside the x-key window");
     if (errflag == 2 || !dense)
       return fail(O3DX_ENOTSUP, "voxel grid spans more than 2^%d cells per axis", kHashBits);
     dense = false;  // points outside the given bounds: retry with the hash table
@@ -596,8 +609,8 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   const int64_t m = counts[0];
   *m_host = m;
   if (geom && grid_kept) {
-    const double gv[12] = {g.mnx, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny, (double)g.nz, 1.0,
-                           (double)counts[2], 0.0, 0.0, nvox};
+    const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny,
+                           (double)g.nz, 1.0, (double)counts[2], (double)g.kx0, 0.0, nvox};
     for (int k = 0; k < 12; ++k) geom[k] = gv[k];
   }
   if ((voxel_of_point || cubic_id) && m > 0) {
@@ -625,4 +638,88 @@ extern "C" int o3dx_voxel_down_sample_grid(const float* xyz, int64_t n, const do
   if (!voxel_pts || !geom_host) return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_grid: null voxel_pts / geom");
   return voxel_impl(xyz, n, min_bound_host, max_bound_host, voxel_size, rep_idx, rep_xyz, m_host, voxel_of_point,
                     cubic_id, voxel_pts, voxel_cells, geom_host, ws, ws_bytes, stream);
+}
+
+extern "C" int o3dx_voxel_down_sample_window(const float* xyz, int64_t n, const double* min_bound_host,
+                                             const double* max_bound_host, double voxel_size, int64_t kx0,
+                                             int64_t kx1, int32_t* rep_idx, float* rep_xyz, int64_t* m_host,
+                                             float* voxel_pts, int64_t voxel_cells, double* geom_host, void* ws,
+                                             size_t ws_bytes, void* stream) {
+  if (!min_bound_host || !max_bound_host)
+    return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_window: the global bounds are required");
+  const int64_t win[2] = {kx0, kx1};
+  return voxel_impl(xyz, n, min_bound_host, max_bound_host, voxel_size, rep_idx, rep_xyz, m_host, nullptr, nullptr,
+                    voxel_pts, voxel_pts ? voxel_cells : 0, geom_host, ws, ws_bytes, stream, win);
+}
+
+// ------------------------------------------------------------ table build
+// The voxel table of an arbitrary point set holding at most one point per
+// voxel (a slab's own + halo representatives): vox[v] = (x, y, z, row).
+__global__ void __launch_bounds__(kBlock) k_table_build(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+                                                        float4* __restrict__ vox, int* __restrict__ err) {
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const P3 q = p[j];
+    int v[3];
+    if (!voxel_of(q, g, v)) {
+      atomicOr(err, 1);
+      continue;
+    }
+    const int64_t at = v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2]);
+    int* w = reinterpret_cast<int*>(&vox[at].w);
+    if (atomicCAS(w, -1, (int)j) != -1) {
+      atomicOr(err, 2);
+      continue;
+    }
+    vox[at].x = q.x;
+    vox[at].y = q.y;
+    vox[at].z = q.z;
+  }
+}
+
+extern "C" size_t o3dx_voxel_table_workspace_bytes(void) { return 256; }
+
+extern "C" int o3dx_voxel_table_build(const float* xyz, int64_t n, const double* min_bound_host,
+                                      const double* max_bound_host, double voxel_size, int64_t kx0, int64_t kx1,
+                                      float* voxel_pts, int64_t voxel_cells, double* geom_host, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  if (geom_host)
+    for (int k = 0; k < 12; ++k) geom_host[k] = 0.0;
+  if (n < 0 || (n > 0 && !xyz) || !voxel_pts || !geom_host || !min_bound_host || !max_bound_host || !ws ||
+      ws_bytes < o3dx_voxel_table_workspace_bytes())
+    return fail(O3DX_EINVAL, "o3dx_voxel_table_build: bad arguments");
+  if (!(voxel_size > 0.0)) return fail(O3DX_EINVAL, "voxel_size <= 0.");
+  double dims[3];
+  voxel_dims(min_bound_host, max_bound_host, voxel_size, dims);
+  if (kx0 < 0 || kx1 <= kx0 || (double)kx1 > dims[0]) return fail(O3DX_EINVAL, "o3dx_voxel_table_build: bad window");
+  VoxelGeom g;
+  g.mnx = min_bound_host[0];
+  g.mny = min_bound_host[1];
+  g.mnz = min_bound_host[2];
+  g.vs = voxel_size;
+  g.kx0 = (int)kx0;
+  g.nx = (int)(kx1 - kx0);
+  g.ny = (int)dims[1];
+  g.nz = (int)dims[2];
+  const int64_t nvox = (int64_t)g.nx * g.ny * g.nz;
+  if (nvox > voxel_cells) return fail(O3DX_ENOMEM, "o3dx_voxel_table_build: table needs %lld voxels", (long long)nvox);
+  hipStream_t s = as_stream(stream);
+  int64_t* cnt = reinterpret_cast<int64_t*>(ws);  // [0] error bits, [1] occupied 2^3 cells
+  O3DX_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(int64_t), s));
+  O3DX_HIP(hipMemsetAsync(voxel_pts, 0xFF, (size_t)nvox * 4 * sizeof(float), s));
+  if (n > 0)
+    hipLaunchKernelGGL(k_table_build, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, g,
+                       reinterpret_cast<float4*>(voxel_pts), reinterpret_cast<int*>(cnt));
+  const int64_t nc2 = (int64_t)((g.nx + 1) / 2) * ((g.ny + 1) / 2) * ((g.nz + 1) / 2);
+  hipLaunchKernelGGL(k_voxel_occ2<float4>, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s,
+                     reinterpret_cast<const float4*>(voxel_pts), g, reinterpret_cast<unsigned long long*>(cnt + 1));
+  O3DX_HIP(hipGetLastError());
+  int64_t c[2];
+  O3DX_TRY(read_back(c, cnt, sizeof(c), s));
+  if (c[0] & 1) return fail(O3DX_EINVAL, "o3dx_voxel_table_build: points outside the window");
+  if (c[0] & 2) return fail(O3DX_EINVAL, "o3dx_voxel_table_build: two points in one voxel");
+  const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny, (double)g.nz,
+                         1.0, (double)c[1], (double)g.kx0, 0.0, (double)nvox};
+  for (int k = 0; k < 12; ++k) geom_host[k] = gv[k];
+  return 0;
 }

@@ -49,6 +49,10 @@ _SIGS = {
     "o3dx_voxel_grid_cells": (_I64, [_I64, _P, _P, _D]),
     "o3dx_voxel_grid_capacity": (_I64, [_I64]),
     "o3dx_voxel_down_sample_grid": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P]),
+    "o3dx_voxel_down_sample_window": (_I32, [_P, _I64, _P, _P, _D, _I64, _I64, _P, _P, _P, _P, _I64, _P, _P, _SZ,
+                                              _P]),
+    "o3dx_voxel_table_workspace_bytes": (_SZ, []),
+    "o3dx_voxel_table_build": (_I32, [_P, _I64, _P, _P, _D, _I64, _I64, _P, _I64, _P, _P, _SZ, _P]),
     "o3dx_normals_workspace_bytes": (_SZ, [_I64]),
     "o3dx_estimate_normals_voxel": (_I32, [_P, _P, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_estimate_normals": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),

@@ -155,7 +155,7 @@ def _exchange(dest: torch.Tensor, world: int, group, *tensors):
 
 
 def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float, knn: int = 30, group=None,
-                        voxel_fn=None, normals_fn=None, halo: Optional[float] = None):
+                        voxel_fn=None, normals_fn=None, halo: Optional[float] = None, presorted: bool = False):
     """C4: voxel_down_sample + estimate_normals(KNN) of one cloud spread over
     the ranks, decomposed into x-slabs aligned to the global voxel grid.
 
@@ -177,9 +177,16 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
     fails it, H doubles and the exchange + normals repeat.  Returns (rep
     global indices ascending, rep xyz, normals) of this rank's slab; the union
     over ranks is the single-GPU result.  Compute defaults to the HIP kernels
-    (ops); tests inject the oracle (normals_fn(p, k) -> (normals, kth_d2))."""
+    (ops); tests inject the oracle (normals_fn(p, k) -> (normals, kth_d2)).
+
+    presorted: the caller guarantees every point already lies in this rank's
+    slab and the rows are in ascending global index (a spatially tiled
+    dataset): the point all-to-all is skipped (a point outside the slab makes
+    the voxel call fail loudly)."""
     from . import ops
 
+    if voxel_fn is None and normals_fn is None and xyz.is_cuda:
+        return _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted)
     world, rank = _world(group)
     if voxel_fn is None:
         def voxel_fn(p, vs, mn, mx):
@@ -250,6 +257,89 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
             break
         H *= 2.0
     return rg, rxyz, nrm[own]
+
+
+def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted):
+    """The HIP form of voxel_normals_slabs: every rank keeps a voxel table of
+    its slab widened by the halo (global keys, x-key window), so the normals
+    run straight off the table (k_normals_stile) on own + halo reps; the halo
+    is a whole number of voxel layers.  Same contract and halo proof."""
+    from . import ops
+
+    world, rank = _world(group)
+    vs = float(voxel_size)
+    # 1. global bounds
+    if xyz.shape[0] > 0:
+        lmn, lmx = ops.aabb(xyz)
+    else:
+        lmn, lmx = np.full(3, np.inf), np.full(3, -np.inf)
+    mn, mx = global_aabb(lmn, lmx, group)
+    keys = slab_bounds(mn, mx, vs, world)
+    k_lo, k_hi, nkeys = keys[rank], keys[rank + 1], keys[-1]
+    # 2. points to their slab owner (unless the input is already tiled)
+    if world > 1 and not presorted:
+        kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+        inner = torch.tensor(keys[1:-1], dtype=torch.int64, device=xyz.device)
+        xyz, gidx = _exchange(torch.searchsorted(inner, kx, right=True), world, group, xyz, gidx)
+        o = torch.argsort(gidx)
+        xyz, gidx = xyz[o].contiguous(), gidx[o].contiguous()
+    # 3. own reps: keys of the global grid, the slab's x keys only
+    if k_hi > k_lo and xyz.shape[0] > 0:
+        out = ops.voxel_down_sample_window(xyz, vs, mn, mx, k_lo, k_hi)
+        rep = out["rep_idx"].long()
+        rxyz, rg = out["rep_xyz"], gidx[rep].contiguous()
+    else:
+        rxyz, rg = xyz[:0], gidx[:0]
+    kxr = torch.floor((rxyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+    x_lo, x_hi = float(mn[0]) + k_lo * vs, float(mn[0]) + k_hi * vs
+    inf = torch.full((rxyz.shape[0],), np.inf, dtype=torch.float64, device=rxyz.device)
+    t = torch.minimum(rxyz[:, 0].double() - x_lo if rank > 0 else inf,
+                      x_hi - rxyz[:, 0].double() if rank < world - 1 else inf)
+    hk = max(1, int(math.ceil(float(halo) / vs))) if halo else 3
+    min_keys = min(keys[r + 1] - keys[r] for r in range(world))
+    n_total = _allreduce_int(rg.numel(), group)
+    table = None
+    while True:
+        if world > 1 and hk >= min_keys:
+            raise RuntimeError("voxel_normals_slabs: the kNN halo is wider than a slab; use fewer ranks")
+        # 4. halo: the own reps of the hk voxel layers next to each interior face
+        if world > 1:
+            send_lo = (kxr < k_lo + hk) & (rank > 0)
+            send_hi = (kxr >= k_hi - hk) & (rank < world - 1)
+            dest = torch.cat([torch.full((int(send_lo.sum()),), rank - 1, dtype=torch.int64, device=rxyz.device),
+                              torch.full((int(send_hi.sum()),), rank + 1, dtype=torch.int64, device=rxyz.device)])
+            hx, hg = _exchange(dest, world, group, torch.cat([rxyz[send_lo], rxyz[send_hi]]),
+                               torch.cat([rg[send_lo], rg[send_hi]]))
+            ux, ug = torch.cat([rxyz, hx]), torch.cat([rg, hg])
+            o = torch.argsort(ug)
+            ux, ug = ux[o].contiguous(), ug[o].contiguous()
+            own = torch.searchsorted(ug, rg)
+        else:
+            ux, ug, own = rxyz, rg, None
+        # 5. the union's voxel table over the slab + halo window, normals off it
+        kx0, kx1 = max(k_lo - hk, 0), min(k_hi + hk, nkeys)
+        if ux.shape[0] > 0:
+            grid = ops.voxel_table(ux, vs, mn, mx, kx0, kx1, table)
+            table = grid.pts
+            nrm, kd2 = ops.estimate_normals(ux, knn=knn, voxel_grid=grid, return_kdist=True)
+        else:
+            nrm, kd2 = ux.new_zeros((0, 3)), ux.new_zeros((0,))
+        if own is not None:
+            nrm, kd2 = nrm[own], kd2[own]
+        # 6. verify every own rep: a missing point lies more than t + hk*vs away
+        ok = 1.0
+        if world > 1 and rg.numel():
+            if ux.shape[0] < min(knn, n_total):
+                ok = 0.0
+            else:
+                ok = 1.0 if bool((torch.sqrt(kd2.double()) < (t + hk * vs) * (1.0 - 1e-9)).all()) else 0.0
+        flag = torch.tensor([ok], dtype=torch.float64, device=_comm_device(group))
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if flag.item() == 1.0:
+            break
+        hk *= 2
+    return rg, rxyz, nrm
 
 
 def _allreduce_int(v: int, group=None) -> int:

@@ -92,6 +92,55 @@ def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_
     return out
 
 
+def voxel_down_sample_window(xyz: torch.Tensor, voxel_size: float, min_bound, max_bound, kx0: int, kx1: int,
+                             keep_grid: bool = False):
+    """Slab form of voxel_down_sample (include/o3dx.h o3dx_voxel_down_sample_window):
+    keys of the GLOBAL min_bound, only the x keys [kx0, kx1) materialised.
+    Returns dict rep_idx, rep_xyz (and voxel_grid if keep_grid)."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    ws = N.workspace(L.o3dx_voxel_workspace_bytes(n), dev)
+    rep = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    rxyz = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev)
+    m = np.zeros(1, np.int64)
+    geom = np.zeros(12, np.float64)
+    cells = int(L.o3dx_voxel_grid_capacity(n)) if keep_grid and n > 0 else 0
+    vox = torch.empty((max(cells, 1), 4), dtype=torch.float32, device=dev) if cells else None
+    N.check(L.o3dx_voxel_down_sample_window(N.ptr(x), n, _np_ptr(_c(min_bound, np.float64)),
+                                            _np_ptr(_c(max_bound, np.float64)), float(voxel_size), int(kx0), int(kx1),
+                                            N.ptr(rep), N.ptr(rxyz), _np_ptr(m), N.ptr(vox), cells, _np_ptr(geom),
+                                            N.ptr(ws), ws.numel(), N.stream_ptr(dev)), "voxel_down_sample_window")
+    M = int(m[0])
+    out = {"rep_idx": rep[:M], "rep_xyz": rxyz[:M]}
+    if keep_grid:
+        out["voxel_grid"] = VoxelGrid(geom, vox, M) if geom[7] == 1.0 else None
+    return out
+
+
+def voxel_table(xyz: torch.Tensor, voxel_size: float, min_bound, max_bound, kx0: int, kx1: int,
+                table: Optional[torch.Tensor] = None):
+    """VoxelGrid of points holding at most one point per voxel (a slab's own +
+    halo representatives), over the x-key window [kx0, kx1) of the global grid
+    (o3dx_voxel_table_build).  `table`: an optional (cells, 4) float32 buffer."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    mnb, mxb = _c(min_bound, np.float64), _c(max_bound, np.float64)
+    dims = np.floor(np.maximum(mxb - mnb, 0.0) / voxel_size) + 1
+    cells = int((kx1 - kx0) * dims[1] * dims[2])
+    if table is None or table.shape[0] < cells:
+        table = torch.empty((cells, 4), dtype=torch.float32, device=dev)
+    geom = np.zeros(12, np.float64)
+    ws = N.workspace(L.o3dx_voxel_table_workspace_bytes(), dev, "table")
+    N.check(L.o3dx_voxel_table_build(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), int(kx0), int(kx1),
+                                     N.ptr(table), table.shape[0], _np_ptr(geom), N.ptr(ws), ws.numel(),
+                                     N.stream_ptr(dev)), "voxel_table")
+    return VoxelGrid(geom, table, n)
+
+
 class VoxelGrid:
     """The voxel table of a voxel_down_sample(keep_grid=True): per voxel the
     representative's (x, y, z, output row) (row -1 empty) + the grid geometry.

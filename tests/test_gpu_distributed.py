@@ -115,3 +115,34 @@ def test_kdist_bound_is_an_upper_bound(dev):
         kd2 = kd2.cpu().numpy().astype(np.float64)
         assert np.all(kd2 >= exact)
         assert np.all(kd2 <= exact * 1.01)
+
+
+def _c4_presorted_rank(rank, world):
+    dev = torch.device("cuda:0")
+    n = 1_000_000
+    vs = S.voxel_size_for(n)
+    pts = S.uniform_cube(n, 44).to(dev)
+    mn, mx = ops.aabb(pts)
+    keys = D.slab_bounds(mn, mx, vs, world)
+    kx = torch.floor((pts[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+    g = torch.nonzero((kx >= keys[rank]) & (kx < keys[rank + 1])).flatten()
+    rg, rx, nrm = D.voxel_normals_slabs(pts[g].contiguous(), g, vs, knn=30, presorted=True)
+    return rg, nrm
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_slabs_presorted_on_device(world):
+    """The bench's C4 step (points already in their slabs, voxel-table normals
+    on own + halo reps): reps and normals bit-identical to one GPU's."""
+    res = spawn(_c4_presorted_rank, world=world)
+    dev = torch.device("cuda:0")
+    n = 1_000_000
+    vs = S.voxel_size_for(n)
+    pts = S.uniform_cube(n, 44).to(dev)
+    out = ops.voxel_down_sample(pts, vs, keep_grid=True)
+    ref = ops.estimate_normals(out["rep_xyz"], knn=30, voxel_grid=out["voxel_grid"]).cpu().numpy()
+    g = np.concatenate([r[0] for r in res])
+    nn = np.concatenate([r[1] for r in res])
+    o = np.argsort(g)
+    assert np.array_equal(g[o], out["rep_idx"].cpu().numpy().astype(np.int64))
+    assert np.array_equal(nn[o], ref)
