@@ -283,9 +283,18 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
         xyz, gidx = _exchange(torch.searchsorted(inner, kx, right=True), world, group, xyz, gidx)
         o = torch.argsort(gidx)
         xyz, gidx = xyz[o].contiguous(), gidx[o].contiguous()
-    # 3. own reps: keys of the global grid, the slab's x keys only
-    if k_hi > k_lo and xyz.shape[0] > 0:
-        out = ops.voxel_down_sample_window(xyz, vs, mn, mx, k_lo, k_hi)
+    # 3. own reps: keys of the global grid, the slab's x keys only (a dense
+    # window table when the slab is not sparse — the same rule as the
+    # library's dense voxel table, 2n + 2^20 cells — else the hash path)
+    dims = np.floor(np.maximum(np.asarray(mx) - np.asarray(mn), 0.0) / vs) + 1
+    layer = int(dims[1] * dims[2])
+    n_loc = int(xyz.shape[0])
+    dense = (k_hi - k_lo + 6) * layer <= 2 * n_loc + (1 << 20)
+    if k_hi > k_lo and n_loc > 0:
+        if dense:
+            out = ops.voxel_down_sample_window(xyz, vs, mn, mx, k_lo, k_hi)
+        else:
+            out = ops.voxel_down_sample(xyz, vs, mn, mx)
         rep = out["rep_idx"].long()
         rxyz, rg = out["rep_xyz"], gidx[rep].contiguous()
     else:
@@ -318,10 +327,12 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
             ux, ug, own = rxyz, rg, None
         # 5. the union's voxel table over the slab + halo window, normals off it
         kx0, kx1 = max(k_lo - hk, 0), min(k_hi + hk, nkeys)
-        if ux.shape[0] > 0:
+        if ux.shape[0] > 0 and (kx1 - kx0) * layer <= 2 * int(ux.shape[0]) + (1 << 20):
             grid = ops.voxel_table(ux, vs, mn, mx, kx0, kx1, table)
             table = grid.pts
             nrm, kd2 = ops.estimate_normals(ux, knn=knn, voxel_grid=grid, return_kdist=True)
+        elif ux.shape[0] > 0:  # sparse slab: the normals sort the union into their own grid
+            nrm, kd2 = ops.estimate_normals(ux, knn=knn, return_kdist=True)
         else:
             nrm, kd2 = ux.new_zeros((0, 3)), ux.new_zeros((0,))
         if own is not None:
