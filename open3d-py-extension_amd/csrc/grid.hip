@@ -1108,12 +1108,30 @@ constexpr double kStencilR = 2.45;         // completeness radius (voxels)
   X(-1, 2, -2, 3) X(0, 2, -2, 3) X(1, 2, -2, 3) X(2, 2, -2, 3) X(3, 2, -1, 2) X(-1, 3, -1, 2)                \
   X(0, 3, -1, 2) X(1, 3, -1, 2) X(2, 3, -1, 2)
 
+// Symmetric stencil (no per-lane mirroring): the 179 voxels whose gap to the
+// query's own voxel is at most 2 voxels in the squared sense (gx^2 + gy^2 +
+// gz^2 <= 4, g = max(0, |d| - 1) per axis) — every point closer than sqrt(5)
+// voxels to any query in the voxel.  37 rows (dy, dz, x0, x1), identical for
+// every lane, so a wave's lanes read one padded box layout at lane-distinct
+// banks (see StileShape).  Generated like tools/stencil_rows.py.
+#define O3DX_SYM_ROWS(X)                                                                                    \
+  X(-1, -3, -1, 1) X(0, -3, -1, 1) X(1, -3, -1, 1) X(-2, -2, -2, 2) X(-1, -2, -2, 2) X(0, -2, -2, 2)        \
+  X(1, -2, -2, 2) X(2, -2, -2, 2) X(-3, -1, -1, 1) X(-2, -1, -2, 2) X(-1, -1, -3, 3) X(0, -1, -3, 3)       \
+  X(1, -1, -3, 3) X(2, -1, -2, 2) X(3, -1, -1, 1) X(-3, 0, -1, 1) X(-2, 0, -2, 2) X(-1, 0, -3, 3)          \
+  X(0, 0, -3, 3) X(1, 0, -3, 3) X(2, 0, -2, 2) X(3, 0, -1, 1) X(-3, 1, -1, 1) X(-2, 1, -2, 2)              \
+  X(-1, 1, -3, 3) X(0, 1, -3, 3) X(1, 1, -3, 3) X(2, 1, -2, 2) X(3, 1, -1, 1) X(-2, 2, -2, 2)              \
+  X(-1, 2, -2, 2) X(0, 2, -2, 2) X(1, 2, -2, 2) X(2, 2, -2, 2) X(-1, 3, -1, 1) X(0, 3, -1, 1)              \
+  X(1, 3, -1, 1)
+constexpr double kSymR2 = 5.0;  // completeness radius^2 of the symmetric stencil (voxels^2)
+
 struct DenseVox {
   const float4* __restrict__ vox;  // (x, y, z, bits(row)), row -1 = empty (0xFF fill: NaN coordinates)
   int nx, ny, nz;                  // voxel dims
   int nbx, nby, nbz;               // 4^3 blocks
   float ox, oy, oz, vs, inv_vs;
   float rc2;                       // completeness radius^2 (world, float32, shrunk by the slack)
+  float rc2w;                      // the same with the symmetric stencil's ring
+  float rt2;                       // k_normals_vlist: the list threshold (<= rc2)
   unsigned long long* stats;       // debug counters (o3dx_search_stats) or null
   int32_t* nbr;                    // test hook (o3dx_set_debug_neighbors) or null
   float* kd2;                      // per row an upper bound of the k-th neighbour d^2, or null
@@ -1168,15 +1186,101 @@ __device__ __forceinline__ void stencil_scan(const float2* txy, const float* tz,
 #undef O3DX_ROW
 }
 
+// The symmetric stencil, compile-time strides: every lane reads the same
+// offsets from its own slot.  Software-pipelined by one row: row i+1's LDS
+// loads are issued before row i's distances (two register buffers of one
+// row), with a scheduling fence per row.  RING: the 72 voxels at gap^2 == 5
+// (56 short rows) that extend the completeness radius to sqrt 6 for the
+// lanes whose k-th neighbour lies beyond sqrt 5 (cloud borders).
+struct SRow {
+  int dy, dz, xa, len;
+};
+#define O3DX_SROW(DY, DZ, XA, XB) SRow{DY, DZ, XA, (XB) - (XA) + 1},
+constexpr SRow kSymRows[] = {O3DX_SYM_ROWS(O3DX_SROW)};
+#undef O3DX_SROW
+constexpr SRow kRingRows[] = {
+    {-2, -3, -1, 3}, {-1, -3, -2, 1}, {-1, -3, 2, 1}, {0, -3, -2, 1},  {0, -3, 2, 1},  {1, -3, -2, 1},
+    {1, -3, 2, 1},   {2, -3, -1, 3},  {-3, -2, -1, 3}, {-1, -2, -3, 1}, {-1, -2, 3, 1}, {0, -2, -3, 1},
+    {0, -2, 3, 1},   {1, -2, -3, 1},  {1, -2, 3, 1},  {3, -2, -1, 3},  {-3, -1, -2, 1}, {-3, -1, 2, 1},
+    {-2, -1, -3, 1}, {-2, -1, 3, 1},  {2, -1, -3, 1},  {2, -1, 3, 1},   {3, -1, -2, 1},  {3, -1, 2, 1},
+    {-3, 0, -2, 1},  {-3, 0, 2, 1},   {-2, 0, -3, 1},  {-2, 0, 3, 1},   {2, 0, -3, 1},   {2, 0, 3, 1},
+    {3, 0, -2, 1},   {3, 0, 2, 1},    {-3, 1, -2, 1},  {-3, 1, 2, 1},   {-2, 1, -3, 1},  {-2, 1, 3, 1},
+    {2, 1, -3, 1},   {2, 1, 3, 1},    {3, 1, -2, 1},   {3, 1, 2, 1},    {-3, 2, -1, 3},  {-1, 2, -3, 1},
+    {-1, 2, 3, 1},   {0, 2, -3, 1},   {0, 2, 3, 1},    {1, 2, -3, 1},   {1, 2, 3, 1},    {3, 2, -1, 3},
+    {-2, 3, -1, 3},  {-1, 3, -2, 1},  {-1, 3, 2, 1},   {0, 3, -2, 1},   {0, 3, 2, 1},    {1, 3, -2, 1},
+    {1, 3, 2, 1},    {2, 3, -1, 3}};
+constexpr double kSymWideR2 = 6.0;  // completeness radius^2 with the ring (voxels^2)
+constexpr int kRowMax = 7;
+
+template <bool RING>
+struct SymRows {
+  static constexpr int N = RING ? (int)(sizeof(kRingRows) / sizeof(SRow)) : (int)(sizeof(kSymRows) / sizeof(SRow));
+  static constexpr SRow at(int i) { return RING ? kRingRows[i] : kSymRows[i]; }
+};
+
+struct RowBuf {
+  float2 a[kRowMax];
+  float c[kRowMax];
+};
+
+template <bool RING, int I, int SY, int SZ>
+__device__ __forceinline__ RowBuf sym_load(const float2* txy, const float* tz, int qs) {
+  constexpr SRow r = SymRows<RING>::at(I);
+  constexpr int off = r.dy * SY + r.dz * SZ + r.xa;
+  RowBuf b;
+#pragma unroll
+  for (int i = 0; i < r.len; ++i) {
+    b.a[i] = txy[qs + off + i];
+    b.c[i] = tz[qs + off + i];
+  }
+  return b;
+}
+
+template <bool RING, int I, int SY, int SZ, class F>
+__device__ __forceinline__ void sym_rows(const float2* txy, const float* tz, int qs, const float4 q, RowBuf cur,
+                                         F& f) {
+  if constexpr (I < SymRows<RING>::N) {
+    RowBuf nxt;
+    if constexpr (I + 1 < SymRows<RING>::N) nxt = sym_load<RING, I + 1, SY, SZ>(txy, tz, qs);
+    constexpr SRow r = SymRows<RING>::at(I);
+    constexpr int off = r.dy * SY + r.dz * SZ + r.xa;
+#pragma unroll
+    for (int i = 0; i + 1 < r.len; i += 2) {
+      const f32x2 dd = dist2_pair(q, (f32x2){cur.a[i].x, cur.a[i + 1].x}, (f32x2){cur.a[i].y, cur.a[i + 1].y},
+                                  (f32x2){cur.c[i], cur.c[i + 1]});
+      f(qs + off + i, dd.x);
+      f(qs + off + i + 1, dd.y);
+    }
+    if constexpr (r.len & 1) f(qs + off + r.len - 1, dist2_f32(q, cur.a[r.len - 1].x, cur.a[r.len - 1].y, cur.c[r.len - 1]));
+    __builtin_amdgcn_sched_barrier(0);
+    sym_rows<RING, I + 1, SY, SZ>(txy, tz, qs, q, nxt, f);
+  }
+}
+
+template <bool RING, int SY, int SZ, class F>
+__device__ __forceinline__ void stencil_scan_sym(const float2* txy, const float* tz, int qs, const float4 q, F&& f) {
+  asm volatile("" : "+v"(qs));
+  sym_rows<RING, 0, SY, SZ>(txy, tz, qs, q, sym_load<RING, 0, SY, SZ>(txy, tz, qs), f);
+}
+
 // Block shapes: WY x WZ waves, each wave a 4^3 voxel block; the block's box is
 // the union (4 x 4WY x 4WZ voxels + the 3-voxel margin), staged once for all
 // its waves — 2x2 waves stage 7.7 slots per query instead of 15.6 and fit
 // 3 blocks (12 waves) per CU in LDS instead of 8 single-wave blocks.
-template <int WY, int WZ>
+// PAD (the symmetric stencil's layout): row pitch 12 slots and a plane pitch
+// = 16 (mod 32) slots, so for any stencil offset the 16 lanes (lx, ly) of one
+// z layer hit 16 distinct float2 bank pairs (2 (lx + 12 ly) mod 32 distinct:
+// ds_read2_b64's 4 x 16 groups) and the 32 lanes of two layers 32 distinct
+// float banks (lx + 12 ly + 16 lz mod 32: ds_read_b32's 2 x 32 groups).
+template <int WY, int WZ, bool PAD = false>
 struct StileShape {
   static constexpr int NW = WY * WZ;
   static constexpr int EY = kVB * WY + 2 * kVM, EZ = kVB * WZ + 2 * kVM;
-  static constexpr int SY = kVE, SZ = kVE * EY, SLOTS = kVE * EY * EZ;
+  static constexpr int SY = PAD ? 12 : kVE;
+  static constexpr int SZ = PAD ? SY * EY + (48 - (SY * EY) % 32) % 32 : kVE * EY;
+  static constexpr int CELLS = kVE * EY * EZ;  // logical box cells
+  static constexpr int SLOTS = SZ * EZ;        // LDS slots (padded)
+  static_assert(!PAD || SZ % 32 == 16, "plane pitch must be 16 mod 32");
 };
 
 // MERGED: the histogram pass also appends every candidate below T2 = 3/4 R2 to
@@ -1188,16 +1292,19 @@ constexpr int kMergedCap = 56;
 constexpr float kMergedFrac = 0.75f;
 
 // WPE: waves per SIMD to register-allocate for (LDS allows 2 for 1x1, 3 for 2x2)
-template <int KMAX, int WY, int WZ, int WPE, bool MERGED>
+template <int KMAX, int WY, int WZ, int WPE, bool MERGED, bool SYM>
 __global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
                 int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
-  using Sh = StileShape<WY, WZ>;
+  using Sh = StileShape<WY, WZ, SYM>;
   constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::SLOTS;
   __shared__ float2 txy[kSlots];
   __shared__ float tz[kSlots];
-  constexpr int kListMax = KMAX + kBndCap;
-  constexpr int kListRows = MERGED && kMergedCap > kListMax ? kMergedCap + 1 : kListMax + 4;
+  // list capacity: the k - 1 points below the k-th bin + that bin (<= kRefineAt
+  // after refinement) + the rounding band; the symmetric layout trims it to
+  // KMAX + 12 so three 2x2 workgroups still fit a CU's LDS
+  constexpr int kListMax = KMAX + (SYM ? 12 : kBndCap);
+  constexpr int kListRows = MERGED && kMergedCap > kListMax ? kMergedCap + 1 : kListMax + 1;
   constexpr int kListWords = (kListRows * 64 * 2 + 3) / 4;
   constexpr int kHistWords = kTileSlots * 64;
   constexpr int kSelWords = MERGED ? kListWords : (kListWords > kHistWords ? kListWords : kHistWords);
@@ -1212,19 +1319,21 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   const int gx0 = bx * kVB - kVM, gy0 = by * (kVB * WY) - kVM, gz0 = bz * (kVB * WZ) - kVM;  // box origin
   {
     constexpr int kT = 64 * Sh::NW;
-    constexpr int J = (kSlots + kT - 1) / kT;
+    constexpr int kCells = Sh::CELLS;
+    constexpr int J = (kCells + kT - 1) / kT;
     float4 buf[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int t = threadIdx.x + kT * j;
-      if (t < kSlots) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kSY) % Sh::EY, gz0 + t / kSZ);
+      if (t < kCells) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kVE) % Sh::EY, gz0 + t / (kVE * Sh::EY));
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int t = threadIdx.x + kT * j;
-      if (t < kSlots) {
-        txy[t] = make_float2(buf[j].x, buf[j].y);
-        tz[t] = buf[j].z;
+      if (t < kCells) {
+        const int a = t % kVE + kSY * ((t / kVE) % Sh::EY) + kSZ * (t / (kVE * Sh::EY));
+        txy[a] = make_float2(buf[j].x, buf[j].y);
+        tz[a] = buf[j].z;
       }
     }
   }
@@ -1247,22 +1356,32 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
     return;
   }
   if (!fb) {
-    const float R2 = d.rc2;
+    float R2 = d.rc2;
     const float T2 = R2 * kMergedFrac;
     int nl = 0;  // MERGED: candidates below T2 appended by the first pass
+    bool wide = false;  // SYM: the gap^2 == 5 ring is scanned too (k-th neighbour beyond sqrt 5)
+    auto scan = [&](auto&& body) {
+      if constexpr (SYM) {
+        stencil_scan_sym<false, kSY, kSZ>(txy, tz, qs, q, body);
+        if (wide) stencil_scan_sym<true, kSY, kSZ>(txy, tz, qs, q, body);
+      } else {
+        stencil_scan(txy, tz, qs, SY, SZ, xpos, q, body);
+      }
+    };
     TileHist th;
     auto hist = [&](float lo_, float sc_, auto app) {
 #pragma unroll
       for (int i = 0; i < kTileSlots; ++i) hw[i * 64 + lane] = 0u;
       const float off_ = -lo_ * sc_;
-      stencil_scan(txy, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
+      auto body = [&](int pp, float d2) {
         const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f);
         atomicAdd(&hw[(ix + 1) * 64 + lane], 1u);
         if constexpr (decltype(app)::value) {
           lst[min(nl, kMergedCap)][lane] = (uint16_t)pp;
           nl += d2 < T2 ? 1 : 0;
         }
-      });
+      };
+      scan(body);
 #pragma unroll
       for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
     };
@@ -1270,6 +1389,14 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
     int total = 0;
 #pragma unroll
     for (int i = 0; i < kHistBins; ++i) total += th.count(i);
+    if (SYM && !MERGED && total < kneed) {  // border lanes: widen to the ring (sqrt 6)
+      wide = true;
+      R2 = d.rc2w;
+      hist(0.0f, (float)kHistBins / R2, std::false_type{});
+      total = 0;
+#pragma unroll
+      for (int i = 0; i < kHistBins; ++i) total += th.count(i);
+    }
     fb = total < kneed;
     if (fb && d.stats) atomicAdd(&d.stats[7], 1ull);
     float lo = 0.f, hi = R2, L = 0.f, U = 0.f;
@@ -1297,12 +1424,13 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
       if (!have) {
         n = 0;
         cap = kListMax;
-        stencil_scan(txy, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) {
+        auto body = [&](int pp, float d2) {
           if (d2 < Up) {  // masked store: only the accepted lanes take part in the LDS banking
             lst[min(n, kListMax)][lane] = (uint16_t)pp;
             ++n;
           }
-        });
+        };
+        scan(body);
       }
       if (dbg == 3) {
         if (n == 12345) out[0] = 0.f;
@@ -1314,7 +1442,7 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
                q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(txy[p].x, txy[p].y, tz[p], 0.f); }, prior,
                oi, out, d.nbr,
                [&](int p) {
-                 const int bx = p % kVE, by = (p / kSY) % Sh::EY, bz = p / kSZ;
+                 const int bz = p / kSZ, r = p - bz * kSZ, by = r / kSY, bx = r - by * kSY;
                  return __float_as_int(
                      d.vox[(gx0 + bx) + (int64_t)d.nx * ((gy0 + by) + (int64_t)d.ny * (gz0 + bz))].w);
                },
@@ -1328,6 +1456,286 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// KNN normals off the dense voxel table, list-first form (k_normals_vlist).
+//
+// The staged box and the stencils are those of k_normals_stile; the selection
+// is reordered so the per-candidate work is one scan instead of two, and the
+// LDS histogram atomics (the count pass' cost) run over a short list instead
+// of the whole stencil:
+//   1. scan — every stencil candidate with f32 d^2 < T (T = (1.14 x the
+//      expected k-th distance)^2, below the stencil's completeness radius) is
+//      appended to the lane's list as its 1-byte stencil position; at one rep
+//      per voxel that is ~1.5 k entries (<= kVCap).  The set {d^2 < T} is
+//      complete, so with >= k entries it contains the k nearest;
+//   2. lanes with fewer than k entries (cloud borders) rescan with T = the
+//      completeness radius (the symmetric stencil adds its ring); lanes still
+//      short, or over the cap, hand off to the wave form;
+//   3. select — a 16-bin histogram of the list over [0, T) (packed 8-bit LDS
+//      counters, one dword column per lane), locate / refine over the list;
+//   4. finish_selection over the list (exact f64 (d^2, index) order at the
+//      band), f64 moments, FastEigen3x3 — as the other forms.
+// Stencil position -> LDS slot through a 1-KB table staged per workgroup.
+constexpr int kVCap = 63;     // list capacity (entries); 64 rows of u8
+constexpr int kPHWords = 5;   // packed histogram: 18 slots x 8 bit
+
+#define O3DX_SROW2(DY, DZ, XA, XB) SRow{DY, DZ, XA, (XB) - (XA) + 1},
+constexpr SRow kMirRows[] = {O3DX_S25_ROWS(O3DX_SROW2)};
+#undef O3DX_SROW2
+
+// S: 0 = mirrored 172-voxel stencil, 1 = symmetric 179, 2 = symmetric + ring (251)
+template <int S>
+struct StDef {
+  static constexpr int NM = (int)(sizeof(kMirRows) / sizeof(SRow));
+  static constexpr int NS = (int)(sizeof(kSymRows) / sizeof(SRow));
+  static constexpr int NR = (int)(sizeof(kRingRows) / sizeof(SRow));
+  static constexpr int N = S == 0 ? NM : S == 1 ? NS : NS + NR;
+  static constexpr SRow at(int i) { return S == 0 ? kMirRows[i] : (i < NS ? kSymRows[i] : kRingRows[i - NS]); }
+  static constexpr int pos0(int i) {
+    int p = 0;
+    for (int j = 0; j < i; ++j) p += at(j).len;
+    return p;
+  }
+  static constexpr int NPOS = pos0(N);
+};
+
+// Position table: symmetric stencils -> the slot offset at the padded layout
+// (SY, SZ); mirrored -> (dy, dz, x) as signed bytes, the lane applies its signs.
+template <int S, int SY, int SZ>
+struct PosTab {
+  int32_t v[StDef<S>::NPOS];
+};
+template <int S, int SY, int SZ>
+constexpr PosTab<S, SY, SZ> make_postab() {
+  PosTab<S, SY, SZ> t{};
+  int p = 0;
+  for (int i = 0; i < StDef<S>::N; ++i) {
+    const SRow r = StDef<S>::at(i);
+    for (int x = r.xa; x < r.xa + r.len; ++x, ++p) {
+      if (S == 0)
+        t.v[p] = (int32_t)((uint32_t)(r.dy & 0xff) | ((uint32_t)(r.dz & 0xff) << 8) | ((uint32_t)(x & 0xff) << 16));
+      else
+        t.v[p] = r.dy * SY + r.dz * SZ + x;
+    }
+  }
+  return t;
+}
+template <int S, int SY, int SZ>
+__constant__ PosTab<S, SY, SZ> c_postab = make_postab<S, SY, SZ>();
+
+// the lane's stencil frame: own slot + (mirrored stencil) signed strides
+struct LaneFrame {
+  int qs, sy, sz;
+  bool xpos;
+};
+
+template <int S, int I, int SY, int SZ>
+__device__ __forceinline__ int st_row_start(const LaneFrame& fr) {
+  constexpr SRow r = StDef<S>::at(I);
+  if constexpr (S == 0) return fr.qs + r.dy * fr.sy + r.dz * fr.sz + (fr.xpos ? r.xa : -(r.xa + r.len - 1));
+  else return fr.qs + r.dy * SY + r.dz * SZ + r.xa;
+}
+
+template <int S, int I, int SY, int SZ>
+__device__ __forceinline__ RowBuf st_load(const float2* txy, const float* tz, const LaneFrame& fr) {
+  constexpr SRow r = StDef<S>::at(I);
+  const int st = st_row_start<S, I, SY, SZ>(fr);
+  RowBuf b;
+#pragma unroll
+  for (int i = 0; i < r.len; ++i) {
+    b.a[i] = txy[st + i];
+    b.c[i] = tz[st + i];
+  }
+  return b;
+}
+
+// f(position, d2) over rows [I, END) of stencil S, pipelined by one row
+template <int S, int I, int END, int SY, int SZ, class F>
+__device__ __forceinline__ void st_rows(const float2* txy, const float* tz, const LaneFrame& fr, const float4 q,
+                                        RowBuf cur, F& f) {
+  if constexpr (I < END) {
+    RowBuf nxt;
+    if constexpr (I + 1 < END) nxt = st_load<S, I + 1, SY, SZ>(txy, tz, fr);
+    constexpr SRow r = StDef<S>::at(I);
+    constexpr int p0 = StDef<S>::pos0(I);
+    auto pos = [&](int i) { return (S == 0 && !fr.xpos) ? p0 + r.len - 1 - i : p0 + i; };
+#pragma unroll
+    for (int i = 0; i + 1 < r.len; i += 2) {
+      const f32x2 dd = dist2_pair(q, (f32x2){cur.a[i].x, cur.a[i + 1].x}, (f32x2){cur.a[i].y, cur.a[i + 1].y},
+                                  (f32x2){cur.c[i], cur.c[i + 1]});
+      f(pos(i), dd.x);
+      f(pos(i + 1), dd.y);
+    }
+    if constexpr (r.len & 1) f(pos(r.len - 1), dist2_f32(q, cur.a[r.len - 1].x, cur.a[r.len - 1].y, cur.c[r.len - 1]));
+    __builtin_amdgcn_sched_barrier(0);
+    st_rows<S, I + 1, END, SY, SZ>(txy, tz, fr, q, nxt, f);
+  }
+}
+
+template <int S, int BEGIN, int END, int SY, int SZ, class F>
+__device__ __forceinline__ void st_scan(const float2* txy, const float* tz, LaneFrame fr, const float4 q, F&& f) {
+  asm volatile("" : "+v"(fr.qs), "+v"(fr.sy), "+v"(fr.sz));  // row bases recomputed per scan
+  st_rows<S, BEGIN, END, SY, SZ>(txy, tz, fr, q, st_load<S, BEGIN, SY, SZ>(txy, tz, fr), f);
+}
+
+template <int KMAX, int WY, int WZ, int WPE, bool SYM>
+__global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_normals_vlist(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
+                int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb) {
+  using Sh = StileShape<WY, WZ, SYM>;
+  constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::SLOTS;
+  constexpr int S0 = SYM ? 1 : 0;              // the scan's stencil
+  constexpr int SW = SYM ? 2 : 0;              // the border rescan's stencil
+  constexpr int NPOS = StDef<SW>::NPOS;        // the position table covers both
+  static_assert(NPOS <= 256, "u8 stencil positions");
+  __shared__ float2 txy[kSlots];
+  __shared__ float tz[kSlots];
+  __shared__ int32_t ptab[NPOS];
+  __shared__ uint8_t lists[Sh::NW][kVCap + 1][64];
+  __shared__ uint32_t hists[Sh::NW][kPHWords * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint8_t(*l8)[64] = lists[wv];
+  uint32_t* hw = hists[wv];
+  const int nb = d.nbx * d.nby * d.nbz;
+  const int b = xcd_block(blockIdx.x, nb);
+  const int bx = b % d.nbx, by = (b / d.nbx) % d.nby, bz = b / (d.nbx * d.nby);
+  const int gx0 = bx * kVB - kVM, gy0 = by * (kVB * WY) - kVM, gz0 = bz * (kVB * WZ) - kVM;  // box origin
+  {
+    constexpr int kT = 64 * Sh::NW;
+    constexpr int kCells = Sh::CELLS;
+    constexpr int J = (kCells + kT - 1) / kT;
+    float4 buf[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int t = threadIdx.x + kT * j;
+      if (t < kCells) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kVE) % Sh::EY, gz0 + t / (kVE * Sh::EY));
+    }
+    for (int t = threadIdx.x; t < NPOS; t += kT) ptab[t] = c_postab<SW, kSY, kSZ>.v[t];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int t = threadIdx.x + kT * j;
+      if (t < kCells) {
+        const int a = t % kVE + kSY * ((t / kVE) % Sh::EY) + kSZ * (t / (kVE * Sh::EY));
+        txy[a] = make_float2(buf[j].x, buf[j].y);
+        tz[a] = buf[j].z;
+      }
+    }
+  }
+  __syncthreads();
+  const int lx = lane & 3, ly = ((lane >> 2) & 3) + kVB * (wv % WY), lz = (lane >> 4) + kVB * (wv / WY);
+  LaneFrame fr;
+  fr.qs = (lx + kVM) + kSY * (ly + kVM) + kSZ * (lz + kVM);
+  const float4 q = make_float4(txy[fr.qs].x, txy[fr.qs].y, tz[fr.qs], 0.0f);
+  if (!(q.x < INFINITY)) return;  // empty voxel or outside the grid: no query (no barrier follows)
+  const int vx = gx0 + kVM + lx, vy = gy0 + kVM + ly, vz = gz0 + kVM + lz;
+  const int64_t vq = vx + (int64_t)d.nx * (vy + (int64_t)d.ny * vz);
+  const int oi = __float_as_int(d.vox[vq].w);
+  if constexpr (!SYM) {  // orientation: the half of its voxel the query lies in, per axis
+    fr.xpos = (q.x - (d.ox + (float)vx * d.vs)) * d.inv_vs >= 0.5f;
+    fr.sy = (q.y - (d.oy + (float)vy * d.vs)) * d.inv_vs >= 0.5f ? kSY : -kSY;
+    fr.sz = (q.z - (d.oz + (float)vz * d.vs)) * d.inv_vs >= 0.5f ? kSZ : -kSZ;
+  } else {
+    fr.xpos = true;
+    fr.sy = kSY;
+    fr.sz = kSZ;
+  }
+  // stencil position -> LDS slot
+  auto slot_of = [&](int p) {
+    const int32_t t = ptab[p];
+    if constexpr (SYM) {
+      return fr.qs + t;
+    } else {
+      const int dy = (int)(int8_t)(t & 0xff), dz = (int)(int8_t)((t >> 8) & 0xff), x = (int)(int8_t)((t >> 16) & 0xff);
+      return fr.qs + __mul24(dy, fr.sy) + __mul24(dz, fr.sz) + (fr.xpos ? x : -x);
+    }
+  };
+  bool fb = force_fb != 0;  // force_fb: tests of the hand-off path
+  float T = d.rt2;
+  int n = 0;
+  if (!fb) {
+    auto app = [&](int p, float d2) {
+      if (d2 < T) {  // masked store: only the accepting lanes take part
+        l8[min(n, kVCap)][lane] = (uint8_t)p;
+        ++n;
+      }
+    };
+    st_scan<S0, 0, StDef<S0>::N, kSY, kSZ>(txy, tz, fr, q, app);
+    if (n < kneed) {  // cloud borders: the complete stencil (+ its ring)
+      T = SYM ? d.rc2w : d.rc2;
+      n = 0;
+      st_scan<SW, 0, StDef<SW>::N, kSY, kSZ>(txy, tz, fr, q, app);
+    }
+    fb = n < kneed || n > kVCap;
+    if (fb && d.stats) atomicAdd(&d.stats[n < kneed ? 7 : 5], 1ull);
+  }
+  float L = 0.f, U = 0.f;
+  if (!fb) {
+    // histogram of the list over [lo, hi) (packed 8-bit counters; <= kVCap entries)
+    TileHist th;
+    auto list_hist = [&](float lo_, float hi_) {
+      const float sc_ = (float)kHistBins / (hi_ - lo_), off_ = -lo_ * sc_;
+#pragma unroll
+      for (int w = 0; w < kPHWords; ++w) hw[w * 64 + lane] = 0u;
+      for (int j = 0; j < n; j += 4) {
+        int sl[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sl[u] = slot_of(l8[min(j + u, n - 1)][lane]);
+        float2 a[4];
+        float c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a[u] = txy[sl[u]];
+          c[u] = tz[sl[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j + u < n) {
+            const float d2 = dist2_f32(q, a[u].x, a[u].y, c[u]);  // the scan's value, bit for bit
+            const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f) + 1;
+            atomicAdd(&hw[(ix >> 2) * 64 + lane], 1u << ((ix & 3) << 3));
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kTileSlots; ++i) th.h[i] = (hw[(i >> 2) * 64 + lane] >> ((i & 3) << 3)) & 0xffu;
+    };
+    list_hist(0.0f, T);
+    float lo = 0.f, hi = T;
+    for (int lvl = 0;; ++lvl) {
+      int cum, cb;
+      if (!hist_locate(th, kneed, th.count(-1), lo, hi, &L, &U, &cum, &cb)) {
+        fb = true;
+        break;
+      }
+      if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
+      lo = L;
+      hi = U;
+      list_hist(lo, hi);
+    }
+  }
+  if (!fb) {
+    const float Lm = L * (1.0f - 2.0f * kRelEps);
+    fb = !finish_selection<KMAX>(
+        q, kneed, n, Lm, U, l8, lane,
+        [&](int p) {
+          const int sl = slot_of(p);
+          return make_float4(txy[sl].x, txy[sl].y, tz[sl], 0.f);
+        },
+        prior, oi, out, d.nbr,
+        [&](int p) {
+          const int sl = slot_of(p);
+          const int bz = sl / kSZ, r = sl - bz * kSZ, by = r / kSY, bx = r - by * kSY;
+          return __float_as_int(d.vox[(gx0 + bx) + (int64_t)d.nx * ((gy0 + by) + (int64_t)d.ny * (gz0 + bz))].w);
+        },
+        d.kd2);
+  }
+  if (fb) {
+    if (d.stats) atomicAdd(&d.stats[4], 1ull);
+    const int at = atomicAdd(fb_len, 1);
+    fb_list[at] = (int32_t)vq;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // KNN normals, wave-per-query form (second level: the queries the tiles hand
@@ -1897,8 +2305,19 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
     maxext = std::max(maxext, ext);
   }
   const double slack = 32.0 * std::ldexp(1.0, -24) * (maxabs + maxext) + 1e-6 * geom[3];
-  const double R = kStencilR * geom[3] - slack;
+  // stencil (O3DX_STILE_STENCIL): "mirror" — 172 voxels mirrored per lane to
+  // the query's half of its voxel (R = 2.45 voxels); "sym" — the 179 voxels at
+  // gap^2 <= 4 (R = sqrt 5), the same for every lane
+  const char* st_env = getenv("O3DX_STILE_STENCIL");
+  const bool sym = st_env && std::string(st_env) == "sym";
+  const double R = (sym ? std::sqrt(kSymR2) : kStencilR) * geom[3] - slack;
   d.rc2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
+  const double Rw = std::sqrt(kSymWideR2) * geom[3] - slack;
+  d.rc2w = (float)(Rw * Rw) * (1.0f - 4.0f * kRelEps);
+  // list threshold: 1.14 x the expected k-th distance (kth voxels, from the
+  // occupancy), never beyond the stencil's completeness radius
+  const double Rt = std::min(1.14 * kth * geom[3], R);
+  d.rt2 = (float)(Rt * Rt) * (1.0f - 4.0f * kRelEps);
   d.stats = search_stats_ptr();
   d.nbr = debug_nbr(kneed, n);
   d.kd2 = kd2;
@@ -1917,12 +2336,27 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
       const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
       const char* mg = getenv("O3DX_STILE_MERGED");
       const bool merged = mg && atoi(mg) != 0;
-#define O3DX_STILE_LAUNCH2(WY, WZ, WPE, MG)                                                                  \
-  hipLaunchKernelGGL((k_normals_stile<32, WY, WZ, WPE, MG>), dim3((unsigned)nb), dim3(64 * WY * WZ), 0, s, d, \
-                     kneed, prior, out, list, lens, ffb, dg)
+#define O3DX_STILE_LAUNCH2(WY, WZ, WPE, MG)                                                              \
+  if (sym)                                                                                                 \
+    hipLaunchKernelGGL((k_normals_stile<32, WY, WZ, WPE, MG, true>), dim3((unsigned)nb), dim3(64 * WY * WZ), \
+                       0, s, d, kneed, prior, out, list, lens, ffb, dg);                                    \
+  else                                                                                                     \
+    hipLaunchKernelGGL((k_normals_stile<32, WY, WZ, WPE, MG, false>), dim3((unsigned)nb), dim3(64 * WY * WZ), \
+                       0, s, d, kneed, prior, out, list, lens, ffb, dg)
 #define O3DX_STILE_LAUNCH(WYZ, WPE, MG) O3DX_STILE_LAUNCH2(WYZ, WYZ, WPE, MG)
       // the launched variant must match the block grid (wy x wz waves) sized above
-      if (merged) {
+      // O3DX_STILE_FORM=vlist: the list-first form (opt-in; measured 0.72-0.76 ms
+      // against 0.66 ms for the two-scan form at C2)
+      const char* form = getenv("O3DX_STILE_FORM");
+      const bool vlist = form && std::string(form) == "vlist";
+      if (vlist && !merged && wy == 2 && wz == 2) {
+        if (sym)
+          hipLaunchKernelGGL((k_normals_vlist<32, 2, 2, 3, true>), dim3((unsigned)nb), dim3(256), 0, s, d, kneed,
+                             prior, out, list, lens, ffb);
+        else
+          hipLaunchKernelGGL((k_normals_vlist<32, 2, 2, 3, false>), dim3((unsigned)nb), dim3(256), 0, s, d, kneed,
+                             prior, out, list, lens, ffb);
+      } else if (merged) {
         if (wy == 1)
           O3DX_STILE_LAUNCH(1, 2, true);
         else if (wz == 3)

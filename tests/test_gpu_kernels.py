@@ -381,6 +381,14 @@ STILE_ENVS = [
     {"O3DX_STILE_MERGED": "1"},
     {"O3DX_STILE_MERGED": "1", "O3DX_STILE_SHAPE": "4"},
     {"O3DX_STILE_MERGED": "1", "O3DX_STILE_SHAPE": "1"},
+    {"O3DX_STILE_STENCIL": "sym"},
+    {"O3DX_STILE_STENCIL": "sym", "O3DX_STILE_SHAPE": "1"},
+    {"O3DX_STILE_STENCIL": "sym", "O3DX_STILE_SHAPE": "4"},
+    {"O3DX_STILE_STENCIL": "sym", "O3DX_STILE_MERGED": "1"},
+    {"O3DX_STILE_STENCIL": "mirror"},
+    {"O3DX_STILE_FORM": "vlist"},
+    {"O3DX_STILE_FORM": "vlist", "O3DX_STILE_STENCIL": "sym"},
+    {"O3DX_STILE_FORCE_FB": "1", "O3DX_STILE_STENCIL": "sym"},
 ]
 
 
