@@ -1132,6 +1132,7 @@ struct DenseVox {
   float rc2;                       // completeness radius^2 (world, float32, shrunk by the slack)
   float rc2w;                      // the same with the symmetric stencil's ring
   float rt2;                       // k_normals_vlist: the list threshold (<= rc2)
+  int vl_hist;                     // k_normals_vlist: histogram during the scan (1) or over the list (0)
   unsigned long long* stats;       // debug counters (o3dx_search_stats) or null
   int32_t* nbr;                    // test hook (o3dx_set_debug_neighbors) or null
   float* kd2;                      // per row an upper bound of the k-th neighbour d^2, or null
@@ -1653,17 +1654,39 @@ k_normals_vlist(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   bool fb = force_fb != 0;  // force_fb: tests of the hand-off path
   float T = d.rt2;
   int n = 0;
+  bool hist_ok = false;  // the scan's own histogram over [0, T) is valid
+  TileHist th;
   if (!fb) {
-    auto app = [&](int p, float d2) {
+#pragma unroll
+    for (int w = 0; w < kPHWords; ++w) hw[w * 64 + lane] = 0u;
+    const float sc0 = (float)kHistBins / T;
+    // append + histogram in one scan (slot 17 = at or beyond T); the packed
+    // 8-bit counters cannot carry: a stencil holds <= 251 candidates and only
+    // slot 17 (the top byte's lower neighbour is unused) can exceed the cap
+    auto app_hist = [&](int p, float d2) {
+      const int ix = (int)fminf(fmaf(d2, sc0, 0.0f), 16.0f) + 1;
+      atomicAdd(&hw[(ix >> 2) * 64 + lane], 1u << ((ix & 3) << 3));
       if (d2 < T) {  // masked store: only the accepting lanes take part
         l8[min(n, kVCap)][lane] = (uint8_t)p;
         ++n;
       }
     };
-    st_scan<S0, 0, StDef<S0>::N, kSY, kSZ>(txy, tz, fr, q, app);
+    auto app = [&](int p, float d2) {
+      if (d2 < T) {
+        l8[min(n, kVCap)][lane] = (uint8_t)p;
+        ++n;
+      }
+    };
+    if (d.vl_hist) {
+      st_scan<S0, 0, StDef<S0>::N, kSY, kSZ>(txy, tz, fr, q, app_hist);
+      hist_ok = true;
+    } else {
+      st_scan<S0, 0, StDef<S0>::N, kSY, kSZ>(txy, tz, fr, q, app);
+    }
     if (n < kneed) {  // cloud borders: the complete stencil (+ its ring)
       T = SYM ? d.rc2w : d.rc2;
       n = 0;
+      hist_ok = false;
       st_scan<SW, 0, StDef<SW>::N, kSY, kSZ>(txy, tz, fr, q, app);
     }
     fb = n < kneed || n > kVCap;
@@ -1672,7 +1695,6 @@ k_normals_vlist(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   float L = 0.f, U = 0.f;
   if (!fb) {
     // histogram of the list over [lo, hi) (packed 8-bit counters; <= kVCap entries)
-    TileHist th;
     auto list_hist = [&](float lo_, float hi_) {
       const float sc_ = (float)kHistBins / (hi_ - lo_), off_ = -lo_ * sc_;
 #pragma unroll
@@ -1700,7 +1722,12 @@ k_normals_vlist(DenseVox d, int kneed, const float* __restrict__ prior, float* _
 #pragma unroll
       for (int i = 0; i < kTileSlots; ++i) th.h[i] = (hw[(i >> 2) * 64 + lane] >> ((i & 3) << 3)) & 0xffu;
     };
-    list_hist(0.0f, T);
+    if (hist_ok) {
+#pragma unroll
+      for (int i = 0; i < kTileSlots; ++i) th.h[i] = (hw[(i >> 2) * 64 + lane] >> ((i & 3) << 3)) & 0xffu;
+    } else {
+      list_hist(0.0f, T);
+    }
     float lo = 0.f, hi = T;
     for (int lvl = 0;; ++lvl) {
       int cum, cb;
@@ -2318,6 +2345,7 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   // occupancy), never beyond the stencil's completeness radius
   const double Rt = std::min(1.14 * kth * geom[3], R);
   d.rt2 = (float)(Rt * Rt) * (1.0f - 4.0f * kRelEps);
+  d.vl_hist = getenv("O3DX_VLIST_LISTHIST") ? 0 : 1;
   d.stats = search_stats_ptr();
   d.nbr = debug_nbr(kneed, n);
   d.kd2 = kd2;
