@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--sorted-grid", action="store_true",
                     help="normals sort the representatives into their own grid (no voxel table hand-over)")
+    ap.add_argument("--two-call", action="store_true",
+                    help="time voxel_down_sample and estimate_normals as two library calls (default: the one-call "
+                         "pipeline o3dx_voxel_down_sample_normals)")
     ap.add_argument("--cpu-n", type=int, default=10_000_000, help="CPU baseline size (C2 input: 10M)")
     ap.add_argument("--cpu-icp-iters", type=int, default=2, help="ICP iterations of the CPU ICP leg (bounded sample)")
     ap.add_argument("--c5-n", type=int, default=200_000_000, help="C5 cloud size (0: skip the C5 leg)")
@@ -295,9 +298,7 @@ def c4_single_gpu(dev, args):
     vs = synthetic.voxel_size_for(n)
 
     def step():
-        out = ops.voxel_down_sample(pts, vs, keep_grid=True)
-        ops.estimate_normals(out["rep_xyz"], knn=args.knn, voxel_grid=out.get("voxel_grid"))
-        return out["rep_idx"].numel()
+        return ops.voxel_down_sample_normals(pts, vs, knn=args.knn)["rep_idx"].numel()
 
     step()
     torch.cuda.synchronize(dev)
@@ -460,12 +461,20 @@ def main():
     torch.cuda.synchronize(dev)
     keep = not args.sorted_grid
 
-    def step():
+    def step_two_call():
         # PointCloud.voxel_down_sample(vs).estimate_normals(): the voxel table
         # of the first call is the search grid of the second
         out = ops.voxel_down_sample(pts, vs, keep_grid=keep)
         nrm = ops.estimate_normals(out["rep_xyz"], knn=args.knn, voxel_grid=out.get("voxel_grid"))
         return out["rep_idx"].numel(), nrm
+
+    def step_fused():
+        # the same pipeline as one library call: the normals are queued behind
+        # the voxel kernels before the representative count is read back
+        out = ops.voxel_down_sample_normals(pts, vs, knn=args.knn)
+        return out["rep_idx"].numel(), out["normals"]
+
+    step = step_two_call if (args.two_call or not keep) else step_fused
 
     for _ in range(args.warmup):
         M, _ = step()
@@ -486,6 +495,16 @@ def main():
     ev_ms = ev0.elapsed_time(ev1)
     kernels = kernel_table()
     value = float(N) * args.steps / elapsed / 1e6
+    other = step_two_call if step is step_fused else (step_fused if keep else None)
+    other_ms = None
+    if other is not None:  # the other call structure, same pipeline, for the record
+        other()
+        torch.cuda.synchronize(dev)
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            other()
+        torch.cuda.synchronize(dev)
+        other_ms = round((time.perf_counter() - ta) / args.steps * 1e3, 3)
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -496,6 +515,9 @@ def main():
         "roofline": roofline(kernels, M, N, args.pmc_json),
         "cpu_baseline": None,
         "extra": {"stream_event_ms_per_step": round(ev_ms / args.steps, 3), "kernels": kernels,
+                  "call_structure": "one call (o3dx_voxel_down_sample_normals)" if step is step_fused
+                  else "two calls (voxel_down_sample, estimate_normals)",
+                  ("two_call_ms_per_step" if step is step_fused else "one_call_ms_per_step"): other_ms,
                   "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps / elapsed / 1e9, 2),
                   "storage_dtype": "f32", "arith": "float64 voxel keys / distances / covariance"},
     }

@@ -235,6 +235,25 @@ int o3dx_estimate_normals_voxel(const double* geom_host,
                                 float* normals_out_dev, float* kth_d2_dev,
                                 void* ws, size_t ws_bytes, void* stream);
 
+/* The pipeline pcd.voxel_down_sample(vs).estimate_normals(KNN(knn))
+ * (reference PointCloud.py:361, :68) in one call: the outputs of
+ * o3dx_voxel_down_sample_grid (rep_idx, rep_xyz, m, voxel_pts, geom) plus
+ * normals_out_dev[0..3m) = o3dx_estimate_normals_voxel on the
+ * representatives, bit for bit.  The normals kernels over the kept table are
+ * queued behind the voxel kernels before m is read back (one host
+ * synchronisation for the whole pipeline besides the bounds); if the table
+ * path turns out not to apply (sparse cloud, m < knn) the normals are
+ * recomputed by the general path.  ws: o3dx_voxel_workspace_bytes(n);
+ * nws: o3dx_normals_workspace_bytes(n); rep_xyz_dev, normals_out_dev cap n. */
+int o3dx_voxel_down_sample_normals(const float* xyz_dev, int64_t n,
+                                   const double* min_bound_host,
+                                   const double* max_bound_host, double voxel_size,
+                                   int knn, int32_t* rep_idx_dev, float* rep_xyz_dev,
+                                   float* normals_out_dev, int64_t* m_host,
+                                   float* voxel_pts_dev, int64_t voxel_cells,
+                                   double* geom_host, void* ws, size_t ws_bytes,
+                                   void* nws, size_t nws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- kNN search
  * Batched form of KDTreeFlann.search_knn_vector_3d / search_hybrid_vector_3d
  * (reference PointCloud.py:148-163).  For each query q: up to K = knn (KNN)

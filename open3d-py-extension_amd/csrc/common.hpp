@@ -188,6 +188,17 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp,
 // receives the exclusive prefix at every index; `idx_out` the compacted
 // indices; *count_dev the total (device int64).
 size_t compact_workspace_ints(int64_t n);
+constexpr int kScanItemsU8 = 16;                      // flags per thread of the u8 compaction
+constexpr int kScanTileBytes = kBlock * kScanItemsU8;  // flags per tile (4096)
+// Hook of voxel_down_sample_hooked: called with the kept table's geometry
+// (geom[8] = -1: occupancy unknown yet) and the table, after the voxel
+// kernels are queued and before the representative count is read back.
+typedef int (*VoxelHook)(void* ctx, const double* geom12, const void* vox);
+int voxel_down_sample_hooked(const float* xyz, int64_t n, const double* min_bound, const double* max_bound,
+                             double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, float* voxel_pts,
+                             int64_t voxel_cells, double* geom, void* ws, size_t ws_bytes, void* stream,
+                             VoxelHook hook, void* ctx);
+int compact_flags_scan(const uint8_t* flags, int64_t n, int64_t* count_dev, int32_t* tmp, hipStream_t s);
 int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* pos_out,
                   int64_t* count_dev, int32_t* tmp, hipStream_t s);
 

@@ -252,6 +252,21 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp,
 
 size_t compact_workspace_ints(int64_t n) { return scan_workspace_ints(n); }
 
+// The tile partial sums of compact_flags, scanned (tmp[tile] = the tile's
+// first output row; *count_dev = total): for callers with their own
+// compaction kernel over the same tiles (kScanTileBytes flags per tile).
+int compact_flags_scan(const uint8_t* flags, int64_t n, int64_t* count_dev, int32_t* tmp, hipStream_t s) {
+  int64_t tiles = (n + kScanTile - 1) / kScanTile;
+  if (tiles == 0) {
+    O3DX_HIP(hipMemsetAsync(count_dev, 0, sizeof(int64_t), s));
+    return 0;
+  }
+  hipLaunchKernelGGL(k_tile_sums_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp);
+  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, tmp, tiles, (int32_t*)nullptr, count_dev);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
 int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* pos_out,
                   int64_t* count_dev, int32_t* tmp, hipStream_t s) {
   int64_t tiles = (n + kScanTile - 1) / kScanTile;

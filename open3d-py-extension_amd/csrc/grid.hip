@@ -2293,16 +2293,34 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
 // KNN normals straight off the dense voxel table (k_normals_stile; hand-offs
 // to the wave form and the register top-k over the table).  1: not applicable
 // (the caller builds a search grid instead).
-static int normals_dense_vox(const double* geom, const float4* vox, const float* xyz, int64_t n, int mode, int knn,
-                             const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (!vox || geom[7] != 1.0 || mode != O3DX_SEARCH_KNN || getenv("O3DX_NO_STILE")) return 1;
+// Whether the normals run straight off the voxel table: KNN with k <= 32 and
+// representatives filling their voxels (occupied fraction of the voxels in
+// occupied 2^3 cells >= 0.7, so the stencil ball (2.45 voxels) holds the k
+// nearest with a wide margin).  *kth: the expected k-th distance (voxels).
+static bool dense_vox_applicable(const double* geom, const float4* vox, int64_t n, int mode, int knn, double* kth) {
+  if (!vox || geom[7] != 1.0 || mode != O3DX_SEARCH_KNN || getenv("O3DX_NO_STILE")) return false;
   const int kneed = (int)std::min<int64_t>(knn, n);
-  if (kneed < 1 || kneed > 32 || !(geom[8] > 0.0)) return 1;
-  // occupied fraction of the voxels inside occupied 2^3 cells: the 5^3
-  // stencil holds the k nearest only where the voxels are well filled
+  if (kneed < 1 || kneed > 32 || !(geom[8] > 0.0)) return false;
   const double dens = (double)n / (8.0 * geom[8]);
-  const double kth = std::cbrt((double)kneed / (std::min(dens, 1.0) * 4.18879020478639098));  // voxels
-  if (dens < 0.7 || kth > 2.0) return 1;  // the stencil ball (2.45 voxels) holds k with a wide margin
+  *kth = std::cbrt((double)kneed / (std::min(dens, 1.0) * 4.18879020478639098));
+  return dens >= 0.7 && *kth <= 2.0;
+}
+
+// spec: launched before the voxel counts are read back (o3dx_voxel_down_sample_normals):
+// n is then only the capacity (rows < n), kneed = knn, and the caller checks
+// dense_vox_applicable once the counts are known.
+static int normals_dense_vox(const double* geom, const float4* vox, const float* xyz, int64_t n, int mode, int knn,
+                             const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes, hipStream_t s,
+                             bool spec = false) {
+  double kth = 0.0;
+  int kneed = knn;
+  if (spec) {
+    if (!vox || mode != O3DX_SEARCH_KNN || knn < 1 || knn > 32 || n < knn || getenv("O3DX_NO_STILE")) return 1;
+    kth = std::cbrt((double)knn / 4.18879020478639098);
+  } else {
+    if (!dense_vox_applicable(geom, vox, n, mode, knn, &kth)) return 1;
+    kneed = (int)std::min<int64_t>(knn, n);
+  }
   DenseVox d;
   d.vox = vox;
   d.nx = (int)geom[4];
@@ -2641,4 +2659,53 @@ extern "C" int o3dx_knn_search(const float* xyz, int64_t n, const float* queries
                   mode == O3DX_SEARCH_HYBRID ? 1 : 0, radius, knn, idx_out, d2_out, cnt_out);
   O3DX_HIP(hipGetLastError());
   return 0;
+}
+
+// -------------------------------------------- voxel_down_sample + normals
+// The pipeline pcd.voxel_down_sample(vs).estimate_normals(KNN) (reference
+// PointCloud.py:361, :68) in one call: the normals kernels over the kept
+// voxel table are queued right behind the voxel kernels, before the host reads
+// the representative count back (their grids and lists do not need it), so
+// the GPU never idles between the two; once the counts are known the
+// applicability test of the table path is replayed, and when it fails the
+// normals are recomputed by o3dx_estimate_normals_voxel's general path.
+namespace o3dx {
+struct SpecNormals {
+  const float* rep_xyz;
+  int64_t ncap;
+  int knn;
+  float* out;
+  void* ws;
+  size_t ws_bytes;
+  hipStream_t s;
+  bool launched;
+};
+static int spec_normals_hook(void* ctx, const double* geom, const void* vox) {
+  SpecNormals& c = *static_cast<SpecNormals*>(ctx);
+  const int rc = normals_dense_vox(geom, static_cast<const float4*>(vox), c.rep_xyz, c.ncap, O3DX_SEARCH_KNN, c.knn,
+                                   nullptr, c.out, nullptr, c.ws, c.ws_bytes, c.s, true);
+  c.launched = rc == 0;
+  return rc == 1 ? 0 : rc;
+}
+}  // namespace o3dx
+
+extern "C" int o3dx_voxel_down_sample_normals(const float* xyz, int64_t n, const double* min_bound,
+                                              const double* max_bound, double voxel_size, int knn, int32_t* rep_idx,
+                                              float* rep_xyz, float* normals, int64_t* m_host, float* voxel_pts,
+                                              int64_t voxel_cells, double* geom, void* ws, size_t ws_bytes, void* nws,
+                                              size_t nws_bytes, void* stream) {
+  if (!rep_xyz || !normals || !voxel_pts || !geom || !nws || nws_bytes < o3dx_normals_workspace_bytes(n))
+    return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_normals: bad arguments");
+  if (knn < 0 || knn > O3DX_MAX_KNN) return fail(O3DX_ENOTSUP, "knn %d outside [0, %d]", knn, O3DX_MAX_KNN);
+  SpecNormals c{rep_xyz, n, knn, normals, nws, nws_bytes, as_stream(stream), false};
+  O3DX_TRY(voxel_down_sample_hooked(xyz, n, min_bound, max_bound, voxel_size, rep_idx, rep_xyz, m_host, voxel_pts,
+                                    voxel_cells, geom, ws, ws_bytes, stream, spec_normals_hook, &c));
+  const int64_t m = *m_host;
+  double kth;
+  if (c.launched && dense_vox_applicable(geom, reinterpret_cast<const float4*>(voxel_pts), m, O3DX_SEARCH_KNN, knn,
+                                         &kth) &&
+      std::min<int64_t>(knn, m) == knn)
+    return 0;
+  return o3dx_estimate_normals_voxel(geom, voxel_pts, rep_xyz, m, O3DX_SEARCH_KNN, knn, 0.0, nullptr, normals, nullptr,
+                                     nws, nws_bytes, stream);
 }

@@ -217,10 +217,14 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restr
 
 // Pass 3: one workgroup per brick: max index per voxel in LDS, then the
 // brick's slice of the dense table (-1 = empty) and flags[rep] = 1.
+// occ2 (nullable; bricks at least 2 voxels along every axis, so the even-
+// aligned 2^3 cells never straddle two bricks): the brick's occupied 2^3
+// cells, one atomic per brick (the normals' local-dimension estimate).
 __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __restrict__ entries,
                                                               const int32_t* __restrict__ boff, int nblk,
                                                               VoxelGeom g, Bricks b, int32_t* __restrict__ table,
-                                                              uint8_t* __restrict__ flags) {
+                                                              uint8_t* __restrict__ flags,
+                                                              unsigned long long* __restrict__ occ2) {
   __shared__ int32_t tab[1 << kMaxBrickBits];
   const int nloc = 1 << (b.sx + b.sy + b.sz);
   for (int k = threadIdx.x; k < nloc; k += kReduceBlock) tab[k] = -1;
@@ -241,6 +245,79 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
     const int32_t r = tab[k];
     table[x + (int64_t)g.nx * (y + (int64_t)g.ny * z)] = r;
     if (r >= 0) flags[r] = 1;
+  }
+  if (occ2) {
+    // 2^3 cells of the brick: cell c = (cx, cy, cz) local, voxels outside the
+    // grid were never assigned (-1)
+    const int csx = b.sx - 1, csy = b.sy - 1, csz = b.sz - 1;
+    const int ncell = 1 << (csx + csy + csz);
+    unsigned long long c = 0;
+    for (int k = threadIdx.x; k < ncell; k += kReduceBlock) {
+      const int cx = (k & ((1 << csx) - 1)) * 2, cy = ((k >> csx) & ((1 << csy) - 1)) * 2, cz = (k >> (csx + csy)) * 2;
+      bool any = false;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const int x = cx + (d & 1), y = cy + ((d >> 1) & 1), z = cz + (d >> 2);
+        any |= tab[x | (y << b.sx) | (z << (b.sx + b.sy))] >= 0;
+      }
+      c += any;
+    }
+    __shared__ unsigned long long sh[kReduceBlock / 64];
+    c = wave_sum(c);
+    if (lane_id() == 0) sh[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long t = 0;
+      for (int w = 0; w < kReduceBlock / 64; ++w) t += sh[w];
+      if (t) atomicAdd(occ2, t);
+    }
+  }
+}
+
+// Flag compaction fused with the kept table's fill (dense path, grid kept):
+// over the same tiles as compact_flags, each representative i (in ascending
+// order, row j) writes rep_idx[j] = i, rep_xyz[j] = xyz[i] and its voxel's
+// table slot (x, y, z, j); pos_out[i] = rows before i (trace).  The reads of
+// xyz follow the ascending flags (no random gather).
+__global__ void __launch_bounds__(kBlock) k_compact_vox(const uint8_t* __restrict__ f, int64_t n,
+                                                        const int32_t* __restrict__ part,
+                                                        const float* __restrict__ xyz, VoxelGeom g,
+                                                        int32_t* __restrict__ idx_out, float* __restrict__ rep_xyz,
+                                                        float4* __restrict__ vox, int32_t* __restrict__ pos_out) {
+  __shared__ int sh[kBlock / 64 + 1];
+  const int64_t base = (int64_t)blockIdx.x * kScanTileBytes + (int64_t)threadIdx.x * kScanItemsU8;
+  uint8_t v[kScanItemsU8];
+  if (base + kScanItemsU8 <= n) {
+    const uint4 q = *reinterpret_cast<const uint4*>(f + base);
+    const uint8_t* bb = reinterpret_cast<const uint8_t*>(&q);
+#pragma unroll
+    for (int j = 0; j < kScanItemsU8; ++j) v[j] = bb[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < kScanItemsU8; ++j) v[j] = (base + j < n) ? f[base + j] : 0;
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItemsU8; ++j) cnt += v[j] != 0;
+  int tot;
+  int ex = block_excl_scan<kBlock>(cnt, sh, &tot) + part[blockIdx.x];
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+#pragma unroll
+  for (int j = 0; j < kScanItemsU8; ++j) {
+    const int64_t i = base + j;
+    if (i < n) {
+      if (pos_out) pos_out[i] = ex;
+      if (v[j]) {
+        const P3 q = p[i];
+        idx_out[ex] = (int32_t)i;
+        if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[ex] = q;
+        double r[3];
+        int vv[3];
+        voxel_ref(q, g, r, vv);  // inside the grid: the dense path accepted every point
+        vox[vv[0] + (int64_t)g.nx * (vv[1] + (int64_t)g.ny * vv[2])] = make_float4(q.x, q.y, q.z, __int_as_float(ex));
+        ++ex;
+      }
+    }
   }
 }
 
@@ -348,26 +425,6 @@ __global__ void __launch_bounds__(kBlock) k_voxel_trace(const float* __restrict_
       int cid = ((r[0] - v[0]) >= 0.5 ? 1 : 0) + ((r[1] - v[1]) >= 0.5 ? 2 : 0) + ((r[2] - v[2]) >= 0.5 ? 4 : 0);
       atomicMax(&cubic[(int64_t)row * 8 + cid], (int32_t)i);
     }
-  }
-}
-
-// Kept voxel grid: vox[v] = (x, y, z, output row as int bits) of voxel v's
-// representative, w = -1 for an empty voxel (the buffer is 0xFF-filled).
-// Thread per representative (its row is j): the gather of rep_xyz plus one
-// 16-byte scatter, so the normals later read the reps in voxel order.
-__global__ void __launch_bounds__(kBlock) k_gather_vox(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
-                                                       const int64_t* __restrict__ cnt, VoxelGeom g,
-                                                       float* __restrict__ rep_xyz, float4* __restrict__ vox) {
-  if ((int)(cnt[1] & 0xffffffff) != 0) return;
-  const int64_t m = cnt[0];
-  const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
-    const P3 q = p[idx[j]];
-    if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q;
-    double r[3];
-    int v[3];
-    voxel_ref(q, g, r, v);  // inside the grid: the dense path accepted every point
-    vox[v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2])] = make_float4(q.x, q.y, q.z, __int_as_float((int)j));
   }
 }
 
@@ -479,7 +536,7 @@ extern "C" int64_t o3dx_voxel_grid_cells(int64_t n, const double* min_bound_host
 static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host, const double* max_bound_host,
                       double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point,
                       int32_t* cubic_id, float* vox, int64_t vox_cap, double* geom, void* ws, size_t ws_bytes,
-                      void* stream, const int64_t* xwin = nullptr) {
+                      void* stream, const int64_t* xwin = nullptr, VoxelHook hook = nullptr, void* hook_ctx = nullptr) {
   if (geom)
     for (int k = 0; k < 12; ++k) geom[k] = 0.0;
   if (n < 0 || (n > 0 && (!xyz || !rep_idx)) || !m_host)
@@ -554,18 +611,29 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       O3DX_TRY(exclusive_scan_i32(w.bhist, w.boff, (int64_t)bricks.nb * nblk, w.scan_tmp, s));
       hipLaunchKernelGGL(k_vbin_scatter, dim3(nblk), dim3(kBinBlock), scatter_lds_bytes(bricks.nb), s, xyz, n, g,
                          bricks, w.boff, w.entries);
+      const bool keep = vox && nslots <= vox_cap;
+      const bool occ_in_reduce = keep && bricks.sx >= 1 && bricks.sy >= 1 && bricks.sz >= 1;
       hipLaunchKernelGGL(k_vbin_reduce, dim3(bricks.nb), dim3(kReduceBlock), 0, s, w.entries, w.boff, (int)nblk, g,
-                         bricks, w.table, w.flags);
+                         bricks, w.table, w.flags,
+                         occ_in_reduce ? reinterpret_cast<unsigned long long*>(w.count + 2) : nullptr);
       kt.stop();
       KTimer kc("voxel_compact", s);
-      O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
-                             w.scan_tmp, s));
-      if (vox && nslots <= vox_cap) {
+      if (keep) {
         O3DX_HIP(hipMemsetAsync(vox, 0xFF, (size_t)nslots * 4 * sizeof(float), s));
-        const int64_t nc2 = (int64_t)((g.nx + 1) / 2) * ((g.ny + 1) / 2) * ((g.nz + 1) / 2);
-        hipLaunchKernelGGL(k_voxel_occ2<int32_t>, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table, g,
-                           reinterpret_cast<unsigned long long*>(w.count + 2));
+        if (!occ_in_reduce) {
+          const int64_t nc2 = (int64_t)((g.nx + 1) / 2) * ((g.ny + 1) / 2) * ((g.nz + 1) / 2);
+          hipLaunchKernelGGL(k_voxel_occ2<int32_t>, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table,
+                             g, reinterpret_cast<unsigned long long*>(w.count + 2));
+        }
+        O3DX_TRY(compact_flags_scan(w.flags, n, w.count, w.scan_tmp, s));
+        const int64_t tiles = (n + kScanTileBytes - 1) / kScanTileBytes;
+        hipLaunchKernelGGL(k_compact_vox, dim3((unsigned)tiles), dim3(kBlock), 0, s, w.flags, n, w.scan_tmp, xyz, g,
+                           rep_idx, rep_xyz, reinterpret_cast<float4*>(vox),
+                           (voxel_of_point || cubic_id) ? w.pos : nullptr);
         grid_kept = true;
+      } else {
+        O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
+                               w.scan_tmp, s));
       }
     } else {
       if (dense) {
@@ -593,11 +661,14 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     // gathers sized by the device-side count (at most n rows), queued ahead
     // of the read-back so they overlap the host round trip
     const unsigned gg = grid_for(n, kBlock, 8192);
-    if (grid_kept)
-      hipLaunchKernelGGL(k_gather_vox, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, g, rep_xyz,
-                         reinterpret_cast<float4*>(vox));
-    else if (rep_xyz)
+    if (!grid_kept && rep_xyz)
       hipLaunchKernelGGL(k_gather_xyz, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, rep_xyz);
+    if (hook && grid_kept && attempt == 0) {
+      // the table geometry (occupancy not yet known) for work queued ahead of the read-back
+      const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny,
+                             (double)g.nz, 1.0, -1.0, (double)g.kx0, 0.0, nvox};
+      O3DX_TRY(hook(hook_ctx, gv, vox));
+    }
     O3DX_TRY(read_back(counts, w.count, 3 * sizeof(int64_t), s));
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
@@ -722,4 +793,12 @@ extern "C" int o3dx_voxel_table_build(const float* xyz, int64_t n, const double*
                          1.0, (double)c[1], (double)g.kx0, 0.0, (double)nvox};
   for (int k = 0; k < 12; ++k) geom_host[k] = gv[k];
   return 0;
+}
+
+int o3dx::voxel_down_sample_hooked(const float* xyz, int64_t n, const double* min_bound, const double* max_bound,
+                             double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, float* voxel_pts,
+                             int64_t voxel_cells, double* geom, void* ws, size_t ws_bytes, void* stream,
+                             VoxelHook hook, void* ctx) {
+  return voxel_impl(xyz, n, min_bound, max_bound, voxel_size, rep_idx, rep_xyz, m_host, nullptr, nullptr, voxel_pts,
+                    voxel_cells, geom, ws, ws_bytes, stream, nullptr, hook, ctx);
 }

@@ -56,6 +56,8 @@ _SIGS = {
     "o3dx_normals_workspace_bytes": (_SZ, [_I64]),
     "o3dx_estimate_normals_voxel": (_I32, [_P, _P, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_estimate_normals": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_voxel_down_sample_normals": (_I32, [_P, _I64, _P, _P, _D, _I32, _P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P,
+                                               _SZ, _P]),
     "o3dx_knn_workspace_bytes": (_SZ, [_I64]),
     "o3dx_knn_search": (_I32, [_P, _I64, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_ransac_samples": (_I32, [_I64, _I32, _I32, ctypes.c_uint64, _P]),

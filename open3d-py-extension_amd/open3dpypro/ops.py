@@ -141,6 +141,39 @@ def voxel_table(xyz: torch.Tensor, voxel_size: float, min_bound, max_bound, kx0:
     return VoxelGrid(geom, table, n)
 
 
+def voxel_down_sample_normals(xyz: torch.Tensor, voxel_size: float, knn: int = 30, min_bound=None, max_bound=None):
+    """voxel_down_sample(keep_grid=True) + estimate_normals(KNN knn, voxel_grid=) on the
+    representatives in one library call (o3dx_voxel_down_sample_normals): the
+    normals are queued behind the voxel kernels without a host round trip.
+    Returns dict rep_idx, rep_xyz, normals (M,3) float32, voxel_grid."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    if n == 0:
+        e = torch.empty((0, 3), dtype=torch.float32, device=dev)
+        return {"rep_idx": torch.empty(0, dtype=torch.int32, device=dev), "rep_xyz": e, "normals": e.clone(),
+                "voxel_grid": None}
+    ws = N.workspace(L.o3dx_voxel_workspace_bytes(n), dev)
+    nws = N.workspace(L.o3dx_normals_workspace_bytes(n), dev, "normals")
+    rep = torch.empty(n, dtype=torch.int32, device=dev)
+    rxyz = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    nrm = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    cells = int(L.o3dx_voxel_grid_capacity(n))
+    vox = torch.empty((cells, 4), dtype=torch.float32, device=dev)
+    mnb = None if min_bound is None else _c(min_bound, np.float64)
+    mxb = None if max_bound is None else _c(max_bound, np.float64)
+    m = np.zeros(1, np.int64)
+    geom = np.zeros(12, np.float64)
+    N.check(L.o3dx_voxel_down_sample_normals(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), int(knn),
+                                             N.ptr(rep), N.ptr(rxyz), N.ptr(nrm), _np_ptr(m), N.ptr(vox), cells,
+                                             _np_ptr(geom), N.ptr(ws), ws.numel(), N.ptr(nws), nws.numel(),
+                                             N.stream_ptr(dev)), "voxel_down_sample_normals")
+    M = int(m[0])
+    return {"rep_idx": rep[:M], "rep_xyz": rxyz[:M], "normals": nrm[:M],
+            "voxel_grid": VoxelGrid(geom, vox, M) if geom[7] == 1.0 else None}
+
+
 class VoxelGrid:
     """The voxel table of a voxel_down_sample(keep_grid=True): per voxel the
     representative's (x, y, z, output row) (row -1 empty) + the grid geometry.

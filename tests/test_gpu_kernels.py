@@ -420,3 +420,29 @@ def test_normals_dense_voxel_table(dev, env, k, monkeypatch):
     tag = "+".join(f"{kk}={vv}" for kk, vv in env.items()) or "default"
     assert_normals(fused, exp, reps, k=k, what=f"dense_vox_{tag}_k{k}")
     assert_neighbour_sets(dn.ids(), reps, k, f"dense_vox_{tag}_k{k}")
+
+
+@pytest.mark.parametrize("case", ["cube", "box", "bunny", "sparse", "tiny"])
+def test_voxel_down_sample_normals_fused(dev, bunny, case):
+    """The one-call pipeline (normals queued before the count read-back) gives
+    the two-call results bit for bit — including where the table path does not
+    apply (sparse cloud, m < k) and the normals are recomputed."""
+    if case == "cube":
+        pts, vs = S.uniform_cube(300_000, 51), S.voxel_size_for(300_000)
+    elif case == "box":
+        pts, vs = S.box_surface(200_000, 52), 0.01
+    elif case == "bunny":
+        pts, vs = torch.from_numpy(bunny), 0.002
+    elif case == "sparse":
+        pts, vs = S.uniform_cube(3000, 53), 0.02
+    else:
+        pts, vs = S.uniform_cube(40, 54), 0.3
+    x = pts.to(dev)
+    f = ops.voxel_down_sample_normals(x, vs, knn=30)
+    a = ops.voxel_down_sample(x, vs, keep_grid=True)
+    ref = ops.estimate_normals(a["rep_xyz"], knn=30, voxel_grid=a["voxel_grid"])
+    assert torch.equal(f["rep_idx"], a["rep_idx"]) and torch.equal(f["rep_xyz"], a["rep_xyz"])
+    assert torch.equal(f["normals"], ref)
+    reps = pts.numpy()[a["rep_idx"].cpu().numpy()]
+    assert_normals(f["normals"].cpu().numpy(), O.estimate_normals(reps, O.KNN, 30), reps, k=30,
+                   what=f"fused_{case}")
