@@ -146,6 +146,8 @@ void timing_release(hipEvent_t e);   // back to the pool
 int host_wait(hipStream_t s);
 // Device -> host copy of a small result, then host_wait.
 int read_back(void* dst_host, const void* src_dev, size_t bytes, hipStream_t s);
+int read_back_begin(const void* src_dev, size_t bytes, hipStream_t s);  // <= 64 KB, one pending per thread
+int read_back_end(void* dst_host, size_t bytes);
 struct KTimer {
   const char* name;
   hipStream_t s;

@@ -63,6 +63,33 @@ int read_back(void* dst_host, const void* src_dev, size_t bytes, hipStream_t s) 
   return host_wait(s);
 }
 
+// Split read-back: the copy into the pinned staging buffer and an event are
+// queued now (read_back_begin), the host waits for that event only
+// (read_back_end) — work queued on the stream in between keeps running.
+static thread_local void* g_rb_pin = nullptr;
+static thread_local hipEvent_t g_rb_ev = nullptr;
+
+int read_back_begin(const void* src_dev, size_t bytes, hipStream_t s) {
+  if (bytes > (64 << 10)) return fail(O3DX_EINVAL, "read_back_begin: %zu bytes", bytes);
+  if (!g_rb_pin) O3DX_HIP(hipHostMalloc(&g_rb_pin, 64 << 10, hipHostMallocDefault));
+  if (!g_rb_ev) O3DX_HIP(hipEventCreateWithFlags(&g_rb_ev, hipEventDisableTiming));
+  O3DX_HIP(hipMemcpyAsync(g_rb_pin, src_dev, bytes, hipMemcpyDeviceToHost, s));
+  O3DX_HIP(hipEventRecord(g_rb_ev, s));
+  return 0;
+}
+
+int read_back_end(void* dst_host, size_t bytes) {
+  bool done = false;
+  for (int i = 0; i < 1 << 16 && !done; ++i) {
+    const hipError_t e = hipEventQuery(g_rb_ev);
+    if (e == hipSuccess) done = true;
+    else if (e != hipErrorNotReady) break;
+  }
+  if (!done) O3DX_HIP(hipEventSynchronize(g_rb_ev));
+  std::memcpy(dst_host, g_rb_pin, bytes);
+  return 0;
+}
+
 int host_wait(hipStream_t s) {
   // poll instead of a blocking wait: the short read-backs on the launch path
   // (counts, bounds) return as soon as the copy lands, without an interrupt

@@ -275,49 +275,47 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
 }
 
 // Flag compaction fused with the kept table's fill (dense path, grid kept):
-// over the same tiles as compact_flags, each representative i (in ascending
-// order, row j) writes rep_idx[j] = i, rep_xyz[j] = xyz[i] and its voxel's
-// table slot (x, y, z, j); pos_out[i] = rows before i (trace).  The reads of
-// xyz follow the ascending flags (no random gather).
+// over the tiles of compact_flags_scan (kScanTileBytes flags each), in 16
+// rounds of 256 consecutive flags — lane-strided, so the flag and xyz reads of
+// a round are coalesced — each representative i (row j, ascending) writes
+// rep_idx[j] = i, rep_xyz[j] = xyz[i] and its voxel's table slot (x, y, z, j);
+// pos_out[i] = rows before i (trace).
 __global__ void __launch_bounds__(kBlock) k_compact_vox(const uint8_t* __restrict__ f, int64_t n,
                                                         const int32_t* __restrict__ part,
                                                         const float* __restrict__ xyz, VoxelGeom g,
                                                         int32_t* __restrict__ idx_out, float* __restrict__ rep_xyz,
                                                         float4* __restrict__ vox, int32_t* __restrict__ pos_out) {
-  __shared__ int sh[kBlock / 64 + 1];
-  const int64_t base = (int64_t)blockIdx.x * kScanTileBytes + (int64_t)threadIdx.x * kScanItemsU8;
-  uint8_t v[kScanItemsU8];
-  if (base + kScanItemsU8 <= n) {
-    const uint4 q = *reinterpret_cast<const uint4*>(f + base);
-    const uint8_t* bb = reinterpret_cast<const uint8_t*>(&q);
-#pragma unroll
-    for (int j = 0; j < kScanItemsU8; ++j) v[j] = bb[j];
-  } else {
-#pragma unroll
-    for (int j = 0; j < kScanItemsU8; ++j) v[j] = (base + j < n) ? f[base + j] : 0;
-  }
-  int cnt = 0;
-#pragma unroll
-  for (int j = 0; j < kScanItemsU8; ++j) cnt += v[j] != 0;
-  int tot;
-  int ex = block_excl_scan<kBlock>(cnt, sh, &tot) + part[blockIdx.x];
+  static_assert(kBlock == 256 && kScanTileBytes == 16 * kBlock, "tile shape");
+  __shared__ int wsum[kBlock / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int row = part[blockIdx.x];
   const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int r = 0; r < 16; ++r) {
+    const int64_t i = (int64_t)blockIdx.x * kScanTileBytes + r * kBlock + threadIdx.x;
+    const bool on = i < n && f[i] != 0;
+    const uint64_t m = __ballot(on);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) wsum[wv] = __popcll(m);
+    __syncthreads();
+    int off = row, tot = 0;
 #pragma unroll
-  for (int j = 0; j < kScanItemsU8; ++j) {
-    const int64_t i = base + j;
-    if (i < n) {
-      if (pos_out) pos_out[i] = ex;
-      if (v[j]) {
-        const P3 q = p[i];
-        idx_out[ex] = (int32_t)i;
-        if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[ex] = q;
-        double r[3];
-        int vv[3];
-        voxel_ref(q, g, r, vv);  // inside the grid: the dense path accepted every point
-        vox[vv[0] + (int64_t)g.nx * (vv[1] + (int64_t)g.ny * vv[2])] = make_float4(q.x, q.y, q.z, __int_as_float(ex));
-        ++ex;
-      }
+    for (int w = 0; w < kBlock / 64; ++w) {
+      off += w < wv ? wsum[w] : 0;
+      tot += wsum[w];
     }
+    const int j = off + below;
+    if (pos_out && i < n) pos_out[i] = j;
+    if (on) {
+      const P3 q = p[i];
+      idx_out[j] = (int32_t)i;
+      if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q;
+      double rr[3];
+      int vv[3];
+      voxel_ref(q, g, rr, vv);  // inside the grid: the dense path accepted every point
+      vox[vv[0] + (int64_t)g.nx * (vv[1] + (int64_t)g.ny * vv[2])] = make_float4(q.x, q.y, q.z, __int_as_float(j));
+    }
+    row += tot;
+    __syncthreads();
   }
 }
 
@@ -664,12 +662,16 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     if (!grid_kept && rep_xyz)
       hipLaunchKernelGGL(k_gather_xyz, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, rep_xyz);
     if (hook && grid_kept && attempt == 0) {
-      // the table geometry (occupancy not yet known) for work queued ahead of the read-back
+      // the counts' copy is queued first, then the hook's work (the table
+      // geometry, occupancy not yet known): the host waits for the copy only
       const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny,
                              (double)g.nz, 1.0, -1.0, (double)g.kx0, 0.0, nvox};
+      O3DX_TRY(read_back_begin(w.count, 3 * sizeof(int64_t), s));
       O3DX_TRY(hook(hook_ctx, gv, vox));
+      O3DX_TRY(read_back_end(counts, 3 * sizeof(int64_t)));
+    } else {
+      O3DX_TRY(read_back(counts, w.count, 3 * sizeof(int64_t), s));
     }
-    O3DX_TRY(read_back(counts, w.count, 3 * sizeof(int64_t), s));
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
     if (xwin) return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_window: points outside the x-key window");
