@@ -274,10 +274,12 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
   }
 }
 
-// Flag compaction fused with the kept table's fill (dense path, grid kept):
-// over the tiles of compact_flags_scan (kScanTileBytes flags each), in 16
-// rounds of 256 consecutive flags — lane-strided, so the flag and xyz reads of
-// a round are coalesced — each representative i (row j, ascending) writes
+// Flag compaction fused with the kept table's fill (dense path, grid kept),
+// over the tiles of compact_flags_scan (kScanTileBytes flags each): every wave
+// first counts its quarter of the tile (one barrier for the wave offsets),
+// then walks it in rounds of 64 consecutive flags with no further barrier —
+// lane-strided, so the flag and xyz reads of a round are coalesced, four
+// rounds' loads in flight.  Each representative i (row j, ascending) writes
 // rep_idx[j] = i, rep_xyz[j] = xyz[i] and its voxel's table slot (x, y, z, j);
 // pos_out[i] = rows before i (trace).
 __global__ void __launch_bounds__(kBlock) k_compact_vox(const uint8_t* __restrict__ f, int64_t n,
@@ -285,37 +287,57 @@ __global__ void __launch_bounds__(kBlock) k_compact_vox(const uint8_t* __restric
                                                         const float* __restrict__ xyz, VoxelGeom g,
                                                         int32_t* __restrict__ idx_out, float* __restrict__ rep_xyz,
                                                         float4* __restrict__ vox, int32_t* __restrict__ pos_out) {
-  static_assert(kBlock == 256 && kScanTileBytes == 16 * kBlock, "tile shape");
-  __shared__ int wsum[kBlock / 64];
+  constexpr int kWaves = kBlock / 64, kChunk = kScanTileBytes / kWaves, kRounds = kChunk / 64;  // 1024, 16
+  static_assert(kChunk % 64 == 0 && kRounds % 4 == 0, "tile shape");
+  __shared__ int wsum[kWaves];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * kScanTileBytes + (int64_t)wv * kChunk;
+  {
+    int cnt = 0;
+    const int64_t b = c0 + (int64_t)lane * 16;
+    if (b + 16 <= n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(f + b);
+      cnt = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // 0/1 bytes
+    } else {
+      for (int k = 0; k < 16; ++k) cnt += (b + k < n) ? (f[b + k] != 0) : 0;
+    }
+    cnt = wave_sum(cnt);
+    if (lane == 0) wsum[wv] = cnt;
+  }
+  __syncthreads();
   int row = part[blockIdx.x];
+  for (int w = 0; w < wv; ++w) row += wsum[w];
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int r = 0; r < 16; ++r) {
-    const int64_t i = (int64_t)blockIdx.x * kScanTileBytes + r * kBlock + threadIdx.x;
-    const bool on = i < n && f[i] != 0;
-    const uint64_t m = __ballot(on);
-    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane == 0) wsum[wv] = __popcll(m);
-    __syncthreads();
-    int off = row, tot = 0;
+  for (int r0 = 0; r0 < kRounds; r0 += 4) {
+    bool on[4];
+    P3 q[4];
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) {
-      off += w < wv ? wsum[w] : 0;
-      tot += wsum[w];
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = c0 + (int64_t)(r0 + u) * 64 + lane;
+      on[u] = i < n && f[i] != 0;
     }
-    const int j = off + below;
-    if (pos_out && i < n) pos_out[i] = j;
-    if (on) {
-      const P3 q = p[i];
-      idx_out[j] = (int32_t)i;
-      if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q;
-      double rr[3];
-      int vv[3];
-      voxel_ref(q, g, rr, vv);  // inside the grid: the dense path accepted every point
-      vox[vv[0] + (int64_t)g.nx * (vv[1] + (int64_t)g.ny * vv[2])] = make_float4(q.x, q.y, q.z, __int_as_float(j));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = c0 + (int64_t)(r0 + u) * 64 + lane;
+      if (on[u]) q[u] = p[i];
     }
-    row += tot;
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = c0 + (int64_t)(r0 + u) * 64 + lane;
+      const uint64_t m = __ballot(on[u]);
+      const int j = row + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      row += __popcll(m);
+      if (pos_out && i < n) pos_out[i] = j;
+      if (on[u]) {
+        idx_out[j] = (int32_t)i;
+        if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q[u];
+        double rr[3];
+        int vv[3];
+        voxel_ref(q[u], g, rr, vv);  // inside the grid: the dense path accepted every point
+        vox[vv[0] + (int64_t)g.nx * (vv[1] + (int64_t)g.ny * vv[2])] =
+            make_float4(q[u].x, q[u].y, q[u].z, __int_as_float(j));
+      }
+    }
   }
 }
 
