@@ -274,14 +274,14 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
   }
 }
 
-// Flag compaction fused with the kept table's fill (dense path, grid kept),
-// over the tiles of compact_flags_scan (kScanTileBytes flags each): every wave
-// first counts its quarter of the tile (one barrier for the wave offsets),
-// then walks it in rounds of 64 consecutive flags with no further barrier —
-// lane-strided, so the flag and xyz reads of a round are coalesced, four
-// rounds' loads in flight.  Each representative i (row j, ascending) writes
-// rep_idx[j] = i, rep_xyz[j] = xyz[i] and its voxel's table slot (x, y, z, j);
-// pos_out[i] = rows before i (trace).
+// Flag compaction fused with the representatives' gather (dense path, grid
+// kept), over the tiles of compact_flags_scan (kScanTileBytes flags each):
+// every wave first counts its quarter of the tile (one barrier for the wave
+// offsets), then walks it in rounds of 64 consecutive flags with no further
+// barrier — lane-strided, so the flag and xyz reads of a round are coalesced,
+// four rounds' loads in flight.  Each representative i (row j, ascending)
+// writes rep_idx[j] = i and rep_xyz[j] = xyz[i] (no random gather);
+// pos_out[i] = rows before i (trace).  k_table_fill then writes the table.
 __global__ void __launch_bounds__(kBlock) k_compact_vox(const uint8_t* __restrict__ f, int64_t n,
                                                         const int32_t* __restrict__ part,
                                                         const float* __restrict__ xyz, VoxelGeom g,
@@ -330,14 +330,26 @@ __global__ void __launch_bounds__(kBlock) k_compact_vox(const uint8_t* __restric
       if (pos_out && i < n) pos_out[i] = j;
       if (on[u]) {
         idx_out[j] = (int32_t)i;
-        if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q[u];
-        double rr[3];
-        int vv[3];
-        voxel_ref(q[u], g, rr, vv);  // inside the grid: the dense path accepted every point
-        vox[vv[0] + (int64_t)g.nx * (vv[1] + (int64_t)g.ny * vv[2])] =
-            make_float4(q[u].x, q[u].y, q[u].z, __int_as_float(j));
+        reinterpret_cast<P3*>(rep_xyz)[j] = q[u];
       }
     }
+  }
+}
+
+// The kept table's slots, thread per representative row j (all lanes busy
+// with the float64 key): rep_xyz[j] read in order, one 16-B store per voxel.
+__global__ void __launch_bounds__(kBlock) k_table_fill(const float* __restrict__ rep_xyz,
+                                                       const int64_t* __restrict__ cnt, VoxelGeom g,
+                                                       float4* __restrict__ vox) {
+  if ((int)(cnt[1] & 0xffffffff) != 0) return;
+  const int64_t m = cnt[0];
+  const P3* p = reinterpret_cast<const P3*>(rep_xyz);
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const P3 q = p[j];
+    double r[3];
+    int v[3];
+    voxel_ref(q, g, r, v);  // inside the grid: the dense path accepted every point
+    vox[v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2])] = make_float4(q.x, q.y, q.z, __int_as_float((int)j));
   }
 }
 
@@ -647,9 +659,11 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
         }
         O3DX_TRY(compact_flags_scan(w.flags, n, w.count, w.scan_tmp, s));
         const int64_t tiles = (n + kScanTileBytes - 1) / kScanTileBytes;
+        float* rx = rep_xyz ? rep_xyz : reinterpret_cast<float*>(w.entries);  // entries are dead here
         hipLaunchKernelGGL(k_compact_vox, dim3((unsigned)tiles), dim3(kBlock), 0, s, w.flags, n, w.scan_tmp, xyz, g,
-                           rep_idx, rep_xyz, reinterpret_cast<float4*>(vox),
-                           (voxel_of_point || cubic_id) ? w.pos : nullptr);
+                           rep_idx, rx, reinterpret_cast<float4*>(vox), (voxel_of_point || cubic_id) ? w.pos : nullptr);
+        hipLaunchKernelGGL(k_table_fill, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, rx, w.count, g,
+                           reinterpret_cast<float4*>(vox));
         grid_kept = true;
       } else {
         O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
