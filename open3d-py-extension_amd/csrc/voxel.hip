@@ -274,85 +274,6 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
   }
 }
 
-// Flag compaction fused with the representatives' gather (dense path, grid
-// kept), over the tiles of compact_flags_scan (kScanTileBytes flags each):
-// every wave first counts its quarter of the tile (one barrier for the wave
-// offsets), then walks it in rounds of 64 consecutive flags with no further
-// barrier — lane-strided, so the flag and xyz reads of a round are coalesced,
-// four rounds' loads in flight.  Each representative i (row j, ascending)
-// writes rep_idx[j] = i and rep_xyz[j] = xyz[i] (no random gather);
-// pos_out[i] = rows before i (trace).  k_table_fill then writes the table.
-__global__ void __launch_bounds__(kBlock) k_compact_vox(const uint8_t* __restrict__ f, int64_t n,
-                                                        const int32_t* __restrict__ part,
-                                                        const float* __restrict__ xyz, VoxelGeom g,
-                                                        int32_t* __restrict__ idx_out, float* __restrict__ rep_xyz,
-                                                        float4* __restrict__ vox, int32_t* __restrict__ pos_out) {
-  constexpr int kWaves = kBlock / 64, kChunk = kScanTileBytes / kWaves, kRounds = kChunk / 64;  // 1024, 16
-  static_assert(kChunk % 64 == 0 && kRounds % 4 == 0, "tile shape");
-  __shared__ int wsum[kWaves];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t c0 = (int64_t)blockIdx.x * kScanTileBytes + (int64_t)wv * kChunk;
-  {
-    int cnt = 0;
-    const int64_t b = c0 + (int64_t)lane * 16;
-    if (b + 16 <= n) {
-      const uint4 v = *reinterpret_cast<const uint4*>(f + b);
-      cnt = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // 0/1 bytes
-    } else {
-      for (int k = 0; k < 16; ++k) cnt += (b + k < n) ? (f[b + k] != 0) : 0;
-    }
-    cnt = wave_sum(cnt);
-    if (lane == 0) wsum[wv] = cnt;
-  }
-  __syncthreads();
-  int row = part[blockIdx.x];
-  for (int w = 0; w < wv; ++w) row += wsum[w];
-  const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int r0 = 0; r0 < kRounds; r0 += 4) {
-    bool on[4];
-    P3 q[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = c0 + (int64_t)(r0 + u) * 64 + lane;
-      on[u] = i < n && f[i] != 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = c0 + (int64_t)(r0 + u) * 64 + lane;
-      if (on[u]) q[u] = p[i];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = c0 + (int64_t)(r0 + u) * 64 + lane;
-      const uint64_t m = __ballot(on[u]);
-      const int j = row + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      row += __popcll(m);
-      if (pos_out && i < n) pos_out[i] = j;
-      if (on[u]) {
-        idx_out[j] = (int32_t)i;
-        reinterpret_cast<P3*>(rep_xyz)[j] = q[u];
-      }
-    }
-  }
-}
-
-// The kept table's slots, thread per representative row j (all lanes busy
-// with the float64 key): rep_xyz[j] read in order, one 16-B store per voxel.
-__global__ void __launch_bounds__(kBlock) k_table_fill(const float* __restrict__ rep_xyz,
-                                                       const int64_t* __restrict__ cnt, VoxelGeom g,
-                                                       float4* __restrict__ vox) {
-  if ((int)(cnt[1] & 0xffffffff) != 0) return;
-  const int64_t m = cnt[0];
-  const P3* p = reinterpret_cast<const P3*>(rep_xyz);
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
-    const P3 q = p[j];
-    double r[3];
-    int v[3];
-    voxel_ref(q, g, r, v);  // inside the grid: the dense path accepted every point
-    vox[v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2])] = make_float4(q.x, q.y, q.z, __int_as_float((int)j));
-  }
-}
-
 // Brick shape: 2^bits voxels, split over the axes by repeatedly doubling the
 // axis with the most bricks left; nb = 0 when the grid needs more than
 // kMaxBuckets bricks (the plain dense path handles it).
@@ -457,6 +378,26 @@ __global__ void __launch_bounds__(kBlock) k_voxel_trace(const float* __restrict_
       int cid = ((r[0] - v[0]) >= 0.5 ? 1 : 0) + ((r[1] - v[1]) >= 0.5 ? 2 : 0) + ((r[2] - v[2]) >= 0.5 ? 4 : 0);
       atomicMax(&cubic[(int64_t)row * 8 + cid], (int32_t)i);
     }
+  }
+}
+
+// Kept voxel grid: vox[v] = (x, y, z, output row as int bits) of voxel v's
+// representative, w = -1 for an empty voxel (the buffer is 0xFF-filled).
+// Thread per representative (its row is j): the gather of rep_xyz plus one
+// 16-byte scatter, so the normals later read the reps in voxel order.
+__global__ void __launch_bounds__(kBlock) k_gather_vox(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
+                                                       const int64_t* __restrict__ cnt, VoxelGeom g,
+                                                       float* __restrict__ rep_xyz, float4* __restrict__ vox) {
+  if ((int)(cnt[1] & 0xffffffff) != 0) return;
+  const int64_t m = cnt[0];
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const P3 q = p[idx[j]];
+    if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q;
+    double r[3];
+    int v[3];
+    voxel_ref(q, g, r, v);  // inside the grid: the dense path accepted every point
+    vox[v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2])] = make_float4(q.x, q.y, q.z, __int_as_float((int)j));
   }
 }
 
@@ -657,18 +598,14 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
           hipLaunchKernelGGL(k_voxel_occ2<int32_t>, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table,
                              g, reinterpret_cast<unsigned long long*>(w.count + 2));
         }
-        O3DX_TRY(compact_flags_scan(w.flags, n, w.count, w.scan_tmp, s));
-        const int64_t tiles = (n + kScanTileBytes - 1) / kScanTileBytes;
-        float* rx = rep_xyz ? rep_xyz : reinterpret_cast<float*>(w.entries);  // entries are dead here
-        hipLaunchKernelGGL(k_compact_vox, dim3((unsigned)tiles), dim3(kBlock), 0, s, w.flags, n, w.scan_tmp, xyz, g,
-                           rep_idx, rx, reinterpret_cast<float4*>(vox), (voxel_of_point || cubic_id) ? w.pos : nullptr);
-        hipLaunchKernelGGL(k_table_fill, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, rx, w.count, g,
-                           reinterpret_cast<float4*>(vox));
         grid_kept = true;
-      } else {
-        O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
-                               w.scan_tmp, s));
       }
+      // (measured: a compaction fused with an in-order gather of the reps'
+      // xyz + a thread-per-rep table fill took 54 + 36 us against 14 + 56 us
+      // for the compaction + k_gather_vox below at C2 — the sparse in-order
+      // read of the cloud costs what the random gather does)
+      O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
+                             w.scan_tmp, s));
     } else {
       if (dense) {
         nslots = (int64_t)nvox;
@@ -695,7 +632,10 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     // gathers sized by the device-side count (at most n rows), queued ahead
     // of the read-back so they overlap the host round trip
     const unsigned gg = grid_for(n, kBlock, 8192);
-    if (!grid_kept && rep_xyz)
+    if (grid_kept)
+      hipLaunchKernelGGL(k_gather_vox, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, g, rep_xyz,
+                         reinterpret_cast<float4*>(vox));
+    else if (rep_xyz)
       hipLaunchKernelGGL(k_gather_xyz, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, rep_xyz);
     if (hook && grid_kept && attempt == 0) {
       // the counts' copy is queued first, then the hook's work (the table
