@@ -478,7 +478,11 @@ def main():
 
     for _ in range(args.warmup):
         M, _ = step()
+    # the timed region records HIP events around the dominant kernel only
+    # (every extra event pair adds launch-path work to the pipeline); the
+    # per-kernel breakdown is a separate, untimed pass below
     _native.reset_kernel_timing()
+    _native.kernel_timing_filter(["normals_stile"])
     _native.set_kernel_timing(True)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -493,7 +497,16 @@ def main():
     _native.set_kernel_timing(False)
     elapsed = t1 - t0
     ev_ms = ev0.elapsed_time(ev1)
-    kernels = kernel_table()
+    dom = kernel_table()
+    _native.kernel_timing_filter(None)
+    _native.reset_kernel_timing()
+    _native.set_kernel_timing(True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    _native.set_kernel_timing(False)
+    kernels = kernel_table()  # breakdown (all timers on; not the timed region)
+    kernels.update(dom)       # the dominant kernel as timed inside the timed region
     value = float(N) * args.steps / elapsed / 1e6
     other = step_two_call if step is step_fused else (step_fused if keep else None)
     other_ms = None

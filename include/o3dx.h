@@ -73,6 +73,8 @@ const char* o3dx_last_error(void);
  * ("voxel_assign", "normals_knn", "grid_build", "plane_count",
  * "icp_accumulate", ...).  Returns 0 if the name was seen, -1 otherwise. */
 void o3dx_set_kernel_timing(int enable);
+/* Restrict timing to the comma-separated timer names ("" or NULL: all). */
+void o3dx_kernel_timing_filter(const char* names_csv);
 void o3dx_reset_kernel_timing(void);
 int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches);
 

@@ -139,6 +139,7 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 // RAII bracket of a launch with hipEvents on its stream (only when enabled by
 // o3dx_set_kernel_timing); read back lazily by o3dx_kernel_timing.
 bool timing_on();
+bool timing_wanted(const char* name);
 void timing_push(const char* name, hipEvent_t a, hipEvent_t b);
 hipEvent_t timing_event();           // from the recycled pool (or new)
 void timing_release(hipEvent_t e);   // back to the pool
@@ -153,7 +154,7 @@ struct KTimer {
   hipStream_t s;
   hipEvent_t a = nullptr, b = nullptr;
   KTimer(const char* n, hipStream_t st) : name(n), s(st) {
-    if (timing_on()) {
+    if (timing_wanted(n)) {
       a = timing_event();
       b = timing_event();
       if (a && b) {

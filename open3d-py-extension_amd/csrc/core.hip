@@ -26,6 +26,16 @@ static std::vector<hipEvent_t> g_free_events;  // recycled: no event creation on
 
 bool timing_on() { return g_timing; }
 
+// o3dx_kernel_timing_filter: when set, only the named timers record (the
+// event records of the others stay out of a timed pipeline)
+static std::string g_tfilter;
+bool timing_wanted(const char* name) {
+  if (!g_timing) return false;
+  if (g_tfilter.empty()) return true;
+  const std::string n = std::string(",") + name + ",";
+  return (std::string(",") + g_tfilter + ",").find(n) != std::string::npos;
+}
+
 hipEvent_t timing_event() {
   {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -428,6 +438,8 @@ extern "C" void o3dx_set_kernel_timing(int enable) {
   if (!enable) timing_drain();
   g_timing = enable != 0;
 }
+
+extern "C" void o3dx_kernel_timing_filter(const char* names_csv) { g_tfilter = names_csv ? names_csv : ""; }
 
 extern "C" void o3dx_reset_kernel_timing(void) {
   timing_drain();

@@ -36,6 +36,7 @@ _SIGS = {
     "o3dx_last_error": (ctypes.c_char_p, []),
     "o3dx_set_kernel_timing": (None, [_I32]),
     "o3dx_reset_kernel_timing": (None, []),
+    "o3dx_kernel_timing_filter": (None, [ctypes.c_char_p]),
     "o3dx_kernel_timing": (_I32, [ctypes.c_char_p, _P, _P]),
     "o3dx_set_search_stats": (_I32, [_I32]),
     "o3dx_search_stats": (_I32, [_P]),
@@ -163,6 +164,11 @@ def workspace(nbytes: int, device: torch.device, slot: str = "main") -> torch.Te
 
 def set_kernel_timing(enable: bool):
     load().o3dx_set_kernel_timing(1 if enable else 0)
+
+
+def kernel_timing_filter(names=None):
+    """Only the named library timers record while timing is on (None: all)."""
+    load().o3dx_kernel_timing_filter(",".join(names).encode() if names else None)
 
 
 def reset_kernel_timing():
