@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--sorted-grid", action="store_true",
                     help="normals sort the representatives into their own grid (no voxel table hand-over)")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="no HIP events inside the timed region (the dominant kernel is then timed in a later pass)")
     ap.add_argument("--two-call", action="store_true",
                     help="time voxel_down_sample and estimate_normals as two library calls (default: the one-call "
                          "pipeline o3dx_voxel_down_sample_normals)")
@@ -483,7 +485,7 @@ def main():
     # per-kernel breakdown is a separate, untimed pass below
     _native.reset_kernel_timing()
     _native.kernel_timing_filter(["normals_stile"])
-    _native.set_kernel_timing(True)
+    _native.set_kernel_timing(not args.no_kernel_events)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     barrier(world, dev)
@@ -506,7 +508,8 @@ def main():
     torch.cuda.synchronize(dev)
     _native.set_kernel_timing(False)
     kernels = kernel_table()  # breakdown (all timers on; not the timed region)
-    kernels.update(dom)       # the dominant kernel as timed inside the timed region
+    if dom:
+        kernels.update(dom)   # the dominant kernel as timed inside the timed region
     value = float(N) * args.steps / elapsed / 1e6
     other = step_two_call if step is step_fused else (step_fused if keep else None)
     other_ms = None
