@@ -87,3 +87,84 @@ def test_icp_1m_parity(dev):
                                          max_iteration=30, relative_fitness=0, relative_rmse=0)
     np.testing.assert_allclose(res["transformation"], T, atol=1e-5)
     assert abs(res["fitness"] - fit) < 1e-6
+
+
+def test_c4_50m_reps_and_normals(dev):
+    """C4's cloud size on one GPU (50M uniform points, 12.3M voxels): the
+    one-call voxel + normals pipeline — representatives bit-exact against the
+    oracle, every normal within 1e-5 of the oracle's, and bit-equal to the
+    two-call path whose selected neighbour sets match the oracle's exactly."""
+    n = 50_000_000
+    vs = S.voxel_size_for(n)
+    pts = S.uniform_cube(n, seed=0, device=dev)
+    f = ops.voxel_down_sample_normals(pts, vs, knn=30)
+    a = ops.voxel_down_sample(pts, vs, keep_grid=True)
+    m = a["rep_idx"].numel()
+    with DebugNeighbors(m, 30, dev) as dn:
+        two = ops.estimate_normals(a["rep_xyz"], knn=30, voxel_grid=a["voxel_grid"])
+    assert torch.equal(f["rep_idx"], a["rep_idx"]) and torch.equal(f["normals"], two)
+    p = pts.cpu().numpy()
+    del pts, a
+    torch.cuda.empty_cache()
+    ref = O.voxel_down_sample(p, vs)
+    assert np.array_equal(f["rep_idx"].cpu().numpy(), ref)
+    reps = p[ref]
+    assert_normals(f["normals"].cpu().numpy(), O.estimate_normals(reps, O.KNN, 30), reps, k=30, what="c4_50m")
+    assert_neighbour_sets(dn.ids(), reps, 30, "c4_50m")
+
+
+def test_icp_10m_parity(dev):
+    """C3's ICP (10M box-surface source and target, 30 iterations from T = I)
+    against the oracle's registration_icp on the same inputs: T within 1e-5."""
+    n = 10_000_000
+    tgt = S.box_surface(n, 1, device=dev)
+    src = S.apply_transform(S.box_surface(n, 2, device=dev), S.rigid_transform())
+    tn = ops.estimate_normals(tgt, knn=30)
+    res = ops.registration_icp(src, tgt, tn, 0.02, max_iteration=30, relative_fitness=0, relative_rmse=0,
+                               return_corr=False)
+    T, fit, rmse, _ = O.registration_icp(src.cpu().numpy(), tgt.cpu().numpy(), tn.cpu().numpy(), 0.02,
+                                         max_iteration=30, relative_fitness=0, relative_rmse=0)
+    np.testing.assert_allclose(res["transformation"], T, atol=1e-5)
+    assert abs(res["fitness"] - fit) < 1e-6 and abs(res["inlier_rmse"] - rmse) < 1e-6
+    assert np.abs(res["transformation"] - np.linalg.inv(S.rigid_transform())).max() < 1e-5
+
+
+def test_c5_200m_properties(dev):
+    """C5 (200M box-surface scene) through the whole pipeline on one GPU,
+    checked by size-independent properties: every representative is the
+    largest index of its voxel (voxel trace), normals are unit length, the
+    per-hypothesis RANSAC counts equal an exact float64 re-score of sampled
+    hypotheses, and ICP of an independent 200M sample moved by T_gt recovers
+    T_gt^-1."""
+    from oracle import np_restate as NPR
+    n = 200_000_000
+    vs = 0.0005
+    tgt = S.box_surface(n, 1, device=dev)
+    out = ops.voxel_down_sample(tgt, vs, trace=True)
+    rep = out["rep_idx"].long()
+    vop = out["voxel_of_point"].long()
+    M = rep.numel()
+    mx = torch.full((M,), -1, dtype=torch.long, device=dev)
+    mx.scatter_reduce_(0, vop, torch.arange(n, device=dev), reduce="amax")
+    assert torch.equal(mx, rep)
+    assert bool((rep[1:] > rep[:-1]).all())
+    del vop, mx, tgt
+    torch.cuda.empty_cache()
+    treps = out["rep_xyz"]
+    tn = ops.estimate_normals(treps, knn=30)
+    assert float((tn.norm(dim=1) - 1).abs().max()) < 1e-5
+    samples = ops.ransac_samples(M, 3, 1000, seed=7)
+    r64 = treps.cpu().numpy().astype(np.float64)
+    planes = np.stack([NPR.triangle_plane(*r64[s]) for s in samples])
+    counts = ops.plane_count(treps, planes, 0.002)
+    for h in (0, 1, 499, 998, int(np.argmax(counts))):
+        if counts[h] >= 0:
+            assert counts[h] == int((NPR.plane_dist(planes[h], r64) < 0.002).sum()), h
+    del r64
+    src = S.apply_transform(S.box_surface(n, 2, device=dev), S.rigid_transform())
+    sreps = ops.voxel_down_sample(src, vs)["rep_xyz"]
+    del src
+    torch.cuda.empty_cache()
+    res = ops.registration_icp(sreps, treps, tn, 0.02, max_iteration=30, relative_fitness=0, relative_rmse=0,
+                               return_corr=False)
+    assert np.abs(res["transformation"] - np.linalg.inv(S.rigid_transform())).max() < 1e-5
