@@ -117,6 +117,107 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
   for (int h = threadIdx.x; h < hc; h += kBlock) partial[(int64_t)blockIdx.x * H + h0 + h] = cnt[h];
 }
 
+// ---------------------------------------------------------------------------
+// The same counts with the distances on the matrix cores.  All hypotheses
+// against all points is a dense (N x 4) . (4 x H) product: one
+// v_mfma_f32_16x16x4_f32 gives 16 points x 16 hypotheses, and its result is
+// bit for bit the k-ordered fmaf chain (MI355X: "exact f32 (== fmaf chain,
+// bitwise)") — with k = (1 | d), (z | c), (y | b), (x | a) it is
+// fma(a, x, fma(b, y, fma(c, z, d))), the VALU kernel's distance exactly, so
+// the same float32 band applies.  The VALU only compares and counts (two
+// v_cmp + one v_addc per result) while the matrix pipe computes; lanes hold
+// per-hypothesis counters (lane l: hypothesis l & 15 of each tile, points
+// (l >> 4) * 4 + r), summed over the four lanes of a hypothesis at the end.
+// A result inside the band is re-decided in float64 in Open3D's order.
+// One wave = a range of points x kMfHT tiles of 16 hypotheses.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kMfHT = 16;   // hypothesis tiles per wave (256 hypotheses)
+constexpr int kMfU = 4;     // 16-point steps per loop trip (loads in flight)
+
+__global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __restrict__ xyz, int64_t n,
+                                                             const float4* __restrict__ pl32,
+                                                             const float4* __restrict__ band,
+                                                             const double* __restrict__ pl64, int H, double thr,
+                                                             int64_t steps_per_wave, int nwp,
+                                                             int32_t* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int wp = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // point range of this wave
+  if (wp >= nwp) return;
+  const int hbase = blockIdx.y * (16 * kMfHT);
+  const int kk = lane >> 4, jj = lane & 15;
+  float bv[kMfHT], lo[kMfHT], hi[kMfHT];
+  int cnt[kMfHT];
+#pragma unroll
+  for (int t = 0; t < kMfHT; ++t) {
+    const int h = hbase + 16 * t + jj;
+    if (h < H) {
+      const float4 P = pl32[h];
+      const float4 B = band[h];
+      bv[t] = kk == 0 ? P.w : kk == 1 ? P.z : kk == 2 ? P.y : P.x;
+      lo[t] = B.x;
+      hi[t] = B.y;
+    } else {
+      bv[t] = 0.0f;
+      lo[t] = -1.0f;  // never counted
+      hi[t] = -1.0f;
+    }
+    cnt[t] = 0;
+  }
+  const float qnan = __int_as_float(0x7fc00000);
+  const int comp = 3 - kk;  // A[i][k]: k = 0 -> 1, 1 -> z, 2 -> y, 3 -> x
+  const int64_t s0 = (int64_t)wp * steps_per_wave;
+  for (int64_t st = 0; st < steps_per_wave; st += kMfU) {
+    float a[kMfU];
+#pragma unroll
+    for (int u = 0; u < kMfU; ++u) {
+      const int64_t pt = (s0 + st + u) * 16 + jj;
+      a[u] = kk == 0 ? 1.0f : (pt < n ? xyz[3 * pt + comp] : qnan);
+    }
+#pragma unroll
+    for (int u = 0; u < kMfU; ++u) {
+      if (st + u >= steps_per_wave) break;  // wave-uniform
+      bool amb[4] = {false, false, false, false};
+#pragma unroll
+      for (int t = 0; t < kMfHT; ++t) {
+        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = fabsf(d[r]);
+          const bool in = e < lo[t];
+          cnt[t] += in ? 1 : 0;
+          amb[r] |= !in && e < hi[t];
+        }
+      }
+      bool anyamb = amb[0] || amb[1] || amb[2] || amb[3];
+      if (__ballot(anyamb)) {  // rare: redo this step's band results in float64, Open3D's order
+#pragma unroll
+        for (int t = 0; t < kMfHT; ++t) {
+          const int h = hbase + 16 * t + jj;
+          const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = fabsf(d[r]);
+            const int64_t pt = (s0 + st + u) * 16 + kk * 4 + r;
+            if (!(e < lo[t]) && e < hi[t] && h < H && pt < n) {
+              const double* pl = pl64 + 4 * h;
+              cnt[t] += plane_dist64(pl, xyz[3 * pt], xyz[3 * pt + 1], xyz[3 * pt + 2]) < thr ? 1 : 0;
+            }
+          }
+        }
+      }
+    }
+  }
+  // the four lanes of a hypothesis (jj, jj + 16, jj + 32, jj + 48)
+#pragma unroll
+  for (int t = 0; t < kMfHT; ++t) {
+    int c = cnt[t];
+    c += __shfl_xor(c, 16, 64);
+    c += __shfl_xor(c, 32, 64);
+    const int h = hbase + 16 * t + jj;
+    if (kk == 0 && h < H) partial[(int64_t)wp * H + h] = c;
+  }
+}
+
 __global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H, int64_t* __restrict__ counts) {
   int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h < H && degenerate[h]) counts[h] = -1;
@@ -253,6 +354,8 @@ static void plane_from_pts(const double* P, int k, double pl[4]) {
 static bool plane_is_zero(const double* pl) { return pl[0] == 0 && pl[1] == 0 && pl[2] == 0 && pl[3] == 0; }
 
 // ------------------------------------------------------------ workspaces
+constexpr int kMfWaves = 2048;  // point ranges of the MFMA count (waves per hypothesis chunk)
+
 static int count_blocks(int64_t n) {
   int64_t tiles = (n + (int64_t)kBlock * kPts - 1) / ((int64_t)kBlock * kPts);
   return (int)std::max<int64_t>(1, std::min<int64_t>(kCountBlocksMax, tiles));
@@ -275,7 +378,7 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   w->band = ar.take<float4>(H);
   w->pl64 = ar.take<double>(4 * (size_t)H);
   w->degen = ar.take<uint8_t>(H);
-  w->partial = ar.take<int32_t>((size_t)count_blocks(n) * H);
+  w->partial = ar.take<int32_t>((size_t)std::max(count_blocks(n), kMfWaves) * H);
   w->counts = ar.take<int64_t>(H);
   w->sum_partial = ar.take<double>((size_t)kSumBlocksX * H);
   w->sums = ar.take<double>(H);
@@ -334,12 +437,23 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   int rc;
   upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, s, &rc);
   if (rc) return rc;
-  const int nb = count_blocks(n);
+  int nb = count_blocks(n);
   KTimer kt("plane_count", s);
-  for (int h0 = 0; h0 < H; h0 += kHChunk) {
-    int hc = std::min(kHChunk, H - h0);
-    hipLaunchKernelGGL(k_plane_count, dim3(nb), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, h0, hc, thr,
+  if (!getenv("O3DX_RANSAC_VALU")) {
+    // matrix-core distances: waves = point ranges x chunks of 256 hypotheses
+    const int64_t steps = (n + 15) / 16;
+    const int nwp = (int)std::max<int64_t>(1, std::min<int64_t>(kMfWaves, (steps + 3) / 4));
+    const int64_t spw = (steps + nwp - 1) / nwp;
+    const dim3 grid((unsigned)((nwp + kBlock / 64 - 1) / (kBlock / 64)), (unsigned)((H + 16 * kMfHT - 1) / (16 * kMfHT)));
+    hipLaunchKernelGGL(k_plane_count_mfma, grid, dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, thr, spw, nwp,
                        w.partial);
+    nb = nwp;
+  } else {
+    for (int h0 = 0; h0 < H; h0 += kHChunk) {
+      int hc = std::min(kHChunk, H - h0);
+      hipLaunchKernelGGL(k_plane_count, dim3(nb), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, h0, hc, thr,
+                         w.partial);
+    }
   }
   O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nb, H, w.counts, s));
   hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);

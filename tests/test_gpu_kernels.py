@@ -446,3 +446,25 @@ def test_voxel_down_sample_normals_fused(dev, bunny, case):
     reps = pts.numpy()[a["rep_idx"].cpu().numpy()]
     assert_normals(f["normals"].cpu().numpy(), O.estimate_normals(reps, O.KNN, 30), reps, k=30,
                    what=f"fused_{case}")
+
+
+@pytest.mark.parametrize("n,H", [(1, 3), (17, 5), (100_003, 257), (1_000_000, 1000)])
+def test_plane_count_mfma_equals_valu_and_oracle(dev, n, H, monkeypatch):
+    """k_plane_count_mfma (matrix-core distances) and the VALU kernel give
+    the same exact counts, equal to the oracle's, for ragged sizes (n not a
+    multiple of 16, H not of 256) and degenerate hypotheses."""
+    pts = S.planted_plane(max(n, 3), 61).numpy()[:n]
+    rng = np.random.default_rng(n)
+    samples = rng.integers(0, n, (H, 3)).astype(np.int32)
+    samples[0] = [0, 0, 0]  # degenerate (collinear / repeated): -1
+    planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
+    x = torch.from_numpy(pts).to(dev)
+    got = ops.plane_count(x, planes, 0.01)
+    monkeypatch.setenv("O3DX_RANSAC_VALU", "1")
+    valu = ops.plane_count(x, planes, 0.01)
+    monkeypatch.delenv("O3DX_RANSAC_VALU")
+    assert np.array_equal(got, valu)
+    ref = NPR.segment_plane_counts(pts, 0.01, samples) if n <= 100_003 else None
+    if ref is not None:
+        assert np.array_equal(got, ref)
+    assert got[0] == -1
