@@ -128,27 +128,30 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
 // v_cmp + one v_addc per result) while the matrix pipe computes; lanes hold
 // per-hypothesis counters (lane l: hypothesis l & 15 of each tile, points
 // (l >> 4) * 4 + r), summed over the four lanes of a hypothesis at the end.
-// A result inside the band is re-decided in float64 in Open3D's order.
-// One wave = a range of points x kMfHT tiles of 16 hypotheses.
+// A result inside the band is appended to a fix-up list (point, hypothesis)
+// that k_plane_fixup re-decides in float64 in Open3D's order afterwards (the
+// main loop carries no float64 code).  One wave = a range of points x HT
+// tiles of 16 hypotheses.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kMfHT = 16;   // hypothesis tiles per wave (256 hypotheses)
-constexpr int kMfU = 4;     // 16-point steps per loop trip (loads in flight)
+constexpr int kMfU = 2;           // 16-point steps per loop trip (loads in flight)
+constexpr int kFixCap = 1 << 20;  // fix-up entries (overflow: the VALU kernel redoes the counts)
 
+template <int HT>
 __global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __restrict__ xyz, int64_t n,
                                                              const float4* __restrict__ pl32,
-                                                             const float4* __restrict__ band,
-                                                             const double* __restrict__ pl64, int H, double thr,
+                                                             const float4* __restrict__ band, int H,
                                                              int64_t steps_per_wave, int nwp,
-                                                             int32_t* __restrict__ partial) {
+                                                             int32_t* __restrict__ partial, int2* __restrict__ fix,
+                                                             int32_t* __restrict__ fix_len) {
   const int lane = threadIdx.x & 63;
   const int wp = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // point range of this wave
   if (wp >= nwp) return;
-  const int hbase = blockIdx.y * (16 * kMfHT);
+  const int hbase = blockIdx.y * (16 * HT);
   const int kk = lane >> 4, jj = lane & 15;
-  float bv[kMfHT], lo[kMfHT], hi[kMfHT];
-  int cnt[kMfHT];
+  float bv[HT], lo[HT], hi[HT];
+  int cnt[HT];
 #pragma unroll
-  for (int t = 0; t < kMfHT; ++t) {
+  for (int t = 0; t < HT; ++t) {
     const int h = hbase + 16 * t + jj;
     if (h < H) {
       const float4 P = pl32[h];
@@ -171,36 +174,35 @@ __global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __rest
 #pragma unroll
     for (int u = 0; u < kMfU; ++u) {
       const int64_t pt = (s0 + st + u) * 16 + jj;
-      a[u] = kk == 0 ? 1.0f : (pt < n ? xyz[3 * pt + comp] : qnan);
+      a[u] = kk == 0 ? 1.0f : (pt < n && st + u < steps_per_wave ? xyz[3 * pt + comp] : qnan);
     }
 #pragma unroll
     for (int u = 0; u < kMfU; ++u) {
-      if (st + u >= steps_per_wave) break;  // wave-uniform
-      bool amb[4] = {false, false, false, false};
 #pragma unroll
-      for (int t = 0; t < kMfHT; ++t) {
+      for (int t = 0; t < HT; ++t) {
         const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        bool amb = false;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = fabsf(d[r]);
           const bool in = e < lo[t];
           cnt[t] += in ? 1 : 0;
-          amb[r] |= !in && e < hi[t];
+          amb |= !in && e < hi[t];
         }
-      }
-      bool anyamb = amb[0] || amb[1] || amb[2] || amb[3];
-      if (__ballot(anyamb)) {  // rare: redo this step's band results in float64, Open3D's order
-#pragma unroll
-        for (int t = 0; t < kMfHT; ++t) {
-          const int h = hbase + 16 * t + jj;
-          const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        if (__ballot(amb)) {  // rare: band results to the float64 fix-up list
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float e = fabsf(d[r]);
-            const int64_t pt = (s0 + st + u) * 16 + kk * 4 + r;
-            if (!(e < lo[t]) && e < hi[t] && h < H && pt < n) {
-              const double* pl = pl64 + 4 * h;
-              cnt[t] += plane_dist64(pl, xyz[3 * pt], xyz[3 * pt + 1], xyz[3 * pt + 2]) < thr ? 1 : 0;
+            const bool am = !(e < lo[t]) && e < hi[t];
+            const uint64_t m = __ballot(am);
+            if (m) {
+              int base = 0;
+              if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(fix_len, __popcll(m));
+              base = __shfl(base, __ffsll((unsigned long long)m) - 1, 64);
+              const int at = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+              if (am && at < kFixCap)
+                fix[at] = make_int2((int)((s0 + st + u) * 16 + kk * 4 + r), hbase + 16 * t + jj);
             }
           }
         }
@@ -209,12 +211,28 @@ __global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __rest
   }
   // the four lanes of a hypothesis (jj, jj + 16, jj + 32, jj + 48)
 #pragma unroll
-  for (int t = 0; t < kMfHT; ++t) {
+  for (int t = 0; t < HT; ++t) {
     int c = cnt[t];
     c += __shfl_xor(c, 16, 64);
     c += __shfl_xor(c, 32, 64);
     const int h = hbase + 16 * t + jj;
     if (kk == 0 && h < H) partial[(int64_t)wp * H + h] = c;
+  }
+}
+
+// The band entries of k_plane_count_mfma, decided in float64 (Open3D's order).
+__global__ void __launch_bounds__(kBlock) k_plane_fixup(const float* __restrict__ xyz, int64_t n,
+                                                        const double* __restrict__ pl64, double thr,
+                                                        const int2* __restrict__ fix,
+                                                        const int32_t* __restrict__ fix_len,
+                                                        int64_t* __restrict__ counts) {
+  const int len = min(*fix_len, kFixCap);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
+    const int2 e = fix[i];
+    if (e.x < 0 || (int64_t)e.x >= n) continue;
+    const double* pl = pl64 + 4 * (int64_t)e.y;
+    if (plane_dist64(pl, xyz[3 * (int64_t)e.x], xyz[3 * (int64_t)e.x + 1], xyz[3 * (int64_t)e.x + 2]) < thr)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&counts[e.y]), 1ull);
   }
 }
 
@@ -367,6 +385,8 @@ struct CountWs {
   double* pl64;
   uint8_t* degen;
   int32_t* partial;
+  int2* fix;
+  int32_t* fix_len;
   int64_t* counts;
   double* sum_partial;
   double* sums;
@@ -379,6 +399,8 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   w->pl64 = ar.take<double>(4 * (size_t)H);
   w->degen = ar.take<uint8_t>(H);
   w->partial = ar.take<int32_t>((size_t)std::max(count_blocks(n), kMfWaves) * H);
+  w->fix = ar.take<int2>(kFixCap);
+  w->fix_len = ar.take<int32_t>(4);
   w->counts = ar.take<int64_t>(H);
   w->sum_partial = ar.take<double>((size_t)kSumBlocksX * H);
   w->sums = ar.take<double>(H);
@@ -439,14 +461,23 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   if (rc) return rc;
   int nb = count_blocks(n);
   KTimer kt("plane_count", s);
-  if (!getenv("O3DX_RANSAC_VALU")) {
-    // matrix-core distances: waves = point ranges x chunks of 256 hypotheses
+  const bool mfma = !getenv("O3DX_RANSAC_VALU");
+  if (mfma) {
+    // matrix-core distances: waves = point ranges x chunks of 16 HT hypotheses
+    const char* ht_env = getenv("O3DX_RANSAC_HT");
+    const int ht = ht_env ? atoi(ht_env) : 8;
     const int64_t steps = (n + 15) / 16;
     const int nwp = (int)std::max<int64_t>(1, std::min<int64_t>(kMfWaves, (steps + 3) / 4));
     const int64_t spw = (steps + nwp - 1) / nwp;
-    const dim3 grid((unsigned)((nwp + kBlock / 64 - 1) / (kBlock / 64)), (unsigned)((H + 16 * kMfHT - 1) / (16 * kMfHT)));
-    hipLaunchKernelGGL(k_plane_count_mfma, grid, dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, thr, spw, nwp,
-                       w.partial);
+    O3DX_HIP(hipMemsetAsync(w.fix_len, 0, sizeof(int32_t), s));
+    const unsigned gx = (unsigned)((nwp + kBlock / 64 - 1) / (kBlock / 64));
+#define O3DX_MF(HT)                                                                                          \
+  hipLaunchKernelGGL(k_plane_count_mfma<HT>, dim3(gx, (unsigned)((H + 16 * HT - 1) / (16 * HT))), dim3(kBlock), \
+                     0, s, xyz, n, w.pl32, w.band, H, spw, nwp, w.partial, w.fix, w.fix_len)
+    if (ht == 16) O3DX_MF(16);
+    else if (ht == 4) O3DX_MF(4);
+    else O3DX_MF(8);
+#undef O3DX_MF
     nb = nwp;
   } else {
     for (int h0 = 0; h0 < H; h0 += kHChunk) {
@@ -456,6 +487,19 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
     }
   }
   O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nb, H, w.counts, s));
+  if (mfma) {
+    hipLaunchKernelGGL(k_plane_fixup, dim3(256), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, w.fix, w.fix_len, w.counts);
+    int32_t nfix = 0;
+    O3DX_TRY(read_back(&nfix, w.fix_len, sizeof(nfix), s));
+    if (nfix > kFixCap) {  // pathological band crowding: the VALU kernel decides every point
+      for (int h0 = 0; h0 < H; h0 += kHChunk) {
+        int hc = std::min(kHChunk, H - h0);
+        hipLaunchKernelGGL(k_plane_count, dim3(count_blocks(n)), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64,
+                           H, h0, hc, thr, w.partial);
+      }
+      O3DX_TRY(reduce_columns_i32_to_i64(w.partial, count_blocks(n), H, w.counts, s));
+    }
+  }
   hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
   kt.stop();
   counts.resize(H);
