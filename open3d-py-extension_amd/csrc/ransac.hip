@@ -16,6 +16,7 @@
 // exactly as Open3D evaluates |(a x + c z) + (b y + d)| < thr; inlier counts
 // are ballot-popcounts into LDS.  Sigma|d| (only needed to break fitness ties)
 // is computed exactly in float64 for the tied hypotheses only.
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -123,88 +124,112 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
 // v_mfma_f32_16x16x4_f32 gives 16 points x 16 hypotheses, and its result is
 // bit for bit the k-ordered fmaf chain (MI355X: "exact f32 (== fmaf chain,
 // bitwise)") — with k = (1 | d), (z | c), (y | b), (x | a) it is
-// fma(a, x, fma(b, y, fma(c, z, d))), the VALU kernel's distance exactly, so
-// the same float32 band applies.  The VALU only compares and counts (two
-// v_cmp + one v_addc per result) while the matrix pipe computes; lanes hold
-// per-hypothesis counters (lane l: hypothesis l & 15 of each tile, points
-// (l >> 4) * 4 + r), summed over the four lanes of a hypothesis at the end.
-// A result inside the band is appended to a fix-up list (point, hypothesis)
-// that k_plane_fixup re-decides in float64 in Open3D's order afterwards (the
-// main loop carries no float64 code).  One wave = a range of points x HT
-// tiles of 16 hypotheses.
+// fma(a, x, fma(b, y, fma(c, z, d))), the VALU kernel's distance exactly.
+// The band is one window [lo, hi) for all hypotheses (the union of their
+// float32 windows), so the VALU does ~3.5 operations per result:
+//   x = |d| - lo            (sign bit set <=> |d| < lo: an inlier)
+//   cnt += bits(x) >> 31
+//   mn = umin(mn, bits(x))  (0 <= x <= fl(hi - lo) <=> bits(x) <= bits(W))
+// A step with any result in the window (rare) re-issues its products and
+// sets one bit per 16-hypothesis tile in a (step, tile) bitmap;
+// k_plane_fixup re-decides those tiles' window results in float64 in
+// Open3D's order.  No call, no list, no capacity: the hot loop carries only
+// the one ballot per step.  Lanes hold per-hypothesis counters (lane l:
+// hypothesis l & 15 of each tile, points (l >> 4) * 4 + r), summed over the
+// four lanes of a hypothesis at the end.  Rows past the wave's range or past
+// n are all-zero (distance 0): they count as inliers of every hypothesis when
+// lo > 0 and the host subtracts that known padding.  One wave = a range of
+// points x HT tiles of 16 hypotheses.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kMfU = 2;           // 16-point steps per loop trip (loads in flight)
-constexpr int kFixCap = 1 << 20;  // fix-up entries (overflow: the VALU kernel redoes the counts)
+constexpr int kMfU = 2;  // 16-point steps per loop trip (loads in flight)
 
 template <int HT>
 __global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __restrict__ xyz, int64_t n,
-                                                             const float4* __restrict__ pl32,
-                                                             const float4* __restrict__ band, int H,
-                                                             int64_t steps_per_wave, int nwp,
-                                                             int32_t* __restrict__ partial, int2* __restrict__ fix,
-                                                             int32_t* __restrict__ fix_len) {
+                                                             const float4* __restrict__ pl32, int H, float lo,
+                                                             uint32_t wbits, int64_t steps_per_wave, int nwp,
+                                                             int wps, int32_t* __restrict__ partial,
+                                                             uint32_t* __restrict__ flags) {
   const int lane = threadIdx.x & 63;
-  const int wp = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // point range of this wave
+  // point range of this wave (wave-uniform: scalar registers)
+  const int wp = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
   if (wp >= nwp) return;
   const int hbase = blockIdx.y * (16 * HT);
   const int kk = lane >> 4, jj = lane & 15;
-  float bv[HT], lo[HT], hi[HT];
-  int cnt[HT];
+  float bv[HT];
+  uint32_t cnt[HT];
 #pragma unroll
   for (int t = 0; t < HT; ++t) {
     const int h = hbase + 16 * t + jj;
+    float b = 0.0f;
     if (h < H) {
       const float4 P = pl32[h];
-      const float4 B = band[h];
-      bv[t] = kk == 0 ? P.w : kk == 1 ? P.z : kk == 2 ? P.y : P.x;
-      lo[t] = B.x;
-      hi[t] = B.y;
-    } else {
-      bv[t] = 0.0f;
-      lo[t] = -1.0f;  // never counted
-      hi[t] = -1.0f;
+      b = kk == 0 ? P.w : kk == 1 ? P.z : kk == 2 ? P.y : P.x;
     }
+    bv[t] = b;
     cnt[t] = 0;
   }
-  const float qnan = __int_as_float(0x7fc00000);
   const int comp = 3 - kk;  // A[i][k]: k = 0 -> 1, 1 -> z, 2 -> y, 3 -> x
   const int64_t s0 = (int64_t)wp * steps_per_wave;
+  const int64_t plim = min(n, (s0 + steps_per_wave) * 16);  // this wave's points end here
+  // the wave's points as a buffer resource: loads past plim return 0 with no
+  // branch, so the next trip's loads stay in flight across this trip
+  const int64_t pbase = s0 * 16;
+  const uint64_t base = reinterpret_cast<uint64_t>(xyz + 3 * pbase);
+  const int nbytes = (int)(max<int64_t>(plim - pbase, 0) * 12);
+  auto load = [&](int64_t st, float (&a)[kMfU]) {
+    // rebuilt from scalars at each use: a resource the allocator parks in
+    // VGPRs would be re-made uniform by a waterfall loop per load
+    const uint64_t b = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)base) |
+                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(b), (short)0, __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < kMfU; ++u) {
+      const int off = (int)((st + u) * 16 + jj);  // point offset inside the wave's range
+      // k = 0 lanes load out of range (0) and OR in the constant 1 of a valid row
+      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, kk == 0 ? 0x7ffffff0 : off * 12 + comp * 4, 0, 0);
+      const uint32_t one = (kk == 0 && pbase + off < plim) ? 0x3f800000u : 0u;
+      a[u] = __uint_as_float(v | one);
+    }
+  };
+  float an[kMfU];
+  load(0, an);
   for (int64_t st = 0; st < steps_per_wave; st += kMfU) {
     float a[kMfU];
 #pragma unroll
-    for (int u = 0; u < kMfU; ++u) {
-      const int64_t pt = (s0 + st + u) * 16 + jj;
-      a[u] = kk == 0 ? 1.0f : (pt < n && st + u < steps_per_wave ? xyz[3 * pt + comp] : qnan);
-    }
+    for (int u = 0; u < kMfU; ++u) a[u] = an[u];
+    load(st + kMfU, an);  // next trip's points in flight during this one
 #pragma unroll
     for (int u = 0; u < kMfU; ++u) {
+      // all tiles' products first (independent results keep the matrix pipe
+      // busy), then the compares
+      f32x4 d[HT];
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+        d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t mn = ~0u;
 #pragma unroll
       for (int t = 0; t < HT; ++t) {
-        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        bool amb = false;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = fabsf(d[r]);
-          const bool in = e < lo[t];
-          cnt[t] += in ? 1 : 0;
-          amb |= !in && e < hi[t];
+          const uint32_t x = __float_as_uint(fabsf(d[t][r]) - lo);
+          cnt[t] += x >> 31;
+          mn = min(mn, x);
         }
-        if (__ballot(amb)) {  // rare: band results to the float64 fix-up list
+      }
+      if (__ballot(mn <= wbits) && st + u < steps_per_wave) {
+        // rare: which tiles hold window results (products re-issued, not kept live)
+        const int64_t g = s0 + st + u;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float e = fabsf(d[r]);
-            const bool am = !(e < lo[t]) && e < hi[t];
-            const uint64_t m = __ballot(am);
-            if (m) {
-              int base = 0;
-              if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(fix_len, __popcll(m));
-              base = __shfl(base, __ffsll((unsigned long long)m) - 1, 64);
-              const int at = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-              if (am && at < kFixCap)
-                fix[at] = make_int2((int)((s0 + st + u) * 16 + kk * 4 + r), hbase + 16 * t + jj);
-            }
-          }
+        for (int t = 0; t < HT; ++t) {
+          const f32x4 e = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          uint32_t m2 = ~0u;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) m2 = min(m2, __float_as_uint(fabsf(e[r]) - lo));
+          const int tile = hbase / 16 + t;
+          if (__ballot(m2 <= wbits) && lane == 0)
+            atomicOr(&flags[g * wps + (tile >> 5)], 1u << (tile & 31));
         }
       }
     }
@@ -212,7 +237,7 @@ __global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __rest
   // the four lanes of a hypothesis (jj, jj + 16, jj + 32, jj + 48)
 #pragma unroll
   for (int t = 0; t < HT; ++t) {
-    int c = cnt[t];
+    int c = (int)cnt[t];
     c += __shfl_xor(c, 16, 64);
     c += __shfl_xor(c, 32, 64);
     const int h = hbase + 16 * t + jj;
@@ -220,25 +245,49 @@ __global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __rest
   }
 }
 
-// The band entries of k_plane_count_mfma, decided in float64 (Open3D's order).
+// The flagged (step, tile) blocks of k_plane_count_mfma: each window result
+// (the same float32 distance, fmaf chain) decided in float64 in Open3D's
+// order.  A wave takes 64 bitmap words; per set bit, its 256 pairs as
+// 4 per lane (point lane & 15, hypotheses 4 (lane >> 4) + q).
 __global__ void __launch_bounds__(kBlock) k_plane_fixup(const float* __restrict__ xyz, int64_t n,
-                                                        const double* __restrict__ pl64, double thr,
-                                                        const int2* __restrict__ fix,
-                                                        const int32_t* __restrict__ fix_len,
-                                                        int64_t* __restrict__ counts) {
-  const int len = min(*fix_len, kFixCap);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
-    const int2 e = fix[i];
-    if (e.x < 0 || (int64_t)e.x >= n) continue;
-    const double* pl = pl64 + 4 * (int64_t)e.y;
-    if (plane_dist64(pl, xyz[3 * (int64_t)e.x], xyz[3 * (int64_t)e.x + 1], xyz[3 * (int64_t)e.x + 2]) < thr)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&counts[e.y]), 1ull);
+                                                        const float4* __restrict__ pl32,
+                                                        const double* __restrict__ pl64, int H, double thr, float lo,
+                                                        uint32_t wbits, const uint32_t* __restrict__ flags,
+                                                        int64_t nwords, int wps, int64_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 64;
+  if (w0 >= nwords) return;
+  const uint32_t word = w0 + lane < nwords ? flags[w0 + lane] : 0u;
+  uint64_t m = __ballot(word != 0);
+  while (m) {
+    const int i = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    uint32_t wd = (uint32_t)__shfl((int)word, i, 64);
+    const int64_t g = (w0 + i) / wps;
+    const int tbase = (int)((w0 + i) % wps) * 32;
+    const int64_t p = g * 16 + (lane & 15);
+    float x = 0.f, y = 0.f, z = 0.f;
+    if (p < n) x = xyz[3 * p], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
+    while (wd) {
+      const int tile = tbase + __ffs((int)wd) - 1;
+      wd &= wd - 1;
+      for (int q = 0; q < 4; ++q) {
+        const int h = tile * 16 + (lane >> 4) * 4 + q;
+        if (p >= n || h >= H) continue;
+        const float4 P = pl32[h];
+        const float d = fmaf(P.x, x, fmaf(P.y, y, fmaf(P.z, z, P.w)));
+        if (__float_as_uint(fabsf(d) - lo) <= wbits && plane_dist64(pl64 + 4 * (int64_t)h, x, y, z) < thr)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&counts[h]), 1ull);
+      }
+    }
   }
 }
 
-__global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H, int64_t* __restrict__ counts) {
+// degenerate hypotheses -> -1; the others lose the padding rows they counted
+__global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H, int64_t pad,
+                                  int64_t* __restrict__ counts) {
   int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h < H && degenerate[h]) counts[h] = -1;
+  if (h < H) counts[h] = degenerate[h] ? -1 : counts[h] - pad;
 }
 
 constexpr int kSumBlocksX = 64;
@@ -374,6 +423,20 @@ static bool plane_is_zero(const double* pl) { return pl[0] == 0 && pl[1] == 0 &&
 // ------------------------------------------------------------ workspaces
 constexpr int kMfWaves = 2048;  // point ranges of the MFMA count (waves per hypothesis chunk)
 
+// MFMA count geometry: nwp point ranges of spw 16-point steps each
+static void mf_geometry(int64_t n, int* nwp, int64_t* spw) {
+  const int64_t steps = (n + 15) / 16;
+  *nwp = (int)std::max<int64_t>(1, std::min<int64_t>(kMfWaves, (steps + 3) / 4));
+  *spw = (steps + *nwp - 1) / *nwp;
+}
+
+static int64_t mf_flag_words(int64_t n, int H) {
+  int nwp;
+  int64_t spw;
+  mf_geometry(n, &nwp, &spw);
+  return (int64_t)nwp * spw * (((H + 15) / 16 + 31) / 32);
+}
+
 static int count_blocks(int64_t n) {
   int64_t tiles = (n + (int64_t)kBlock * kPts - 1) / ((int64_t)kBlock * kPts);
   return (int)std::max<int64_t>(1, std::min<int64_t>(kCountBlocksMax, tiles));
@@ -385,8 +448,7 @@ struct CountWs {
   double* pl64;
   uint8_t* degen;
   int32_t* partial;
-  int2* fix;
-  int32_t* fix_len;
+  uint32_t* flags;  // (step, 16-hypothesis tile) bitmap of the MFMA count
   int64_t* counts;
   double* sum_partial;
   double* sums;
@@ -399,8 +461,7 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   w->pl64 = ar.take<double>(4 * (size_t)H);
   w->degen = ar.take<uint8_t>(H);
   w->partial = ar.take<int32_t>((size_t)std::max(count_blocks(n), kMfWaves) * H);
-  w->fix = ar.take<int2>(kFixCap);
-  w->fix_len = ar.take<int32_t>(4);
+  w->flags = ar.take<uint32_t>((size_t)mf_flag_words(n, H));
   w->counts = ar.take<int64_t>(H);
   w->sum_partial = ar.take<double>((size_t)kSumBlocksX * H);
   w->sums = ar.take<double>(H);
@@ -461,46 +522,57 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   if (rc) return rc;
   int nb = count_blocks(n);
   KTimer kt("plane_count", s);
-  const bool mfma = !getenv("O3DX_RANSAC_VALU");
+  // the matrix-core path needs finite planes (its single window and sign-bit
+  // count); any other hypothesis set goes to the VALU kernel
+  bool finite = true;
+  for (int h = 0; h < 4 * H; ++h) finite = finite && std::isfinite(planes[h]);
+  const bool mfma = finite && !getenv("O3DX_RANSAC_VALU");
+  int64_t pad = 0;
   if (mfma) {
+    // one window for all hypotheses: the union of their float32 windows
+    float lo = -1.0f, hi = -1.0f;
+    bool any = false;
+    for (int h = 0; h < H; ++h)
+      if (!dg[h]) {
+        lo = any ? std::min(lo, bnd[h].x) : bnd[h].x;
+        hi = any ? std::max(hi, bnd[h].y) : bnd[h].y;
+        any = true;
+      }
+    const float wdt = hi - lo;  // >= 0; fl() is monotone, so |d| < hi => fl(|d| - lo) <= wdt
+    uint32_t wbits;
+    std::memcpy(&wbits, &wdt, 4);
     // matrix-core distances: waves = point ranges x chunks of 16 HT hypotheses
     const char* ht_env = getenv("O3DX_RANSAC_HT");
     const int ht = ht_env ? atoi(ht_env) : 8;
-    const int64_t steps = (n + 15) / 16;
-    const int nwp = (int)std::max<int64_t>(1, std::min<int64_t>(kMfWaves, (steps + 3) / 4));
-    const int64_t spw = (steps + nwp - 1) / nwp;
-    O3DX_HIP(hipMemsetAsync(w.fix_len, 0, sizeof(int32_t), s));
+    int nwp;
+    int64_t spw;
+    mf_geometry(n, &nwp, &spw);
+    const int wps = ((H + 15) / 16 + 31) / 32;  // bitmap words per step
+    const int64_t nwords = mf_flag_words(n, H);
+    O3DX_HIP(hipMemsetAsync(w.flags, 0, (size_t)nwords * sizeof(uint32_t), s));
     const unsigned gx = (unsigned)((nwp + kBlock / 64 - 1) / (kBlock / 64));
 #define O3DX_MF(HT)                                                                                          \
   hipLaunchKernelGGL(k_plane_count_mfma<HT>, dim3(gx, (unsigned)((H + 16 * HT - 1) / (16 * HT))), dim3(kBlock), \
-                     0, s, xyz, n, w.pl32, w.band, H, spw, nwp, w.partial, w.fix, w.fix_len)
+                     0, s, xyz, n, w.pl32, H, lo, wbits, spw, nwp, wps, w.partial, w.flags)
     if (ht == 16) O3DX_MF(16);
     else if (ht == 4) O3DX_MF(4);
     else O3DX_MF(8);
 #undef O3DX_MF
-    nb = nwp;
+    // all-zero rows (distance 0) counted by every hypothesis when 0 < lo
+    if (lo > 0.0f) pad = (int64_t)nwp * ((spw + kMfU - 1) / kMfU * kMfU) * 16 - n;
+    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));
+    const int64_t fwaves = (nwords + 63) / 64;
+    hipLaunchKernelGGL(k_plane_fixup, dim3((unsigned)((fwaves + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0,
+                       s, xyz, n, w.pl32, w.pl64, H, thr, lo, wbits, w.flags, nwords, wps, w.counts);
   } else {
     for (int h0 = 0; h0 < H; h0 += kHChunk) {
       int hc = std::min(kHChunk, H - h0);
       hipLaunchKernelGGL(k_plane_count, dim3(nb), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, h0, hc, thr,
                          w.partial);
     }
+    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nb, H, w.counts, s));
   }
-  O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nb, H, w.counts, s));
-  if (mfma) {
-    hipLaunchKernelGGL(k_plane_fixup, dim3(256), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, w.fix, w.fix_len, w.counts);
-    int32_t nfix = 0;
-    O3DX_TRY(read_back(&nfix, w.fix_len, sizeof(nfix), s));
-    if (nfix > kFixCap) {  // pathological band crowding: the VALU kernel decides every point
-      for (int h0 = 0; h0 < H; h0 += kHChunk) {
-        int hc = std::min(kHChunk, H - h0);
-        hipLaunchKernelGGL(k_plane_count, dim3(count_blocks(n)), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64,
-                           H, h0, hc, thr, w.partial);
-      }
-      O3DX_TRY(reduce_columns_i32_to_i64(w.partial, count_blocks(n), H, w.counts, s));
-    }
-  }
-  hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
+  hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, pad, w.counts);
   kt.stop();
   counts.resize(H);
   O3DX_TRY(read_back(counts.data(), w.counts, H * sizeof(int64_t), s));

@@ -27,6 +27,21 @@ from .params import KDTreeSearchParamKNN, resolve
 _SEED = [None]
 
 
+def _sor_keep_sequential(avg: np.ndarray, nv: int, std_ratio: float) -> np.ndarray:
+    """RemoveStatisticalOutliers' cloud statistics in Open3D's order:
+    std::accumulate of the positive means, std::inner_product of their
+    squared deviations (both sequential over the index), then the decision."""
+    pos = avg > 0
+    S = np.add.accumulate(np.where(pos, avg, 0.0))[-1]
+    m = S / nv
+    t = np.where(pos, (avg - m) * (avg - m), 0.0)
+    sq = np.add.accumulate(t)[-1]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        std = np.sqrt(sq / np.float64(nv - 1))
+    thr = m + std_ratio * std
+    return np.nonzero(pos & (avg < thr))[0].astype(np.int64)
+
+
 def set_random_seed(seed: int):
     """Counterpart of o3d.utility.random.seed: seeds segment_plane's sampler."""
     _SEED[0] = int(seed)
@@ -619,11 +634,25 @@ class PointCloudUtility(PointCloudSelections):
             return self.__class__()
         return self._select_by_idx(np.arange(self.size())[:: int(1 / down_sample_ratio)])
 
+    # scale of the rounding band around the outlier threshold (tests raise it
+    # to force the exact sequential re-decision on every call)
+    _SOR_BAND_SCALE = 8.0
+
     def remove_statistical_outlier(self, nb_neighbors: int = 20, std_ratio: float = 2.0,
                                    print_progress: bool = False):
-        """Open3D RemoveStatisticalOutliers (reference PointCloud.py:370-372):
-        mean distance to the nb_neighbors nearest (self included), keep points
-        with 0 < mean < cloud_mean + std_ratio * std (Bessel-corrected)."""
+        """Open3D RemoveStatisticalOutliers (reference PointCloud.py:370-372),
+        index-exact: per point the mean of sqrt(d2) over its nb_neighbors
+        nearest (self included), summed sequentially in ascending-distance
+        order on the GPU (float64, the kernel's exact d2); keep points with
+        0 < mean < cloud_mean + std_ratio * std (Bessel-corrected).
+
+        Open3D forms cloud_mean and std with sequential std::accumulate /
+        std::inner_product over all points in index order.  The GPU reduces
+        them in a different order; their difference is bounded (a rounding
+        band around the threshold).  When no point's mean lies inside that
+        band the GPU decision is Open3D's; otherwise the two statistics are
+        re-formed in Open3D's sequential order on the host (np.add.accumulate)
+        and every point is decided against that threshold."""
         if nb_neighbors < 1 or std_ratio <= 0:
             raise RuntimeError("Illegal input parameters, the number of neighbors and standard deviation "
                                "ratio must be positive.")
@@ -631,18 +660,35 @@ class PointCloudUtility(PointCloudSelections):
             return self.__class__(), []
         x = self._dev_points()
         idx, d2, cnt = ops.knn_search(x, x, mode=N.SEARCH_KNN, knn=nb_neighbors)
+        n = x.shape[0]
+        col = torch.arange(d2.shape[1], device=d2.device)
+        d = torch.where(col[None, :] < cnt[:, None].long(), torch.sqrt(d2.clamp_min(0)), torch.zeros_like(d2))
+        acc = torch.zeros(n, dtype=torch.float64, device=d2.device)
+        for j in range(d.shape[1]):  # std::accumulate order: ascending distance
+            acc = acc + d[:, j]
         valid = cnt > 0
-        d = torch.sqrt(torch.where(torch.isfinite(d2), d2, torch.zeros_like(d2)))
-        avg = torch.where(valid, d.sum(1) / cnt.clamp_min(1).double(), torch.full_like(d[:, 0], -1.0))
+        avg = torch.where(valid, acc / cnt.clamp_min(1).double(), torch.full_like(acc, -1.0))
         nv = int(valid.sum().item())
         if nv == 0:
             return self.__class__(), []
         pos = avg > 0
-        mean = avg[pos].sum() / nv
-        sq = torch.where(pos, (avg - mean) ** 2, torch.zeros_like(avg)).sum()
-        std = torch.sqrt(sq / (nv - 1)) if nv > 1 else torch.zeros_like(sq)
-        thr = mean + std_ratio * std
-        keep = torch.nonzero((avg > 0) & (avg < thr)).reshape(-1)
+        S = float(torch.where(pos, avg, torch.zeros_like(avg)).sum().item())
+        m = S / nv
+        sq = float(torch.where(pos, (avg - m) * (avg - m), torch.zeros_like(avg)).sum().item())
+        std = float(np.sqrt(sq / (nv - 1))) if nv > 1 else float("nan")
+        thr = m + std_ratio * std
+        # |GPU order - sequential order| bounds (first order, n-term sums)
+        E = (n + 4) * np.ldexp(1.0, -53)
+        dm = 2.0 * E * m
+        dsq = 2.0 * E * sq + 2.0 * dm * np.sqrt(max(n, 1) * sq)
+        dstd = (std * (dsq / (2.0 * sq) + E)) if sq > 0 and np.isfinite(std) else 2.0 * np.sqrt(dsq / max(nv - 1, 1))
+        band = self._SOR_BAND_SCALE * (dm + std_ratio * dstd) + abs(thr) * np.ldexp(1.0, -50)
+        near = int((pos & ((avg - thr).abs() <= band)).sum().item()) if np.isfinite(thr) else 0
+        if near == 0:
+            keep = torch.nonzero(pos & (avg < thr)).reshape(-1)
+        else:
+            a = avg.cpu().numpy()
+            keep = torch.from_numpy(_sor_keep_sequential(a, nv, std_ratio)).to(x.device)
         kept = keep.cpu().numpy().tolist()
         return self._select_by_idx(keep), kept
 

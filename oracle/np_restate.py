@@ -106,6 +106,34 @@ def segment_plane_counts(xyz, thr, samples):
     return np.array(out, np.int64)
 
 
+def remove_statistical_outlier(xyz, nb_neighbors, std_ratio, knn_d2):
+    """Open3D PointCloud::RemoveStatisticalOutliers (0.19, geometry/
+    PointCloud.cpp; the reference calls it at PointCloud.py:370-372):
+    mean of sqrt(d2) over the nb_neighbors nearest (self included; the
+    kd-tree's ascending order, std::accumulate), cloud mean over the positive
+    means (std::accumulate, index order), sum of squared deviations
+    (std::inner_product, index order), std with n - 1, keep
+    0 < mean < cloud_mean + std_ratio * std.  knn_d2: (n, k) float64 squared
+    distances of the kNN search (oracle.knn_search)."""
+    d2 = np.asarray(knn_d2, np.float64)
+    n = d2.shape[0]
+    if n == 0:
+        return np.zeros(0, np.int64)
+    k = min(nb_neighbors, n)
+    d = np.sqrt(d2[:, :k])
+    acc = np.zeros(n)
+    for j in range(k):
+        acc = acc + d[:, j]
+    avg = acc / k
+    pos = avg > 0
+    m = np.add.accumulate(np.where(pos, avg, 0.0))[-1] / n
+    sq = np.add.accumulate(np.where(pos, (avg - m) * (avg - m), 0.0))[-1]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        std = np.sqrt(sq / np.float64(n - 1))
+    thr = m + std_ratio * std
+    return np.nonzero(pos & (avg < thr))[0].astype(np.int64)
+
+
 # ---------------------------------------------------------------------------
 # Restatements of the reference's own torch branches (pinned by
 # tests/golden/ref_torch_branch.npz, generated from the reference itself).

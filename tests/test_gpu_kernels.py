@@ -355,6 +355,10 @@ def test_normals_on_voxel_grid_modes_and_prior(dev, bunny):
         got = ops.estimate_normals(reps, mode=mode, knn=kk, radius=r, voxel_grid=vg).cpu().numpy()
         ref = ops.estimate_normals(reps, mode=mode, knn=kk, radius=r).cpu().numpy()
         assert np.mean(np.abs(got - ref).max(1) < 1e-6) > 0.9999
+        if mode == O.HYBRID:
+            rp = reps.cpu().numpy()
+            assert_normals(got, O.estimate_normals(rp, mode, kk, r), rp, mode=mode, k=kk, radius=r,
+                           what="voxel_grid_hybrid")
     prior = -ops.estimate_normals(reps, knn=30)
     got = ops.estimate_normals(reps, knn=30, prior=prior, voxel_grid=vg)
     assert (torch.sum(got * prior, 1) >= 0).all()
@@ -448,23 +452,50 @@ def test_voxel_down_sample_normals_fused(dev, bunny, case):
                    what=f"fused_{case}")
 
 
-@pytest.mark.parametrize("n,H", [(1, 3), (17, 5), (100_003, 257), (1_000_000, 1000)])
-def test_plane_count_mfma_equals_valu_and_oracle(dev, n, H, monkeypatch):
+def test_plane_count_window_overflow_and_nonfinite(dev, monkeypatch):
+    """Every pair inside the float32 window (points at |d| == thr of z = 0):
+    the fix-up list overflows and the VALU kernel recounts; non-finite planes
+    take the VALU kernel too.  Both equal the oracle's counts."""
+    n = 1_200_000
+    rng = np.random.default_rng(3)
+    pts = np.stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n), np.full(n, 0.01)], 1).astype(np.float32)
+    pts[::3, 2] = -0.01
+    planes = np.array([[0.0, 0.0, 1.0, 0.0], [0.0, 0.0, -1.0, 0.0], [0.0, 0.6, 0.8, 0.0]])
+    x = torch.from_numpy(pts).to(dev)
+    got = ops.plane_count(x, planes, 0.01)
+    monkeypatch.setenv("O3DX_RANSAC_VALU", "1")
+    valu = ops.plane_count(x, planes, 0.01)
+    monkeypatch.delenv("O3DX_RANSAC_VALU")
+    p64 = pts.astype(np.float64)
+    ref = [int((np.abs(NPR.plane_dist(pl, p64)) < 0.01).sum()) for pl in planes]
+    assert got.tolist() == ref and valu.tolist() == ref
+    bad = np.vstack([planes, [[np.nan, 0.0, 1.0, 0.0]]])
+    got = ops.plane_count(x, bad, 0.01)
+    assert got[:3].tolist() == ref and got[3] == 0
+
+
+@pytest.mark.parametrize("n,H,thr,ht", [(1, 3, 0.01, "8"), (17, 5, 0.01, "8"), (100_003, 257, 0.01, "8"),
+                                        (100_003, 257, 0.01, "4"), (100_003, 257, 0.01, "16"),
+                                        (100_003, 257, 1e-7, "8"), (1_000_000, 1000, 0.01, "8")])
+def test_plane_count_mfma_equals_valu_and_oracle(dev, n, H, thr, ht, monkeypatch):
     """k_plane_count_mfma (matrix-core distances) and the VALU kernel give
     the same exact counts, equal to the oracle's, for ragged sizes (n not a
-    multiple of 16, H not of 256) and degenerate hypotheses."""
+    multiple of 16, H not of 256), degenerate hypotheses, every tile width,
+    and a threshold below the float32 window (lo < 0: padding rows are not
+    counted, the window holds the near-plane points)."""
+    monkeypatch.setenv("O3DX_RANSAC_HT", ht)
     pts = S.planted_plane(max(n, 3), 61).numpy()[:n]
     rng = np.random.default_rng(n)
     samples = rng.integers(0, n, (H, 3)).astype(np.int32)
     samples[0] = [0, 0, 0]  # degenerate (collinear / repeated): -1
     planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
     x = torch.from_numpy(pts).to(dev)
-    got = ops.plane_count(x, planes, 0.01)
+    got = ops.plane_count(x, planes, thr)
     monkeypatch.setenv("O3DX_RANSAC_VALU", "1")
-    valu = ops.plane_count(x, planes, 0.01)
+    valu = ops.plane_count(x, planes, thr)
     monkeypatch.delenv("O3DX_RANSAC_VALU")
     assert np.array_equal(got, valu)
-    ref = NPR.segment_plane_counts(pts, 0.01, samples) if n <= 100_003 else None
+    ref = NPR.segment_plane_counts(pts, thr, samples) if n <= 100_003 else None
     if ref is not None:
         assert np.array_equal(got, ref)
     assert got[0] == -1

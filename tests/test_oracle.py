@@ -81,8 +81,7 @@ def test_oracle_normals_match_reference_torch_normals(gold):
     ref = gold["torch_normals_k16"]
     got = O.estimate_normals(x, O.KNN, 16)
     err = np.minimum(np.abs(got - ref).max(1), np.abs(got + ref).max(1))
-    assert np.median(err) < 1e-5
-    assert np.mean(err < 1e-4) > 0.99
+    assert err.max() <= 1e-5  # measured 5.9e-7: same kNN sets, float32 SVD rounding
 
 
 def test_voxel_torch_branch_restatement(gold):

@@ -1,0 +1,58 @@
+"""GPU timing of the RANSAC count kernels at C3 (10M points x 1000 hypotheses).
+
+Each variant (env switches read per call by ransac.hip run_count) is timed
+with the library's own HIP-event timer "plane_count" over a few calls and
+checked equal to the first variant's counts.
+Usage (GPU box): python tools/ransac_time.py [reps]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "open3d-py-extension_amd"))
+from open3dpypro import _native as N, ops, synthetic as S  # noqa: E402
+
+VARIANTS = [("mfma_ht8", {}), ("mfma_ht4", {"O3DX_RANSAC_HT": "4"}), ("mfma_ht16", {"O3DX_RANSAC_HT": "16"}),
+            ("valu", {"O3DX_RANSAC_VALU": "1"})]
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    dev = torch.device("cuda:0")
+    n, H = 10_000_000, 1000
+    x = S.planted_plane(n, 0, device=dev)
+    pts = x.cpu().numpy().astype(np.float64)
+    idx = np.random.default_rng(0).integers(0, n, (H, 3))
+    a, b, c = pts[idx[:, 0]], pts[idx[:, 1]], pts[idx[:, 2]]
+    nrm = np.cross(b - a, c - a)
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-300)
+    planes = np.concatenate([nrm, -np.sum(nrm * a, 1, keepdims=True)], 1)
+    ref = None
+    out = {}
+    for name, env in VARIANTS:
+        for k in ("O3DX_RANSAC_HT", "O3DX_RANSAC_VALU"):
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        got = ops.plane_count(x, planes, 0.01)  # warm-up
+        N.set_kernel_timing(True)
+        N.reset_kernel_timing()
+        for _ in range(reps):
+            got = ops.plane_count(x, planes, 0.01)
+        torch.cuda.synchronize()
+        ms, cnt = N.kernel_timing("plane_count")
+        N.set_kernel_timing(False)
+        if ref is None:
+            ref = got
+        out[name] = {"ms": ms / max(cnt, 1), "equal": bool(np.array_equal(got, ref)),
+                     "pairs_per_s": n * H / (ms / max(cnt, 1) * 1e-3)}
+        print(json.dumps({name: out[name]}), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ransac_time.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
