@@ -164,7 +164,7 @@ static int64_t cell_space(const int64_t d[3], bool blocked) {
 
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
                hipStream_t s, GridBuild* out, float4* extra_sorted, const float* extra_src, bool blocked,
-               int cap_mult) {
+               int cap_mult, bool ordered) {
   GridLayout L = grid_layout(n, cap_mult);
   if (ws_bytes < L.total) return fail(O3DX_ENOMEM, "grid workspace too small (need %zu)", L.total);
   char* w = (char*)ws;
@@ -270,7 +270,10 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     kt_count.stop();
     KTimer kt_sort("grid_sort", s);
     O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));
-    if (n > 0) {
+    if (n > 0 && !ordered) {  // cell order only (the in-cell order is the atomic ranks')
+      hipLaunchKernelGGL(k_grid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, G.cell, G.rank,
+                         G.start, G.pts, extra_src, extra_sorted);
+    } else if (n > 0) {
       float4* tmp = (float4*)(w + L.tmp);
       float4* tmp_extra = extra_sorted ? (float4*)(w + L.tmp_extra) : nullptr;
       hipLaunchKernelGGL(k_grid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, G.cell, G.rank,

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "grid.hpp"
 
 namespace o3dx {
 
@@ -119,175 +120,276 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// The same counts with the distances on the matrix cores.  All hypotheses
-// against all points is a dense (N x 4) . (4 x H) product: one
-// v_mfma_f32_16x16x4_f32 gives 16 points x 16 hypotheses, and its result is
-// bit for bit the k-ordered fmaf chain (MI355X: "exact f32 (== fmaf chain,
-// bitwise)") — with k = (1 | d), (z | c), (y | b), (x | a) it is
-// fma(a, x, fma(b, y, fma(c, z, d))), the VALU kernel's distance exactly.
-// The band is one window [lo, hi) for all hypotheses (the union of their
-// float32 windows), so the VALU does ~3.5 operations per result:
-//   x = |d| - lo            (sign bit set <=> |d| < lo: an inlier)
-//   cnt += bits(x) >> 31
-//   mn = umin(mn, bits(x))  (0 <= x <= fl(hi - lo) <=> bits(x) <= bits(W))
-// A step with any result in the window (rare) re-issues its products and
-// sets one bit per 16-hypothesis tile in a (step, tile) bitmap;
-// k_plane_fixup re-decides those tiles' window results in float64 in
-// Open3D's order.  No call, no list, no capacity: the hot loop carries only
-// the one ballot per step.  Lanes hold per-hypothesis counters (lane l:
-// hypothesis l & 15 of each tile, points (l >> 4) * 4 + r), summed over the
-// four lanes of a hypothesis at the end.  Rows past the wave's range or past
-// n are all-zero (distance 0): they count as inliers of every hypothesis when
-// lo > 0 and the host subtracts that known padding.  One wave = a range of
-// points x HT tiles of 16 hypotheses.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kMfU = 2;  // 16-point steps per loop trip (loads in flight)
+// The counts, one sweep over all hypotheses.  A wave holds a batch of 64 PL
+// points (PL per lane, packed pairs) and HC hypotheses (planes read out of
+// one register per coefficient with v_readlane: no memory latency in the
+// loop).  One float32 window serves every hypothesis (the union of their
+// windows [lo, hi)), tested on squares so that no |d| is needed:
+//   d = fma(a, x, fma(b, y, fma(c, z, d)))   packed: 1.5 ops per point
+//   t = fma(d, d, -Llo)                      packed: 0.5 (t < 0 <=> d^2 < Llo <= lo^2)
+//   inliers: v_cmp t < 0, popcount on the scalar unit (counts are wave-uniform)
+//   mn = umin(mn, bits(t))                   0 <= t <= fl(Lhi - Llo) covers lo <= |d| < hi
+// Per batch and hypothesis one ballot of mn <= W marks window results; the
+// wave stores one bit per hypothesis in the (batch, chunk) word of a bitmap,
+// and k_plane_fixup re-decides those (batch, hypothesis) blocks in float64
+// in Open3D's order.  Points past n are NaN: neither counted (t < 0 is
+// false) nor in the window (their bits exceed W).  Blocks are mapped so that
+// the waves sharing a batch range (all hypothesis chunks) run on one XCD
+// (its L2 serves the re-reads of the points).
+// Shapes: HC hypotheses per wave x PL points per lane per batch (batch =
+// 64 PL points).  Default 32 x 16; O3DX_RANSAC_SHAPE=HCxPL picks another
+// instantiated shape (tuning).
+constexpr int kCountWaves = 2048;      // batch ranges (waves per hypothesis chunk)
+constexpr int kMinBatchPts = 64 * 8;   // smallest instantiated batch (bitmap sizing)
+constexpr int kMinHC = 16;             // smallest instantiated chunk (bitmap sizing)
 
-template <int HT>
-__global__ void __launch_bounds__(kBlock) k_plane_count_mfma(const float* __restrict__ xyz, int64_t n,
-                                                             const float4* __restrict__ pl32, int H, float lo,
-                                                             uint32_t wbits, int64_t steps_per_wave, int nwp,
-                                                             int wps, int32_t* __restrict__ partial,
-                                                             uint32_t* __restrict__ flags) {
-  const int lane = threadIdx.x & 63;
-  // point range of this wave (wave-uniform: scalar registers)
-  const int wp = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
-  if (wp >= nwp) return;
-  const int hbase = blockIdx.y * (16 * HT);
-  const int kk = lane >> 4, jj = lane & 15;
-  float bv[HT];
-  uint32_t cnt[HT];
+template <int PL>
+__device__ __forceinline__ void plane_batch_load(const P3* __restrict__ p, int64_t n, int64_t gb, int lane,
+                                                 f32x2 (&X)[PL / 2], f32x2 (&Y)[PL / 2], f32x2 (&Z)[PL / 2]) {
+  const float qnan = __int_as_float(0x7fc00000);
 #pragma unroll
-  for (int t = 0; t < HT; ++t) {
-    const int h = hbase + 16 * t + jj;
-    float b = 0.0f;
-    if (h < H) {
-      const float4 P = pl32[h];
-      b = kk == 0 ? P.w : kk == 1 ? P.z : kk == 2 ? P.y : P.x;
-    }
-    bv[t] = b;
-    cnt[t] = 0;
-  }
-  const int comp = 3 - kk;  // A[i][k]: k = 0 -> 1, 1 -> z, 2 -> y, 3 -> x
-  const int64_t s0 = (int64_t)wp * steps_per_wave;
-  const int64_t plim = min(n, (s0 + steps_per_wave) * 16);  // this wave's points end here
-  // the wave's points as a buffer resource: loads past plim return 0 with no
-  // branch, so the next trip's loads stay in flight across this trip
-  const int64_t pbase = s0 * 16;
-  const uint64_t base = reinterpret_cast<uint64_t>(xyz + 3 * pbase);
-  const int nbytes = (int)(max<int64_t>(plim - pbase, 0) * 12);
-  auto load = [&](int64_t st, float (&a)[kMfU]) {
-    // rebuilt from scalars at each use: a resource the allocator parks in
-    // VGPRs would be re-made uniform by a waterfall loop per load
-    const uint64_t b = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)base) |
-                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32);
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(b), (short)0, __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
-#pragma unroll
-    for (int u = 0; u < kMfU; ++u) {
-      const int off = (int)((st + u) * 16 + jj);  // point offset inside the wave's range
-      // k = 0 lanes load out of range (0) and OR in the constant 1 of a valid row
-      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, kk == 0 ? 0x7ffffff0 : off * 12 + comp * 4, 0, 0);
-      const uint32_t one = (kk == 0 && pbase + off < plim) ? 0x3f800000u : 0u;
-      a[u] = __uint_as_float(v | one);
-    }
-  };
-  float an[kMfU];
-  load(0, an);
-  for (int64_t st = 0; st < steps_per_wave; st += kMfU) {
-    float a[kMfU];
-#pragma unroll
-    for (int u = 0; u < kMfU; ++u) a[u] = an[u];
-    load(st + kMfU, an);  // next trip's points in flight during this one
-#pragma unroll
-    for (int u = 0; u < kMfU; ++u) {
-      // all tiles' products first (independent results keep the matrix pipe
-      // busy), then the compares
-      f32x4 d[HT];
-#pragma unroll
-      for (int t = 0; t < HT; ++t)
-        d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      uint32_t mn = ~0u;
-#pragma unroll
-      for (int t = 0; t < HT; ++t) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t x = __float_as_uint(fabsf(d[t][r]) - lo);
-          cnt[t] += x >> 31;
-          mn = min(mn, x);
-        }
-      }
-      if (__ballot(mn <= wbits) && st + u < steps_per_wave) {
-        // rare: which tiles hold window results (products re-issued, not kept live)
-        const int64_t g = s0 + st + u;
-#pragma unroll
-        for (int t = 0; t < HT; ++t) {
-          const f32x4 e = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[t], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          uint32_t m2 = ~0u;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) m2 = min(m2, __float_as_uint(fabsf(e[r]) - lo));
-          const int tile = hbase / 16 + t;
-          if (__ballot(m2 <= wbits) && lane == 0)
-            atomicOr(&flags[g * wps + (tile >> 5)], 1u << (tile & 31));
-        }
-      }
-    }
-  }
-  // the four lanes of a hypothesis (jj, jj + 16, jj + 32, jj + 48)
-#pragma unroll
-  for (int t = 0; t < HT; ++t) {
-    int c = (int)cnt[t];
-    c += __shfl_xor(c, 16, 64);
-    c += __shfl_xor(c, 32, 64);
-    const int h = hbase + 16 * t + jj;
-    if (kk == 0 && h < H) partial[(int64_t)wp * H + h] = c;
+  for (int k = 0; k < PL / 2; ++k) {
+    const int64_t i0 = gb * (64 * PL) + (int64_t)(2 * k) * 64 + lane, i1 = i0 + 64;
+    // clamped, unconditional loads; rows past n become NaN afterwards
+    const P3 a = p[min(i0, n - 1)];
+    const P3 b = p[min(i1, n - 1)];
+    X[k] = (f32x2){i0 < n ? a.x : qnan, i1 < n ? b.x : qnan};
+    Y[k] = (f32x2){i0 < n ? a.y : qnan, i1 < n ? b.y : qnan};
+    Z[k] = (f32x2){i0 < n ? a.z : qnan, i1 < n ? b.z : qnan};
   }
 }
 
-// The flagged (step, tile) blocks of k_plane_count_mfma: each window result
-// (the same float32 distance, fmaf chain) decided in float64 in Open3D's
-// order.  A wave takes 64 bitmap words; per set bit, its 256 pairs as
-// 4 per lane (point lane & 15, hypotheses 4 (lane >> 4) + q).
+// two points' distances per packed fma (measured faster here than scalar
+// fmas), each element the fmaf chain fma(a, x, fma(b, y, fma(c, z, d)))
+__device__ __forceinline__ f32x2 plane_dist_pk(const float4 P, f32x2 x, f32x2 y, f32x2 z) {
+  return __builtin_elementwise_fma((f32x2){P.x, P.x}, x,
+                                   __builtin_elementwise_fma((f32x2){P.y, P.y}, y,
+                                                             __builtin_elementwise_fma((f32x2){P.z, P.z}, z,
+                                                                                       (f32x2){P.w, P.w})));
+}
+
+// t = d * d - L in one rounding: t < 0 <=> d^2 < L exactly (the sign of an
+// fma is the sign of its exact value), so no |d| is needed and two points
+// share one packed op
+__device__ __forceinline__ f32x2 plane_sq_test(f32x2 d, float L) {
+  return __builtin_elementwise_fma(d, d, (f32x2){-L, -L});
+}
+
+// block -> (batch range, group of 4 hypothesis chunks), XCD-aware: the
+// launch's blocks are dealt round-robin over the 8 XCDs, so logical block
+// l = (b % 8) * (nb / 8) + b / 8 puts consecutive l on one XCD.
+__device__ __forceinline__ int xcd_logical_block(int b, int nb) {
+  if (nb % 8) return b;
+  return (b % 8) * (nb / 8) + b / 8;
+}
+
+template <int kHC, int kPL>  // kHC <= 32: one bitmap bit per hypothesis
+__global__ void __launch_bounds__(kBlock) k_plane_count_v(const float* __restrict__ xyz, int64_t n,
+                                                          const float4* __restrict__ pl32, int H, float Llo,
+                                                          uint32_t wbits, int64_t batches_per_wave, int nwp,
+                                                          int ncg, int32_t* __restrict__ partial,
+                                                          uint32_t* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int wp = lb / ncg;                                                      // batch range
+  const int chunk = __builtin_amdgcn_readfirstlane((lb % ncg) * (kBlock / 64) + (threadIdx.x >> 6));
+  const int nchunks = (H + kHC - 1) / kHC;
+  if (wp >= nwp || chunk >= nchunks) return;
+  const int h0 = chunk * kHC;
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  int cnt = 0;  // lane h: hypothesis h0 + h's count (popcounts of its inlier ballots)
+  // lane j holds plane h0 + (j % kHC) (h0 + j >= H: a copy of the last plane,
+  // its counts never written back)
+  float4 Pl = pl32[min(h0 + (lane % kHC), H - 1)];
+  constexpr int kBatchPts = 64 * kPL;
+  const int64_t nbatches = (n + kBatchPts - 1) / kBatchPts;
+  for (int64_t b = 0; b < batches_per_wave; ++b) {
+    const int64_t gb = (int64_t)wp * batches_per_wave + b;
+    if (gb >= nbatches) break;
+    // the planes are read out of Pl per batch, not hoisted out of the batch
+    // loop into 128 scalar registers (an empty asm that "changes" Pl)
+    asm volatile("" : "+v"(Pl.x), "+v"(Pl.y), "+v"(Pl.z), "+v"(Pl.w));
+    f32x2 X[kPL / 2], Y[kPL / 2], Z[kPL / 2];
+    plane_batch_load<kPL>(p, n, gb, lane, X, Y, Z);
+    uint32_t word = 0;
+#pragma unroll
+    for (int h = 0; h < kHC; ++h) {
+      // plane h from lane h (v_readlane into scalar registers: no memory
+      // latency inside the loop)
+      const float4 P = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.x), h)),
+                                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.y), h)),
+                                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.z), h)),
+                                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.w), h)));
+      uint32_t mn = ~0u;
+      int sc = 0;  // wave-uniform
+#pragma unroll
+      for (int k = 0; k < kPL / 2; ++k) {
+        const f32x2 t = plane_sq_test(plane_dist_pk(P, X[k], Y[k], Z[k]), Llo);
+        // inliers: one v_cmp per point, counted on the scalar unit
+        sc += __popcll(__ballot(t.x < 0.0f)) + __popcll(__ballot(t.y < 0.0f));
+        asm("" : "+s"(sc));  // summed as they come (a deferred sum tree spills the masks)
+        mn = min(mn, min(__float_as_uint(t.x), __float_as_uint(t.y)));
+      }
+      cnt += lane == h ? sc : 0;
+      if (__ballot(mn <= wbits)) word |= 1u << h;
+    }
+    if (lane == 0) flags[gb * nchunks + chunk] = word;
+  }
+  if (lane < kHC && h0 + lane < H) partial[(int64_t)wp * H + h0 + lane] = cnt;
+}
+
+// The window results of the flagged (batch, hypothesis) blocks decided in
+// float64 (Open3D's order).  A wave per bitmap word: its batch's points are
+// loaded once, then every flagged hypothesis is re-evaluated (the same packed
+// fma chain: the same float32 distance), window results decided in float64,
+// counted per lane, summed over the wave, one atomic per hypothesis.
+template <int kHC, int kPL>
 __global__ void __launch_bounds__(kBlock) k_plane_fixup(const float* __restrict__ xyz, int64_t n,
                                                         const float4* __restrict__ pl32,
-                                                        const double* __restrict__ pl64, int H, double thr, float lo,
+                                                        const double* __restrict__ pl64, int H, double thr, float Llo,
                                                         uint32_t wbits, const uint32_t* __restrict__ flags,
-                                                        int64_t nwords, int wps, int64_t* __restrict__ counts) {
+                                                        int64_t nwords, int64_t* __restrict__ counts) {
   const int lane = threadIdx.x & 63;
-  const int64_t w0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 64;
-  if (w0 >= nwords) return;
-  const uint32_t word = w0 + lane < nwords ? flags[w0 + lane] : 0u;
-  uint64_t m = __ballot(word != 0);
-  while (m) {
-    const int i = __ffsll((unsigned long long)m) - 1;
-    m &= m - 1;
-    uint32_t wd = (uint32_t)__shfl((int)word, i, 64);
-    const int64_t g = (w0 + i) / wps;
-    const int tbase = (int)((w0 + i) % wps) * 32;
-    const int64_t p = g * 16 + (lane & 15);
-    float x = 0.f, y = 0.f, z = 0.f;
-    if (p < n) x = xyz[3 * p], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
-    while (wd) {
-      const int tile = tbase + __ffs((int)wd) - 1;
-      wd &= wd - 1;
-      for (int q = 0; q < 4; ++q) {
-        const int h = tile * 16 + (lane >> 4) * 4 + q;
-        if (p >= n || h >= H) continue;
-        const float4 P = pl32[h];
-        const float d = fmaf(P.x, x, fmaf(P.y, y, fmaf(P.z, z, P.w)));
-        if (__float_as_uint(fabsf(d) - lo) <= wbits && plane_dist64(pl64 + 4 * (int64_t)h, x, y, z) < thr)
-          atomicAdd(reinterpret_cast<unsigned long long*>(&counts[h]), 1ull);
+  const int nchunks = (H + kHC - 1) / kHC;
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w < nwords;
+       w += (int64_t)gridDim.x * (kBlock / 64)) {
+    uint32_t word = flags[w];
+    if (!word) continue;
+    const int64_t gb = w / nchunks;
+    const int h0 = (int)(w % nchunks) * kHC;
+    f32x2 X[kPL / 2], Y[kPL / 2], Z[kPL / 2];
+    plane_batch_load<kPL>(p, n, gb, lane, X, Y, Z);
+    while (word) {
+      const int h = h0 + __ffs((int)word) - 1;
+      word &= word - 1;
+      if (h >= H) continue;
+      const float4 P = pl32[h];
+      const double* pl = pl64 + 4 * (int64_t)h;
+      int c = 0;
+#pragma unroll
+      for (int k = 0; k < kPL / 2; ++k) {
+        const f32x2 t = plane_sq_test(plane_dist_pk(P, X[k], Y[k], Z[k]), Llo);
+        if (__float_as_uint(t.x) <= wbits && plane_dist64(pl, X[k].x, Y[k].x, Z[k].x) < thr) ++c;
+        if (__float_as_uint(t.y) <= wbits && plane_dist64(pl, X[k].y, Y[k].y, Z[k].y) < thr) ++c;
       }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (lane == 0 && c) atomicAdd(reinterpret_cast<unsigned long long*>(&counts[h]), (unsigned long long)c);
     }
   }
 }
 
-// degenerate hypotheses -> -1; the others lose the padding rows they counted
-__global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H, int64_t pad,
-                                  int64_t* __restrict__ counts) {
+// ---------------------------------------------------------------------------
+// The counts over a cell grid of the cloud (grid.hpp: points grouped by
+// cell, rows of cells along x contiguous).  Along a row the distance of the
+// cell centres to a plane is affine in x, so the cells the slab
+// |n.p + d| < thr can reach form one interval of x, found in float64 with a
+// rigorous reach (|a|+|b|+|c|) (h/2 + assignment slack) and widened by a
+// cell on each side; every other cell of the row holds no inlier.  The
+// interval's points are one contiguous range of the sorted points.  A wave
+// takes one hypothesis x 64 rows (a lane computes one row's range), cuts the
+// ranges into chunks of 64 points and tests chunk after chunk with all
+// lanes (coalesced loads, several chunks in flight), with the per-point
+// window (t = fma(d, d, -Llo) < 0 certain, 0 <= t <= W decided in float64 in
+// Open3D's order).
+__global__ void __launch_bounds__(kBlock) k_plane_count_grid(GridView g, const float4* __restrict__ pl32,
+                                                             const double* __restrict__ pl64, int H, double thr,
+                                                             float Llo, uint32_t wbits, double cmargin,
+                                                             int groups_per_h, int32_t* __restrict__ counts32) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t ntasks = (int64_t)H * groups_per_h;
+  const int rows = g.ny * g.nz;
+  for (int64_t t = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t < ntasks; t += nwaves) {
+    const int h = (int)(t / groups_per_h);
+    const int row = (int)(t % groups_per_h) * 64 + lane;
+    const float4 P = pl32[h];
+    const double* pl = pl64 + 4 * (int64_t)h;
+    const double a = pl[0], b = pl[1], c = pl[2], d = pl[3];
+    int pa = 0, pb = 0;
+    if (row < rows) {
+      const int y = row % g.ny, z = row / g.ny;
+      const double hh = (double)g.h;
+      const double A = a * ((double)g.ox + 0.5 * hh) + b * ((double)g.oy + ((double)y + 0.5) * hh) +
+                       c * ((double)g.oz + ((double)z + 0.5) * hh) + d;
+      const double B = a * hh;
+      const double T = thr + (fabs(a) + fabs(b) + fabs(c)) * (0.5 * hh + (double)g.slack) + cmargin;
+      int x0 = 0, x1 = g.nx - 1;  // non-finite planes: the whole row (the points decide)
+      if (isfinite(A) && isfinite(B)) {
+        if (B != 0.0) {
+          double u = (-T - A) / B, v = (T - A) / B;
+          if (u > v) {
+            const double w = u;
+            u = v;
+            v = w;
+          }
+          u = fmin(fmax(u, -2.0), (double)g.nx + 2.0);
+          v = fmin(fmax(v, -2.0), (double)g.nx + 2.0);
+          x0 = max((int)floor(u) - 1, 0);
+          x1 = min((int)ceil(v) + 1, g.nx - 1);
+        } else if (!(fabs(A) < T)) {
+          x1 = -1;
+        }
+      }
+      if (x0 <= x1) {
+        const int rb = g.nx * (y + g.ny * z);
+        pa = g.start[rb + x0];
+        pb = g.start[rb + x1 + 1];
+      }
+    }
+    // the 64 rows' ranges as chunks of 64 points, processed by the whole
+    // wave (coalesced): chunk numbering by an inclusive scan of the rows'
+    // chunk counts, chunk -> row by a binary search over the lanes
+    const int nch = (pb - pa + 63) >> 6;
+    int incl = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    const int excl = incl - nch;
+    const int C = __shfl(incl, 63, 64);
+    int acc = 0;
+    for (int cb = 0; cb < C; cb += 64) {
+      const int cc = cb + lane;
+      int j = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const int e = __shfl(excl, min(j + step, 63), 64);
+        if (j + step < 64 && e <= cc) j += step;
+      }
+      const int rbase = __shfl(pa, j, 64), rexcl = __shfl(excl, j, 64), rend = __shfl(pb, j, 64);
+      const int cbase = cc < C ? rbase + (cc - rexcl) * 64 : 0;
+      const int cend = cc < C ? rend : 0;
+      const int nk = min(64, C - cb);
+#pragma unroll 4
+      for (int k = 0; k < nk; ++k) {
+        const int base = __builtin_amdgcn_readlane(cbase, k), end = __builtin_amdgcn_readlane(cend, k);
+        const int p = base + lane;
+        if (p < end) {
+          const float4 v = g.pts[p];
+          const float dd = fmaf(P.x, v.x, fmaf(P.y, v.y, fmaf(P.z, v.z, P.w)));
+          const float tt = fmaf(dd, dd, -Llo);
+          if (tt < 0.0f) ++acc;
+          else if (__float_as_uint(tt) <= wbits && plane_dist64(pl, v.x, v.y, v.z) < thr) ++acc;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0 && acc) atomicAdd(&counts32[h], acc);
+  }
+}
+
+__global__ void k_counts_widen(const int32_t* __restrict__ c32, int H, int64_t* __restrict__ counts) {
   int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h < H) counts[h] = degenerate[h] ? -1 : counts[h] - pad;
+  if (h < H) counts[h] = c32[h];
+}
+
+__global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H, int64_t* __restrict__ counts) {
+  int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h < H && degenerate[h]) counts[h] = -1;
 }
 
 constexpr int kSumBlocksX = 64;
@@ -421,20 +523,17 @@ static void plane_from_pts(const double* P, int k, double pl[4]) {
 static bool plane_is_zero(const double* pl) { return pl[0] == 0 && pl[1] == 0 && pl[2] == 0 && pl[3] == 0; }
 
 // ------------------------------------------------------------ workspaces
-constexpr int kMfWaves = 2048;  // point ranges of the MFMA count (waves per hypothesis chunk)
 
-// MFMA count geometry: nwp point ranges of spw 16-point steps each
-static void mf_geometry(int64_t n, int* nwp, int64_t* spw) {
-  const int64_t steps = (n + 15) / 16;
-  *nwp = (int)std::max<int64_t>(1, std::min<int64_t>(kMfWaves, (steps + 3) / 4));
-  *spw = (steps + *nwp - 1) / *nwp;
+// count geometry: nwp ranges of bpw batches of `batch` points
+static void count_geometry(int64_t n, int batch, int* nwp, int64_t* bpw) {
+  const int64_t nb = std::max<int64_t>(1, (n + batch - 1) / batch);
+  *nwp = (int)std::min<int64_t>(kCountWaves, nb);
+  *bpw = (nb + *nwp - 1) / *nwp;
 }
 
-static int64_t mf_flag_words(int64_t n, int H) {
-  int nwp;
-  int64_t spw;
-  mf_geometry(n, &nwp, &spw);
-  return (int64_t)nwp * spw * (((H + 15) / 16 + 31) / 32);
+// window bitmap: one word per (batch, chunk of hc hypotheses)
+static int64_t count_flag_words(int64_t n, int H, int batch, int hc) {
+  return std::max<int64_t>(1, (n + batch - 1) / batch) * ((std::max(H, 1) + hc - 1) / hc);
 }
 
 static int count_blocks(int64_t n) {
@@ -448,7 +547,10 @@ struct CountWs {
   double* pl64;
   uint8_t* degen;
   int32_t* partial;
-  uint32_t* flags;  // (step, 16-hypothesis tile) bitmap of the MFMA count
+  uint32_t* flags;  // (batch, hypothesis chunk) window bitmap of the brute-force count
+  int32_t* counts32;
+  void* grid_ws;    // cell grid of the cloud (the default count)
+  size_t grid_ws_bytes;
   int64_t* counts;
   double* sum_partial;
   double* sums;
@@ -460,8 +562,11 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   w->band = ar.take<float4>(H);
   w->pl64 = ar.take<double>(4 * (size_t)H);
   w->degen = ar.take<uint8_t>(H);
-  w->partial = ar.take<int32_t>((size_t)std::max(count_blocks(n), kMfWaves) * H);
-  w->flags = ar.take<uint32_t>((size_t)mf_flag_words(n, H));
+  w->partial = ar.take<int32_t>((size_t)std::max(count_blocks(n), kCountWaves) * H);
+  w->flags = ar.take<uint32_t>((size_t)count_flag_words(n, H, kMinBatchPts, kMinHC));
+  w->counts32 = ar.take<int32_t>(H);
+  w->grid_ws_bytes = grid_ws_bytes(std::max<int64_t>(n, 1));
+  w->grid_ws = ar.take<char>(w->grid_ws_bytes);
   w->counts = ar.take<int64_t>(H);
   w->sum_partial = ar.take<double>((size_t)kSumBlocksX * H);
   w->sums = ar.take<double>(H);
@@ -481,7 +586,10 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
     p32[h] = make_float4((float)pl[0], (float)pl[1], (float)pl[2], (float)pl[3]);
     double S = std::fabs(pl[0]) * absmax[0] + std::fabs(pl[1]) * absmax[1] + std::fabs(pl[2]) * absmax[2] +
                std::fabs(pl[3]);
-    double g = 16.0 * std::ldexp(1.0, -24) * S + std::ldexp(1.0, -20) * thr;
+    // float32 error of the fma chain: the four coefficients rounded (2^-24 S)
+    // + three fma roundings (each <= 2^-24 S); 6 for margin, + 2^-20 thr for
+    // the float32 rounding of lo / hi and Open3D's own float64 rounding
+    double g = 6.0 * std::ldexp(1.0, -24) * S + std::ldexp(1.0, -20) * thr;
     float lo = (float)(thr - g), hi = (float)(thr + g);
     if (dg[h]) {
       lo = -1.0f;  // never an inlier
@@ -522,49 +630,74 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   if (rc) return rc;
   int nb = count_blocks(n);
   KTimer kt("plane_count", s);
-  // the matrix-core path needs finite planes (its single window and sign-bit
-  // count); any other hypothesis set goes to the VALU kernel
-  bool finite = true;
-  for (int h = 0; h < 4 * H; ++h) finite = finite && std::isfinite(planes[h]);
-  const bool mfma = finite && !getenv("O3DX_RANSAC_VALU");
-  int64_t pad = 0;
-  if (mfma) {
+  if (!getenv("O3DX_RANSAC_VALU")) {
     // one window for all hypotheses: the union of their float32 windows
+    // (degenerate and non-finite planes are never counted: left out)
     float lo = -1.0f, hi = -1.0f;
     bool any = false;
     for (int h = 0; h < H; ++h)
-      if (!dg[h]) {
+      if (!dg[h] && std::isfinite(bnd[h].x) && std::isfinite(bnd[h].y)) {
         lo = any ? std::min(lo, bnd[h].x) : bnd[h].x;
         hi = any ? std::max(hi, bnd[h].y) : bnd[h].y;
         any = true;
       }
-    const float wdt = hi - lo;  // >= 0; fl() is monotone, so |d| < hi => fl(|d| - lo) <= wdt
+    // squares: Llo <= lo^2 (rounded down; 0 when lo <= 0 or tiny: nothing is
+    // certain), Lhi >= hi^2 (rounded up), window bits(t) <= bits(fl(Lhi - Llo)):
+    // d^2 < Lhi => t = fl(d^2 - Llo) <= fl(Lhi - Llo) (rounding is monotone)
+    auto f32_down = [](double v) { float f = (float)v; return (double)f > v ? std::nextafter(f, -INFINITY) : f; };
+    auto f32_up = [](double v) { float f = (float)v; return (double)f < v ? std::nextafter(f, INFINITY) : f; };
+    const double lo2 = (double)lo * (double)lo, hi2 = (double)hi * (double)hi;
+    const float Llo = (lo > 0.0f && lo2 > std::ldexp(1.0, -100)) ? f32_down(lo2) : 0.0f;
+    const float Lhi = hi > 0.0f ? f32_up(hi2) : 0.0f;
+    const float wdt = (float)((double)Lhi - (double)Llo);  // exact difference, one rounding
     uint32_t wbits;
     std::memcpy(&wbits, &wdt, 4);
-    // matrix-core distances: waves = point ranges x chunks of 16 HT hypotheses
-    const char* ht_env = getenv("O3DX_RANSAC_HT");
-    const int ht = ht_env ? atoi(ht_env) : 8;
+    if (!getenv("O3DX_RANSAC_BRUTE")) {
+      // cell grid of the cloud: whole cells decided per hypothesis
+      GridBuild G;
+      const double occ = getenv("O3DX_RANSAC_OCC") ? atof(getenv("O3DX_RANSAC_OCC")) : 48.0;
+      O3DX_TRY(grid_build(xyz, n, occ, 0.0, w.grid_ws, w.grid_ws_bytes, s, &G, nullptr, nullptr, false, 4,
+                          /*ordered=*/false));
+      const GridView& g = G.view;
+      const double hh = g.h, amax = std::max(std::max(absmax[0], absmax[1]), absmax[2]);
+      // float64 rounding of a cell-centre distance and of Open3D's distance
+      const double cmargin = 64.0 * std::ldexp(1.0, -52) * (3.0 * (amax + 4 * hh) + amax + 1.0) * 2.0 + 1e-12 * thr;
+      const int rows = g.ny * g.nz;
+      const int gph = (rows + 63) / 64;  // 64-row groups per hypothesis
+      const int64_t tasks = (int64_t)H * gph;
+      O3DX_HIP(hipMemsetAsync(w.counts32, 0, (size_t)H * sizeof(int32_t), s));
+      hipLaunchKernelGGL(k_plane_count_grid, dim3(grid_for(tasks, kBlock / 64, 16384)), dim3(kBlock), 0, s, g,
+                         w.pl32, w.pl64, H, thr, Llo, wbits, cmargin, gph, w.counts32);
+      hipLaunchKernelGGL(k_counts_widen, dim3((H + 255) / 256), dim3(256), 0, s, w.counts32, H, w.counts);
+      hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
+      kt.stop();
+      counts.resize(H);
+      O3DX_TRY(read_back(counts.data(), w.counts, H * sizeof(int64_t), s));
+      O3DX_HIP(hipGetLastError());
+      return 0;
+    }
+    // brute force: every point against every hypothesis
+    int hc = 32, pl = 16;
+    if (const char* e = getenv("O3DX_RANSAC_SHAPE")) sscanf(e, "%dx%d", &hc, &pl);
     int nwp;
-    int64_t spw;
-    mf_geometry(n, &nwp, &spw);
-    const int wps = ((H + 15) / 16 + 31) / 32;  // bitmap words per step
-    const int64_t nwords = mf_flag_words(n, H);
-    O3DX_HIP(hipMemsetAsync(w.flags, 0, (size_t)nwords * sizeof(uint32_t), s));
-    const unsigned gx = (unsigned)((nwp + kBlock / 64 - 1) / (kBlock / 64));
-#define O3DX_MF(HT)                                                                                          \
-  hipLaunchKernelGGL(k_plane_count_mfma<HT>, dim3(gx, (unsigned)((H + 16 * HT - 1) / (16 * HT))), dim3(kBlock), \
-                     0, s, xyz, n, w.pl32, H, lo, wbits, spw, nwp, wps, w.partial, w.flags)
-    if (ht == 16) O3DX_MF(16);
-    else if (ht == 4) O3DX_MF(4);
-    else O3DX_MF(8);
-#undef O3DX_MF
-    // all-zero rows (distance 0) counted by every hypothesis when 0 < lo
-    if (lo > 0.0f) pad = (int64_t)nwp * ((spw + kMfU - 1) / kMfU * kMfU) * 16 - n;
-    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));
-    const int64_t fwaves = (nwords + 63) / 64;
-    hipLaunchKernelGGL(k_plane_fixup, dim3((unsigned)((fwaves + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0,
-                       s, xyz, n, w.pl32, w.pl64, H, thr, lo, wbits, w.flags, nwords, wps, w.counts);
-  } else {
+    int64_t bpw;
+    count_geometry(n, 64 * pl, &nwp, &bpw);
+    const int nchunks = (H + hc - 1) / hc;
+    const int ncg = (nchunks + kBlock / 64 - 1) / (kBlock / 64);  // blocks per batch range
+    const int64_t nwords = count_flag_words(n, H, 64 * pl, hc);
+    const unsigned fgrid = grid_for(nwords, kBlock / 64, 16384);
+#define O3DX_COUNT(HC, PL)                                                                                         \
+  if (hc == HC && pl == PL) {                                                                                      \
+    hipLaunchKernelGGL((k_plane_count_v<HC, PL>), dim3((unsigned)(nwp * ncg)), dim3(kBlock), 0, s, xyz, n, w.pl32, \
+                       H, Llo, wbits, bpw, nwp, ncg, w.partial, w.flags);                                          \
+    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));                                          \
+    hipLaunchKernelGGL((k_plane_fixup<HC, PL>), dim3(fgrid), dim3(kBlock), 0, s, xyz, n, w.pl32, w.pl64, H, thr,   \
+                       Llo, wbits, w.flags, nwords, w.counts);                                                      \
+  } else
+    O3DX_COUNT(32, 16) O3DX_COUNT(32, 8) O3DX_COUNT(16, 16) O3DX_COUNT(16, 8)
+    return fail(O3DX_EINVAL, "O3DX_RANSAC_SHAPE: instantiated shapes are 32x16, 32x8, 16x16, 16x8");
+#undef O3DX_COUNT
+  } else {  // the ballot/popcount kernel with per-hypothesis windows (A/B reference)
     for (int h0 = 0; h0 < H; h0 += kHChunk) {
       int hc = std::min(kHChunk, H - h0);
       hipLaunchKernelGGL(k_plane_count, dim3(nb), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, h0, hc, thr,
@@ -572,7 +705,7 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
     }
     O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nb, H, w.counts, s));
   }
-  hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, pad, w.counts);
+  hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
   kt.stop();
   counts.resize(H);
   O3DX_TRY(read_back(counts.data(), w.counts, H * sizeof(int64_t), s));

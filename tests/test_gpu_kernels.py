@@ -266,6 +266,28 @@ def test_icp_accumulate_sorted_source_layout(dev):
     np.testing.assert_allclose(b[:30], ref[:30], rtol=1e-9, atol=1e-9)
 
 
+@pytest.mark.parametrize("shift", [0.0, 0.006, 0.015, 0.05])
+def test_icp_block_occupancy_search_exact(dev, shift, monkeypatch):
+    """The block-occupancy path of the 1-NN search (GridView::occ: empty
+    4x4x4 blocks skipped) returns exactly the plain shell search's matches
+    — sources displaced by up to and beyond max_correspondence_distance, as
+    at ICP's first iteration — and the oracle's moments."""
+    src, tgt = _icp_case(40000, seed=6)
+    tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
+    T = S.rigid_transform(2.0, (0, 1, 1), (shift, -shift / 2, shift / 3))
+    target = ops.ICPTarget(torch.from_numpy(tgt).to(dev), torch.from_numpy(tn).to(dev), 0.02)
+    s = torch.from_numpy(src).to(dev)
+    a, ca = target.accumulate(s, T, want_corr=True)
+    monkeypatch.setenv("O3DX_ICP_NO_OCC", "1")
+    b, cb = target.accumulate(s, T, want_corr=True)
+    monkeypatch.delenv("O3DX_ICP_NO_OCC")
+    assert torch.equal(ca, cb)
+    assert a[28] == b[28] and np.array_equal(a[:30], b[:30])
+    ref = O.icp_accumulate(src, tgt, tn, 0.02, T)
+    assert a[28] == ref[28]
+    np.testing.assert_allclose(a[:30], ref[:30], rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("k", [5, 30, 64])
 @pytest.mark.parametrize("shape", ["cube", "surface", "dups"])
 def test_normals_knn_paths_agree(dev, k, shape):
@@ -452,10 +474,49 @@ def test_voxel_down_sample_normals_fused(dev, bunny, case):
                    what=f"fused_{case}")
 
 
+@pytest.mark.parametrize("shape", ["32x16", "32x8", "16x16", "16x8"])
+def test_plane_count_shapes(dev, shape, monkeypatch):
+    """Every instantiated (hypotheses per wave x points per lane) shape of
+    the brute-force kernel gives the oracle's counts (ragged n and H)."""
+    monkeypatch.setenv("O3DX_RANSAC_BRUTE", "1")
+    monkeypatch.setenv("O3DX_RANSAC_SHAPE", shape)
+    n, H = 70_001, 101
+    pts = S.planted_plane(n, 62).numpy()
+    samples = np.random.default_rng(9).integers(0, n, (H, 3)).astype(np.int32)
+    planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
+    got = ops.plane_count(torch.from_numpy(pts).to(dev), planes, 0.01)
+    assert np.array_equal(got, NPR.segment_plane_counts(pts, 0.01, samples))
+
+
+@pytest.mark.parametrize("occ", ["2", "48", "2000"])
+@pytest.mark.parametrize("cloud", ["planted", "flat", "line"])
+def test_plane_count_grid_cells_exact(dev, cloud, occ, monkeypatch):
+    """The cell-grid count skips, per hypothesis and row of cells, the cells
+    the slab cannot reach: fine and coarse grids, a flat cloud (the slab of
+    its own plane covers whole rows), a line-like cloud (one-row grids);
+    counts equal the oracle's."""
+    monkeypatch.setenv("O3DX_RANSAC_OCC", occ)
+    rng = np.random.default_rng(11)
+    n = 60_000
+    if cloud == "planted":
+        pts = S.planted_plane(n, 63).numpy()
+    elif cloud == "flat":
+        pts = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1, 1, n), rng.normal(0.3, 0.001, n)], 1).astype(np.float32)
+    else:
+        pts = np.stack([rng.uniform(0, 50, n), rng.normal(0, 0.01, n), rng.normal(0, 0.01, n)], 1).astype(np.float32)
+    samples = rng.integers(0, n, (300, 3)).astype(np.int32)
+    planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
+    planes[5] = [0.0, 0.0, 1.0, -0.3]  # the flat cloud's own plane
+    got = o3p_counts = ops.plane_count(torch.from_numpy(pts).to(dev), planes, 0.01)
+    p64 = pts.astype(np.float64)
+    ref = np.array([int((NPR.plane_dist(pl, p64) < 0.01).sum()) if pl.any() else -1 for pl in planes])
+    assert np.array_equal(o3p_counts, ref), np.nonzero(got != ref)[0][:10]
+
+
 def test_plane_count_window_overflow_and_nonfinite(dev, monkeypatch):
     """Every pair inside the float32 window (points at |d| == thr of z = 0):
-    the fix-up list overflows and the VALU kernel recounts; non-finite planes
-    take the VALU kernel too.  Both equal the oracle's counts."""
+    every (batch, hypothesis) block goes through the float64 fix-up; planes
+    with NaN coefficients count nothing.  Both kernels equal the oracle."""
     n = 1_200_000
     rng = np.random.default_rng(3)
     pts = np.stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n), np.full(n, 0.01)], 1).astype(np.float32)
@@ -474,16 +535,14 @@ def test_plane_count_window_overflow_and_nonfinite(dev, monkeypatch):
     assert got[:3].tolist() == ref and got[3] == 0
 
 
-@pytest.mark.parametrize("n,H,thr,ht", [(1, 3, 0.01, "8"), (17, 5, 0.01, "8"), (100_003, 257, 0.01, "8"),
-                                        (100_003, 257, 0.01, "4"), (100_003, 257, 0.01, "16"),
-                                        (100_003, 257, 1e-7, "8"), (1_000_000, 1000, 0.01, "8")])
-def test_plane_count_mfma_equals_valu_and_oracle(dev, n, H, thr, ht, monkeypatch):
-    """k_plane_count_mfma (matrix-core distances) and the VALU kernel give
-    the same exact counts, equal to the oracle's, for ragged sizes (n not a
-    multiple of 16, H not of 256), degenerate hypotheses, every tile width,
-    and a threshold below the float32 window (lo < 0: padding rows are not
-    counted, the window holds the near-plane points)."""
-    monkeypatch.setenv("O3DX_RANSAC_HT", ht)
+@pytest.mark.parametrize("n,H,thr", [(1, 3, 0.01), (17, 5, 0.01), (1025, 33, 0.01), (100_003, 257, 0.01),
+                                     (100_003, 257, 1e-7), (1_000_000, 1000, 0.01)])
+def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatch):
+    """The cell-grid count (default), the brute-force lane-counter kernel and
+    the ballot kernel give the same exact counts, equal to the oracle's, for
+    ragged sizes (n not a multiple of the 1024-point batch, H not of the
+    32-hypothesis chunk), degenerate hypotheses, and a threshold below the
+    float32 window (lo < 0: the window holds the near-plane points)."""
     pts = S.planted_plane(max(n, 3), 61).numpy()[:n]
     rng = np.random.default_rng(n)
     samples = rng.integers(0, n, (H, 3)).astype(np.int32)
@@ -491,10 +550,13 @@ def test_plane_count_mfma_equals_valu_and_oracle(dev, n, H, thr, ht, monkeypatch
     planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
     x = torch.from_numpy(pts).to(dev)
     got = ops.plane_count(x, planes, thr)
+    monkeypatch.setenv("O3DX_RANSAC_BRUTE", "1")
+    brute = ops.plane_count(x, planes, thr)
+    monkeypatch.delenv("O3DX_RANSAC_BRUTE")
     monkeypatch.setenv("O3DX_RANSAC_VALU", "1")
     valu = ops.plane_count(x, planes, thr)
     monkeypatch.delenv("O3DX_RANSAC_VALU")
-    assert np.array_equal(got, valu)
+    assert np.array_equal(got, brute) and np.array_equal(got, valu)
     ref = NPR.segment_plane_counts(pts, thr, samples) if n <= 100_003 else None
     if ref is not None:
         assert np.array_equal(got, ref)
