@@ -477,8 +477,7 @@ def test_voxel_down_sample_normals_fused(dev, bunny, case):
 @pytest.mark.parametrize("shape", ["32x16", "32x8", "16x16", "16x8"])
 def test_plane_count_shapes(dev, shape, monkeypatch):
     """Every instantiated (hypotheses per wave x points per lane) shape of
-    the brute-force kernel gives the oracle's counts (ragged n and H)."""
-    monkeypatch.setenv("O3DX_RANSAC_BRUTE", "1")
+    the lane-counter kernel gives the oracle's counts (ragged n and H)."""
     monkeypatch.setenv("O3DX_RANSAC_SHAPE", shape)
     n, H = 70_001, 101
     pts = S.planted_plane(n, 62).numpy()
@@ -486,31 +485,6 @@ def test_plane_count_shapes(dev, shape, monkeypatch):
     planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
     got = ops.plane_count(torch.from_numpy(pts).to(dev), planes, 0.01)
     assert np.array_equal(got, NPR.segment_plane_counts(pts, 0.01, samples))
-
-
-@pytest.mark.parametrize("occ", ["2", "48", "2000"])
-@pytest.mark.parametrize("cloud", ["planted", "flat", "line"])
-def test_plane_count_grid_cells_exact(dev, cloud, occ, monkeypatch):
-    """The cell-grid count skips, per hypothesis and row of cells, the cells
-    the slab cannot reach: fine and coarse grids, a flat cloud (the slab of
-    its own plane covers whole rows), a line-like cloud (one-row grids);
-    counts equal the oracle's."""
-    monkeypatch.setenv("O3DX_RANSAC_OCC", occ)
-    rng = np.random.default_rng(11)
-    n = 60_000
-    if cloud == "planted":
-        pts = S.planted_plane(n, 63).numpy()
-    elif cloud == "flat":
-        pts = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1, 1, n), rng.normal(0.3, 0.001, n)], 1).astype(np.float32)
-    else:
-        pts = np.stack([rng.uniform(0, 50, n), rng.normal(0, 0.01, n), rng.normal(0, 0.01, n)], 1).astype(np.float32)
-    samples = rng.integers(0, n, (300, 3)).astype(np.int32)
-    planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
-    planes[5] = [0.0, 0.0, 1.0, -0.3]  # the flat cloud's own plane
-    got = o3p_counts = ops.plane_count(torch.from_numpy(pts).to(dev), planes, 0.01)
-    p64 = pts.astype(np.float64)
-    ref = np.array([int((NPR.plane_dist(pl, p64) < 0.01).sum()) if pl.any() else -1 for pl in planes])
-    assert np.array_equal(o3p_counts, ref), np.nonzero(got != ref)[0][:10]
 
 
 def test_plane_count_window_overflow_and_nonfinite(dev, monkeypatch):
@@ -538,8 +512,8 @@ def test_plane_count_window_overflow_and_nonfinite(dev, monkeypatch):
 @pytest.mark.parametrize("n,H,thr", [(1, 3, 0.01), (17, 5, 0.01), (1025, 33, 0.01), (100_003, 257, 0.01),
                                      (100_003, 257, 1e-7), (1_000_000, 1000, 0.01)])
 def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatch):
-    """The cell-grid count (default), the brute-force lane-counter kernel and
-    the ballot kernel give the same exact counts, equal to the oracle's, for
+    """The lane-counter count (default), the matrix-core count and the
+    ballot kernel give the same exact counts, equal to the oracle's, for
     ragged sizes (n not a multiple of the 1024-point batch, H not of the
     32-hypothesis chunk), degenerate hypotheses, and a threshold below the
     float32 window (lo < 0: the window holds the near-plane points)."""
@@ -550,9 +524,9 @@ def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatc
     planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
     x = torch.from_numpy(pts).to(dev)
     got = ops.plane_count(x, planes, thr)
-    monkeypatch.setenv("O3DX_RANSAC_BRUTE", "1")
+    monkeypatch.setenv("O3DX_RANSAC_MFMA", "1")
     brute = ops.plane_count(x, planes, thr)
-    monkeypatch.delenv("O3DX_RANSAC_BRUTE")
+    monkeypatch.delenv("O3DX_RANSAC_MFMA")
     monkeypatch.setenv("O3DX_RANSAC_VALU", "1")
     valu = ops.plane_count(x, planes, thr)
     monkeypatch.delenv("O3DX_RANSAC_VALU")

@@ -16,10 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "open3d-py-extension_amd"))
 from open3dpypro import _native as N, ops, synthetic as S  # noqa: E402
 
-VARIANTS = [("grid_occ48", {}), ("grid_occ8", {"O3DX_RANSAC_OCC": "8"}), ("grid_occ16", {"O3DX_RANSAC_OCC": "16"}),
-            ("grid_occ128", {"O3DX_RANSAC_OCC": "128"}),
-            ("brute_16x16", {"O3DX_RANSAC_BRUTE": "1", "O3DX_RANSAC_SHAPE": "16x16"}),
-            ("ballot_legacy", {"O3DX_RANSAC_VALU": "1"})]
+VARIANTS = [("counters_32x16", {}), ("counters_16x16", {"O3DX_RANSAC_SHAPE": "16x16"}),
+            ("mfma", {"O3DX_RANSAC_MFMA": "1"}), ("ballot_legacy", {"O3DX_RANSAC_VALU": "1"})]
 
 
 def main():
@@ -36,7 +34,7 @@ def main():
     ref = None
     out = {}
     for name, env in VARIANTS:
-        for k in ("O3DX_RANSAC_VALU", "O3DX_RANSAC_SHAPE", "O3DX_RANSAC_BRUTE", "O3DX_RANSAC_OCC", "O3DX_RANSAC_RPT"):
+        for k in ("O3DX_RANSAC_VALU", "O3DX_RANSAC_SHAPE", "O3DX_RANSAC_MFMA"):
             os.environ.pop(k, None)
         os.environ.update(env)
         got = ops.plane_count(x, planes, 0.01)  # warm-up
