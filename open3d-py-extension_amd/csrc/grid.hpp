@@ -30,10 +30,6 @@ struct GridView {
                               // coordinates, w = -1) and start is the identity (start may be null)
   int32_t* nbr = nullptr;     // test hook (o3dx_set_debug_neighbors): k selected ids per output row
   float* kd2 = nullptr;       // KNN normals: per output row an upper bound of the k-th neighbour d^2
-  // ICP targets: occupancy of 4x4x4 cell blocks (bit (x&3) + 4 (y&3) + 16 (z&3)
-  // of block (x>>2, y>>2, z>>2), row-major over onx x ony x ceil(nz/4)); null = none
-  const unsigned long long* occ = nullptr;
-  int onx = 0, ony = 0;
 };
 
 // First sorted position of cell c (dense tables: the cell itself).
@@ -309,61 +305,6 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
       *best_pos = bp;
       return bi;
     }
-  }
-  if (g.occ) {
-    // Block shells: a block of 4x4x4 cells with no points is skipped on one
-    // load, a block whose box lies beyond the bound on one test, and inside
-    // a block only its occupied cells are visited.  (A query far from the
-    // surface, e.g. ICP's first iteration, crosses mostly empty space.)
-    const int obx = cx >> 2, oby = cy >> 2, obz = cz >> 2;
-    const int onz = (g.nz + 3) >> 2;
-    const int rmaxb = max(max(max(obx, g.onx - 1 - obx), max(oby, g.ony - 1 - oby)), max(obz, onz - 1 - obz));
-    const float hb = 4.0f * g.h;
-    for (int R = 0;; ++R) {
-      for (int dz = -R; dz <= R; ++dz) {
-        const int bz = obz + dz;
-        if (bz < 0 || bz >= onz) continue;
-        const bool zf = (dz == -R) || (dz == R);
-        for (int dy = -R; dy <= R; ++dy) {
-          const int by = oby + dy;
-          if (by < 0 || by >= g.ony) continue;
-          const int step = (zf || dy == -R || dy == R) ? 1 : 2 * R;
-          for (int dx = -R; dx <= R; dx += (step > 0 ? step : 1)) {
-            const int bx = obx + dx;
-            if (bx < 0 || bx >= g.onx) continue;
-            unsigned long long m = g.occ[bx + g.onx * (by + g.ony * bz)];
-            if (!m) continue;
-            const float bx0 = g.ox + (float)(4 * bx) * g.h, by0 = g.oy + (float)(4 * by) * g.h,
-                        bz0 = g.oz + (float)(4 * bz) * g.h;
-            const float ex = fmaxf(fmaxf(bx0 - fx, fx - (bx0 + hb)) - sl3, 0.0f);
-            const float ey = fmaxf(fmaxf(by0 - fy, fy - (by0 + hb)) - sl3, 0.0f);
-            const float ez = fmaxf(fmaxf(bz0 - fz, fz - (bz0 + hb)) - sl3, 0.0f);
-            if (fmaf(ez, ez, fmaf(ey, ey, ex * ex)) >= thr) continue;
-            while (m) {
-              const int b = __ffsll(m) - 1;
-              m &= m - 1;
-              const int x = 4 * bx + (b & 3), y = 4 * by + ((b >> 2) & 3), z = 4 * bz + (b >> 4);
-              if (x != cx || y != cy || z != cz) visit_cell(x, y, z);
-            }
-          }
-        }
-      }
-      // every point within B of q lies in the visited block cube
-      double B = INFINITY;
-      if (4 * (obx - R) > 0) B = fmin(B, qx - ((double)g.ox + (double)(4 * (obx - R)) * g.h));
-      if (4 * (obx + R + 1) <= g.nx - 1) B = fmin(B, ((double)g.ox + (double)(4 * (obx + R + 1)) * g.h) - qx);
-      if (4 * (oby - R) > 0) B = fmin(B, qy - ((double)g.oy + (double)(4 * (oby - R)) * g.h));
-      if (4 * (oby + R + 1) <= g.ny - 1) B = fmin(B, ((double)g.oy + (double)(4 * (oby + R + 1)) * g.h) - qy);
-      if (4 * (obz - R) > 0) B = fmin(B, qz - ((double)g.oz + (double)(4 * (obz - R)) * g.h));
-      if (4 * (obz + R + 1) <= g.nz - 1) B = fmin(B, ((double)g.oz + (double)(4 * (obz + R + 1)) * g.h) - qz);
-      B -= g.slack;
-      if (B >= radius || R >= rmaxb) break;
-      if (bi >= 0 && B > 0.0 && bd < B * B) break;
-    }
-    search_stats(g, st_cells, st_cands, 3);
-    *best_d2 = bd;
-    *best_pos = bp;
-    return bi;
   }
   for (;; ++r) {
     // every point within B of q has been visited (or pruned by the bound)

@@ -129,19 +129,6 @@ __global__ void __launch_bounds__(kBlock) k_icp_moments(const float* __restrict_
   if (threadIdx.x < kNS - 30) partial[(int64_t)blockIdx.x * kNS + 30 + threadIdx.x] = 0.0;
 }
 
-// Occupancy of 4x4x4 cell blocks of the target grid (GridView::occ): one
-// bit per non-empty cell.
-__global__ void __launch_bounds__(kBlock) k_occ_build(const int32_t* __restrict__ start, int nx, int ny, int nz,
-                                                      int onx, int ony, unsigned long long* __restrict__ occ) {
-  const int64_t nc = (int64_t)nx * ny * nz;
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
-    if (start[c + 1] == start[c]) continue;
-    const int x = (int)(c % nx), y = (int)((c / nx) % ny), z = (int)(c / ((int64_t)nx * ny));
-    const int b = (x & 3) + 4 * (y & 3) + 16 * (z & 3);
-    atomicOr(&occ[(x >> 2) + (int64_t)onx * ((y >> 2) + (int64_t)ony * (z >> 2))], 1ull << b);
-  }
-}
-
 __global__ void __launch_bounds__(kBlock) k_corr_flags(const int32_t* __restrict__ cj, int64_t ns,
                                                        uint8_t* __restrict__ flags) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x)
@@ -257,7 +244,7 @@ static void desc_pack(const GridBuild& G, const void* base, const float4* normal
   d[11] = (double)((const char*)G.start - (const char*)base);
   d[12] = (double)((const char*)normals - (const char*)base);
   d[13] = kDescMagic;
-  d[14] = d[15] = 0;  // block occupancy: offset, present flag (set by the target build)
+  d[14] = d[15] = 0;
 }
 
 static bool desc_unpack(const double* d, const void* base, GridView* g, const float4** normals) {
@@ -271,13 +258,6 @@ static bool desc_unpack(const double* d, const void* base, GridView* g, const fl
   g->pts = (const float4*)((const char*)base + (int64_t)d[10]);
   g->start = (const int32_t*)((const char*)base + (int64_t)d[11]);
   *normals = (const float4*)((const char*)base + (int64_t)d[12]);
-  g->occ = nullptr;
-  g->onx = g->ony = 0;
-  if (d[15] == 1.0 && !getenv("O3DX_ICP_NO_OCC")) {
-    g->occ = (const unsigned long long*)((const char*)base + (int64_t)d[14]);
-    g->onx = (g->nx + 3) / 4;
-    g->ony = (g->ny + 3) / 4;
-  }
   return true;
 }
 
@@ -380,21 +360,6 @@ extern "C" int o3dx_icp_target_build(const float* tgt, const float* tgt_normals,
   O3DX_TRY(grid_build(tgt, nt, icp_occ(), icp_min_h(max_corr), target_ws, target_ws_bytes, as_stream(stream), &G, nullptr,
                       tgt_normals, false, icp_cap_mult()));
   desc_pack(G, target_ws, G.extra, desc);
-  // block occupancy in the build's per-cell count buffer (free once built)
-  const GridView& g = G.view;
-  const int64_t onx = (g.nx + 3) / 4, ony = (g.ny + 3) / 4, onz = (g.nz + 3) / 4;
-  const int64_t blocks = onx * ony * onz;
-  if (nt > 0 && blocks * 8 <= (G.cap_cells + 1) * 4 && ((uintptr_t)G.count & 7) == 0) {
-    hipStream_t s = as_stream(stream);
-    unsigned long long* occ = reinterpret_cast<unsigned long long*>(G.count);
-    O3DX_HIP(hipMemsetAsync(occ, 0, (size_t)blocks * 8, s));
-    const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
-    hipLaunchKernelGGL(k_occ_build, dim3(grid_for(nc, kBlock, 16384)), dim3(kBlock), 0, s, g.start, g.nx, g.ny, g.nz,
-                       (int)onx, (int)ony, occ);
-    O3DX_HIP(hipGetLastError());
-    desc[14] = (double)((const char*)occ - (const char*)target_ws);
-    desc[15] = 1.0;
-  }
   return 0;
 }
 

@@ -267,20 +267,18 @@ def test_icp_accumulate_sorted_source_layout(dev):
 
 
 @pytest.mark.parametrize("shift", [0.0, 0.006, 0.015, 0.05])
-def test_icp_block_occupancy_search_exact(dev, shift, monkeypatch):
-    """The block-occupancy path of the 1-NN search (GridView::occ: empty
-    4x4x4 blocks skipped) returns exactly the plain shell search's matches
-    — sources displaced by up to and beyond max_correspondence_distance, as
-    at ICP's first iteration — and the oracle's moments."""
+def test_icp_displaced_source_exact(dev, shift):
+    """ICP correspondences for sources displaced by up to and beyond
+    max_correspondence_distance (ICP's first iterations): the sorted and the
+    caller-order source give the same matches, and the moments equal the
+    oracle's."""
     src, tgt = _icp_case(40000, seed=6)
     tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
     T = S.rigid_transform(2.0, (0, 1, 1), (shift, -shift / 2, shift / 3))
     target = ops.ICPTarget(torch.from_numpy(tgt).to(dev), torch.from_numpy(tn).to(dev), 0.02)
     s = torch.from_numpy(src).to(dev)
     a, ca = target.accumulate(s, T, want_corr=True)
-    monkeypatch.setenv("O3DX_ICP_NO_OCC", "1")
-    b, cb = target.accumulate(s, T, want_corr=True)
-    monkeypatch.delenv("O3DX_ICP_NO_OCC")
+    b, cb = target.accumulate(ops.spatial_sort(s), T, want_corr=True)
     assert torch.equal(ca, cb)
     assert a[28] == b[28] and np.array_equal(a[:30], b[:30])
     ref = O.icp_accumulate(src, tgt, tn, 0.02, T)

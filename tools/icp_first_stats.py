@@ -9,7 +9,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "open3d-py-extension_amd"))
 
-SETTINGS = [{}, {"O3DX_ICP_NO_OCC": "1"}, {"O3DX_ICP_OCC": "4"}, {"O3DX_ICP_OCC": "1"}, {"O3DX_ICP_MINH_DIV": "8"},
+SETTINGS = [{}, {"O3DX_ICP_OCC": "4"}, {"O3DX_ICP_OCC": "1"}, {"O3DX_ICP_MINH_DIV": "8"},
             {"O3DX_ICP_MINH_DIV": "32"}, {"O3DX_ICP_CAP": "24"}]
 
 
