@@ -339,6 +339,205 @@ __global__ void __launch_bounds__(kBlock) k_voxel_assign_hash(const float* __res
   }
 }
 
+// ------------------------------------------------- hash-binned sparse path
+// Grids too large for a dense table (sparse scenes at fine voxel sizes, C5):
+// instead of one global hash table hit by two random memory-side atomics per
+// point, the points are binned by a hash of their voxel into kHBins bins (the
+// brick path's count / scan / scatter shape: one LDS histogram per block,
+// runs written contiguously), then one workgroup per bin takes the max index
+// per distinct voxel in an LDS hash table.  Every voxel lands in exactly one
+// bin, so the per-bin maxima are the global ones.
+// The hash is a bijection of the k-bit linear voxel id (xorshifts and odd
+// multiplies mod 2^k), so a voxel is its bin (top 12 bits) plus the other
+// k - 12 bits: one 8-B entry (rest << 32 | point index) per point, a 4-B LDS
+// key.  A bin whose distinct voxels fill its LDS table, or points outside the
+// grid, set err bits 4 / 8 and the caller redoes the call with the global
+// hash table.
+constexpr int kHBins = 4096;                  // = kMaxBuckets (count histogram in LDS)
+constexpr int kHBinBits = 12;
+constexpr int kHSlotsMax = 16384;             // LDS table per bin: 16384 x (4 B key + 4 B max)
+constexpr int kHReduceBlock = 1024;
+constexpr int kHMaxBits = kHBinBits + 31;     // the rest must fit 31 bits (0xFFFFFFFF = empty)
+
+struct HMix {
+  int k;          // bits of the linear voxel id
+  int sh;         // xorshift
+  uint64_t mask;  // 2^k - 1
+};
+
+__device__ __forceinline__ uint64_t hmix(uint64_t h, const HMix& m) {
+  h ^= h >> m.sh;
+  h = (h * 0x9E3779B97F4A7C15ull) & m.mask;
+  h ^= h >> m.sh;
+  h = (h * 0xC2B2AE3D27D4EB4Full) & m.mask;
+  h ^= h >> m.sh;
+  return h;
+}
+
+// the point's mixed voxel id, false when the point is outside the grid
+__device__ __forceinline__ bool voxel_hid(const P3& q, const VoxelGeom& g, const HMix& m, uint64_t* h) {
+  int v[3];
+  if (!voxel_of(q, g, v)) return false;
+  *h = hmix((uint64_t)v[0] + (uint64_t)g.nx * ((uint64_t)v[1] + (uint64_t)g.ny * (uint64_t)v[2]), m);
+  return true;
+}
+
+__device__ __forceinline__ int hbin_of(uint64_t h, const HMix& m) { return (int)(h >> (m.k - kHBinBits)); }
+
+__global__ void __launch_bounds__(kBinBlock) k_hbin_count(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+                                                       HMix m, int32_t* __restrict__ bhist, int* __restrict__ err) {
+  __shared__ int32_t hist[kHBins];
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int k = threadIdx.x; k < kHBins; k += kBinBlock) hist[k] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kBinChunk;
+  bool bad = false;
+#pragma unroll 4
+  for (int j = 0; j < kBinPer; ++j) {
+    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    if (i >= n) break;
+    uint64_t h;
+    if (voxel_hid(p[i], g, m, &h))
+      atomicAdd(&hist[hbin_of(h, m)], 1);
+    else
+      bad = true;
+  }
+  if (bad) *err = 8;
+  __syncthreads();
+  for (int k = threadIdx.x; k < kHBins; k += kBinBlock) bhist[(int64_t)k * gridDim.x + blockIdx.x] = hist[k];
+}
+
+// dynamic LDS: stage[kBinRound] (u64), cur[kHBins], loc[kHBins]
+inline size_t hscatter_lds_bytes() { return kBinRound * sizeof(uint64_t) + 2 * (size_t)kHBins * sizeof(int32_t); }
+
+__global__ void __launch_bounds__(kBinBlock) k_hbin_scatter(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+                                                         HMix m, const int32_t* __restrict__ boff,
+                                                         uint64_t* __restrict__ entries) {
+  extern __shared__ uint64_t lds_u64[];
+  uint64_t* stage = lds_u64;
+  int32_t* cur = reinterpret_cast<int32_t*>(lds_u64 + kBinRound);  // global address of stage slot 0, per bin
+  int32_t* loc = cur + kHBins;                                       // round: count -> offset -> cursor
+  __shared__ int32_t wsum[kBinBlock / 64 + 1];
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int k = threadIdx.x; k < kHBins; k += kBinBlock) cur[k] = boff[(int64_t)k * gridDim.x + blockIdx.x];
+  const int64_t base = (int64_t)blockIdx.x * kBinChunk;
+  constexpr int kPer = kBinRound / kBinBlock;
+  constexpr int span = kHBins / kBinBlock;
+  const int rbits = m.k - kHBinBits;
+  for (int r0 = 0; r0 < kBinChunk && base + r0 < n; r0 += kBinRound) {
+    for (int k = threadIdx.x; k < kHBins; k += kBinBlock) loc[k] = 0;
+    __syncthreads();
+    // entry per point: bin << 52 | rest << 32 | index (~0: none)
+    uint64_t en[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = base + r0 + threadIdx.x + (int64_t)j * kBinBlock;
+      uint64_t h;
+      en[j] = ~0ull;
+      if (i < n && voxel_hid(p[i], g, m, &h)) {
+        en[j] = ((uint64_t)hbin_of(h, m) << 52) | ((h & ((1ull << rbits) - 1)) << 32) | (uint32_t)i;
+        atomicAdd(&loc[(int)(en[j] >> 52)], 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    const int k0 = threadIdx.x * span, k1 = k0 + span;
+    int run = 0;
+    for (int k = k0; k < k1; ++k) run += loc[k];
+    int tot;
+    int ex = block_excl_scan<kBinBlock>(run, wsum, &tot);
+    for (int k = k0; k < k1; ++k) {
+      const int c = loc[k];
+      loc[k] = ex;
+      cur[k] -= ex;
+      ex += c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (en[j] == ~0ull) continue;
+      stage[atomicAdd(&loc[(int)(en[j] >> 52)], 1)] = en[j];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < tot; t += kBinBlock) {
+      const uint64_t e = stage[t];
+      entries[cur[(int)(e >> 52)] + t] = e & 0x000fffffffffffffull;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kHBins; k += kBinBlock) cur[k] += loc[k];
+    __syncthreads();
+  }
+}
+
+// One workgroup per bin: the max index per distinct voxel in an LDS hash table
+// of `slots` (power of two) entries; flags[rep] = 1; with the trace, rep by
+// global slot (bin * slots + slot) and each point's global slot.
+__global__ void __launch_bounds__(kHReduceBlock) k_hbin_reduce(const uint64_t* __restrict__ entries,
+                                                               const int32_t* __restrict__ boff, int nblk, int slots,
+                                                               uint8_t* __restrict__ flags, int32_t* __restrict__ rep,
+                                                               int32_t* __restrict__ vid, int* __restrict__ err) {
+  __shared__ uint32_t hk[kHSlotsMax];
+  __shared__ int32_t hr[kHSlotsMax];
+  __shared__ int full;
+  for (int k = threadIdx.x; k < slots; k += kHReduceBlock) {
+    hk[k] = 0xFFFFFFFFu;
+    hr[k] = -1;
+  }
+  if (threadIdx.x == 0) full = 0;
+  __syncthreads();
+  const int bk = blockIdx.x;
+  const uint32_t mask = (uint32_t)slots - 1u;
+  const int32_t e0 = boff[(int64_t)bk * nblk], e1 = boff[(int64_t)(bk + 1) * nblk];
+  for (int32_t e = e0 + threadIdx.x; e < e1; e += kHReduceBlock) {
+    const uint64_t w = entries[e];
+    const uint32_t key = (uint32_t)(w >> 32);
+    const int32_t idx = (int32_t)(uint32_t)w;
+    uint32_t s = key & mask;  // the rest is already mixed
+    int probes = 0;
+    while (true) {
+      const uint32_t prev = atomicCAS(&hk[s], 0xFFFFFFFFu, key);
+      if (prev == 0xFFFFFFFFu || prev == key) break;
+      s = (s + 1) & mask;
+      if (++probes == slots) break;
+    }
+    if (probes == slots) {  // the bin's table is full
+      full = 1;
+      continue;
+    }
+    atomicMax(&hr[s], idx);
+    if (vid) vid[idx] = bk * slots + (int32_t)s;
+  }
+  __syncthreads();
+  if (full) {
+    if (threadIdx.x == 0) atomicOr(err, 4);
+    return;
+  }
+  for (int k = threadIdx.x; k < slots; k += kHReduceBlock) {
+    const int32_t r = hr[k];
+    if (rep) rep[(int64_t)bk * slots + k] = r;
+    if (r >= 0) flags[r] = 1;
+  }
+}
+
+// LDS slots per bin: room for every point of an average bin at load <= 1/2,
+// at least 256 (the trace's rep table, kHBins x slots ints, then fits the
+// dense-table region) and at most kHSlotsMax
+static int hbin_slots(int64_t n) {
+  int s = 256;
+  while (s < kHSlotsMax && (int64_t)s < 2 * ((n + kHBins - 1) / kHBins)) s <<= 1;
+  return s;
+}
+
+static HMix hbin_mix(double nvox) {
+  HMix m{};
+  int k = kHBinBits + 1;
+  while (k < 63 && std::ldexp(1.0, k) < nvox) ++k;
+  m.k = k;
+  m.sh = std::max(1, (k + 1) / 2);
+  m.mask = k >= 64 ? ~0ull : (1ull << k) - 1;
+  return m;
+}
+
 __global__ void __launch_bounds__(kBlock) k_voxel_mark(const int32_t* __restrict__ rep, int64_t nslots,
                                                        uint8_t* __restrict__ flags) {
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nslots; v += (int64_t)gridDim.x * blockDim.x) {
@@ -569,7 +768,13 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   const unsigned grid = grid_for(n, kBlock, 8192);
   int64_t counts[3];
   bool grid_kept = false;
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  // sparse grids: hash-binned reduction from kHBinMin points (below it the
+  // global table is small enough to stay in cache), the global hash table
+  // otherwise or when a bin's LDS table overflowed
+  int64_t hbin_min = (int64_t)1 << 22;
+  if (const char* e = getenv("O3DX_VOXEL_HBIN_MIN")) hbin_min = atoll(e);  // tests / tuning
+  bool hbin_ok = hbin_min >= 0;
+  for (int attempt = 0; attempt < 3; ++attempt) {
     grid_kept = false;
     int64_t nslots;
     O3DX_HIP(hipMemsetAsync(w.count, 0, 8 * sizeof(int64_t), s));
@@ -606,6 +811,26 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       // read of the cloud costs what the random gather does)
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
                              w.scan_tmp, s));
+    } else if (!dense && hbin_ok && n >= hbin_min && hbin_mix(nvox).k <= kHMaxBits) {
+      const unsigned nblk = (unsigned)((n + kBinChunk - 1) / kBinChunk);
+      const HMix hm = hbin_mix(nvox);
+      int slots = hbin_slots(n);
+      if (const char* e = getenv("O3DX_VOXEL_HBIN_SLOTS"))  // tests: force the overflow fall-back
+        slots = std::max(2, std::min(slots, atoi(e)));
+      const bool trace = voxel_of_point || cubic_id;
+      KTimer kt("voxel_assign", s);
+      O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
+      hipLaunchKernelGGL(k_hbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, hm, w.bhist,
+                         reinterpret_cast<int*>(w.count + 1));
+      O3DX_TRY(exclusive_scan_i32(w.bhist, w.boff, (int64_t)kHBins * nblk, w.scan_tmp, s));
+      hipLaunchKernelGGL(k_hbin_scatter, dim3(nblk), dim3(kBinBlock), hscatter_lds_bytes(), s, xyz, n, g, hm, w.boff,
+                         w.entries);
+      hipLaunchKernelGGL(k_hbin_reduce, dim3(kHBins), dim3(kHReduceBlock), 0, s, w.entries, w.boff, (int)nblk, slots,
+                         w.flags, trace ? w.table : nullptr, trace ? w.vid : nullptr,
+                         reinterpret_cast<int*>(w.count + 1));
+      kt.stop();
+      KTimer kc("voxel_compact", s);
+      O3DX_TRY(compact_flags(w.flags, n, rep_idx, trace ? w.pos : nullptr, w.count, w.scan_tmp, s));
     } else {
       if (dense) {
         nslots = (int64_t)nvox;
@@ -650,6 +875,10 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     }
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
+    if ((errflag & 12) && !(errflag & ~12)) {  // hash-binned path: bin table full / point outside: global hash
+      hbin_ok = false;
+      continue;
+    }
     if (xwin) return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_window: points outside the x-key window");
     if (errflag == 2 || !dense)
       return fail(O3DX_ENOTSUP, "voxel grid spans more than 2^%d cells per axis", kHashBits);
