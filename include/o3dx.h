@@ -325,6 +325,20 @@ int o3dx_plane_inliers(const float* xyz_dev, int64_t n, const double* plane_host
                        double distance_threshold, int32_t* idx_out_dev,
                        int64_t* count_host, void* ws, size_t ws_bytes,
                        void* stream);
+/* Plane selection / distance (PointCloudSelections.get_index_by_plane,
+ * select_by_plane, distance2plane — reference PointCloud.py:278-290, 400-404;
+ * the seg_planes / remove_plane_outlier rounds, :406-409, :941-985).
+ * s = ((x*a + y*b) + z*c + d) / sqrt(a*a + b*b + c*c) in float64, unfused (the
+ * order of numpy's (p*abc).sum(1) + d).  dist_out_dev (optional): s per point.
+ * idx_out_dev (optional): ascending indices with |s| < hi (band == 0) or
+ * lo < s < hi (band == 1), complemented when invert != 0; count_host gets
+ * their number.  Workspace only needed with idx_out_dev. */
+size_t o3dx_plane_select_workspace_bytes(int64_t n);
+int o3dx_plane_select(const float* xyz_dev, int64_t n, const double* plane_host,
+                      int band, double lo, double hi, int invert,
+                      double* dist_out_dev, int32_t* idx_out_dev,
+                      int64_t* count_host, void* ws, size_t ws_bytes,
+                      void* stream);
 int o3dx_plane_moments(const float* xyz_dev, const int32_t* idx_dev,
                        int64_t count, const double* centroid_host,
                        double* sums_host, void* ws, size_t ws_bytes,

@@ -1261,6 +1261,77 @@ __device__ __forceinline__ void sym_rows(const float2* txy, const float* tz, int
   }
 }
 
+// The mirrored stencil with a stencil position per candidate (compact lists,
+// k_normals_stile<..., CL = true>): position P0(row) + i of row (dy, dz, xa..xb)
+// is slot qs + dy*SY + dz*SZ + (xpos ? xa + i : -xb + i), so a 1-byte list
+// entry (172 positions) replaces the 16-bit LDS slot; s25_slot decodes it
+// from the per-block table of (dy, dz, xa + i, -xb + i) bytes.
+constexpr SRow kS25Rows[] = {
+#define O3DX_SROW(DY, DZ, XA, XB) SRow{DY, DZ, XA, (XB) - (XA) + 1},
+    O3DX_S25_ROWS(O3DX_SROW)
+#undef O3DX_SROW
+};
+constexpr int kS25N = (int)(sizeof(kS25Rows) / sizeof(SRow));
+constexpr int s25_pos0(int i) {
+  int p = 0;
+  for (int j = 0; j < i; ++j) p += kS25Rows[j].len;
+  return p;
+}
+constexpr int kS25Pos = s25_pos0(kS25N);
+static_assert(kS25Pos <= 256, "stencil positions must fit a byte");
+
+__device__ __forceinline__ int32_t s25_entry(int p) {  // host of the per-block table
+  int r = 0;
+  while (r + 1 < kS25N && s25_pos0(r + 1) <= p) ++r;
+  const SRow w = kS25Rows[r];
+  const int i = p - s25_pos0(r);
+  return (int32_t)((uint32_t)(w.dy & 0xFF) | ((uint32_t)(w.dz & 0xFF) << 8) | ((uint32_t)((w.xa + i) & 0xFF) << 16) |
+                   ((uint32_t)((i - (w.xa + w.len - 1)) & 0xFF) << 24));
+}
+
+__device__ __forceinline__ int s25_slot(int32_t e, int qs, int SY, int SZ, bool xpos) {
+  const int dy = __builtin_amdgcn_sbfe(e, 0, 8), dz = __builtin_amdgcn_sbfe(e, 8, 8);
+  const int dx = xpos ? __builtin_amdgcn_sbfe(e, 16, 8) : (e >> 24);
+  return qs + dy * SY + dz * SZ + dx;
+}
+
+template <int L, int P0, class F>
+__device__ __forceinline__ void scan_run_p(const float2* txy, const float* tz, int st, const float4 q, F& f) {
+  float2 a[L];
+  float c[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    a[i] = txy[st + i];
+    c[i] = tz[st + i];
+  }
+#pragma unroll
+  for (int i = 0; i + 1 < L; i += 2) {
+    const f32x2 dd = dist2_pair(q, (f32x2){a[i].x, a[i + 1].x}, (f32x2){a[i].y, a[i + 1].y}, (f32x2){c[i], c[i + 1]});
+    f(P0 + i, st + i, dd.x);
+    f(P0 + i + 1, st + i + 1, dd.y);
+  }
+  if (L & 1) f(P0 + L - 1, st + L - 1, dist2_f32(q, a[L - 1].x, a[L - 1].y, c[L - 1]));
+}
+
+template <int I, class F>
+__device__ __forceinline__ void s25_rows(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
+                                         const float4 q, F& f) {
+  if constexpr (I < kS25N) {
+    constexpr SRow r = kS25Rows[I];
+    scan_run_p<r.len, s25_pos0(I)>(txy, tz, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)), q, f);
+    __builtin_amdgcn_sched_barrier(0);
+    s25_rows<I + 1>(txy, tz, qs, SY, SZ, xpos, q, f);
+  }
+}
+
+// stencil_scan with f(position, slot, d2)
+template <class F>
+__device__ __forceinline__ void stencil_scan_p(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
+                                               const float4 q, F&& f) {
+  asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
+  s25_rows<0>(txy, tz, qs, SY, SZ, xpos, q, f);
+}
+
 template <bool RING, int SY, int SZ, class F>
 __device__ __forceinline__ void stencil_scan_sym(const float2* txy, const float* tz, int qs, const float4 q, F&& f) {
   asm volatile("" : "+v"(qs));
@@ -1296,26 +1367,33 @@ constexpr int kMergedCap = 56;
 constexpr float kMergedFrac = 0.75f;
 
 // WPE: waves per SIMD to register-allocate for (LDS allows 2 for 1x1, 3 for 2x2)
-template <int KMAX, int WY, int WZ, int WPE, bool MERGED, bool SYM>
+// CL (compact LDS, mirrored stencil only): list entries are 1-byte stencil
+// positions (decoded through the per-block table ptab) and the histogram
+// counters are packed 16-bit — a 2x2 workgroup then needs 36 KB instead of
+// 50 KB, so 4 workgroups (16 waves) fit a CU instead of 3.
+template <int KMAX, int WY, int WZ, int WPE, bool MERGED, bool SYM, bool CL = false>
 __global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
                 int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
+  static_assert(!CL || (!SYM && !MERGED), "compact lists: mirrored two-scan form only");
   using Sh = StileShape<WY, WZ, SYM>;
+  using LT = typename std::conditional<CL, uint8_t, uint16_t>::type;
   constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::SLOTS;
   __shared__ float2 txy[kSlots];
   __shared__ float tz[kSlots];
+  __shared__ int32_t ptab[CL ? kS25Pos : 1];
   // list capacity: the k - 1 points below the k-th bin + that bin (<= kRefineAt
   // after refinement) + the rounding band; the symmetric layout trims it to
   // KMAX + 12 so three 2x2 workgroups still fit a CU's LDS
   constexpr int kListMax = KMAX + (SYM ? 12 : kBndCap);
   constexpr int kListRows = MERGED && kMergedCap > kListMax ? kMergedCap + 1 : kListMax + 1;
-  constexpr int kListWords = (kListRows * 64 * 2 + 3) / 4;
-  constexpr int kHistWords = kTileSlots * 64;
+  constexpr int kListWords = (kListRows * 64 * (int)sizeof(LT) + 3) / 4;
+  constexpr int kHistWords = (CL ? (kTileSlots + 1) / 2 : kTileSlots) * 64;
   constexpr int kSelWords = MERGED ? kListWords : (kListWords > kHistWords ? kListWords : kHistWords);
   __shared__ uint32_t selbuf[Sh::NW][kSelWords];
   __shared__ uint32_t histbuf[MERGED ? Sh::NW : 1][MERGED ? kHistWords : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint16_t(*lst)[64] = reinterpret_cast<uint16_t(*)[64]>(selbuf[wv]);
+  LT(*lst)[64] = reinterpret_cast<LT(*)[64]>(selbuf[wv]);
   uint32_t* hw = MERGED ? histbuf[MERGED ? wv : 0] : selbuf[wv];
   const int nb = d.nbx * d.nby * d.nbz;
   const int b = xcd_block(blockIdx.x, nb);
@@ -1340,6 +1418,8 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
         tz[a] = buf[j].z;
       }
     }
+    if constexpr (CL)
+      for (int t = threadIdx.x; t < kS25Pos; t += kT) ptab[t] = s25_entry(t);
   }
   __syncthreads();
   const int lx = lane & 3, ly = ((lane >> 2) & 3) + kVB * (wv % WY), lz = (lane >> 4) + kVB * (wv / WY);
@@ -1364,30 +1444,48 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
     const float T2 = R2 * kMergedFrac;
     int nl = 0;  // MERGED: candidates below T2 appended by the first pass
     bool wide = false;  // SYM: the gap^2 == 5 ring is scanned too (k-th neighbour beyond sqrt 5)
+    // body(stencil position, LDS slot, f32 d^2); the position is only known
+    // (compile-time) to the compact-list scan
     auto scan = [&](auto&& body) {
       if constexpr (SYM) {
-        stencil_scan_sym<false, kSY, kSZ>(txy, tz, qs, q, body);
-        if (wide) stencil_scan_sym<true, kSY, kSZ>(txy, tz, qs, q, body);
+        auto b3 = [&](int pp, float d2) { body(0, pp, d2); };
+        stencil_scan_sym<false, kSY, kSZ>(txy, tz, qs, q, b3);
+        if (wide) stencil_scan_sym<true, kSY, kSZ>(txy, tz, qs, q, b3);
+      } else if constexpr (CL) {
+        stencil_scan_p(txy, tz, qs, SY, SZ, xpos, q, body);
       } else {
-        stencil_scan(txy, tz, qs, SY, SZ, xpos, q, body);
+        stencil_scan(txy, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) { body(0, pp, d2); });
       }
     };
     TileHist th;
     auto hist = [&](float lo_, float sc_, auto app) {
+      constexpr int kHW = CL ? (kTileSlots + 1) / 2 : kTileSlots;
 #pragma unroll
-      for (int i = 0; i < kTileSlots; ++i) hw[i * 64 + lane] = 0u;
+      for (int i = 0; i < kHW; ++i) hw[i * 64 + lane] = 0u;
       const float off_ = -lo_ * sc_;
-      auto body = [&](int pp, float d2) {
+      auto body = [&](int ps, int pp, float d2) {
         const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f);
-        atomicAdd(&hw[(ix + 1) * 64 + lane], 1u);
+        if constexpr (CL)
+          atomicAdd(&hw[((ix + 1) >> 1) * 64 + lane], 1u << (((ix + 1) & 1) * 16));
+        else
+          atomicAdd(&hw[(ix + 1) * 64 + lane], 1u);
         if constexpr (decltype(app)::value) {
-          lst[min(nl, kMergedCap)][lane] = (uint16_t)pp;
+          lst[min(nl, kMergedCap)][lane] = (LT)pp;
           nl += d2 < T2 ? 1 : 0;
         }
       };
       scan(body);
+      if constexpr (CL) {
 #pragma unroll
-      for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
+        for (int i = 0; i < kTileSlots; i += 2) {
+          const uint32_t w = hw[(i >> 1) * 64 + lane];
+          th.h[i] = w & 0xFFFFu;
+          if (i + 1 < kTileSlots) th.h[i + 1] = w >> 16;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
+      }
     };
     hist(0.0f, (float)kHistBins / R2, std::integral_constant<bool, MERGED>{});
     int total = 0;
@@ -1428,9 +1526,9 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
       if (!have) {
         n = 0;
         cap = kListMax;
-        auto body = [&](int pp, float d2) {
+        auto body = [&](int ps, int pp, float d2) {
           if (d2 < Up) {  // masked store: only the accepted lanes take part in the LDS banking
-            lst[min(n, kListMax)][lane] = (uint16_t)pp;
+            lst[min(n, kListMax)][lane] = (LT)(CL ? ps : pp);
             ++n;
           }
         };
@@ -1441,11 +1539,18 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
         return;
       }
       if (n > cap && d.stats) atomicAdd(&d.stats[5], 1ull);
+      // list entry -> LDS slot (compact lists: decode the stencil position)
+      auto slot = [&](int p) { return CL ? s25_slot(ptab[p], qs, SY, SZ, xpos) : p; };
       fb = n > cap ||
            !finish_selection<KMAX>(
-               q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(txy[p].x, txy[p].y, tz[p], 0.f); }, prior,
-               oi, out, d.nbr,
+               q, kneed, n, Lm, U, lst, lane,
                [&](int p) {
+                 const int sp = slot(p);
+                 return make_float4(txy[sp].x, txy[sp].y, tz[sp], 0.f);
+               },
+               prior, oi, out, d.nbr,
+               [&](int p0) {
+                 const int p = slot(p0);
                  const int bz = p / kSZ, r = p - bz * kSZ, by = r / kSY, bx = r - by * kSY;
                  return __float_as_int(
                      d.vox[(gx0 + bx) + (int64_t)d.nx * ((gy0 + by) + (int64_t)d.ny * (gz0 + bz))].w);
@@ -2331,10 +2436,12 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   d.nz = (int)geom[6];
   // block shape (O3DX_STILE_SHAPE): 3 (default) 2x2 waves sharing one box, allocated
   // for 3 waves/SIMD; 2: the same block at 2 waves/SIMD; 1: one wave per 4^3
-  // block; 4: 2x3 waves (a larger shared box, 2 workgroups = 12 waves per CU)
+  // block; 4: 2x3 waves (a larger shared box, 2 workgroups = 12 waves per CU);
+  // 5 / 6: 2x2 / 2x3 waves with compact lists (1-byte stencil positions,
+  // packed histogram: 4 x 4 / 3 x 6 waves per CU)
   const char* shape_env = getenv("O3DX_STILE_SHAPE");
   const int shape = shape_env ? atoi(shape_env) : 3;
-  const int wy = shape == 1 ? 1 : 2, wz = shape == 1 ? 1 : shape == 4 ? 3 : 2;
+  const int wy = shape == 1 ? 1 : 2, wz = shape == 1 ? 1 : (shape == 4 || shape == 6) ? 3 : 2;
   d.nbx = (d.nx + kVB - 1) / kVB;
   d.nby = (d.ny + kVB * wy - 1) / (kVB * wy);
   d.nbz = (d.nz + kVB * wz - 1) / (kVB * wz);
@@ -2418,6 +2525,12 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
         O3DX_STILE_LAUNCH2(2, 3, 3, false);
       } else if (shape == 3) {
         O3DX_STILE_LAUNCH(2, 3, false);
+      } else if (shape == 6 && !sym) {
+        hipLaunchKernelGGL((k_normals_stile<32, 2, 3, 4, false, false, true>), dim3((unsigned)nb), dim3(384), 0, s, d,
+                           kneed, prior, out, list, lens, ffb, dg);
+      } else if (shape == 5 && !sym) {
+        hipLaunchKernelGGL((k_normals_stile<32, 2, 2, 4, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, d,
+                           kneed, prior, out, list, lens, ffb, dg);
       } else {
         O3DX_STILE_LAUNCH(2, 2, false);
       }

@@ -480,6 +480,29 @@ __global__ void __launch_bounds__(kBlock) k_plane_flags(const float* __restrict_
   }
 }
 
+// Plane selection of the reference's PointCloudSelections (PointCloud.py:
+// 278-290, 400-404): s = ((x*a + y*b) + z*c + d) / nrm, unfused, the order of
+// numpy's `(p*abc).sum(1) + d` (distance2plane); flag = |s| < thr (BAND 0) or
+// lo < s < hi (BAND 1), xor invert.  dist (optional) receives s.
+template <bool BAND>
+__global__ void __launch_bounds__(kBlock) k_plane_band(const float* __restrict__ xyz, int64_t n, double a, double b,
+                                                       double c, double d, double nrm, double lo, double hi,
+                                                       int invert, uint8_t* __restrict__ flags,
+                                                       double* __restrict__ dist) {
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const P3 q = p[i];
+    const double t = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn((double)q.x, a), __dmul_rn((double)q.y, b)),
+                                         __dmul_rn((double)q.z, c)), d);
+    const double s = __ddiv_rn(t, nrm);
+    if (dist) dist[i] = s;
+    if (flags) {
+      const bool in = BAND ? (s > lo && s < hi) : (fabs(s) < hi);
+      flags[i] = (uint8_t)(in != (invert != 0));
+    }
+  }
+}
+
 constexpr int kMomBlocks = 256;
 
 // pass 1 (centroid == nullptr): {x, y, z}; pass 2: centred {xx, xy, xz, yy, yz, zz}
@@ -996,6 +1019,49 @@ extern "C" int o3dx_plane_inliers(const float* xyz, int64_t n, const double* pla
                      plane[2], plane[3], thr, flags);
   O3DX_TRY(compact_flags(flags, n, idx_out, nullptr, cnt, tmp, s));
   O3DX_TRY(read_back(count_host, cnt, sizeof(int64_t), s));
+  return 0;
+}
+
+extern "C" size_t o3dx_plane_select_workspace_bytes(int64_t n) {
+  return Arena::align(n + 17) + Arena::align(compact_workspace_ints(n) * 4 + 1) + 512;
+}
+
+extern "C" int o3dx_plane_select(const float* xyz, int64_t n, const double* plane, int band, double lo, double hi,
+                                 int invert, double* dist_out, int32_t* idx_out, int64_t* count_host, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  if (n < 0 || !plane || (n > 0 && !xyz) || (idx_out && !count_host) || (!idx_out && !dist_out))
+    return fail(O3DX_EINVAL, "o3dx_plane_select: bad args");
+  if (idx_out && (!ws || ws_bytes < o3dx_plane_select_workspace_bytes(n)))
+    return fail(O3DX_ENOMEM, "plane_select workspace too small");
+  if (n == 0) {
+    if (count_host) *count_host = 0;
+    return 0;
+  }
+  // (a**2 + b**2 + c**2) ** 0.5 (Python: correctly rounded squares, left-to-right sum)
+  const double nrm = std::sqrt(plane[0] * plane[0] + plane[1] * plane[1] + plane[2] * plane[2]);
+  hipStream_t s = as_stream(stream);
+  uint8_t* flags = nullptr;
+  int32_t* tmp = nullptr;
+  int64_t* cnt = nullptr;
+  if (idx_out) {
+    Arena ar(ws, ws_bytes);
+    flags = ar.take<uint8_t>(n + 16);
+    tmp = ar.take<int32_t>(compact_workspace_ints(n));
+    cnt = ar.take<int64_t>(2);
+    O3DX_ARENA_CHECK(ar);
+  }
+  const unsigned g = grid_for(n, kBlock, 8192);
+  if (band)
+    hipLaunchKernelGGL(k_plane_band<true>, dim3(g), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1], plane[2], plane[3],
+                       nrm, lo, hi, invert, flags, dist_out);
+  else
+    hipLaunchKernelGGL(k_plane_band<false>, dim3(g), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1], plane[2], plane[3],
+                       nrm, lo, hi, invert, flags, dist_out);
+  O3DX_HIP(hipGetLastError());
+  if (idx_out) {
+    O3DX_TRY(compact_flags(flags, n, idx_out, nullptr, cnt, tmp, s));
+    O3DX_TRY(read_back(count_host, cnt, sizeof(int64_t), s));
+  }
   return 0;
 }
 

@@ -288,13 +288,18 @@ class PointCloudBase:
     def segment_plane(self, thickness: float = 0.01, ransac_n: int = 3, num_iterations: int = 450,
                       probability: float = 0.99999999, seed=None, samples=None) -> Tuple[List, List[int]]:
         """Open3D SegmentPlane (reference PointCloud.py:75-77) -> ([a,b,c,d], inlier indices)."""
+        plane, inl = self._segment_plane_dev(thickness, ransac_n, num_iterations, probability, seed, samples)
+        return plane, inl.cpu().numpy().astype(np.int64).tolist()
+
+    def _segment_plane_dev(self, thickness=0.01, ransac_n=3, num_iterations=450, probability=0.99999999, seed=None,
+                           samples=None):
+        """segment_plane with the inlier indices left on the device (int32)."""
         x = self._dev_points()
         n = x.shape[0]
         if samples is None and n >= ransac_n >= 3 and 0 < probability <= 1:
             samples = ops.ransac_samples(n, ransac_n, num_iterations, _next_seed() if seed is None else seed)
         plane, inl = ops.segment_plane(x, thickness, ransac_n, num_iterations, probability, samples=samples)
-        a, b, c, d = (float(v) for v in plane)
-        return [a, b, c, d], inl.cpu().numpy().astype(np.int64).tolist()
+        return [float(v) for v in plane], inl
 
     def get_aabb(self):
         if not self.has_points():
@@ -542,19 +547,19 @@ class PointCloudSelections(PointCloudBase):
         return self._select_by_idx(self.get_index_by_radius(r), invert=invert)
 
     def get_index_by_plane(self, model, thickness=0.03, invert: bool = False):
-        """|p.abc + d| / |abc| < thickness (strict), or a (lo, hi) signed band
-        (reference PointCloud.py:278-290)."""
-        p = self.get_points()
-        a, b, c, d = model
-        s = (p @ np.asarray([a, b, c], np.float64) + d) / (a ** 2 + b ** 2 + c ** 2) ** 0.5
-        if isinstance(thickness, tuple):
-            res = np.logical_and(s > thickness[0], s < thickness[1])
-        else:
-            res = np.abs(s) < thickness
-        return self._bool2index(res, invert=invert)
+        """|s| < thickness (strict), or a (lo, hi) signed band, s the point's
+        signed distance to the plane (reference PointCloud.py:278-290), decided
+        on the GPU (o3dx_plane_select) in float64; ascending numpy indices."""
+        return self._plane_index_dev(model, thickness, invert).cpu().numpy().astype(np.int64)
+
+    def _plane_index_dev(self, model, thickness, invert: bool = False) -> torch.Tensor:
+        if not self.has_points():
+            return torch.zeros(0, dtype=torch.int32, device=_device())
+        return ops.plane_select(self._dev_points(), np.asarray(model, np.float64).reshape(4), thickness, invert)
 
     def select_by_plane(self, model, thickness=0.03, invert: bool = False):
-        return self._select_by_idx(self.get_index_by_plane(model, thickness), invert=invert)
+        # indices stay on the device (reference PointCloud.py:289-290)
+        return self._select_by_idx(self._plane_index_dev(model, thickness), invert=invert)
 
     def get_index_by_aabb(self, aabb_min, aabb_max, invert: bool = False):
         p = self.get_points()
@@ -715,15 +720,19 @@ class PointCloudUtility(PointCloudSelections):
         return self.merge_pcds([self, pcd], rgb=rgb, intensity=intensity, normals=normals, labels=labels)
 
     def distance2plane(self, plane) -> np.ndarray:
-        a, b, c, d = plane
-        return ((self.get_points() * np.asarray([a, b, c])).sum(1) + d) / (a ** 2 + b ** 2 + c ** 2) ** 0.5
+        """Signed float64 distance to the plane (reference PointCloud.py:400-404),
+        computed on the GPU in numpy's order ((x*a + y*b) + z*c + d) / |abc|."""
+        if not self.has_points():
+            return np.zeros(0)
+        return ops.plane_distance(self._dev_points(), np.asarray(plane, np.float64).reshape(4)).cpu().numpy()
 
     def remove_plane_outlier(self, plane_model, thickness: float = 0.03, similarity: float = 0.999,
                              invert: bool = False):
         cand = self.get_index_by_normals_cosine(plane_model, similarity)
         sub = self._select_by_idx(cand)
-        floor_idx = np.arange(self.size())[cand][sub.get_index_by_plane(plane_model, thickness)]
-        return self._select_by_idx(floor_idx), floor_idx
+        on = sub._plane_index_dev(plane_model, thickness).long()
+        floor_idx = torch.as_tensor(np.asarray(cand, np.int64), device=on.device)[on]
+        return self._select_by_idx(floor_idx), floor_idx.cpu().numpy()
 
     def project2plane(self, plane):
         plane = np.asarray(plane, np.float64)
@@ -832,7 +841,8 @@ class PointCloud(PointCloudUtility):
             return planes, pcds, aabbs
         while rest.size() / raw > minPointsRatio:
             try:
-                plane, inl = rest.segment_plane(thickness, ransac_n, num_iterations)
+                # the inliers stay on the device between the rounds
+                plane, inl = rest._segment_plane_dev(thickness, ransac_n, num_iterations)
             except RuntimeError as e:
                 print(e)
                 break

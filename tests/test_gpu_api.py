@@ -91,6 +91,72 @@ def test_segment_plane_api_and_seg_planes():
     assert len(planes) >= 1 and sum(p.size() for p in pcds) == len(pts)
 
 
+def test_plane_selection_small_cases():
+    """Reference PointCloud.py:278-290, 400-404 on the hand-checked cloud."""
+    pc = o3p.PointCloud(np.array([[0, 0, 0.0], [0, 0, 0.5], [0, 0, 1.0], [3, 0, 0]]))
+    assert list(pc.get_index_by_plane([0, 0, 2, -1], 0.1)) == [1]          # normalised distance
+    assert list(pc.get_index_by_plane([0, 0, 1, -0.5], (-0.6, 0.1))) == [0, 1, 3]
+    assert list(pc.get_index_by_plane([0, 0, 1, -0.5], (-0.6, 0.1), invert=True)) == [2]
+    assert pc.select_by_plane([0, 0, 2, -1], 0.1, invert=True).size() == 3
+    np.testing.assert_array_equal(pc.distance2plane([0, 0, 2, -1]), [-0.5, 0, 0.5, -0.5])
+    empty = o3p.PointCloud()
+    assert len(empty.get_index_by_plane([0, 0, 1, 0], 0.1)) == 0 and len(empty.distance2plane([0, 0, 1, 0])) == 0
+
+
+@pytest.mark.parametrize("n", [1, 1000, 1_000_003])
+def test_plane_selection_bit_exact(n):
+    """distance2plane bit-equal to numpy's ((p*abc).sum(1) + d) / |abc| (the
+    reference's expression), and the |s| < t / (lo, hi) band selections equal to
+    numpy's on the same float64 distances (both orders, invert)."""
+    rng = np.random.default_rng(n)
+    pts = (rng.random((n, 3)) * 4 - 2).astype(np.float32)
+    pc = o3p.PointCloud(pts.astype(np.float64))
+    for plane in ([0.3, -1.2, 2.0, 0.1], [0.0, 0.0, 1.0, -0.25], [1e-3, 5.0, -0.5, 3.0]):
+        a, b, c, d = plane
+        s = ((pts.astype(np.float64) * np.asarray([a, b, c])).sum(1) + d) / (a ** 2 + b ** 2 + c ** 2) ** 0.5
+        got = pc.distance2plane(plane)
+        assert got.dtype == np.float64 and np.array_equal(got, s)
+        for thk in (0.05, 0.5, (-0.2, 0.7), (0.3, -0.3)):
+            exp = (np.logical_and(s > thk[0], s < thk[1]) if isinstance(thk, tuple) else np.abs(s) < thk)
+            assert np.array_equal(pc.get_index_by_plane(plane, thk), np.nonzero(exp)[0])
+            assert np.array_equal(pc.get_index_by_plane(plane, thk, invert=True), np.nonzero(~exp)[0])
+        sel = pc.select_by_plane(plane, 0.05)
+        assert np.array_equal(sel.get_points(), pts[np.abs(s) < 0.05].astype(np.float64))
+
+
+def test_seg_planes_rounds_vs_oracle():
+    """seg_planes (reference PointCloud.py:941-985, loop fixed as documented in
+    INTEGRATION.md): every round's plane, inlier cloud and AABB equal the
+    oracle's SegmentPlane on the remaining points with the same seeded samples;
+    the inliers never leave the device between the rounds."""
+    rng = np.random.default_rng(3)
+    n = 120_000
+    a = np.c_[rng.random((48000, 2)), np.full(48000, 0.3) + rng.normal(0, 0.002, 48000)]
+    b = np.c_[np.full(36000, 0.7) + rng.normal(0, 0.002, 36000), rng.random((36000, 2))]
+    pts = np.concatenate([a, b, rng.random((n - 84000, 3))]).astype(np.float32)
+    pts = pts[rng.permutation(n)]
+    pc = o3p.PointCloud(pts.astype(np.float64))
+    seed0, iters, thr, top_n, ratio = 11, 300, 0.01, 3, 0.2
+    o3p.set_random_seed(seed0)
+    planes, pcds, aabbs = pc.seg_planes(thr, 3, iters, top_n=top_n, minPointsRatio=ratio)
+    rest, seed, r = np.arange(n), seed0, 0
+    while len(rest) / n > ratio:
+        s, seed = seed & 0xFFFFFFFF, (seed * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
+        samples = O.ransac_samples(len(rest), 3, iters, s)
+        rplane, rinl, *_ = O.segment_plane(pts[rest], thr, 3, iters, samples)
+        np.testing.assert_allclose(planes[r], rplane, atol=1e-9)
+        sel = rest[rinl]
+        assert np.array_equal(pcds[r].get_points(), pts[sel].astype(np.float64))
+        np.testing.assert_array_equal(aabbs[r][0], pts[sel].min(0).astype(np.float64))
+        np.testing.assert_array_equal(aabbs[r][1], pts[sel].max(0).astype(np.float64))
+        rest = np.delete(rest, rinl)
+        r += 1
+        if r > top_n:
+            break
+    assert len(planes) == r >= 2 and len(pcds) == r + 1
+    assert np.array_equal(pcds[-1].get_points(), pts[rest].astype(np.float64))
+
+
 def test_kdtree_helpers(bunny):
     pc = o3p.PointCloud(bunny.astype(np.float64))
     k, idx, d2 = pc.get_points_by_knn(100, 20)

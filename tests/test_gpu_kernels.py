@@ -429,6 +429,9 @@ STILE_ENVS = [
     {"O3DX_STILE_SHAPE": "1"},
     {"O3DX_STILE_SHAPE": "2"},
     {"O3DX_STILE_SHAPE": "4"},
+    {"O3DX_STILE_SHAPE": "5"},
+    {"O3DX_STILE_SHAPE": "6"},
+    {"O3DX_STILE_SHAPE": "5", "O3DX_STILE_FORCE_FB": "1"},
     {"O3DX_STILE_MERGED": "1"},
     {"O3DX_STILE_MERGED": "1", "O3DX_STILE_SHAPE": "4"},
     {"O3DX_STILE_MERGED": "1", "O3DX_STILE_SHAPE": "1"},
