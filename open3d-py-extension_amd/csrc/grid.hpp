@@ -228,7 +228,9 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
 }
 
 // Nearest neighbour with d^2 < radius^2 (SearchHybrid(p, r, 1)); returns its
-// original index, -1 if none.
+// original index, -1 if none.  ROWS: the walk beyond the own cell goes by
+// (y, z) rows (below); else by Chebyshev shells of cells.
+template <bool ROWS = true>
 __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, double qy, double qz, double radius,
                                              double* best_d2, int* best_pos) {
   double bd = INFINITY;
@@ -259,6 +261,18 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   auto bound_of = [&](double dist) { return (float)((dist + dl) * (dist + dl) * (1.0 + 1e-6)); };
   float thr = bound_of(radius);
   const float sl3 = 3.0f * g.slack;
+  auto visit_point = [&](int p, const float4 v) {
+    if (dist2_f32(qf, v.x, v.y, v.z) < thr) {
+      const double d = dist2_f64(qx, qy, qz, v);
+      const int oi = __float_as_int(v.w);
+      if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
+        bd = d;
+        bi = oi;
+        bp = p;
+        thr = bound_of(sqrt(d));
+      }
+    }
+  };
   auto visit_cell = [&](int x, int y, int z) {
     const float bx0 = g.ox + (float)x * g.h, by0 = g.oy + (float)y * g.h, bz0 = g.oz + (float)z * g.h;
     const float ex = fmaxf(fmaxf(bx0 - fx, fx - (bx0 + g.h)) - sl3, 0.0f);
@@ -271,18 +285,7 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
       ++st_cells;
       st_cands += p1 - p0;
     }
-    for_points4(g, p0, p1, [&](int p, const float4 v) {
-      if (dist2_f32(qf, v.x, v.y, v.z) < thr) {
-        const double d = dist2_f64(qx, qy, qz, v);
-        const int oi = __float_as_int(v.w);
-        if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
-          bd = d;
-          bi = oi;
-          bp = p;
-          thr = bound_of(sqrt(d));
-        }
-      }
-    });
+    for_points4(g, p0, p1, visit_point);
   };
   visit_cell(cx, cy, cz);
   if (bi >= 0) {
@@ -305,6 +308,61 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
       *best_pos = bp;
       return bi;
     }
+  }
+  if (ROWS) {
+    // Row-ring walk: the (y, z) rows of the cell grid in rings k = max(|y -
+    // cy|, |z - cz|) = 0, 1, 2, ...; each row contributes the x-chord of the
+    // bound ball (cells whose box, grown by the slack, comes closer than
+    // sqrt(thr)) as ONE contiguous point range of the row-major cell array.
+    // Ring k's rows all lie at least g_k from q across y or z, so once
+    // (g_k - slack)^2 reaches thr no later row can hold a point below the
+    // bound.  Per ring O(k) row tests instead of O(k^2) cell tests (the shell
+    // walk below): the far-displaced queries of the first iterations.
+    const int kmax = max(max(cy, g.ny - 1 - cy), max(cz, g.nz - 1 - cz));
+    const double inv_hd = 1.0 / (double)g.h;
+    int rows = 0;
+    for (int k = 0; k <= kmax; ++k) {
+      if (k > 0) {
+        float gk = INFINITY;  // smallest y/z gap of ring k's rows to q (sides with rows only)
+        if (cy - k >= 0) gk = fminf(gk, fy - (g.oy + (float)(cy - k + 1) * g.h));
+        if (cy + k < g.ny) gk = fminf(gk, (g.oy + (float)(cy + k) * g.h) - fy);
+        if (cz - k >= 0) gk = fminf(gk, fz - (g.oz + (float)(cz - k + 1) * g.h));
+        if (cz + k < g.nz) gk = fminf(gk, (g.oz + (float)(cz + k) * g.h) - fz);
+        const float e = gk - sl3;
+        if (e > 0.0f && e * e >= thr) break;
+      }
+      for (int dz = -k; dz <= k; ++dz) {
+        const int z = cz + dz;
+        if (z < 0 || z >= g.nz) continue;
+        const bool zedge = dz == -k || dz == k;
+        const int step = (zedge || k == 0) ? 1 : 2 * k;
+        for (int dy = -k; dy <= k; dy += step) {
+          const int y = cy + dy;
+          if (y < 0 || y >= g.ny) continue;
+          const float by0 = g.oy + (float)y * g.h, bz0 = g.oz + (float)z * g.h;
+          const float ey = fmaxf(fmaxf(by0 - fy, fy - (by0 + g.h)) - sl3, 0.0f);
+          const float ez = fmaxf(fmaxf(bz0 - fz, fz - (bz0 + g.h)) - sl3, 0.0f);
+          const float eyz = fmaf(ez, ez, ey * ey);
+          if (eyz >= thr) continue;
+          const double rx = (double)sqrtf(thr - eyz) + (double)sl3;
+          const int xa = max(0, (int)floor(((double)fx - rx - (double)g.ox) * inv_hd));
+          const int xb = min(g.nx - 1, (int)floor(((double)fx + rx - (double)g.ox) * inv_hd));
+          if (xa > xb) continue;
+          const int rb = g.nx * (y + g.ny * z);
+          const int p0 = g.start[rb + xa], p1 = g.start[rb + xb + 1];
+          if (g.stats) {
+            ++rows;
+            st_cands += p1 - p0;
+          }
+          for_points4(g, p0, p1, visit_point);
+        }
+      }
+      r = k;
+    }
+    search_stats(g, st_cells + rows, st_cands, r + 1);
+    *best_d2 = bd;
+    *best_pos = bp;
+    return bi;
   }
   for (;; ++r) {
     // every point within B of q has been visited (or pruned by the bound)

@@ -85,7 +85,8 @@ __device__ __forceinline__ int64_t icp_source(const float* __restrict__ src, int
 // position (-1: none) and, when asked, the target's original index by source
 // index.  No accumulators live here, so the search runs at full occupancy
 // (the search is latency-bound: many waves hide the dependent cell loads).
-template <bool SORTED>
+// ROWS: the search beyond the own cell walks (y, z) rows (nn_search_dev).
+template <bool SORTED, bool ROWS>
 __global__ void __launch_bounds__(kBlock) k_icp_match(const float* __restrict__ src, int64_t ns, GridView g, Mat4 T,
                                                       double radius, int32_t* __restrict__ mpos,
                                                       int32_t* __restrict__ cj) {
@@ -95,7 +96,7 @@ __global__ void __launch_bounds__(kBlock) k_icp_match(const float* __restrict__ 
   const int64_t i = icp_source<SORTED>(src, j, T, &px, &py, &pz);
   double d2;
   int pos;
-  const int tj = nn_search_dev(g, px, py, pz, radius, &d2, &pos);
+  const int tj = nn_search_dev<ROWS>(g, px, py, pz, radius, &d2, &pos);
   mpos[j] = pos;
   if (cj) cj[i] = tj;
 }
@@ -295,10 +296,17 @@ static int accumulate(const float* src, int64_t ns, bool sorted, const GridView&
     int32_t* cj = want_corr ? w.cj : (int32_t*)nullptr;
     const unsigned nm = grid_for(ns, kBlock, 1 << 30);
     KTimer km("icp_match", s);
-    if (sorted)
-      hipLaunchKernelGGL(k_icp_match<true>, dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
+    // O3DX_ICP_SHELL=1: the Chebyshev shell walk (round 1-2 form) instead of the row walk
+    const bool shell = getenv("O3DX_ICP_SHELL") != nullptr;
+    if (sorted && !shell)
+      hipLaunchKernelGGL((k_icp_match<true, true>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
+    else if (sorted)
+      hipLaunchKernelGGL((k_icp_match<true, false>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
+    else if (!shell)
+      hipLaunchKernelGGL((k_icp_match<false, true>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
     else
-      hipLaunchKernelGGL(k_icp_match<false>, dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
+      hipLaunchKernelGGL((k_icp_match<false, false>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos,
+                         cj);
     km.stop();
     if (sorted)
       hipLaunchKernelGGL(k_icp_moments<true>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, w.partial);

@@ -313,6 +313,30 @@ def test_icp_displaced_source_exact(dev, shift):
     np.testing.assert_allclose(a[:30], ref[:30], rtol=1e-9, atol=1e-9)
 
 
+@pytest.mark.parametrize("shift", [0.0, 0.004, 0.012, 0.03, 0.3])
+def test_icp_row_walk_equals_shell_walk(dev, shift, monkeypatch):
+    """The 1-NN row walk (default) and the Chebyshev shell walk
+    (O3DX_ICP_SHELL=1) return the same correspondence for every source point
+    (the exact (d^2, index) minimum within max_correspondence_distance), for
+    sources displaced within, across and far beyond the radius (0.3: queries
+    outside the target grid), and the moments equal the oracle's."""
+    src, tgt = _icp_case(60000, seed=9)
+    tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
+    T = S.rigid_transform(3.0, (1, 2, 0), (shift, shift / 3, -shift / 2))
+    target = ops.ICPTarget(torch.from_numpy(tgt).to(dev), torch.from_numpy(tn).to(dev), 0.02)
+    s4 = ops.spatial_sort(torch.from_numpy(src).to(dev))
+    a, ca = target.accumulate(s4, T, want_corr=True)
+    monkeypatch.setenv("O3DX_ICP_SHELL", "1")
+    b, cb = target.accumulate(s4, T, want_corr=True)
+    monkeypatch.delenv("O3DX_ICP_SHELL")
+    assert torch.equal(ca, cb)
+    assert a[28] == b[28]
+    np.testing.assert_array_equal(a[:30], b[:30])
+    ref = O.icp_accumulate(src, tgt, tn, 0.02, T)
+    assert a[28] == ref[28]
+    np.testing.assert_allclose(a[:30], ref[:30], rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("k", [5, 30, 64])
 @pytest.mark.parametrize("shape", ["cube", "surface", "dups"])
 def test_normals_knn_paths_agree(dev, k, shape):
