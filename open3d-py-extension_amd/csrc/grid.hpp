@@ -299,10 +299,48 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
     const int z0 = max(0, (int)floorf((fz - rb - g.oz) * g.inv_h)), z1 = min(g.nz - 1, (int)floorf((fz + rb - g.oz) * g.inv_h));
     if ((x1 - x0) <= 2 && (y1 - y0) <= 2 && (z1 - z0) <= 2 && x0 <= cx && cx <= x1 && y0 <= cy && cy <= y1 &&
         z0 <= cz && cz <= z1) {
-      for (int z = z0; z <= z1; ++z)
-        for (int y = y0; y <= y1; ++y)
-          for (int x = x0; x <= x1; ++x)
-            if (x != cx || y != cy || z != cz) visit_cell(x, y, z);
+      if (ROWS) {
+        // <= 9 rows, each the contiguous run of its cells that pass the box
+        // test (convex in x): one pair of cell-start loads per row, not per cell
+        for (int z = z0; z <= z1; ++z)
+          for (int y = y0; y <= y1; ++y) {
+            const float by0 = g.oy + (float)y * g.h, bz0 = g.oz + (float)z * g.h;
+            const float ey = fmaxf(fmaxf(by0 - fy, fy - (by0 + g.h)) - sl3, 0.0f);
+            const float ez = fmaxf(fmaxf(bz0 - fz, fz - (bz0 + g.h)) - sl3, 0.0f);
+            const float eyz = fmaf(ez, ez, ey * ey);
+            if (eyz >= thr) continue;
+            int xa = x1 + 1, xb = x0 - 1;
+            for (int x = x0; x <= x1; ++x) {
+              const float bx0 = g.ox + (float)x * g.h;
+              const float ex = fmaxf(fmaxf(bx0 - fx, fx - (bx0 + g.h)) - sl3, 0.0f);
+              if (fmaf(ex, ex, eyz) < thr) {
+                xa = min(xa, x);
+                xb = x;
+              }
+            }
+            const int rb = g.nx * (y + g.ny * z);
+            auto run = [&](int a, int b) {  // cells [a, b] of the row
+              if (a > b) return;
+              const int p0 = g.start[rb + a], p1 = g.start[rb + b + 1];
+              if (g.stats) {
+                ++st_cells;
+                st_cands += p1 - p0;
+              }
+              for_points4(g, p0, p1, visit_point);
+            };
+            if (y == cy && z == cz) {  // the own cell is done
+              run(xa, min(xb, cx - 1));
+              run(max(xa, cx + 1), xb);
+            } else {
+              run(xa, xb);
+            }
+          }
+      } else {
+        for (int z = z0; z <= z1; ++z)
+          for (int y = y0; y <= y1; ++y)
+            for (int x = x0; x <= x1; ++x)
+              if (x != cx || y != cy || z != cz) visit_cell(x, y, z);
+      }
       search_stats(g, st_cells, st_cands, 2);
       *best_d2 = bd;
       *best_pos = bp;
@@ -318,47 +356,60 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
     // (g_k - slack)^2 reaches thr no later row can hold a point below the
     // bound.  Per ring O(k) row tests instead of O(k^2) cell tests (the shell
     // walk below): the far-displaced queries of the first iterations.
+    // Without a match yet the chord would span the whole radius, so a first
+    // pass (CLIP) keeps each ring's chords inside its Chebyshev cube (x within
+    // k of cx) and ends with the ring that finds a match: it only sets the
+    // bound; the full pass after it alone decides (and is complete).
     const int kmax = max(max(cy, g.ny - 1 - cy), max(cz, g.nz - 1 - cz));
     const double inv_hd = 1.0 / (double)g.h;
     int rows = 0;
-    for (int k = 0; k <= kmax; ++k) {
-      if (k > 0) {
-        float gk = INFINITY;  // smallest y/z gap of ring k's rows to q (sides with rows only)
-        if (cy - k >= 0) gk = fminf(gk, fy - (g.oy + (float)(cy - k + 1) * g.h));
-        if (cy + k < g.ny) gk = fminf(gk, (g.oy + (float)(cy + k) * g.h) - fy);
-        if (cz - k >= 0) gk = fminf(gk, fz - (g.oz + (float)(cz - k + 1) * g.h));
-        if (cz + k < g.nz) gk = fminf(gk, (g.oz + (float)(cz + k) * g.h) - fz);
-        const float e = gk - sl3;
-        if (e > 0.0f && e * e >= thr) break;
-      }
-      for (int dz = -k; dz <= k; ++dz) {
-        const int z = cz + dz;
-        if (z < 0 || z >= g.nz) continue;
-        const bool zedge = dz == -k || dz == k;
-        const int step = (zedge || k == 0) ? 1 : 2 * k;
-        for (int dy = -k; dy <= k; dy += step) {
-          const int y = cy + dy;
-          if (y < 0 || y >= g.ny) continue;
-          const float by0 = g.oy + (float)y * g.h, bz0 = g.oz + (float)z * g.h;
-          const float ey = fmaxf(fmaxf(by0 - fy, fy - (by0 + g.h)) - sl3, 0.0f);
-          const float ez = fmaxf(fmaxf(bz0 - fz, fz - (bz0 + g.h)) - sl3, 0.0f);
-          const float eyz = fmaf(ez, ez, ey * ey);
-          if (eyz >= thr) continue;
-          const double rx = (double)sqrtf(thr - eyz) + (double)sl3;
-          const int xa = max(0, (int)floor(((double)fx - rx - (double)g.ox) * inv_hd));
-          const int xb = min(g.nx - 1, (int)floor(((double)fx + rx - (double)g.ox) * inv_hd));
-          if (xa > xb) continue;
-          const int rb = g.nx * (y + g.ny * z);
-          const int p0 = g.start[rb + xa], p1 = g.start[rb + xb + 1];
-          if (g.stats) {
-            ++rows;
-            st_cands += p1 - p0;
-          }
-          for_points4(g, p0, p1, visit_point);
+    auto ring_walk = [&](bool clip) {
+      for (int k = 0; k <= kmax; ++k) {
+        if (k > 0) {
+          float gk = INFINITY;  // smallest y/z gap of ring k's rows to q (sides with rows only)
+          if (cy - k >= 0) gk = fminf(gk, fy - (g.oy + (float)(cy - k + 1) * g.h));
+          if (cy + k < g.ny) gk = fminf(gk, (g.oy + (float)(cy + k) * g.h) - fy);
+          if (cz - k >= 0) gk = fminf(gk, fz - (g.oz + (float)(cz - k + 1) * g.h));
+          if (cz + k < g.nz) gk = fminf(gk, (g.oz + (float)(cz + k) * g.h) - fz);
+          const float e = gk - sl3;
+          if (e > 0.0f && e * e >= thr) break;
         }
+        for (int dz = -k; dz <= k; ++dz) {
+          const int z = cz + dz;
+          if (z < 0 || z >= g.nz) continue;
+          const bool zedge = dz == -k || dz == k;
+          const int step = (zedge || k == 0) ? 1 : 2 * k;
+          for (int dy = -k; dy <= k; dy += step) {
+            const int y = cy + dy;
+            if (y < 0 || y >= g.ny) continue;
+            const float by0 = g.oy + (float)y * g.h, bz0 = g.oz + (float)z * g.h;
+            const float ey = fmaxf(fmaxf(by0 - fy, fy - (by0 + g.h)) - sl3, 0.0f);
+            const float ez = fmaxf(fmaxf(bz0 - fz, fz - (bz0 + g.h)) - sl3, 0.0f);
+            const float eyz = fmaf(ez, ez, ey * ey);
+            if (eyz >= thr) continue;
+            const double rx = (double)sqrtf(thr - eyz) + (double)sl3;
+            int xa = max(0, (int)floor(((double)fx - rx - (double)g.ox) * inv_hd));
+            int xb = min(g.nx - 1, (int)floor(((double)fx + rx - (double)g.ox) * inv_hd));
+            if (clip && bi < 0) {
+              xa = max(xa, cx - k);
+              xb = min(xb, cx + k);
+            }
+            if (xa > xb) continue;
+            const int rb = g.nx * (y + g.ny * z);
+            const int p0 = g.start[rb + xa], p1 = g.start[rb + xb + 1];
+            if (g.stats) {
+              ++rows;
+              st_cands += p1 - p0;
+            }
+            for_points4(g, p0, p1, visit_point);
+          }
+        }
+        r = k;
+        if (clip && bi >= 0) break;
       }
-      r = k;
-    }
+    };
+    if (bi < 0) ring_walk(true);
+    ring_walk(false);
     search_stats(g, st_cells + rows, st_cands, r + 1);
     *best_d2 = bd;
     *best_pos = bp;

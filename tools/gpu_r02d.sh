@@ -14,3 +14,15 @@ for mode in rows shell; do
     2> gpurun_out/icp_$mode.err || exit $?
   python -c "import json,sys; d=json.load(open('gpurun_out/icp_$mode.json')); print('$mode', d['extra']['icp'])"
 done
+unset O3DX_ICP_SHELL
+# target-grid settings under the row walk
+: > gpurun_out/icp_sweep_rows.txt
+for kv in O3DX_ICP_OCC=1 O3DX_ICP_OCC=3 O3DX_ICP_MINH_DIV=8 O3DX_ICP_MINH_DIV=24; do
+  env "$kv" timeout -k 10 200 python bench.py --no-cpu --c4-n 0 --c5-n 0 --steps 2 --warmup 1 \
+    > gpurun_out/sweep_one.json 2> gpurun_out/sweep_one.err || exit $?
+  python -c "
+import json; d=json.load(open('gpurun_out/sweep_one.json'))['extra']['icp']
+print('$kv', d['iters_per_s'], d['match_kernel_ms'], d['accumulate_kernel_ms'], d['fitness'], d['T_err_vs_gt_inverse'])" \
+    >> gpurun_out/icp_sweep_rows.txt
+done
+cat gpurun_out/icp_sweep_rows.txt
