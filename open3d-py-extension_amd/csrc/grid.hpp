@@ -299,48 +299,10 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
     const int z0 = max(0, (int)floorf((fz - rb - g.oz) * g.inv_h)), z1 = min(g.nz - 1, (int)floorf((fz + rb - g.oz) * g.inv_h));
     if ((x1 - x0) <= 2 && (y1 - y0) <= 2 && (z1 - z0) <= 2 && x0 <= cx && cx <= x1 && y0 <= cy && cy <= y1 &&
         z0 <= cz && cz <= z1) {
-      if (ROWS) {
-        // <= 9 rows, each the contiguous run of its cells that pass the box
-        // test (convex in x): one pair of cell-start loads per row, not per cell
-        for (int z = z0; z <= z1; ++z)
-          for (int y = y0; y <= y1; ++y) {
-            const float by0 = g.oy + (float)y * g.h, bz0 = g.oz + (float)z * g.h;
-            const float ey = fmaxf(fmaxf(by0 - fy, fy - (by0 + g.h)) - sl3, 0.0f);
-            const float ez = fmaxf(fmaxf(bz0 - fz, fz - (bz0 + g.h)) - sl3, 0.0f);
-            const float eyz = fmaf(ez, ez, ey * ey);
-            if (eyz >= thr) continue;
-            int xa = x1 + 1, xb = x0 - 1;
-            for (int x = x0; x <= x1; ++x) {
-              const float bx0 = g.ox + (float)x * g.h;
-              const float ex = fmaxf(fmaxf(bx0 - fx, fx - (bx0 + g.h)) - sl3, 0.0f);
-              if (fmaf(ex, ex, eyz) < thr) {
-                xa = min(xa, x);
-                xb = x;
-              }
-            }
-            const int rb = g.nx * (y + g.ny * z);
-            auto run = [&](int a, int b) {  // cells [a, b] of the row
-              if (a > b) return;
-              const int p0 = g.start[rb + a], p1 = g.start[rb + b + 1];
-              if (g.stats) {
-                ++st_cells;
-                st_cands += p1 - p0;
-              }
-              for_points4(g, p0, p1, visit_point);
-            };
-            if (y == cy && z == cz) {  // the own cell is done
-              run(xa, min(xb, cx - 1));
-              run(max(xa, cx + 1), xb);
-            } else {
-              run(xa, xb);
-            }
-          }
-      } else {
-        for (int z = z0; z <= z1; ++z)
-          for (int y = y0; y <= y1; ++y)
-            for (int x = x0; x <= x1; ++x)
-              if (x != cx || y != cy || z != cz) visit_cell(x, y, z);
-      }
+      for (int z = z0; z <= z1; ++z)
+        for (int y = y0; y <= y1; ++y)
+          for (int x = x0; x <= x1; ++x)
+            if (x != cx || y != cy || z != cz) visit_cell(x, y, z);
       search_stats(g, st_cells, st_cands, 2);
       *best_d2 = bd;
       *best_pos = bp;

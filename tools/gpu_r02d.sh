@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "${1:-icp}" \
   > gpurun_out/r02d_tests.log 2>&1 || { tail -30 gpurun_out/r02d_tests.log; exit 1; }
 tail -2 gpurun_out/r02d_tests.log
-for mode in rows shell; do
+for mode in ${ICP_MODES:-rows shell}; do
   if [ $mode = shell ]; then export O3DX_ICP_SHELL=1; fi
   timeout -k 10 200 python bench.py --no-cpu --c4-n 0 --c5-n 0 --steps 5 > gpurun_out/icp_$mode.json \
     2> gpurun_out/icp_$mode.err || exit $?
@@ -17,7 +17,7 @@ done
 unset O3DX_ICP_SHELL
 # target-grid settings under the row walk
 : > gpurun_out/icp_sweep_rows.txt
-for kv in O3DX_ICP_OCC=1 O3DX_ICP_OCC=3 O3DX_ICP_MINH_DIV=8 O3DX_ICP_MINH_DIV=24; do
+for kv in ${ICP_SWEEP:-O3DX_ICP_MINH_DIV=20 O3DX_ICP_MINH_DIV=24 O3DX_ICP_MINH_DIV=32}; do
   env "$kv" timeout -k 10 200 python bench.py --no-cpu --c4-n 0 --c5-n 0 --steps 2 --warmup 1 \
     > gpurun_out/sweep_one.json 2> gpurun_out/sweep_one.err || exit $?
   python -c "
