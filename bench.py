@@ -52,8 +52,9 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=25,
+                    help="untimed steps first (the clocks settle over ~20 steps: profiles/r02_call_structure.txt)")
     ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU (C2: 10M)")
     ap.add_argument("--knn", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
