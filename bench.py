@@ -423,6 +423,12 @@ def kernel_table():
     return kernels
 
 
+# VALU instruction mix of the dominant kernels (fractions of their VALU
+# instructions; static count over the disassembly of the launched variant,
+# tools/valu_mix.py -> profiles/r02_valu_mix.json)
+VALU_MIX = {"normals_stile": {"pk": 1476 / 9328, "f64": 1337 / 9328, "trans": 67 / 9328}}
+
+
 def roofline(kernels, M, N, pmc_json):
     # algorithmic bytes per launch:
     #   normals_stile / normals_tile: M queries x (12 B xyz read + 12 B normal written)
@@ -444,6 +450,15 @@ def roofline(kernels, M, N, pmc_json):
         floor_ms = pmc["SQ_INSTS_VALU"] * 2.0 / (1024 * 2.4e9) * 1e3
         roof["valu_issue_floor_ms"] = round(floor_ms, 4)
         roof["valu_issue_frac"] = round(floor_ms / kernels[dom]["avg_ms"], 4)
+        mix = VALU_MIX.get(dom)
+        if mix:
+            # weighted by the kernel's instruction mix (static count from its disassembly,
+            # profiles/r02_valu_mix.json): packed f32 and f64 at 4 cycles, transcendental 8,
+            # the rest 2 (the FP32 vector peak is the non-packed v_fma_f32 rate)
+            cyc = 2.0 * (1 - mix["pk"] - mix["f64"] - mix["trans"]) + 4.0 * (mix["pk"] + mix["f64"]) + 8.0 * mix["trans"]
+            wf = pmc["SQ_INSTS_VALU"] * cyc / (1024 * 2.4e9) * 1e3
+            roof["valu_issue_floor_weighted_ms"] = round(wf, 4)
+            roof["valu_issue_weighted_frac"] = round(wf / kernels[dom]["avg_ms"], 4)
     if pmc.get("SQ_LDS_IDX_ACTIVE") and pmc.get("GRBM_GUI_ACTIVE"):
         # LDS busy share: SQ_LDS_IDX_ACTIVE (LDS-array cycles, summed over CUs) / (256 CUs x kernel cycles)
         cyc = pmc["GRBM_GUI_ACTIVE"] / 8.0  # GRBM_GUI_ACTIVE sums the 8 XCDs
