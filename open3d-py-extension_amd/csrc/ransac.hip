@@ -857,17 +857,44 @@ static int select_best(const int64_t* counts, const double* sums, const double* 
   return best;
 }
 
-// hypotheses whose count equals another non-degenerate hypothesis' count
-static std::vector<int32_t> tied_hypotheses(const std::vector<int64_t>& counts) {
-  std::vector<std::pair<int64_t, int32_t>> v;
-  for (int h = 0; h < (int)counts.size(); ++h)
-    if (counts[h] > 0) v.emplace_back(counts[h], h);
-  std::sort(v.begin(), v.end());
-  std::vector<int32_t> out;
-  for (size_t i = 0; i < v.size(); ++i) {
-    bool t = (i > 0 && v[i].first == v[i - 1].first) || (i + 1 < v.size() && v[i].first == v[i + 1].first);
-    if (t) out.push_back(v[i].second);
+// The hypotheses whose rmse select_best can consult.  Its running best count
+// (and with it the early-break point) follows from the counts alone — rmse
+// only decides WHICH of equal-count hypotheses is the best — so a replay on
+// the counts finds every comparison "fit == best_fit && rmse < best_rmse": the
+// hypotheses processed while their count equals the running maximum, for
+// every maximum reached by at least two of them.  Usually the best count is
+// unique and no Sigma |d| pass is needed at all.
+static std::vector<int32_t> tied_hypotheses(const std::vector<int64_t>& counts, const double* planes, int64_t n,
+                                            int ransac_n, double probability) {
+  const int H = (int)counts.size();
+  std::vector<int32_t> out, run;  // run: the hypotheses at the current running maximum
+  int64_t best = 0;
+  size_t break_iteration = std::numeric_limits<size_t>::max();
+  int iteration_count = 0;
+  auto flush = [&]() {
+    if (run.size() >= 2) out.insert(out.end(), run.begin(), run.end());
+    run.clear();
+  };
+  for (int it = 0; it < H; ++it) {
+    if ((size_t)iteration_count > break_iteration) continue;
+    if (counts[it] < 0 || (planes && plane_is_zero(planes + 4 * it))) continue;
+    if (counts[it] > 0 && counts[it] >= best) {
+      if (counts[it] > best) {
+        flush();
+        best = counts[it];
+        const double fit = (double)best / (double)n;
+        if (fit < 1.0) {
+          double bi = std::min(std::log(1 - probability) / std::log(1 - std::pow(fit, ransac_n)), (double)H);
+          break_iteration = (size_t)bi;
+        } else {
+          break_iteration = 0;
+        }
+      }
+      run.push_back(it);
+    }
+    iteration_count++;
   }
+  flush();
   std::sort(out.begin(), out.end());
   return out;
 }
@@ -1122,7 +1149,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
   if (H > 0) {
     std::vector<int64_t> counts;
     O3DX_TRY(run_count(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts));
-    std::vector<int32_t> tied = tied_hypotheses(counts);
+    std::vector<int32_t> tied = tied_hypotheses(counts, planes.data(), n, ransac_n, probability);
     std::vector<double> sums(H, std::numeric_limits<double>::quiet_NaN());
     if (!tied.empty()) {
       std::vector<double> ts(tied.size());

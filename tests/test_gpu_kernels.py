@@ -233,6 +233,20 @@ def test_segment_plane_ties_small(dev):
     np.testing.assert_allclose(plane, rplane, atol=1e-9)
 
 
+@pytest.mark.parametrize("n,thr,seed,prob", [(40, 0.05, 2, 0.99999999), (60, 0.2, 3, 1.0), (200, 0.05, 4, 0.99999999),
+                                             (200, 0.3, 5, 1.0), (1000, 0.02, 6, 0.99)])
+def test_segment_plane_tie_replay(dev, n, thr, seed, prob):
+    """Small clouds where many hypotheses share counts: only the ties the
+    sequential selection can consult get their Sigma |d| (replay on the
+    counts); the chosen plane and inliers still equal the oracle's."""
+    pts = S.planted_plane(n, seed).numpy()
+    samples = O.ransac_samples(n, 3, 300, seed)
+    plane, inl = ops.segment_plane(torch.from_numpy(pts).to(dev), thr, 3, 300, prob, samples=samples)
+    rplane, rinl, _, _, _ = O.segment_plane(pts, thr, 3, 300, samples, probability=prob)
+    assert np.array_equal(inl.cpu().numpy().astype(np.int64), rinl)
+    np.testing.assert_allclose(plane, rplane, atol=1e-9)
+
+
 def test_segment_plane_errors(dev):
     x = torch.rand(2, 3, device=dev)
     with pytest.raises(RuntimeError, match="ransac_n"):
