@@ -347,9 +347,37 @@ int reduce_columns_f64(const double* part, int64_t rows, int width, double* out,
   return 0;
 }
 
+// Integer columns: the rows are split over blockIdx.y as well (a few columns
+// x thousands of rows would leave one block per 64 columns streaming every
+// row), each block adding its partial column sums with a 64-bit integer
+// atomic — integer addition, so the result is the same in any order.
+constexpr int64_t kRedRowsPerBlock = 128;
+
+__global__ void __launch_bounds__(1024) k_reduce_columns_i64(const int32_t* __restrict__ part, int64_t rows,
+                                                             int width, int64_t* __restrict__ out) {
+  __shared__ int64_t sh[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * kRedRowsPerBlock, r1 = min(rows, r0 + kRedRowsPerBlock);
+  int64_t acc = 0;
+  if (c < width)
+    for (int64_t r = r0 + g; r < r1; r += 16) acc += part[r * width + c];
+  sh[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g == 0 && c < width) {
+    int64_t t = 0;
+    for (int k = 0; k < 16; ++k) t += sh[k][threadIdx.x & 63];
+    if (t) atomicAdd(reinterpret_cast<unsigned long long*>(&out[c]), (unsigned long long)t);
+  }
+}
+
 int reduce_columns_i32_to_i64(const int32_t* part, int64_t rows, int width, int64_t* out, hipStream_t s) {
-  hipLaunchKernelGGL((k_reduce_columns<int32_t, int64_t>), dim3((width + 63) / 64), dim3(1024), 0, s, part, rows,
-                     width, out);
+  if (width <= 0) return 0;
+  O3DX_HIP(hipMemsetAsync(out, 0, (size_t)width * sizeof(int64_t), s));
+  const int64_t by = std::max<int64_t>(1, (rows + kRedRowsPerBlock - 1) / kRedRowsPerBlock);
+  if (by > 65535) return fail(O3DX_EINVAL, "reduce_columns: too many rows");
+  hipLaunchKernelGGL(k_reduce_columns_i64, dim3((width + 63) / 64, (unsigned)by), dim3(1024), 0, s, part, rows, width,
+                     out);
   O3DX_HIP(hipGetLastError());
   return 0;
 }
