@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-2 closing evidence: full -m gpu suite, smoke(), bench line + rocprofv3 stats
+# Round-2 closing evidence: smoke(), bench line + rocprofv3 stats, then the full -m gpu suite
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/gpu_tests.sh || exit $?
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-bash tools/gpu_r02_bench.sh
+bash tools/gpu_r02_bench.sh || exit $?
+bash tools/gpu_tests.sh
