@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define O3DX_ABI_VERSION 2
+#define O3DX_ABI_VERSION 3
 
 #define O3DX_OK 0
 #define O3DX_EIO (-5)
@@ -339,6 +339,14 @@ int o3dx_plane_select(const float* xyz_dev, int64_t n, const double* plane_host,
                       double* dist_out_dev, int32_t* idx_out_dev,
                       int64_t* count_host, void* ws, size_t ws_bytes,
                       void* stream);
+/* The same on float64 coordinates (ABI 3): a cloud built from float64 host
+ * data keeps the caller's exact values, and the reference evaluates the
+ * distance on them (PointCloud.py:400-404 on get_points(), float64). */
+int o3dx_plane_select_f64(const double* xyz_dev, int64_t n, const double* plane_host,
+                          int band, double lo, double hi, int invert,
+                          double* dist_out_dev, int32_t* idx_out_dev,
+                          int64_t* count_host, void* ws, size_t ws_bytes,
+                          void* stream);
 int o3dx_plane_moments(const float* xyz_dev, const int32_t* idx_dev,
                        int64_t count, const double* centroid_host,
                        double* sums_host, void* ws, size_t ws_bytes,

@@ -484,16 +484,14 @@ __global__ void __launch_bounds__(kBlock) k_plane_flags(const float* __restrict_
 // 278-290, 400-404): s = ((x*a + y*b) + z*c + d) / nrm, unfused, the order of
 // numpy's `(p*abc).sum(1) + d` (distance2plane); flag = |s| < thr (BAND 0) or
 // lo < s < hi (BAND 1), xor invert.  dist (optional) receives s.
-template <bool BAND>
-__global__ void __launch_bounds__(kBlock) k_plane_band(const float* __restrict__ xyz, int64_t n, double a, double b,
+template <bool BAND, class T>
+__global__ void __launch_bounds__(kBlock) k_plane_band(const T* __restrict__ xyz, int64_t n, double a, double b,
                                                        double c, double d, double nrm, double lo, double hi,
                                                        int invert, uint8_t* __restrict__ flags,
                                                        double* __restrict__ dist) {
-  const P3* p = reinterpret_cast<const P3*>(xyz);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const P3 q = p[i];
-    const double t = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn((double)q.x, a), __dmul_rn((double)q.y, b)),
-                                         __dmul_rn((double)q.z, c)), d);
+    const double x = (double)xyz[3 * i], y = (double)xyz[3 * i + 1], z = (double)xyz[3 * i + 2];
+    const double t = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(x, a), __dmul_rn(y, b)), __dmul_rn(z, c)), d);
     const double s = __ddiv_rn(t, nrm);
     if (dist) dist[i] = s;
     if (flags) {
@@ -1053,9 +1051,10 @@ extern "C" size_t o3dx_plane_select_workspace_bytes(int64_t n) {
   return Arena::align(n + 17) + Arena::align(compact_workspace_ints(n) * 4 + 1) + 512;
 }
 
-extern "C" int o3dx_plane_select(const float* xyz, int64_t n, const double* plane, int band, double lo, double hi,
-                                 int invert, double* dist_out, int32_t* idx_out, int64_t* count_host, void* ws,
-                                 size_t ws_bytes, void* stream) {
+template <class T>
+static int plane_select_impl(const T* xyz, int64_t n, const double* plane, int band, double lo, double hi, int invert,
+                             double* dist_out, int32_t* idx_out, int64_t* count_host, void* ws, size_t ws_bytes,
+                             void* stream) {
   if (n < 0 || !plane || (n > 0 && !xyz) || (idx_out && !count_host) || (!idx_out && !dist_out))
     return fail(O3DX_EINVAL, "o3dx_plane_select: bad args");
   if (idx_out && (!ws || ws_bytes < o3dx_plane_select_workspace_bytes(n)))
@@ -1079,17 +1078,29 @@ extern "C" int o3dx_plane_select(const float* xyz, int64_t n, const double* plan
   }
   const unsigned g = grid_for(n, kBlock, 8192);
   if (band)
-    hipLaunchKernelGGL(k_plane_band<true>, dim3(g), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1], plane[2], plane[3],
-                       nrm, lo, hi, invert, flags, dist_out);
+    hipLaunchKernelGGL((k_plane_band<true, T>), dim3(g), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1], plane[2],
+                       plane[3], nrm, lo, hi, invert, flags, dist_out);
   else
-    hipLaunchKernelGGL(k_plane_band<false>, dim3(g), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1], plane[2], plane[3],
-                       nrm, lo, hi, invert, flags, dist_out);
+    hipLaunchKernelGGL((k_plane_band<false, T>), dim3(g), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1], plane[2],
+                       plane[3], nrm, lo, hi, invert, flags, dist_out);
   O3DX_HIP(hipGetLastError());
   if (idx_out) {
     O3DX_TRY(compact_flags(flags, n, idx_out, nullptr, cnt, tmp, s));
     O3DX_TRY(read_back(count_host, cnt, sizeof(int64_t), s));
   }
   return 0;
+}
+
+extern "C" int o3dx_plane_select(const float* xyz, int64_t n, const double* plane, int band, double lo, double hi,
+                                 int invert, double* dist_out, int32_t* idx_out, int64_t* count_host, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  return plane_select_impl(xyz, n, plane, band, lo, hi, invert, dist_out, idx_out, count_host, ws, ws_bytes, stream);
+}
+
+extern "C" int o3dx_plane_select_f64(const double* xyz, int64_t n, const double* plane, int band, double lo,
+                                     double hi, int invert, double* dist_out, int32_t* idx_out, int64_t* count_host,
+                                     void* ws, size_t ws_bytes, void* stream) {
+  return plane_select_impl(xyz, n, plane, band, lo, hi, invert, dist_out, idx_out, count_host, ws, ws_bytes, stream);
 }
 
 extern "C" int o3dx_plane_moments(const float* xyz, const int32_t* idx, int64_t count, const double* centroid,

@@ -427,16 +427,23 @@ __global__ void __launch_bounds__(kBinBlock) k_hbin_scatter(const float* __restr
   for (int r0 = 0; r0 < kBinChunk && base + r0 < n; r0 += kBinRound) {
     for (int k = threadIdx.x; k < kHBins; k += kBinBlock) loc[k] = 0;
     __syncthreads();
-    // entry per point: bin << 52 | rest << 32 | index (~0: none)
+    // staged entry per point: rest << 24 | bin << 12 | position in the round
+    // (~0: none).  The rest takes up to 31 bits, the bin 12 and the round
+    // position 12 (kBinRound = 4096), so no field overlaps another for any
+    // k <= kHMaxBits; the point index is re-formed from the position on the
+    // way out.
+    static_assert(kBinRound == 4096 && kHBinBits == 12, "staged entry layout");
     uint64_t en[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      const int64_t i = base + r0 + threadIdx.x + (int64_t)j * kBinBlock;
+      const int pos = threadIdx.x + j * kBinBlock;
+      const int64_t i = base + r0 + pos;
       uint64_t h;
       en[j] = ~0ull;
       if (i < n && voxel_hid(p[i], g, m, &h)) {
-        en[j] = ((uint64_t)hbin_of(h, m) << 52) | ((h & ((1ull << rbits) - 1)) << 32) | (uint32_t)i;
-        atomicAdd(&loc[(int)(en[j] >> 52)], 1);
+        const int bin = hbin_of(h, m);
+        en[j] = ((h & ((1ull << rbits) - 1)) << 24) | ((uint64_t)bin << 12) | (uint64_t)pos;
+        atomicAdd(&loc[bin], 1);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -456,12 +463,15 @@ __global__ void __launch_bounds__(kBinBlock) k_hbin_scatter(const float* __restr
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       if (en[j] == ~0ull) continue;
-      stage[atomicAdd(&loc[(int)(en[j] >> 52)], 1)] = en[j];
+      stage[atomicAdd(&loc[(int)((en[j] >> 12) & 0xfff)], 1)] = en[j];
     }
     __syncthreads();
+    // global entry: rest << 32 | point index (the rest < 2^31, so a key never
+    // equals the reduce's empty marker 0xFFFFFFFF)
     for (int t = threadIdx.x; t < tot; t += kBinBlock) {
       const uint64_t e = stage[t];
-      entries[cur[(int)(e >> 52)] + t] = e & 0x000fffffffffffffull;
+      const uint32_t i = (uint32_t)(base + r0 + (int64_t)(e & 0xfff));
+      entries[cur[(int)((e >> 12) & 0xfff)] + t] = ((e >> 24) << 32) | i;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < kHBins; k += kBinBlock) cur[k] += loc[k];

@@ -139,6 +139,7 @@ class PointCloudBase:
         self.column_index = []
         self._pts = None        # (N,3) float32 tensor on the device
         self._pts_host = None   # (N,3) float64 exact host copy (when supplied from host)
+        self._pts64 = None      # device float64 copy of _pts_host (plane selections), made on demand
         self._normals = None    # (N,3) float32 tensor
         self._colors = None     # (N,3) float32 tensor in [0,1]
         self.pcd_tree = None
@@ -181,6 +182,7 @@ class PointCloudBase:
     def _copy_from(self, other: "PointCloudBase"):
         self._pts = other._pts
         self._pts_host = other._pts_host
+        self._pts64 = other._pts64
         self._normals = other._normals
         self._colors = other._colors
         self.intensity = other.intensity
@@ -195,6 +197,17 @@ class PointCloudBase:
         if self._pts.device.type != "cuda" and torch.cuda.is_available():
             self._pts = self._pts.to(_device())
         return self._pts
+
+    def _plane_points(self) -> torch.Tensor:
+        """The coordinates the plane selections evaluate: the caller's exact
+        float64 values when the cloud came from float64 host data (the
+        reference computes distance2plane on get_points(), float64:
+        PointCloud.py:400-404), else the float32 device points."""
+        if self._pts_host is None:
+            return self._dev_points()
+        if self._pts64 is None or self._pts64.device.type != "cuda":
+            self._pts64 = torch.as_tensor(self._pts_host, dtype=torch.float64, device=N.default_device())
+        return self._pts64
 
     @staticmethod
     def _to_dev(a, dtype=torch.float32) -> torch.Tensor:
@@ -229,7 +242,7 @@ class PointCloudBase:
         T = np.asarray(T, np.float64).reshape(4, 4)
         if self.has_points():
             if self._pts_host is not None:
-                h = self._pts_host @ T[:3, :3].T + T[:3, 3]
+                h = self._pts_host @ T[:3, :3].T + T[:3, 3]  # set_points drops _pts64
                 w = self._pts_host @ T[3, :3] + T[3, 3]
                 self.set_points(h / w[:, None])
             else:
@@ -336,10 +349,12 @@ class PointCloudBase:
             _check3(points, "points")
             self._pts = self._to_dev(points)
             self._pts_host = None
+            self._pts64 = None
         else:
             p = np.asarray(points)
             _check3(p, "points")
             self._pts_host = np.ascontiguousarray(p, dtype=np.float64)
+            self._pts64 = None
             self._pts = self._to_dev(self._pts_host.astype(np.float32))
         self.pcd_tree = None
         return self
@@ -555,7 +570,7 @@ class PointCloudSelections(PointCloudBase):
     def _plane_index_dev(self, model, thickness, invert: bool = False) -> torch.Tensor:
         if not self.has_points():
             return torch.zeros(0, dtype=torch.int32, device=_device())
-        return ops.plane_select(self._dev_points(), np.asarray(model, np.float64).reshape(4), thickness, invert)
+        return ops.plane_select(self._plane_points(), np.asarray(model, np.float64).reshape(4), thickness, invert)
 
     def select_by_plane(self, model, thickness=0.03, invert: bool = False):
         # indices stay on the device (reference PointCloud.py:289-290)
@@ -721,10 +736,11 @@ class PointCloudUtility(PointCloudSelections):
 
     def distance2plane(self, plane) -> np.ndarray:
         """Signed float64 distance to the plane (reference PointCloud.py:400-404),
-        computed on the GPU in numpy's order ((x*a + y*b) + z*c + d) / |abc|."""
+        computed on the GPU in numpy's order ((x*a + y*b) + z*c + d) / |abc|, on
+        the caller's float64 coordinates when the cloud holds them."""
         if not self.has_points():
             return np.zeros(0)
-        return ops.plane_distance(self._dev_points(), np.asarray(plane, np.float64).reshape(4)).cpu().numpy()
+        return ops.plane_distance(self._plane_points(), np.asarray(plane, np.float64).reshape(4)).cpu().numpy()
 
     def remove_plane_outlier(self, plane_model, thickness: float = 0.03, similarity: float = 0.999,
                              invert: bool = False):

@@ -72,6 +72,7 @@ _SIGS = {
     "o3dx_plane_inliers": (_I32, [_P, _I64, _P, _D, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_select_workspace_bytes": (_SZ, [_I64]),
     "o3dx_plane_select": (_I32, [_P, _I64, _P, _I32, _D, _D, _I32, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_plane_select_f64": (_I32, [_P, _I64, _P, _I32, _D, _D, _I32, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_moments": (_I32, [_P, _P, _I64, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_from_moments": (_I32, [_P, _I64, _P, _P]),
     "o3dx_icp_target_workspace_bytes": (_SZ, [_I64]),

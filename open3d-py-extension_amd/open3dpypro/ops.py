@@ -329,12 +329,24 @@ def plane_inliers(xyz: torch.Tensor, plane, distance_threshold: float) -> torch.
     return idx[: int(k[0])]
 
 
+def _plane_pts(xyz: torch.Tensor):
+    """(tensor, entry point) for the plane selection: float64 coordinates go to
+    o3dx_plane_select_f64 unrounded, anything else as float32."""
+    if isinstance(xyz, torch.Tensor) and xyz.dtype == torch.float64:
+        N.require_device(xyz, "points")
+        if xyz.ndim != 2 or xyz.shape[1] != 3:
+            raise RuntimeError(f"points must have shape (n, 3), got {tuple(xyz.shape)}")
+        return xyz.contiguous(), N.load().o3dx_plane_select_f64
+    return _xyz(xyz), N.load().o3dx_plane_select
+
+
 def plane_select(xyz: torch.Tensor, plane, thickness, invert: bool = False) -> torch.Tensor:
     """Ascending int32 device indices of the points within `thickness` of the
     plane (|s| < thickness, or thickness[0] < s < thickness[1] for a tuple),
     complemented with `invert`; s = distance2plane (reference PointCloud.py:
-    278-290, 400-404).  o3dx_plane_select."""
-    x = _xyz(xyz)
+    278-290, 400-404).  o3dx_plane_select (float32 points) or
+    o3dx_plane_select_f64 (float64 points)."""
+    x, fn = _plane_pts(xyz)
     L = N.load()
     n = x.shape[0]
     pl = _c(plane, np.float64).reshape(4)
@@ -343,21 +355,20 @@ def plane_select(xyz: torch.Tensor, plane, thickness, invert: bool = False) -> t
     idx = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
     k = np.zeros(1, np.int64)
     ws = N.workspace(int(L.o3dx_plane_select_workspace_bytes(n)), x.device)
-    N.check(L.o3dx_plane_select(N.ptr(x), n, _np_ptr(pl), int(band), lo, hi, int(bool(invert)), None, N.ptr(idx),
-                                _np_ptr(k), N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "plane_select")
+    N.check(fn(N.ptr(x), n, _np_ptr(pl), int(band), lo, hi, int(bool(invert)), None, N.ptr(idx), _np_ptr(k),
+               N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "plane_select")
     return idx[: int(k[0])]
 
 
 def plane_distance(xyz: torch.Tensor, plane) -> torch.Tensor:
     """float64 signed distance of every point to the plane, in the order of the
-    reference's distance2plane (PointCloud.py:400-404).  o3dx_plane_select."""
-    x = _xyz(xyz)
-    L = N.load()
+    reference's distance2plane (PointCloud.py:400-404).  o3dx_plane_select(_f64)."""
+    x, fn = _plane_pts(xyz)
     n = x.shape[0]
     pl = _c(plane, np.float64).reshape(4)
     out = torch.empty(n, dtype=torch.float64, device=x.device)
-    N.check(L.o3dx_plane_select(N.ptr(x), n, _np_ptr(pl), 0, 0.0, 0.0, 0, N.ptr(out), None, None, None, 0,
-                                N.stream_ptr(x.device)), "plane_distance")
+    N.check(fn(N.ptr(x), n, _np_ptr(pl), 0, 0.0, 0.0, 0, N.ptr(out), None, None, None, 0,
+               N.stream_ptr(x.device)), "plane_distance")
     return out
 
 

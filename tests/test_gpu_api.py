@@ -124,6 +124,31 @@ def test_plane_selection_bit_exact(n):
         assert np.array_equal(sel.get_points(), pts[np.abs(s) < 0.05].astype(np.float64))
 
 
+@pytest.mark.parametrize("n", [1000, 1_000_003])
+def test_plane_selection_float64_input(n):
+    """A cloud built from genuinely float64 data (no float32 round trip): the
+    reference evaluates distance2plane on get_points(), i.e. the caller's
+    float64 values (PointCloud.py:400-404), so distances, band selections and
+    remove_plane_outlier-style rounds are bit-equal to numpy on those values
+    (the float32 device copy drifted by the coordinates' rounding)."""
+    rng = np.random.default_rng(100 + n)
+    pts = rng.random((n, 3)) * 4 - 2
+    pc = o3p.PointCloud(pts)
+    for plane in ([0.3, -1.2, 2.0, 0.1], [0.0, 0.0, 1.0, -0.25]):
+        a, b, c, d = plane
+        s = ((pts * np.asarray([a, b, c])).sum(1) + d) / (a ** 2 + b ** 2 + c ** 2) ** 0.5
+        assert np.array_equal(pc.distance2plane(plane), s)
+        for thk in (0.05, (-0.2, 0.7)):
+            exp = (np.logical_and(s > thk[0], s < thk[1]) if isinstance(thk, tuple) else np.abs(s) < thk)
+            assert np.array_equal(pc.get_index_by_plane(plane, thk), np.nonzero(exp)[0])
+        sel = pc.select_by_plane(plane, 0.05, invert=True)
+        assert np.array_equal(sel.get_points(), pts[~(np.abs(s) < 0.05)])
+        # a selection of the cloud keeps evaluating the float64 values
+        sub = pc.select_by_plane(plane, 0.5)
+        s2 = s[np.abs(s) < 0.5]
+        assert np.array_equal(sub.distance2plane(plane), s2)
+
+
 def test_seg_planes_rounds_vs_oracle():
     """seg_planes (reference PointCloud.py:941-985, loop fixed as documented in
     INTEGRATION.md): every round's plane, inlier cloud and AABB equal the

@@ -74,11 +74,14 @@ def test_voxel_hash_path_and_bounds(dev):
 
 
 @pytest.mark.parametrize("path", ["hbin", "hbin_overflow", "global_hash"])
-@pytest.mark.parametrize("case", ["clusters", "surface"])
+@pytest.mark.parametrize("case", ["clusters", "surface", "surface_2e10"])
 def test_voxel_sparse_paths(dev, monkeypatch, path, case):
     """Sparse grids (box >> 2n voxels): the hash-binned reduction (LDS table
     per bin), its fall-back when a bin's table overflows, and the global hash
-    table all give the oracle's representatives and trace."""
+    table all give the oracle's representatives and trace.  surface_2e10: a
+    1.3 m cube at 0.5 mm = 2601^3 = 1.76e10 voxels (a 35-bit voxel id, so the
+    per-bin rest takes 23 bits: more than the 20 the round-2 entry layout had
+    room for)."""
     monkeypatch.setenv("O3DX_VOXEL_HBIN_MIN", "-1" if path == "global_hash" else "0")
     if path == "hbin_overflow":
         monkeypatch.setenv("O3DX_VOXEL_HBIN_SLOTS", "4")
@@ -87,8 +90,11 @@ def test_voxel_sparse_paths(dev, monkeypatch, path, case):
         c = rng.uniform(-1000, 1000, (50, 3))
         pts = (c[rng.integers(0, 50, 60000)] + rng.normal(0, 0.05, (60000, 3))).astype(np.float32)
         vs = 0.01
-    else:
+    elif case == "surface":
         pts = S.box_surface(300_000, 17).numpy()
+        vs = 0.0005
+    else:
+        pts = S.box_surface(300_000, 19, dims=(1.3, 1.3, 1.3)).numpy()
         vs = 0.0005
     out = ops.voxel_down_sample(torch.from_numpy(pts).to(dev), vs, trace=True)
     ref, vop, cub = O.voxel_down_sample(pts, vs, trace=True)
