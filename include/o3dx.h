@@ -65,6 +65,9 @@ extern "C" {
 /* ---------------------------------------------------------------- misc */
 int o3dx_abi_version(void);
 const char* o3dx_last_error(void);
+/* fx sums (see o3dx_plane_moments) -> float64: k rows {lo, hi, q, 0} ->
+ * out[k] = (hi * 2^32 + lo) * 2^q, correctly rounded.  Host only. */
+int o3dx_fx_to_double(const int64_t* fx_host, int64_t k, double* out_host);
 
 /* Kernel timing (measurement support, off by default): when enabled, the
  * library brackets its main kernel launches with hipEvents on the launch
@@ -116,6 +119,10 @@ int o3dx_libm_probe(const double* x_dev, int64_t n, int fn, double* out_dev, voi
 size_t o3dx_aabb_workspace_bytes(int64_t n);
 int o3dx_aabb(const float* xyz_dev, int64_t n, double* minmax_host,
               void* ws, size_t ws_bytes, void* stream);
+/* The same into a device double[6], asynchronous (no host wait): the
+ * multi-GPU path all-reduces the bounds on the device before one read. */
+int o3dx_aabb_device(const float* xyz_dev, int64_t n, double* minmax_dev,
+                     void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- voxel
  * Replaces o3d PointCloud.voxel_down_sample_and_trace(voxel_size, min_bound,
@@ -305,9 +312,23 @@ int o3dx_segment_plane(const float* xyz_dev, int64_t n,
  *   winning hypothesis index (or -1). needs sums for count ties (NaN else).
  * o3dx_plane_inliers: ascending indices with |n.p+d| < thr (float64).
  * o3dx_plane_moments: sums over idx of {x,y,z} (pass 1, centroid NULL) or of
- *   centred {xx,xy,xz,yy,yz,zz} (pass 2), float64, for GetPlaneFromPoints.
+ *   centred {xx,xy,xz,yy,yz,zz} (pass 2), for GetPlaneFromPoints.
+ *   absmax_host (nullable: the selected points' own): |x|,|y|,|z| bounds of
+ *   the cloud, which fix the sums' fx quantum (below) — a sharded cloud
+ *   passes the global bounds on every rank.
+ * Sums of float terms here and in o3dx_icp_accumulate are "fx" sums: every
+ *   term is rounded to an integer multiple of 2^q (q from a bound of the
+ *   terms every rank derives alike) and the integers are added, so the sum
+ *   does not depend on how the points are split over blocks or GPUs.
+ *   fx_out_host (nullable) receives one row {lo, hi, q, 0} (int64) per sum:
+ *   value = (hi * 2^32 + lo) * 2^q.  Rows of the same sum on several ranks
+ *   add digit-wise (int64), then o3dx_fx_to_double rounds once. 
  * o3dx_plane_from_moments: host-only GetPlaneFromPoints from those sums. */
 int o3dx_plane_from_points(const double* pts_host, int k, double* plane_host);
+/* ComputeTrianglePlane / GetPlaneFromPoints of H hypotheses at once: coords
+ * (H x ransac_n x 3 float64, host) -> planes (H x 4, host; zero = degenerate). */
+int o3dx_planes_from_samples(const double* coords_host, int num_hypotheses,
+                             int ransac_n, double* planes_host);
 size_t o3dx_plane_count_workspace_bytes(int64_t n, int num_hypotheses);
 int o3dx_plane_count(const float* xyz_dev, int64_t n, const double* planes_host,
                      int num_hypotheses, double distance_threshold,
@@ -316,8 +337,14 @@ int o3dx_plane_count(const float* xyz_dev, int64_t n, const double* planes_host,
 int o3dx_plane_abs_sum(const float* xyz_dev, int64_t n,
                        const double* planes_host, const int32_t* which_host,
                        int num_which, double distance_threshold,
-                       double* sums_host, void* ws, size_t ws_bytes,
-                       void* stream);
+                       double* sums_host, int64_t* fx_out_host, void* ws,
+                       size_t ws_bytes, void* stream);
+/* The hypotheses whose Sigma|d| Open3D's selection can consult (equal-count
+ * ties at a running maximum, with its early break replayed on the counts),
+ * ascending, into out_host (capacity num_hypotheses); *n_out = their number. */
+int o3dx_ransac_tied(const int64_t* counts_host, const double* planes_host,
+                     int num_hypotheses, int64_t n, int ransac_n,
+                     double probability, int32_t* out_host, int32_t* n_out);
 int o3dx_ransac_select(const int64_t* counts_host, const double* sums_host,
                        const double* planes_host, int num_hypotheses,
                        int64_t n, int ransac_n, double probability);
@@ -347,9 +374,11 @@ int o3dx_plane_select_f64(const double* xyz_dev, int64_t n, const double* plane_
                           double* dist_out_dev, int32_t* idx_out_dev,
                           int64_t* count_host, void* ws, size_t ws_bytes,
                           void* stream);
+size_t o3dx_plane_moments_workspace_bytes(int64_t count);
 int o3dx_plane_moments(const float* xyz_dev, const int32_t* idx_dev,
                        int64_t count, const double* centroid_host,
-                       double* sums_host, void* ws, size_t ws_bytes,
+                       const double* absmax_host, double* sums_host,
+                       int64_t* fx_out_host, void* ws, size_t ws_bytes,
                        void* stream);
 int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
                             const double* centred_host, double* plane_host);
@@ -371,10 +400,14 @@ int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
  *   passed in this layout (src_sorted4 = 1) so that 64 consecutive queries
  *   form a compact patch (one LDS tile of target points); results are
  *   reported by original index.
- * o3dx_icp_accumulate: one fused pass over the source: transform by T_host
- *   (row-major 4x4, float64), 1-NN, residual/Jacobian, fixed-order float64
- *   reduction into sums_host[O3DX_ICP_NSUMS].  corr_out_dev (nullable, 2*ns
- *   int32 pairs (i,j)) + ncorr_host receive the correspondence set.
+ * o3dx_icp_accumulate: one pass over the source: transform by T_host
+ *   (row-major 4x4, float64), 1-NN, residual/Jacobian, exact fx sums
+ *   (o3dx_plane_moments note) into sums_host[O3DX_ICP_NSUMS] and, when
+ *   fx_out_host is given, their rows (O3DX_ICP_NSUMS x 4 int64).
+ *   src_absmax_host (nullable: this source's own): |x|,|y|,|z| bounds of the
+ *   WHOLE source (a sharded source passes the global ones), which with T and
+ *   the distance fix the fx quanta.  corr_out_dev (nullable, 2*ns int32
+ *   pairs (i,j)) + ncorr_host receive the correspondence set.
  * o3dx_icp_solve_point_to_plane: host-only 6x6 LDLT solve of the summed
  *   system -> update_host (4x4 row-major); returns 1 if solved, 0 if singular
  *   (identity update, as Open3D).
@@ -390,10 +423,15 @@ size_t o3dx_icp_accumulate_workspace_bytes(int64_t ns);
 int o3dx_icp_accumulate(const float* src_dev, int64_t ns, int src_sorted4,
                         const void* target_ws, const double* desc_host,
                         const double* T_host, double max_correspondence_distance,
-                        double* sums_host, int32_t* corr_out_dev,
+                        const double* src_absmax_host, double* sums_host,
+                        int64_t* fx_out_host, int32_t* corr_out_dev,
                         int64_t* ncorr_host, void* ws, size_t ws_bytes,
                         void* stream);
 int o3dx_icp_solve_point_to_plane(const double* sums_host, double* update_host);
+/* One ICP step on the host: solve the summed system and T <- update * T
+ * (T_host row-major 4x4, in place), in the same float64 order as the
+ * library's own registration loop; returns 1 if solved, 0 if singular. */
+int o3dx_icp_update(const double* sums_host, double* T_host);
 size_t o3dx_spatial_sort_workspace_bytes(int64_t n);
 int o3dx_spatial_sort(const float* xyz_dev, int64_t n, double target_occ,
                       float* sorted4_dev, void* ws, size_t ws_bytes,

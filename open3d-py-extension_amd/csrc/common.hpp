@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cmath>
 #include <cstdint>
@@ -135,6 +136,79 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
   return r;  // valid in thread 0
 }
 
+// ------------------------------------------- exact (order-free) float sums
+// "fx" sums: a float64 term t with |t| <= B becomes the integer
+// v = round(t * 2^-q), q = fx_exp(B) = (frexp exponent of B) - kFxBits, so
+// |v| < 2^51, and the integers are summed.  Integer addition is associative:
+// a sum is the same bits for any lane, block or rank split — what the
+// multi-GPU path needs (results identical for 1/2/4/8 GPUs)
+// and what a float64 reduction cannot give.  One fma does the conversion:
+// fma(t, 2^-q, 1.5 * 2^52) rounds t * 2^-q (exact: a power-of-two scale) to
+// the nearest integer, whose bits minus the magic's bits are v.  A lane adds
+// up to kFxLaneTerms terms in one int64 (< 2^63); across lanes, blocks and
+// ranks the sums travel as two int64 digits {lo = low 32 bits (>= 0), hi =
+// the rest}, which cannot overflow for < 2^31 terms.  The value is rounded to
+// float64 once, at the end (fx_to_double).  Error: <= n 2^-52 B (round to
+// nearest per term), the same order as a float64 sum's, but order-free.
+constexpr int kFxBits = 51;
+constexpr int64_t kFxLaneTerms = 4096;
+constexpr double kFxMagic = 6755399441055744.0;  // 1.5 * 2^52
+constexpr int64_t kFxMagicBits = 0x4338000000000000ll;
+
+inline int fx_exp(double B) {
+  int e = 0;
+  const double b = (B > 0.0 && std::isfinite(B)) ? std::max(B, std::ldexp(1.0, -900)) : 1.0;
+  std::frexp(b, &e);
+  return e - kFxBits;
+}
+inline double fx_scale(int q) { return std::ldexp(1.0, -q); }
+
+__device__ __forceinline__ int64_t fx_term(double t, double scale) {
+  return (int64_t)__double_as_longlong(fma(t, scale, kFxMagic)) - kFxMagicBits;
+}
+
+// Block partial of K lane accumulators: out[2k] = sum of the low 32-bit
+// digits, out[2k+1] = sum of the high parts (valid after the call in every
+// thread's view of `out`, written by threads < 2K).  sh: (BLOCK/64) * 2K.
+template <int BLOCK, int K>
+__device__ __forceinline__ void block_fx(const int64_t (&acc)[K], int64_t* sh, int64_t* out) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int64_t lo = acc[k] & 0xffffffffll, hi = acc[k] >> 32;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo += __shfl_xor(lo, o, 64);
+      hi += __shfl_xor(hi, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      sh[w * 2 * K + 2 * k] = lo;
+      sh[w * 2 * K + 2 * k + 1] = hi;
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * K; t += BLOCK) {
+    int64_t s = 0;
+#pragma unroll
+    for (int v = 0; v < BLOCK / 64; ++v) s += sh[v * 2 * K + t];
+    out[t] = s;
+  }
+  __syncthreads();
+}
+
+// {lo, hi} digit sums + exponent of k sums (row j: {lo, hi, q, 0}) -> float64,
+// correctly rounded (one rounding of the exact integer, then the exact scale)
+void fx_to_double(const int64_t* fx4, int64_t k, double* out);
+// digit sums (k rows {lo, hi}) + per-sum exponents -> the ABI's {lo, hi, q, 0} rows
+inline void fx_pack(const int64_t* digits, const int* q, int64_t k, int64_t* fx4) {
+  for (int64_t j = 0; j < k; ++j) {
+    fx4[4 * j] = digits[2 * j];
+    fx4[4 * j + 1] = digits[2 * j + 1];
+    fx4[4 * j + 2] = q[j];
+    fx4[4 * j + 3] = 0;
+  }
+}
+
 // ---------------------------------------------------------- kernel timing
 // RAII bracket of a launch with hipEvents on its stream (only when enabled by
 // o3dx_set_kernel_timing); read back lazily by o3dx_kernel_timing.
@@ -210,6 +284,8 @@ int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* po
 enum class RedOp { kSumF64, kSumI64, kMinF32, kMaxF32 };
 int reduce_columns_f64(const double* part, int64_t rows, int width, double* out, hipStream_t s);
 int reduce_columns_i32_to_i64(const int32_t* part, int64_t rows, int width, int64_t* out, hipStream_t s);
+// int64 columns (fx digit partials): exact, any order
+int reduce_columns_i64(const int64_t* part, int64_t rows, int width, int64_t* out, hipStream_t s);
 
 // AABB on device into a device double[6] (no sync).
 size_t aabb_ws_bytes(int64_t n);

@@ -353,15 +353,16 @@ int reduce_columns_f64(const double* part, int64_t rows, int width, double* out,
 // atomic — integer addition, so the result is the same in any order.
 constexpr int64_t kRedRowsPerBlock = 128;
 
-__global__ void __launch_bounds__(1024) k_reduce_columns_i64(const int32_t* __restrict__ part, int64_t rows,
-                                                             int width, int64_t* __restrict__ out) {
+template <class T>
+__global__ void __launch_bounds__(1024) k_reduce_columns_i64(const T* __restrict__ part, int64_t rows, int width,
+                                                             int64_t* __restrict__ out) {
   __shared__ int64_t sh[16][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.y * kRedRowsPerBlock, r1 = min(rows, r0 + kRedRowsPerBlock);
   int64_t acc = 0;
   if (c < width)
-    for (int64_t r = r0 + g; r < r1; r += 16) acc += part[r * width + c];
+    for (int64_t r = r0 + g; r < r1; r += 16) acc += (int64_t)part[r * width + c];
   sh[g][threadIdx.x & 63] = acc;
   __syncthreads();
   if (g == 0 && c < width) {
@@ -371,15 +372,31 @@ __global__ void __launch_bounds__(1024) k_reduce_columns_i64(const int32_t* __re
   }
 }
 
-int reduce_columns_i32_to_i64(const int32_t* part, int64_t rows, int width, int64_t* out, hipStream_t s) {
+template <class T>
+static int reduce_columns_to_i64(const T* part, int64_t rows, int width, int64_t* out, hipStream_t s) {
   if (width <= 0) return 0;
   O3DX_HIP(hipMemsetAsync(out, 0, (size_t)width * sizeof(int64_t), s));
   const int64_t by = std::max<int64_t>(1, (rows + kRedRowsPerBlock - 1) / kRedRowsPerBlock);
   if (by > 65535) return fail(O3DX_EINVAL, "reduce_columns: too many rows");
-  hipLaunchKernelGGL(k_reduce_columns_i64, dim3((width + 63) / 64, (unsigned)by), dim3(1024), 0, s, part, rows, width,
-                     out);
+  hipLaunchKernelGGL(k_reduce_columns_i64<T>, dim3((width + 63) / 64, (unsigned)by), dim3(1024), 0, s, part, rows,
+                     width, out);
   O3DX_HIP(hipGetLastError());
   return 0;
+}
+
+int reduce_columns_i32_to_i64(const int32_t* part, int64_t rows, int width, int64_t* out, hipStream_t s) {
+  return reduce_columns_to_i64(part, rows, width, out, s);
+}
+
+int reduce_columns_i64(const int64_t* part, int64_t rows, int width, int64_t* out, hipStream_t s) {
+  return reduce_columns_to_i64(part, rows, width, out, s);
+}
+
+void fx_to_double(const int64_t* fx4, int64_t k, double* out) {
+  for (int64_t j = 0; j < k; ++j) {
+    const __int128 v = (__int128)fx4[4 * j + 1] * ((__int128)1 << 32) + (__int128)fx4[4 * j];
+    out[j] = std::ldexp((double)v, (int)fx4[4 * j + 2]);  // (double) of __int128: round to nearest even
+  }
 }
 
 // ------------------------------------------------------------------- AABB
@@ -491,7 +508,20 @@ extern "C" int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* l
 
 extern "C" const char* o3dx_last_error(void) { return g_err.c_str(); }
 
+extern "C" int o3dx_fx_to_double(const int64_t* fx4, int64_t k, double* out) {
+  if (k < 0 || (k > 0 && (!fx4 || !out))) return fail(O3DX_EINVAL, "o3dx_fx_to_double: bad arguments");
+  fx_to_double(fx4, k, out);
+  return 0;
+}
+
 extern "C" size_t o3dx_aabb_workspace_bytes(int64_t n) { return aabb_ws_bytes(n) + 256; }
+
+extern "C" int o3dx_aabb_device(const float* xyz, int64_t n, double* minmax_dev, void* ws, size_t ws_bytes,
+                                void* stream) {
+  if (n < 0 || (n > 0 && !xyz) || !minmax_dev) return fail(O3DX_EINVAL, "o3dx_aabb_device: bad arguments");
+  if (!ws || ws_bytes < o3dx_aabb_workspace_bytes(n)) return fail(O3DX_ENOMEM, "o3dx_aabb_device: workspace too small");
+  return aabb_device(xyz, n, minmax_dev, ws, as_stream(stream));
+}
 
 extern "C" int o3dx_aabb(const float* xyz, int64_t n, double* minmax_host, void* ws, size_t ws_bytes,
                          void* stream) {

@@ -562,7 +562,72 @@ struct MomAcc {
   }
 };
 
-__device__ __forceinline__ void finish_normal(int cnt, const MomAcc& acc, const float* __restrict__ prior, int oi,
+// Exact-sum form of MomAcc for the sorted-grid kernels: each moment is a
+// double-double (h, l) grown by TwoSum.  The terms are exact (coordinates
+// are float32 values, their pairwise products fit float64), and while a
+// neighbourhood's non-zero coordinates lie within a factor 2^22 of each other
+// every (h, l) stays the exact partial sum, so h + l rounded once is the
+// correctly rounded exact sum: the same bits in ANY summation order.  The
+// sorted grid's scan order depends on its cell geometry, which depends on the
+// cloud given (a slab's own + halo points in the multi-GPU path, the whole
+// cloud on one GPU); with exact sums the normals do not.  (The voxel-table
+// kernels scan the global voxel grid in a fixed stencil order and keep the
+// plain sums.)
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+
+struct MomAccDD {
+  double m[9];  // h parts; cov() reads h + l
+  double l[9];
+  __device__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) m[j] = l[j] = 0.0;
+  }
+  __device__ __forceinline__ void put(int j, double t) {
+    double s, e;
+    two_sum(m[j], t, s, e);
+    m[j] = s;
+    l[j] += e;
+  }
+  __device__ void add(double x, double y, double z) {
+    put(0, x);
+    put(1, y);
+    put(2, z);
+    put(3, x * x);
+    put(4, x * y);
+    put(5, x * z);
+    put(6, y * y);
+    put(7, y * z);
+    put(8, z * z);
+  }
+  __device__ void cov(int k, double c[6]) const {
+    MomAcc a;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) a.m[j] = m[j] + l[j];
+    a.cov(k, c);
+  }
+};
+
+// wave-wide exact sum of exact terms (the same condition as MomAccDD): an
+// xor tree of (h, l) pairs joined by TwoSum, h + l rounded once
+__device__ __forceinline__ double wave_sum_exact(double t) {
+  double h = t, l = 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double h2 = __shfl_xor(h, o, 64), l2 = __shfl_xor(l, o, 64);
+    double s, e;
+    two_sum(h, h2, s, e);
+    h = s;
+    l = (l + l2) + e;
+  }
+  return h + l;
+}
+
+template <class Acc>
+__device__ __forceinline__ void finish_normal(int cnt, const Acc& acc, const float* __restrict__ prior, int oi,
                                               float* __restrict__ out) {
   double c[6];
   if (cnt >= 3) acc.cov(cnt, c);
@@ -611,7 +676,7 @@ __device__ __forceinline__ void knn_normal_query(const GridView& g, const float*
   double bd[K];
   int bi[K];
   const int cnt = knn_search_dev<K>(g, q.x, q.y, q.z, kneed, hybrid != 0, radius, bd, bi);
-  MomAcc acc;
+  MomAccDD acc;
   acc.zero();
 #pragma unroll
   for (int j = 0; j < K; ++j)
@@ -720,12 +785,12 @@ __device__ __forceinline__ bool hist_locate(const H& hist, int kneed, int below,
 // A band that overflows or a separation within rounding (ties included)
 // hands the query on (false) to the exact wave form.  Writes the normal of
 // original point `oi`.
-template <int KMAX, class T, class Fetch, class Ident>
+template <int KMAX, class Acc = MomAcc, class T, class Fetch, class Ident>
 __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int n, float Lm, float U, T (*lst)[64],
                                                  int lane, Fetch&& fetch, const float* __restrict__ prior, int oi,
                                                  float* __restrict__ out, int32_t* __restrict__ nbr, Ident&& ident,
                                                  float* __restrict__ kd2, bool skip_eigen = false) {
-  MomAcc acc;
+  Acc acc;
   acc.zero();
   int nsel = 0, nb = 0, nU = 0;
   float cmax = 0.0f;  // largest certain key
@@ -1054,7 +1119,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
             if (n == 12345) out[0] = 0.f;  // keep the scan alive
           } else
           fb = n > kListMax ||
-               !finish_selection<KMAX>(
+               !finish_selection<KMAX, MomAccDD>(
                    q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
                    prior, __float_as_int(q.w), out, g.nbr,
                    [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, g.kd2, dbg == 4);
@@ -2150,16 +2215,12 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
         for (int o = 32; o > 0; o >>= 1) dk = fmax(dk, __shfl_xor(dk, o, 64));
         if (lane == 0) g.kd2[__float_as_int(q.w)] = (float)(dk * (1.0 + 1e-6));
       }
+      // exact sums over the lanes (MomAccDD): the lane a neighbour landed on
+      // (the scan order) does not change the bits
       MomAcc acc;
-      acc.m[0] = wave_sum(x);
-      acc.m[1] = wave_sum(y);
-      acc.m[2] = wave_sum(z);
-      acc.m[3] = wave_sum(x * x);
-      acc.m[4] = wave_sum(x * y);
-      acc.m[5] = wave_sum(x * z);
-      acc.m[6] = wave_sum(y * y);
-      acc.m[7] = wave_sum(y * z);
-      acc.m[8] = wave_sum(z * z);
+      const double t9[9] = {x, y, z, x * x, x * y, x * z, y * y, y * z, z * z};
+#pragma unroll
+      for (int j = 0; j < 9; ++j) acc.m[j] = wave_sum_exact(t9[j]);
       if (lane == 0) finish_normal(kneed, acc, prior, __float_as_int(q.w), out);
     }
   }
@@ -2204,7 +2265,7 @@ __global__ void __launch_bounds__(kBlock) k_normals_radius(GridView g, double ra
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
   const int rmax = shell_rmax(g, cx, cy, cz);
   const double r2 = radius * radius, qx = q.x, qy = q.y, qz = q.z;
-  MomAcc acc;
+  MomAccDD acc;
   acc.zero();
   int cnt = 0;
   for (int r = 0; r <= rmax; ++r) {

@@ -26,10 +26,12 @@ struct Mat4 {
   double m[16];
 };
 
-// One correspondence into the 30 float64 moments: r = (vs - vt).nt,
+// One correspondence -> its 30 float64 moment terms: r = (vs - vt).nt,
 // J = [vs x nt ; nt] (Open3D ComputeJTJandJTr order), plus count and d^2.
-__device__ __forceinline__ void icp_add(double acc[30], double px, double py, double pz, const float4 vt,
-                                        const float4 nt, double d2) {
+constexpr int kNT = 30;
+
+__device__ __forceinline__ void icp_terms(double t[kNT], double px, double py, double pz, const float4 vt,
+                                          const float4 nt, double d2) {
   const double nx = nt.x, ny = nt.y, nz = nt.z;
   const double r = ((px - (double)vt.x) * nx + (py - (double)vt.y) * ny) + (pz - (double)vt.z) * nz;
   double J[6];
@@ -43,13 +45,18 @@ __device__ __forceinline__ void icp_add(double acc[30], double px, double py, do
 #pragma unroll
   for (int a = 0; a < 6; ++a)
 #pragma unroll
-    for (int b = a; b < 6; ++b) acc[k++] += J[a] * J[b];
+    for (int b = a; b < 6; ++b) t[k++] = J[a] * J[b];
 #pragma unroll
-  for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
-  acc[27] += r * r;
-  acc[28] += 1.0;
-  acc[29] += d2;
+  for (int a = 0; a < 6; ++a) t[21 + a] = J[a] * r;
+  t[27] = r * r;
+  t[28] = 1.0;
+  t[29] = d2;
 }
+
+// fx scales (2^-q) of the 30 sums, from bounds every rank derives alike
+struct FxScales {
+  double s[kNT];
+};
 
 // Source point j -> (original index, float64 position under T).  SORTED: src
 // is float4 (x, y, z, bits(original index)) in the compact spatial order of
@@ -102,32 +109,34 @@ __global__ void __launch_bounds__(kBlock) k_icp_match(const float* __restrict__ 
 }
 
 // Pass 2 — moments: a streaming pass over the matched pairs (source point,
-// target point + normal gathered by sorted position), the 30 float64 sums per
-// lane, wave xor-tree, block, block partials (fixed order: bit-identical run
-// to run).  d^2 is recomputed exactly as the search computed it.
+// target point + normal gathered by sorted position), the 30 moment terms per
+// pair as exact fx integers (common.hpp), summed per lane in int64, then per
+// block into {lo, hi} digit partials: the sums are the same bits for any
+// split of the source over lanes, blocks or ranks.  d^2 is recomputed exactly
+// as the search computed it.
 template <bool SORTED>
 __global__ void __launch_bounds__(kBlock) k_icp_moments(const float* __restrict__ src, int64_t ns, GridView g,
                                                         const float4* __restrict__ tnorm, Mat4 T,
-                                                        const int32_t* __restrict__ mpos,
-                                                        double* __restrict__ partial) {
-  __shared__ double sh[kBlock / 64];
-  double acc[30];
+                                                        const int32_t* __restrict__ mpos, FxScales sc,
+                                                        int64_t* __restrict__ partial) {
+  __shared__ int64_t sh[(kBlock / 64) * 2 * kNT];
+  int64_t acc[kNT];
 #pragma unroll
-  for (int k = 0; k < 30; ++k) acc[k] = 0.0;
+  for (int k = 0; k < kNT; ++k) acc[k] = 0;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += (int64_t)gridDim.x * blockDim.x) {
     const int pos = mpos[j];
     if (pos < 0) continue;
     double px, py, pz;
     icp_source<SORTED>(src, j, T, &px, &py, &pz);
     const float4 vt = g.pts[pos];
-    icp_add(acc, px, py, pz, vt, tnorm[pos], dist2_f64(px, py, pz, vt));
-  }
+    double t[kNT];
+    icp_terms(t, px, py, pz, vt, tnorm[pos], dist2_f64(px, py, pz, vt));
 #pragma unroll
-  for (int k = 0; k < 30; ++k) {
-    double v = block_sum_f64<kBlock>(acc[k], sh);
-    if (threadIdx.x == 0) partial[(int64_t)blockIdx.x * kNS + k] = v;
+    for (int k = 0; k < kNT; ++k) acc[k] += fx_term(t[k], sc.s[k]);
   }
-  if (threadIdx.x < kNS - 30) partial[(int64_t)blockIdx.x * kNS + 30 + threadIdx.x] = 0.0;
+  int64_t* out = partial + (int64_t)blockIdx.x * 2 * kNS;
+  block_fx<kBlock, kNT>(acc, sh, out);
+  if (threadIdx.x < 2 * (kNS - kNT)) out[2 * kNT + threadIdx.x] = 0;
 }
 
 __global__ void __launch_bounds__(kBlock) k_corr_flags(const int32_t* __restrict__ cj, int64_t ns,
@@ -262,35 +271,120 @@ static bool desc_unpack(const double* d, const void* base, GridView* g, const fl
   return true;
 }
 
+// fx exponents of the 32 sums (common.hpp) from bounds that every rank
+// derives alike — the source's |x|,|y|,|z| bounds (the whole source's, on
+// every rank), T and max_correspondence_distance:
+//   |p|  <= Pn = |(|T| absmax + |t|)| (row bounds of T (x,y,z,1), Euclidean)
+//   |J_a| <= Pn |n| (a < 3), |n_a| (a >= 3), |n| <= 1.01 (float32 unit normal)
+//   |r| = |(p - vt).n| <= d |n| < max_corr |n|,  d^2 < max_corr^2
+// (1.01: margin for float rounding; a looser bound only coarsens the quantum).
+static void icp_fx_exps(const double absmax[3], const double* T, double max_corr, int q[kNS]) {
+  double P2 = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    const double Pi = ((std::fabs(T[4 * i]) * absmax[0] + std::fabs(T[4 * i + 1]) * absmax[1]) +
+                       std::fabs(T[4 * i + 2]) * absmax[2]) + std::fabs(T[4 * i + 3]);
+    P2 += Pi * Pi;
+  }
+  const double pn = std::sqrt(P2) * 1.01;
+  double bJ[6];
+  for (int a = 0; a < 6; ++a) bJ[a] = (a < 3 ? pn : 1.0) * 1.01;
+  const double br = max_corr * 1.01 * 1.01;
+  int k = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int b = a; b < 6; ++b) q[k++] = fx_exp(bJ[a] * bJ[b] * 1.01);
+  for (int a = 0; a < 6; ++a) q[21 + a] = fx_exp(bJ[a] * br * 1.01);
+  q[27] = fx_exp(br * br * 1.01);
+  q[28] = fx_exp(1.0);
+  q[29] = fx_exp(max_corr * max_corr * 1.01);
+  q[30] = q[31] = 0;
+}
+
 struct AccWs {
-  double* partial;
-  double* sums;
+  int64_t* partial;
+  int64_t* digits;
   int32_t* cj;
   int32_t* mpos;
   uint8_t* flags;
   int32_t* src_idx;
   int32_t* scan_tmp;
   int64_t* cnt;
+  char* aabb;
+  double* mm;
 };
 
+// blocks of the moments pass: <= kFxLaneTerms pairs per lane
+static int icp_blocks(int64_t ns) {
+  const int64_t need = (ns + (int64_t)kBlock * kFxLaneTerms - 1) / ((int64_t)kBlock * kFxLaneTerms);
+  return (int)std::max<int64_t>(1, std::max<int64_t>(need, std::min<int64_t>(kIcpBlocks, (ns + kBlock - 1) / kBlock)));
+}
+
 static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
-  w->partial = ar.take<double>((size_t)kIcpBlocks * kNS);
-  w->sums = ar.take<double>(kNS);
+  w->partial = ar.take<int64_t>((size_t)icp_blocks(ns) * 2 * kNS);
+  w->digits = ar.take<int64_t>(2 * kNS);
   w->cj = ar.take<int32_t>(ns);
   w->mpos = ar.take<int32_t>(ns);
   w->flags = ar.take<uint8_t>(ns + 16);
   w->src_idx = ar.take<int32_t>(ns);
   w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(ns));
   w->cnt = ar.take<int64_t>(2);
+  w->aabb = ar.take<char>(aabb_ws_bytes(ns));
+  w->mm = ar.take<double>(8);
   return ar.used;
 }
 
+__global__ void __launch_bounds__(kBlock) k_absmax4(const float4* __restrict__ p, int64_t n, unsigned int* __restrict__ out) {
+  float m[3] = {0.f, 0.f, 0.f};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = p[i];
+    m[0] = fmaxf(m[0], fabsf(v.x));
+    m[1] = fmaxf(m[1], fabsf(v.y));
+    m[2] = fmaxf(m[2], fabsf(v.z));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) m[a] = fmaxf(m[a], __shfl_xor(m[a], o, 64));
+  // non-negative floats order as their bits: an integer max is the float max
+  if ((threadIdx.x & 63) == 0)
+    for (int a = 0; a < 3; ++a) atomicMax(&out[a], __float_as_uint(m[a]));
+}
+
+// |x|,|y|,|z| bounds of a source: (n,3) float32 or the (n,4) sorted form
+static int source_absmax(const float* src, int64_t ns, bool sorted, AccWs& w, hipStream_t s, double out[3]) {
+  if (sorted) {
+    unsigned int* u = reinterpret_cast<unsigned int*>(w.mm);
+    O3DX_HIP(hipMemsetAsync(u, 0, 4 * sizeof(unsigned int), s));
+    hipLaunchKernelGGL(k_absmax4, dim3(grid_for(ns, kBlock, 1024)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const float4*>(src), ns, u);
+    unsigned int b[4];
+    O3DX_TRY(read_back(b, u, sizeof(b), s));
+    for (int a = 0; a < 3; ++a) {
+      float f;
+      std::memcpy(&f, &b[a], 4);
+      out[a] = f;
+    }
+    return 0;
+  }
+  double mm[6];
+  O3DX_TRY(aabb_device(src, ns, w.mm, w.aabb, s));
+  O3DX_TRY(read_back(mm, w.mm, sizeof(mm), s));
+  for (int a = 0; a < 3; ++a) out[a] = std::max(std::fabs(mm[a]), std::fabs(mm[3 + a]));
+  return 0;
+}
+
+// absmax: the source's coordinate bounds (host, 3) — the same on every rank
+// of a sharded source; fx_out (nullable, host 4 x kNS): the exact sums.
 static int accumulate(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, const double* T,
-                      double radius, AccWs& w, hipStream_t s, double* sums_host, int32_t* corr_out, int64_t* ncorr) {
+                      double radius, const double* absmax, AccWs& w, hipStream_t s, double* sums_host,
+                      int64_t* fx_out, int32_t* corr_out, int64_t* ncorr) {
   Mat4 M;
   std::memcpy(M.m, T, sizeof(M.m));
-  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kIcpBlocks, (ns + kBlock - 1) / kBlock));
+  const int nb = icp_blocks(ns);
   const bool want_corr = corr_out != nullptr;
+  int q[kNS];
+  icp_fx_exps(absmax, T, radius, q);
+  FxScales sc;
+  for (int k = 0; k < kNT; ++k) sc.s[k] = fx_scale(q[k]);
   KTimer kt("icp_accumulate", s);
   if (ns > 0) {
     int32_t* cj = want_corr ? w.cj : (int32_t*)nullptr;
@@ -309,13 +403,13 @@ static int accumulate(const float* src, int64_t ns, bool sorted, const GridView&
                          cj);
     km.stop();
     if (sorted)
-      hipLaunchKernelGGL(k_icp_moments<true>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, w.partial);
+      hipLaunchKernelGGL(k_icp_moments<true>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, sc, w.partial);
     else
-      hipLaunchKernelGGL(k_icp_moments<false>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, w.partial);
+      hipLaunchKernelGGL(k_icp_moments<false>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, sc, w.partial);
+    O3DX_TRY(reduce_columns_i64(w.partial, nb, 2 * kNS, w.digits, s));
   } else {
-    O3DX_HIP(hipMemsetAsync(w.partial, 0, kNS * sizeof(double), s));
+    O3DX_HIP(hipMemsetAsync(w.digits, 0, 2 * kNS * sizeof(int64_t), s));
   }
-  O3DX_TRY(reduce_columns_f64(w.partial, ns > 0 ? nb : 1, kNS, w.sums, s));
   kt.stop();
   if (want_corr && ns > 0) {
     hipLaunchKernelGGL(k_corr_flags, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, ns, w.flags);
@@ -329,8 +423,12 @@ static int accumulate(const float* src, int64_t ns, bool sorted, const GridView&
   } else if (ncorr) {
     *ncorr = -1;
   }
-  O3DX_TRY(read_back(sums_host, w.sums, kNS * sizeof(double), s));
+  int64_t digits[2 * kNS], fx[4 * kNS];
+  O3DX_TRY(read_back(digits, w.digits, sizeof(digits), s));
   O3DX_HIP(hipGetLastError());
+  fx_pack(digits, q, kNS, fx);
+  fx_to_double(fx, kNS, sums_host);
+  if (fx_out) std::memcpy(fx_out, fx, sizeof(fx));
   if (ncorr && !want_corr) *ncorr = (int64_t)sums_host[28];
   return 0;
 }
@@ -378,8 +476,9 @@ extern "C" size_t o3dx_icp_accumulate_workspace_bytes(int64_t ns) {
 }
 
 extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, int src_sorted4, const void* target_ws,
-                                   const double* desc, const double* T, double max_corr, double* sums,
-                                   int32_t* corr_out, int64_t* ncorr, void* ws, size_t ws_bytes, void* stream) {
+                                   const double* desc, const double* T, double max_corr, const double* src_absmax,
+                                   double* sums, int64_t* fx_out, int32_t* corr_out, int64_t* ncorr, void* ws,
+                                   size_t ws_bytes, void* stream) {
   if (ns < 0 || (ns > 0 && !src) || !target_ws || !T || !sums) return fail(O3DX_EINVAL, "o3dx_icp_accumulate: bad args");
   GridView g;
   const float4* tn;
@@ -388,7 +487,11 @@ extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, int src_sorted4
   Arena ar(ws, ws_bytes);
   AccWs w;
   acc_carve(ar, std::max<int64_t>(ns, 1), &w);
-  return accumulate(src, ns, src_sorted4 != 0, g, tn, T, max_corr, w, as_stream(stream), sums, corr_out, ncorr);
+  hipStream_t s = as_stream(stream);
+  double am[3] = {0, 0, 0};
+  if (src_absmax) std::memcpy(am, src_absmax, sizeof(am));
+  else if (ns > 0) O3DX_TRY(source_absmax(src, ns, src_sorted4 != 0, w, s, am));
+  return accumulate(src, ns, src_sorted4 != 0, g, tn, T, max_corr, am, w, s, sums, fx_out, corr_out, ncorr);
 }
 
 extern "C" size_t o3dx_spatial_sort_workspace_bytes(int64_t n) { return grid_ws_bytes(n) + 1024; }
@@ -409,6 +512,14 @@ extern "C" int o3dx_spatial_sort(const float* xyz, int64_t n, double target_occ,
 extern "C" int o3dx_icp_solve_point_to_plane(const double* sums, double* upd) {
   if (!sums || !upd) return fail(O3DX_EINVAL, "o3dx_icp_solve_point_to_plane: bad args");
   return solve_update(sums, upd);
+}
+
+extern "C" int o3dx_icp_update(const double* sums, double* T) {
+  if (!sums || !T) return fail(O3DX_EINVAL, "o3dx_icp_update: bad args");
+  double upd[16];
+  const int solved = solve_update(sums, upd);
+  mat4_mul(upd, T, T);
+  return solved;
 }
 
 extern "C" size_t o3dx_registration_icp_workspace_bytes(int64_t ns) {
@@ -445,6 +556,8 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
   else
     for (int a = 0; a < 16; ++a) T[a] = (a % 5 == 0) ? 1.0 : 0.0;
   double sums[kNS];
+  double am[3] = {0, 0, 0};
+  if (ns > 0) O3DX_TRY(source_absmax(src4, ns, true, w, s, am));
   auto metrics = [&](const double* sm, double& fit, double& rm) {
     double c = sm[28];
     if (c <= 0 || ns == 0) {
@@ -455,7 +568,7 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
       rm = std::sqrt(sm[29] / c);
     }
   };
-  O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, nullptr, nullptr));
+  O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, nullptr, nullptr));
   double fit, rm;
   metrics(sums, fit, rm);
   for (int it = 0; it < max_iteration; ++it) {
@@ -464,14 +577,14 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
     mat4_mul(upd, T, T);
     const double pf = fit, pr = rm;
     const bool last = (it + 1 == max_iteration);
-    O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, last ? corr_out : nullptr, last ? ncorr : nullptr));
+    O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, last ? corr_out : nullptr, last ? ncorr : nullptr));
     metrics(sums, fit, rm);
     if (std::fabs(pf - fit) < rel_fit && std::fabs(pr - rm) < rel_rmse) {
-      if (!last && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
+      if (!last && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, corr_out, ncorr));
       break;
     }
   }
-  if (max_iteration <= 0 && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, w, s, sums, corr_out, ncorr));
+  if (max_iteration <= 0 && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, corr_out, ncorr));
   std::memcpy(T_out, T, sizeof(T));
   *fitness = fit;
   *rmse = rm;

@@ -454,20 +454,26 @@ __global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H,
 
 constexpr int kSumBlocksX = 64;
 
+// Sigma |d| over the points with |d| < thr, one hypothesis per blockIdx.y, as
+// an exact fx sum (common.hpp; |d| < thr bounds every term): the same bits for
+// any split of the cloud over blocks or ranks.  partial: [y][x] {lo, hi}.
 __global__ void __launch_bounds__(kBlock) k_plane_abs_sum(const float* __restrict__ xyz, int64_t n,
-                                                          const double* __restrict__ pl64, double thr,
-                                                          double* __restrict__ partial) {
-  __shared__ double sh[kBlock / 64];
+                                                          const double* __restrict__ pl64, double thr, double scale,
+                                                          int64_t* __restrict__ partial) {
+  __shared__ int64_t sh[(kBlock / 64) * 2];
   const double* pl = pl64 + 4 * blockIdx.y;
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  double acc = 0.0;
+  int64_t acc[1] = {0};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     P3 q = p[i];
     double d = plane_dist64(pl, q.x, q.y, q.z);
-    if (d < thr) acc += d;
+    if (d < thr) acc[0] += fx_term(d, scale);
   }
-  double r = block_sum_f64<kBlock>(acc, sh);
-  if (threadIdx.x == 0) partial[blockIdx.y * gridDim.x + blockIdx.x] = r;
+  block_fx<kBlock, 1>(acc, sh, partial + 2 * ((int64_t)blockIdx.y * gridDim.x + blockIdx.x));
+}
+
+static int abs_sum_blocks(int64_t n) {
+  return (int)std::max<int64_t>(kSumBlocksX, (n + (int64_t)kBlock * kFxLaneTerms - 1) / ((int64_t)kBlock * kFxLaneTerms));
 }
 
 __global__ void __launch_bounds__(kBlock) k_plane_flags(const float* __restrict__ xyz, int64_t n, double a, double b,
@@ -503,33 +509,49 @@ __global__ void __launch_bounds__(kBlock) k_plane_band(const T* __restrict__ xyz
 
 constexpr int kMomBlocks = 256;
 
-// pass 1 (centroid == nullptr): {x, y, z}; pass 2: centred {xx, xy, xz, yy, yz, zz}
+// GetPlaneFromPoints moments over the inliers as exact fx sums (common.hpp),
+// so the refit plane is the same bits for any split of the inliers over
+// blocks or ranks.  pass 1 (pass2 == 0): {x, y, z}; pass 2: centred
+// {xx, xy, xz, yy, yz, zz}.  sc: the fx scales of the pass's sums.
+struct MomScales {
+  double s[6];
+};
+
 __global__ void __launch_bounds__(kBlock) k_plane_moments(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
                                                           int64_t m, double cx, double cy, double cz, int pass2,
-                                                          double* __restrict__ partial) {
-  __shared__ double sh[kBlock / 64];
-  double acc[6] = {0, 0, 0, 0, 0, 0};
+                                                          MomScales sc, int64_t* __restrict__ partial) {
+  __shared__ int64_t sh[(kBlock / 64) * 12];
+  int64_t acc[6] = {0, 0, 0, 0, 0, 0};
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     int64_t i = idx ? idx[j] : j;
     double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
     if (!pass2) {
-      acc[0] += x;
-      acc[1] += y;
-      acc[2] += z;
+      acc[0] += fx_term(x, sc.s[0]);
+      acc[1] += fx_term(y, sc.s[1]);
+      acc[2] += fx_term(z, sc.s[2]);
     } else {
       double r0 = x - cx, r1 = y - cy, r2 = z - cz;
-      acc[0] += r0 * r0;
-      acc[1] += r0 * r1;
-      acc[2] += r0 * r2;
-      acc[3] += r1 * r1;
-      acc[4] += r1 * r2;
-      acc[5] += r2 * r2;
+      acc[0] += fx_term(r0 * r0, sc.s[0]);
+      acc[1] += fx_term(r0 * r1, sc.s[1]);
+      acc[2] += fx_term(r0 * r2, sc.s[2]);
+      acc[3] += fx_term(r1 * r1, sc.s[3]);
+      acc[4] += fx_term(r1 * r2, sc.s[4]);
+      acc[5] += fx_term(r2 * r2, sc.s[5]);
     }
   }
-  for (int k = 0; k < 6; ++k) {
-    double r = block_sum_f64<kBlock>(acc[k], sh);
-    if (threadIdx.x == 0) partial[blockIdx.x * 6 + k] = r;
-  }
+  block_fx<kBlock, 6>(acc, sh, partial + (int64_t)blockIdx.x * 12);
+}
+
+static int mom_blocks(int64_t m) {
+  const int64_t need = (m + (int64_t)kBlock * kFxLaneTerms - 1) / ((int64_t)kBlock * kFxLaneTerms);
+  return (int)std::max<int64_t>(1, std::max<int64_t>(need, std::min<int64_t>(kMomBlocks, (m + kBlock - 1) / kBlock)));
+}
+
+// fx exponents of the moment sums from A = the largest |coordinate| of the
+// cloud (every rank of a sharded cloud passes the global one): |x| <= A;
+// centred |x - c| <= 2A, products <= 4A^2 (x 1.01 for rounding)
+static void mom_fx_exps(double A, bool pass2, int q[6]) {
+  for (int k = 0; k < 6; ++k) q[k] = pass2 ? fx_exp(4.0 * A * A * 1.01) : (k < 3 ? fx_exp(A) : 0);
 }
 
 __global__ void k_gather_samples(const float* __restrict__ xyz, const int32_t* __restrict__ idx, int64_t m,
@@ -645,8 +667,7 @@ struct CountWs {
   uint32_t* flags;  // (batch, hypothesis chunk) window bitmap of the brute-force count
   uint32_t* mflags;  // (16-point step, 16-hypothesis tile) window bitmap of the MFMA count
   int64_t* counts;
-  double* sum_partial;
-  double* sums;
+  int64_t* sum_partial;
 };
 
 static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
@@ -659,8 +680,7 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   w->flags = ar.take<uint32_t>((size_t)count_flag_words(n, H, kMinBatchPts, kMinHC));
   w->mflags = ar.take<uint32_t>((size_t)mf_flag_words(n, H));
   w->counts = ar.take<int64_t>(H);
-  w->sum_partial = ar.take<double>((size_t)kSumBlocksX * H);
-  w->sums = ar.take<double>(H);
+  w->sum_partial = ar.take<int64_t>((size_t)2 * abs_sum_blocks(n) * H);
   return ar.used;
 }
 
@@ -714,9 +734,10 @@ static int absmax_of(const float* xyz, int64_t n, void* aabb_ws, double* mm_dev,
 }
 
 static int run_count(const float* xyz, int64_t n, const double* planes, int H, double thr, CountWs& w, void* aabb_ws,
-                     double* mm_dev, hipStream_t s, std::vector<int64_t>& counts) {
+                     double* mm_dev, hipStream_t s, std::vector<int64_t>& counts, const double* absmax_in = nullptr) {
   double absmax[3];
-  O3DX_TRY(absmax_of(xyz, n, aabb_ws, mm_dev, s, absmax));
+  if (absmax_in) std::memcpy(absmax, absmax_in, sizeof(absmax));
+  else O3DX_TRY(absmax_of(xyz, n, aabb_ws, mm_dev, s, absmax));
   std::vector<float4> p32;
   std::vector<float4> bnd;
   std::vector<uint8_t> dg;
@@ -808,23 +829,36 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   return 0;
 }
 
+// Sigma |d| of the hypotheses `which` (exact fx sums; fx_host: {lo, hi, q, 0}
+// rows, nullable), their float64 values into sums_host.
 static int run_abs_sum(const float* xyz, int64_t n, const double* planes, const int32_t* which, int L, double thr,
-                       CountWs& w, hipStream_t s, double* sums_host) {
+                       CountWs& w, hipStream_t s, double* sums_host, int64_t* fx_host = nullptr) {
   if (L == 0) return 0;
   std::vector<double> sel((size_t)4 * L);
   for (int j = 0; j < L; ++j)
     for (int a = 0; a < 4; ++a) sel[4 * j + a] = planes[4 * which[j] + a];
   O3DX_HIP(hipMemcpyAsync(w.pl64, sel.data(), sel.size() * sizeof(double), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_plane_abs_sum, dim3(kSumBlocksX, L), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, w.sum_partial);
-  // fixed-order final sums on the host
-  std::vector<double> part((size_t)kSumBlocksX * L);
-  O3DX_TRY(read_back(part.data(), w.sum_partial, part.size() * sizeof(double), s));
+  const int bx = abs_sum_blocks(n);
+  const int q = fx_exp(thr);
+  hipLaunchKernelGGL(k_plane_abs_sum, dim3(bx, L), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, fx_scale(q),
+                     w.sum_partial);
+  std::vector<int64_t> part((size_t)2 * bx * L);
+  O3DX_TRY(read_back(part.data(), w.sum_partial, part.size() * sizeof(int64_t), s));
   O3DX_HIP(hipGetLastError());
+  std::vector<int64_t> fx((size_t)4 * L);
   for (int j = 0; j < L; ++j) {
-    double t = 0.0;
-    for (int b = 0; b < kSumBlocksX; ++b) t += part[(size_t)j * kSumBlocksX + b];
-    sums_host[j] = t;
+    int64_t lo = 0, hi = 0;  // integer sums: any order
+    for (int b = 0; b < bx; ++b) {
+      lo += part[2 * ((size_t)j * bx + b)];
+      hi += part[2 * ((size_t)j * bx + b) + 1];
+    }
+    fx[4 * j] = lo;
+    fx[4 * j + 1] = hi;
+    fx[4 * j + 2] = q;
+    fx[4 * j + 3] = 0;
   }
+  fx_to_double(fx.data(), L, sums_host);
+  if (fx_host) std::memcpy(fx_host, fx.data(), fx.size() * sizeof(int64_t));
   return 0;
 }
 
@@ -897,18 +931,28 @@ static std::vector<int32_t> tied_hypotheses(const std::vector<int64_t>& counts, 
   return out;
 }
 
-static int run_moments(const float* xyz, const int32_t* idx, int64_t m, const double* centroid, double* part,
-                       double* out_dev, hipStream_t s, double out[6]) {
-  if (m == 0) {
-    for (int k = 0; k < 6; ++k) out[k] = 0;
-    return 0;
+// moments pass (fx sums, common.hpp) over idx[0..m) (or the first m points);
+// A bounds |coordinate|; out: 3 (pass 1) or 6 (pass 2) float64; fx_host
+// (nullable): their {lo, hi, q, 0} rows
+static int run_moments(const float* xyz, const int32_t* idx, int64_t m, const double* centroid, double A,
+                       int64_t* part, int64_t* out_dev, hipStream_t s, double out[6], int64_t* fx_host = nullptr) {
+  const int K = centroid ? 6 : 3;
+  int q[6];
+  mom_fx_exps(A, centroid != nullptr, q);
+  int64_t digits[12] = {0}, fx[24];
+  if (m > 0) {
+    const int nb = mom_blocks(m);
+    MomScales sc;
+    for (int k = 0; k < 6; ++k) sc.s[k] = fx_scale(q[k]);
+    hipLaunchKernelGGL(k_plane_moments, dim3(nb), dim3(kBlock), 0, s, xyz, idx, m, centroid ? centroid[0] : 0.0,
+                       centroid ? centroid[1] : 0.0, centroid ? centroid[2] : 0.0, centroid ? 1 : 0, sc, part);
+    O3DX_TRY(reduce_columns_i64(part, nb, 12, out_dev, s));
+    O3DX_TRY(read_back(digits, out_dev, sizeof(digits), s));
+    O3DX_HIP(hipGetLastError());
   }
-  const int nb = (int)std::min<int64_t>(kMomBlocks, (m + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_plane_moments, dim3(nb), dim3(kBlock), 0, s, xyz, idx, m, centroid ? centroid[0] : 0.0,
-                     centroid ? centroid[1] : 0.0, centroid ? centroid[2] : 0.0, centroid ? 1 : 0, part);
-  O3DX_TRY(reduce_columns_f64(part, nb, 6, out_dev, s));
-  O3DX_TRY(read_back(out, out_dev, 6 * sizeof(double), s));
-  O3DX_HIP(hipGetLastError());
+  fx_pack(digits, q, K, fx);
+  fx_to_double(fx, K, out);
+  if (fx_host) std::memcpy(fx_host, fx, (size_t)4 * K * sizeof(int64_t));
   return 0;
 }
 
@@ -921,8 +965,8 @@ struct SegWs {
   char* aabb;
   double* mm;
   int64_t* cnt;
-  double* mom_part;
-  double* mom_out;
+  int64_t* mom_part;
+  int64_t* mom_out;
 };
 
 static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
@@ -934,8 +978,8 @@ static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
   w->aabb = ar.take<char>(aabb_ws_bytes(n));
   w->mm = ar.take<double>(8);
   w->cnt = ar.take<int64_t>(4);
-  w->mom_part = ar.take<double>(kMomBlocks * 6);
-  w->mom_out = ar.take<double>(8);
+  w->mom_part = ar.take<int64_t>((size_t)mom_blocks(n) * 12);
+  w->mom_out = ar.take<int64_t>(16);
   return ar.used;
 }
 
@@ -963,6 +1007,13 @@ extern "C" int o3dx_ransac_samples(int64_t n, int ransac_n, int iters, uint64_t 
 extern "C" int o3dx_plane_from_points(const double* pts, int k, double* plane) {
   if (!pts || !plane || k < 3) return fail(O3DX_EINVAL, "o3dx_plane_from_points: need k >= 3");
   plane_from_pts(pts, k, plane);
+  return 0;
+}
+
+extern "C" int o3dx_planes_from_samples(const double* coords, int H, int ransac_n, double* planes) {
+  if (H < 0 || ransac_n < 3 || (H > 0 && (!coords || !planes)))
+    return fail(O3DX_EINVAL, "o3dx_planes_from_samples: bad arguments");
+  for (int h = 0; h < H; ++h) plane_from_pts(coords + (size_t)h * ransac_n * 3, ransac_n, planes + 4 * (size_t)h);
   return 0;
 }
 
@@ -1005,19 +1056,35 @@ extern "C" int o3dx_plane_count(const float* xyz, int64_t n, const double* plane
 }
 
 extern "C" int o3dx_plane_abs_sum(const float* xyz, int64_t n, const double* planes, const int32_t* which, int L,
-                                  double thr, double* sums, void* ws, size_t ws_bytes, void* stream) {
+                                  double thr, double* sums, int64_t* fx_out, void* ws, size_t ws_bytes, void* stream) {
   if (n < 0 || L < 0 || (L > 0 && (!planes || !which || !sums))) return fail(O3DX_EINVAL, "o3dx_plane_abs_sum: bad args");
   if (!ws || ws_bytes < o3dx_plane_count_workspace_bytes(n, L)) return fail(O3DX_ENOMEM, "abs_sum workspace too small");
   if (L == 0) return 0;
   if (n == 0) {
-    for (int j = 0; j < L; ++j) sums[j] = 0;
+    for (int j = 0; j < L; ++j) {
+      sums[j] = 0;
+      if (fx_out) {
+        fx_out[4 * j] = fx_out[4 * j + 1] = fx_out[4 * j + 3] = 0;
+        fx_out[4 * j + 2] = fx_exp(thr);
+      }
+    }
     return 0;
   }
   Arena ar(ws, ws_bytes);
   CountWs w;
   count_carve(ar, n, L, &w);
   O3DX_ARENA_CHECK(ar);
-  return run_abs_sum(xyz, n, planes, which, L, thr, w, as_stream(stream), sums);
+  return run_abs_sum(xyz, n, planes, which, L, thr, w, as_stream(stream), sums, fx_out);
+}
+
+extern "C" int o3dx_ransac_tied(const int64_t* counts, const double* planes, int H, int64_t n, int ransac_n,
+                                double probability, int32_t* out, int32_t* n_out) {
+  if (!counts || !out || !n_out || H < 0 || n <= 0) return fail(O3DX_EINVAL, "o3dx_ransac_tied: bad args");
+  std::vector<int64_t> c(counts, counts + H);
+  const std::vector<int32_t> t = tied_hypotheses(c, planes, n, ransac_n, probability);
+  std::memcpy(out, t.data(), t.size() * sizeof(int32_t));
+  *n_out = (int32_t)t.size();
+  return 0;
 }
 
 extern "C" int o3dx_ransac_select(const int64_t* counts, const double* sums, const double* planes, int H, int64_t n,
@@ -1103,15 +1170,52 @@ extern "C" int o3dx_plane_select_f64(const double* xyz, int64_t n, const double*
   return plane_select_impl(xyz, n, plane, band, lo, hi, invert, dist_out, idx_out, count_host, ws, ws_bytes, stream);
 }
 
+__global__ void __launch_bounds__(kBlock) k_absmax_sel(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
+                                                       int64_t m, unsigned int* __restrict__ out) {
+  float a[3] = {0.f, 0.f, 0.f};
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = idx ? idx[j] : j;
+    for (int c = 0; c < 3; ++c) a[c] = fmaxf(a[c], fabsf(xyz[3 * i + c]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a[c] = fmaxf(a[c], __shfl_xor(a[c], o, 64));
+  if ((threadIdx.x & 63) == 0)
+    for (int c = 0; c < 3; ++c) atomicMax(&out[c], __float_as_uint(a[c]));  // non-negative: bits order as values
+}
+
+extern "C" size_t o3dx_plane_moments_workspace_bytes(int64_t count) {
+  return Arena::align((size_t)mom_blocks(std::max<int64_t>(count, 1)) * 12 * sizeof(int64_t) + 1) + 1024;
+}
+
 extern "C" int o3dx_plane_moments(const float* xyz, const int32_t* idx, int64_t count, const double* centroid,
-                                  double* sums, void* ws, size_t ws_bytes, void* stream) {
+                                  const double* absmax, double* sums, int64_t* fx_out, void* ws, size_t ws_bytes,
+                                  void* stream) {
   if (count < 0 || !sums || (count > 0 && !xyz)) return fail(O3DX_EINVAL, "o3dx_plane_moments: bad args");
-  if (!ws || ws_bytes < 8192 + kMomBlocks * 6 * sizeof(double)) return fail(O3DX_ENOMEM, "moments workspace too small");
+  if (!ws || ws_bytes < o3dx_plane_moments_workspace_bytes(count))
+    return fail(O3DX_ENOMEM, "moments workspace too small");
+  hipStream_t s = as_stream(stream);
   Arena ar(ws, ws_bytes);
-  double* part = ar.take<double>(kMomBlocks * 6);
-  double* outd = ar.take<double>(8);
+  int64_t* part = ar.take<int64_t>((size_t)mom_blocks(std::max<int64_t>(count, 1)) * 12);
+  int64_t* outd = ar.take<int64_t>(16);
+  double A = 0.0;
+  if (absmax) {
+    A = std::max(absmax[0], std::max(absmax[1], absmax[2]));
+  } else if (count > 0) {  // the selected points' own bound
+    unsigned int* u = reinterpret_cast<unsigned int*>(outd);
+    O3DX_HIP(hipMemsetAsync(u, 0, 4 * sizeof(unsigned int), s));
+    hipLaunchKernelGGL(k_absmax_sel, dim3(grid_for(count, kBlock, 1024)), dim3(kBlock), 0, s, xyz, idx, count, u);
+    unsigned int b[4];
+    O3DX_TRY(read_back(b, u, sizeof(b), s));
+    for (int c = 0; c < 3; ++c) {
+      float f;
+      std::memcpy(&f, &b[c], 4);
+      A = std::max(A, (double)f);
+    }
+  }
   double tmp[6];
-  O3DX_TRY(run_moments(xyz, idx, count, centroid, part, outd, as_stream(stream), tmp));
+  O3DX_TRY(run_moments(xyz, idx, count, centroid, A, part, outd, s, tmp, fx_out));
   std::memcpy(sums, tmp, (centroid ? 6 : 3) * sizeof(double));
   return 0;
 }
@@ -1156,10 +1260,15 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
       plane_from_pts(P.data(), ransac_n, &planes[(size_t)4 * h]);
     }
   }
+  // |x|,|y|,|z| bounds of the cloud: the count's float32 window and the fx
+  // quantum of the refit moments (a sharded driver passes the global ones)
+  double absmax[3];
+  O3DX_TRY(absmax_of(xyz, n, w.aabb, w.mm, s, absmax));
+  const double A = std::max(absmax[0], std::max(absmax[1], absmax[2]));
   int best = -1;
   if (H > 0) {
     std::vector<int64_t> counts;
-    O3DX_TRY(run_count(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts));
+    O3DX_TRY(run_count(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax));
     std::vector<int32_t> tied = tied_hypotheses(counts, planes.data(), n, ransac_n, probability);
     std::vector<double> sums(H, std::numeric_limits<double>::quiet_NaN());
     if (!tied.empty()) {
@@ -1185,9 +1294,9 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     return 0;
   }
   double s1[6], s2[6], c[3];
-  O3DX_TRY(run_moments(xyz, inliers_out, k, nullptr, w.mom_part, w.mom_out, s, s1));
+  O3DX_TRY(run_moments(xyz, inliers_out, k, nullptr, A, w.mom_part, w.mom_out, s, s1));
   for (int a = 0; a < 3; ++a) c[a] = s1[a] / (double)k;
-  O3DX_TRY(run_moments(xyz, inliers_out, k, c, w.mom_part, w.mom_out, s, s2));
+  O3DX_TRY(run_moments(xyz, inliers_out, k, c, A, w.mom_part, w.mom_out, s, s2));
   plane_from_centred(c, s2, plane_host);
   return 0;
 }

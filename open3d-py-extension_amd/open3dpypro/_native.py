@@ -34,6 +34,7 @@ _SZ = ctypes.c_size_t
 _SIGS = {
     "o3dx_abi_version": (_I32, []),
     "o3dx_last_error": (ctypes.c_char_p, []),
+    "o3dx_fx_to_double": (_I32, [_P, _I64, _P]),
     "o3dx_set_kernel_timing": (None, [_I32]),
     "o3dx_reset_kernel_timing": (None, []),
     "o3dx_kernel_timing_filter": (None, [ctypes.c_char_p]),
@@ -45,6 +46,7 @@ _SIGS = {
     "o3dx_libm_probe": (_I32, [_P, _I64, _I32, _P, _P]),
     "o3dx_aabb_workspace_bytes": (_SZ, [_I64]),
     "o3dx_aabb": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
+    "o3dx_aabb_device": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
     "o3dx_voxel_workspace_bytes": (_SZ, [_I64]),
     "o3dx_voxel_down_sample": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_voxel_grid_cells": (_I64, [_I64, _P, _P, _D]),
@@ -65,26 +67,30 @@ _SIGS = {
     "o3dx_segment_plane_workspace_bytes": (_SZ, [_I64, _I32]),
     "o3dx_segment_plane": (_I32, [_P, _I64, _D, _I32, _I32, _D, _P, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_from_points": (_I32, [_P, _I32, _P]),
+    "o3dx_planes_from_samples": (_I32, [_P, _I32, _I32, _P]),
     "o3dx_plane_count_workspace_bytes": (_SZ, [_I64, _I32]),
     "o3dx_plane_count": (_I32, [_P, _I64, _P, _I32, _D, _P, _P, _SZ, _P]),
-    "o3dx_plane_abs_sum": (_I32, [_P, _I64, _P, _P, _I32, _D, _P, _P, _SZ, _P]),
+    "o3dx_plane_abs_sum": (_I32, [_P, _I64, _P, _P, _I32, _D, _P, _P, _P, _SZ, _P]),
+    "o3dx_ransac_tied": (_I32, [_P, _P, _I32, _I64, _I32, _D, _P, _P]),
     "o3dx_ransac_select": (_I32, [_P, _P, _P, _I32, _I64, _I32, _D]),
     "o3dx_plane_inliers": (_I32, [_P, _I64, _P, _D, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_select_workspace_bytes": (_SZ, [_I64]),
     "o3dx_plane_select": (_I32, [_P, _I64, _P, _I32, _D, _D, _I32, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_select_f64": (_I32, [_P, _I64, _P, _I32, _D, _D, _I32, _P, _P, _P, _P, _SZ, _P]),
-    "o3dx_plane_moments": (_I32, [_P, _P, _I64, _P, _P, _P, _SZ, _P]),
+    "o3dx_plane_moments_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_plane_moments": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_from_moments": (_I32, [_P, _I64, _P, _P]),
     "o3dx_icp_target_workspace_bytes": (_SZ, [_I64]),
     "o3dx_icp_target_build": (_I32, [_P, _P, _I64, _D, _P, _SZ, _P, _P]),
     "o3dx_icp_accumulate_workspace_bytes": (_SZ, [_I64]),
-    "o3dx_icp_accumulate": (_I32, [_P, _I64, _I32, _P, _P, _P, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_icp_accumulate": (_I32, [_P, _I64, _I32, _P, _P, _P, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_spatial_sort_workspace_bytes": (_SZ, [_I64]),
     "o3dx_spatial_sort": (_I32, [_P, _I64, _D, _P, _P, _SZ, _P]),
     "o3dx_pcd_unpack": (_I32, [_P, _I64, _I32, _P, _P, _P, _P, _P, _P]),
     "o3dx_lzf_decompress": (_I64, [_P, _I64, _P, _I64]),
     "o3dx_registration_icp_workspace_bytes": (_SZ, [_I64]),
     "o3dx_icp_solve_point_to_plane": (_I32, [_P, _P]),
+    "o3dx_icp_update": (_I32, [_P, _P]),
     "o3dx_registration_icp_point_to_plane": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,
                                                      _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
 }

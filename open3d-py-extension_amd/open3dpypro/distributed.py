@@ -4,17 +4,25 @@
 The path shards by space with no data-path collective except where the
 algorithm itself exchanges:
 
-  * AABB: a 6-value min/max all-reduce (`global_aabb`);
+  * AABB: a 6-value min/max all-reduce (`global_aabb`, `global_bounds_device`);
   * voxel slabs: x-slabs aligned to the global voxel grid, so every voxel
     (and its representative) belongs to exactly one rank (`slab_bounds`,
     `slab_of`);
-  * RANSAC: per-hypothesis integer counts, summed exactly (`allreduce_counts`);
-  * ICP: the 29 float64 moments per iteration, all-gathered and summed in
-    rank order, so every rank solves the same 6x6 system to the same bits
-    (`allreduce_icp_sums`, `registration_icp_point_to_plane`);
-  * voxel + normals of one cloud over x-slabs (C4): points to their slab
-    owner, then one halo exchange of the representatives near each slab face
-    (`voxel_normals_slabs`).
+  * voxel + normals of one cloud over x-slabs (C4): one halo exchange of the
+    representatives near each slab face (`voxel_normals_slabs`);
+  * RANSAC with the points sharded (`segment_plane_sharded`): the sampled
+    points' coordinates (bit patterns, summed exactly), per-hypothesis
+    integer counts, the tie sums and the refit moments as exact "fx" sums
+    (`allreduce_fx`);
+  * ICP with the source sharded and the target replicated
+    (`registration_icp_sharded`): the 29 moments per iteration as fx sums;
+  * C5, the whole chain voxel -> normals -> RANSAC -> ICP over the ranks
+    (`pipeline_sharded`).
+
+Every float sum that crosses ranks is an fx sum (libo3dx: each term rounded
+to an integer multiple of a power of two every rank derives alike, the
+integers added), so results are the same bits for any number of GPUs —
+including one: the single-GPU library calls use the same sums.
 
 Every function takes an optional process group; with no initialised process
 group they degrade to the single-process identity.
@@ -30,6 +38,8 @@ import torch.distributed as dist
 
 from . import _native as N
 
+_I64_MAX = (1 << 63) - 1
+
 
 def _world(group=None) -> Tuple[int, int]:
     if not (dist.is_available() and dist.is_initialized()):
@@ -44,6 +54,7 @@ def _comm_device(group=None) -> torch.device:
     return torch.device("cpu")
 
 
+# ------------------------------------------------------------ small collectives
 def global_aabb(local_min, local_max, group=None) -> Tuple[np.ndarray, np.ndarray]:
     """Global (min_bound, max_bound) from every rank's local bounds (f64).
     A rank with no points passes +inf / -inf."""
@@ -54,6 +65,36 @@ def global_aabb(local_min, local_max, group=None) -> Tuple[np.ndarray, np.ndarra
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
         v = t.cpu().numpy()
     return v[:3].copy(), -v[3:].copy()
+
+
+def global_bounds_device(xyz: torch.Tensor, group=None) -> Tuple[np.ndarray, np.ndarray]:
+    """Global (min_bound, max_bound) of a cloud spread over the ranks: the
+    device AABB of this rank's points (o3dx_aabb_device, no host wait), one
+    all-reduce, one host read.  +inf / -inf when every rank is empty."""
+    from . import ops
+
+    world, _ = _world(group)
+    if xyz.shape[0] > 0:
+        mm = ops.aabb_device(xyz)
+        v = torch.cat([mm[:3], -mm[3:]])
+    else:
+        v = torch.full((6,), math.inf, dtype=torch.float64, device=xyz.device)
+    if world > 1:
+        v = v.to(_comm_device(group))
+        dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
+    h = v.cpu().numpy()
+    return h[:3].copy(), -h[3:].copy()
+
+
+def allreduce_max(v, group=None) -> np.ndarray:
+    """Element-wise max over the ranks of a small float64 vector (exact)."""
+    world, _ = _world(group)
+    a = np.asarray(v, np.float64).copy()
+    if world > 1:
+        t = torch.from_numpy(a).to(_comm_device(group))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        a = t.cpu().numpy()
+    return a
 
 
 def slab_bounds(min_bound, max_bound, voxel_size: float, world: int):
@@ -87,9 +128,25 @@ def allreduce_counts(counts: np.ndarray, group=None) -> np.ndarray:
     return np.where(c < 0, -1, out)
 
 
+def allreduce_fx(fx, group=None) -> np.ndarray:
+    """Sum over the ranks of fx sums ((k, 4) int64 rows {lo, hi, q, 0}, from
+    libo3dx): the integer digits add exactly (int64 all-reduce), the exponent
+    q is the same on every rank by construction.  The value of a row is
+    (hi * 2^32 + lo) * 2^q; convert with ops.fx_to_double."""
+    world, _ = _world(group)
+    f = np.array(fx, np.int64).reshape(-1, 4)
+    if world > 1:
+        t = torch.from_numpy(np.ascontiguousarray(f[:, :2])).to(_comm_device(group))
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        f[:, :2] = t.cpu().numpy()
+    return f
+
+
 def allreduce_icp_sums(sums: np.ndarray, group=None) -> np.ndarray:
-    """Sum of every rank's ICP moment vector (float64, N.ICP_NSUMS), gathered and
-    added in rank order so that all ranks hold identical bits."""
+    """Sum of every rank's float64 ICP moment vector (N.ICP_NSUMS), gathered
+    and added in rank order so that all ranks hold identical bits (for
+    accumulate functions that return plain float64 sums; the library's own
+    return fx sums, which need no ordering)."""
     world, _ = _world(group)
     s = np.asarray(sums, np.float64)
     if world == 1:
@@ -104,16 +161,128 @@ def allreduce_icp_sums(sums: np.ndarray, group=None) -> np.ndarray:
     return acc
 
 
+def _allreduce_int(v: int, group=None) -> int:
+    world, _ = _world(group)
+    if world == 1:
+        return int(v)
+    t = torch.tensor([int(v)], dtype=torch.int64, device=_comm_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return int(t.item())
+
+
+def shard_range(n: int, world: int, rank: int, align: int = 1) -> Tuple[int, int]:
+    """Contiguous [a, b) share of n items for `rank` (boundaries multiples of `align`)."""
+    per = -(-n // world)
+    per = -(-per // align) * align
+    a = min(n, rank * per)
+    return a, min(n, a + per)
+
+
+def _all_gather_rows(t: torch.Tensor, counts, group=None) -> torch.Tensor:
+    """Concatenation in rank order of every rank's rows of `t` (row counts known
+    on every rank): padded all_gather on the collective's device."""
+    world, _ = _world(group)
+    if world == 1:
+        return t
+    cd = _comm_device(group)
+    cap = max(int(max(counts)), 1)
+    buf = torch.zeros((cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=cd)
+    buf[: t.shape[0]] = t.to(cd)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return torch.cat([p[: int(c)] for p, c in zip(parts, counts)]).to(t.device)
+
+
+def global_positions(g: torch.Tensor, group=None) -> Tuple[torch.Tensor, int]:
+    """Positions of this rank's items in the union over the ranks ordered by
+    global index (`g`: ascending on every rank, distinct across ranks) — the
+    row numbers the single-GPU call gives the same items — and the union's
+    size.  When every rank's indices lie above the previous rank's (a
+    spatially tiled dataset) the positions are prefix sums of the counts
+    (one 3-value all-gather); otherwise the indices are all-gathered."""
+    world, rank = _world(group)
+    n = int(g.numel())
+    if world == 1:
+        return torch.arange(n, dtype=torch.int64, device=g.device), n
+    lo = g[:1].long() if n else torch.full((1,), _I64_MAX, dtype=torch.int64, device=g.device)
+    hi = g[-1:].long() if n else torch.full((1,), -1, dtype=torch.int64, device=g.device)
+    info = torch.cat([torch.full((1,), n, dtype=torch.int64, device=g.device), lo, hi]).to(_comm_device(group))
+    parts = [torch.empty_like(info) for _ in range(world)]
+    dist.all_gather(parts, info, group=group)
+    tab = torch.stack(parts).cpu().numpy()
+    counts = tab[:, 0]
+    total = int(counts.sum())
+    ranges = [(int(a), int(b)) for c, a, b in tab if c > 0]
+    if all(ranges[i][1] < ranges[i + 1][0] for i in range(len(ranges) - 1)):
+        off = int(counts[:rank].sum())
+        return torch.arange(off, off + n, dtype=torch.int64, device=g.device), total
+    allg, _ = torch.sort(_all_gather_rows(g.long(), counts, group))
+    return torch.searchsorted(allg, g.long()), total
+
+
+# ------------------------------------------------------------------ compute
+class _HipBackend:
+    """Per-rank compute of the sharded drivers: the HIP kernels (ops).  The
+    CPU tests substitute the oracle (tests/test_distributed.py)."""
+
+    def absmax(self, x):
+        from . import ops
+        return ops.absmax(x)
+
+    def rows_f64(self, x, idx):
+        return x[idx].double()
+
+    def plane_count(self, x, planes, thr):
+        from . import ops
+        return ops.plane_count(x, planes, thr)
+
+    def abs_sum_fx(self, x, planes, which, thr):
+        from . import ops
+        return ops.plane_abs_sum(x, planes, which, thr, return_fx=True)[1]
+
+    def plane_inliers(self, x, plane, thr):
+        from . import ops
+        return ops.plane_inliers(x, plane, thr).long()
+
+    def moments_fx(self, x, idx, centroid, absmax):
+        from . import ops
+        return ops.plane_moments(x, idx, centroid, absmax=absmax, return_fx=True)[1]
+
+    def icp_target(self, tgt, tn, max_corr):
+        from . import ops
+        return ops.ICPTarget(tgt, tn, max_corr)
+
+    def icp_source(self, src):
+        from . import ops
+        return ops.spatial_sort(src)
+
+    def icp_accumulate_fx(self, target, src, T, absmax):
+        return target.accumulate(src, T, absmax=absmax, return_fx=True)[2]
+
+
+_HIP = _HipBackend()
+
+
 def registration_icp_point_to_plane(accumulate: Callable[[np.ndarray], np.ndarray], n_source_total: int,
                                     init=None, max_iteration: int = 30, relative_fitness: float = 1e-6,
                                     relative_rmse: float = 1e-6, group=None):
     """Open3D registration_icp (point-to-plane) with the source sharded over
-    ranks and the target replicated.  `accumulate(T) -> sums` computes this
-    rank's moments (e.g. `ops.ICPTarget.accumulate(src_shard, T)[0]`); the
-    loop mirrors o3dx_registration_icp_point_to_plane with the moments
-    all-reduced once per iteration.  Returns (T, fitness, inlier_rmse)."""
+    ranks and the target replicated.  `accumulate(T)` computes this rank's
+    moments: fx rows ((32, 4) int64, e.g. ops.ICPTarget.accumulate(...,
+    return_fx=True)[2]) — summed exactly over the ranks, so T is the
+    single-GPU o3dx_registration_icp_point_to_plane's to the bit — or plain
+    float64 sums (summed in rank order).  The loop, the update T <- upd * T
+    (ops.icp_update, the library's own float64 order) and the convergence
+    test mirror the library's.  Returns (T, fitness, inlier_rmse)."""
+    from . import ops
+
     T = np.eye(4) if init is None else np.array(init, np.float64).reshape(4, 4)
-    solve = N.load().o3dx_icp_solve_point_to_plane
+
+    def reduce(v):
+        v = np.asarray(v)
+        if v.dtype == np.int64 and v.ndim == 2:
+            return ops.fx_to_double(allreduce_fx(v, group))
+        return allreduce_icp_sums(v, group)
 
     def metrics(sm):
         c = sm[28]
@@ -121,21 +290,102 @@ def registration_icp_point_to_plane(accumulate: Callable[[np.ndarray], np.ndarra
             return 0.0, 0.0
         return c / n_source_total, math.sqrt(sm[29] / c)
 
-    sums = allreduce_icp_sums(accumulate(T), group)
+    sums = reduce(accumulate(T))
     fit, rm = metrics(sums)
     for _ in range(max_iteration):
-        upd = np.zeros((4, 4), np.float64)
-        solve(np.ascontiguousarray(sums).ctypes.data_as(N.ctypes.c_void_p),
-              upd.ctypes.data_as(N.ctypes.c_void_p))
-        T = upd @ T
+        T = ops.icp_update(sums, T)
         pf, pr = fit, rm
-        sums = allreduce_icp_sums(accumulate(T), group)
+        sums = reduce(accumulate(T))
         fit, rm = metrics(sums)
         if abs(pf - fit) < relative_fitness and abs(pr - rm) < relative_rmse:
             break
     return T, fit, rm
 
 
+def registration_icp_sharded(src: torch.Tensor, target, init=None, max_iteration: int = 30,
+                             relative_fitness: float = 1e-6, relative_rmse: float = 1e-6, group=None,
+                             backend=None, n_source_total: Optional[int] = None):
+    """Point-to-plane ICP of a source spread over the ranks (this rank's (n,3)
+    float32 share) onto a replicated target (`backend.icp_target(...)`, e.g.
+    ops.ICPTarget): the fx quanta come from the GLOBAL source bounds, so T,
+    fitness and rmse equal ops.registration_icp on the whole source to the
+    bit.  Returns (T, fitness, inlier_rmse)."""
+    be = backend or _HIP
+    am = allreduce_max(be.absmax(src) if src.shape[0] else np.zeros(3), group)
+    n_total = _allreduce_int(src.shape[0], group) if n_source_total is None else int(n_source_total)
+    s = be.icp_source(src)
+    return registration_icp_point_to_plane(lambda T: be.icp_accumulate_fx(target, s, T, am), n_total, init,
+                                           max_iteration, relative_fitness, relative_rmse, group)
+
+
+def segment_plane_sharded(x: torch.Tensor, pos: torch.Tensor, n_total: int, distance_threshold: float,
+                          ransac_n: int = 3, num_iterations: int = 1000, probability: float = 0.99999999,
+                          samples: Optional[np.ndarray] = None, seed: int = 0, absmax=None, group=None,
+                          backend=None):
+    """Open3D SegmentPlane of a cloud whose rows are spread over the ranks:
+    this rank holds the rows `pos` (ascending positions in the global row
+    order) as `x` (n,3) float32.  The hypotheses are the replicated sample
+    list (RandomSampler over n_total, or `samples`); each rank contributes the
+    sampled rows it holds (bit patterns, summed: exact), counts its rows
+    (integer sums), the Sigma|d| of the tie-relevant hypotheses and the refit
+    moments as fx sums under the GLOBAL coordinate bounds (`absmax`).  Every
+    rank then replays the same selection, so the plane and the inlier set are
+    o3dx_segment_plane's on the whole cloud to the bit.  Returns (plane
+    float64[4], this rank's inlier rows as local indices (device int64))."""
+    from . import ops
+
+    be = backend or _HIP
+    if not (0.0 < probability <= 1.0):
+        raise RuntimeError("Probability must be > 0 or <= 1.0")
+    if ransac_n < 3:
+        raise RuntimeError("ransac_n should be set to higher than or equal to 3.")
+    if n_total < ransac_n:
+        raise RuntimeError("There must be at least 'ransac_n' points.")
+    world, _ = _world(group)
+    H = int(num_iterations)
+    if samples is None:
+        samples = ops.ransac_samples(n_total, ransac_n, H, seed)
+    samples = np.asarray(samples, np.int64).reshape(H, ransac_n)
+    if absmax is None:
+        absmax = allreduce_max(be.absmax(x) if x.shape[0] else np.zeros(3), group)
+    empty = torch.zeros(0, dtype=torch.int64, device=x.device)
+    if H == 0:
+        return np.zeros(4), empty
+    # 1. the sampled rows' coordinates: the owner contributes the float64 bits
+    flat = torch.as_tensor(samples.reshape(-1), device=pos.device)
+    if pos.numel():
+        j = torch.searchsorted(pos, flat).clamp_max(pos.numel() - 1)
+        own = pos[j] == flat
+        bits = be.rows_f64(x, j).contiguous().view(torch.int64)
+        bits = torch.where(own[:, None], bits, torch.zeros_like(bits))
+    else:
+        bits = torch.zeros((flat.numel(), 3), dtype=torch.int64, device=pos.device)
+    if world > 1:
+        bits = bits.to(_comm_device(group))
+        dist.all_reduce(bits, op=dist.ReduceOp.SUM, group=group)
+    coords = bits.cpu().numpy().view(np.float64).reshape(H, ransac_n, 3)
+    planes = ops.planes_from_samples(coords, ransac_n)
+    # 2. per-hypothesis counts, 3. tie sums, selection replay
+    counts = allreduce_counts(be.plane_count(x, planes, distance_threshold), group)
+    tied = ops.ransac_tied(counts, planes, n_total, ransac_n, probability)
+    sums = np.full(H, np.nan)
+    if len(tied):
+        sums[tied] = ops.fx_to_double(allreduce_fx(be.abs_sum_fx(x, planes, tied, distance_threshold), group))
+    best = ops.ransac_select(counts, sums, planes, n_total, ransac_n, probability)
+    if best < 0 or not planes[best].any():
+        return np.zeros(4), empty
+    # 4. final inliers (local rows), 5. GetPlaneFromPoints refit over all ranks' inliers
+    inl = be.plane_inliers(x, planes[best], distance_threshold)
+    k_total = _allreduce_int(inl.numel(), group)
+    if k_total == 0:
+        return np.zeros(4), inl
+    s1 = ops.fx_to_double(allreduce_fx(be.moments_fx(x, inl, None, absmax), group))
+    c = s1 / float(k_total)
+    s2 = ops.fx_to_double(allreduce_fx(be.moments_fx(x, inl, c, absmax), group))
+    return ops.plane_from_moments(s1, k_total, s2), inl
+
+
+# ------------------------------------------------------------- C4: x-slabs
 def _exchange(dest: torch.Tensor, world: int, group, *tensors):
     """all_to_all of the rows of each tensor to rank dest[i] (rows keep their
     relative order per source rank; sources are concatenated in rank order)."""
@@ -181,8 +431,8 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
 
     presorted: the caller guarantees every point already lies in this rank's
     slab and the rows are in ascending global index (a spatially tiled
-    dataset): the point all-to-all is skipped (a point outside the slab makes
-    the voxel call fail loudly)."""
+    dataset): the point all-to-all is skipped; a point outside the slab is an
+    error (RuntimeError on every rank)."""
     from . import ops
 
     if voxel_fn is None and normals_fn is None and xyz.is_cuda:
@@ -194,25 +444,7 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
     if normals_fn is None:
         def normals_fn(p, k):
             return ops.estimate_normals(p, knn=k, return_kdist=True)
-    # 1. global bounds (a rank with no points contributes nothing)
-    if xyz.shape[0] > 0:
-        lmn = xyz.double().min(0).values.cpu().numpy()
-        lmx = xyz.double().max(0).values.cpu().numpy()
-    else:
-        lmn, lmx = np.full(3, np.inf), np.full(3, -np.inf)
-    mn, mx = global_aabb(lmn, lmx, group)
-    # 2. points to their slab owner, then into global-index order
-    keys = slab_bounds(mn, mx, voxel_size, world)
-    kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / voxel_size).to(torch.int64)
-    inner = torch.tensor(keys[1:-1], dtype=torch.int64, device=xyz.device)
-    owner = torch.searchsorted(inner, kx, right=True)
-    if world > 1:
-        xyz, gidx = _exchange(owner, world, group, xyz, gidx)
-    o = torch.argsort(gidx)
-    xyz, gidx = xyz[o].contiguous(), gidx[o].contiguous()
-    # 3. local reps with the global bounds
-    rep = voxel_fn(xyz, voxel_size, mn, mx)
-    rxyz, rg = xyz[rep].contiguous(), gidx[rep].contiguous()
+    rg, rxyz, mn, mx, keys = _slab_reps_generic(xyz, gidx, voxel_size, group, voxel_fn, presorted)
     x_lo = float(mn[0]) + keys[rank] * voxel_size
     x_hi = float(mn[0]) + keys[rank + 1] * voxel_size
     t_lo = rxyz[:, 0].double() - x_lo  # distance to the slab faces
@@ -259,116 +491,278 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
     return rg, rxyz, nrm[own]
 
 
-def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted):
-    """The HIP form of voxel_normals_slabs: every rank keeps a voxel table of
-    its slab widened by the halo (global keys, x-key window), so the normals
-    run straight off the table (k_normals_stile) on own + halo reps; the halo
-    is a whole number of voxel layers.  Same contract and halo proof."""
-    from . import ops
-
+def _slab_reps_generic(xyz, gidx, voxel_size, group, voxel_fn, presorted):
+    """Global bounds, points to their slab owner, the slab's voxel reps with
+    the global bounds (any per-rank compute: `voxel_fn(p, vs, mn, mx)` ->
+    rep rows).  Returns (rep gidx ascending, rep xyz, mn, mx, slab keys)."""
     world, rank = _world(group)
-    vs = float(voxel_size)
-    # 1. global bounds
     if xyz.shape[0] > 0:
-        lmn, lmx = ops.aabb(xyz)
+        lmn = xyz.double().min(0).values.cpu().numpy()
+        lmx = xyz.double().max(0).values.cpu().numpy()
     else:
         lmn, lmx = np.full(3, np.inf), np.full(3, -np.inf)
     mn, mx = global_aabb(lmn, lmx, group)
+    keys = slab_bounds(mn, mx, voxel_size, world)
+    kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / voxel_size).to(torch.int64)
+    if world > 1 and not presorted:
+        inner = torch.tensor(keys[1:-1], dtype=torch.int64, device=xyz.device)
+        xyz, gidx = _exchange(torch.searchsorted(inner, kx, right=True), world, group, xyz, gidx)
+        o = torch.argsort(gidx)
+        xyz, gidx = xyz[o].contiguous(), gidx[o].contiguous()
+    elif presorted and xyz.shape[0] and bool(((kx < keys[rank]) | (kx >= keys[rank + 1])).any()):
+        raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside this rank's slab")
+    rep = voxel_fn(xyz, voxel_size, mn, mx)
+    return gidx[rep].contiguous(), xyz[rep].contiguous(), mn, mx, keys
+
+
+def _slab_reps_device(xyz, gidx, vs, group, presorted):
+    """HIP form of the slab voxel step: global bounds on the device (one
+    all-reduce, one read), points to their slab owner unless presorted, the
+    slab's reps with GLOBAL keys (a dense x-key window table when the slab is
+    not sparse — the library's dense rule, 2n + 2^20 cells — else the hash
+    path).  Returns (rep gidx ascending, rep xyz, mn, mx, keys, dims, bad)
+    where `bad` is a device count of points outside the slab (sparse
+    presorted path; the dense window call fails loudly by itself) or None."""
+    from . import ops
+
+    world, rank = _world(group)
+    mn, mx = global_bounds_device(xyz, group)
+    if not np.all(np.isfinite(mn)):
+        raise RuntimeError("voxel_normals_slabs: the cloud is empty on every rank")
     keys = slab_bounds(mn, mx, vs, world)
-    k_lo, k_hi, nkeys = keys[rank], keys[rank + 1], keys[-1]
-    # 2. points to their slab owner (unless the input is already tiled)
+    k_lo, k_hi = keys[rank], keys[rank + 1]
     if world > 1 and not presorted:
         kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
         inner = torch.tensor(keys[1:-1], dtype=torch.int64, device=xyz.device)
         xyz, gidx = _exchange(torch.searchsorted(inner, kx, right=True), world, group, xyz, gidx)
         o = torch.argsort(gidx)
         xyz, gidx = xyz[o].contiguous(), gidx[o].contiguous()
-    # 3. own reps: keys of the global grid, the slab's x keys only (a dense
-    # window table when the slab is not sparse — the same rule as the
-    # library's dense voxel table, 2n + 2^20 cells — else the hash path)
     dims = np.floor(np.maximum(np.asarray(mx) - np.asarray(mn), 0.0) / vs) + 1
     layer = int(dims[1] * dims[2])
     n_loc = int(xyz.shape[0])
-    dense = (k_hi - k_lo + 6) * layer <= 2 * n_loc + (1 << 20)
+    bad = None
     if k_hi > k_lo and n_loc > 0:
-        if dense:
+        if (k_hi - k_lo + 6) * layer <= 2 * n_loc + (1 << 20):
             out = ops.voxel_down_sample_window(xyz, vs, mn, mx, k_lo, k_hi)
         else:
             out = ops.voxel_down_sample(xyz, vs, mn, mx)
-        rep = out["rep_idx"].long()
-        rxyz, rg = out["rep_xyz"], gidx[rep].contiguous()
+            if presorted and world > 1:
+                kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+                bad = ((kx < k_lo) | (kx >= k_hi)).sum()
+        rxyz, rg = out["rep_xyz"], gidx[out["rep_idx"].long()].contiguous()
     else:
         rxyz, rg = xyz[:0], gidx[:0]
+        if n_loc > 0:
+            bad = torch.full((), n_loc, dtype=torch.int64, device=xyz.device)
+    return rg, rxyz, mn, mx, keys, dims, bad
+
+
+def voxel_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float, group=None, presorted: bool = False):
+    """voxel_down_sample of one cloud spread over the ranks (the slab voxel
+    step of voxel_normals_slabs, without the normals): this rank's (rep
+    global indices ascending, rep xyz); the union over ranks is the
+    single-GPU result with the cloud's global bounds."""
+    rg, rxyz, _, _, _, _, bad = _slab_reps_device(xyz, gidx, float(voxel_size), group, presorted)
+    nbad = torch.zeros((), dtype=torch.int64, device=xyz.device) if bad is None else bad
+    if _allreduce_int(int(nbad.item()), group):
+        raise RuntimeError("voxel_slabs(presorted=True): a point lies outside its rank's slab")
+    return rg, rxyz
+
+
+def _two_part_rows(mask_a: torch.Tensor, mask_b: torch.Tensor):
+    """Rows of mask_a then rows of mask_b (each ascending; a row may be in
+    both) as one index buffer, with the counts — on the device, no host wait."""
+    n = mask_a.numel()
+    na = mask_a.sum()
+    ia = torch.cumsum(mask_a, 0) - 1
+    ib = torch.cumsum(mask_b, 0) - 1 + na
+    rows = torch.arange(n, device=mask_a.device)
+    buf = torch.zeros(2 * n + 1, dtype=torch.int64, device=mask_a.device)
+    buf.scatter_(0, torch.where(mask_a, ia, torch.full_like(ia, 2 * n)), rows)
+    buf.scatter_(0, torch.where(mask_b, ib, torch.full_like(ib, 2 * n)), rows)
+    return buf, torch.stack([na, mask_b.sum()])
+
+
+def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted):
+    """The HIP form of voxel_normals_slabs: every rank keeps a voxel table of
+    its slab widened by the halo (global keys, x-key window), so the normals
+    run straight off the table (k_normals_stile) on own + halo reps; the halo
+    is a whole number of voxel layers.  Same contract and halo proof.
+
+    Host waits per step: the bounds (after a device all-reduce), the rep
+    count, per halo round the halo counts (one all-to-all of two counts), the
+    table's occupancy and the verdict (one all-gather of four values).  The
+    halo rows travel as one packed (x, y, z, gidx bits) payload all-to-all,
+    and the union is merged by position (searchsorted) instead of sorted."""
+    from . import ops
+
+    world, rank = _world(group)
+    vs = float(voxel_size)
+    rg, rxyz, mn, mx, keys, dims, bad = _slab_reps_device(xyz, gidx, vs, group, presorted)
+    k_lo, k_hi, nkeys = keys[rank], keys[rank + 1], keys[-1]
+    layer = int(dims[1] * dims[2])
+    dev = rxyz.device
+    n_own = int(rg.numel())  # global indices travel as int32 bits (< 2^31, Open3D's int point ids)
     kxr = torch.floor((rxyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
     x_lo, x_hi = float(mn[0]) + k_lo * vs, float(mn[0]) + k_hi * vs
-    inf = torch.full((rxyz.shape[0],), np.inf, dtype=torch.float64, device=rxyz.device)
+    inf = torch.full((n_own,), np.inf, dtype=torch.float64, device=dev)
     t = torch.minimum(rxyz[:, 0].double() - x_lo if rank > 0 else inf,
                       x_hi - rxyz[:, 0].double() if rank < world - 1 else inf)
     hk = max(1, int(math.ceil(float(halo) / vs))) if halo else 3
     min_keys = min(keys[r + 1] - keys[r] for r in range(world))
-    n_total = _allreduce_int(rg.numel(), group)
+    packed = torch.cat([rxyz, rg.to(torch.int32).view(torch.float32)[:, None]], 1) if world > 1 else None
+    nbad = torch.zeros((), dtype=torch.int64, device=dev) if bad is None else bad.to(torch.int64)
+    cd = _comm_device(group)
     table = None
     while True:
         if world > 1 and hk >= min_keys:
             raise RuntimeError("voxel_normals_slabs: the kNN halo is wider than a slab; use fewer ranks")
-        # 4. halo: the own reps of the hk voxel layers next to each interior face
+        # halo: the own reps of the hk voxel layers next to each interior face
         if world > 1:
-            send_lo = (kxr < k_lo + hk) & (rank > 0)
-            send_hi = (kxr >= k_hi - hk) & (rank < world - 1)
-            dest = torch.cat([torch.full((int(send_lo.sum()),), rank - 1, dtype=torch.int64, device=rxyz.device),
-                              torch.full((int(send_hi.sum()),), rank + 1, dtype=torch.int64, device=rxyz.device)])
-            hx, hg = _exchange(dest, world, group, torch.cat([rxyz[send_lo], rxyz[send_hi]]),
-                               torch.cat([rg[send_lo], rg[send_hi]]))
-            ux, ug = torch.cat([rxyz, hx]), torch.cat([rg, hg])
-            o = torch.argsort(ug)
-            ux, ug = ux[o].contiguous(), ug[o].contiguous()
-            own = torch.searchsorted(ug, rg)
+            zero = torch.zeros(n_own, dtype=torch.bool, device=dev)
+            send_lo = (kxr < k_lo + hk) if rank > 0 else zero
+            send_hi = (kxr >= k_hi - hk) if rank < world - 1 else zero
+            rows, cnt = _two_part_rows(send_lo, send_hi)
+            sc = torch.zeros(world, dtype=torch.int64, device=dev)
+            if rank > 0:
+                sc[rank - 1] = cnt[0]
+            if rank < world - 1:
+                sc[rank + 1] = cnt[1]
+            sc = sc.to(cd)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=group)
+            counts = torch.cat([sc, rc]).cpu()  # the one host wait of the exchange
+            ss, rs = counts[:world].tolist(), counts[world:].tolist()
+            send = packed[rows[: sum(ss)]].to(cd)
+            recv = torch.empty((sum(rs), 4), dtype=torch.float32, device=cd)
+            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=group)
+            recv = recv.to(dev)
+            na = rs[rank - 1] if rank > 0 else 0
+            ha, hb = recv[:na], recv[na:]
+            ga = ha[:, 3].contiguous().view(torch.int32).long()
+            gb = hb[:, 3].contiguous().view(torch.int32).long()
+            # merge by position: own, lower-neighbour and upper-neighbour rows are
+            # each ascending in global index
+            p_own = torch.arange(n_own, device=dev) + torch.searchsorted(ga, rg) + torch.searchsorted(gb, rg)
+            p_a = torch.arange(ga.numel(), device=dev) + torch.searchsorted(rg, ga) + torch.searchsorted(gb, ga)
+            p_b = torch.arange(gb.numel(), device=dev) + torch.searchsorted(rg, gb) + torch.searchsorted(ga, gb)
+            nu = n_own + ga.numel() + gb.numel()
+            ux = torch.empty((nu, 3), dtype=torch.float32, device=dev)
+            ux[p_own] = rxyz
+            ux[p_a] = ha[:, :3]
+            ux[p_b] = hb[:, :3]
+            own = p_own
         else:
-            ux, ug, own = rxyz, rg, None
-        # 5. the union's voxel table over the slab + halo window, normals off it
+            ux, own, nu = rxyz, None, n_own
+        # the union's voxel table over the slab + halo window, normals off it
         kx0, kx1 = max(k_lo - hk, 0), min(k_hi + hk, nkeys)
-        if ux.shape[0] > 0 and (kx1 - kx0) * layer <= 2 * int(ux.shape[0]) + (1 << 20):
+        if nu > 0 and (kx1 - kx0) * layer <= 2 * nu + (1 << 20):
             grid = ops.voxel_table(ux, vs, mn, mx, kx0, kx1, table)
             table = grid.pts
             nrm, kd2 = ops.estimate_normals(ux, knn=knn, voxel_grid=grid, return_kdist=True)
-        elif ux.shape[0] > 0:  # sparse slab: the normals sort the union into their own grid
+        elif nu > 0:  # sparse slab: the normals sort the union into their own grid
             nrm, kd2 = ops.estimate_normals(ux, knn=knn, return_kdist=True)
         else:
             nrm, kd2 = ux.new_zeros((0, 3)), ux.new_zeros((0,))
         if own is not None:
             nrm, kd2 = nrm[own], kd2[own]
-        # 6. verify every own rep: a missing point lies more than t + hk*vs away
-        ok = 1.0
-        if world > 1 and rg.numel():
-            if ux.shape[0] < min(knn, n_total):
-                ok = 0.0
-            else:
-                ok = 1.0 if bool((torch.sqrt(kd2.double()) < (t + hk * vs) * (1.0 - 1e-9)).all()) else 0.0
-        flag = torch.tensor([ok], dtype=torch.float64, device=_comm_device(group))
-        if world > 1:
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
-        if flag.item() == 1.0:
+        if world == 1:
+            if int(nbad.item()):
+                raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside this rank's slab")
+            break
+        # verdict of every rank in one all-gather: proof failures, own reps,
+        # union size, points outside the slab
+        fail = (torch.sqrt(kd2.double()) >= (t + hk * vs) * (1.0 - 1e-9)).any() if n_own else \
+            torch.zeros((), dtype=torch.bool, device=dev)
+        info = torch.zeros(4, dtype=torch.int64, device=dev)  # filled on the device: no host copies
+        info[0] = fail.to(torch.int64)
+        info[1].fill_(n_own)
+        info[2].fill_(nu)
+        info[3] = nbad
+        info = info.to(cd)
+        parts = [torch.empty_like(info) for _ in range(world)]
+        dist.all_gather(parts, info, group=group)
+        tab = torch.stack(parts).cpu().numpy()
+        if tab[:, 3].sum():
+            raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside its rank's slab")
+        n_total = int(tab[:, 1].sum())
+        short = any(r[1] > 0 and r[2] < min(knn, n_total) for r in tab)  # fewer than k points: unverifiable
+        if not tab[:, 0].any() and not short:
             break
         hk *= 2
     return rg, rxyz, nrm
 
 
-def _allreduce_int(v: int, group=None) -> int:
+# ----------------------------------------------------------------- C5 chain
+def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tensor, src_gidx: torch.Tensor,
+                     voxel_size: float, knn: int = 30, distance_threshold: float = 0.002, ransac_n: int = 3,
+                     num_iterations: int = 1000, seed: int = 7, max_correspondence_distance: float = 0.02,
+                     icp_iterations: int = 30, presorted: bool = False, group=None, timings: Optional[dict] = None):
+    """C5 over the ranks (BASELINE configs[4]; the reference's chain
+    test_pipeline.py:406-434 — VoxelDownsample -> normals -> PlaneDetection —
+    plus the north star's ICP, with each cloud's device placement per rank as
+    processors.py:206-207 places whole clouds):
+
+      1. target: slab voxel reps + KNN normals (voxel_normals_slabs, C4);
+      2. source: slab voxel reps with the source's global bounds (voxel_slabs);
+      3. segment_plane on the target reps (segment_plane_sharded; the
+         hypotheses sample the reps' global row order, RandomSampler(seed));
+      4. point-to-plane ICP of the source reps onto the target reps
+         (registration_icp_sharded: target reps + normals all-gathered in
+         global order, the source sharded, fx moments all-reduced per
+         iteration), icp_iterations iterations from T = I (relative criteria 0).
+
+    Every result equals the single-GPU chain (ops.voxel_down_sample ->
+    estimate_normals -> segment_plane -> registration_icp) bit for bit.
+    Returns a dict: target_rep_gidx / target_rep_xyz / target_normals (this
+    rank's), source_reps (global count), plane, plane_inlier_rows (global row
+    positions of this rank's inliers among the target reps), target_reps
+    (global count), transformation, fitness, inlier_rmse."""
+    import time
+
+    from . import ops
+
+    def mark(name, t0):
+        if timings is not None:
+            torch.cuda.synchronize()
+            timings[name] = round((time.perf_counter() - t0) * 1e3, 3)
+        return time.perf_counter()
+
+    t0 = time.perf_counter()
+    trg, trx, tn = voxel_normals_slabs(tgt, tgt_gidx, voxel_size, knn, group, presorted=presorted)
+    t0 = mark("voxel_normals_target", t0)
+    srg, srx = voxel_slabs(src, src_gidx, voxel_size, group, presorted=presorted)
+    t0 = mark("voxel_source", t0)
+    pos, mt = global_positions(trg, group)
+    am = allreduce_max(ops.absmax(trx) if trx.shape[0] else np.zeros(3), group)
+    samples = ops.ransac_samples(mt, ransac_n, num_iterations, seed)
+    plane, inl = segment_plane_sharded(trx, pos, mt, distance_threshold, ransac_n, num_iterations,
+                                       samples=samples, absmax=am, group=group)
+    t0 = mark("segment_plane", t0)
     world, _ = _world(group)
-    if world == 1:
-        return int(v)
-    t = torch.tensor([int(v)], dtype=torch.int64, device=_comm_device(group))
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return int(t.item())
+    if world > 1:
+        info = torch.full((1,), int(trx.shape[0]), dtype=torch.int64, device=_comm_device(group))
+        parts = [torch.empty_like(info) for _ in range(world)]
+        dist.all_gather(parts, info, group=group)
+        counts = [int(p.item()) for p in parts]
+        rows = torch.cat([trx, tn], 1)
+        allrows = _all_gather_rows(rows, counts, group)
+        allpos = _all_gather_rows(pos, counts, group)
+        full = torch.empty_like(allrows)
+        full[allpos] = allrows
+        t_all, n_all = full[:, :3].contiguous(), full[:, 3:].contiguous()
+    else:
+        t_all, n_all = trx, tn
+    target = ops.ICPTarget(t_all, n_all, max_correspondence_distance)
+    T, fit, rm = registration_icp_sharded(srx, target, max_iteration=icp_iterations, relative_fitness=0.0,
+                                          relative_rmse=0.0, group=group)
+    mark("icp", t0)
+    return {"target_rep_gidx": trg, "target_rep_xyz": trx, "target_normals": tn, "target_reps": mt,
+            "source_reps": _allreduce_int(srx.shape[0], group), "plane": plane, "plane_inlier_rows": pos[inl],
+            "transformation": T, "fitness": fit, "inlier_rmse": rm}
 
 
-def shard_range(n: int, world: int, rank: int, align: int = 1) -> Tuple[int, int]:
-    """Contiguous [a, b) share of n items for `rank` (boundaries multiples of `align`)."""
-    per = -(-n // world)
-    per = -(-per // align) * align
-    a = min(n, rank * per)
-    return a, min(n, a + per)
-
-
-__all__ = ["global_aabb", "slab_bounds", "slab_of", "allreduce_counts", "allreduce_icp_sums",
-           "registration_icp_point_to_plane", "voxel_normals_slabs", "shard_range"]
+__all__ = ["global_aabb", "global_bounds_device", "slab_bounds", "slab_of", "allreduce_counts", "allreduce_fx",
+           "allreduce_max", "allreduce_icp_sums", "registration_icp_point_to_plane", "registration_icp_sharded",
+           "segment_plane_sharded", "global_positions", "voxel_normals_slabs", "voxel_slabs", "pipeline_sharded",
+           "shard_range"]

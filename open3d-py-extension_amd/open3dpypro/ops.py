@@ -42,6 +42,18 @@ def aabb(xyz: torch.Tensor):
     return out[:3].copy(), out[3:].copy()
 
 
+def aabb_device(xyz: torch.Tensor) -> torch.Tensor:
+    """(6,) float64 device tensor {min, max} of the cloud, asynchronous
+    (o3dx_aabb_device; zeros for an empty cloud)."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    ws = N.workspace(L.o3dx_aabb_workspace_bytes(n), x.device, "aabb")
+    out = torch.empty(6, dtype=torch.float64, device=x.device)
+    N.check(L.o3dx_aabb_device(N.ptr(x), n, N.ptr(out), N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "aabb_device")
+    return out
+
+
 def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_bound=None,
                       with_xyz: bool = True, trace: bool = False, keep_grid: bool = False):
     """Open3D VoxelDownSampleAndTrace + idxmat.max(1) + _select_by_idx.
@@ -288,17 +300,58 @@ def plane_count(xyz: torch.Tensor, planes: np.ndarray, distance_threshold: float
     return counts[:H]
 
 
-def plane_abs_sum(xyz: torch.Tensor, planes: np.ndarray, which, distance_threshold: float) -> np.ndarray:
+def plane_abs_sum(xyz: torch.Tensor, planes: np.ndarray, which, distance_threshold: float, return_fx: bool = False):
+    """Sigma |d| over |d| < thr of the hypotheses `which` (exact fx sums):
+    float64 (L,), and with return_fx their (L, 4) int64 fx rows."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
     P = _c(planes, np.float64).reshape(-1, 4)
     w = _c(which, np.int32)
     sums = np.zeros(max(len(w), 1), np.float64)
+    fx = np.zeros((max(len(w), 1), 4), np.int64)
     ws = N.workspace(L.o3dx_plane_count_workspace_bytes(n, max(len(w), 1)), x.device)
     N.check(L.o3dx_plane_abs_sum(N.ptr(x), n, _np_ptr(P), _np_ptr(w), len(w), float(distance_threshold),
-                                 _np_ptr(sums), N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "plane_abs_sum")
-    return sums[: len(w)]
+                                 _np_ptr(sums), _np_ptr(fx), N.ptr(ws), ws.numel(), N.stream_ptr(x.device)),
+            "plane_abs_sum")
+    return (sums[: len(w)], fx[: len(w)]) if return_fx else sums[: len(w)]
+
+
+def ransac_tied(counts, planes, n: int, ransac_n: int, probability: float = 0.99999999) -> np.ndarray:
+    """Hypotheses whose Sigma|d| Open3D's selection can consult (o3dx_ransac_tied)."""
+    c = _c(counts, np.int64)
+    P = _c(planes, np.float64).reshape(-1, 4)
+    out = np.zeros(max(len(c), 1), np.int32)
+    k = np.zeros(1, np.int32)
+    N.check(N.load().o3dx_ransac_tied(_np_ptr(c), _np_ptr(P), len(c), int(n), int(ransac_n), float(probability),
+                                      _np_ptr(out), _np_ptr(k)), "ransac_tied")
+    return out[: int(k[0])].copy()
+
+
+def fx_to_double(fx) -> np.ndarray:
+    """fx rows {lo, hi, q, 0} (int64, k x 4) -> float64 (k,), correctly rounded
+    (o3dx_fx_to_double): the one conversion every path uses."""
+    f = _c(fx, np.int64).reshape(-1, 4)
+    out = np.zeros(max(len(f), 1), np.float64)
+    N.check(N.load().o3dx_fx_to_double(_np_ptr(f), len(f), _np_ptr(out)), "fx_to_double")
+    return out[: len(f)]
+
+
+def absmax(xyz: torch.Tensor) -> np.ndarray:
+    """|x|,|y|,|z| bounds of a cloud (from its AABB), float64 (3,)."""
+    if xyz.shape[0] == 0:
+        return np.zeros(3)
+    mn, mx = aabb(xyz)
+    return np.maximum(np.abs(mn), np.abs(mx))
+
+
+def planes_from_samples(coords: np.ndarray, ransac_n: int) -> np.ndarray:
+    """(H, ransac_n, 3) float64 sample coordinates -> (H, 4) planes
+    (ComputeTrianglePlane / GetPlaneFromPoints, o3dx_planes_from_samples)."""
+    c = _c(coords, np.float64).reshape(-1, ransac_n, 3)
+    out = np.zeros((max(len(c), 1), 4), np.float64)
+    N.check(N.load().o3dx_planes_from_samples(_np_ptr(c), len(c), int(ransac_n), _np_ptr(out)), "planes_from_samples")
+    return out[: len(c)]
 
 
 def plane_from_points(pts: np.ndarray) -> np.ndarray:
@@ -372,17 +425,25 @@ def plane_distance(xyz: torch.Tensor, plane) -> torch.Tensor:
     return out
 
 
-def plane_moments(xyz: torch.Tensor, idx: Optional[torch.Tensor], centroid=None) -> np.ndarray:
+def plane_moments(xyz: torch.Tensor, idx: Optional[torch.Tensor], centroid=None, absmax=None,
+                  return_fx: bool = False):
+    """GetPlaneFromPoints moments over idx (exact fx sums): {x,y,z} (pass 1) or
+    centred {xx,xy,xz,yy,yz,zz} (pass 2, `centroid` given).  absmax: the
+    cloud's |x|,|y|,|z| bounds fixing the fx quantum (a sharded cloud passes
+    the global ones).  With return_fx also the (3|6, 4) fx rows."""
     x = _xyz(xyz)
     L = N.load()
     count = x.shape[0] if idx is None else idx.numel()
     c = None if centroid is None else _c(centroid, np.float64)
+    am = None if absmax is None else _c(absmax, np.float64)
     out = np.zeros(6, np.float64)
-    ws = N.workspace(65536, x.device, "moments")
+    fx = np.zeros((6, 4), np.int64)
+    ws = N.workspace(int(L.o3dx_plane_moments_workspace_bytes(count)), x.device, "moments")
     ii = None if idx is None else idx.to(torch.int32).contiguous()
-    N.check(L.o3dx_plane_moments(N.ptr(x), N.ptr(ii), count, _np_ptr(c), _np_ptr(out), N.ptr(ws), ws.numel(),
-                                 N.stream_ptr(x.device)), "plane_moments")
-    return out if centroid is not None else out[:3]
+    N.check(L.o3dx_plane_moments(N.ptr(x), N.ptr(ii), count, _np_ptr(c), _np_ptr(am), _np_ptr(out), _np_ptr(fx),
+                                 N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "plane_moments")
+    k = 6 if centroid is not None else 3
+    return (out[:k], fx[:k]) if return_fx else out[:k]
 
 
 def plane_from_moments(sum_xyz, count, centred) -> np.ndarray:
@@ -409,33 +470,43 @@ class ICPTarget:
                                         self.ws.numel(), _np_ptr(self.desc), N.stream_ptr(self.xyz.device)),
                 "icp_target_build")
 
-    def accumulate(self, src: torch.Tensor, T: np.ndarray, want_corr: bool = False):
-        """Fused transform + 1-NN + point-to-plane moments: (sums[32], corr or None).
-        `src` is (n,3) float32, or the (n,4) output of spatial_sort (faster)."""
+    def accumulate(self, src: torch.Tensor, T: np.ndarray, want_corr: bool = False, absmax=None,
+                   return_fx: bool = False):
+        """Transform + 1-NN + point-to-plane moments: (sums[32], corr or None)
+        (+ the (32, 4) int64 fx rows with return_fx).  `src` is (n,3) float32,
+        or the (n,4) output of spatial_sort (faster).  absmax: |x|,|y|,|z|
+        bounds of the WHOLE source (a sharded source passes the global ones);
+        default: spatial_sort's record of them, else the library measures src."""
         sorted4 = src.ndim == 2 and src.shape[1] == 4
         if sorted4:
             N.require_device(src, "source points")
             s = src.float().contiguous()
         else:
             s = _xyz(src.to(self.xyz.device), "source points")
+        if absmax is None:
+            absmax = getattr(src, "absmax", None)
         L = N.load()
         ns = s.shape[0]
         TT = _c(T, np.float64).reshape(4, 4)
+        am = None if absmax is None else _c(absmax, np.float64).reshape(3)
         sums = np.zeros(N.ICP_NSUMS, np.float64)
+        fx = np.zeros((N.ICP_NSUMS, 4), np.int64)
         corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if want_corr else None
         nc = np.zeros(1, np.int64)
         ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp_acc")
         N.check(L.o3dx_icp_accumulate(N.ptr(s), ns, 1 if sorted4 else 0, N.ptr(self.ws), _np_ptr(self.desc),
-                                      _np_ptr(TT), self.max_corr,
-                                      _np_ptr(sums), N.ptr(corr), _np_ptr(nc), N.ptr(ws), ws.numel(),
+                                      _np_ptr(TT), self.max_corr, _np_ptr(am),
+                                      _np_ptr(sums), _np_ptr(fx), N.ptr(corr), _np_ptr(nc), N.ptr(ws), ws.numel(),
                                       N.stream_ptr(s.device)), "icp_accumulate")
-        return sums, (corr[: int(nc[0])] if want_corr else None)
+        out = (sums, (corr[: int(nc[0])] if want_corr else None))
+        return out + (fx,) if return_fx else out
 
 
 def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
     """(n,4) float32 copy of the cloud in a compact spatial order (8^3 blocks of
     grid cells, Morton order inside a block); column 3 holds the original
-    int32 index bits (o3dx_spatial_sort)."""
+    int32 index bits (o3dx_spatial_sort).  The tensor carries `.absmax`, the
+    cloud's |x|,|y|,|z| bounds (ICPTarget.accumulate's default)."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
@@ -443,7 +514,16 @@ def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
     ws = N.workspace(L.o3dx_spatial_sort_workspace_bytes(n), x.device, "sort")
     N.check(L.o3dx_spatial_sort(N.ptr(x), n, float(target_occ), N.ptr(out), N.ptr(ws), ws.numel(),
                                 N.stream_ptr(x.device)), "spatial_sort")
-    return out[:n]
+    res = out[:n]
+    res.absmax = absmax(x)  # the cloud's coordinate bounds, for ICPTarget.accumulate's fx quanta
+    return res
+
+
+def icp_update(sums, T: np.ndarray) -> np.ndarray:
+    """T <- solve(sums) * T in the library's own float64 order (o3dx_icp_update)."""
+    TT = np.array(T, np.float64).reshape(4, 4).copy()
+    N.load().o3dx_icp_update(_np_ptr(_c(sums, np.float64)), _np_ptr(TT))
+    return TT
 
 
 def icp_solve(sums) -> np.ndarray:

@@ -188,3 +188,46 @@ def ransac_batched_fp32(xyz, thr, samples, batch):
             best_c = int(cnt[j])
             best = np.concatenate([nrm[j], [d[j]]]).astype(np.float64)
     return best, best_c
+
+
+# ---------------------------------------------------------------------------
+# Exact order-free ("fx") sums — the form libo3dx gives every float sum that
+# may cross GPUs (include/o3dx.h, o3dx_plane_moments note), restated in numpy:
+# each term rounded to the nearest integer multiple of 2^q (ties to even),
+# q = frexp-exponent(B) - 51 for a bound B of the terms, integers added.
+
+def fx_exp(B):
+    b = float(B) if (B > 0 and math.isfinite(B)) else 1.0
+    return math.frexp(max(b, math.ldexp(1.0, -900)))[1] - 51
+
+
+def fx_row(terms, q):
+    """fx row {lo, hi, q, 0} of float64 terms at exponent q."""
+    v = np.rint(np.ldexp(np.asarray(terms, np.float64), -q)).astype(np.int64)
+    return np.array([int((v & 0xFFFFFFFF).sum()), int((v >> 32).sum()), q, 0], np.int64)
+
+
+def fx_value(row):
+    """float64 value of an fx row (Python's int -> float rounding: to nearest, ties to even)."""
+    lo, hi, q = int(row[0]), int(row[1]), int(row[2])
+    return math.ldexp(float((hi << 32) + lo), q)
+
+
+def plane_abs_sum_fx(pts, plane, thr):
+    """Sigma |d| over |d| < thr (EvaluateRANSACBasedOnDistance's error sum) as an fx row."""
+    d = plane_dist(plane, np.asarray(pts, np.float32).astype(np.float64).reshape(-1, 3))
+    return fx_row(d[d < thr], fx_exp(thr))
+
+
+def plane_moments_fx(pts, A, centroid=None):
+    """GetPlaneFromPoints' sums over pts as fx rows: {x, y, z} (q from A, the
+    cloud's largest |coordinate|) or, with the centroid, centred {xx, xy, xz,
+    yy, yz, zz} (q from 4 A^2 * 1.01)."""
+    p = np.asarray(pts, np.float32).astype(np.float64).reshape(-1, 3)
+    if centroid is None:
+        q = fx_exp(A)
+        return np.stack([fx_row(p[:, a], q) for a in range(3)])
+    r = p - np.asarray(centroid, np.float64)
+    q = fx_exp(4.0 * A * A * 1.01)
+    pairs = [(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2)]
+    return np.stack([fx_row(r[:, a] * r[:, b], q) for a, b in pairs])

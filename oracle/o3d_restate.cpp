@@ -1033,6 +1033,87 @@ void oref_icp_accumulate(const float* src, int64_t ns, const float* tgt, const f
   }
 }
 
+// The exact order-free ("fx") form of the same sums (libo3dx common.hpp /
+// include/o3dx.h o3dx_plane_moments note), restated independently for the
+// sharded tests: every term rounded to the nearest integer multiple of 2^q
+// (ties to even), the integers added in 128 bits.  q per sum from the same
+// bounds as icp.hip icp_fx_exps: source |x|,|y|,|z| bounds (absmax), T and
+// max_dist.  fx_out: 32 rows {lo = low 32 bits, hi = the rest, q, 0}.
+static int fx_exp_of(double B) {
+  int e = 0;
+  const double b = (B > 0.0 && std::isfinite(B)) ? std::max(B, std::ldexp(1.0, -900)) : 1.0;
+  std::frexp(b, &e);
+  return e - 51;
+}
+
+static void fx_rows(const __int128* acc, const int* q, int k, int64_t* out) {
+  for (int j = 0; j < k; ++j) {
+    const __int128 v = acc[j];
+    const __int128 lo = v & (__int128)0xffffffff;
+    out[4 * j] = (int64_t)lo;
+    out[4 * j + 1] = (int64_t)((v - lo) / ((__int128)1 << 32));
+    out[4 * j + 2] = q[j];
+    out[4 * j + 3] = 0;
+  }
+}
+
+static __int128 fx_int(double t, int q) { return (__int128)std::nearbyint(std::ldexp(t, -q)); }
+
+void oref_icp_accumulate_fx(const float* src, int64_t ns, const float* tgt, const float* tgt_n, int64_t nt,
+                            double max_dist, const double* T, const double* absmax, int64_t* fx_out) {
+  std::vector<V3> tp = to_v3(tgt, nt);
+  std::vector<V3> tn = to_v3(tgt_n, nt);
+  std::vector<V3> sp = to_v3(src, ns);
+  transform_points(T, sp);
+  KDTree tree;
+  tree.build(tp.data(), (int)nt);
+  int q[32] = {0};
+  double P2 = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    const double Pi = ((std::fabs(T[4 * i]) * absmax[0] + std::fabs(T[4 * i + 1]) * absmax[1]) +
+                       std::fabs(T[4 * i + 2]) * absmax[2]) + std::fabs(T[4 * i + 3]);
+    P2 += Pi * Pi;
+  }
+  const double pn = std::sqrt(P2) * 1.01;
+  double bJ[6];
+  for (int a = 0; a < 6; ++a) bJ[a] = (a < 3 ? pn : 1.0) * 1.01;
+  const double br = max_dist * 1.01 * 1.01;
+  int t = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int b = a; b < 6; ++b) q[t++] = fx_exp_of(bJ[a] * bJ[b] * 1.01);
+  for (int a = 0; a < 6; ++a) q[21 + a] = fx_exp_of(bJ[a] * br * 1.01);
+  q[27] = fx_exp_of(br * br * 1.01);
+  q[28] = fx_exp_of(1.0);
+  q[29] = fx_exp_of(max_dist * max_dist * 1.01);
+  __int128 acc[32] = {0};
+  std::vector<int> idx;
+  std::vector<double> d2;
+  for (int64_t i = 0; i < ns; ++i) {
+    int k = tree.search(sp[i], 2, 1, max_dist, idx, d2);
+    if (k == 0) continue;
+    const V3& vs = sp[i];
+    const V3& vt = tp[idx[0]];
+    const V3& nt_ = tn[idx[0]];
+    double d[3] = {vs.x - vt.x, vs.y - vt.y, vs.z - vt.z};
+    double nn[3] = {nt_.x, nt_.y, nt_.z};
+    double r = dot3(d, nn);
+    double vv[3] = {vs.x, vs.y, vs.z};
+    double J[6];
+    cross(vv, nn, J);
+    J[3] = nn[0];
+    J[4] = nn[1];
+    J[5] = nn[2];
+    int u = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int b = a; b < 6; ++b, ++u) acc[u] += fx_int(J[a] * J[b], q[u]);
+    for (int a = 0; a < 6; ++a) acc[21 + a] += fx_int(J[a] * r, q[21 + a]);
+    acc[27] += fx_int(r * r, q[27]);
+    acc[28] += fx_int(1.0, q[28]);
+    acc[29] += fx_int(d2[0], q[29]);
+  }
+  fx_rows(acc, q, 32, fx_out);
+}
+
 // host solve from sums (for the sharded CPU test path)
 int oref_icp_solve(const double* sums, double* upd) {
   double JTJ[36];

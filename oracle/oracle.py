@@ -55,6 +55,7 @@ def lib():
                                             _P, _P, _P, _P, _P]
         L.oref_registration_icp.restype = _I32
         L.oref_icp_accumulate.argtypes = [_P, _I64, _P, _P, _I64, _D, _P, _P]
+        L.oref_icp_accumulate_fx.argtypes = [_P, _I64, _P, _P, _I64, _D, _P, _P, _P]
         L.oref_icp_solve.argtypes = [_P, _P]
         L.oref_icp_solve.restype = _I32
         _lib = L
@@ -230,6 +231,20 @@ def icp_accumulate(src, tgt, tgt_normals, max_dist, T):
     lib().oref_icp_accumulate(_ptr(s), len(s), _ptr(t), _ptr(tn), len(t), float(max_dist),
                               _ptr(TT), _ptr(sums))
     return sums
+
+
+def icp_accumulate_fx(src, tgt, tgt_normals, max_dist, T, absmax):
+    """The same sums as exact fx rows (32, 4) int64 {lo, hi, q, 0} (the
+    order-free form libo3dx uses; restated with 128-bit integers)."""
+    s = _f32(src)
+    t = _f32(tgt)
+    tn = _f32(tgt_normals)
+    TT = np.ascontiguousarray(T, np.float64)
+    am = np.ascontiguousarray(absmax, np.float64).reshape(3)
+    fx = np.zeros((32, 4), np.int64)
+    lib().oref_icp_accumulate_fx(_ptr(s), len(s), _ptr(t), _ptr(tn), len(t), float(max_dist), _ptr(TT), _ptr(am),
+                                 _ptr(fx))
+    return fx
 
 
 def icp_solve(sums):

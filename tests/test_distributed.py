@@ -260,3 +260,120 @@ def test_c4_slabs_clustered_halo(world):
     assert np.any((t >= H0) & (dk > t + H0))
     res = spawn(_clustered_rank, world=world)
     _check_slabs(res, pts, CL_VS)
+
+
+# ----------------------------------------------------- exact (fx) sharded sums
+class OracleBackend:
+    """The per-rank compute of distributed.segment_plane_sharded /
+    registration_icp_sharded restated on the CPU (oracle: test infrastructure)
+    — the same interface as distributed._HipBackend, fx sums from numpy /
+    the oracle's 128-bit restatement."""
+
+    def absmax(self, x):
+        p = x.numpy().astype(np.float64)
+        return np.abs(p).max(0) if len(p) else np.zeros(3)
+
+    def rows_f64(self, x, idx):
+        return x[idx].double()
+
+    def plane_count(self, x, planes, thr):
+        p = x.numpy().astype(np.float64)
+        out = []
+        for pl in planes:
+            if not pl.any():
+                out.append(-1)
+            elif not np.all(np.isfinite(pl)):
+                out.append(0)
+            else:
+                out.append(int((NPR.plane_dist(pl, p) < thr).sum()))
+        return np.array(out, np.int64)
+
+    def abs_sum_fx(self, x, planes, which, thr):
+        return np.stack([NPR.plane_abs_sum_fx(x.numpy(), planes[w], thr) for w in which])
+
+    def plane_inliers(self, x, plane, thr):
+        p = x.numpy().astype(np.float64)
+        return torch.from_numpy(np.nonzero(NPR.plane_dist(plane, p) < thr)[0].astype(np.int64))
+
+    def moments_fx(self, x, idx, centroid, absmax):
+        return NPR.plane_moments_fx(x.numpy()[idx.numpy()], float(np.max(absmax)), centroid)
+
+    def icp_target(self, tgt, tn, max_corr):
+        return (tgt.numpy(), tn.numpy(), max_corr)
+
+    def icp_source(self, src):
+        return src.numpy()
+
+    def icp_accumulate_fx(self, target, src, T, absmax):
+        tgt, tn, mc = target
+        return O.icp_accumulate_fx(src, tgt, tn, mc, T, absmax)
+
+
+def _plane_cloud():
+    pts = S.planted_plane(30_000, 12, frac=0.3).numpy()
+    return pts
+
+
+def _plane_rank(rank, world, thr=0.01):
+    from open3dpypro import distributed as Dm
+    pts = _plane_cloud()
+    pos = torch.arange(rank, len(pts), world, dtype=torch.int64)  # interleaved rows: not rank-ordered
+    samples = O.ransac_samples(len(pts), 3, 300, 21)
+    plane, inl = Dm.segment_plane_sharded(torch.from_numpy(pts)[pos], pos, len(pts), thr, 3, 300, samples=samples,
+                                          backend=OracleBackend())
+    return plane, pos[inl]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_segment_plane_sharded_bit_identical(world):
+    """RANSAC with the rows spread over the ranks (sampled rows summed as bit
+    patterns, integer counts, fx tie sums and refit moments): plane and
+    inliers the same bits as one process, and equal to the oracle's
+    SegmentPlane (inliers exactly, the plane within its float64-summation
+    rounding)."""
+    res = spawn(_plane_rank, world=world)
+    p1, i1 = _plane_rank(0, 1)
+    for pl, _ in res:
+        assert np.array_equal(pl, p1)
+    inl = np.sort(np.concatenate([r[1] for r in res]))
+    assert np.array_equal(inl, i1)
+    pts = _plane_cloud()
+    rplane, rinl, *_ = O.segment_plane(pts, 0.01, 3, 300, O.ransac_samples(len(pts), 3, 300, 21))
+    assert np.array_equal(i1, rinl)
+    np.testing.assert_allclose(p1, rplane, rtol=0, atol=1e-12)
+
+
+def _icp_fx_rank(rank, world):
+    from open3dpypro import distributed as Dm
+    src, tgt, tn = _icp_clouds()
+    a, b = D.shard_range(len(src), world, rank)
+    be = OracleBackend()
+    target = be.icp_target(torch.from_numpy(tgt), torch.from_numpy(tn.astype(np.float32)), 0.05)
+    return Dm.registration_icp_sharded(torch.from_numpy(src[a:b]), target, max_iteration=12, backend=be)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_icp_sharded_fx_bit_identical(world):
+    """Point-to-plane ICP with the source sharded: the fx moments make T,
+    fitness and rmse the same bits for 1, 2 and 3 ranks; the loop is the
+    oracle's registration_icp to 1e-9."""
+    res = spawn(_icp_fx_rank, world=world)
+    T1, f1, r1 = _icp_fx_rank(0, 1)
+    for T, f, r in res:
+        assert np.array_equal(T, T1) and f == f1 and r == r1
+    src, tgt, tn = _icp_clouds()
+    To, fo, ro = O.registration_icp(src, tgt, tn.astype(np.float32), 0.05, max_iteration=12)[:3]
+    assert np.abs(T1 - To).max() < 1e-9 and abs(f1 - fo) < 1e-12 and abs(r1 - ro) < 1e-9
+
+
+def test_fx_rows_oracle_vs_numpy():
+    """The oracle's 128-bit fx ICP sums and their float64 values against the
+    plain float64 sums (the same terms): equal to within the fx rounding."""
+    src, tgt, tn = _icp_clouds()
+    T = S.rigid_transform(0.5, (0, 1, 0), (0.002, 0, 0))
+    am = np.abs(src.astype(np.float64)).max(0)
+    fx = O.icp_accumulate_fx(src, tgt, tn, 0.05, T, am)
+    ref = O.icp_accumulate(src, tgt, tn, 0.05, T)
+    vals = np.array([NPR.fx_value(r) for r in fx[:30]])
+    assert vals[28] == ref[28]
+    np.testing.assert_allclose(vals, ref[:30], rtol=1e-11, atol=1e-13)

@@ -30,19 +30,24 @@ def _rank(rank, world):
     tn = ops.estimate_normals(t, knn=30)
     target = ops.ICPTarget(t, tn, 0.02)
     a, b = D.shard_range(len(src), world, rank)
-    shard = ops.spatial_sort(torch.from_numpy(src[a:b]).to(dev))
-    return D.registration_icp_point_to_plane(lambda T: target.accumulate(shard, T)[0], len(src), max_iteration=20)
+    return D.registration_icp_sharded(torch.from_numpy(src[a:b]).to(dev), target, max_iteration=20)
 
 
-def test_sharded_icp_on_device_matches_single():
-    (Ta, fa, ra), (Tb, fb, rb) = spawn(_rank)
-    assert np.array_equal(Ta, Tb) and fa == fb and ra == rb
-    T1, f1, r1 = _rank(0, 1)
-    assert np.abs(Ta - T1).max() < 1e-9 and abs(fa - f1) < 1e-12
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_icp_on_device_matches_single(world):
+    """ICP with the source sharded over ranks (HIP kernels, fx moments summed
+    over the ranks): T, fitness and rmse the same bits as the single-GPU
+    o3dx_registration_icp_point_to_plane, and within 1e-5 of the oracle."""
+    res = spawn(_rank, world=world)
     src, tgt = _clouds()
-    tn = O.estimate_normals(tgt, O.KNN, 30)
-    To, fo, ro = O.registration_icp(src, tgt, tn, 0.02, max_iteration=20)[:3]
-    assert np.abs(T1 - To).max() < 1e-5 and abs(f1 - fo) < 1e-5
+    dev = torch.device("cuda:0")
+    t = torch.from_numpy(tgt).to(dev)
+    tn = ops.estimate_normals(t, knn=30)
+    one = ops.registration_icp(torch.from_numpy(src).to(dev), t, tn, 0.02, max_iteration=20, return_corr=False)
+    for T, f, r in res:
+        assert np.array_equal(T, one["transformation"]) and f == one["fitness"] and r == one["inlier_rmse"]
+    To, fo, ro = O.registration_icp(src, tgt, tn.cpu().numpy(), 0.02, max_iteration=20)[:3]
+    assert np.abs(one["transformation"] - To).max() < 1e-5 and abs(one["fitness"] - fo) < 1e-5
 
 
 def _c4_rank(rank, world):
@@ -146,3 +151,137 @@ def test_c4_slabs_presorted_on_device(world):
     o = np.argsort(g)
     assert np.array_equal(g[o], out["rep_idx"].cpu().numpy().astype(np.int64))
     assert np.array_equal(nn[o], ref)
+
+
+# ------------------------------------------------------ C4 at its own size
+C4_N = 50_000_000
+
+
+def _c4_big_rank(rank, world, presorted):
+    dev = torch.device("cuda:0")
+    vs = S.voxel_size_for(C4_N)
+    pts = S.uniform_cube(C4_N, 0, device=dev)
+    if presorted:
+        mn, mx = ops.aabb(pts)
+        keys = D.slab_bounds(mn, mx, vs, world)
+        kx = torch.floor((pts[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+        g = torch.nonzero((kx >= keys[rank]) & (kx < keys[rank + 1])).flatten()
+        del kx
+    else:
+        g = torch.arange(rank, C4_N, world, dtype=torch.int64, device=dev)
+    x = pts[g].contiguous()
+    del pts
+    rg, _, nrm = D.voxel_normals_slabs(x, g, vs, knn=30, presorted=presorted)
+    return rg, nrm
+
+
+@pytest.mark.parametrize("world,presorted", [(2, True), (4, True), (2, False), (4, False)])
+def test_c4_50m_slabs_match_single(world, presorted):
+    """C4 at BASELINE configs[3]'s size: one 50M-point cloud over 2 and 4
+    ranks (gloo rendezvous, the ranks share the one GPU of the test box),
+    points already in their slabs (presorted, the bench's layout) or an
+    arbitrary share moved to their slab owners: representatives and normals
+    bit-identical to the single-GPU call (whose neighbour sets are checked
+    bit-exact against the oracle at 50M in test_gpu_scale)."""
+    res = spawn(_C4Big(presorted), world=world)
+    dev = torch.device("cuda:0")
+    pts = S.uniform_cube(C4_N, 0, device=dev)
+    out = ops.voxel_down_sample_normals(pts, S.voxel_size_for(C4_N), knn=30)
+    del pts
+    g = np.concatenate([r[0] for r in res])
+    o = np.argsort(g, kind="stable")
+    assert np.array_equal(g[o], out["rep_idx"].cpu().numpy().astype(np.int64))
+    nn = np.concatenate([r[1] for r in res])
+    assert np.array_equal(nn[o], out["normals"].cpu().numpy())
+
+
+class _C4Big:
+    """picklable per-rank entry (spawn)"""
+
+    def __init__(self, presorted):
+        self.presorted = presorted
+
+    def __call__(self, rank, world):
+        return _c4_big_rank(rank, world, self.presorted)
+
+
+# --------------------------------------------------------------------- C5
+C5_N, C5_VS = 2_000_000, 0.002
+
+
+def _c5_clouds(world, tiled):
+    tgt = S.box_surface(C5_N, 1)
+    src = S.apply_transform(S.box_surface(C5_N, 2), S.rigid_transform())
+    if not tiled:
+        return tgt, src
+    out = []
+    for c in (tgt, src):  # a spatially tiled dataset: the cloud is its slabs in rank order
+        mn = c.double().min(0).values.numpy()
+        mx = c.double().max(0).values.numpy()
+        keys = D.slab_bounds(mn, mx, C5_VS, world)
+        kx = torch.floor((c[:, 0].double() - float(mn[0])) / C5_VS).to(torch.int64)
+        owner = torch.searchsorted(torch.tensor(keys[1:-1], dtype=torch.int64), kx, right=True)
+        out.append(c[torch.argsort(owner, stable=True)].contiguous())
+    return out[0], out[1]
+
+
+def _c5_share(c, world, rank, tiled):
+    if not tiled:
+        return torch.arange(rank, c.shape[0], world, dtype=torch.int64)
+    mn = c.double().min(0).values.numpy()
+    mx = c.double().max(0).values.numpy()
+    keys = D.slab_bounds(mn, mx, C5_VS, world)
+    kx = torch.floor((c[:, 0].double() - float(mn[0])) / C5_VS).to(torch.int64)
+    return torch.nonzero((kx >= keys[rank]) & (kx < keys[rank + 1])).flatten()
+
+
+class _C5Rank:
+    def __init__(self, tiled):
+        self.tiled = tiled
+
+    def __call__(self, rank, world):
+        dev = torch.device("cuda:0")
+        tgt, src = _c5_clouds(world, self.tiled)
+        gt, gs = _c5_share(tgt, world, rank, self.tiled), _c5_share(src, world, rank, self.tiled)
+        out = D.pipeline_sharded(tgt[gt].to(dev), gt.to(dev), src[gs].to(dev), gs.to(dev), C5_VS, knn=30,
+                                 distance_threshold=0.002, num_iterations=300, seed=7,
+                                 max_correspondence_distance=0.02, icp_iterations=10, presorted=self.tiled)
+        return (out["target_rep_gidx"], out["target_normals"], out["plane"], out["plane_inlier_rows"],
+                out["transformation"], out["fitness"], out["inlier_rmse"], out["target_reps"], out["source_reps"])
+
+
+@pytest.mark.parametrize("world,tiled", [(2, True), (3, True), (2, False)])
+def test_c5_pipeline_sharded_matches_single(world, tiled):
+    """C5 (BASELINE configs[4]) over the ranks: target voxel reps + KNN30
+    normals on x-slabs with the halo exchange, source voxel reps on its own
+    slabs, segment_plane with the rows sharded (exact counts and fx sums),
+    ICP with the source sharded and the fx moments all-reduced per
+    iteration.  Against the single-GPU chain (ops.voxel_down_sample ->
+    estimate_normals -> segment_plane -> registration_icp) on the same cloud:
+    reps, normals, plane, inliers, T, fitness and rmse all bit-identical.
+    tiled: the dataset is its slabs in rank order (positions by prefix sums);
+    otherwise an interleaved share (positions by an index all-gather)."""
+    res = spawn(_C5Rank(tiled), world=world)
+    dev = torch.device("cuda:0")
+    tgt, src = _c5_clouds(world, tiled)
+    vt = ops.voxel_down_sample(tgt.to(dev), C5_VS, keep_grid=True)
+    treps = vt["rep_xyz"]
+    tn = ops.estimate_normals(treps, knn=30, voxel_grid=vt["voxel_grid"])
+    sreps = ops.voxel_down_sample(src.to(dev), C5_VS)["rep_xyz"]
+    M = treps.shape[0]
+    samples = ops.ransac_samples(M, 3, 300, 7)
+    plane, inl = ops.segment_plane(treps, 0.002, 3, 300, samples=samples)
+    icp = ops.registration_icp(sreps, treps, tn, 0.02, max_iteration=10, relative_fitness=0.0, relative_rmse=0.0,
+                               return_corr=False)
+    g = np.concatenate([r[0] for r in res])
+    o = np.argsort(g, kind="stable")
+    assert np.array_equal(g[o], vt["rep_idx"].cpu().numpy().astype(np.int64))
+    assert np.array_equal(np.concatenate([r[1] for r in res])[o], tn.cpu().numpy())
+    rows = np.sort(np.concatenate([r[3] for r in res]))
+    assert np.array_equal(rows, inl.cpu().numpy().astype(np.int64)) and len(rows) > 0
+    for r in res:
+        assert r[7] == M and r[8] == sreps.shape[0]
+        assert np.array_equal(r[2], plane)
+        assert np.array_equal(r[4], icp["transformation"])
+        assert r[5] == icp["fitness"] and r[6] == icp["inlier_rmse"]
+    assert np.abs(icp["transformation"] - np.linalg.inv(S.rigid_transform())).max() < 1e-3

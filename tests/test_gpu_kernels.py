@@ -215,8 +215,31 @@ def test_ransac_counts_exact(dev, n, iters):
     got = ops.plane_count(torch.from_numpy(pts).to(dev), planes, 0.01)
     assert np.array_equal(got, counts)
     ok = counts > 0
-    gs = ops.plane_abs_sum(torch.from_numpy(pts).to(dev), planes, np.nonzero(ok)[0], 0.01)
+    which = np.nonzero(ok)[0]
+    gs, gfx = ops.plane_abs_sum(torch.from_numpy(pts).to(dev), planes, which, 0.01, return_fx=True)
     np.testing.assert_allclose(gs, sums[ok], rtol=1e-12)
+    # the exact fx sums: the same integers as the numpy restatement (any split)
+    for j, h in enumerate(which[:40]):
+        exp = NPR.plane_abs_sum_fx(pts, planes[h], 0.01)
+        assert NPR.fx_value(gfx[j]) == NPR.fx_value(exp) == gs[j]
+
+
+def test_plane_moments_fx_exact(dev):
+    """GetPlaneFromPoints moments as fx sums: the same values as the numpy
+    restatement over the same inliers (exact integers, any order)."""
+    pts = S.planted_plane(200_000, 7).numpy()
+    x = torch.from_numpy(pts).to(dev)
+    idx = torch.nonzero(torch.from_numpy(np.abs(pts[:, 2] - 0.5) < 0.01)).flatten().to(dev)
+    am = np.abs(pts.astype(np.float64)).max(0)
+    A = float(am.max())
+    s1, f1 = ops.plane_moments(x, idx, absmax=am, return_fx=True)
+    sel = pts[idx.cpu().numpy()]
+    e1 = NPR.plane_moments_fx(sel, A)
+    assert [NPR.fx_value(r) for r in f1] == [NPR.fx_value(r) for r in e1] == list(s1)
+    c = s1 / idx.numel()
+    s2, f2 = ops.plane_moments(x, idx, centroid=c, absmax=am, return_fx=True)
+    e2 = NPR.plane_moments_fx(sel, A, c)
+    assert [NPR.fx_value(r) for r in f2] == [NPR.fx_value(r) for r in e2] == list(s2)
 
 
 @pytest.mark.parametrize("n,iters,ransac_n", [(30_000, 450, 3), (200_000, 1000, 3), (20_000, 100, 5)])
@@ -273,10 +296,14 @@ def test_icp_accumulate_matches_oracle(dev):
     tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
     T = S.rigid_transform(0.3, (0, 0, 1), (0.001, 0, 0))
     target = ops.ICPTarget(torch.from_numpy(tgt).to(dev), torch.from_numpy(tn).to(dev), 0.02)
-    sums, corr = target.accumulate(torch.from_numpy(src).to(dev), T, want_corr=True)
+    sums, corr, fx = target.accumulate(torch.from_numpy(src).to(dev), T, want_corr=True, return_fx=True)
     ref = O.icp_accumulate(src, tgt, tn, 0.02, T)
     assert sums[28] == ref[28]
     np.testing.assert_allclose(sums[:30], ref[:30], rtol=1e-9, atol=1e-9)
+    # the exact fx sums equal the oracle's independent 128-bit restatement
+    rfx = O.icp_accumulate_fx(src, tgt, tn, 0.02, T, np.abs(src.astype(np.float64)).max(0))
+    assert np.array_equal(fx[:, 2], rfx[:, 2])
+    assert np.array_equal(ops.fx_to_double(fx), ops.fx_to_double(rfx))
 
 
 def test_registration_icp_parity(dev):
@@ -305,8 +332,7 @@ def test_icp_accumulate_sorted_source_layout(dev):
                        torch.arange(len(src), device=dev))
     a, ca = target.accumulate(s, T, want_corr=True)
     b, cb = target.accumulate(s4, T, want_corr=True)
-    assert a[28] == b[28]
-    np.testing.assert_allclose(a[:30], b[:30], rtol=1e-10, atol=1e-12)
+    assert np.array_equal(a, b)  # fx sums: the order of the source does not matter
     assert torch.equal(ca, cb)
     ref = O.icp_accumulate(src, tgt, tn, 0.02, T)
     np.testing.assert_allclose(b[:30], ref[:30], rtol=1e-9, atol=1e-9)
@@ -326,8 +352,7 @@ def test_icp_displaced_source_exact(dev, shift):
     a, ca = target.accumulate(s, T, want_corr=True)
     b, cb = target.accumulate(ops.spatial_sort(s), T, want_corr=True)
     assert torch.equal(ca, cb)
-    assert a[28] == b[28]  # the moments differ only in summation order
-    np.testing.assert_allclose(a[:30], b[:30], rtol=1e-9, atol=1e-9)
+    assert np.array_equal(a, b)  # fx sums: the same bits in any source order
     ref = O.icp_accumulate(src, tgt, tn, 0.02, T)
     assert a[28] == ref[28]
     np.testing.assert_allclose(a[:30], ref[:30], rtol=1e-9, atol=1e-9)

@@ -67,6 +67,50 @@ def test_icp_solve_host():
     assert np.allclose(upd[:3, 3], x[3:])
 
 
+def test_fx_to_double_correctly_rounded():
+    """o3dx_fx_to_double (the one conversion of every exact fx sum) equals
+    Python's correctly rounded int -> float on random digits, on values with
+    more than 53 significant bits, on halfway cases (ties to even), negative
+    and extreme exponents; and the numpy restatement's fx rows agree."""
+    from oracle import np_restate as NPR
+    rng = np.random.default_rng(3)
+    rows = []
+    for _ in range(2000):
+        lo = int(rng.integers(0, 1 << 62))
+        hi = int(rng.integers(-(1 << 62), 1 << 62))
+        rows.append([lo, hi, int(rng.integers(-200, 100)), 0])
+    for v in (2 ** 53 + 1, 2 ** 53 + 3, -(2 ** 54) - 2, 2 ** 80 + 2 ** 27, (1 << 90) - 1, 0, -1, 1):
+        rows.append([v & 0xFFFFFFFF, v >> 32, -40, 0])
+    fx = np.array(rows, np.int64)
+    got = o3p.ops.fx_to_double(fx)
+    exp = np.array([NPR.fx_value(r) for r in fx])
+    assert np.array_equal(got, exp)
+    # digit sums of split terms equal the row of all terms (any order, any split)
+    t = rng.normal(0, 1e-3, 10000)
+    q = NPR.fx_exp(0.01)
+    a, b = NPR.fx_row(t[:3333], q), NPR.fx_row(t[3333:], q)
+    whole = NPR.fx_row(t[::-1], q)
+    assert NPR.fx_value(a + np.array([b[0], b[1], 0, 0])) == NPR.fx_value(whole)
+    assert abs(NPR.fx_value(whole) - t.sum()) < 1e-15
+
+
+def test_planes_from_samples_and_icp_update_host():
+    from oracle import np_restate as NPR
+    rng = np.random.default_rng(4)
+    c = rng.random((20, 3, 3))
+    c[5, 2] = c[5, 0]  # degenerate triple
+    P = o3p.ops.planes_from_samples(c, 3)
+    for h in range(20):
+        assert np.array_equal(P[h], NPR.triangle_plane(*c[h]))
+    sums = np.zeros(32)
+    sums[[0, 6, 11, 15, 18, 20]] = 1.0
+    sums[21:27] = [0, 0, -0.01, -0.1, 0.2, -0.3]
+    sums[28] = 5
+    T0 = S.rigid_transform(3.0)
+    T1 = o3p.ops.icp_update(sums, T0)
+    assert np.allclose(T1, o3p.ops.icp_solve(sums) @ T0, atol=1e-15)
+
+
 @pytest.mark.skipif(GPU, reason="checks the no-GPU behaviour")
 def test_compute_fails_loudly_without_gpu():
     pc = o3p.PointCloud(np.random.rand(100, 3))
