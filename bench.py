@@ -143,7 +143,8 @@ def host_info():
 def cpu_baseline(n_cpu: int, pts_dev=None):
     """The oracle (an Open3D-equivalent C++ restatement, oracle/) of the C2
     step on the C2 input itself: voxel trace single-threaded as Open3D's,
-    KD-tree KNN30 normals with OpenMP."""
+    KD-tree KNN30 normals with OpenMP — on the inherited OMP_NUM_THREADS (the
+    box's share, 16) and again on every host thread (os.cpu_count())."""
     from oracle import oracle as O
 
     pts = (pts_dev.cpu().numpy() if pts_dev is not None and pts_dev.shape[0] == n_cpu
@@ -156,12 +157,23 @@ def cpu_baseline(n_cpu: int, pts_dev=None):
     O.estimate_normals(pts[rep], O.KNN, 30)
     t2 = time.perf_counter()
     el = t2 - t0
-    return {"value": round(n_cpu / el / 1e6, 4), "unit": "Mpoints/s", "cores": O.num_threads(),
-            "kind": "port",
-            "sample": (f"the C2 input itself (N={n_cpu}, M={len(rep)}): Open3D-equivalent C++ restatement "
-                       f"(oracle/o3d_restate.cpp): voxel trace 1 thread {t1 - t0:.2f}s + KD-tree KNN30 normals "
-                       f"{O.num_threads()} OpenMP threads {t2 - t1:.2f}s"),
-            "seconds": round(el, 3), **host_info()}
+    out = {"value": round(n_cpu / el / 1e6, 4), "unit": "Mpoints/s", "cores": O.num_threads(),
+           "kind": "port",
+           "sample": (f"the C2 input itself (N={n_cpu}, M={len(rep)}): Open3D-equivalent C++ restatement "
+                      f"(oracle/o3d_restate.cpp): voxel trace 1 thread {t1 - t0:.2f}s + KD-tree KNN30 normals "
+                      f"{O.num_threads()} OpenMP threads {t2 - t1:.2f}s"),
+           "seconds": round(el, 3), **host_info()}
+    allc = os.cpu_count() or 1
+    if allc > O.num_threads():
+        # the normals on every host thread (the voxel trace stays serial, as Open3D's)
+        O.set_num_threads(allc)
+        t3 = time.perf_counter()
+        O.estimate_normals(pts[rep], O.KNN, 30)
+        t4 = time.perf_counter()
+        O.set_num_threads(out["cores"])
+        out["all_threads"] = {"cores": allc, "normals_s": round(t4 - t3, 3),
+                              "value": round(n_cpu / ((t1 - t0) + (t4 - t3)) / 1e6, 4)}
+    return out
 
 
 def cpu_secondary(dev, args, tn_dev=None):
@@ -228,7 +240,17 @@ def secondary(dev, args):
                      "plane_count_kernel_ms": round(pc_ms, 3), "inliers": int(inl.numel()),
                      "plane": [round(float(v), 6) for v in plane],
                      "Gpairs_per_s": round(pairs / (pc_ms * 1e-3) / 1e9, 2) if pc_ms > 0 else None}
-    del pts, inl
+    del inl
+    # the general path on the raw C3 cloud (no voxel table: sorted search grid,
+    # its thin dense plane puts hundreds of points in a cell)
+    ops.estimate_normals(pts, knn=30)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ops.estimate_normals(pts, knn=30)
+    torch.cuda.synchronize(dev)
+    out["normals_raw_c3"] = {"n": n, "ms": round((time.perf_counter() - t0) * 1e3, 3),
+                             "path": "sorted grid (estimate_normals on the raw planted-plane cloud)"}
+    del pts
     # ICP: box-surface target with KNN30 normals, source = independent sample moved by T_gt
     tgt = synthetic.box_surface(n, seed=1, device=dev)
     src = synthetic.apply_transform(synthetic.box_surface(n, seed=2, device=dev), synthetic.rigid_transform())
@@ -279,9 +301,10 @@ def secondary(dev, args):
 
 
 def secondary_sharded_icp(dev, args, world, rank):
-    """C3/C5-style ICP with the source sharded over the ranks (strong scaling of
-    one 10M source) and the target replicated; the 29 float64 moments are
-    all-gathered over RCCL once per iteration (open3dpypro.distributed)."""
+    """C3-style ICP with the source sharded over the ranks (strong scaling of
+    one 10M source) and the target replicated; the moments are exact fx sums
+    all-reduced over RCCL once per iteration (open3dpypro.distributed), so T
+    is the single-GPU result to the bit."""
     from open3dpypro import distributed as D
 
     n = args.icp_n
@@ -289,21 +312,21 @@ def secondary_sharded_icp(dev, args, world, rank):
     src = synthetic.apply_transform(synthetic.box_surface(n, seed=2, device=dev), synthetic.rigid_transform())
     target = ops.ICPTarget(tgt, ops.estimate_normals(tgt, knn=30), 0.02)
     a, b = D.shard_range(n, world, rank)
-    shard = ops.spatial_sort(src[a:b].contiguous())
+    shard = src[a:b].contiguous()
     del src
-    acc = lambda T: target.accumulate(shard, T)[0]  # noqa: E731
-    D.registration_icp_point_to_plane(acc, n, max_iteration=1)  # warm
+    D.registration_icp_sharded(shard, target, max_iteration=1)  # warm
     barrier(world, dev)
     t0 = time.perf_counter()
-    T, fit, rm = D.registration_icp_point_to_plane(acc, n, max_iteration=args.icp_iters, relative_fitness=0.0,
-                                                   relative_rmse=0.0)
+    T, fit, rm = D.registration_icp_sharded(shard, target, max_iteration=args.icp_iters, relative_fitness=0.0,
+                                            relative_rmse=0.0)
     barrier(world, dev)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     err = float(np.abs(T - np.linalg.inv(synthetic.rigid_transform())).max())
     return {"icp_sharded": {"n_source": n, "n_target": n, "ranks": world, "iterations": args.icp_iters,
                             "iters_per_s": round(args.icp_iters / el, 3), "fitness": round(fit, 6),
                             "T_err_vs_gt_inverse": err,
-                            "collective": "all_gather of 32 float64 per iteration (RCCL), summed in rank order"}}
+                            "collective": "all_reduce of 32 x 2 int64 fx digits per iteration (RCCL): exact, "
+                                          "order-free"}}
 
 
 def c4_single_gpu(dev, args):
@@ -424,6 +447,65 @@ def c4_headline(dev, args, world, rank):
     m = torch.tensor([rg.numel()], dtype=torch.int64, device=comm_dev(dev))
     dist.all_reduce(m)
     return elapsed, int(m.item()), int(pts.shape[0])
+
+
+def c5_sharded(dev, args, world, rank):
+    """C5 over the ranks (BASELINE configs[4]): 200M-point box-surface target
+    and an independent 200M sample of it moved by T_gt, each a spatially
+    tiled dataset (every rank holds its x-slab; placement untimed), one pass =
+    open3dpypro.distributed.pipeline_sharded: slab voxel reps + KNN30 normals
+    of the target (halo exchange), slab voxel reps of the source,
+    segment_plane 1000 hypotheses with the reps sharded (exact count / fx
+    all-reduces), 30 ICP iterations with the source sharded and the fx
+    moments all-reduced per iteration (RCCL).  Bit-identical to one GPU
+    (tests/test_gpu_distributed.py::test_c5_pipeline_sharded_matches_single)."""
+    from open3dpypro import distributed as D
+
+    n = args.c5_n
+    vs = 0.0005
+
+    def tile(c):
+        mn, mx = ops.aabb(c)
+        keys = D.slab_bounds(mn, mx, vs, world)
+        kx = torch.floor((c[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+        owner = torch.searchsorted(torch.tensor(keys[1:-1], dtype=torch.int64, device=dev), kx, right=True)
+        counts = torch.bincount(owner, minlength=world).cpu().tolist()
+        own = torch.nonzero(owner == rank).flatten()
+        start = sum(counts[:rank])
+        return c[own].contiguous(), torch.arange(start, start + own.numel(), dtype=torch.int64, device=dev)
+
+    t = synthetic.box_surface(n, seed=1, device=dev)
+    tgt, tg = tile(t)
+    del t
+    s_ = synthetic.apply_transform(synthetic.box_surface(n, seed=2, device=dev), synthetic.rigid_transform())
+    src, sg = tile(s_)
+    del s_
+    torch.cuda.empty_cache()
+
+    def run(timings=None):
+        return D.pipeline_sharded(tgt, tg, src, sg, vs, knn=30, distance_threshold=0.002,
+                                  num_iterations=args.ransac_iters, seed=7, max_correspondence_distance=0.02,
+                                  icp_iterations=args.icp_iters, presorted=True, timings=timings)
+
+    run()  # warm
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    out = run()
+    barrier(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    stages = {}
+    run(stages)  # per-stage breakdown (synchronised stages; not the timed pass)
+    res = {"n": n, "voxel_size": vs, "ranks": world, "ms": round(el * 1e3, 3),
+           "Mpoints_per_s_target": round(n / el / 1e6, 2), "target_reps": out["target_reps"],
+           "source_reps": out["source_reps"], "plane": [round(float(v), 6) for v in out["plane"]],
+           "icp_fitness": round(out["fitness"], 6),
+           "T_err_vs_gt_inverse": float(np.abs(out["transformation"] - np.linalg.inv(synthetic.rigid_transform())).max()),
+           "stages_ms_rank0": stages,
+           "collectives": "all_reduce (bounds, counts, fx digit sums, halo proof), all_to_all (halo reps), "
+                          "all_gather (target reps + normals for the replicated ICP target)"}
+    del tgt, src, tg, sg, out
+    torch.cuda.empty_cache()
+    return {"c5_sharded": res}
 
 
 def kernel_table():
@@ -553,7 +635,7 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "scaling": None, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": "C2: uniform-random 10M pts float32, voxel_down_sample(vs=(4/N)^(1/3)) "
                                "+ estimate_normals(KNN30) on the representatives",
                    "n_points": N, "voxel_size": vs, "voxels": int(M), "knn": args.knn, "parallelism": "single"},
@@ -622,10 +704,13 @@ def main_multi(args, world, rank, dev):
     }
     torch.cuda.empty_cache()
     if not args.no_secondary:
-        try:
-            line["extra"].update(secondary_sharded_icp(dev, args, world, rank))
-        except RuntimeError as e:  # report, never hide
-            line["extra"]["secondary_error"] = str(e)
+        for name, fn in (("icp_sharded", lambda: secondary_sharded_icp(dev, args, world, rank)),
+                         ("c5", lambda: c5_sharded(dev, args, world, rank) if args.c5_n > 0 else {})):
+            try:
+                line["extra"].update(fn())
+            except RuntimeError as e:  # report, never hide
+                line["extra"][f"{name}_error"] = str(e)
+            torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(line), flush=True)
     dist.barrier()

@@ -56,49 +56,80 @@ __global__ void __launch_bounds__(kBlock) k_grid_scatter(const float* __restrict
 // Deterministic in-cell order (ascending original index; atomic ranks are
 // not): every point counts the points of its cell with a smaller index and
 // moves there — thread per point, O(cell size) reads each, all L2-local.
-// Cells above kRankCell points are copied as they are and sorted by
-// k_grid_cell_sort (serial insertion, only such cells).
+// Cells above kRankCell points are left to k_grid_big_cells (a workgroup per
+// such cell, listed on the device by their first point): the cell's indices
+// are staged in LDS tiles and each thread ranks its points against them, so a
+// cell of c points costs c^2 / 1024 LDS reads per thread instead of a serial
+// c^2 insertion sort (the round-2 cliff: 54 ms for a dense planted plane).
 constexpr int kRankCell = 256;
+constexpr int kBigTile = 8192;   // indices per LDS tile (32 KB)
+constexpr int kBigBlock = 1024;
 
 __global__ void __launch_bounds__(kBlock) k_grid_rank_fix(const float4* __restrict__ tmp,
                                                           const float4* __restrict__ tmp_extra, int64_t n,
                                                           const int32_t* __restrict__ cell,
                                                           const int32_t* __restrict__ start, float4* __restrict__ pts,
-                                                          float4* __restrict__ extra) {
+                                                          float4* __restrict__ extra, int32_t* __restrict__ big,
+                                                          int32_t* __restrict__ nbig) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
     const float4 v = tmp[p];
     const int i = __float_as_int(v.w);
     const int c = cell[i];
     const int s0 = start[c], s1 = start[c + 1];
-    int dst = (int)p;
-    if (s1 - s0 <= kRankCell) {
-      int r = 0;
-      for (int q = s0; q < s1; ++q) r += __float_as_int(tmp[q].w) < i ? 1 : 0;
-      dst = s0 + r;
+    if (s1 - s0 > kRankCell) {  // the cell's workgroup places it
+      if (p == s0) big[atomicAdd(nbig, 1)] = c;
+      continue;
     }
+    int r = 0;
+    for (int q = s0; q < s1; ++q) r += __float_as_int(tmp[q].w) < i ? 1 : 0;
+    const int dst = s0 + r;
     pts[dst] = v;
     if (extra) extra[dst] = tmp_extra[p];
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_grid_cell_sort(const int32_t* __restrict__ start, int64_t nc,
-                                                           float4* __restrict__ pts, float4* __restrict__ extra) {
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
-    int s0 = start[c], s1 = start[c + 1];
-    if (s1 - s0 <= kRankCell) continue;
-    for (int i = s0 + 1; i < s1; ++i) {
-      float4 v = pts[i];
-      float4 e = extra ? extra[i] : make_float4(0, 0, 0, 0);
-      int key = __float_as_int(v.w);
-      int j = i - 1;
-      while (j >= s0 && __float_as_int(pts[j].w) > key) {
-        pts[j + 1] = pts[j];
-        if (extra) extra[j + 1] = extra[j];
-        --j;
+__global__ void __launch_bounds__(kBigBlock) k_grid_big_cells(const float4* __restrict__ tmp,
+                                                              const float4* __restrict__ tmp_extra,
+                                                              const int32_t* __restrict__ start,
+                                                              const int32_t* __restrict__ big,
+                                                              const int32_t* __restrict__ nbig,
+                                                              float4* __restrict__ pts, float4* __restrict__ extra) {
+  __shared__ int32_t ids[kBigTile];
+  const int nb = *nbig;
+  for (int b = blockIdx.x; b < nb; b += gridDim.x) {
+    const int c = big[b];
+    const int s0 = start[c], s1 = start[c + 1];
+    const int m = s1 - s0;
+    constexpr int kPer = 8;  // points ranked per thread per round
+    for (int base = 0; base < m; base += kBigBlock * kPer) {
+      int key[kPer], r[kPer];
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int j = base + threadIdx.x + u * kBigBlock;
+        key[u] = j < m ? __float_as_int(tmp[s0 + j].w) : INT_MAX;
+        r[u] = 0;
       }
-      pts[j + 1] = v;
-      if (extra) extra[j + 1] = e;
+      for (int t0 = 0; t0 < m; t0 += kBigTile) {
+        const int tn = min(kBigTile, m - t0);
+        __syncthreads();
+        for (int j = threadIdx.x; j < tn; j += kBigBlock) ids[j] = __float_as_int(tmp[s0 + t0 + j].w);
+        __syncthreads();
+        for (int j = 0; j < tn; ++j) {
+          const int id = ids[j];  // broadcast read
+#pragma unroll
+          for (int u = 0; u < kPer; ++u) r[u] += id < key[u] ? 1 : 0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int j = base + threadIdx.x + u * kBigBlock;
+        if (j < m) {
+          pts[s0 + r[u]] = tmp[s0 + j];
+          if (extra) extra[s0 + r[u]] = tmp_extra[s0 + j];
+        }
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -278,10 +309,13 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
       float4* tmp_extra = extra_sorted ? (float4*)(w + L.tmp_extra) : nullptr;
       hipLaunchKernelGGL(k_grid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, G.cell, G.rank,
                          G.start, tmp, extra_src, tmp_extra);
+      // the big-cell list reuses the per-point rank array (free after the scatter)
+      int32_t* nbig = reinterpret_cast<int32_t*>(G.scratch + 1);
+      O3DX_HIP(hipMemsetAsync(nbig, 0, sizeof(int32_t), s));
       hipLaunchKernelGGL(k_grid_rank_fix, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, tmp, tmp_extra, n,
-                         G.cell, G.start, G.pts, extra_sorted);
-      hipLaunchKernelGGL(k_grid_cell_sort, dim3(grid_for(nc, kBlock, 8192)), dim3(kBlock), 0, s, G.start, nc, G.pts,
-                         extra_sorted);
+                         G.cell, G.start, G.pts, extra_sorted, G.rank, nbig);
+      hipLaunchKernelGGL(k_grid_big_cells, dim3(512), dim3(kBigBlock), 0, s, tmp, tmp_extra, G.start, G.rank, nbig,
+                         G.pts, extra_sorted);
     }
     O3DX_HIP(hipGetLastError());
     break;
@@ -1145,62 +1179,83 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
 // voxels occupied — any volumetric cloud after down-sampling).  No search
 // grid is built: the voxel table is the grid, at voxel granularity.
 //
-// One wave = one block of 4^3 voxels (lane = voxel, <= 64 queries).  The
-// block's box (the block + 3 voxels on every side, 10^3) is staged from the
-// table into LDS as dense SoA float32 slots (empty voxel: +inf, never inside
-// any bound).  Every lane scans a fixed ball-shaped stencil around its own
-// voxel: the 172 voxels (33 rows of 4-6) that can hold a point within 2.45
+// One workgroup = 2 x 2 waves, each wave a block of 4^3 voxels (lane = voxel
+// = query).  The workgroup's box (4 x 8 x 8 voxels + a 3-voxel margin) is
+// staged once from the table into LDS ((x, y) interleaved float2 + z apart;
+// empty voxel: +inf, never inside any bound).  Every lane scans a fixed
+// stencil around its own voxel: the voxels that can hold a point within R
 // voxels of a query in the upper half of its voxel along each axis, mirrored
 // per axis to the half the lane's query is in.  Row offsets and lengths are
-// compile-time constants (one base, one sign per axis), so the lanes never
-// diverge in the scans, and every point closer than R = 2.45 voxels (minus
-// the rounding slack) has been seen: at one rep per voxel that ball holds ~60
-// points, k = 30 lie within ~1.94 voxels.  Steps as the LDS tile above: count
-// over [0, R), locate / refine, list pass, exact finish (finish_selection).
-// Queries whose k-th neighbour lies beyond R (cloud borders) go, by voxel
-// index, to the wave form (from shell 3) and the register top-k over the table
-// itself (a dense GridView).
+// compile-time constants, so lanes never diverge in the scans.
+//   count   R = 2.2 voxels (148 voxels; the k = 30 neighbour of an interior
+//           query at one rep per voxel lies within 2.2 for all but ~1e-5 of
+//           them): f32 d^2 into 16 LDS bins over [(1.5 voxels)^2, R^2) (the
+//           k-th neighbour of a voxelised cloud is never that close in
+//           practice: bins where the k-th distances are; a k-th below them
+//           hands the query on);
+//   locate  the bin holding the k-th distance -> [L, U) (refined <= 2 times);
+//   list    rescan with the smallest of the R = 2.1 / 2.2 stencils (136 / 148
+//           voxels) that covers the wave's largest U, appending d^2 < U;
+//   finish  exact (d^2, index) selection (finish_selection), f64 moments,
+//           FastEigen3x3.
+// Queries whose k-th neighbour lies beyond R (cloud borders, sparse spots) go
+// by voxel index to the wave form and the register top-k over the table.
+// (Measured and dropped, DESIGN.md §4.1: a symmetric stencil, a merged
+// count+list pass, a list-first form, compact 1-byte lists, 1x1 / 2x3 blocks.)
 constexpr int kVB = 4;                     // block edge (voxels)
 constexpr int kVM = 3;                     // box margin (the stencil's reach in voxels)
 constexpr int kVE = kVB + 2 * kVM;         // box edge (10)
-constexpr double kStencilR = 2.45;         // completeness radius (voxels)
+constexpr double kStencilR = 2.2;          // completeness radius of the count stencil (voxels)
+constexpr double kListR = 2.1;             // the smaller list stencil (voxels)
+constexpr double kHistLo = 1.5;            // the count histogram's lower edge (voxels)
+constexpr double kWideR = 2.45;            // the border waves' stencil (voxels)
+constexpr int kEdge = 3;                   // border waves: within kEdge voxels of a table face
 
-// (dy, dz, x0, x1) in the oriented frame (query in [0.49, 1) of its voxel on
-// every axis): the voxels within kStencilR of any such query, generated by
-// tools/stencil_rows.py.
-#define O3DX_S25_ROWS(X)                                                                                     \
-  X(-2, -2, -1, 2) X(-1, -2, -2, 2) X(0, -2, -2, 2) X(1, -2, -2, 2) X(2, -2, -2, 2) X(-2, -1, -2, 2)         \
-  X(-1, -1, -2, 3) X(0, -1, -2, 3) X(1, -1, -2, 3) X(2, -1, -2, 3) X(3, -1, -1, 2) X(-2, 0, -2, 2)           \
-  X(-1, 0, -2, 3) X(0, 0, -2, 3) X(1, 0, -2, 3) X(2, 0, -2, 3) X(3, 0, -1, 2) X(-2, 1, -2, 2)                \
-  X(-1, 1, -2, 3) X(0, 1, -2, 3) X(1, 1, -2, 3) X(2, 1, -2, 3) X(3, 1, -1, 2) X(-2, 2, -2, 2)                \
-  X(-1, 2, -2, 3) X(0, 2, -2, 3) X(1, 2, -2, 3) X(2, 2, -2, 3) X(3, 2, -1, 2) X(-1, 3, -1, 2)                \
-  X(0, 3, -1, 2) X(1, 3, -1, 2) X(2, 3, -1, 2)
+struct SRow {
+  int dy, dz, xa, len;
+};
 
-// Symmetric stencil (no per-lane mirroring): the 179 voxels whose gap to the
-// query's own voxel is at most 2 voxels in the squared sense (gx^2 + gy^2 +
-// gz^2 <= 4, g = max(0, |d| - 1) per axis) — every point closer than sqrt(5)
-// voxels to any query in the voxel.  37 rows (dy, dz, x0, x1), identical for
-// every lane, so a wave's lanes read one padded box layout at lane-distinct
-// banks (see StileShape).  Generated like tools/stencil_rows.py.
-#define O3DX_SYM_ROWS(X)                                                                                    \
-  X(-1, -3, -1, 1) X(0, -3, -1, 1) X(1, -3, -1, 1) X(-2, -2, -2, 2) X(-1, -2, -2, 2) X(0, -2, -2, 2)        \
-  X(1, -2, -2, 2) X(2, -2, -2, 2) X(-3, -1, -1, 1) X(-2, -1, -2, 2) X(-1, -1, -3, 3) X(0, -1, -3, 3)       \
-  X(1, -1, -3, 3) X(2, -1, -2, 2) X(3, -1, -1, 1) X(-3, 0, -1, 1) X(-2, 0, -2, 2) X(-1, 0, -3, 3)          \
-  X(0, 0, -3, 3) X(1, 0, -3, 3) X(2, 0, -2, 2) X(3, 0, -1, 1) X(-3, 1, -1, 1) X(-2, 1, -2, 2)              \
-  X(-1, 1, -3, 3) X(0, 1, -3, 3) X(1, 1, -3, 3) X(2, 1, -2, 2) X(3, 1, -1, 1) X(-2, 2, -2, 2)              \
-  X(-1, 2, -2, 2) X(0, 2, -2, 2) X(1, 2, -2, 2) X(2, 2, -2, 2) X(-1, 3, -1, 1) X(0, 3, -1, 1)              \
-  X(1, 3, -1, 1)
-constexpr double kSymR2 = 5.0;  // completeness radius^2 of the symmetric stencil (voxels^2)
+// (dy, dz, x0, len) in the oriented frame (query in [0.49, 1) of its voxel on
+// every axis): the voxels within R of any such query (tools/stencil_rows.py)
+struct Stencil220 {
+  static constexpr SRow rows[] = {
+      {-2, -2, -1, 3}, {-1, -2, -2, 5}, {0, -2, -2, 5}, {1, -2, -2, 5}, {2, -2, -1, 4}, {-2, -1, -2, 5},
+      {-1, -1, -2, 6}, {0, -1, -2, 6},  {1, -1, -2, 6}, {2, -1, -2, 5}, {3, -1, -1, 3}, {-2, 0, -2, 5},
+      {-1, 0, -2, 6},  {0, 0, -2, 6},   {1, 0, -2, 6},  {2, 0, -2, 5},  {3, 0, -1, 3},  {-2, 1, -2, 5},
+      {-1, 1, -2, 6},  {0, 1, -2, 6},   {1, 1, -2, 6},  {2, 1, -2, 5},  {3, 1, -1, 3},  {-2, 2, -1, 4},
+      {-1, 2, -2, 5},  {0, 2, -2, 5},   {1, 2, -2, 5},  {2, 2, -2, 5},  {-1, 3, -1, 3}, {0, 3, -1, 3},
+      {1, 3, -1, 3}};
+  static constexpr int N = (int)(sizeof(rows) / sizeof(SRow));
+};
+struct Stencil245 {  // the waves at the cloud's borders (a wider ball keeps their k nearest in it)
+  static constexpr SRow rows[] = {
+      {-2, -2, -1, 4}, {-1, -2, -2, 5}, {0, -2, -2, 5}, {1, -2, -2, 5}, {2, -2, -2, 5}, {-2, -1, -2, 5},
+      {-1, -1, -2, 6}, {0, -1, -2, 6},  {1, -1, -2, 6}, {2, -1, -2, 6}, {3, -1, -1, 4}, {-2, 0, -2, 5},
+      {-1, 0, -2, 6},  {0, 0, -2, 6},   {1, 0, -2, 6},  {2, 0, -2, 6},  {3, 0, -1, 4},  {-2, 1, -2, 5},
+      {-1, 1, -2, 6},  {0, 1, -2, 6},   {1, 1, -2, 6},  {2, 1, -2, 6},  {3, 1, -1, 4},  {-2, 2, -2, 5},
+      {-1, 2, -2, 6},  {0, 2, -2, 6},   {1, 2, -2, 6},  {2, 2, -2, 6},  {3, 2, -1, 4},  {-1, 3, -1, 4},
+      {0, 3, -1, 4},   {1, 3, -1, 4},   {2, 3, -1, 4}};
+  static constexpr int N = (int)(sizeof(rows) / sizeof(SRow));
+};
+struct Stencil210 {
+  static constexpr SRow rows[] = {
+      {-1, -2, -1, 4}, {0, -2, -1, 4}, {1, -2, -1, 4}, {2, -2, -1, 4}, {-2, -1, -1, 4}, {-1, -1, -2, 5},
+      {0, -1, -2, 6},  {1, -1, -2, 6}, {2, -1, -2, 5}, {3, -1, 0, 2},  {-2, 0, -1, 4},  {-1, 0, -2, 6},
+      {0, 0, -2, 6},   {1, 0, -2, 6},  {2, 0, -2, 5},  {3, 0, -1, 3},  {-2, 1, -1, 4},  {-1, 1, -2, 6},
+      {0, 1, -2, 6},   {1, 1, -2, 6},  {2, 1, -2, 5},  {3, 1, -1, 3},  {-2, 2, -1, 4},  {-1, 2, -2, 5},
+      {0, 2, -2, 5},   {1, 2, -2, 5},  {2, 2, -2, 5},  {-1, 3, 0, 2},  {0, 3, -1, 3},   {1, 3, -1, 3}};
+  static constexpr int N = (int)(sizeof(rows) / sizeof(SRow));
+};
 
 struct DenseVox {
   const float4* __restrict__ vox;  // (x, y, z, bits(row)), row -1 = empty (0xFF fill: NaN coordinates)
   int nx, ny, nz;                  // voxel dims
-  int nbx, nby, nbz;               // 4^3 blocks
+  int nbx, nby, nbz;               // workgroup blocks
   float ox, oy, oz, vs, inv_vs;
-  float rc2;                       // completeness radius^2 (world, float32, shrunk by the slack)
-  float rc2w;                      // the same with the symmetric stencil's ring
-  float rt2;                       // k_normals_vlist: the list threshold (<= rc2)
-  int vl_hist;                     // k_normals_vlist: histogram during the scan (1) or over the list (0)
+  float rc2;                       // completeness radius^2 of the count stencil (world, f32, shrunk by the slack)
+  float rl2;                       // the same for the smaller list stencil
+  float rw2;                       // the same for the border waves' wider stencil
+  float hlo2;                      // the count histogram's lower edge (world d^2)
   unsigned long long* stats;       // debug counters (o3dx_search_stats) or null
   int32_t* nbr;                    // test hook (o3dx_set_debug_neighbors) or null
   float* kd2;                      // per row an upper bound of the k-th neighbour d^2, or null
@@ -1221,7 +1276,7 @@ __device__ __forceinline__ float4 dvox_load(const DenseVox& d, int x, int y, int
 // The row's loads are all issued before its first f (whose LDS atomics /
 // stores the compiler cannot move reads across).
 template <int L, class F>
-__device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int st, const float4 q, F&& f) {
+__device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int st, const float4 q, F& f) {
   float2 a[L];
   float c[L];
 #pragma unroll
@@ -1238,253 +1293,83 @@ __device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int
   if (L & 1) f(st + L - 1, dist2_f32(q, a[L - 1].x, a[L - 1].y, c[L - 1]));
 }
 
+// a scheduling fence per row keeps the unrolled stencil from hoisting every
+// row's loads (register pressure; the other waves hide the LDS latency)
+template <class St, int I, class F>
+__device__ __forceinline__ void mir_rows(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
+                                         const float4 q, F& f) {
+  if constexpr (I < St::N) {
+    constexpr SRow r = St::rows[I];
+    scan_run<r.len>(txy, tz, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)), q, f);
+    __builtin_amdgcn_sched_barrier(0);
+    mir_rows<St, I + 1>(txy, tz, qs, SY, SZ, xpos, q, f);
+  }
+}
+
 // The lane's stencil: qs = its own slot, SY / SZ = the y / z slot strides
 // signed by the orientation, xpos = x orientation.
-template <class F>
+template <class St, class F>
 __device__ __forceinline__ void stencil_scan(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
                                              const float4 q, F&& f) {
   // the row bases are recomputed per scan (laundered inputs): hoisted and
   // shared across the kernel's scans they would stay live throughout
   asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
-  // a scheduling fence per row keeps the unrolled stencil from hoisting every
-  // row's loads (register pressure; the other waves hide the LDS latency)
-#define O3DX_ROW(DY, DZ, XA, XB)                                                                   \
-  scan_run<(XB) - (XA) + 1>(txy, tz, qs + (DY) * SY + (DZ) * SZ + (xpos ? (XA) : -(XB)), q, f); \
-  __builtin_amdgcn_sched_barrier(0);
-  O3DX_S25_ROWS(O3DX_ROW)
-#undef O3DX_ROW
+  mir_rows<St, 0>(txy, tz, qs, SY, SZ, xpos, q, f);
 }
 
-// The symmetric stencil, compile-time strides: every lane reads the same
-// offsets from its own slot.  Software-pipelined by one row: row i+1's LDS
-// loads are issued before row i's distances (two register buffers of one
-// row), with a scheduling fence per row.  RING: the 72 voxels at gap^2 == 5
-// (56 short rows) that extend the completeness radius to sqrt 6 for the
-// lanes whose k-th neighbour lies beyond sqrt 5 (cloud borders).
-struct SRow {
-  int dy, dz, xa, len;
-};
-#define O3DX_SROW(DY, DZ, XA, XB) SRow{DY, DZ, XA, (XB) - (XA) + 1},
-constexpr SRow kSymRows[] = {O3DX_SYM_ROWS(O3DX_SROW)};
-#undef O3DX_SROW
-constexpr SRow kRingRows[] = {
-    {-2, -3, -1, 3}, {-1, -3, -2, 1}, {-1, -3, 2, 1}, {0, -3, -2, 1},  {0, -3, 2, 1},  {1, -3, -2, 1},
-    {1, -3, 2, 1},   {2, -3, -1, 3},  {-3, -2, -1, 3}, {-1, -2, -3, 1}, {-1, -2, 3, 1}, {0, -2, -3, 1},
-    {0, -2, 3, 1},   {1, -2, -3, 1},  {1, -2, 3, 1},  {3, -2, -1, 3},  {-3, -1, -2, 1}, {-3, -1, 2, 1},
-    {-2, -1, -3, 1}, {-2, -1, 3, 1},  {2, -1, -3, 1},  {2, -1, 3, 1},   {3, -1, -2, 1},  {3, -1, 2, 1},
-    {-3, 0, -2, 1},  {-3, 0, 2, 1},   {-2, 0, -3, 1},  {-2, 0, 3, 1},   {2, 0, -3, 1},   {2, 0, 3, 1},
-    {3, 0, -2, 1},   {3, 0, 2, 1},    {-3, 1, -2, 1},  {-3, 1, 2, 1},   {-2, 1, -3, 1},  {-2, 1, 3, 1},
-    {2, 1, -3, 1},   {2, 1, 3, 1},    {3, 1, -2, 1},   {3, 1, 2, 1},    {-3, 2, -1, 3},  {-1, 2, -3, 1},
-    {-1, 2, 3, 1},   {0, 2, -3, 1},   {0, 2, 3, 1},    {1, 2, -3, 1},   {1, 2, 3, 1},    {3, 2, -1, 3},
-    {-2, 3, -1, 3},  {-1, 3, -2, 1},  {-1, 3, 2, 1},   {0, 3, -2, 1},   {0, 3, 2, 1},    {1, 3, -2, 1},
-    {1, 3, 2, 1},    {2, 3, -1, 3}};
-constexpr double kSymWideR2 = 6.0;  // completeness radius^2 with the ring (voxels^2)
-constexpr int kRowMax = 7;
-
-template <bool RING>
-struct SymRows {
-  static constexpr int N = RING ? (int)(sizeof(kRingRows) / sizeof(SRow)) : (int)(sizeof(kSymRows) / sizeof(SRow));
-  static constexpr SRow at(int i) { return RING ? kRingRows[i] : kSymRows[i]; }
-};
-
-struct RowBuf {
-  float2 a[kRowMax];
-  float c[kRowMax];
-};
-
-template <bool RING, int I, int SY, int SZ>
-__device__ __forceinline__ RowBuf sym_load(const float2* txy, const float* tz, int qs) {
-  constexpr SRow r = SymRows<RING>::at(I);
-  constexpr int off = r.dy * SY + r.dz * SZ + r.xa;
-  RowBuf b;
-#pragma unroll
-  for (int i = 0; i < r.len; ++i) {
-    b.a[i] = txy[qs + off + i];
-    b.c[i] = tz[qs + off + i];
-  }
-  return b;
-}
-
-template <bool RING, int I, int SY, int SZ, class F>
-__device__ __forceinline__ void sym_rows(const float2* txy, const float* tz, int qs, const float4 q, RowBuf cur,
-                                         F& f) {
-  if constexpr (I < SymRows<RING>::N) {
-    RowBuf nxt;
-    if constexpr (I + 1 < SymRows<RING>::N) nxt = sym_load<RING, I + 1, SY, SZ>(txy, tz, qs);
-    constexpr SRow r = SymRows<RING>::at(I);
-    constexpr int off = r.dy * SY + r.dz * SZ + r.xa;
-#pragma unroll
-    for (int i = 0; i + 1 < r.len; i += 2) {
-      const f32x2 dd = dist2_pair(q, (f32x2){cur.a[i].x, cur.a[i + 1].x}, (f32x2){cur.a[i].y, cur.a[i + 1].y},
-                                  (f32x2){cur.c[i], cur.c[i + 1]});
-      f(qs + off + i, dd.x);
-      f(qs + off + i + 1, dd.y);
-    }
-    if constexpr (r.len & 1) f(qs + off + r.len - 1, dist2_f32(q, cur.a[r.len - 1].x, cur.a[r.len - 1].y, cur.c[r.len - 1]));
-    __builtin_amdgcn_sched_barrier(0);
-    sym_rows<RING, I + 1, SY, SZ>(txy, tz, qs, q, nxt, f);
-  }
-}
-
-// The mirrored stencil with a stencil position per candidate (compact lists,
-// k_normals_stile<..., CL = true>): position P0(row) + i of row (dy, dz, xa..xb)
-// is slot qs + dy*SY + dz*SZ + (xpos ? xa + i : -xb + i), so a 1-byte list
-// entry (172 positions) replaces the 16-bit LDS slot; s25_slot decodes it
-// from the per-block table of (dy, dz, xa + i, -xb + i) bytes.
-constexpr SRow kS25Rows[] = {
-#define O3DX_SROW(DY, DZ, XA, XB) SRow{DY, DZ, XA, (XB) - (XA) + 1},
-    O3DX_S25_ROWS(O3DX_SROW)
-#undef O3DX_SROW
-};
-constexpr int kS25N = (int)(sizeof(kS25Rows) / sizeof(SRow));
-constexpr int s25_pos0(int i) {
-  int p = 0;
-  for (int j = 0; j < i; ++j) p += kS25Rows[j].len;
-  return p;
-}
-constexpr int kS25Pos = s25_pos0(kS25N);
-static_assert(kS25Pos <= 256, "stencil positions must fit a byte");
-
-__device__ __forceinline__ int32_t s25_entry(int p) {  // host of the per-block table
-  int r = 0;
-  while (r + 1 < kS25N && s25_pos0(r + 1) <= p) ++r;
-  const SRow w = kS25Rows[r];
-  const int i = p - s25_pos0(r);
-  return (int32_t)((uint32_t)(w.dy & 0xFF) | ((uint32_t)(w.dz & 0xFF) << 8) | ((uint32_t)((w.xa + i) & 0xFF) << 16) |
-                   ((uint32_t)((i - (w.xa + w.len - 1)) & 0xFF) << 24));
-}
-
-__device__ __forceinline__ int s25_slot(int32_t e, int qs, int SY, int SZ, bool xpos) {
-  const int dy = __builtin_amdgcn_sbfe(e, 0, 8), dz = __builtin_amdgcn_sbfe(e, 8, 8);
-  const int dx = xpos ? __builtin_amdgcn_sbfe(e, 16, 8) : (e >> 24);
-  return qs + dy * SY + dz * SZ + dx;
-}
-
-template <int L, int P0, class F>
-__device__ __forceinline__ void scan_run_p(const float2* txy, const float* tz, int st, const float4 q, F& f) {
-  float2 a[L];
-  float c[L];
-#pragma unroll
-  for (int i = 0; i < L; ++i) {
-    a[i] = txy[st + i];
-    c[i] = tz[st + i];
-  }
-#pragma unroll
-  for (int i = 0; i + 1 < L; i += 2) {
-    const f32x2 dd = dist2_pair(q, (f32x2){a[i].x, a[i + 1].x}, (f32x2){a[i].y, a[i + 1].y}, (f32x2){c[i], c[i + 1]});
-    f(P0 + i, st + i, dd.x);
-    f(P0 + i + 1, st + i + 1, dd.y);
-  }
-  if (L & 1) f(P0 + L - 1, st + L - 1, dist2_f32(q, a[L - 1].x, a[L - 1].y, c[L - 1]));
-}
-
-template <int I, class F>
-__device__ __forceinline__ void s25_rows(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
-                                         const float4 q, F& f) {
-  if constexpr (I < kS25N) {
-    constexpr SRow r = kS25Rows[I];
-    scan_run_p<r.len, s25_pos0(I)>(txy, tz, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)), q, f);
-    __builtin_amdgcn_sched_barrier(0);
-    s25_rows<I + 1>(txy, tz, qs, SY, SZ, xpos, q, f);
-  }
-}
-
-// stencil_scan with f(position, slot, d2)
-template <class F>
-__device__ __forceinline__ void stencil_scan_p(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
-                                               const float4 q, F&& f) {
-  asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
-  s25_rows<0>(txy, tz, qs, SY, SZ, xpos, q, f);
-}
-
-template <bool RING, int SY, int SZ, class F>
-__device__ __forceinline__ void stencil_scan_sym(const float2* txy, const float* tz, int qs, const float4 q, F&& f) {
-  asm volatile("" : "+v"(qs));
-  sym_rows<RING, 0, SY, SZ>(txy, tz, qs, q, sym_load<RING, 0, SY, SZ>(txy, tz, qs), f);
-}
-
-// Block shapes: WY x WZ waves, each wave a 4^3 voxel block; the block's box is
+// Block shape: WY x WZ waves, each wave a 4^3 voxel block; the block's box is
 // the union (4 x 4WY x 4WZ voxels + the 3-voxel margin), staged once for all
 // its waves — 2x2 waves stage 7.7 slots per query instead of 15.6 and fit
-// 3 blocks (12 waves) per CU in LDS instead of 8 single-wave blocks.
-// PAD (the symmetric stencil's layout): row pitch 12 slots and a plane pitch
-// = 16 (mod 32) slots, so for any stencil offset the 16 lanes (lx, ly) of one
-// z layer hit 16 distinct float2 bank pairs (2 (lx + 12 ly) mod 32 distinct:
-// ds_read2_b64's 4 x 16 groups) and the 32 lanes of two layers 32 distinct
-// float banks (lx + 12 ly + 16 lz mod 32: ds_read_b32's 2 x 32 groups).
-template <int WY, int WZ, bool PAD = false>
+// 3 workgroups (12 waves) per CU in LDS.
+template <int WY, int WZ>
 struct StileShape {
   static constexpr int NW = WY * WZ;
   static constexpr int EY = kVB * WY + 2 * kVM, EZ = kVB * WZ + 2 * kVM;
-  static constexpr int SY = PAD ? 12 : kVE;
-  static constexpr int SZ = PAD ? SY * EY + (48 - (SY * EY) % 32) % 32 : kVE * EY;
-  static constexpr int CELLS = kVE * EY * EZ;  // logical box cells
-  static constexpr int SLOTS = SZ * EZ;        // LDS slots (padded)
-  static_assert(!PAD || SZ % 32 == 16, "plane pitch must be 16 mod 32");
+  static constexpr int SY = kVE;
+  static constexpr int SZ = kVE * EY;
+  static constexpr int CELLS = kVE * EY * EZ;  // box cells = LDS slots
 };
 
-// MERGED: the histogram pass also appends every candidate below T2 = 3/4 R2 to
-// the list (at one rep per voxel the k = 30 band lies below it for all but
-// ~0.1 % of the queries, and <= 52 points do); the list pass then only runs
-// for lanes whose Up exceeds T2 or whose list overflowed.  Saves the second
-// stencil scan (3 LDS reads per candidate); the histogram gets its own LDS.
-constexpr int kMergedCap = 56;
-constexpr float kMergedFrac = 0.75f;
-
-// WPE: waves per SIMD to register-allocate for (LDS allows 2 for 1x1, 3 for 2x2)
-// CL (compact LDS, mirrored stencil only): list entries are 1-byte stencil
-// positions (decoded through the per-block table ptab) and the histogram
-// counters are packed 16-bit — a 2x2 workgroup then needs 36 KB instead of
-// 50 KB, so 4 workgroups (16 waves) fit a CU instead of 3.
-template <int KMAX, int WY, int WZ, int WPE, bool MERGED, bool SYM, bool CL = false>
+// WPE: waves per SIMD to register-allocate for (LDS allows 3 for 2x2)
+template <int KMAX, int WY, int WZ, int WPE>
 __global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
                 int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
-  static_assert(!CL || (!SYM && !MERGED), "compact lists: mirrored two-scan form only");
-  using Sh = StileShape<WY, WZ, SYM>;
-  using LT = typename std::conditional<CL, uint8_t, uint16_t>::type;
-  constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::SLOTS;
+  using Sh = StileShape<WY, WZ>;
+  constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::CELLS;
   __shared__ float2 txy[kSlots];
   __shared__ float tz[kSlots];
-  __shared__ int32_t ptab[CL ? kS25Pos : 1];
   // list capacity: the k - 1 points below the k-th bin + that bin (<= kRefineAt
-  // after refinement) + the rounding band; the symmetric layout trims it to
-  // KMAX + 12 so three 2x2 workgroups still fit a CU's LDS
-  constexpr int kListMax = KMAX + (SYM ? 12 : kBndCap);
-  constexpr int kListRows = MERGED && kMergedCap > kListMax ? kMergedCap + 1 : kListMax + 1;
-  constexpr int kListWords = (kListRows * 64 * (int)sizeof(LT) + 3) / 4;
-  constexpr int kHistWords = (CL ? (kTileSlots + 1) / 2 : kTileSlots) * 64;
-  constexpr int kSelWords = MERGED ? kListWords : (kListWords > kHistWords ? kListWords : kHistWords);
+  // after refinement) + the rounding band
+  constexpr int kListMax = KMAX + kBndCap;
+  constexpr int kListWords = ((kListMax + 1) * 64 * (int)sizeof(uint16_t) + 3) / 4;
+  constexpr int kHistWords = kTileSlots * 64;
+  constexpr int kSelWords = kListWords > kHistWords ? kListWords : kHistWords;
   __shared__ uint32_t selbuf[Sh::NW][kSelWords];
-  __shared__ uint32_t histbuf[MERGED ? Sh::NW : 1][MERGED ? kHistWords : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  LT(*lst)[64] = reinterpret_cast<LT(*)[64]>(selbuf[wv]);
-  uint32_t* hw = MERGED ? histbuf[MERGED ? wv : 0] : selbuf[wv];
+  uint16_t(*lst)[64] = reinterpret_cast<uint16_t(*)[64]>(selbuf[wv]);
+  uint32_t* hw = selbuf[wv];
   const int nb = d.nbx * d.nby * d.nbz;
   const int b = xcd_block(blockIdx.x, nb);
   const int bx = b % d.nbx, by = (b / d.nbx) % d.nby, bz = b / (d.nbx * d.nby);
   const int gx0 = bx * kVB - kVM, gy0 = by * (kVB * WY) - kVM, gz0 = bz * (kVB * WZ) - kVM;  // box origin
   {
     constexpr int kT = 64 * Sh::NW;
-    constexpr int kCells = Sh::CELLS;
-    constexpr int J = (kCells + kT - 1) / kT;
+    constexpr int J = (kSlots + kT - 1) / kT;
     float4 buf[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int t = threadIdx.x + kT * j;
-      if (t < kCells) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kVE) % Sh::EY, gz0 + t / (kVE * Sh::EY));
+      if (t < kSlots) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kVE) % Sh::EY, gz0 + t / (kVE * Sh::EY));
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int t = threadIdx.x + kT * j;
-      if (t < kCells) {
-        const int a = t % kVE + kSY * ((t / kVE) % Sh::EY) + kSZ * (t / (kVE * Sh::EY));
-        txy[a] = make_float2(buf[j].x, buf[j].y);
-        tz[a] = buf[j].z;
+      if (t < kSlots) {
+        txy[t] = make_float2(buf[j].x, buf[j].y);
+        tz[t] = buf[j].z;
       }
     }
-    if constexpr (CL)
-      for (int t = threadIdx.x; t < kS25Pos; t += kT) ptab[t] = s25_entry(t);
   }
   __syncthreads();
   const int lx = lane & 3, ly = ((lane >> 2) & 3) + kVB * (wv % WY), lz = (lane >> 4) + kVB * (wv / WY);
@@ -1504,405 +1389,44 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
     if (q.x == 12345.f) out[0] = 0.f;
     return;
   }
-  if (!fb) {
-    float R2 = d.rc2;
-    const float T2 = R2 * kMergedFrac;
-    int nl = 0;  // MERGED: candidates below T2 appended by the first pass
-    bool wide = false;  // SYM: the gap^2 == 5 ring is scanned too (k-th neighbour beyond sqrt 5)
-    // body(stencil position, LDS slot, f32 d^2); the position is only known
-    // (compile-time) to the compact-list scan
-    auto scan = [&](auto&& body) {
-      if constexpr (SYM) {
-        auto b3 = [&](int pp, float d2) { body(0, pp, d2); };
-        stencil_scan_sym<false, kSY, kSZ>(txy, tz, qs, q, b3);
-        if (wide) stencil_scan_sym<true, kSY, kSZ>(txy, tz, qs, q, b3);
-      } else if constexpr (CL) {
-        stencil_scan_p(txy, tz, qs, SY, SZ, xpos, q, body);
-      } else {
-        stencil_scan(txy, tz, qs, SY, SZ, xpos, q, [&](int pp, float d2) { body(0, pp, d2); });
-      }
-    };
-    TileHist th;
-    auto hist = [&](float lo_, float sc_, auto app) {
-      constexpr int kHW = CL ? (kTileSlots + 1) / 2 : kTileSlots;
-#pragma unroll
-      for (int i = 0; i < kHW; ++i) hw[i * 64 + lane] = 0u;
-      const float off_ = -lo_ * sc_;
-      auto body = [&](int ps, int pp, float d2) {
-        const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f);
-        if constexpr (CL)
-          atomicAdd(&hw[((ix + 1) >> 1) * 64 + lane], 1u << (((ix + 1) & 1) * 16));
-        else
-          atomicAdd(&hw[(ix + 1) * 64 + lane], 1u);
-        if constexpr (decltype(app)::value) {
-          lst[min(nl, kMergedCap)][lane] = (LT)pp;
-          nl += d2 < T2 ? 1 : 0;
-        }
-      };
-      scan(body);
-      if constexpr (CL) {
-#pragma unroll
-        for (int i = 0; i < kTileSlots; i += 2) {
-          const uint32_t w = hw[(i >> 1) * 64 + lane];
-          th.h[i] = w & 0xFFFFu;
-          if (i + 1 < kTileSlots) th.h[i + 1] = w >> 16;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
-      }
-    };
-    hist(0.0f, (float)kHistBins / R2, std::integral_constant<bool, MERGED>{});
-    int total = 0;
-#pragma unroll
-    for (int i = 0; i < kHistBins; ++i) total += th.count(i);
-    if (SYM && !MERGED && total < kneed) {  // border lanes: widen to the ring (sqrt 6)
-      wide = true;
-      R2 = d.rc2w;
-      hist(0.0f, (float)kHistBins / R2, std::false_type{});
-      total = 0;
-#pragma unroll
-      for (int i = 0; i < kHistBins; ++i) total += th.count(i);
-    }
-    fb = total < kneed;
-    if (fb && d.stats) atomicAdd(&d.stats[7], 1ull);
-    float lo = 0.f, hi = R2, L = 0.f, U = 0.f;
-    for (int lvl = 0; !fb; ++lvl) {
-      int cum, cb;
-      if (!hist_locate(th, kneed, th.count(-1), lo, hi, &L, &U, &cum, &cb)) {
-        fb = true;
-        break;
-      }
-      if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
-      lo = L;
-      hi = U;
-      hist(lo, (float)kHistBins / (hi - lo), std::false_type{});
-    }
-    if (dbg == 2) {
-      if (L == 12345.f) out[0] = 0.f;
-      return;
-    }
-    if (!fb) {
-      const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
-      // the merged list holds every candidate below T2 >= Up (the rest of it,
-      // Up <= d2 < T2, is skipped by finish_selection)
-      const bool have = MERGED && Up <= T2 && nl <= kMergedCap;
-      int n = nl, cap = kMergedCap;
-      if (!have) {
-        n = 0;
-        cap = kListMax;
-        auto body = [&](int ps, int pp, float d2) {
-          if (d2 < Up) {  // masked store: only the accepted lanes take part in the LDS banking
-            lst[min(n, kListMax)][lane] = (LT)(CL ? ps : pp);
-            ++n;
-          }
-        };
-        scan(body);
-      }
-      if (dbg == 3) {
-        if (n == 12345) out[0] = 0.f;
-        return;
-      }
-      if (n > cap && d.stats) atomicAdd(&d.stats[5], 1ull);
-      // list entry -> LDS slot (compact lists: decode the stencil position)
-      auto slot = [&](int p) { return CL ? s25_slot(ptab[p], qs, SY, SZ, xpos) : p; };
-      fb = n > cap ||
-           !finish_selection<KMAX>(
-               q, kneed, n, Lm, U, lst, lane,
-               [&](int p) {
-                 const int sp = slot(p);
-                 return make_float4(txy[sp].x, txy[sp].y, tz[sp], 0.f);
-               },
-               prior, oi, out, d.nbr,
-               [&](int p0) {
-                 const int p = slot(p0);
-                 const int bz = p / kSZ, r = p - bz * kSZ, by = r / kSY, bx = r - by * kSY;
-                 return __float_as_int(
-                     d.vox[(gx0 + bx) + (int64_t)d.nx * ((gy0 + by) + (int64_t)d.ny * (gz0 + bz))].w);
-               },
-               d.kd2, dbg == 4);
-    }
-  }
-  if (fb) {
-    if (d.stats) atomicAdd(&d.stats[4], 1ull);
-    const int at = atomicAdd(fb_len, 1);
-    fb_list[at] = (int32_t)vq;
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// KNN normals off the dense voxel table, list-first form (k_normals_vlist).
-//
-// The staged box and the stencils are those of k_normals_stile; the selection
-// is reordered so the per-candidate work is one scan instead of two, and the
-// LDS histogram atomics (the count pass' cost) run over a short list instead
-// of the whole stencil:
-//   1. scan — every stencil candidate with f32 d^2 < T (T = (1.14 x the
-//      expected k-th distance)^2, below the stencil's completeness radius) is
-//      appended to the lane's list as its 1-byte stencil position; at one rep
-//      per voxel that is ~1.5 k entries (<= kVCap).  The set {d^2 < T} is
-//      complete, so with >= k entries it contains the k nearest;
-//   2. lanes with fewer than k entries (cloud borders) rescan with T = the
-//      completeness radius (the symmetric stencil adds its ring); lanes still
-//      short, or over the cap, hand off to the wave form;
-//   3. select — a 16-bin histogram of the list over [0, T) (packed 8-bit LDS
-//      counters, one dword column per lane), locate / refine over the list;
-//   4. finish_selection over the list (exact f64 (d^2, index) order at the
-//      band), f64 moments, FastEigen3x3 — as the other forms.
-// Stencil position -> LDS slot through a 1-KB table staged per workgroup.
-constexpr int kVCap = 63;     // list capacity (entries); 64 rows of u8
-constexpr int kPHWords = 5;   // packed histogram: 18 slots x 8 bit
-
-#define O3DX_SROW2(DY, DZ, XA, XB) SRow{DY, DZ, XA, (XB) - (XA) + 1},
-constexpr SRow kMirRows[] = {O3DX_S25_ROWS(O3DX_SROW2)};
-#undef O3DX_SROW2
-
-// S: 0 = mirrored 172-voxel stencil, 1 = symmetric 179, 2 = symmetric + ring (251)
-template <int S>
-struct StDef {
-  static constexpr int NM = (int)(sizeof(kMirRows) / sizeof(SRow));
-  static constexpr int NS = (int)(sizeof(kSymRows) / sizeof(SRow));
-  static constexpr int NR = (int)(sizeof(kRingRows) / sizeof(SRow));
-  static constexpr int N = S == 0 ? NM : S == 1 ? NS : NS + NR;
-  static constexpr SRow at(int i) { return S == 0 ? kMirRows[i] : (i < NS ? kSymRows[i] : kRingRows[i - NS]); }
-  static constexpr int pos0(int i) {
-    int p = 0;
-    for (int j = 0; j < i; ++j) p += at(j).len;
-    return p;
-  }
-  static constexpr int NPOS = pos0(N);
-};
-
-// Position table: symmetric stencils -> the slot offset at the padded layout
-// (SY, SZ); mirrored -> (dy, dz, x) as signed bytes, the lane applies its signs.
-template <int S, int SY, int SZ>
-struct PosTab {
-  int32_t v[StDef<S>::NPOS];
-};
-template <int S, int SY, int SZ>
-constexpr PosTab<S, SY, SZ> make_postab() {
-  PosTab<S, SY, SZ> t{};
-  int p = 0;
-  for (int i = 0; i < StDef<S>::N; ++i) {
-    const SRow r = StDef<S>::at(i);
-    for (int x = r.xa; x < r.xa + r.len; ++x, ++p) {
-      if (S == 0)
-        t.v[p] = (int32_t)((uint32_t)(r.dy & 0xff) | ((uint32_t)(r.dz & 0xff) << 8) | ((uint32_t)(x & 0xff) << 16));
-      else
-        t.v[p] = r.dy * SY + r.dz * SZ + x;
-    }
-  }
-  return t;
-}
-template <int S, int SY, int SZ>
-__constant__ PosTab<S, SY, SZ> c_postab = make_postab<S, SY, SZ>();
-
-// the lane's stencil frame: own slot + (mirrored stencil) signed strides
-struct LaneFrame {
-  int qs, sy, sz;
-  bool xpos;
-};
-
-template <int S, int I, int SY, int SZ>
-__device__ __forceinline__ int st_row_start(const LaneFrame& fr) {
-  constexpr SRow r = StDef<S>::at(I);
-  if constexpr (S == 0) return fr.qs + r.dy * fr.sy + r.dz * fr.sz + (fr.xpos ? r.xa : -(r.xa + r.len - 1));
-  else return fr.qs + r.dy * SY + r.dz * SZ + r.xa;
-}
-
-template <int S, int I, int SY, int SZ>
-__device__ __forceinline__ RowBuf st_load(const float2* txy, const float* tz, const LaneFrame& fr) {
-  constexpr SRow r = StDef<S>::at(I);
-  const int st = st_row_start<S, I, SY, SZ>(fr);
-  RowBuf b;
-#pragma unroll
-  for (int i = 0; i < r.len; ++i) {
-    b.a[i] = txy[st + i];
-    b.c[i] = tz[st + i];
-  }
-  return b;
-}
-
-// f(position, d2) over rows [I, END) of stencil S, pipelined by one row
-template <int S, int I, int END, int SY, int SZ, class F>
-__device__ __forceinline__ void st_rows(const float2* txy, const float* tz, const LaneFrame& fr, const float4 q,
-                                        RowBuf cur, F& f) {
-  if constexpr (I < END) {
-    RowBuf nxt;
-    if constexpr (I + 1 < END) nxt = st_load<S, I + 1, SY, SZ>(txy, tz, fr);
-    constexpr SRow r = StDef<S>::at(I);
-    constexpr int p0 = StDef<S>::pos0(I);
-    auto pos = [&](int i) { return (S == 0 && !fr.xpos) ? p0 + r.len - 1 - i : p0 + i; };
-#pragma unroll
-    for (int i = 0; i + 1 < r.len; i += 2) {
-      const f32x2 dd = dist2_pair(q, (f32x2){cur.a[i].x, cur.a[i + 1].x}, (f32x2){cur.a[i].y, cur.a[i + 1].y},
-                                  (f32x2){cur.c[i], cur.c[i + 1]});
-      f(pos(i), dd.x);
-      f(pos(i + 1), dd.y);
-    }
-    if constexpr (r.len & 1) f(pos(r.len - 1), dist2_f32(q, cur.a[r.len - 1].x, cur.a[r.len - 1].y, cur.c[r.len - 1]));
-    __builtin_amdgcn_sched_barrier(0);
-    st_rows<S, I + 1, END, SY, SZ>(txy, tz, fr, q, nxt, f);
-  }
-}
-
-template <int S, int BEGIN, int END, int SY, int SZ, class F>
-__device__ __forceinline__ void st_scan(const float2* txy, const float* tz, LaneFrame fr, const float4 q, F&& f) {
-  asm volatile("" : "+v"(fr.qs), "+v"(fr.sy), "+v"(fr.sz));  // row bases recomputed per scan
-  st_rows<S, BEGIN, END, SY, SZ>(txy, tz, fr, q, st_load<S, BEGIN, SY, SZ>(txy, tz, fr), f);
-}
-
-template <int KMAX, int WY, int WZ, int WPE, bool SYM>
-__global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
-k_normals_vlist(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
-                int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb) {
-  using Sh = StileShape<WY, WZ, SYM>;
-  constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::SLOTS;
-  constexpr int S0 = SYM ? 1 : 0;              // the scan's stencil
-  constexpr int SW = SYM ? 2 : 0;              // the border rescan's stencil
-  constexpr int NPOS = StDef<SW>::NPOS;        // the position table covers both
-  static_assert(NPOS <= 256, "u8 stencil positions");
-  __shared__ float2 txy[kSlots];
-  __shared__ float tz[kSlots];
-  __shared__ int32_t ptab[NPOS];
-  __shared__ uint8_t lists[Sh::NW][kVCap + 1][64];
-  __shared__ uint32_t hists[Sh::NW][kPHWords * 64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint8_t(*l8)[64] = lists[wv];
-  uint32_t* hw = hists[wv];
-  const int nb = d.nbx * d.nby * d.nbz;
-  const int b = xcd_block(blockIdx.x, nb);
-  const int bx = b % d.nbx, by = (b / d.nbx) % d.nby, bz = b / (d.nbx * d.nby);
-  const int gx0 = bx * kVB - kVM, gy0 = by * (kVB * WY) - kVM, gz0 = bz * (kVB * WZ) - kVM;  // box origin
-  {
-    constexpr int kT = 64 * Sh::NW;
-    constexpr int kCells = Sh::CELLS;
-    constexpr int J = (kCells + kT - 1) / kT;
-    float4 buf[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int t = threadIdx.x + kT * j;
-      if (t < kCells) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kVE) % Sh::EY, gz0 + t / (kVE * Sh::EY));
-    }
-    for (int t = threadIdx.x; t < NPOS; t += kT) ptab[t] = c_postab<SW, kSY, kSZ>.v[t];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int t = threadIdx.x + kT * j;
-      if (t < kCells) {
-        const int a = t % kVE + kSY * ((t / kVE) % Sh::EY) + kSZ * (t / (kVE * Sh::EY));
-        txy[a] = make_float2(buf[j].x, buf[j].y);
-        tz[a] = buf[j].z;
-      }
-    }
-  }
-  __syncthreads();
-  const int lx = lane & 3, ly = ((lane >> 2) & 3) + kVB * (wv % WY), lz = (lane >> 4) + kVB * (wv / WY);
-  LaneFrame fr;
-  fr.qs = (lx + kVM) + kSY * (ly + kVM) + kSZ * (lz + kVM);
-  const float4 q = make_float4(txy[fr.qs].x, txy[fr.qs].y, tz[fr.qs], 0.0f);
-  if (!(q.x < INFINITY)) return;  // empty voxel or outside the grid: no query (no barrier follows)
-  const int vx = gx0 + kVM + lx, vy = gy0 + kVM + ly, vz = gz0 + kVM + lz;
-  const int64_t vq = vx + (int64_t)d.nx * (vy + (int64_t)d.ny * vz);
-  const int oi = __float_as_int(d.vox[vq].w);
-  if constexpr (!SYM) {  // orientation: the half of its voxel the query lies in, per axis
-    fr.xpos = (q.x - (d.ox + (float)vx * d.vs)) * d.inv_vs >= 0.5f;
-    fr.sy = (q.y - (d.oy + (float)vy * d.vs)) * d.inv_vs >= 0.5f ? kSY : -kSY;
-    fr.sz = (q.z - (d.oz + (float)vz * d.vs)) * d.inv_vs >= 0.5f ? kSZ : -kSZ;
-  } else {
-    fr.xpos = true;
-    fr.sy = kSY;
-    fr.sz = kSZ;
-  }
-  // stencil position -> LDS slot
-  auto slot_of = [&](int p) {
-    const int32_t t = ptab[p];
-    if constexpr (SYM) {
-      return fr.qs + t;
-    } else {
-      const int dy = (int)(int8_t)(t & 0xff), dz = (int)(int8_t)((t >> 8) & 0xff), x = (int)(int8_t)((t >> 16) & 0xff);
-      return fr.qs + __mul24(dy, fr.sy) + __mul24(dz, fr.sz) + (fr.xpos ? x : -x);
-    }
-  };
-  bool fb = force_fb != 0;  // force_fb: tests of the hand-off path
-  float T = d.rt2;
-  int n = 0;
-  bool hist_ok = false;  // the scan's own histogram over [0, T) is valid
-  TileHist th;
-  if (!fb) {
-#pragma unroll
-    for (int w = 0; w < kPHWords; ++w) hw[w * 64 + lane] = 0u;
-    const float sc0 = (float)kHistBins / T;
-    // append + histogram in one scan (slot 17 = at or beyond T); the packed
-    // 8-bit counters cannot carry: a stencil holds <= 251 candidates and only
-    // slot 17 (the top byte's lower neighbour is unused) can exceed the cap
-    auto app_hist = [&](int p, float d2) {
-      const int ix = (int)fminf(fmaf(d2, sc0, 0.0f), 16.0f) + 1;
-      atomicAdd(&hw[(ix >> 2) * 64 + lane], 1u << ((ix & 3) << 3));
-      if (d2 < T) {  // masked store: only the accepting lanes take part
-        l8[min(n, kVCap)][lane] = (uint8_t)p;
-        ++n;
-      }
-    };
-    auto app = [&](int p, float d2) {
-      if (d2 < T) {
-        l8[min(n, kVCap)][lane] = (uint8_t)p;
-        ++n;
-      }
-    };
-    if (d.vl_hist) {
-      st_scan<S0, 0, StDef<S0>::N, kSY, kSZ>(txy, tz, fr, q, app_hist);
-      hist_ok = true;
-    } else {
-      st_scan<S0, 0, StDef<S0>::N, kSY, kSZ>(txy, tz, fr, q, app);
-    }
-    if (n < kneed) {  // cloud borders: the complete stencil (+ its ring)
-      T = SYM ? d.rc2w : d.rc2;
-      n = 0;
-      hist_ok = false;
-      st_scan<SW, 0, StDef<SW>::N, kSY, kSZ>(txy, tz, fr, q, app);
-    }
-    fb = n < kneed || n > kVCap;
-    if (fb && d.stats) atomicAdd(&d.stats[n < kneed ? 7 : 5], 1ull);
-  }
+  // waves within kEdge voxels of a table face (the cloud's borders of a
+  // volumetric cloud) scan the wider 2.45-voxel stencil: there the 2.2 ball is
+  // cut by the border and would hand many queries on; a wave-uniform choice
+  const int wx0 = gx0 + kVM, wy0 = gy0 + kVM + kVB * (wv % WY), wz0 = gz0 + kVM + kVB * (wv / WY);
+  const bool wide = wx0 < kEdge || wy0 < kEdge || wz0 < kEdge || wx0 + kVB > d.nx - kEdge ||
+                    wy0 + kVB > d.ny - kEdge || wz0 + kVB > d.nz - kEdge;
   float L = 0.f, U = 0.f;
   if (!fb) {
-    // histogram of the list over [lo, hi) (packed 8-bit counters; <= kVCap entries)
-    auto list_hist = [&](float lo_, float hi_) {
-      const float sc_ = (float)kHistBins / (hi_ - lo_), off_ = -lo_ * sc_;
+    const float R2 = wide ? d.rw2 : d.rc2;
+    TileHist th;
+    float lo = d.hlo2, hi = R2;
+    for (int lvl = 0;; ++lvl) {
+      // histogram over [lo, hi): slot = bin + 1 (0: below lo, 17: at or above hi);
+      // the +1 rides in the fma
 #pragma unroll
-      for (int w = 0; w < kPHWords; ++w) hw[w * 64 + lane] = 0u;
-      for (int j = 0; j < n; j += 4) {
-        int sl[4];
+      for (int i = 0; i < kTileSlots; ++i) hw[i * 64 + lane] = 0u;
+      const float sc_ = (float)kHistBins / (hi - lo), off_ = 1.0f - lo * sc_;
+      auto body = [&](int, float d2) {
+        const int ix = (int)__builtin_amdgcn_fmed3f(fmaf(d2, sc_, off_), 0.0f, 17.0f);
+        atomicAdd(&hw[ix * 64 + lane], 1u);
+      };
+      if (wide)
+        stencil_scan<Stencil245>(txy, tz, qs, SY, SZ, xpos, q, body);
+      else
+        stencil_scan<Stencil220>(txy, tz, qs, SY, SZ, xpos, q, body);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) sl[u] = slot_of(l8[min(j + u, n - 1)][lane]);
-        float2 a[4];
-        float c[4];
+      for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
+      if (lvl == 0) {
+        int total = th.count(-1);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          a[u] = txy[sl[u]];
-          c[u] = tz[sl[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (j + u < n) {
-            const float d2 = dist2_f32(q, a[u].x, a[u].y, c[u]);  // the scan's value, bit for bit
-            const int ix = (int)fminf(fmaxf(fmaf(d2, sc_, off_), -1.0f), 16.0f) + 1;
-            atomicAdd(&hw[(ix >> 2) * 64 + lane], 1u << ((ix & 3) << 3));
-          }
+        for (int i = 0; i < kHistBins; ++i) total += th.count(i);
+        // the k-th beyond R (or below the histogram's range): handed on
+        fb = total < kneed || th.count(-1) >= kneed;
+        if (fb) {
+          if (d.stats) atomicAdd(&d.stats[7], 1ull);
+          break;
         }
       }
-#pragma unroll
-      for (int i = 0; i < kTileSlots; ++i) th.h[i] = (hw[(i >> 2) * 64 + lane] >> ((i & 3) << 3)) & 0xffu;
-    };
-    if (hist_ok) {
-#pragma unroll
-      for (int i = 0; i < kTileSlots; ++i) th.h[i] = (hw[(i >> 2) * 64 + lane] >> ((i & 3) << 3)) & 0xffu;
-    } else {
-      list_hist(0.0f, T);
-    }
-    float lo = 0.f, hi = T;
-    for (int lvl = 0;; ++lvl) {
       int cum, cb;
       if (!hist_locate(th, kneed, th.count(-1), lo, hi, &L, &U, &cum, &cb)) {
         fb = true;
@@ -1911,24 +1435,44 @@ k_normals_vlist(DenseVox d, int kneed, const float* __restrict__ prior, float* _
       if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
       lo = L;
       hi = U;
-      list_hist(lo, hi);
     }
   }
+  if (dbg == 2) {
+    if (L == 12345.f) out[0] = 0.f;
+    return;
+  }
+  const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
+  // the wave's list stencil: the smallest that covers every lane's Up
+  const int lsel = wide ? 2 : __ballot(!fb && !(Up < d.rl2)) == 0 ? 0 : 1;
   if (!fb) {
-    const float Lm = L * (1.0f - 2.0f * kRelEps);
-    fb = !finish_selection<KMAX>(
-        q, kneed, n, Lm, U, l8, lane,
-        [&](int p) {
-          const int sl = slot_of(p);
-          return make_float4(txy[sl].x, txy[sl].y, tz[sl], 0.f);
-        },
-        prior, oi, out, d.nbr,
-        [&](int p) {
-          const int sl = slot_of(p);
-          const int bz = sl / kSZ, r = sl - bz * kSZ, by = r / kSY, bx = r - by * kSY;
-          return __float_as_int(d.vox[(gx0 + bx) + (int64_t)d.nx * ((gy0 + by) + (int64_t)d.ny * (gz0 + bz))].w);
-        },
-        d.kd2);
+    int n = 0;
+    auto body = [&](int pp, float d2) {
+      if (d2 < Up) {  // masked store: only the accepted lanes take part in the LDS banking
+        lst[min(n, kListMax)][lane] = (uint16_t)pp;
+        ++n;
+      }
+    };
+    if (lsel == 0)
+      stencil_scan<Stencil210>(txy, tz, qs, SY, SZ, xpos, q, body);
+    else if (lsel == 1)
+      stencil_scan<Stencil220>(txy, tz, qs, SY, SZ, xpos, q, body);
+    else
+      stencil_scan<Stencil245>(txy, tz, qs, SY, SZ, xpos, q, body);
+    if (dbg == 3) {
+      if (n == 12345) out[0] = 0.f;
+      return;
+    }
+    if (n > kListMax && d.stats) atomicAdd(&d.stats[5], 1ull);
+    fb = n > kListMax ||
+         !finish_selection<KMAX>(
+             q, kneed, n, Lm, U, lst, lane,
+             [&](int p) { return make_float4(txy[p].x, txy[p].y, tz[p], 0.f); }, prior, oi, out, d.nbr,
+             [&](int p) {
+               const int bz_ = p / kSZ, r = p - bz_ * kSZ, by_ = r / kSY, bx_ = r - by_ * kSY;
+               return __float_as_int(
+                   d.vox[(gx0 + bx_) + (int64_t)d.nx * ((gy0 + by_) + (int64_t)d.ny * (gz0 + bz_))].w);
+             },
+             d.kd2, dbg == 4);
   }
   if (fb) {
     if (d.stats) atomicAdd(&d.stats[4], 1ull);
@@ -2495,14 +2039,8 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   d.nx = (int)geom[4];
   d.ny = (int)geom[5];
   d.nz = (int)geom[6];
-  // block shape (O3DX_STILE_SHAPE): 3 (default) 2x2 waves sharing one box, allocated
-  // for 3 waves/SIMD; 2: the same block at 2 waves/SIMD; 1: one wave per 4^3
-  // block; 4: 2x3 waves (a larger shared box, 2 workgroups = 12 waves per CU);
-  // 5 / 6: 2x2 / 2x3 waves with compact lists (1-byte stencil positions,
-  // packed histogram: 4 x 4 / 3 x 6 waves per CU)
-  const char* shape_env = getenv("O3DX_STILE_SHAPE");
-  const int shape = shape_env ? atoi(shape_env) : 3;
-  const int wy = shape == 1 ? 1 : 2, wz = shape == 1 ? 1 : (shape == 4 || shape == 6) ? 3 : 2;
+  // 2 x 2 waves per workgroup sharing one staged box, registers for 3 waves / SIMD
+  constexpr int wy = 2, wz = 2;
   d.nbx = (d.nx + kVB - 1) / kVB;
   d.nby = (d.ny + kVB * wy - 1) / (kVB * wy);
   d.nbz = (d.nz + kVB * wz - 1) / (kVB * wz);
@@ -2521,20 +2059,14 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
     maxext = std::max(maxext, ext);
   }
   const double slack = 32.0 * std::ldexp(1.0, -24) * (maxabs + maxext) + 1e-6 * geom[3];
-  // stencil (O3DX_STILE_STENCIL): "mirror" — 172 voxels mirrored per lane to
-  // the query's half of its voxel (R = 2.45 voxels); "sym" — the 179 voxels at
-  // gap^2 <= 4 (R = sqrt 5), the same for every lane
-  const char* st_env = getenv("O3DX_STILE_STENCIL");
-  const bool sym = st_env && std::string(st_env) == "sym";
-  const double R = (sym ? std::sqrt(kSymR2) : kStencilR) * geom[3] - slack;
+  // completeness radii of the count (2.2 voxels) and the smaller list stencil
+  // (2.1), shrunk by the float32 slack; the histogram's lower edge (1.5 voxels)
+  const double R = kStencilR * geom[3] - slack, Rl = kListR * geom[3] - slack;
   d.rc2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
-  const double Rw = std::sqrt(kSymWideR2) * geom[3] - slack;
-  d.rc2w = (float)(Rw * Rw) * (1.0f - 4.0f * kRelEps);
-  // list threshold: 1.14 x the expected k-th distance (kth voxels, from the
-  // occupancy), never beyond the stencil's completeness radius
-  const double Rt = std::min(1.14 * kth * geom[3], R);
-  d.rt2 = (float)(Rt * Rt) * (1.0f - 4.0f * kRelEps);
-  d.vl_hist = getenv("O3DX_VLIST_LISTHIST") ? 0 : 1;
+  d.rl2 = (float)(Rl * Rl) * (1.0f - 4.0f * kRelEps);
+  const double Rw = kWideR * geom[3] - slack;
+  d.rw2 = (float)(Rw * Rw) * (1.0f - 4.0f * kRelEps);
+  d.hlo2 = (float)(kHistLo * geom[3] * kHistLo * geom[3]);
   d.stats = search_stats_ptr();
   d.nbr = debug_nbr(kneed, n);
   d.kd2 = kd2;
@@ -2551,52 +2083,8 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
       // O3DX_TILE_DEBUG=1/2/3/4: stop after staging / histogram / list scan / moments (profiling only)
       const char* dbg = getenv("O3DX_TILE_DEBUG");
       const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
-      const char* mg = getenv("O3DX_STILE_MERGED");
-      const bool merged = mg && atoi(mg) != 0;
-#define O3DX_STILE_LAUNCH2(WY, WZ, WPE, MG)                                                              \
-  if (sym)                                                                                                 \
-    hipLaunchKernelGGL((k_normals_stile<32, WY, WZ, WPE, MG, true>), dim3((unsigned)nb), dim3(64 * WY * WZ), \
-                       0, s, d, kneed, prior, out, list, lens, ffb, dg);                                    \
-  else                                                                                                     \
-    hipLaunchKernelGGL((k_normals_stile<32, WY, WZ, WPE, MG, false>), dim3((unsigned)nb), dim3(64 * WY * WZ), \
-                       0, s, d, kneed, prior, out, list, lens, ffb, dg)
-#define O3DX_STILE_LAUNCH(WYZ, WPE, MG) O3DX_STILE_LAUNCH2(WYZ, WYZ, WPE, MG)
-      // the launched variant must match the block grid (wy x wz waves) sized above
-      // O3DX_STILE_FORM=vlist: the list-first form (opt-in; measured 0.72-0.76 ms
-      // against 0.66 ms for the two-scan form at C2)
-      const char* form = getenv("O3DX_STILE_FORM");
-      const bool vlist = form && std::string(form) == "vlist";
-      if (vlist && !merged && wy == 2 && wz == 2) {
-        if (sym)
-          hipLaunchKernelGGL((k_normals_vlist<32, 2, 2, 3, true>), dim3((unsigned)nb), dim3(256), 0, s, d, kneed,
-                             prior, out, list, lens, ffb);
-        else
-          hipLaunchKernelGGL((k_normals_vlist<32, 2, 2, 3, false>), dim3((unsigned)nb), dim3(256), 0, s, d, kneed,
-                             prior, out, list, lens, ffb);
-      } else if (merged) {
-        if (wy == 1)
-          O3DX_STILE_LAUNCH(1, 2, true);
-        else if (wz == 3)
-          O3DX_STILE_LAUNCH2(2, 3, 2, true);
-        else
-          O3DX_STILE_LAUNCH(2, 2, true);
-      } else if (wy == 1) {
-        O3DX_STILE_LAUNCH(1, 2, false);
-      } else if (shape == 4) {
-        O3DX_STILE_LAUNCH2(2, 3, 3, false);
-      } else if (shape == 3) {
-        O3DX_STILE_LAUNCH(2, 3, false);
-      } else if (shape == 6 && !sym) {
-        hipLaunchKernelGGL((k_normals_stile<32, 2, 3, 4, false, false, true>), dim3((unsigned)nb), dim3(384), 0, s, d,
-                           kneed, prior, out, list, lens, ffb, dg);
-      } else if (shape == 5 && !sym) {
-        hipLaunchKernelGGL((k_normals_stile<32, 2, 2, 4, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, d,
-                           kneed, prior, out, list, lens, ffb, dg);
-      } else {
-        O3DX_STILE_LAUNCH(2, 2, false);
-      }
-#undef O3DX_STILE_LAUNCH
-#undef O3DX_STILE_LAUNCH2
+      hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d, kneed,
+                         prior, out, list, lens, ffb, dg);
     }
     // the table as a dense GridView (identity cell starts, <= 1 point per cell)
     GridView g{};

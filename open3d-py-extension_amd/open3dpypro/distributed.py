@@ -753,10 +753,12 @@ def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tenso
         t_all, n_all = full[:, :3].contiguous(), full[:, 3:].contiguous()
     else:
         t_all, n_all = trx, tn
+    t0 = mark("icp_gather_target", t0)
     target = ops.ICPTarget(t_all, n_all, max_correspondence_distance)
+    t0 = mark("icp_target_build", t0)
     T, fit, rm = registration_icp_sharded(srx, target, max_iteration=icp_iterations, relative_fitness=0.0,
                                           relative_rmse=0.0, group=group)
-    mark("icp", t0)
+    mark("icp_iterations", t0)
     return {"target_rep_gidx": trg, "target_rep_xyz": trx, "target_normals": tn, "target_reps": mt,
             "source_reps": _allreduce_int(srx.shape[0], group), "plane": plane, "plane_inlier_rows": pos[inl],
             "transformation": T, "fitness": fit, "inlier_rmse": rm}

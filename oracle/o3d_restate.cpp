@@ -594,6 +594,7 @@ void transform_points(const double T[16], std::vector<V3>& pts) {
 extern "C" {
 
 int oref_num_threads(void) { return omp_get_max_threads(); }
+void oref_set_num_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
 // Reference: PointCloud.get_aabb (PointCloud.py:145-146).  [upstream]
 // Geometry3D::ComputeMinBound/MaxBound (zero vector for an empty cloud).

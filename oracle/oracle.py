@@ -40,6 +40,7 @@ def lib():
             build()
         L = ctypes.CDLL(_LIB_PATH)
         L.oref_num_threads.restype = _I32
+        L.oref_set_num_threads.argtypes = [_I32]
         L.oref_aabb.argtypes = [_P, _I64, _P]
         L.oref_voxel_down_sample.argtypes = [_P, _I64, _P, _P, _D, _P, _P, _P, _P]
         L.oref_voxel_down_sample.restype = _I32
@@ -72,6 +73,10 @@ def _ptr(a):
 
 def num_threads() -> int:
     return lib().oref_num_threads()
+
+
+def set_num_threads(n: int) -> None:
+    lib().oref_set_num_threads(int(n))
 
 
 def aabb(xyz):

@@ -382,6 +382,19 @@ def test_icp_row_walk_equals_shell_walk(dev, shift, monkeypatch):
     np.testing.assert_allclose(a[:30], ref[:30], rtol=1e-9, atol=1e-9)
 
 
+def test_normals_raw_planted_plane_big_cells(dev):
+    """estimate_normals on a raw (not down-sampled) planted-plane cloud whose
+    thin dense plane puts > 256 points in many grid cells (the in-cell order
+    then comes from the workgroup-per-cell ranking, k_grid_big_cells): every
+    row within 1e-5 of the oracle; run to run bit-identical."""
+    pts = S.planted_plane(1_000_000, 5, frac=0.8, sigma=0.0005).numpy()
+    x = torch.from_numpy(pts).to(dev)
+    a = ops.estimate_normals(x, knn=30).cpu().numpy()
+    b = ops.estimate_normals(x, knn=30).cpu().numpy()
+    assert np.array_equal(a, b)
+    assert_normals(a, O.estimate_normals(pts, O.KNN, 30), pts, k=30, what="raw_planted_plane_1m")
+
+
 @pytest.mark.parametrize("k", [5, 30, 64])
 @pytest.mark.parametrize("shape", ["cube", "surface", "dups"])
 def test_normals_knn_paths_agree(dev, k, shape):
@@ -495,23 +508,6 @@ STILE_ENVS = [
     {},
     {"O3DX_STILE_FORCE_FB": "1"},
     {"O3DX_NO_STILE": "1"},
-    {"O3DX_STILE_SHAPE": "1"},
-    {"O3DX_STILE_SHAPE": "2"},
-    {"O3DX_STILE_SHAPE": "4"},
-    {"O3DX_STILE_SHAPE": "5"},
-    {"O3DX_STILE_SHAPE": "6"},
-    {"O3DX_STILE_SHAPE": "5", "O3DX_STILE_FORCE_FB": "1"},
-    {"O3DX_STILE_MERGED": "1"},
-    {"O3DX_STILE_MERGED": "1", "O3DX_STILE_SHAPE": "4"},
-    {"O3DX_STILE_MERGED": "1", "O3DX_STILE_SHAPE": "1"},
-    {"O3DX_STILE_STENCIL": "sym"},
-    {"O3DX_STILE_STENCIL": "sym", "O3DX_STILE_SHAPE": "1"},
-    {"O3DX_STILE_STENCIL": "sym", "O3DX_STILE_SHAPE": "4"},
-    {"O3DX_STILE_STENCIL": "sym", "O3DX_STILE_MERGED": "1"},
-    {"O3DX_STILE_STENCIL": "mirror"},
-    {"O3DX_STILE_FORM": "vlist"},
-    {"O3DX_STILE_FORM": "vlist", "O3DX_STILE_STENCIL": "sym"},
-    {"O3DX_STILE_FORCE_FB": "1", "O3DX_STILE_STENCIL": "sym"},
 ]
 
 
@@ -519,9 +515,9 @@ STILE_ENVS = [
 @pytest.mark.parametrize("k", [5, 30])
 def test_normals_dense_voxel_table(dev, env, k, monkeypatch):
     """Volumetric reps fill their voxels: estimate_normals(voxel_grid=) runs
-    straight off the dense voxel table (k_normals_stile in every block shape /
-    variant; its hand-off path — wave form and register top-k over the table —
-    forced for every query by O3DX_STILE_FORCE_FB): every row within 1e-5 of
+    straight off the dense voxel table (k_normals_stile; its hand-off path —
+    wave form and register top-k over the table — forced for every query by
+    O3DX_STILE_FORCE_FB; the sorted-grid path with O3DX_NO_STILE): every row within 1e-5 of
     the oracle, the selected neighbour sets bit-equal to the oracle's.
     Non-cubic box, dims not multiples of the 4^3 tile blocks."""
     n = 200_000

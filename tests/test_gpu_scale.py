@@ -45,16 +45,11 @@ def test_normals_10m_reps(cloud10m, dev):
     assert np.abs(np.linalg.norm(got, axis=1) - 1).max() < 1e-5
 
 
-@pytest.mark.parametrize("form", ["vlist", "stile"])
-@pytest.mark.parametrize("stencil", ["mirror", "sym"])
-def test_normals_10m_voxel_table(cloud10m, dev, stencil, form, monkeypatch):
+def test_normals_10m_voxel_table(cloud10m, dev):
     """The bench's exact step: voxel_down_sample(keep_grid) -> estimate_normals
-    on the dense voxel table (k_normals_stile with either stencil, wave form,
-    register top-k), against the oracle on the same representatives: every
-    row within 1e-5 signed, and every selected neighbour set bit-equal to the
-    oracle's."""
-    monkeypatch.setenv("O3DX_STILE_STENCIL", stencil)
-    monkeypatch.setenv("O3DX_STILE_FORM", form)
+    on the dense voxel table (k_normals_stile, wave form, register top-k),
+    against the oracle on the same representatives: every row within 1e-5
+    signed, and every selected neighbour set bit-equal to the oracle's."""
     vs = S.voxel_size_for(N)
     out = ops.voxel_down_sample(cloud10m, vs, keep_grid=True)
     reps = out["rep_xyz"]
@@ -62,8 +57,8 @@ def test_normals_10m_voxel_table(cloud10m, dev, stencil, form, monkeypatch):
         got = ops.estimate_normals(reps, knn=30, voxel_grid=out["voxel_grid"]).cpu().numpy()
     r = reps.cpu().numpy()
     ref = O.estimate_normals(r, O.KNN, 30)
-    assert_normals(got, ref, r, k=30, what=f"c2_voxel_table_{form}_{stencil}")
-    assert_neighbour_sets(dn.ids(), r, 30, f"c2_voxel_table_{form}_{stencil}")
+    assert_normals(got, ref, r, k=30, what="c2_voxel_table")
+    assert_neighbour_sets(dn.ids(), r, 30, "c2_voxel_table")
     assert np.abs(np.linalg.norm(got, axis=1) - 1).max() < 1e-5
 
 
