@@ -204,8 +204,9 @@ class Processors:
             for p in pcds_data:
                 if isinstance(p, torch.Tensor):
                     res.append(p[p[:, :3].norm(dim=1) <= self.radius])
-                else:
-                    res.append(p[np.linalg.norm(p[:, :3], axis=1) <= self.radius][:, :3])
+                else:  # reference: PointCloud(xyz).select_by_radius(r).get_points() -> float64 xyz
+                    q = np.asarray(p[:, :3], np.float64)
+                    res.append(q[(q[:, 0] ** 2 + q[:, 1] ** 2 + q[:, 2] ** 2) ** 0.5 <= self.radius])
             return res
 
     class VoxelDownsample(PointCloudMatProcessor):
@@ -313,7 +314,12 @@ class Processors:
 
     class PlaneNormalize(PointCloudMatProcessor):
         """Rotate each cloud so the detected plane (meta[detection_uuid]) becomes
-        z = 0 (reference processors.py:701-759)."""
+        z = 0 (reference processors.py:701-759).  T is built the reference's
+        way, in the data's dtype on the data's device (rotation_matrix_from_
+        vectors, including its quirk: normals within 1e-6 of parallel OR
+        anti-parallel to z give the identity, :713-714), and applied as the
+        homogeneous product (T @ [xyz | 1]^T)^T, so the output equals the
+        reference's bit for bit."""
         title: str = "plane_normalize"
         detection_uuid: str
         filter_pcd: bool = False
@@ -321,40 +327,43 @@ class Processors:
         def validate_pcd(self, idx, pcd):
             self.init_common_utility_methods(idx, pcd.is_ndarray())
 
-        @staticmethod
-        def plane_transform(plane) -> np.ndarray:
-            a, b, c, d = [float(v) for v in plane]
-            n = np.array([a, b, c])
-            z = np.array([0.0, 0.0, 1.0])
-            an = n / np.linalg.norm(n)
-            v = np.cross(an, z)
-            if np.linalg.norm(v) < 1e-6:
-                R = np.eye(3)
-            else:
-                cth = float(an @ z)
-                s = np.linalg.norm(v)
-                K = np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
-                R = np.eye(3) + K + K @ K * ((1 - cth) / s ** 2)
-            t = -R @ (-d * n / (n @ n))
-            T = np.eye(4)
+        def rotation_matrix_from_vectors(self, vec1, vec2, device=None, i=0):
+            f = self._mat_funcs[i]
+            a = vec1 / f.norm(vec1)
+            b = vec2 / f.norm(vec2)
+            v = f.cross(a, b)
+            if f.norm(v) < 1e-6:
+                return f.eye(3, dtype=a.dtype, device=device)
+            c = f.dot(a, b)
+            s = f.norm(v)
+            kmat = f.mat([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]], dtype=a.dtype, device=device)
+            return f.eye(3, dtype=a.dtype, device=device) + kmat + f.matmul(kmat, kmat) * ((1 - c) / (s ** 2))
+
+        def rotate_to_plane(self, pcd_data, plane, device=None, i=0):
+            f = self._mat_funcs[i]
+            a, b, c, d = plane
+            xyz = pcd_data[:, :3]
+            normal = f.mat([a, b, c], dtype=pcd_data.dtype, device=device)
+            z_axis = f.mat([0, 0, 1], dtype=pcd_data.dtype, device=device)
+            R = self.rotation_matrix_from_vectors(normal, z_axis, device, i)
+            point_on_plane = -d * normal / f.dot(normal, normal)
+            t = -f.matmul(R, point_on_plane)
+            T = f.eye(4, dtype=pcd_data.dtype, device=device)
             T[:3, :3] = R
             T[:3, 3] = t
-            return T
+            ones_row = f.ones((pcd_data.shape[0], 1), dtype=pcd_data.dtype, device=device)
+            homo = f.hstack([xyz, ones_row])
+            return f.matmul(T, homo.T).T[:, :3], T
 
         def forward_raw(self, pcds_data, pcds_info=[], meta={}):
             planes = meta[self.detection_uuid]
             self.forward_T = []
             res = []
             for i, p in enumerate(pcds_data):
-                T = self.plane_transform(planes[i])
-                self.forward_T.append(T.tolist())
-                if isinstance(p, torch.Tensor):
-                    Tt = torch.as_tensor(T, dtype=p.dtype, device=p.device)
-                    xyz = p[:, :3] @ Tt[:3, :3].T + Tt[:3, 3]
-                    res.append(torch.hstack([xyz, p[:, 3:]]) if p.shape[1] > 3 else xyz)
-                else:
-                    xyz = (p[:, :3] @ T[:3, :3].T + T[:3, 3]).astype(p.dtype)
-                    res.append(np.hstack([xyz, p[:, 3:]]) if p.shape[1] > 3 else xyz)
+                device = p.device if hasattr(p, "device") else None
+                xyz, T = self.rotate_to_plane(p, planes[i], device=device, i=i)
+                res.append(self._mat_funcs[i].hstack([xyz, p[:, 3:]]) if p.shape[1] > 3 else xyz)
+                self.forward_T.append(self._mat_funcs[i].to_numpy(T).tolist())
             return res
 
     class ICP(PointCloudMatProcessor):

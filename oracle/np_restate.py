@@ -231,3 +231,75 @@ def plane_moments_fx(pts, A, centroid=None):
     q = fx_exp(4.0 * A * A * 1.01)
     pairs = [(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2)]
     return np.stack([fx_row(r[:, a] * r[:, b], q) for a, b in pairs])
+
+
+# ---------------------------------------------------------------------------
+# The reference's processor glue around the hot path, restated for value
+# parity (reference open3dpypro/processors.py; these are its own formulas —
+# numpy or torch, in the data's dtype — not Open3D's).
+
+def rotation_matrix_from_vectors_ref(vec1, vec2, lib, device=None):
+    """PlaneNormalize.rotation_matrix_from_vectors (processors.py:709-723)."""
+    if lib == "torch":
+        import torch
+        norm, cross, eye, dot = torch.norm, (lambda a, b: torch.cross(a, b, dim=-1)), torch.eye, torch.dot
+        mat = lambda l, dtype: torch.tensor(l, dtype=dtype, device=device)  # noqa: E731
+        mm = torch.matmul
+        eye_ = lambda n, dtype: torch.eye(n, dtype=dtype, device=device)  # noqa: E731
+    else:
+        norm, cross, dot = np.linalg.norm, (lambda a, b: np.cross(a, b, axis=-1)), np.dot
+        mat = lambda l, dtype: np.array(l, dtype=dtype)  # noqa: E731
+        mm = lambda a, b: a @ b  # noqa: E731
+        eye_ = lambda n, dtype: np.eye(n, dtype=dtype)  # noqa: E731
+    a = vec1 / norm(vec1)
+    b = vec2 / norm(vec2)
+    v = cross(a, b)
+    if norm(v) < 1e-6:
+        return eye_(3, a.dtype)
+    c = dot(a, b)
+    s = norm(v)
+    kmat = mat([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]], a.dtype)
+    return eye_(3, a.dtype) + kmat + mm(kmat, kmat) * ((1 - c) / (s ** 2))
+
+
+def rotate_to_plane_ref(pcd, plane):
+    """PlaneNormalize.rotate_to_plane (processors.py:725-744): T in the data's
+    dtype, applied as (T @ [xyz | 1]^T)^T.  Returns (xyz', T)."""
+    a, b, c, d = plane
+    if hasattr(pcd, "device") and not isinstance(pcd, np.ndarray):
+        import torch
+        lib, dev = "torch", pcd.device
+        mat = lambda l: torch.tensor(l, dtype=pcd.dtype, device=dev)  # noqa: E731
+        normal, z = mat([a, b, c]), mat([0, 0, 1])
+        R = rotation_matrix_from_vectors_ref(normal, z, lib, dev)
+        pop = -d * normal / torch.dot(normal, normal)
+        t = -torch.matmul(R, pop)
+        T = torch.eye(4, dtype=pcd.dtype, device=dev)
+        T[:3, :3] = R
+        T[:3, 3] = t
+        homo = torch.cat([pcd[:, :3], torch.ones((pcd.shape[0], 1), dtype=pcd.dtype, device=dev)], dim=1)
+        return torch.matmul(T, homo.T).T[:, :3], T
+    normal = np.array([a, b, c], dtype=pcd.dtype)
+    z = np.array([0, 0, 1], dtype=pcd.dtype)
+    R = rotation_matrix_from_vectors_ref(normal, z, "numpy")
+    pop = -d * normal / np.dot(normal, normal)
+    t = -(R @ pop)
+    T = np.eye(4, dtype=pcd.dtype)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    homo = np.hstack([pcd[:, :3], np.ones((pcd.shape[0], 1), dtype=pcd.dtype)])
+    return (T @ homo.T).T[:, :3], T
+
+
+def plane_flip_ref(plane_model):
+    """PlaneDetection.cpu_model's orientation (processors.py:640-650, 644-646): flip so
+    the sensor origin lies on the normal's side."""
+    plane_model = np.asarray(plane_model)
+    n, d = plane_model[:3], plane_model[3]
+    v = np.zeros(3) - (-d * n)
+    return -plane_model if np.dot(n, v) < 0 else plane_model
+
+
+def ema_ref(best, plane, alpha):
+    """PlaneDetection.forward_raw's blend (processors.py:697)."""
+    return (np.asarray(best) * (1.0 - alpha) + plane * alpha).tolist()

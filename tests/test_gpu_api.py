@@ -267,6 +267,90 @@ def test_processors_numpy_and_torch_branches(dev):
     assert plane[3] >= 0 and abs(abs(plane[2]) - 1) < 1e-2 and abs(abs(plane[3]) - 0.5) < 1e-2
 
 
+@pytest.mark.parametrize("branch", ["numpy", "torch"])
+def test_plane_detection_ema_value_parity(dev, branch):
+    """PlaneDetection's published meta[uuid] over 3 frames at alpha = 0.1,
+    against the reference's CPU-branch glue restated (processors.py:633-650,
+    697): Open3D SegmentPlane (the oracle) on the same RandomSampler samples,
+    the d >= 0 flip, the EMA.  Within 1e-9 (the oracle sums sequentially)."""
+    frames = [S.planted_plane(40_000, 30 + f, z0=0.4 + 0.05 * f).numpy() for f in range(3)]
+    det = o3p.Processors.PlaneDetection(distance_threshold=0.01, alpha=0.1, seed=17, num_iterations=300)
+    best = [0.0, 0.0, 0.0, 0.0]
+    meta = {}
+    for f, pts in enumerate(frames):
+        m = _mat(pts) if branch == "numpy" else _mat(torch.from_numpy(pts).to(dev))
+        if f == 0:
+            _, meta = det.validate([m], meta)
+        else:
+            _, meta = det([m], meta)
+        plane, *_ = O.segment_plane(pts, 0.01, 3, 300, O.ransac_samples(len(pts), 3, 300, 17))
+        best = NPR.ema_ref(best, NPR.plane_flip_ref(plane), 0.1)
+        np.testing.assert_allclose(meta[det.uuid][0], best, rtol=0, atol=1e-9)
+    assert meta[det.uuid][0][3] > 0
+
+
+@pytest.mark.parametrize("kind", ["numpy64", "numpy32", "torch64", "torch32", "antiparallel"])
+def test_plane_normalize_value_parity(dev, kind):
+    """PlaneNormalize's T and output against the reference's rotate_to_plane
+    restated in the data's dtype (processors.py:709-744): bit-equal (the same
+    operations on the same device), including the anti-parallel quirk — a
+    normal along -z gives R = I (:713-714)."""
+    rng = np.random.default_rng(8)
+    pts = np.c_[rng.random((5000, 3)) * 2 - 1, rng.random((5000, 1))]  # x y z + one extra column
+    plane = [0.05, -0.1, 0.99, -0.3] if kind != "antiparallel" else [0.0, 0.0, -1.0, 0.25]
+    dt = np.float32 if kind.endswith("32") else np.float64
+    data = pts.astype(dt)
+    if kind.startswith("torch"):
+        data = torch.from_numpy(data).to(dev)
+    pn = o3p.Processors.PlaneNormalize(uuid="PlaneNormalize:pv", detection_uuid="det")
+    st = ShapeType.XYZi
+    out, _ = pn.validate([_mat(data, st)], {"det": [plane]})
+    exp_xyz, exp_T = NPR.rotate_to_plane_ref(data, plane)
+    got = out[0].data()
+    if isinstance(got, torch.Tensor):
+        assert torch.equal(got[:, :3], exp_xyz) and torch.equal(got[:, 3:], data[:, 3:])
+        exp_T = exp_T.cpu().numpy()
+    else:
+        assert np.array_equal(got[:, :3], exp_xyz) and np.array_equal(got[:, 3:], data[:, 3:])
+    assert np.array_equal(np.asarray(pn.forward_T[0], exp_T.dtype), exp_T)
+    if kind == "antiparallel":
+        assert np.array_equal(exp_T[:3, :3], np.eye(3))
+
+
+@pytest.mark.parametrize("branch", ["numpy", "torch"])
+def test_random_sample_radius_selection_value_parity(dev, branch):
+    """RandomSample / RadiusSelection against the reference's own formulas
+    (processors.py:320-416): the same RNG draws for the same seed (numpy
+    randint / torch.randint on the data's device); the radius mask |p| <= r
+    — numpy branch: PointCloud(xyz).select_by_radius(r).get_points(), float64
+    xyz (so XYZ mats only); torch branch: xyz.norm(dim=1) <= r, every column
+    kept."""
+    rng = np.random.default_rng(5)
+    pts = (rng.random((20000, 4)) * 6 - 3).astype(np.float32)
+    rs = o3p.Processors.RandomSample(n_samples=5000)
+    rsel = o3p.Processors.RadiusSelection(radius=2.0)
+    if branch == "numpy":
+        np.random.seed(11)
+        o, _ = rs.validate([_mat(pts, ShapeType.XYZi)], {})
+        np.random.seed(11)
+        idx = np.random.randint(0, len(pts), (5000,))
+        assert np.array_equal(o[0].data(), pts[idx])
+        # the reference's numpy branch returns xyz only, so it serves XYZ mats
+        o2, _ = rsel.validate([_mat(np.ascontiguousarray(pts[:, :3]))], {})
+        q = pts[:, :3].astype(np.float64)
+        exp = q[(q[:, 0] ** 2 + q[:, 1] ** 2 + q[:, 2] ** 2) ** 0.5 <= 2.0]
+        assert o2[0].data().dtype == np.float64 and np.array_equal(o2[0].data(), exp)
+    else:
+        x = torch.from_numpy(pts).to(dev)
+        torch.manual_seed(11)
+        o, _ = rs.validate([_mat(x, ShapeType.XYZi)], {})
+        torch.manual_seed(11)
+        idx = torch.randint(0, len(x), (5000,), device=dev)
+        assert torch.equal(o[0].data(), x[idx])
+        o2, _ = rsel.validate([_mat(x, ShapeType.XYZi)], {})
+        assert torch.equal(o2[0].data(), x[x[:, :3].norm(dim=1) <= 2.0])
+
+
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "ref_torch_branch.npz")
 
 
