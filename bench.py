@@ -227,7 +227,9 @@ def secondary(dev, args):
     _native.reset_kernel_timing()
     ops.segment_plane(pts, 0.01, 3, args.ransac_iters, samples=samples)  # kernel times (events on)
     torch.cuda.synchronize(dev)
-    pc_ms, pc_n = _native.kernel_timing("plane_count")
+    ub_ms, _ = _native.kernel_timing("plane_count_upper")  # the sweep: all hypotheses, upper bounds
+    ex_ms, ex_n = _native.kernel_timing("plane_count")  # exact re-counts of the consulted few
+    pc_ms = ub_ms + ex_ms
     _native.set_kernel_timing(False)  # the timed call carries no instrumentation events
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -237,7 +239,9 @@ def secondary(dev, args):
     _native.set_kernel_timing(True)
     pairs = float(n) * args.ransac_iters
     out["ransac"] = {"n": n, "iterations": args.ransac_iters, "ms": round((t1 - t0) * 1e3, 3),
-                     "plane_count_kernel_ms": round(pc_ms, 3), "inliers": int(inl.numel()),
+                     "plane_count_kernel_ms": round(pc_ms, 3), "upper_sweep_ms": round(ub_ms, 3),
+                     "exact_recount_ms": round(ex_ms, 3), "exact_recount_calls": ex_n,
+                     "inliers": int(inl.numel()),
                      "plane": [round(float(v), 6) for v in plane],
                      "Gpairs_per_s": round(pairs / (pc_ms * 1e-3) / 1e9, 2) if pc_ms > 0 else None}
     del inl

@@ -334,6 +334,24 @@ int o3dx_plane_count(const float* xyz_dev, int64_t n, const double* planes_host,
                      int num_hypotheses, double distance_threshold,
                      int64_t* counts_host, void* ws, size_t ws_bytes,
                      void* stream);
+/* Upper bounds of the inlier counts (counts_host[h] >= the exact count;
+ * degenerate hypotheses -1): the float32 distance against the largest float32
+ * window edge, no float64 re-decision.  absmax_host (nullable: the cloud's
+ * own): |x|,|y|,|z| bounds of the cloud.  Paired with o3dx_ransac_needed, a
+ * selection counts exactly only the hypotheses Open3D's replay consults. */
+int o3dx_plane_count_upper(const float* xyz_dev, int64_t n, const double* planes_host,
+                           int num_hypotheses, double distance_threshold,
+                           const double* absmax_host, int64_t* counts_host, void* ws,
+                           size_t ws_bytes, void* stream);
+/* counts_host: exact counts where known_host[h] != 0, upper bounds elsewhere.
+ * out_host (capacity num_hypotheses) receives the unknown hypotheses that
+ * Open3D's selection replay on these values consults (records and ties,
+ * ascending); *n_out == 0 means the selection (o3dx_ransac_tied /
+ * o3dx_ransac_select on these values) equals the one on exact counts. */
+int o3dx_ransac_needed(const int64_t* counts_host, const uint8_t* known_host,
+                       const double* planes_host, int num_hypotheses, int64_t n,
+                       int ransac_n, double probability, int32_t* out_host,
+                       int32_t* n_out);
 int o3dx_plane_abs_sum(const float* xyz_dev, int64_t n,
                        const double* planes_host, const int32_t* which_host,
                        int num_which, double distance_threshold,

@@ -140,21 +140,25 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
 // instantiated shape (tuning).
 constexpr int kCountWaves = 2048;      // batch ranges (waves per hypothesis chunk)
 constexpr int kMinBatchPts = 64 * 8;   // smallest instantiated batch (bitmap sizing)
-constexpr int kMinHC = 16;             // smallest instantiated chunk (bitmap sizing)
+constexpr int kMinHC = 8;              // smallest instantiated chunk (bitmap sizing)
 
 template <int PL>
 __device__ __forceinline__ void plane_batch_load(const P3* __restrict__ p, int64_t n, int64_t gb, int lane,
                                                  f32x2 (&X)[PL / 2], f32x2 (&Y)[PL / 2], f32x2 (&Z)[PL / 2]) {
   const float qnan = __int_as_float(0x7fc00000);
+  // wave-uniform batch base and remainder; 32-bit lane offsets (saddr form)
+  const P3* base = p + gb * (64 * PL);
+  const int64_t rem64 = n - gb * (64 * PL);
+  const uint32_t rem = (uint32_t)min<int64_t>(rem64, 64 * PL);
 #pragma unroll
   for (int k = 0; k < PL / 2; ++k) {
-    const int64_t i0 = gb * (64 * PL) + (int64_t)(2 * k) * 64 + lane, i1 = i0 + 64;
+    const uint32_t i0 = (uint32_t)(2 * k) * 64 + lane, i1 = i0 + 64;
     // clamped, unconditional loads; rows past n become NaN afterwards
-    const P3 a = p[min(i0, n - 1)];
-    const P3 b = p[min(i1, n - 1)];
-    X[k] = (f32x2){i0 < n ? a.x : qnan, i1 < n ? b.x : qnan};
-    Y[k] = (f32x2){i0 < n ? a.y : qnan, i1 < n ? b.y : qnan};
-    Z[k] = (f32x2){i0 < n ? a.z : qnan, i1 < n ? b.z : qnan};
+    const P3 a = base[min(i0, rem - 1)];
+    const P3 b = base[min(i1, rem - 1)];
+    X[k] = (f32x2){i0 < rem ? a.x : qnan, i1 < rem ? b.x : qnan};
+    Y[k] = (f32x2){i0 < rem ? a.y : qnan, i1 < rem ? b.y : qnan};
+    Z[k] = (f32x2){i0 < rem ? a.z : qnan, i1 < rem ? b.z : qnan};
   }
 }
 
@@ -174,6 +178,12 @@ __device__ __forceinline__ f32x2 plane_sq_test(f32x2 d, float L) {
   return __builtin_elementwise_fma(d, d, (f32x2){-L, -L});
 }
 
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // block -> (batch range, group of 4 hypothesis chunks), XCD-aware: the
 // launch's blocks are dealt round-robin over the 8 XCDs, so logical block
 // l = (b % 8) * (nb / 8) + b / 8 puts consecutive l on one XCD.
@@ -182,12 +192,16 @@ __device__ __forceinline__ int xcd_logical_block(int b, int nb) {
   return (b % 8) * (nb / 8) + b / 8;
 }
 
-template <int kHC, int kPL>  // kHC <= 32: one bitmap bit per hypothesis
-__global__ void __launch_bounds__(kBlock) k_plane_count_v(const float* __restrict__ xyz, int64_t n,
-                                                          const float4* __restrict__ pl32, int H, float Llo,
-                                                          uint32_t wbits, int64_t batches_per_wave, int nwp,
-                                                          int ncg, int32_t* __restrict__ partial,
-                                                          uint32_t* __restrict__ flags) {
+// Per hypothesis of the chunk the wave keeps its count in a scalar register
+// across the whole batch range (popcounts summed on the scalar unit), so the
+// per-batch work is exactly: 4 v_readlane (the plane), PL/2 x (3 + 1) packed
+// fmas, PL compares, PL/2 v_min3 and one window ballot.  PF: the next batch's
+// points are loaded while the current one is evaluated.
+template <int kHC, int kPL, int kPF>  // kHC <= 32: one bitmap bit per hypothesis
+__device__ __forceinline__ void plane_count_body(const float* __restrict__ xyz, int64_t n,
+                                                 const float4* __restrict__ pl32, int H, float Llo, uint32_t wbits,
+                                                 int64_t batches_per_wave, int nwp, int ncg,
+                                                 int32_t* __restrict__ partial, uint32_t* __restrict__ flags) {
   const int lane = threadIdx.x & 63;
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
   const int wp = lb / ncg;                                                      // batch range
@@ -196,20 +210,25 @@ __global__ void __launch_bounds__(kBlock) k_plane_count_v(const float* __restric
   if (wp >= nwp || chunk >= nchunks) return;
   const int h0 = chunk * kHC;
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  int cnt = 0;  // lane h: hypothesis h0 + h's count (popcounts of its inlier ballots)
+  int sc[kHC];  // wave-uniform counts of hypotheses h0 .. h0 + kHC
+#pragma unroll
+  for (int h = 0; h < kHC; ++h) sc[h] = 0;
   // lane j holds plane h0 + (j % kHC) (h0 + j >= H: a copy of the last plane,
   // its counts never written back)
   float4 Pl = pl32[min(h0 + (lane % kHC), H - 1)];
   constexpr int kBatchPts = 64 * kPL;
   const int64_t nbatches = (n + kBatchPts - 1) / kBatchPts;
-  for (int64_t b = 0; b < batches_per_wave; ++b) {
-    const int64_t gb = (int64_t)wp * batches_per_wave + b;
-    if (gb >= nbatches) break;
+  const int64_t gb0 = (int64_t)wp * batches_per_wave;
+  const int64_t gbe = min(gb0 + batches_per_wave, nbatches);
+  f32x2 X[kPL / 2], Y[kPL / 2], Z[kPL / 2];
+  if (kPF && gb0 < gbe) plane_batch_load<kPL>(p, n, gb0, lane, X, Y, Z);
+  for (int64_t gb = gb0; gb < gbe; ++gb) {
+    if (!kPF) plane_batch_load<kPL>(p, n, gb, lane, X, Y, Z);
+    f32x2 Xn[kPL / 2], Yn[kPL / 2], Zn[kPL / 2];
+    if (kPF && gb + 1 < gbe) plane_batch_load<kPL>(p, n, gb + 1, lane, Xn, Yn, Zn);
     // the planes are read out of Pl per batch, not hoisted out of the batch
     // loop into 128 scalar registers (an empty asm that "changes" Pl)
     asm volatile("" : "+v"(Pl.x), "+v"(Pl.y), "+v"(Pl.z), "+v"(Pl.w));
-    f32x2 X[kPL / 2], Y[kPL / 2], Z[kPL / 2];
-    plane_batch_load<kPL>(p, n, gb, lane, X, Y, Z);
     uint32_t word = 0;
 #pragma unroll
     for (int h = 0; h < kHC; ++h) {
@@ -220,21 +239,123 @@ __global__ void __launch_bounds__(kBlock) k_plane_count_v(const float* __restric
                                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.z), h)),
                                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.w), h)));
       uint32_t mn = ~0u;
-      int sc = 0;  // wave-uniform
+      int c = 0;  // wave-uniform
 #pragma unroll
       for (int k = 0; k < kPL / 2; ++k) {
         const f32x2 t = plane_sq_test(plane_dist_pk(P, X[k], Y[k], Z[k]), Llo);
         // inliers: one v_cmp per point, counted on the scalar unit
-        sc += __popcll(__ballot(t.x < 0.0f)) + __popcll(__ballot(t.y < 0.0f));
-        asm("" : "+s"(sc));  // summed as they come (a deferred sum tree spills the masks)
-        mn = min(mn, min(__float_as_uint(t.x), __float_as_uint(t.y)));
+        c += __popcll(__ballot(t.x < 0.0f)) + __popcll(__ballot(t.y < 0.0f));
+        asm("" : "+s"(c));  // summed as they come (a deferred sum tree spills the masks)
+        mn = umin3(mn, __float_as_uint(t.x), __float_as_uint(t.y));
       }
-      cnt += lane == h ? sc : 0;
+      sc[h] += c;
       if (__ballot(mn <= wbits)) word |= 1u << h;
     }
     if (lane == 0) flags[gb * nchunks + chunk] = word;
+    if (kPF && gb + 1 < gbe) {
+#pragma unroll
+      for (int k = 0; k < kPL / 2; ++k) {
+        X[k] = Xn[k];
+        Y[k] = Yn[k];
+        Z[k] = Zn[k];
+      }
+    }
   }
-  if (lane < kHC && h0 + lane < H) partial[(int64_t)wp * H + h0 + lane] = cnt;
+  int mine = 0;
+#pragma unroll
+  for (int h = 0; h < kHC; ++h) mine = lane == h ? sc[h] : mine;
+  if (lane < kHC && h0 + lane < H) partial[(int64_t)wp * H + h0 + lane] = mine;
+}
+
+// W > 0: the register budget of W waves per SIMD (occupancy for the
+// dependent fma -> compare -> popcount chains)
+template <int kHC, int kPL, int kPF>
+__global__ void __launch_bounds__(kBlock) k_plane_count_v(const float* __restrict__ xyz, int64_t n,
+                                                          const float4* __restrict__ pl32, int H, float Llo,
+                                                          uint32_t wbits, int64_t bpw, int nwp, int ncg,
+                                                          int32_t* __restrict__ partial, uint32_t* __restrict__ flags) {
+  plane_count_body<kHC, kPL, kPF>(xyz, n, pl32, H, Llo, wbits, bpw, nwp, ncg, partial, flags);
+}
+template <int kHC, int kPL, int kPF>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_plane_count_w8(const float* __restrict__ xyz, int64_t n, const float4* __restrict__ pl32, int H, float Llo,
+                 uint32_t wbits, int64_t bpw, int nwp, int ncg, int32_t* __restrict__ partial,
+                 uint32_t* __restrict__ flags) {
+  plane_count_body<kHC, kPL, kPF>(xyz, n, pl32, H, Llo, wbits, bpw, nwp, ncg, partial, flags);
+}
+template <int kHC, int kPL, int kPF>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 6)))
+k_plane_count_w6(const float* __restrict__ xyz, int64_t n, const float4* __restrict__ pl32, int H, float Llo,
+                 uint32_t wbits, int64_t bpw, int nwp, int ncg, int32_t* __restrict__ partial,
+                 uint32_t* __restrict__ flags) {
+  plane_count_body<kHC, kPL, kPF>(xyz, n, pl32, H, Llo, wbits, bpw, nwp, ncg, partial, flags);
+}
+
+// Upper bounds of the counts (ub >= the exact count, bit-exactly so): a point
+// is counted when its float32 |d| < hi, hi >= thr + g of every hypothesis
+// (rounded up), so every float64 inlier is counted.  No window and no
+// bitmap: per batch and hypothesis 4 v_readlane, PL/2 x 3 packed fmas and PL
+// compares (|d| through the abs modifier).  segment_plane selects on these
+// and counts exactly only the hypotheses its replay could consult
+// (needed_exact below) — Open3D's records, typically ~ln H of H.
+template <int kHC, int kPL>
+__device__ __forceinline__ void plane_upper_body(const float* __restrict__ xyz, int64_t n,
+                                                 const float4* __restrict__ pl32, int H, float hi,
+                                                 int64_t batches_per_wave, int nwp, int ncg,
+                                                 int32_t* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int wp = lb / ncg;
+  const int chunk = __builtin_amdgcn_readfirstlane((lb % ncg) * (kBlock / 64) + (threadIdx.x >> 6));
+  const int nchunks = (H + kHC - 1) / kHC;
+  if (wp >= nwp || chunk >= nchunks) return;
+  const int h0 = chunk * kHC;
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  int sc[kHC];
+#pragma unroll
+  for (int h = 0; h < kHC; ++h) sc[h] = 0;
+  float4 Pl = pl32[min(h0 + (lane % kHC), H - 1)];
+  constexpr int kBatchPts = 64 * kPL;
+  const int64_t nbatches = (n + kBatchPts - 1) / kBatchPts;
+  const int64_t gb0 = (int64_t)wp * batches_per_wave;
+  const int64_t gbe = min(gb0 + batches_per_wave, nbatches);
+  for (int64_t gb = gb0; gb < gbe; ++gb) {
+    f32x2 X[kPL / 2], Y[kPL / 2], Z[kPL / 2];
+    plane_batch_load<kPL>(p, n, gb, lane, X, Y, Z);
+    asm volatile("" : "+v"(Pl.x), "+v"(Pl.y), "+v"(Pl.z), "+v"(Pl.w));
+#pragma unroll
+    for (int h = 0; h < kHC; ++h) {
+      const float4 P = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.x), h)),
+                                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.y), h)),
+                                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.z), h)),
+                                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Pl.w), h)));
+      int c = 0;
+#pragma unroll
+      for (int k = 0; k < kPL / 2; ++k) {
+        const f32x2 d = plane_dist_pk(P, X[k], Y[k], Z[k]);
+        c += __popcll(__ballot(fabsf(d.x) < hi)) + __popcll(__ballot(fabsf(d.y) < hi));
+        asm("" : "+s"(c));  // summed as they come
+      }
+      sc[h] += c;
+    }
+  }
+  int mine = 0;
+#pragma unroll
+  for (int h = 0; h < kHC; ++h) mine = lane == h ? sc[h] : mine;
+  if (lane < kHC && h0 + lane < H) partial[(int64_t)wp * H + h0 + lane] = mine;
+}
+
+template <int kHC, int kPL>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 6)))
+k_plane_upper(const float* __restrict__ xyz, int64_t n, const float4* __restrict__ pl32, int H, float hi,
+              int64_t bpw, int nwp, int ncg, int32_t* __restrict__ partial) {
+  plane_upper_body<kHC, kPL>(xyz, n, pl32, H, hi, bpw, nwp, ncg, partial);
+}
+template <int kHC, int kPL>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_plane_upper_w8(const float* __restrict__ xyz, int64_t n, const float4* __restrict__ pl32, int H, float hi,
+                 int64_t bpw, int nwp, int ncg, int32_t* __restrict__ partial) {
+  plane_upper_body<kHC, kPL>(xyz, n, pl32, H, hi, bpw, nwp, ncg, partial);
 }
 
 // The window results of the flagged (batch, hypothesis) blocks decided in
@@ -277,174 +398,6 @@ __global__ void __launch_bounds__(kBlock) k_plane_fixup(const float* __restrict_
       if (lane == 0 && c) atomicAdd(reinterpret_cast<unsigned long long*>(&counts[h]), (unsigned long long)c);
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// The same counts with the distances on the matrix cores (O3DX_RANSAC_MFMA=1;
-// measured 1.54 ms against 1.53 ms for k_plane_count_v at 10M x 1000: the
-// VALU work after the products — squares, sign-bit counts, window min —
-// costs as much issue as the fma chain it replaces, and the matrix pipe and
-// the VALU overlap little at 4-6 waves per SIMD).
-// All hypotheses against all points is a dense (N x 4) . (4 x H) product:
-// one v_mfma_f32_16x16x4_f32 gives 16 points x 16 hypotheses, and its result
-// is bit for bit the k-ordered fmaf chain (MI355X_MICROARCH: "exact f32
-// (== fmaf chain, bitwise)") — with k = (1 | d), (z | c), (y | b), (x | a)
-// it is fma(a, x, fma(b, y, fma(c, z, d))), the VALU kernels' distance.
-// The eight products of a step are issued by one asm statement with VGPR
-// results (the compiler's AGPR form copies every result out right after its
-// MFMA and serialises the matrix pipe); the statement carries its own wait
-// states: s_nop 1 ahead (operands just written by the VALU) and s_nop 11 at
-// the end (an 8-pass MFMA's D before any reader or writer).  The VALU then
-// tests the squares (t = fma(d, d, -Llo), packed), counts sign bits into
-// per-lane counters (lane l: hypothesis l & 15 of each tile, points
-// (l >> 4) * 4 + r) and keeps one min for the window; a step with a window
-// result (rare) re-issues its products and marks its tiles in a
-// (step, tile) bitmap for k_plane_fixup_mf.  Rows past the wave's range or
-// past n are all-zero (d = 0): they count as inliers of every hypothesis
-// when Llo > 0 and the host subtracts that known padding.
-constexpr int kMfHT = 8;                 // tiles of 16 hypotheses per wave
-constexpr int kMfU = 2;                  // 16-point steps per loop trip
-constexpr int kMfWaves = 2048;           // point ranges per hypothesis chunk
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void mfma8(float a, const float (&b)[kMfHT], f32x4 (&d)[kMfHT]) {
-  asm("s_nop 1\n\t"
-      "v_mfma_f32_16x16x4_f32 %0, %8, %9, 0\n\t"
-      "v_mfma_f32_16x16x4_f32 %1, %8, %10, 0\n\t"
-      "v_mfma_f32_16x16x4_f32 %2, %8, %11, 0\n\t"
-      "v_mfma_f32_16x16x4_f32 %3, %8, %12, 0\n\t"
-      "v_mfma_f32_16x16x4_f32 %4, %8, %13, 0\n\t"
-      "v_mfma_f32_16x16x4_f32 %5, %8, %14, 0\n\t"
-      "v_mfma_f32_16x16x4_f32 %6, %8, %15, 0\n\t"
-      "v_mfma_f32_16x16x4_f32 %7, %8, %16, 0\n\t"
-      "s_nop 11"
-      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7])
-      : "v"(a), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
-}
-
-__global__ void __launch_bounds__(kBlock) k_plane_count_mf(const float* __restrict__ xyz, int64_t n,
-                                                           const float4* __restrict__ pl32, int H, float Llo,
-                                                           uint32_t wbits, int64_t steps_per_wave, int nwp,
-                                                           int wps, int32_t* __restrict__ partial,
-                                                           uint32_t* __restrict__ flags) {
-  const int lane = threadIdx.x & 63;
-  const int wp = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
-  if (wp >= nwp) return;
-  const int hbase = blockIdx.y * (16 * kMfHT);
-  const int kk = lane >> 4, jj = lane & 15;
-  float bv[kMfHT];
-  uint32_t cnt[kMfHT];
-#pragma unroll
-  for (int t = 0; t < kMfHT; ++t) {
-    const int h = hbase + 16 * t + jj;
-    float b = 0.0f;
-    if (h < H) {
-      const float4 P = pl32[h];
-      b = kk == 0 ? P.w : kk == 1 ? P.z : kk == 2 ? P.y : P.x;
-    }
-    bv[t] = b;
-    cnt[t] = 0;
-  }
-  const int comp = 3 - kk;  // A[i][k]: k = 0 -> 1, 1 -> z, 2 -> y, 3 -> x
-  const int64_t s0 = (int64_t)wp * steps_per_wave;
-  const int64_t plim = min(n, (s0 + steps_per_wave) * 16);  // this wave's points end here
-  const f32x2 nL = (f32x2){-Llo, -Llo};
-  for (int64_t st = 0; st < steps_per_wave; st += kMfU) {
-    float a[kMfU];
-#pragma unroll
-    for (int u = 0; u < kMfU; ++u) {
-      const int64_t pt = (s0 + st + u) * 16 + jj;
-      const float v = xyz[3 * min(pt, n - 1) + comp];  // clamped, unconditional
-      a[u] = pt < plim ? (kk == 0 ? 1.0f : v) : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < kMfU; ++u) {
-      f32x4 d[kMfHT];
-      mfma8(a[u], bv, d);
-      uint32_t mn = ~0u;
-#pragma unroll
-      for (int t = 0; t < kMfHT; ++t) {
-        const f32x2 q0 = __builtin_elementwise_fma((f32x2){d[t].x, d[t].y}, (f32x2){d[t].x, d[t].y}, nL);
-        const f32x2 q1 = __builtin_elementwise_fma((f32x2){d[t].z, d[t].w}, (f32x2){d[t].z, d[t].w}, nL);
-        uint32_t x0 = __float_as_uint(q0.x), x1 = __float_as_uint(q0.y), x2 = __float_as_uint(q1.x),
-                 x3 = __float_as_uint(q1.y);
-        mn = min(mn, min(min(x0, x1), min(x2, x3)));
-        // cnt += sign bits, accumulated here (a deferred sum spills the values)
-        asm("v_lshrrev_b32 %1, 31, %1\n\tv_lshrrev_b32 %2, 31, %2\n\tv_add3_u32 %0, %0, %1, %2"
-            : "+v"(cnt[t]), "+v"(x0), "+v"(x1));
-        asm("v_lshrrev_b32 %1, 31, %1\n\tv_lshrrev_b32 %2, 31, %2\n\tv_add3_u32 %0, %0, %1, %2"
-            : "+v"(cnt[t]), "+v"(x2), "+v"(x3));
-      }
-      if (__ballot(mn <= wbits) && st + u < steps_per_wave) {
-        // rare: which tiles hold window results (products re-issued)
-        const int64_t g = s0 + st + u;
-        f32x4 e[kMfHT];
-        mfma8(a[u], bv, e);
-#pragma unroll
-        for (int t = 0; t < kMfHT; ++t) {
-          uint32_t m2 = ~0u;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) m2 = min(m2, __float_as_uint(fmaf(e[t][r], e[t][r], -Llo)));
-          const int tile = hbase / 16 + t;
-          if (__ballot(m2 <= wbits) && lane == 0) atomicOr(&flags[g * wps + (tile >> 5)], 1u << (tile & 31));
-        }
-      }
-    }
-  }
-  // the four lanes of a hypothesis (jj, jj + 16, jj + 32, jj + 48)
-#pragma unroll
-  for (int t = 0; t < kMfHT; ++t) {
-    int c = (int)cnt[t];
-    c += __shfl_xor(c, 16, 64);
-    c += __shfl_xor(c, 32, 64);
-    const int h = hbase + 16 * t + jj;
-    if (kk == 0 && h < H) partial[(int64_t)wp * H + h] = c;
-  }
-}
-
-// The flagged (step, tile) blocks of k_plane_count_mf: each window result
-// (the same float32 distance: the fmaf chain) decided in float64 in Open3D's
-// order.  A wave takes 64 bitmap words; per set bit, its 256 pairs as 4 per
-// lane (point lane & 15, hypotheses 4 (lane >> 4) + q).
-__global__ void __launch_bounds__(kBlock) k_plane_fixup_mf(const float* __restrict__ xyz, int64_t n,
-                                                           const float4* __restrict__ pl32,
-                                                           const double* __restrict__ pl64, int H, double thr,
-                                                           float Llo, uint32_t wbits, const uint32_t* __restrict__ flags,
-                                                           int64_t nwords, int wps, int64_t* __restrict__ counts) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 64;
-  if (w0 >= nwords) return;
-  const uint32_t word = w0 + lane < nwords ? flags[w0 + lane] : 0u;
-  uint64_t m = __ballot(word != 0);
-  while (m) {
-    const int i = __ffsll((unsigned long long)m) - 1;
-    m &= m - 1;
-    uint32_t wd = (uint32_t)__shfl((int)word, i, 64);
-    const int64_t g = (w0 + i) / wps;
-    const int tbase = (int)((w0 + i) % wps) * 32;
-    const int64_t p = g * 16 + (lane & 15);
-    float x = 0.f, y = 0.f, z = 0.f;
-    if (p < n) x = xyz[3 * p], y = xyz[3 * p + 1], z = xyz[3 * p + 2];
-    while (wd) {
-      const int tile = tbase + __ffs((int)wd) - 1;
-      wd &= wd - 1;
-      for (int q = 0; q < 4; ++q) {
-        const int h = tile * 16 + (lane >> 4) * 4 + q;
-        if (p >= n || h >= H) continue;
-        const float4 P = pl32[h];
-        const float d = fmaf(P.x, x, fmaf(P.y, y, fmaf(P.z, z, P.w)));
-        if (__float_as_uint(fmaf(d, d, -Llo)) <= wbits && plane_dist64(pl64 + 4 * (int64_t)h, x, y, z) < thr)
-          atomicAdd(reinterpret_cast<unsigned long long*>(&counts[h]), 1ull);
-      }
-    }
-  }
-}
-
-// degenerate hypotheses -> -1; the others lose the padding rows they counted
-__global__ void k_mark_degenerate_pad(const uint8_t* __restrict__ degenerate, int H, int64_t pad,
-                                      int64_t* __restrict__ counts) {
-  int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h < H) counts[h] = degenerate[h] == 1 ? -1 : degenerate[h] == 2 ? counts[h] : counts[h] - pad;
 }
 
 __global__ void k_mark_degenerate(const uint8_t* __restrict__ degenerate, int H, int64_t* __restrict__ counts) {
@@ -507,7 +460,7 @@ __global__ void __launch_bounds__(kBlock) k_plane_band(const T* __restrict__ xyz
   }
 }
 
-constexpr int kMomBlocks = 256;
+constexpr int kMomBlocks = 2048;  // gathers over the inlier list: enough waves in flight
 
 // GetPlaneFromPoints moments over the inliers as exact fx sums (common.hpp),
 // so the refit plane is the same bits for any split of the inliers over
@@ -627,24 +580,17 @@ static bool plane_is_zero(const double* pl) { return pl[0] == 0 && pl[1] == 0 &&
 
 // ------------------------------------------------------------ workspaces
 
-// MFMA count geometry: nwp point ranges of spw 16-point steps each
-static void mf_geometry(int64_t n, int* nwp, int64_t* spw) {
-  const int64_t steps = std::max<int64_t>(1, (n + 15) / 16);
-  *nwp = (int)std::max<int64_t>(1, std::min<int64_t>(kMfWaves, (steps + 3) / 4));
-  *spw = (steps + *nwp - 1) / *nwp;
-}
-
-static int64_t mf_flag_words(int64_t n, int H) {
-  int nwp;
-  int64_t spw;
-  mf_geometry(n, &nwp, &spw);
-  return (int64_t)nwp * spw * (((std::max(H, 1) + 15) / 16 + 31) / 32);
-}
-
 // count geometry: nwp ranges of bpw batches of `batch` points
-static void count_geometry(int64_t n, int batch, int* nwp, int64_t* bpw) {
+// count geometry: nwp ranges of bpw batches of `batch` points.  Few
+// hypothesis chunks (a re-count of a handful of hypotheses) get more ranges,
+// so the launch still fills the chip (~16K waves), within the partial
+// buffer's capacity (cap_ints >= nwp * H).
+static void count_geometry(int64_t n, int batch, int* nwp, int64_t* bpw, int nchunks = 32, int H = 1,
+                           size_t cap_ints = 0) {
   const int64_t nb = std::max<int64_t>(1, (n + batch - 1) / batch);
-  *nwp = (int)std::min<int64_t>(kCountWaves, nb);
+  int64_t want = std::max<int64_t>(kCountWaves, 16384 / std::max(nchunks, 1));
+  if (cap_ints) want = std::min<int64_t>(want, std::max<int64_t>(kCountWaves, (int64_t)(cap_ints / std::max(H, 1))));
+  *nwp = (int)std::min<int64_t>(want, nb);
   *bpw = (nb + *nwp - 1) / *nwp;
 }
 
@@ -664,21 +610,23 @@ struct CountWs {
   double* pl64;
   uint8_t* degen;
   int32_t* partial;
+  size_t partial_ints;
   uint32_t* flags;  // (batch, hypothesis chunk) window bitmap of the brute-force count
-  uint32_t* mflags;  // (16-point step, 16-hypothesis tile) window bitmap of the MFMA count
   int64_t* counts;
   int64_t* sum_partial;
 };
 
 static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   H = std::max(H, 1);
-  w->pl32 = ar.take<float4>(H);
-  w->band = ar.take<float4>(H);
-  w->pl64 = ar.take<double>(4 * (size_t)H);
-  w->degen = ar.take<uint8_t>(H);
-  w->partial = ar.take<int32_t>((size_t)std::max(count_blocks(n), kCountWaves) * H);
+  // the per-hypothesis inputs in one block: one upload (upload_planes)
+  uint8_t* up = ar.take<uint8_t>(65 * (size_t)H);
+  w->pl32 = reinterpret_cast<float4*>(up);
+  w->band = reinterpret_cast<float4*>(up + 16 * (size_t)H);
+  w->pl64 = reinterpret_cast<double*>(up + 32 * (size_t)H);
+  w->degen = up + 64 * (size_t)H;
+  w->partial_ints = (size_t)std::max(count_blocks(n), kCountWaves) * H;
+  w->partial = ar.take<int32_t>(w->partial_ints);
   w->flags = ar.take<uint32_t>((size_t)count_flag_words(n, H, kMinBatchPts, kMinHC));
-  w->mflags = ar.take<uint32_t>((size_t)mf_flag_words(n, H));
   w->counts = ar.take<int64_t>(H);
   w->sum_partial = ar.take<int64_t>((size_t)2 * abs_sum_blocks(n) * H);
   return ar.used;
@@ -687,14 +635,15 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
 // scale of |a x| + |b y| + |c z| + |d| over the cloud, for the float32 band
 static void upload_planes(const double* planes, int H, const double absmax[3], double thr, CountWs& w,
                           std::vector<float4>& p32, std::vector<float4>& bnd, std::vector<uint8_t>& dg,
-                          hipStream_t s, int* rc) {
+                          std::vector<uint8_t>& st, hipStream_t s, int* rc, double* hi_max = nullptr) {
+  if (hi_max) *hi_max = -1.0;
   p32.resize(H);
   bnd.resize(H);
   dg.resize(H);
   for (int h = 0; h < H; ++h) {
     const double* pl = planes + 4 * h;
     // 1: degenerate (count -1); 2: non-finite coefficients (count 0: no
-    // distance is < thr, and the MFMA count's zero rows are not counted either)
+    // distance is < thr)
     dg[h] = plane_is_zero(pl) ? 1
             : (std::isfinite(pl[0]) && std::isfinite(pl[1]) && std::isfinite(pl[2]) && std::isfinite(pl[3])) ? 0
                                                                                                             : 2;
@@ -706,6 +655,7 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
     // the float32 rounding of lo / hi and Open3D's own float64 rounding
     double g = 6.0 * std::ldexp(1.0, -24) * S + std::ldexp(1.0, -20) * thr;
     float lo = (float)(thr - g), hi = (float)(thr + g);
+    if (hi_max && !dg[h]) *hi_max = std::max(*hi_max, thr + g);
     if (dg[h]) {
       lo = -1.0f;  // never an inlier
       hi = -1.0f;
@@ -718,10 +668,16 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
     bnd[h] = make_float4(lo, hi, mid, half);
   }
   *rc = 0;
-  if (hipMemcpyAsync(w.pl32, p32.data(), H * sizeof(float4), hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(w.band, bnd.data(), H * sizeof(float4), hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(w.pl64, planes, 4 * H * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(w.degen, dg.data(), H, hipMemcpyHostToDevice, s) != hipSuccess)
+  // one copy of the block laid out as count_carve placed it
+  uint8_t* base = reinterpret_cast<uint8_t*>(w.pl32);
+  const size_t ob = reinterpret_cast<uint8_t*>(w.band) - base, o64 = reinterpret_cast<uint8_t*>(w.pl64) - base,
+               odg = w.degen - base;
+  st.resize(odg + H);  // the caller keeps it alive until the stream is synchronised
+  std::memcpy(st.data(), p32.data(), H * sizeof(float4));
+  std::memcpy(st.data() + ob, bnd.data(), H * sizeof(float4));
+  std::memcpy(st.data() + o64, planes, 4 * H * sizeof(double));
+  std::memcpy(st.data() + odg, dg.data(), H);
+  if (hipMemcpyAsync(base, st.data(), st.size(), hipMemcpyHostToDevice, s) != hipSuccess)
     *rc = fail(O3DX_EIO, "plane upload failed");
 }
 
@@ -741,8 +697,9 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   std::vector<float4> p32;
   std::vector<float4> bnd;
   std::vector<uint8_t> dg;
+  std::vector<uint8_t> st;
   int rc;
-  upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, s, &rc);
+  upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, st, s, &rc);
   if (rc) return rc;
   int nb = count_blocks(n);
   KTimer kt("plane_count", s);
@@ -768,50 +725,35 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
     const float wdt = (float)((double)Lhi - (double)Llo);  // exact difference, one rounding
     uint32_t wbits;
     std::memcpy(&wbits, &wdt, 4);
-    if (getenv("O3DX_RANSAC_MFMA")) {
-      // matrix-core distances: waves = point ranges x chunks of 8 tiles of 16 hypotheses
-      int nwp;
-      int64_t spw;
-      mf_geometry(n, &nwp, &spw);
-      const int wps = ((H + 15) / 16 + 31) / 32;  // bitmap words per step
-      const int64_t nwords = mf_flag_words(n, H);
-      O3DX_HIP(hipMemsetAsync(w.mflags, 0, (size_t)nwords * sizeof(uint32_t), s));
-      const unsigned gx = (unsigned)((nwp + kBlock / 64 - 1) / (kBlock / 64));
-      hipLaunchKernelGGL(k_plane_count_mf, dim3(gx, (unsigned)((H + 16 * kMfHT - 1) / (16 * kMfHT))), dim3(kBlock), 0,
-                         s, xyz, n, w.pl32, H, Llo, wbits, spw, nwp, wps, w.partial, w.mflags);
-      O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));
-      const int64_t fwaves = (nwords + 63) / 64;
-      hipLaunchKernelGGL(k_plane_fixup_mf, dim3((unsigned)((fwaves + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock),
-                         0, s, xyz, n, w.pl32, w.pl64, H, thr, Llo, wbits, w.mflags, nwords, wps, w.counts);
-      // all-zero rows (d = 0) counted by every hypothesis when 0 < Llo
-      const int64_t pad = Llo > 0.0f ? (int64_t)nwp * ((spw + kMfU - 1) / kMfU * kMfU) * 16 - n : 0;
-      hipLaunchKernelGGL(k_mark_degenerate_pad, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, pad, w.counts);
-      kt.stop();
-      counts.resize(H);
-      O3DX_TRY(read_back(counts.data(), w.counts, H * sizeof(int64_t), s));
-      O3DX_HIP(hipGetLastError());
-      return 0;
-    }
     // the default: every point against every hypothesis on the VALU
-    int hc = 32, pl = 16;
-    if (const char* e = getenv("O3DX_RANSAC_SHAPE")) sscanf(e, "%dx%d", &hc, &pl);
+    // measured: 6 waves/SIMD fastest (r03); re-counts of a few hypotheses
+    // (segment_plane's exact rounds) take a narrower chunk
+    int hc = H <= 8 ? 8 : H <= 16 ? 16 : 32, pl = 16, pf = 0, wv = H <= 16 ? 8 : 6;
+    if (const char* e = getenv("O3DX_RANSAC_SHAPE")) sscanf(e, "%dx%dx%dx%d", &hc, &pl, &pf, &wv);
     int nwp;
     int64_t bpw;
-    count_geometry(n, 64 * pl, &nwp, &bpw);
     const int nchunks = (H + hc - 1) / hc;
+    count_geometry(n, 64 * pl, &nwp, &bpw, nchunks, H, w.partial_ints);
     const int ncg = (nchunks + kBlock / 64 - 1) / (kBlock / 64);  // blocks per batch range
     const int64_t nwords = count_flag_words(n, H, 64 * pl, hc);
     const unsigned fgrid = grid_for(nwords, kBlock / 64, 16384);
-#define O3DX_COUNT(HC, PL)                                                                                         \
-  if (hc == HC && pl == PL) {                                                                                      \
-    hipLaunchKernelGGL((k_plane_count_v<HC, PL>), dim3((unsigned)(nwp * ncg)), dim3(kBlock), 0, s, xyz, n, w.pl32, \
-                       H, Llo, wbits, bpw, nwp, ncg, w.partial, w.flags);                                          \
+    auto kcount = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)(nwp * ncg)), dim3(kBlock), 0, s, xyz, n, w.pl32, H, Llo, wbits, bpw,
+                         nwp, ncg, w.partial, w.flags);
+    };
+#define O3DX_COUNT(HC, PL, PF)                                                                                     \
+  if (hc == HC && pl == PL && pf == PF) {                                                                          \
+    if (wv == 8) kcount(k_plane_count_w8<HC, PL, PF>);                                                             \
+    else if (wv == 6) kcount(k_plane_count_w6<HC, PL, PF>);                                                        \
+    else kcount(k_plane_count_v<HC, PL, PF>);                                                                      \
     O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));                                          \
     hipLaunchKernelGGL((k_plane_fixup<HC, PL>), dim3(fgrid), dim3(kBlock), 0, s, xyz, n, w.pl32, w.pl64, H, thr,   \
                        Llo, wbits, w.flags, nwords, w.counts);                                                      \
   } else
-    O3DX_COUNT(32, 16) O3DX_COUNT(32, 8) O3DX_COUNT(16, 16) O3DX_COUNT(16, 8)
-    return fail(O3DX_EINVAL, "O3DX_RANSAC_SHAPE: instantiated shapes are 32x16, 32x8, 16x16, 16x8");
+    O3DX_COUNT(32, 16, 0) O3DX_COUNT(32, 16, 1) O3DX_COUNT(32, 8, 0) O3DX_COUNT(16, 16, 0) O3DX_COUNT(16, 16, 1)
+    O3DX_COUNT(32, 24, 0) O3DX_COUNT(8, 16, 0)
+    return fail(O3DX_EINVAL,
+                "O3DX_RANSAC_SHAPE: instantiated shapes are 32x16x{0,1}, 32x8x0, 16x16x{0,1}, 32x24x0, 8x16x0");
 #undef O3DX_COUNT
   } else {  // the ballot/popcount kernel with per-hypothesis windows (A/B reference)
     for (int h0 = 0; h0 < H; h0 += kHChunk) {
@@ -825,6 +767,51 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   kt.stop();
   counts.resize(H);
   O3DX_TRY(read_back(counts.data(), w.counts, H * sizeof(int64_t), s));
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+// Upper bounds of the counts (k_plane_upper); degenerate hypotheses -1.
+static int run_count_upper(const float* xyz, int64_t n, const double* planes, int H, double thr, CountWs& w,
+                           void* aabb_ws, double* mm_dev, hipStream_t s, std::vector<int64_t>& ub,
+                           const double* absmax_in = nullptr) {
+  double absmax[3];
+  if (absmax_in) std::memcpy(absmax, absmax_in, sizeof(absmax));
+  else O3DX_TRY(absmax_of(xyz, n, aabb_ws, mm_dev, s, absmax));
+  std::vector<float4> p32;
+  std::vector<float4> bnd;
+  std::vector<uint8_t> dg;
+  std::vector<uint8_t> st;
+  int rc;
+  double hmax;
+  upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, st, s, &rc, &hmax);
+  if (rc) return rc;
+  // hi >= thr + g of every hypothesis (rounded up; nothing counted without any)
+  float hi = (float)hmax;
+  if ((double)hi < hmax) hi = std::nextafter(hi, INFINITY);
+  if (hmax < 0) hi = -1.0f;
+  KTimer kt("plane_count_upper", s);
+  int hc = 32, pl = 16, wv = 6;
+  if (const char* e = getenv("O3DX_RANSAC_UPPER")) sscanf(e, "%dx%dx%d", &hc, &pl, &wv);
+  int nwp;
+  int64_t bpw;
+  const int nchunks = (H + hc - 1) / hc;
+  count_geometry(n, 64 * pl, &nwp, &bpw, nchunks, H, w.partial_ints);
+  const int ncg = (nchunks + kBlock / 64 - 1) / (kBlock / 64);
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nwp * ncg)), dim3(kBlock), 0, s, xyz, n, w.pl32, H, hi, bpw, nwp, ncg,
+                       w.partial);
+  };
+  if (hc == 32 && pl == 16 && wv == 6) launch(k_plane_upper<32, 16>);
+  else if (hc == 32 && pl == 16 && wv == 8) launch(k_plane_upper_w8<32, 16>);
+  else if (hc == 16 && pl == 16 && wv == 8) launch(k_plane_upper_w8<16, 16>);
+  else if (hc == 32 && pl == 8 && wv == 8) launch(k_plane_upper_w8<32, 8>);
+  else return fail(O3DX_EINVAL, "O3DX_RANSAC_UPPER: instantiated shapes are 32x16x6, 32x16x8, 16x16x8, 32x8x8");
+  O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));
+  hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
+  kt.stop();
+  ub.resize(H);
+  O3DX_TRY(read_back(ub.data(), w.counts, H * sizeof(int64_t), s));
   O3DX_HIP(hipGetLastError());
   return 0;
 }
@@ -931,6 +918,42 @@ static std::vector<int32_t> tied_hypotheses(const std::vector<int64_t>& counts, 
   return out;
 }
 
+// Which hypotheses still need an exact count before the selection is
+// decided.  v: exact counts where known[h], upper bounds elsewhere.  The
+// replay of select_best / tied_hypotheses on v consults a hypothesis's count
+// only when it is a record or a tie (v > 0 and v >= the running best); an
+// unknown one outside those positions has exact <= ub < best (or ub == 0), so
+// the exact replay skips it too, with the same running best and early break.
+// Empty result: every consulted count is exact, and replays on v decide as
+// on the exact counts.  Otherwise the unknown records/ties of this replay
+// (speculative: the ones a later replay may still add are few).
+static std::vector<int32_t> needed_exact(const int64_t* v, const uint8_t* known, const double* planes, int H,
+                                         int64_t n, int ransac_n, double probability) {
+  std::vector<int32_t> out;
+  int64_t best = 0;
+  size_t break_iteration = std::numeric_limits<size_t>::max();
+  int iteration_count = 0;
+  for (int it = 0; it < H; ++it) {
+    if ((size_t)iteration_count > break_iteration) continue;
+    if (v[it] < 0 || (planes && plane_is_zero(planes + 4 * it))) continue;
+    if (v[it] > 0 && v[it] >= best) {
+      if (!known[it]) out.push_back(it);
+      if (v[it] > best) {
+        best = v[it];
+        const double fit = (double)best / (double)n;
+        if (fit < 1.0) {
+          double bi = std::min(std::log(1 - probability) / std::log(1 - std::pow(fit, ransac_n)), (double)H);
+          break_iteration = (size_t)bi;
+        } else {
+          break_iteration = 0;
+        }
+      }
+    }
+    iteration_count++;
+  }
+  return out;
+}
+
 // moments pass (fx sums, common.hpp) over idx[0..m) (or the first m points);
 // A bounds |coordinate|; out: 3 (pass 1) or 6 (pass 2) float64; fx_host
 // (nullable): their {lo, hi, q, 0} rows
@@ -972,11 +995,13 @@ struct SegWs {
 static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
   count_carve(ar, n, H, &w->cw);
   w->sidx = ar.take<int32_t>((size_t)H * rn);
-  w->scoord = ar.take<float>((size_t)H * rn * 3);
+  // sampled coordinates and the cloud's min/max side by side: one read-back
+  const size_t nsc = ((size_t)H * rn * 3 + 1) & ~size_t(1);
+  w->scoord = ar.take<float>(nsc + 16);
+  w->mm = reinterpret_cast<double*>(w->scoord + nsc);
   w->flags = ar.take<uint8_t>(n + 16);
   w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(n));
   w->aabb = ar.take<char>(aabb_ws_bytes(n));
-  w->mm = ar.take<double>(8);
   w->cnt = ar.take<int64_t>(4);
   w->mom_part = ar.take<int64_t>((size_t)mom_blocks(n) * 12);
   w->mom_out = ar.take<int64_t>(16);
@@ -1052,6 +1077,38 @@ extern "C" int o3dx_plane_count(const float* xyz, int64_t n, const double* plane
   std::vector<int64_t> c;
   O3DX_TRY(run_count(xyz, n, planes, H, thr, w, aabb, mm, s, c));
   std::memcpy(counts, c.data(), H * sizeof(int64_t));
+  return 0;
+}
+
+extern "C" int o3dx_plane_count_upper(const float* xyz, int64_t n, const double* planes, int H, double thr,
+                                      const double* absmax, int64_t* counts, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || H < 0 || (H > 0 && (!planes || !counts)) || (n > 0 && !xyz))
+    return fail(O3DX_EINVAL, "o3dx_plane_count_upper: bad arguments");
+  if (!ws || ws_bytes < o3dx_plane_count_workspace_bytes(n, H)) return fail(O3DX_ENOMEM, "count workspace too small");
+  if (H == 0) return 0;
+  if (n == 0) {
+    for (int h = 0; h < H; ++h) counts[h] = plane_is_zero(planes + 4 * h) ? -1 : 0;
+    return 0;
+  }
+  hipStream_t s = as_stream(stream);
+  Arena ar(ws, ws_bytes);
+  CountWs w;
+  count_carve(ar, n, H, &w);
+  char* aabb = ar.take<char>(aabb_ws_bytes(n));
+  double* mm = ar.take<double>(8);
+  O3DX_ARENA_CHECK(ar);
+  std::vector<int64_t> c;
+  O3DX_TRY(run_count_upper(xyz, n, planes, H, thr, w, aabb, mm, s, c, absmax));
+  std::memcpy(counts, c.data(), H * sizeof(int64_t));
+  return 0;
+}
+
+extern "C" int o3dx_ransac_needed(const int64_t* counts, const uint8_t* known, const double* planes, int H, int64_t n,
+                                  int ransac_n, double probability, int32_t* out, int32_t* n_out) {
+  if (!counts || !known || !out || !n_out || H < 0 || n <= 0) return fail(O3DX_EINVAL, "o3dx_ransac_needed: bad args");
+  const std::vector<int32_t> t = needed_exact(counts, known, planes, H, n, ransac_n, probability);
+  std::memcpy(out, t.data(), t.size() * sizeof(int32_t));
+  *n_out = (int32_t)t.size();
   return 0;
 }
 
@@ -1252,23 +1309,50 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
       if (samples_host[j] < 0 || samples_host[j] >= n) return fail(O3DX_EINVAL, "sample index out of range");
     O3DX_HIP(hipMemcpyAsync(w.sidx, samples_host, ns * sizeof(int32_t), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_gather_samples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, xyz, w.sidx, ns, w.scoord);
-    std::vector<float> sc((size_t)ns * 3);
-    O3DX_TRY(read_back(sc.data(), w.scoord, sc.size() * sizeof(float), s));
+  }
+  // |x|,|y|,|z| bounds of the cloud: the count's float32 window and the fx
+  // quantum of the refit moments (a sharded driver passes the global ones);
+  // read back together with the sampled coordinates
+  O3DX_TRY(aabb_device(xyz, n, w.mm, w.aabb, s));
+  const size_t off_mm = reinterpret_cast<char*>(w.mm) - reinterpret_cast<char*>(w.scoord);
+  std::vector<char> rb(off_mm + 6 * sizeof(double));
+  O3DX_TRY(read_back(rb.data(), w.scoord, rb.size(), s));
+  double absmax[3];
+  {
+    double mmh[6];
+    std::memcpy(mmh, rb.data() + off_mm, sizeof(mmh));
+    for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(mmh[a]), std::fabs(mmh[3 + a]));
+  }
+  if (H > 0) {
+    const float* sc = reinterpret_cast<const float*>(rb.data());
     std::vector<double> P((size_t)ransac_n * 3);
     for (int h = 0; h < H; ++h) {
       for (int j = 0; j < ransac_n * 3; ++j) P[j] = (double)sc[(size_t)h * ransac_n * 3 + j];
       plane_from_pts(P.data(), ransac_n, &planes[(size_t)4 * h]);
     }
   }
-  // |x|,|y|,|z| bounds of the cloud: the count's float32 window and the fx
-  // quantum of the refit moments (a sharded driver passes the global ones)
-  double absmax[3];
-  O3DX_TRY(absmax_of(xyz, n, w.aabb, w.mm, s, absmax));
   const double A = std::max(absmax[0], std::max(absmax[1], absmax[2]));
   int best = -1;
   if (H > 0) {
+    // upper bounds for all, exact counts for the hypotheses the replay consults
     std::vector<int64_t> counts;
-    O3DX_TRY(run_count(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax));
+    O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax));
+    std::vector<uint8_t> known(H, 0);
+    std::vector<double> sub;
+    std::vector<int64_t> ec;
+    for (;;) {
+      const std::vector<int32_t> need =
+          needed_exact(counts.data(), known.data(), planes.data(), H, n, ransac_n, probability);
+      if (need.empty()) break;
+      const int L = (int)need.size();
+      sub.resize((size_t)4 * L);
+      for (int j = 0; j < L; ++j) std::memcpy(&sub[(size_t)4 * j], &planes[(size_t)4 * need[j]], 4 * sizeof(double));
+      O3DX_TRY(run_count(xyz, n, sub.data(), L, thr, w.cw, w.aabb, w.mm, s, ec, absmax));
+      for (int j = 0; j < L; ++j) {
+        counts[need[j]] = ec[j];
+        known[need[j]] = 1;
+      }
+    }
     std::vector<int32_t> tied = tied_hypotheses(counts, planes.data(), n, ransac_n, probability);
     std::vector<double> sums(H, std::numeric_limits<double>::quiet_NaN());
     if (!tied.empty()) {

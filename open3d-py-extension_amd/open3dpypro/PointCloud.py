@@ -9,7 +9,9 @@ row / column indices are plain numpy attributes, as in the reference.
 
 The hot-path methods call libo3dx.so (ops.py); there is no CPU fallback —
 without an MI355X they raise RuntimeError.  Host-only helpers (selections by
-numpy predicate, splitting, I/O) run anywhere.
+numpy predicate, splitting, I/O) run anywhere.  Out of scope (SURVEY.md §2
+rows 2 and 5) and not mirrored: DBSCAN, to_2D_Img, the colour-cosine
+selections.
 """
 from __future__ import annotations
 
@@ -542,12 +544,6 @@ class PointCloudSelections(PointCloudBase):
     def get_index_by_colors(self, comfunc: Callable = lambda rgb: np.ones(len(rgb), dtype=bool), invert=False):
         return self._bool2index(comfunc(self.get_colors()), invert=invert)
 
-    def get_index_by_colors_cosine(self, model, similarity: float = 0.99, invert: bool = False):
-        return self.get_index_by_colors(comfunc=self._cosine(model, similarity), invert=invert)
-
-    def select_by_colors_cosine(self, model, similarity: float = 0.99, invert: bool = False):
-        return self._select_by_idx(self.get_index_by_colors_cosine(model, similarity), invert=invert)
-
     def get_index_by_XYZ(self, comfunc: Callable = lambda X, Y, Z: np.ones(len(X), dtype=bool), invert=False):
         p = self.get_points()
         return self._bool2index(comfunc(p[:, 0], p[:, 1], p[:, 2]), invert=invert)
@@ -820,32 +816,6 @@ class PointCloud(PointCloudUtility):
         return self, T
 
     rotate_to_plane = rotate_by_normal
-
-    def to_2D_Img(self, resolution: float = 0.05, color: bool = False):
-        use_color = color and self.has_colors()
-        p = self.get_points()
-        minx, miny = p[:, 0].min(), p[:, 1].min()
-        ir = 1.0 / resolution
-        T = np.diag([ir, ir, ir, 1.0]) @ np.array([[1, 0, 0, -minx], [0, 1, 0, -miny], [0, 0, 1, 0], [0, 0, 0, 1.0]])
-        q = (p @ T[:3, :3].T + T[:3, 3]).round().astype(int)
-        ix, iy = q[:, 0], q[:, 1]
-        sx, sy = ix.max(), iy.max()
-        ix = np.clip(ix, 0, sx - 1)
-        iy = np.clip(iy, 0, sy - 1)
-        if use_color:
-            img = np.zeros((sy, sx, 3), np.uint8)
-            img[iy, ix] = (self.get_colors() * 255).astype(np.uint8)
-        else:
-            img = np.zeros((sy, sx), np.uint8)
-            img[iy, ix] = 255
-        return img, minx, T, miny, np.linalg.inv(T), resolution, list(zip(ix, iy))
-
-    def DBSCAN(self, eps: float = 0.05, min_samples: int = 3):
-        from sklearn.cluster import DBSCAN
-
-        labels = DBSCAN(eps=eps, min_samples=min_samples).fit(self.get_points()).labels_
-        return [self._select_by_idx(np.arange(len(labels))[labels == i]) for i in
-                range(len(set(labels) - {-1}))], labels
 
     def seg_planes(self, thickness: float = 0.01, ransac_n: int = 3, num_iterations: int = 450,
                    top_n: float = 10e9, minPointsRatio: float = 0.1):

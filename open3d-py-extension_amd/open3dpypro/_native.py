@@ -72,6 +72,8 @@ _SIGS = {
     "o3dx_plane_count": (_I32, [_P, _I64, _P, _I32, _D, _P, _P, _SZ, _P]),
     "o3dx_plane_abs_sum": (_I32, [_P, _I64, _P, _P, _I32, _D, _P, _P, _P, _SZ, _P]),
     "o3dx_ransac_tied": (_I32, [_P, _P, _I32, _I64, _I32, _D, _P, _P]),
+    "o3dx_plane_count_upper": (_I32, [_P, _I64, _P, _I32, _D, _P, _P, _P, _SZ, _P]),
+    "o3dx_ransac_needed": (_I32, [_P, _P, _P, _I32, _I64, _I32, _D, _P, _P]),
     "o3dx_ransac_select": (_I32, [_P, _P, _P, _I32, _I64, _I32, _D]),
     "o3dx_plane_inliers": (_I32, [_P, _I64, _P, _D, _P, _P, _P, _SZ, _P]),
     "o3dx_plane_select_workspace_bytes": (_SZ, [_I64]),

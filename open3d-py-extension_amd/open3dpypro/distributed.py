@@ -236,6 +236,10 @@ class _HipBackend:
         from . import ops
         return ops.plane_count(x, planes, thr)
 
+    def plane_count_upper(self, x, planes, thr, absmax):
+        from . import ops
+        return ops.plane_count_upper(x, planes, thr, absmax)
+
     def abs_sum_fx(self, x, planes, which, thr):
         from . import ops
         return ops.plane_abs_sum(x, planes, which, thr, return_fx=True)[1]
@@ -330,7 +334,8 @@ def segment_plane_sharded(x: torch.Tensor, pos: torch.Tensor, n_total: int, dist
     (integer sums), the Sigma|d| of the tie-relevant hypotheses and the refit
     moments as fx sums under the GLOBAL coordinate bounds (`absmax`).  Every
     rank then replays the same selection, so the plane and the inlier set are
-    o3dx_segment_plane's on the whole cloud to the bit.  Returns (plane
+    o3dx_segment_plane's on the whole cloud to the bit (the count upper bounds
+    differ from one GPU's, but the replay consults exact counts only).  Returns (plane
     float64[4], this rank's inlier rows as local indices (device int64))."""
     from . import ops
 
@@ -365,8 +370,17 @@ def segment_plane_sharded(x: torch.Tensor, pos: torch.Tensor, n_total: int, dist
         dist.all_reduce(bits, op=dist.ReduceOp.SUM, group=group)
     coords = bits.cpu().numpy().view(np.float64).reshape(H, ransac_n, 3)
     planes = ops.planes_from_samples(coords, ransac_n)
-    # 2. per-hypothesis counts, 3. tie sums, selection replay
-    counts = allreduce_counts(be.plane_count(x, planes, distance_threshold), group)
+    # 2. per-hypothesis count upper bounds (summed over the ranks), exact
+    # counts of the hypotheses the replay consults (o3dx_ransac_needed),
+    # 3. tie sums, selection replay
+    counts = allreduce_counts(be.plane_count_upper(x, planes, distance_threshold, absmax), group)
+    known = np.zeros(H, bool)
+    while True:
+        need = ops.ransac_needed(counts, known, planes, n_total, ransac_n, probability)
+        if not len(need):
+            break
+        counts[need] = allreduce_counts(be.plane_count(x, planes[need], distance_threshold), group)
+        known[need] = True
     tied = ops.ransac_tied(counts, planes, n_total, ransac_n, probability)
     sums = np.full(H, np.nan)
     if len(tied):

@@ -300,6 +300,38 @@ def plane_count(xyz: torch.Tensor, planes: np.ndarray, distance_threshold: float
     return counts[:H]
 
 
+def plane_count_upper(xyz: torch.Tensor, planes: np.ndarray, distance_threshold: float, absmax=None) -> np.ndarray:
+    """Upper bounds of the per-hypothesis inlier counts (>= exact; -1 for
+    degenerate planes), o3dx_plane_count_upper; absmax: the cloud's |x|,|y|,|z|
+    bounds (None: its own)."""
+    x = _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    P = _c(planes, np.float64).reshape(-1, 4)
+    H = P.shape[0]
+    counts = np.zeros(max(H, 1), np.int64)
+    am = None if absmax is None else _c(absmax, np.float64)
+    ws = N.workspace(L.o3dx_plane_count_workspace_bytes(n, H), x.device)
+    N.check(L.o3dx_plane_count_upper(N.ptr(x), n, _np_ptr(P), H, float(distance_threshold),
+                                     None if am is None else _np_ptr(am), _np_ptr(counts), N.ptr(ws), ws.numel(),
+                                     N.stream_ptr(x.device)), "plane_count_upper")
+    return counts[:H]
+
+
+def ransac_needed(counts, known, planes, n: int, ransac_n: int, probability: float = 0.99999999) -> np.ndarray:
+    """The hypotheses without an exact count (known False) that Open3D's
+    selection replay on `counts` consults (o3dx_ransac_needed); empty: the
+    selection on these counts is the exact one."""
+    c = _c(counts, np.int64)
+    k8 = _c(np.asarray(known, bool).astype(np.uint8), np.uint8)
+    P = _c(planes, np.float64).reshape(-1, 4)
+    out = np.zeros(max(len(c), 1), np.int32)
+    k = np.zeros(1, np.int32)
+    N.check(N.load().o3dx_ransac_needed(_np_ptr(c), _np_ptr(k8), _np_ptr(P), len(c), int(n), int(ransac_n),
+                                        float(probability), _np_ptr(out), _np_ptr(k)), "ransac_needed")
+    return out[: int(k[0])].copy()
+
+
 def plane_abs_sum(xyz: torch.Tensor, planes: np.ndarray, which, distance_threshold: float, return_fx: bool = False):
     """Sigma |d| over |d| < thr of the hypotheses `which` (exact fx sums):
     float64 (L,), and with return_fx their (L, 4) int64 fx rows."""

@@ -288,6 +288,12 @@ class OracleBackend:
                 out.append(int((NPR.plane_dist(pl, p) < thr).sum()))
         return np.array(out, np.int64)
 
+    def plane_count_upper(self, x, planes, thr, absmax):
+        # a valid upper bound that differs from the exact count, so the exact
+        # rounds of the sharded selection (o3dx_ransac_needed) are exercised
+        c = self.plane_count(x, planes, thr)
+        return np.where(c >= 0, c + np.arange(len(c)) % 3, c)
+
     def abs_sum_fx(self, x, planes, which, thr):
         return np.stack([NPR.plane_abs_sum_fx(x.numpy(), planes[w], thr) for w in which])
 

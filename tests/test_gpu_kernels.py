@@ -567,10 +567,10 @@ def test_voxel_down_sample_normals_fused(dev, bunny, case):
                    what=f"fused_{case}")
 
 
-@pytest.mark.parametrize("shape", ["32x16", "32x8", "16x16", "16x8"])
+@pytest.mark.parametrize("shape", ["32x16x0x0", "32x16x0", "32x16x1x0", "32x8x0", "16x16x0x8", "16x16x1x0", "32x24x0x0", "32x16x0x8", "8x16x0x8"])
 def test_plane_count_shapes(dev, shape, monkeypatch):
-    """Every instantiated (hypotheses per wave x points per lane) shape of
-    the lane-counter kernel gives the oracle's counts (ragged n and H)."""
+    """Every instantiated (hypotheses per wave x points per lane x prefetch)
+    shape of the count kernel gives the oracle's counts (ragged n and H)."""
     monkeypatch.setenv("O3DX_RANSAC_SHAPE", shape)
     n, H = 70_001, 101
     pts = S.planted_plane(n, 62).numpy()
@@ -597,16 +597,18 @@ def test_plane_count_window_overflow_and_nonfinite(dev, monkeypatch):
     p64 = pts.astype(np.float64)
     ref = [int((np.abs(NPR.plane_dist(pl, p64)) < 0.01).sum()) for pl in planes]
     assert got.tolist() == ref and valu.tolist() == ref
+    assert (ops.plane_count_upper(x, planes, 0.01) >= got).all()
     bad = np.vstack([planes, [[np.nan, 0.0, 1.0, 0.0]]])
     got = ops.plane_count(x, bad, 0.01)
     assert got[:3].tolist() == ref and got[3] == 0
+    assert ops.plane_count_upper(x, bad, 0.01)[3] == 0
 
 
 @pytest.mark.parametrize("n,H,thr", [(1, 3, 0.01), (17, 5, 0.01), (1025, 33, 0.01), (100_003, 257, 0.01),
                                      (100_003, 257, 1e-7), (1_000_000, 1000, 0.01)])
 def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatch):
-    """The lane-counter count (default), the matrix-core count and the
-    ballot kernel give the same exact counts, equal to the oracle's, for
+    """The scalar-counter count (default) and the ballot kernel give the
+    same exact counts, equal to the oracle's, for
     ragged sizes (n not a multiple of the 1024-point batch, H not of the
     32-hypothesis chunk), degenerate hypotheses, and a threshold below the
     float32 window (lo < 0: the window holds the near-plane points)."""
@@ -617,13 +619,14 @@ def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatc
     planes = np.stack([NPR.triangle_plane(*pts[s].astype(np.float64)) for s in samples])
     x = torch.from_numpy(pts).to(dev)
     got = ops.plane_count(x, planes, thr)
-    monkeypatch.setenv("O3DX_RANSAC_MFMA", "1")
-    brute = ops.plane_count(x, planes, thr)
-    monkeypatch.delenv("O3DX_RANSAC_MFMA")
     monkeypatch.setenv("O3DX_RANSAC_VALU", "1")
     valu = ops.plane_count(x, planes, thr)
     monkeypatch.delenv("O3DX_RANSAC_VALU")
-    assert np.array_equal(got, brute) and np.array_equal(got, valu)
+    assert np.array_equal(got, valu)
+    # segment_plane's sweep: upper bounds, -1 exactly where degenerate
+    ub = ops.plane_count_upper(x, planes, thr)
+    assert np.array_equal(ub < 0, got < 0) and (ub >= got).all()
+    assert (ub - got).max() <= max(8, n // 10000)  # only window points add
     ref = NPR.segment_plane_counts(pts, thr, samples) if n <= 100_003 else None
     if ref is not None:
         assert np.array_equal(got, ref)

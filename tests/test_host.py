@@ -111,6 +111,39 @@ def test_planes_from_samples_and_icp_update_host():
     assert np.allclose(T1, o3p.ops.icp_solve(sums) @ T0, atol=1e-15)
 
 
+def test_ransac_needed_rounds_select_like_exact_counts():
+    """Selection on count upper bounds (o3dx_plane_count_upper) refined by
+    o3dx_ransac_needed rounds: the tied set and the selected hypothesis equal
+    those on the exact counts — random counts, zero planes, degenerate -1,
+    ties, and small n so that Open3D's early break (probability) is active."""
+    rng = np.random.default_rng(11)
+    ops = o3p.ops
+    for trial in range(300):
+        H = int(rng.integers(1, 200))
+        n = int(rng.choice([40, 60, 1000]))
+        prob = float(rng.choice([0.5, 0.9, 0.99999999, 1.0]))
+        exact = rng.integers(-1, min(n, 45), H)
+        planes = rng.normal(size=(H, 4))
+        planes[exact < 0] = 0.0
+        planes[rng.random(H) < 0.05] = 0.0  # zero planes the replay skips
+        ub = np.where(exact >= 0, exact + rng.integers(0, 4, H), exact)
+        counts, known, rounds = ub.copy(), np.zeros(H, bool), 0
+        while True:
+            need = ops.ransac_needed(counts, known, planes, n, 3, prob)
+            if not len(need):
+                break
+            assert not known[need].any()
+            counts[need] = exact[need]
+            known[need] = True
+            rounds += 1
+        assert rounds <= H
+        tie_e = ops.ransac_tied(exact, planes, n, 3, prob)
+        assert np.array_equal(ops.ransac_tied(counts, planes, n, 3, prob), tie_e)
+        sums = np.full(H, np.nan)
+        sums[tie_e] = rng.random(len(tie_e))
+        assert ops.ransac_select(counts, sums, planes, n, 3, prob) == ops.ransac_select(exact, sums, planes, n, 3, prob)
+
+
 @pytest.mark.skipif(GPU, reason="checks the no-GPU behaviour")
 def test_compute_fails_loudly_without_gpu():
     pc = o3p.PointCloud(np.random.rand(100, 3))

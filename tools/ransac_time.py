@@ -16,12 +16,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "open3d-py-extension_amd"))
 from open3dpypro import _native as N, ops, synthetic as S  # noqa: E402
 
-VARIANTS = [("counters_32x16", {}), ("counters_16x16", {"O3DX_RANSAC_SHAPE": "16x16"}),
-            ("mfma", {"O3DX_RANSAC_MFMA": "1"}), ("ballot_legacy", {"O3DX_RANSAC_VALU": "1"})]
+if os.environ.get("O3DX_LIB_CMP"):  # A/B: a library built from an earlier ransac.hip
+    N.LIB_PATH = os.environ["O3DX_LIB_CMP"]
+
+VARIANTS = [("s32x16x0x6", {}), ("s32x16x0x0", {"O3DX_RANSAC_SHAPE": "32x16x0x0"}),
+            ("s16x16x0x8", {"O3DX_RANSAC_SHAPE": "16x16x0x8"}), ("ballot_legacy", {"O3DX_RANSAC_VALU": "1"})]
 
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    variants = VARIANTS if len(sys.argv) < 3 else [v for v in VARIANTS if v[0] in sys.argv[2].split(",")]
     dev = torch.device("cuda:0")
     n, H = 10_000_000, 1000
     x = S.planted_plane(n, 0, device=dev)
@@ -33,8 +37,8 @@ def main():
     planes = np.concatenate([nrm, -np.sum(nrm * a, 1, keepdims=True)], 1)
     ref = None
     out = {}
-    for name, env in VARIANTS:
-        for k in ("O3DX_RANSAC_VALU", "O3DX_RANSAC_SHAPE", "O3DX_RANSAC_MFMA"):
+    for name, env in variants:
+        for k in ("O3DX_RANSAC_VALU", "O3DX_RANSAC_SHAPE"):
             os.environ.pop(k, None)
         os.environ.update(env)
         got = ops.plane_count(x, planes, 0.01)  # warm-up
@@ -50,8 +54,35 @@ def main():
         out[name] = {"ms": ms / max(cnt, 1), "equal": bool(np.array_equal(got, ref)),
                      "pairs_per_s": n * H / (ms / max(cnt, 1) * 1e-3)}
         print(json.dumps({name: out[name]}), flush=True)
+    # the upper-bound count (segment_plane's sweep) and the whole segment_plane
+    for name in (os.environ.get("UPPER", "32x16x6,32x16x8,16x16x8,32x8x8")).split(","):
+        os.environ["O3DX_RANSAC_UPPER"] = name
+        ub = ops.plane_count_upper(x, planes, 0.01)
+        N.set_kernel_timing(True)
+        N.reset_kernel_timing()
+        for _ in range(reps):
+            ub = ops.plane_count_upper(x, planes, 0.01)
+        torch.cuda.synchronize()
+        ms, cnt = N.kernel_timing("plane_count_upper")
+        N.set_kernel_timing(False)
+        ok = bool(np.all(ub >= ref)) and bool(np.all((ub < 0) == (ref < 0)))
+        out["upper_" + name] = {"ms": ms / max(cnt, 1), "upper_bound_ok": ok, "max_slack": int((ub - ref).max()),
+                                "sum_slack": int((ub - ref).sum())}
+        print(json.dumps({"upper_" + name: out["upper_" + name]}), flush=True)
+    os.environ.pop("O3DX_RANSAC_UPPER", None)
+    samples = ops.ransac_samples(n, 3, H, 0)
+    ops.segment_plane(x, 0.01, 3, H, samples=samples)
+    torch.cuda.synchronize()
+    import time
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        plane, inl = ops.segment_plane(x, 0.01, 3, H, samples=samples)
+    torch.cuda.synchronize()
+    out["segment_plane_ms"] = (time.perf_counter() - t0) / reps * 1e3
+    print(json.dumps({"segment_plane_ms": out["segment_plane_ms"], "inliers": int(inl.numel())}), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ransac_time.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ransac_time%s.json" % os.environ.get("TAG", "")), "w"),
+              indent=1)
 
 
 if __name__ == "__main__":
