@@ -164,7 +164,8 @@ int o3dx_voxel_down_sample(const float* xyz_dev, int64_t n,
  *   voxel_pts_dev[0..4 nvox)  per voxel (x, y, z, output row as int32 bits)
  *                             of its representative, row -1 when empty
  *   geom_host[12]             {min_bound xyz, voxel_size, nx, ny, nz, valid,
- *                              occupied 2^3-voxel cells, 0, 0, nvox}
+ *                              occupied 2^3-voxel cells, x-key offset,
+ *                              build attempt (0: first), nvox}
  * valid = 0 when the table could not be kept (too sparse, larger than
  * voxel_cells, or points outside the bounds).  One host synchronisation for
  * m (two with null bounds). */

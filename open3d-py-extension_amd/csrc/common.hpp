@@ -290,5 +290,17 @@ int reduce_columns_i64(const int64_t* part, int64_t rows, int width, int64_t* ou
 // AABB on device into a device double[6] (no sync).
 size_t aabb_ws_bytes(int64_t n);
 int aabb_device(const float* xyz, int64_t n, double* mm_dev, void* ws, hipStream_t s);
+// The bounds straight to the host: the final kernel writes them into mapped
+// pinned memory followed by a sequence number the host polls (no copy kernel,
+// no stream query).  aabb_begin queues the kernels (work queued after it
+// keeps running while the host waits); aabb_end waits and returns {min, max}.
+// z0..z2: device ranges the AABB kernel zeroes on the way (clears folded in)
+struct ZeroSpan {
+  uint8_t* p = nullptr;
+  size_t bytes = 0;
+};
+int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0 = {}, ZeroSpan z1 = {},
+               ZeroSpan z2 = {});
+int aabb_end(double mm_host[6], hipStream_t s);
 
 }  // namespace o3dx

@@ -8,6 +8,8 @@
 #include <mutex>
 #include <vector>
 
+#include <atomic>
+
 #include "common.hpp"
 
 namespace o3dx {
@@ -406,13 +408,54 @@ struct P3 {
   float x, y, z;
 };
 
+// Aligned clouds are read as 16-B vectors, four points per three loads
+// (x y z x | y z x y | z x y z), two chunks in flight per lane; the rows
+// past the last whole chunk (and unaligned clouds) one point at a time.
+// zero [p, p + bytes) with the whole grid (16-B stores on the aligned middle)
+__device__ __forceinline__ void grid_zero(uint8_t* p, size_t bytes) {
+  if (!p || !bytes) return;
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
+  const size_t head = std::min(bytes, (size_t)((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15));
+  const size_t nv = (bytes - head) / 16;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  for (size_t k = t0; k < nv; k += st) q[k] = make_uint4(0, 0, 0, 0);
+  for (size_t k = t0; k < head; k += st) p[k] = 0;
+  for (size_t k = head + nv * 16 + t0; k < bytes; k += st) p[k] = 0;
+}
+
 __global__ void __launch_bounds__(kBlock) k_aabb_partial(const float* __restrict__ xyz, int64_t n,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, ZeroSpan z0 = {},
+                                                         ZeroSpan z1 = {}, ZeroSpan z2 = {}) {
+  grid_zero(z0.p, z0.bytes);
+  grid_zero(z1.p, z1.bytes);
+  grid_zero(z2.p, z2.bytes);
   float mn[3] = {INFINITY, INFINITY, INFINITY};
   float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  int64_t i0 = 0;
+  if ((reinterpret_cast<uintptr_t>(xyz) & 15) == 0) {
+    const float4* q = reinterpret_cast<const float4*>(xyz);
+    const int64_t nch = n / 4;
+    i0 = nch * 4;
+    auto take = [&](const float4 a, const float4 b, const float4 d) {
+      mn[0] = fminf(mn[0], fminf(fminf(a.x, a.w), fminf(b.z, d.y)));
+      mn[1] = fminf(mn[1], fminf(fminf(a.y, b.x), fminf(b.w, d.z)));
+      mn[2] = fminf(mn[2], fminf(fminf(a.z, b.y), fminf(d.x, d.w)));
+      mx[0] = fmaxf(mx[0], fmaxf(fmaxf(a.x, a.w), fmaxf(b.z, d.y)));
+      mx[1] = fmaxf(mx[1], fmaxf(fmaxf(a.y, b.x), fmaxf(b.w, d.z)));
+      mx[2] = fmaxf(mx[2], fmaxf(fmaxf(a.z, b.y), fmaxf(d.x, d.w)));
+    };
+    int64_t c = t0;
+    for (; c + st < nch; c += 2 * st) {
+      const float4 a = q[3 * c], b = q[3 * c + 1], d = q[3 * c + 2];
+      const float4 a2 = q[3 * (c + st)], b2 = q[3 * (c + st) + 1], d2 = q[3 * (c + st) + 2];
+      take(a, b, d);
+      take(a2, b2, d2);
+    }
+    if (c < nch) take(q[3 * c], q[3 * c + 1], q[3 * c + 2]);
+  }
+  for (int64_t i = i0 + t0; i < n; i += st) {
     P3 q = p[i];
     mn[0] = fminf(mn[0], q.x);
     mn[1] = fminf(mn[1], q.y);
@@ -460,6 +503,81 @@ __global__ void __launch_bounds__(1024) k_aabb_final(const float* __restrict__ p
     for (int k = 1; k < 170; ++k) r = a < 3 ? fminf(r, sh[a][k]) : fmaxf(r, sh[a][k]);
     mm[a] = n == 0 ? 0.0 : (double)r;
   }
+}
+
+// k_aabb_final's host-visible twin: thread a reduces column a, then the
+// values are published to mapped host memory before the sequence number
+__global__ void __launch_bounds__(1024) k_aabb_final_host(const float* __restrict__ part, int nb, int64_t n,
+                                                          double* __restrict__ mm_host, uint64_t seq,
+                                                          volatile uint64_t* seq_host) {
+  __shared__ float sh[6][171];
+  const int a = threadIdx.x % 6, g = threadIdx.x / 6;
+  if (g < 170) {
+    float r = a < 3 ? INFINITY : -INFINITY;
+    for (int b = g; b < nb; b += 170) r = a < 3 ? fminf(r, part[b * 6 + a]) : fmaxf(r, part[b * 6 + a]);
+    sh[a][g] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float r = sh[a][0];
+    for (int k = 1; k < 170; ++k) r = a < 3 ? fminf(r, sh[a][k]) : fmaxf(r, sh[a][k]);
+    mm_host[a] = n == 0 ? 0.0 : (double)r;
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    *seq_host = seq;
+  }
+}
+
+namespace {
+struct AabbMailbox {
+  uint64_t* host = nullptr;  // [0] sequence, [1..6] bounds (mapped, coherent)
+  uint64_t* dev = nullptr;
+  uint64_t seq = 0;
+};
+thread_local AabbMailbox g_ambox;
+}  // namespace
+
+int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0, ZeroSpan z1, ZeroSpan z2) {
+  AabbMailbox& m = g_ambox;
+  if (!m.host) {
+    void* h = nullptr;
+    O3DX_HIP(hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocCoherent));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return fail(O3DX_EIO, "aabb_begin: no device view of the mailbox");
+    }
+    m.host = static_cast<uint64_t*>(h);
+    m.dev = static_cast<uint64_t*>(d);
+    m.host[0] = 0;
+  }
+  ++m.seq;
+  float* part = reinterpret_cast<float*>(ws);
+  int nb = (int)std::min<int64_t>(kAabbBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
+  if (z0.bytes || z1.bytes || z2.bytes) nb = kAabbBlocks;  // the clears want the whole grid
+  hipLaunchKernelGGL(k_aabb_partial, dim3(nb), dim3(kBlock), 0, s, xyz, n, part, z0, z1, z2);
+  hipLaunchKernelGGL(k_aabb_final_host, dim3(1), dim3(1024), 0, s, part, nb, n,
+                     reinterpret_cast<double*>(m.dev + 1), m.seq, static_cast<volatile uint64_t*>(m.dev));
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+int aabb_end(double mm_host[6], hipStream_t s) {
+  AabbMailbox& m = g_ambox;
+  volatile uint64_t* q = m.host;
+  bool seen = false;
+  for (int i = 0; i < (1 << 22) && !seen; ++i) seen = *q == m.seq;  // ~ms of polling
+  if (!seen) {  // slow path: wait for the stream (errors surface here)
+    O3DX_TRY(host_wait(s));
+    seen = *q == m.seq;
+    if (!seen) return fail(O3DX_EIO, "aabb_end: bounds never arrived");
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  std::memcpy(mm_host, const_cast<const uint64_t*>(m.host) + 1, 6 * sizeof(double));
+  return 0;
 }
 
 size_t aabb_ws_bytes(int64_t) { return Arena::align(kAabbBlocks * 6 * sizeof(float)) + 256; }

@@ -2367,7 +2367,7 @@ extern "C" int o3dx_voxel_down_sample_normals(const float* xyz, int64_t n, const
                                     voxel_cells, geom, ws, ws_bytes, stream, spec_normals_hook, &c));
   const int64_t m = *m_host;
   double kth;
-  if (c.launched && dense_vox_applicable(geom, reinterpret_cast<const float4*>(voxel_pts), m, O3DX_SEARCH_KNN, knn,
+  if (c.launched && geom[10] == 0.0 && dense_vox_applicable(geom, reinterpret_cast<const float4*>(voxel_pts), m, O3DX_SEARCH_KNN, knn,
                                          &kth) &&
       std::min<int64_t>(knn, m) == knn)
     return 0;

@@ -116,13 +116,18 @@ __device__ __forceinline__ uint32_t brick_code(const int v[3], const Bricks& b) 
   return (bk << 16) | lx | (ly << b.sx) | (lz << (b.sx + b.sy));
 }
 
-// Pass 1: brick counts per block (LDS histogram), stored brick-major —
-// hist[k * nblk + block] — so that one exclusive scan gives every block its
-// run in every brick (no global atomics).  Also writes the voxel id per
-// point when the trace needs it.
+// Pass 1: brick counts per block (LDS histogram); each block reserves its run
+// in every brick it touches with one atomic on the brick's total (totals on
+// separate 64-B lines), so no scan over (brick, block) is needed: the order of
+// the runs inside a brick is the atomics' (the reduce takes a max, which does
+// not care).  roff[block * nb + k] = the block's offset inside brick k.  Also
+// writes the voxel id per point when the trace needs it.
+constexpr int kTotStride = 16;  // int32 per brick total (one 64-B line each)
+
 __global__ void __launch_bounds__(kBinBlock) k_vbin_count(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                       Bricks b, int32_t* __restrict__ bhist,
-                                                       int32_t* __restrict__ vid, int* __restrict__ err) {
+                                                       Bricks b, int32_t* __restrict__ roff,
+                                                       int32_t* __restrict__ btot, int32_t* __restrict__ vid,
+                                                       int* __restrict__ err) {
   __shared__ int32_t hist[kMaxBuckets];
   const P3* p = reinterpret_cast<const P3*>(xyz);
   for (int k = threadIdx.x; k < b.nb; k += kBinBlock) hist[k] = 0;
@@ -141,7 +146,27 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_count(const float* __restric
   }
   if (bad) *err = 1;
   __syncthreads();
-  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) bhist[(int64_t)k * gridDim.x + blockIdx.x] = hist[k];
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) {
+    const int c = hist[k];
+    roff[(int64_t)blockIdx.x * b.nb + k] = c ? atomicAdd(&btot[k * kTotStride], c) : 0;
+  }
+}
+
+// Exclusive scan of the brick totals into LDS base[0..nb] (each thread a span
+// of bricks); every scatter block and the reduce recompute it from the totals.
+__device__ __forceinline__ void brick_bases(const int32_t* __restrict__ btot, int nb, int32_t* base, int32_t* wsum) {
+  const int span = (nb + kBinBlock - 1) / kBinBlock;
+  const int k0 = threadIdx.x * span, k1 = min(k0 + span, nb);
+  int run = 0;
+  for (int k = k0; k < k1; ++k) run += btot[k * kTotStride];
+  int tot;
+  int ex = block_excl_scan<kBinBlock>(run, wsum, &tot);
+  for (int k = k0; k < k1; ++k) {
+    base[k] = ex;
+    ex += btot[k * kTotStride];
+  }
+  if (threadIdx.x == 0) base[nb] = tot;
+  __syncthreads();
 }
 
 // Pass 2: scatter (local << 32 | index) into the block's run of each brick
@@ -150,11 +175,13 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_count(const float* __restric
 // leave as one contiguous run (coalesced stores instead of one line per lane).
 constexpr int kBinRound = 4096;
 
-// dynamic LDS: stage[kBinRound] (u64), cur[nb], loc[nb]
-inline size_t scatter_lds_bytes(int nb) { return kBinRound * sizeof(uint64_t) + 2 * (size_t)nb * sizeof(int32_t); }
+// dynamic LDS: stage[kBinRound] (u64), cur[nb], loc[nb + 1]
+inline size_t scatter_lds_bytes(int nb) { return kBinRound * sizeof(uint64_t) + (2 * (size_t)nb + 1) * sizeof(int32_t); }
 
 __global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                         Bricks b, const int32_t* __restrict__ boff,
+                                                         Bricks b, const int32_t* __restrict__ roff,
+                                                         const int32_t* __restrict__ btot,
+                                                         int32_t* __restrict__ bbase,
                                                          uint64_t* __restrict__ entries) {
   static_assert(kBinChunk % kBinRound == 0 && kBinRound % kBinBlock == 0, "round shape");
   extern __shared__ uint64_t lds_u64[];
@@ -163,7 +190,11 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restr
   int32_t* loc = cur + b.nb;                                         // round: count -> offset -> cursor
   __shared__ int32_t wsum[kBinBlock / 64 + 1];
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) cur[k] = boff[(int64_t)k * gridDim.x + blockIdx.x];
+  brick_bases(btot, b.nb, loc, wsum);  // loc[] holds the bases until the first round resets it
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) cur[k] = loc[k] + roff[(int64_t)blockIdx.x * b.nb + k];
+  if (blockIdx.x == 0)
+    for (int k = threadIdx.x; k <= b.nb; k += kBinBlock) bbase[k] = loc[k];
+  __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kBinChunk;
   constexpr int kPer = kBinRound / kBinBlock;           // points per thread per round
   const int span = (b.nb + kBinBlock - 1) / kBinBlock;  // bricks per thread in the local scan
@@ -215,23 +246,108 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restr
   }
 }
 
+// One-pass binning (replaces count + scatter when every brick's entries fit
+// a fixed segment of `cap` slots): a block bins its 8192 points by brick in
+// LDS, reserves each brick's run with one atomic on the brick's total (the
+// run lands at k * cap + offset: no scan over bricks or blocks), and writes
+// the runs from the LDS stage.  A brick whose total passes cap drops the
+// excess and raises err bit 16: the host reruns with count + scatter.
+constexpr int kFusePer = 16;
+constexpr int kFuseChunk = kBinBlock * kFusePer;
+
+// dynamic LDS: stage[kFuseChunk] (u64), loc[nb + 1], dst[nb]
+inline size_t fused_lds_bytes(int nb) { return kFuseChunk * sizeof(uint64_t) + (2 * (size_t)nb + 1) * sizeof(int32_t); }
+
+__global__ void __launch_bounds__(kBinBlock) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+                                                       Bricks b, int cap, int32_t* __restrict__ btot,
+                                                       uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
+                                                       int* __restrict__ err) {
+  extern __shared__ uint64_t lds_u64[];
+  uint64_t* stage = lds_u64;
+  int32_t* loc = reinterpret_cast<int32_t*>(lds_u64 + kFuseChunk);  // count -> offset -> cursor
+  int32_t* dst = loc + b.nb + 1;                                      // segment index of stage slot 0, per brick
+  __shared__ int32_t wsum[kBinBlock / 64 + 1];
+  __shared__ int ovf;
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) loc[k] = 0;
+  if (threadIdx.x == 0) ovf = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kFuseChunk;
+  uint32_t code[kFusePer];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < kFusePer; ++j) {
+    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    code[j] = ~0u;
+    if (i < n) {
+      int v[3];
+      if (voxel_of(p[i], g, v)) {
+        code[j] = brick_code(v, b);
+        atomicAdd(&loc[code[j] >> 16], 1);
+        if (vid) vid[i] = v[0] + g.nx * (v[1] + g.ny * v[2]);
+      } else {
+        bad = true;
+        if (vid) vid[i] = -1;
+      }
+    }
+  }
+  if (bad) *err = 1;
+  __syncthreads();
+  const int span = (b.nb + kBinBlock - 1) / kBinBlock;
+  const int k0 = threadIdx.x * span, k1 = min(k0 + span, b.nb);
+  int run = 0;
+  for (int k = k0; k < k1; ++k) run += loc[k];
+  int tot;
+  int ex = block_excl_scan<kBinBlock>(run, wsum, &tot);
+  for (int k = k0; k < k1; ++k) {
+    const int c = loc[k];
+    loc[k] = ex;
+    if (c) {
+      const int o = atomicAdd(&btot[k * kTotStride], c);
+      if (o + c > cap) ovf = 1;
+      dst[k] = o - ex;  // slot t of brick k -> k * cap + dst[k] + t
+    }
+    ex += c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kFusePer; ++j) {
+    if (code[j] == ~0u) continue;
+    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    const int at = atomicAdd(&loc[code[j] >> 16], 1);
+    stage[at] = ((uint64_t)(code[j] >> 16) << 48) | ((uint64_t)(code[j] & 0xffffu) << 32) | (uint32_t)i;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < tot; t += kBinBlock) {
+    const uint64_t e = stage[t];
+    const int k = (int)(e >> 48);
+    const int o = dst[k] + t;
+    if (o < cap) entries[(int64_t)k * cap + o] = e & 0x0000ffffffffffffull;
+  }
+  if (threadIdx.x == 0 && ovf) atomicOr(err, 16);
+}
+
 // Pass 3: one workgroup per brick: max index per voxel in LDS, then the
 // brick's slice of the dense table (-1 = empty) and flags[rep] = 1.
 // occ2 (nullable; bricks at least 2 voxels along every axis, so the even-
 // aligned 2^3 cells never straddle two bricks): the brick's occupied 2^3
 // cells, one atomic per brick (the normals' local-dimension estimate).
 __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __restrict__ entries,
-                                                              const int32_t* __restrict__ boff, int nblk,
-                                                              VoxelGeom g, Bricks b, int32_t* __restrict__ table,
+                                                              const int32_t* __restrict__ bbase, int cap,
+                                                              const int32_t* __restrict__ btot, VoxelGeom g,
+                                                              Bricks b, int32_t* __restrict__ table,
                                                               uint8_t* __restrict__ flags,
-                                                              unsigned long long* __restrict__ occ2) {
+                                                              unsigned long long* __restrict__ occ2,
+                                                              float4* __restrict__ vox_empty) {
   __shared__ int32_t tab[1 << kMaxBrickBits];
   const int nloc = 1 << (b.sx + b.sy + b.sz);
   for (int k = threadIdx.x; k < nloc; k += kReduceBlock) tab[k] = -1;
   __syncthreads();
   const int bk = blockIdx.x;
-  const int32_t e0 = boff[(int64_t)bk * nblk], e1 = boff[(int64_t)(bk + 1) * nblk];
-  for (int32_t e = e0 + threadIdx.x; e < e1; e += kReduceBlock) {
+  // the brick's entries: its run of the scanned layout, or its fixed segment
+  const int64_t e0 = cap ? (int64_t)bk * cap : bbase[bk];
+  const int64_t e1 = cap ? e0 + min(btot[bk * kTotStride], cap) : bbase[bk + 1];
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kReduceBlock) {
     const uint64_t w = entries[e];
     atomicMax(&tab[(int)(w >> 32)], (int32_t)(uint32_t)w);
   }
@@ -243,8 +359,12 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
     const int z = (bz << b.sz) + (k >> (b.sx + b.sy));
     if (x >= g.nx || y >= g.ny || z >= g.nz) continue;
     const int32_t r = tab[k];
-    table[x + (int64_t)g.nx * (y + (int64_t)g.ny * z)] = r;
+    const int64_t at = x + (int64_t)g.nx * (y + (int64_t)g.ny * z);
+    if (table) table[at] = r;
     if (r >= 0) flags[r] = 1;
+    // the kept table's empty slots (k_gather_vox fills the occupied ones)
+    else if (vox_empty) vox_empty[at] = make_float4(__int_as_float(-1), __int_as_float(-1), __int_as_float(-1),
+                                                     __int_as_float(-1));
   }
   if (occ2) {
     // 2^3 cells of the brick: cell c = (cx, cy, cz) local, voxels outside the
@@ -644,6 +764,9 @@ __global__ void __launch_bounds__(kBlock) k_voxel_occ2(const T* __restrict__ tab
 }
 
 static int64_t dense_cap(int64_t n) { return 2 * n + (1 << 20); }
+// binned entries: n for the scanned layout, + 1/2 + 2^20 of segment slack
+static int64_t entries_cap(int64_t n) { return n + n / 2 + (1 << 20); }
+static thread_local uint64_t g_fused_overflow_key = ~0ull;  // last geometry whose one-pass binning overflowed
 static int64_t bin_blocks(int64_t n) { return (n + kBinChunk - 1) / kBinChunk; }
 static int64_t bin_hist_ints(int64_t n) { return bin_blocks(n) * kMaxBuckets; }
 static int64_t hash_cap(int64_t n) {
@@ -674,9 +797,9 @@ static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
   char* tb = ar.take<char>(table_bytes);
   w->table = reinterpret_cast<int32_t*>(tb);
   w->keys = tb ? reinterpret_cast<unsigned long long*>(tb + Arena::align(hc * sizeof(int32_t))) : nullptr;
-  w->entries = ar.take<uint64_t>(n);
+  w->entries = ar.take<uint64_t>(entries_cap(n));
   w->bhist = ar.take<int32_t>(bin_hist_ints(n));
-  w->boff = ar.take<int32_t>(bin_hist_ints(n) + 1);
+  w->boff = ar.take<int32_t>(std::max<int64_t>(bin_hist_ints(n) + 1, (int64_t)kMaxBuckets * (kTotStride + 1) + 1));
   w->vid = ar.take<int32_t>(n);
   w->flags = ar.take<uint8_t>(n + 16);
   w->pos = ar.take<int32_t>(n);
@@ -734,15 +857,26 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
                                                  Arena::align(hash_cap(std::max<int64_t>(n, 1)) * 4));
 
   double mn[3], mx[3];
+  // the clears that do not depend on the geometry run while the host waits
+  // for the bounds (the first attempt below skips them)
+  auto clears = [&]() -> int {
+    O3DX_HIP(hipMemsetAsync(w.count, 0, 8 * sizeof(int64_t), s));
+    O3DX_HIP(hipMemsetAsync(w.boff, 0, (size_t)kMaxBuckets * kTotStride * sizeof(int32_t), s));
+    if (n > 0) O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
+    return 0;
+  };
   if (!min_bound_host || !max_bound_host) {
     double mm[6];
-    O3DX_TRY(aabb_device(xyz, n, w.mm, w.aabb, s));
-    O3DX_TRY(read_back(mm, w.mm, 6 * sizeof(double), s));
+    O3DX_TRY(aabb_begin(xyz, n, w.aabb, s, ZeroSpan{reinterpret_cast<uint8_t*>(w.count), 8 * sizeof(int64_t)},
+                        ZeroSpan{reinterpret_cast<uint8_t*>(w.boff), (size_t)kMaxBuckets * kTotStride * sizeof(int32_t)},
+                        ZeroSpan{w.flags, (size_t)n}));
+    O3DX_TRY(aabb_end(mm, s));
     for (int a = 0; a < 3; ++a) {
       mn[a] = min_bound_host ? min_bound_host[a] : mm[a];
       mx[a] = max_bound_host ? max_bound_host[a] : mm[3 + a];
     }
   } else {
+    O3DX_TRY(clears());
     for (int a = 0; a < 3; ++a) {
       mn[a] = min_bound_host[a];
       mx[a] = max_bound_host[a];
@@ -784,30 +918,54 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   int64_t hbin_min = (int64_t)1 << 22;
   if (const char* e = getenv("O3DX_VOXEL_HBIN_MIN")) hbin_min = atoll(e);  // tests / tuning
   bool hbin_ok = hbin_min >= 0;
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  bool fused_ok = true;
+  int attempts_made = 0;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    attempts_made = attempt;
     grid_kept = false;
     int64_t nslots;
-    O3DX_HIP(hipMemsetAsync(w.count, 0, 8 * sizeof(int64_t), s));
+    if (attempt > 0) O3DX_TRY(clears());
     const Bricks bricks = dense ? plan_bricks(g.nx, g.ny, g.nz) : Bricks{};
     if (dense && bricks.nb > 0 && !getenv("O3DX_VOXEL_PLAIN")) {
       nslots = (int64_t)nvox;
       const unsigned nblk = (unsigned)((n + kBinChunk - 1) / kBinChunk);
       KTimer kt("voxel_assign", s);
-      O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
-      hipLaunchKernelGGL(k_vbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bhist,
-                         (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
-      O3DX_TRY(exclusive_scan_i32(w.bhist, w.boff, (int64_t)bricks.nb * nblk, w.scan_tmp, s));
-      hipLaunchKernelGGL(k_vbin_scatter, dim3(nblk), dim3(kBinBlock), scatter_lds_bytes(bricks.nb), s, xyz, n, g,
-                         bricks, w.boff, w.entries);
+      // the brick totals (w.boff, cleared with the counts)
+      int32_t* btot = w.boff;
+      int32_t* bbase = w.boff + (size_t)kMaxBuckets * kTotStride;
+      // one pass into fixed per-brick segments when a segment holds a full
+      // brick's share of a uniform cloud with room to spare (and this
+      // geometry did not overflow last time)
+      const int64_t seg = entries_cap(n) / bricks.nb;
+      const double full = (double)n * std::ldexp(1.0, bricks.sx + bricks.sy + bricks.sz) / nvox;
+      const uint64_t gkey = ((uint64_t)g.nx * 73856093u) ^ ((uint64_t)g.ny * 19349663u) ^
+                            ((uint64_t)g.nz * 83492791u) ^ (uint64_t)n;
+      const bool fused = fused_ok && seg <= INT32_MAX && (double)seg >= 1.03 * full + 2048.0 &&
+                         g_fused_overflow_key != gkey && !getenv("O3DX_VOXEL_TWOPASS");
+      const int cap = fused ? (int)seg : 0;
+      if (fused) {
+        const unsigned nfb = (unsigned)((n + kFuseChunk - 1) / kFuseChunk);
+        hipLaunchKernelGGL(k_vbin_fused, dim3(nfb), dim3(kBinBlock), fused_lds_bytes(bricks.nb), s, xyz, n, g, bricks,
+                           cap, btot, w.entries, (voxel_of_point || cubic_id) ? w.vid : nullptr,
+                           reinterpret_cast<int*>(w.count + 1));
+      } else {
+        hipLaunchKernelGGL(k_vbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bhist, btot,
+                           (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
+        hipLaunchKernelGGL(k_vbin_scatter, dim3(nblk), dim3(kBinBlock), scatter_lds_bytes(bricks.nb), s, xyz, n, g,
+                           bricks, w.bhist, btot, bbase, w.entries);
+      }
       const bool keep = vox && nslots <= vox_cap;
       const bool occ_in_reduce = keep && bricks.sx >= 1 && bricks.sy >= 1 && bricks.sz >= 1;
-      hipLaunchKernelGGL(k_vbin_reduce, dim3(bricks.nb), dim3(kReduceBlock), 0, s, w.entries, w.boff, (int)nblk, g,
-                         bricks, w.table, w.flags,
-                         occ_in_reduce ? reinterpret_cast<unsigned long long*>(w.count + 2) : nullptr);
+      const bool trace = voxel_of_point || cubic_id;
+      // the int32 table is only read by the trace and the standalone occupancy pass
+      hipLaunchKernelGGL(k_vbin_reduce, dim3(bricks.nb), dim3(kReduceBlock), 0, s, w.entries, bbase, cap, btot, g,
+                         bricks,
+                         (trace || (keep && !occ_in_reduce)) ? w.table : nullptr, w.flags,
+                         occ_in_reduce ? reinterpret_cast<unsigned long long*>(w.count + 2) : nullptr,
+                         keep ? reinterpret_cast<float4*>(vox) : nullptr);
       kt.stop();
       KTimer kc("voxel_compact", s);
       if (keep) {
-        O3DX_HIP(hipMemsetAsync(vox, 0xFF, (size_t)nslots * 4 * sizeof(float), s));
         if (!occ_in_reduce) {
           const int64_t nc2 = (int64_t)((g.nx + 1) / 2) * ((g.ny + 1) / 2) * ((g.nz + 1) / 2);
           hipLaunchKernelGGL(k_voxel_occ2<int32_t>, dim3(grid_for(nc2, kBlock, 1024)), dim3(kBlock), 0, s, w.table,
@@ -829,7 +987,6 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
         slots = std::max(2, std::min(slots, atoi(e)));
       const bool trace = voxel_of_point || cubic_id;
       KTimer kt("voxel_assign", s);
-      O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
       hipLaunchKernelGGL(k_hbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, hm, w.bhist,
                          reinterpret_cast<int*>(w.count + 1));
       O3DX_TRY(exclusive_scan_i32(w.bhist, w.boff, (int64_t)kHBins * nblk, w.scan_tmp, s));
@@ -858,7 +1015,6 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
                            (uint32_t)(nslots - 1), w.vid, reinterpret_cast<int*>(w.count + 1));
       }
       KTimer kt("voxel_compact", s);
-      O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
       hipLaunchKernelGGL(k_voxel_mark, dim3(grid_for(nslots, kBlock, 8192)), dim3(kBlock), 0, s, w.table, nslots,
                          w.flags);
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
@@ -885,6 +1041,13 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     }
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
+    if (errflag & 16) {  // a brick outgrew its one-pass segment: count + scatter (and remember)
+      g_fused_overflow_key = ((uint64_t)g.nx * 73856093u) ^ ((uint64_t)g.ny * 19349663u) ^
+                             ((uint64_t)g.nz * 83492791u) ^ (uint64_t)n;
+      fused_ok = false;
+      if (!(errflag & ~16)) continue;
+      errflag &= ~16;
+    }
     if ((errflag & 12) && !(errflag & ~12)) {  // hash-binned path: bin table full / point outside: global hash
       hbin_ok = false;
       continue;
@@ -897,8 +1060,10 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   const int64_t m = counts[0];
   *m_host = m;
   if (geom && grid_kept) {
+    // geom[10]: the attempt that built the table (> 0: a hook fired on attempt
+    // 0 saw a table that was rebuilt since)
     const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny,
-                           (double)g.nz, 1.0, (double)counts[2], (double)g.kx0, 0.0, nvox};
+                           (double)g.nz, 1.0, (double)counts[2], (double)g.kx0, (double)attempts_made, nvox};
     for (int k = 0; k < 12; ++k) geom[k] = gv[k];
   }
   if ((voxel_of_point || cubic_id) && m > 0) {

@@ -58,6 +58,38 @@ def test_voxel_uniform(dev, n, seed):
         assert np.array_equal(rep, NPR.voxel_down_sample(pts.numpy(), vs))
 
 
+@pytest.mark.parametrize("case", ["uniform", "hot_brick"])
+def test_voxel_binning_one_pass_and_fallback(dev, monkeypatch, case):
+    """The one-pass binning into fixed per-brick segments (uniform cloud) and
+    its fall-back to count + scatter when a brick outgrows its segment (75 %
+    of the points in one brick): representatives, trace and the one-call
+    normals equal the oracle's / the two-pass path's.  The hot-brick one-call
+    run fires the normals on attempt 0's table and must redo them on the
+    rebuilt one (geom[10])."""
+    rng = np.random.default_rng(41)
+    if case == "uniform":
+        n = 400_001
+        pts = rng.random((n, 3)).astype(np.float32)
+    else:
+        n = 400_003
+        pts = np.concatenate([rng.random((300_003, 3)) * 0.01, rng.random((100_000, 3))]).astype(np.float32)
+        pts = pts[rng.permutation(n)]
+    vs = 0.01
+    x = torch.from_numpy(pts).to(dev)
+    f = ops.voxel_down_sample_normals(x, vs, knn=30)  # first: the one-pass attempt (and its overflow)
+    out = ops.voxel_down_sample(x, vs, trace=True)
+    ref, vop, cub = O.voxel_down_sample(pts, vs, trace=True)
+    assert np.array_equal(out["rep_idx"].cpu().numpy(), ref)
+    assert np.array_equal(out["voxel_of_point"].cpu().numpy(), vop)
+    assert np.array_equal(out["cubic_id"].cpu().numpy(), cub)
+    monkeypatch.setenv("O3DX_VOXEL_TWOPASS", "1")
+    a = ops.voxel_down_sample(x, vs, keep_grid=True)
+    monkeypatch.delenv("O3DX_VOXEL_TWOPASS")
+    assert np.array_equal(a["rep_idx"].cpu().numpy(), ref)
+    ref_n = ops.estimate_normals(a["rep_xyz"], knn=30, voxel_grid=a["voxel_grid"])
+    assert torch.equal(f["rep_idx"], a["rep_idx"]) and torch.equal(f["normals"], ref_n)
+
+
 def test_voxel_hash_path_and_bounds(dev):
     # sparse clusters far apart -> grid box >> 2n cells -> hash table path
     rng = np.random.default_rng(5)
