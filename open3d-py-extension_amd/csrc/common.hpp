@@ -302,5 +302,8 @@ struct ZeroSpan {
 int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0 = {}, ZeroSpan z1 = {},
                ZeroSpan z2 = {});
 int aabb_end(double mm_host[6], hipStream_t s);
+// device view of the bounds aabb_begin's kernels publish ({min, max}, 6
+// doubles): readable by kernels queued after it on the same stream
+const double* aabb_mailbox_dev();
 
 }  // namespace o3dx

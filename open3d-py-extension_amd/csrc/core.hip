@@ -565,6 +565,8 @@ int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0
   return 0;
 }
 
+const double* aabb_mailbox_dev() { return reinterpret_cast<const double*>(g_ambox.dev + 1); }
+
 int aabb_end(double mm_host[6], hipStream_t s) {
   AabbMailbox& m = g_ambox;
   volatile uint64_t* q = m.host;

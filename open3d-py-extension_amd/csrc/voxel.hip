@@ -32,7 +32,8 @@ constexpr int kHashOff = 1 << (kHashBits - 1);
 struct VoxelGeom {
   double mnx, mny, mnz, vs;
   int nx, ny, nz;
-  int kx0 = 0;  // x-key window [kx0, kx0 + nx) of a slab (keys stay those of min_bound)
+  int kx0 = 0;     // x-key window [kx0, kx0 + nx) of a slab (keys stay those of min_bound)
+  double ivs = 0;  // 1 / vs (the binning's multiply; keys stay the division's, voxel_of)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t k) {
@@ -103,9 +104,22 @@ struct Bricks {
   int nb;
 };
 
+// floor(d / vs) through a multiply: q = d * (1/vs) is within |q| 2^-51 of the
+// division's correctly rounded quotient, so their floors can only differ
+// when an integer lies within that distance of q; those keys (~2^-20 of
+// them) take the division.  Bit-identical keys at a third of the f64 work.
+__device__ __forceinline__ int voxel_key(double d, double vs, double ivs) {
+  const double q = d * ivs;
+  const double k = floor(q);
+  const double f = q - k;
+  const double tol = fabs(q) * 0x1p-50;
+  return (int)((f <= tol || f >= 1.0 - tol) ? floor(d / vs) : k);
+}
+
 __device__ __forceinline__ bool voxel_of(const P3& q, const VoxelGeom& g, int v[3]) {
-  double r[3];
-  voxel_ref(q, g, r, v);
+  v[0] = voxel_key((double)q.x - g.mnx, g.vs, g.ivs) - g.kx0;
+  v[1] = voxel_key((double)q.y - g.mny, g.vs, g.ivs);
+  v[2] = voxel_key((double)q.z - g.mnz, g.vs, g.ivs);
   return v[0] >= 0 && v[0] < g.nx && v[1] >= 0 && v[1] < g.ny && v[2] >= 0 && v[2] < g.nz;
 }
 
@@ -258,10 +272,10 @@ constexpr int kFuseChunk = kBinBlock * kFusePer;
 // dynamic LDS: stage[kFuseChunk] (u64), loc[nb + 1], dst[nb]
 inline size_t fused_lds_bytes(int nb) { return kFuseChunk * sizeof(uint64_t) + (2 * (size_t)nb + 1) * sizeof(int32_t); }
 
-__global__ void __launch_bounds__(kBinBlock) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                       Bricks b, int cap, int32_t* __restrict__ btot,
-                                                       uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
-                                                       int* __restrict__ err) {
+__device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, int64_t n, const VoxelGeom& g,
+                                                const Bricks& b, int cap, int32_t* __restrict__ btot,
+                                                uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
+                                                int* __restrict__ err) {
   extern __shared__ uint64_t lds_u64[];
   uint64_t* stage = lds_u64;
   int32_t* loc = reinterpret_cast<int32_t*>(lds_u64 + kFuseChunk);  // count -> offset -> cursor
@@ -275,13 +289,17 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_fused(const float* __restric
   const int64_t base = (int64_t)blockIdx.x * kFuseChunk;
   uint32_t code[kFusePer];
   bool bad = false;
+  // every load of the chunk first (clamped, unconditional), then the keys
+  P3 q[kFusePer];
+#pragma unroll
+  for (int j = 0; j < kFusePer; ++j) q[j] = p[min(base + threadIdx.x + (int64_t)j * kBinBlock, n - 1)];
 #pragma unroll
   for (int j = 0; j < kFusePer; ++j) {
     const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
     code[j] = ~0u;
     if (i < n) {
       int v[3];
-      if (voxel_of(p[i], g, v)) {
+      if (voxel_of(q[j], g, v)) {
         code[j] = brick_code(v, b);
         atomicAdd(&loc[code[j] >> 16], 1);
         if (vid) vid[i] = v[0] + g.nx * (v[1] + g.ny * v[2]);
@@ -325,6 +343,13 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_fused(const float* __restric
     if (o < cap) entries[(int64_t)k * cap + o] = e & 0x0000ffffffffffffull;
   }
   if (threadIdx.x == 0 && ovf) atomicOr(err, 16);
+}
+
+__global__ void __launch_bounds__(kBinBlock) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+                                                       Bricks b, int cap, int32_t* __restrict__ btot,
+                                                       uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
+                                                       int* __restrict__ err) {
+  vbin_fused_body(xyz, n, g, b, cap, btot, entries, vid, err);
 }
 
 // Pass 3: one workgroup per brick: max index per voxel in LDS, then the
@@ -397,7 +422,7 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
 // Brick shape: 2^bits voxels, split over the axes by repeatedly doubling the
 // axis with the most bricks left; nb = 0 when the grid needs more than
 // kMaxBuckets bricks (the plain dense path handles it).
-static Bricks plan_bricks(int nx, int ny, int nz) {
+__host__ __device__ static Bricks plan_bricks(int nx, int ny, int nz, int max_buckets = kMaxBuckets) {
   Bricks b{};
   for (int bits = 12; bits <= kMaxBrickBits; ++bits) {
     int sh[3] = {0, 0, 0};
@@ -418,12 +443,82 @@ static Bricks plan_bricks(int nx, int ny, int nz) {
     int64_t nb[3];
     for (int a = 0; a < 3; ++a) nb[a] = (d[a] + (1ll << sh[a]) - 1) >> sh[a];
     const int64_t total = nb[0] * nb[1] * nb[2];
-    if (total <= kMaxBuckets) {
+    if (total <= max_buckets) {
       b = Bricks{sh[0], sh[1], sh[2], (int)nb[0], (int)nb[1], (int)nb[2], (int)total};
       return b;
     }
   }
   return b;
+}
+
+// The one-pass binning's plan from the bounds, the same function on the host
+// and (pre-launched, before the host has the bounds) on the device.
+// the one-pass kernel's LDS (64 KB stage + 8 B per brick + statics) stays
+// under 80 KB for this many bricks: two workgroups per CU
+constexpr int kFuseMaxBricks = 1536;
+static int64_t dense_cap(int64_t n);
+static int64_t entries_cap(int64_t n);
+__host__ __device__ inline int64_t dense_cap_hd(int64_t n) { return 2 * n + (1 << 20); }
+__host__ __device__ inline int64_t entries_cap_hd(int64_t n) { return n + n / 2 + (1 << 20); }
+
+struct BinPlan {
+  VoxelGeom g;
+  Bricks b;
+  int cap;  // segment slots per brick; 0: not the one-pass path
+  int ok;
+};
+
+__host__ __device__ inline uint64_t geom_key(const VoxelGeom& g, int64_t n) {
+  return ((uint64_t)g.nx * 73856093u) ^ ((uint64_t)g.ny * 19349663u) ^ ((uint64_t)g.nz * 83492791u) ^ (uint64_t)n;
+}
+
+__host__ __device__ inline void fused_plan(const double mn[3], const double mx[3], double vs, int64_t n, int allow,
+                                           uint64_t skip_key, BinPlan* P) {
+  P->ok = 0;
+  P->cap = 0;
+  double dims[3];
+  for (int a = 0; a < 3; ++a) dims[a] = floor(fmax(0.0, mx[a] - mn[a]) / vs) + 1.0;
+  const double ext = fmax(mx[0] - mn[0], fmax(mx[1] - mn[1], mx[2] - mn[2]));
+  const double nvox = dims[0] * dims[1] * dims[2];
+  if (!allow || n <= 0 || vs * (double)INT32_MAX < ext || !(nvox <= (double)dense_cap_hd(n))) return;
+  VoxelGeom g;
+  g.mnx = mn[0];
+  g.mny = mn[1];
+  g.mnz = mn[2];
+  g.vs = vs;
+  g.ivs = 1.0 / vs;
+  g.nx = (int)dims[0];
+  g.ny = (int)dims[1];
+  g.nz = (int)dims[2];
+  const Bricks b = plan_bricks(g.nx, g.ny, g.nz, kFuseMaxBricks);
+  if (b.nb <= 0 || b.nb > kFuseMaxBricks) return;
+  const int64_t seg = entries_cap_hd(n) / b.nb;
+  const double full = (double)n * (double)(1ll << (b.sx + b.sy + b.sz)) / nvox;
+  if (seg > INT32_MAX || !((double)seg >= 1.03 * full + 2048.0) || geom_key(g, n) == skip_key) return;
+  P->g = g;
+  P->b = b;
+  P->cap = (int)seg;
+  P->ok = 1;
+}
+
+__global__ void k_bin_plan(const double* mm, double vs, int64_t n, int allow, uint64_t skip_key,
+                           BinPlan* __restrict__ plan) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const double mn[3] = {mm[0], mm[1], mm[2]}, mx[3] = {mm[3], mm[4], mm[5]};
+    BinPlan P;
+    fused_plan(mn, mx, vs, n, allow, skip_key, &P);
+    *plan = P;
+  }
+}
+
+__global__ void __launch_bounds__(kBinBlock) k_vbin_fused_pre(const float* __restrict__ xyz, int64_t n,
+                                                           const BinPlan* __restrict__ plan,
+                                                           int32_t* __restrict__ btot, uint64_t* __restrict__ entries,
+                                                           int32_t* __restrict__ vid, int* __restrict__ err) {
+  if (!plan->ok) return;
+  const VoxelGeom g = plan->g;
+  const Bricks b = plan->b;
+  vbin_fused_body(xyz, n, g, b, plan->cap, btot, entries, vid, err);
 }
 
 __global__ void __launch_bounds__(kBlock) k_voxel_assign_hash(const float* __restrict__ xyz, int64_t n,
@@ -723,9 +818,8 @@ __global__ void __launch_bounds__(kBlock) k_gather_vox(const float* __restrict__
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     const P3 q = p[idx[j]];
     if (rep_xyz) reinterpret_cast<P3*>(rep_xyz)[j] = q;
-    double r[3];
     int v[3];
-    voxel_ref(q, g, r, v);  // inside the grid: the dense path accepted every point
+    voxel_of(q, g, v);  // inside the grid: the dense path accepted every point
     vox[v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2])] = make_float4(q.x, q.y, q.z, __int_as_float((int)j));
   }
 }
@@ -763,9 +857,9 @@ __global__ void __launch_bounds__(kBlock) k_voxel_occ2(const T* __restrict__ tab
   }
 }
 
-static int64_t dense_cap(int64_t n) { return 2 * n + (1 << 20); }
+static int64_t dense_cap(int64_t n) { return dense_cap_hd(n); }
 // binned entries: n for the scanned layout, + 1/2 + 2^20 of segment slack
-static int64_t entries_cap(int64_t n) { return n + n / 2 + (1 << 20); }
+static int64_t entries_cap(int64_t n) { return entries_cap_hd(n); }
 static thread_local uint64_t g_fused_overflow_key = ~0ull;  // last geometry whose one-pass binning overflowed
 static int64_t bin_blocks(int64_t n) { return (n + kBinChunk - 1) / kBinChunk; }
 static int64_t bin_hist_ints(int64_t n) { return bin_blocks(n) * kMaxBuckets; }
@@ -788,6 +882,7 @@ struct VoxelWs {
   char* aabb;
   double* mm;
   int64_t* count;  // [0] = m, [1] = err (as int), [2] occupied 2^3 cells
+  BinPlan* plan;   // the pre-launched one-pass binning's plan
 };
 
 static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
@@ -807,6 +902,7 @@ static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
   w->aabb = ar.take<char>(aabb_ws_bytes(n));
   w->mm = ar.take<double>(8);
   w->count = ar.take<int64_t>(8);
+  w->plan = ar.take<BinPlan>(1);
   return ar.used;
 }
 
@@ -865,11 +961,24 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     if (n > 0) O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
     return 0;
   };
+  // one-pass binning allowed (the plan decides whether it applies)
+  const int allow_fused = !getenv("O3DX_VOXEL_TWOPASS") && !getenv("O3DX_VOXEL_PLAIN") && !xwin ? 1 : 0;
+  bool pre_launched = false;
   if (!min_bound_host || !max_bound_host) {
     double mm[6];
     O3DX_TRY(aabb_begin(xyz, n, w.aabb, s, ZeroSpan{reinterpret_cast<uint8_t*>(w.count), 8 * sizeof(int64_t)},
                         ZeroSpan{reinterpret_cast<uint8_t*>(w.boff), (size_t)kMaxBuckets * kTotStride * sizeof(int32_t)},
                         ZeroSpan{w.flags, (size_t)n}));
+    if (!min_bound_host && !max_bound_host && allow_fused && n > 0 && !getenv("O3DX_VOXEL_NOPRE")) {
+      // the binning starts on the device's own plan while the host waits for
+      // the bounds (the host replays the same plan below)
+      hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, aabb_mailbox_dev(), voxel_size, n, allow_fused,
+                         g_fused_overflow_key, w.plan);
+      hipLaunchKernelGGL(k_vbin_fused_pre, dim3((unsigned)((n + kFuseChunk - 1) / kFuseChunk)), dim3(kBinBlock),
+                         fused_lds_bytes(kFuseMaxBricks), s, xyz, n, w.plan, w.boff, w.entries,
+                         (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
+      pre_launched = true;
+    }
     O3DX_TRY(aabb_end(mm, s));
     for (int a = 0; a < 3; ++a) {
       mn[a] = min_bound_host ? min_bound_host[a] : mm[a];
@@ -894,6 +1003,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   g.mny = mn[1];
   g.mnz = mn[2];
   g.vs = voxel_size;
+  g.ivs = 1.0 / voxel_size;
   double dims[3];
   voxel_dims(mn, mx, voxel_size, dims);
   if (xwin) {  // slab: only the x keys [xwin[0], xwin[1]) exist, every point must fall inside
@@ -925,7 +1035,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     grid_kept = false;
     int64_t nslots;
     if (attempt > 0) O3DX_TRY(clears());
-    const Bricks bricks = dense ? plan_bricks(g.nx, g.ny, g.nz) : Bricks{};
+    Bricks bricks = dense ? plan_bricks(g.nx, g.ny, g.nz) : Bricks{};
     if (dense && bricks.nb > 0 && !getenv("O3DX_VOXEL_PLAIN")) {
       nslots = (int64_t)nvox;
       const unsigned nblk = (unsigned)((n + kBinChunk - 1) / kBinChunk);
@@ -936,14 +1046,14 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       // one pass into fixed per-brick segments when a segment holds a full
       // brick's share of a uniform cloud with room to spare (and this
       // geometry did not overflow last time)
-      const int64_t seg = entries_cap(n) / bricks.nb;
-      const double full = (double)n * std::ldexp(1.0, bricks.sx + bricks.sy + bricks.sz) / nvox;
-      const uint64_t gkey = ((uint64_t)g.nx * 73856093u) ^ ((uint64_t)g.ny * 19349663u) ^
-                            ((uint64_t)g.nz * 83492791u) ^ (uint64_t)n;
-      const bool fused = fused_ok && seg <= INT32_MAX && (double)seg >= 1.03 * full + 2048.0 &&
-                         g_fused_overflow_key != gkey && !getenv("O3DX_VOXEL_TWOPASS");
-      const int cap = fused ? (int)seg : 0;
-      if (fused) {
+      BinPlan plan;
+      fused_plan(mn, mx, voxel_size, n, fused_ok && allow_fused, g_fused_overflow_key, &plan);
+      const bool fused = plan.ok && !xwin;
+      if (fused) bricks = plan.b;  // the one-pass plan's (larger) bricks
+      const int cap = fused ? plan.cap : 0;
+      if (fused && attempt == 0 && pre_launched) {
+        // already running on the device's identical plan
+      } else if (fused) {
         const unsigned nfb = (unsigned)((n + kFuseChunk - 1) / kFuseChunk);
         hipLaunchKernelGGL(k_vbin_fused, dim3(nfb), dim3(kBinBlock), fused_lds_bytes(bricks.nb), s, xyz, n, g, bricks,
                            cap, btot, w.entries, (voxel_of_point || cubic_id) ? w.vid : nullptr,
@@ -1042,8 +1152,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
     if (errflag & 16) {  // a brick outgrew its one-pass segment: count + scatter (and remember)
-      g_fused_overflow_key = ((uint64_t)g.nx * 73856093u) ^ ((uint64_t)g.ny * 19349663u) ^
-                             ((uint64_t)g.nz * 83492791u) ^ (uint64_t)n;
+      g_fused_overflow_key = geom_key(g, n);
       fused_ok = false;
       if (!(errflag & ~16)) continue;
       errflag &= ~16;
@@ -1150,6 +1259,7 @@ extern "C" int o3dx_voxel_table_build(const float* xyz, int64_t n, const double*
   g.mny = min_bound_host[1];
   g.mnz = min_bound_host[2];
   g.vs = voxel_size;
+  g.ivs = 1.0 / voxel_size;
   g.kx0 = (int)kx0;
   g.nx = (int)(kx1 - kx0);
   g.ny = (int)dims[1];
