@@ -267,7 +267,8 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restr
 // the runs from the LDS stage.  A brick whose total passes cap drops the
 // excess and raises err bit 16: the host reruns with count + scatter.
 constexpr int kFusePer = 16;
-constexpr int kFuseChunk = kBinBlock * kFusePer;
+constexpr int kFuseBlock = 1024;
+constexpr int kFuseChunk = kFuseBlock * kFusePer;
 
 // dynamic LDS: stage[kFuseChunk] (u64), loc[nb + 1], dst[nb]
 inline size_t fused_lds_bytes(int nb) { return kFuseChunk * sizeof(uint64_t) + (2 * (size_t)nb + 1) * sizeof(int32_t); }
@@ -280,10 +281,10 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   uint64_t* stage = lds_u64;
   int32_t* loc = reinterpret_cast<int32_t*>(lds_u64 + kFuseChunk);  // count -> offset -> cursor
   int32_t* dst = loc + b.nb + 1;                                      // segment index of stage slot 0, per brick
-  __shared__ int32_t wsum[kBinBlock / 64 + 1];
+  __shared__ int32_t wsum[kFuseBlock / 64 + 1];
   __shared__ int ovf;
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int k = threadIdx.x; k < b.nb; k += kBinBlock) loc[k] = 0;
+  for (int k = threadIdx.x; k < b.nb; k += kFuseBlock) loc[k] = 0;
   if (threadIdx.x == 0) ovf = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kFuseChunk;
@@ -292,10 +293,10 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   // every load of the chunk first (clamped, unconditional), then the keys
   P3 q[kFusePer];
 #pragma unroll
-  for (int j = 0; j < kFusePer; ++j) q[j] = p[min(base + threadIdx.x + (int64_t)j * kBinBlock, n - 1)];
+  for (int j = 0; j < kFusePer; ++j) q[j] = p[min(base + threadIdx.x + (int64_t)j * kFuseBlock, n - 1)];
 #pragma unroll
   for (int j = 0; j < kFusePer; ++j) {
-    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    const int64_t i = base + threadIdx.x + (int64_t)j * kFuseBlock;
     code[j] = ~0u;
     if (i < n) {
       int v[3];
@@ -311,12 +312,12 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   }
   if (bad) *err = 1;
   __syncthreads();
-  const int span = (b.nb + kBinBlock - 1) / kBinBlock;
+  const int span = (b.nb + kFuseBlock - 1) / kFuseBlock;
   const int k0 = threadIdx.x * span, k1 = min(k0 + span, b.nb);
   int run = 0;
   for (int k = k0; k < k1; ++k) run += loc[k];
   int tot;
-  int ex = block_excl_scan<kBinBlock>(run, wsum, &tot);
+  int ex = block_excl_scan<kFuseBlock>(run, wsum, &tot);
   for (int k = k0; k < k1; ++k) {
     const int c = loc[k];
     loc[k] = ex;
@@ -331,12 +332,12 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
 #pragma unroll
   for (int j = 0; j < kFusePer; ++j) {
     if (code[j] == ~0u) continue;
-    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
+    const int64_t i = base + threadIdx.x + (int64_t)j * kFuseBlock;
     const int at = atomicAdd(&loc[code[j] >> 16], 1);
     stage[at] = ((uint64_t)(code[j] >> 16) << 48) | ((uint64_t)(code[j] & 0xffffu) << 32) | (uint32_t)i;
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < tot; t += kBinBlock) {
+  for (int t = threadIdx.x; t < tot; t += kFuseBlock) {
     const uint64_t e = stage[t];
     const int k = (int)(e >> 48);
     const int o = dst[k] + t;
@@ -345,7 +346,7 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   if (threadIdx.x == 0 && ovf) atomicOr(err, 16);
 }
 
-__global__ void __launch_bounds__(kBinBlock) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
+__global__ void __launch_bounds__(kFuseBlock) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
                                                        Bricks b, int cap, int32_t* __restrict__ btot,
                                                        uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
                                                        int* __restrict__ err) {
@@ -511,7 +512,7 @@ __global__ void k_bin_plan(const double* mm, double vs, int64_t n, int allow, ui
   }
 }
 
-__global__ void __launch_bounds__(kBinBlock) k_vbin_fused_pre(const float* __restrict__ xyz, int64_t n,
+__global__ void __launch_bounds__(kFuseBlock) k_vbin_fused_pre(const float* __restrict__ xyz, int64_t n,
                                                            const BinPlan* __restrict__ plan,
                                                            int32_t* __restrict__ btot, uint64_t* __restrict__ entries,
                                                            int32_t* __restrict__ vid, int* __restrict__ err) {
@@ -974,7 +975,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       // the bounds (the host replays the same plan below)
       hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, aabb_mailbox_dev(), voxel_size, n, allow_fused,
                          g_fused_overflow_key, w.plan);
-      hipLaunchKernelGGL(k_vbin_fused_pre, dim3((unsigned)((n + kFuseChunk - 1) / kFuseChunk)), dim3(kBinBlock),
+      hipLaunchKernelGGL(k_vbin_fused_pre, dim3((unsigned)((n + kFuseChunk - 1) / kFuseChunk)), dim3(kFuseBlock),
                          fused_lds_bytes(kFuseMaxBricks), s, xyz, n, w.plan, w.boff, w.entries,
                          (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
       pre_launched = true;
@@ -1055,7 +1056,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
         // already running on the device's identical plan
       } else if (fused) {
         const unsigned nfb = (unsigned)((n + kFuseChunk - 1) / kFuseChunk);
-        hipLaunchKernelGGL(k_vbin_fused, dim3(nfb), dim3(kBinBlock), fused_lds_bytes(bricks.nb), s, xyz, n, g, bricks,
+        hipLaunchKernelGGL(k_vbin_fused, dim3(nfb), dim3(kFuseBlock), fused_lds_bytes(bricks.nb), s, xyz, n, g, bricks,
                            cap, btot, w.entries, (voxel_of_point || cubic_id) ? w.vid : nullptr,
                            reinterpret_cast<int*>(w.count + 1));
       } else {
