@@ -543,6 +543,18 @@ def roofline(kernels, M, N, pmc_json):
             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": pmc.get("hbm_bytes_per_launch"),
             "algorithmic_bytes_per_launch": algo_bytes[dom],
             "note": "exact kNN selection is LDS / VALU-issue work, not HBM streaming: DESIGN.md §4.1"}
+    if pmc.get("SQ_INSTS_VALU") and dom.startswith("normals"):
+        # the measured limit (PMC): VALU issue.  achieved = the launch's VALU
+        # wave-instructions / its duration; peak = one wave64 VALU instruction
+        # per 2 cycles per SIMD (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
+        valu_peak = 1024 * 2.4e9 / 2.0 / 1e9
+        valu_ach = pmc["SQ_INSTS_VALU"] / avg_s / 1e9
+        roof.update({"bound": "valu", "achieved": round(valu_ach, 2), "peak": valu_peak,
+                     "unit": "G wave64-VALU-instr/s", "frac": round(valu_ach / valu_peak, 4),
+                     "hbm_algorithmic": {"achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                         "frac": round(ach / HBM_PEAK_GBS, 5)},
+                     "note": "exact kNN selection is VALU-issue / LDS work, not HBM streaming (PMC in "
+                             "profiles/pmc_traffic.json; DESIGN.md §4.1)"})
     if pmc.get("SQ_INSTS_VALU"):
         # VALU-issue floor (MI355X_MICROARCH.md: a wave64 VALU instruction issues in 2 cycles on a SIMD
         # holding >= 2 waves; float64 / transcendental ones take longer, so this is a lower bound)
@@ -689,6 +701,17 @@ def main_multi(args, world, rank, dev):
     """N > 1: the C4 headline (strong scaling of one 50M cloud over the ranks)."""
     elapsed, M, n_local = c4_headline(dev, args, world, rank)
     kernels = kernel_table()
+    # host/kernel split of the step: the library's event-timed kernel spans
+    # (voxel, compaction, normals) per step on this rank, summed over the ranks
+    # (on a shared GPU the ranks' kernels serialise, so the step is at least
+    # their sum); host = the rest of the wall time (collectives, launches, syncs)
+    k_ms = sum(v["avg_ms"] * v["launches"] for v in kernels.values()) / max(args.steps, 1)
+    k_all = torch.tensor([k_ms], dtype=torch.float64, device=comm_dev(dev))
+    dist.all_reduce(k_all, op=dist.ReduceOp.SUM)
+    k_all = float(k_all.item())
+    wall = elapsed / args.steps * 1e3
+    shared = os.environ.get("O3DX_BENCH_SHARED_GPU") == "1"
+    busy = k_all if shared else k_ms
     N = args.c4_n
     value = float(N) * args.steps / elapsed / 1e6
     line = {
@@ -703,6 +726,9 @@ def main_multi(args, world, rank, dev):
         "roofline": roofline(kernels, M / world, N / world, args.pmc_json),
         "cpu_baseline": None,
         "extra": {"kernels_rank0": kernels,
+                  "step_breakdown": {"wall_ms": round(wall, 4), "kernel_ms_rank0": round(k_ms, 4),
+                                     "kernel_ms_all_ranks": round(k_all, 4), "gpu_shared_by_ranks": shared,
+                                     "host_frac": round(max(0.0, 1.0 - busy / wall), 4) if wall > 0 else None},
                   "collectives": "all_reduce (AABB, halo proof), all_to_all (halo representatives)",
                   "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps / elapsed / 1e9, 2)},
     }

@@ -1,29 +1,39 @@
 #!/bin/bash
-# Round-end evidence in one GPU call: the full -m gpu suite, the PMC passes over
-# the normals (profiles/pmc_traffic.json refreshed for bench.py's roofline),
-# the default bench line, and the rocprofv3 kernel trace + stats of the bench.
-# Usage (via gpurun): bash tools/gpu_final.sh
+# Round-end evidence (r03), in two GPU calls:
+#   bash tools/gpu_final.sh tests   — the full -m gpu suite + smoke()
+#   bash tools/gpu_final.sh bench   — PMC passes (profiles/pmc_traffic.json refreshed
+#                                     for bench.py's roofline), the default bench line,
+#                                     and the rocprofv3 kernel trace + stats of the bench
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-  > gpurun_out/r01_gpu_tests.log 2>&1 || { tail -30 gpurun_out/r01_gpu_tests.log; exit 1; }
-tail -2 gpurun_out/r01_gpu_tests.log
+R=${ROUND:-r03}
+if [ "$1" = tests ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/${R}_gpu_tests.log 2>&1 || { tail -30 gpurun_out/${R}_gpu_tests.log; exit 1; }
+  tail -2 gpurun_out/${R}_gpu_tests.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+    > gpurun_out/${R}_smoke.log 2>&1 || { cat gpurun_out/${R}_smoke.log; exit 1; }
+  tail -3 gpurun_out/${R}_smoke.log
+  exit 0
+fi
 rm -rf gpurun_out/pmc
-bash tools/pmc.sh gpurun_out/pmc -- python tools/prof_kernels.py normals > gpurun_out/pmc.log 2>&1 || exit $?
+bash tools/pmc.sh gpurun_out/pmc -- python tools/prof_kernels.py ${PMC_WHAT:-all} > gpurun_out/pmc.log 2>&1 || exit $?
 python tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_summary.json || exit $?
-python - <<'EOF' || exit $?
+python - <<'PYEOF' || exit $?
 import json
 old = json.load(open("profiles/pmc_traffic.json"))
 new = json.load(open("gpurun_out/pmc_summary.json"))
 old["kernels"].update(new["kernels"])
+old["round"] = "r03"
 for p in ("profiles/pmc_traffic.json", "gpurun_out/pmc_traffic.json"):
     with open(p, "w") as f:
         json.dump(old, f, indent=1, sort_keys=True)
-EOF
-timeout -k 10 400 python bench.py > gpurun_out/r01_bench.json 2> gpurun_out/r01_bench.err || exit $?
-rm -rf gpurun_out/prof
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-  python bench.py --no-cpu > gpurun_out/r01_prof_bench.log 2>&1 || exit $?
-cat gpurun_out/r01_bench.json
+PYEOF
+timeout -k 10 500 python bench.py > gpurun_out/${R}_bench.json 2> gpurun_out/${R}_bench.err || exit $?
+cat gpurun_out/${R}_bench.json
+rm -rf gpurun_out/prof_${R}
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R} -o run --output-format csv -- \
+  python bench.py --no-cpu > gpurun_out/${R}_prof_bench.log 2>&1 || exit $?
+echo FINAL_DONE

@@ -18,7 +18,8 @@ SHORT = {"k_normals_stile": "normals_stile", "k_normals_vlist": "normals_stile",
          "k_icp_match": "icp_match", "k_icp_moments": "icp_moments", "k_vbin_scatter": "vbin_scatter",
          "k_plane_count": "plane_count", "k_plane_fixup": "plane_fixup", "k_grid_count": "grid_count", "k_grid_cell_sort": "grid_sort",
          "k_vbin_count": "vbin_count", "k_vbin_reduce": "vbin_reduce", "k_gather_vox": "gather_vox",
-         "k_aabb_partial": "aabb_partial", "k_tile_compact_u8": "compact_u8"}
+         "k_aabb_partial": "aabb_partial", "k_tile_compact_u8": "compact_u8",
+         "k_vbin_fused": "vbin_fused", "k_plane_upper": "plane_upper", "k_icp_match": "icp_match"}
 
 
 def short(name):
