@@ -252,7 +252,20 @@ def secondary(dev, args):
     t0 = time.perf_counter()
     ops.estimate_normals(pts, knn=30)
     torch.cuda.synchronize(dev)
-    out["normals_raw_c3"] = {"n": n, "ms": round((time.perf_counter() - t0) * 1e3, 3),
+    el_raw = (time.perf_counter() - t0) * 1e3
+    # the grid build (count + cell sort: round 2's cliff) and the two search
+    # kernels, event-timed in a second call
+    _native.set_kernel_timing(True)
+    _native.reset_kernel_timing()
+    ops.estimate_normals(pts, knn=30)
+    torch.cuda.synchronize(dev)
+    parts = {}
+    for name in ("grid_count", "grid_sort", "normals_tile", "normals_wave", "normals_knn"):
+        ms, cnt = _native.kernel_timing(name)
+        if cnt:
+            parts[name + "_ms"] = round(ms, 3)
+    out["normals_raw_c3"] = {"n": n, "ms": round(el_raw, 3), **parts,
+                             "grid_build_ms": round(parts.get("grid_count_ms", 0) + parts.get("grid_sort_ms", 0), 3),
                              "path": "sorted grid (estimate_normals on the raw planted-plane cloud)"}
     del pts
     # ICP: box-surface target with KNN30 normals, source = independent sample moved by T_gt

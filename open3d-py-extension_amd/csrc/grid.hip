@@ -1617,6 +1617,18 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   // reach + h/2: that ball first (fewer rows and x-cells of the 5^3 cube),
   // then the whole shell.
   bool trial = s0 >= 2;
+  // A dense own cell (a thin plane or a cluster far above the grid's mean
+  // occupancy) holds the k nearest within a much smaller ball: a first try at
+  // the radius its density suggests (2-D estimate, x2 margin; any radius below
+  // the scanned reach is exact, too few points inside just moves on to the
+  // shell's own ball).
+  float Rd = INFINITY;
+  {
+    const int c = cell_index(g, cx, cy, cz);
+    const int cown = cell_start(g, c + 1) - cell_start(g, c);
+    if (cown >= 4 * kneed) Rd = g.h * sqrtf(2.0f * (float)kneed / (float)cown);
+  }
+  bool dtry = Rd < INFINITY;
   for (;;) {
     if (S >= rmax || S > kWaveMaxS) {  // beyond the row table, or the whole grid: the exact path
       fb = true;
@@ -1624,9 +1636,11 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
     }
     double R = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, S) - g.slack;
     if (trial) R = fmin(R, cube_reach(g, q.x, q.y, q.z, cx, cy, cz, S - 1) - g.slack + 0.5 * (double)g.h);
+    if (dtry) R = fmin(R, (double)Rd);
     if (R <= 0.0) {
       ++S;
       trial = false;
+      dtry = false;
       continue;
     }
     R2 = (float)(R * R) * (1.0f - 4.0f * kRelEps);
@@ -1652,7 +1666,9 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
       break;
     }
     if (tot >= kneed) break;
-    if (trial)
+    if (dtry)
+      dtry = false;
+    else if (trial)
       trial = false;
     else
       ++S;
