@@ -45,10 +45,11 @@ __global__ void __launch_bounds__(kBlock) k_grid_scatter(const float* __restrict
                                                          const int32_t* __restrict__ rank,
                                                          const int32_t* __restrict__ start, float4* __restrict__ pts,
                                                          const float* __restrict__ extra_src,
-                                                         float4* __restrict__ extra) {
+                                                         float4* __restrict__ extra,
+                                                         const int32_t* __restrict__ ids) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t pos = (int64_t)start[cell[i]] + rank[i];
-    pts[pos] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __int_as_float((int)i));
+    pts[pos] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __int_as_float(ids ? ids[i] : (int)i));
     if (extra) extra[pos] = make_float4(extra_src[3 * i], extra_src[3 * i + 1], extra_src[3 * i + 2], 0.f);
   }
 }
@@ -195,7 +196,8 @@ static int64_t cell_space(const int64_t d[3], bool blocked) {
 
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
                hipStream_t s, GridBuild* out, float4* extra_sorted, const float* extra_src, bool blocked,
-               int cap_mult, bool ordered) {
+               int cap_mult, bool ordered, const int32_t* ids, double max_h) {
+  if (ids) ordered = false;  // the in-cell ranking reads the cell of point w
   GridLayout L = grid_layout(n, cap_mult);
   if (ws_bytes < L.total) return fail(O3DX_ENOMEM, "grid workspace too small (need %zu)", L.total);
   char* w = (char*)ws;
@@ -240,6 +242,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     h = hn;
   }
   if (min_h > 0) h = std::max(h, min_h);
+  if (max_h > 0) h = std::min(h, max_h);
   if (!(h > 0) || !std::isfinite(h)) h = 1.0;
   auto fit_cap = [&](double hh) {
     int64_t d[3];
@@ -303,12 +306,12 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));
     if (n > 0 && !ordered) {  // cell order only (the in-cell order is the atomic ranks')
       hipLaunchKernelGGL(k_grid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, G.cell, G.rank,
-                         G.start, G.pts, extra_src, extra_sorted);
+                         G.start, G.pts, extra_src, extra_sorted, ids);
     } else if (n > 0) {
       float4* tmp = (float4*)(w + L.tmp);
       float4* tmp_extra = extra_sorted ? (float4*)(w + L.tmp_extra) : nullptr;
       hipLaunchKernelGGL(k_grid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, G.cell, G.rank,
-                         G.start, tmp, extra_src, tmp_extra);
+                         G.start, tmp, extra_src, tmp_extra, (const int32_t*)nullptr);
       // the big-cell list reuses the per-point rank array (free after the scatter)
       int32_t* nbig = reinterpret_cast<int32_t*>(G.scratch + 1);
       O3DX_HIP(hipMemsetAsync(nbig, 0, sizeof(int32_t), s));
@@ -1055,11 +1058,17 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   const int c = xcd_block(blockIdx.x, nreal);
   const int q0 = chunk_starts[c], q1 = chunk_starts[c + 1];
   const int64_t s = (int64_t)q0 + lane;
-  const bool active = s < q1;
+  bool active = s < q1;
   // the chunk lies in one z slab and spans a few y rows (each sorted by x)
   const float4 q = g.pts[active ? s : (int64_t)q0];
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
+  const int qw = __float_as_int(q.w);
+  if (g.outer) {
+    active = active && qw >= 0;  // a nested grid's candidate-only point
+  } else if (g.skip_cells) {     // the queries near dense cells are the nested grid's
+    active = active && !g.skip_cells[cell_index(g, cx, cy, cz)];
+  }
   int az;
   {
     const float4 f = g.pts[q0];
@@ -1098,7 +1107,8 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
       if (fb && g.stats) atomicAdd(&g.stats[6], 1ull);
       if (!fb) {
         const double reach = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, 1);
-        const double R = (reach == INFINITY) ? (double)(g.nx + g.ny + g.nz) * g.h : reach - g.slack;
+        double R = (reach == INFINITY) ? (double)(g.nx + g.ny + g.nz) * g.h : reach - g.slack;
+        R = fmin(R, outer_reach(g, q.x, q.y, q.z));
         const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
         uint32_t* hw = selbuf;
         TileHist th;
@@ -1155,8 +1165,9 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
           fb = n > kListMax ||
                !finish_selection<KMAX, MomAccDD>(
                    q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
-                   prior, __float_as_int(q.w), out, g.nbr,
-                   [&](int p) { return __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w); }, g.kd2, dbg == 4);
+                   prior, out_row(g, qw), out, g.nbr,
+                   [&](int p) { return out_row(g, __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w)); }, g.kd2,
+                   dbg == 4);
         }
       }
     }
@@ -1165,7 +1176,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
   if (fb) {
     if (g.stats) atomicAdd(&g.stats[4], 1ull);
     const int at = atomicAdd(fb_len, 1);
-    fb_list[at] = (int32_t)s;
+    fb_list[at] = g.outer ? qw : (int32_t)s;  // the outer grid's wave form takes a nested grid's hand-offs
   }
 }
 #undef O3DX_TILE_SCAN
@@ -1557,10 +1568,10 @@ __device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int 
 #define O3DX_WAVE_SCAN(S, BODY)                                                  \
   {                                                                              \
     int row_ = 0;                                                                \
-    for (int b_ = 0; b_ < ncand; b_ += 256) {                                    \
-      float4 v_[4];                                                              \
-      int p_[4];                                                                 \
-      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+    for (int b_ = 0; b_ < ncand; b_ += 64 * WU) {                                \
+      float4 v_[WU];                                                             \
+      int p_[WU];                                                                \
+      _Pragma("unroll") for (int u_ = 0; u_ < WU; ++u_) {                        \
         const int f_ = b_ + u_ * 64 + lane;                                      \
         p_[u_] = -1;                                                             \
         if (f_ < ncand) {                                                        \
@@ -1569,7 +1580,7 @@ __device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int 
         }                                                                        \
         v_[u_] = g.pts[p_[u_] >= 0 ? p_[u_] : 0];                                \
       }                                                                          \
-      _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+      _Pragma("unroll") for (int u_ = 0; u_ < WU; ++u_) {                        \
         const int pp = p_[u_];                                                   \
         const bool valid = pp >= 0;                                              \
         const int fidx = b_ + u_ * 64 + lane;                                    \
@@ -1597,7 +1608,7 @@ __device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int 
     O3DX_WAVE_SCAN(S, BODY)        \
   }
 
-template <int KMAX>
+template <int KMAX, int WU>
 __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const float* __restrict__ prior,
                                            float* __restrict__ out, int64_t s, int lane, int32_t* sel, int32_t* bnd,
                                            int32_t* __restrict__ ra, int32_t* __restrict__ rp,
@@ -1795,7 +1806,7 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
 #undef O3DX_WAVE_SCAN_L
 #undef O3DX_WAVE_ANY
 
-template <int KMAX>
+template <int KMAX, int WU = 4>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4))) k_normals_knn_wave(
     GridView g, int kneed, const float* __restrict__ prior, float* __restrict__ out,
     const int32_t* __restrict__ in_list, const int32_t* __restrict__ in_len, int32_t* __restrict__ fb_list,
@@ -1810,7 +1821,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_wav
   const int64_t lim = in_list ? (int64_t)*in_len : g.n;
   for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wv; t < lim; t += (int64_t)gridDim.x * kWavesPerBlock) {
     const int64_t s = in_list ? (int64_t)__builtin_amdgcn_readfirstlane(in_list[t]) : t;
-    wave_query<KMAX>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], ra[wv], rp[wv], cd2[wv], cpos[wv], fb_list,
+    wave_query<KMAX, WU>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], ra[wv], rp[wv], cd2[wv], cpos[wv], fb_list,
                      fb_len, s0);
   }
 }
@@ -2134,6 +2145,170 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
 // The normals on a built grid: shared by o3dx_estimate_normals (grid sorted
 // from the points) and o3dx_estimate_normals_voxel (grid read off the voxel
 // table).  `xyz` is the caller's point array the grid's w fields index.
+// ------------------------------------------------------------ nested grids
+// A cloud of mixed density (a thin dense plane or cluster inside a sparse
+// volume: raw scans, C3's planted plane) puts hundreds of points in the outer
+// grid's cells there: their LDS tiles overflow and every such query would go
+// to the one-wave-per-query form, whose candidate count grows with the cell
+// size (round 3: 2.65M of C3's 10M queries, 37 of 44 ms).  Those queries are
+// served instead by a nested grid: the dense cells (>= t points) and their 26
+// neighbours (D1) are its queries, the cells within two of a dense cell (D2)
+// its points; same tile kernel, cells sized for the dense region, every
+// search capped at the outer shell-1 reach (the 27 cells around a D1 cell lie
+// in D2, so every point inside that reach is in the nested grid); what it
+// cannot settle goes to the outer wave form.
+constexpr int64_t kNestedMinQueries = 4096;
+
+// f(c') over the <= 27 cells around cell c of a row-major grid
+template <class F>
+__device__ __forceinline__ bool any_around(const GridView& g, int64_t c, F&& f) {
+  const int cx = (int)(c % g.nx), cy = (int)((c / g.nx) % g.ny), cz = (int)(c / ((int64_t)g.nx * g.ny));
+  for (int z = max(cz - 1, 0); z <= min(cz + 1, g.nz - 1); ++z)
+    for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ny - 1); ++y)
+      for (int x = max(cx - 1, 0); x <= min(cx + 1, g.nx - 1); ++x)
+        if (f((int64_t)x + (int64_t)g.nx * (y + (int64_t)g.ny * z))) return true;
+  return false;
+}
+
+__global__ void __launch_bounds__(kBlock) k_nested_mark(GridView g, int t, uint8_t* __restrict__ d1) {
+  const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x)
+    d1[c] = any_around(g, c, [&](int64_t o) { return g.start[o + 1] - g.start[o] >= t; }) ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_nested_cells(GridView g, const uint8_t* __restrict__ d1,
+                                                         int32_t* __restrict__ sub_cnt,
+                                                         unsigned long long* __restrict__ tot) {
+  const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
+  unsigned long long a = 0, b = 0;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+    const int own = g.start[c + 1] - g.start[c];
+    const bool d2 = own > 0 && any_around(g, c, [&](int64_t o) { return d1[o] != 0; });
+    sub_cnt[c] = d2 ? own : 0;
+    a += d2 ? (unsigned long long)own : 0ull;
+    b += d1[c] ? (unsigned long long)own : 0ull;
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane_id() == 0 && (a | b)) {
+    atomicAdd(&tot[0], a);
+    atomicAdd(&tot[1], b);
+  }
+}
+
+// The nested grid's input: the points of the D2 cells, in outer order, with
+// w = outer position (a query: D1) or -(position + 1).
+__global__ void __launch_bounds__(kBlock) k_nested_gather(GridView g, const uint8_t* __restrict__ d1,
+                                                          const int32_t* __restrict__ sub_cnt,
+                                                          const int32_t* __restrict__ sub_off,
+                                                          float* __restrict__ sub_xyz, int32_t* __restrict__ sub_id) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < g.n; p += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = g.pts[p];
+    int cx, cy, cz;
+    grid_cell(g, v.x, v.y, v.z, cx, cy, cz);
+    const int c = cell_index(g, cx, cy, cz);
+    if (sub_cnt[c] == 0) continue;
+    const int64_t d = (int64_t)sub_off[c] + (p - g.start[c]);
+    sub_xyz[3 * d] = v.x;
+    sub_xyz[3 * d + 1] = v.y;
+    sub_xyz[3 * d + 2] = v.z;
+    sub_id[d] = d1[c] ? (int32_t)p : -(int32_t)p - 1;
+  }
+}
+
+struct NestedWs {
+  int32_t *sub_cnt, *sub_off, *scan_tmp, *chunks;
+  uint8_t* d1;
+  unsigned long long* tot;
+  float* sub_xyz;
+  int32_t* sub_id;
+  void *gws, *pws;
+  size_t gws_bytes, pws_bytes;
+  int64_t cap;  // nested points
+};
+
+static void nested_carve(Arena& ar, int64_t n, NestedWs& w) {
+  const int64_t nc = cap_cells(std::max<int64_t>(n, 1), 4);
+  w.cap = n / 2 + 4096;
+  w.d1 = ar.take<uint8_t>(nc + 1);
+  w.sub_cnt = ar.take<int32_t>(nc + 1);
+  w.sub_off = ar.take<int32_t>(nc + 1);
+  w.scan_tmp = ar.take<int32_t>(scan_workspace_ints(nc + 1));
+  w.tot = ar.take<unsigned long long>(2);
+  w.sub_xyz = ar.take<float>(3 * w.cap);
+  w.sub_id = ar.take<int32_t>(w.cap);
+  w.gws_bytes = grid_ws_bytes(w.cap);
+  w.gws = ar.take<char>(w.gws_bytes);
+  const int64_t rows = cap_cells(w.cap, 4);
+  w.chunks = ar.take<int32_t>(w.cap / kTileQ + rows + 4);
+  w.pws_bytes = chunk_plan_ws_bytes(w.cap, rows);
+  w.pws = ar.take<char>(w.pws_bytes);
+}
+
+static size_t nested_ws_bytes(int64_t n) {
+  Arena ar(nullptr, 0);
+  NestedWs w;
+  nested_carve(ar, n, w);
+  return ar.used;
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// Builds the nested grid and runs its tiles (hand-offs appended to fb_list as
+// outer positions); on return G.view.skip_cells tells the outer tiles which
+// queries are taken.  Does nothing when the cloud has no dense cells.
+static int nested_tiles(GridBuild& G, int64_t n, int kneed, double occ, const float* prior, float* out,
+                        int32_t* fb_list, int32_t* fb_len, Arena& ar, hipStream_t s) {
+  NestedWs w;
+  nested_carve(ar, n, w);
+  O3DX_ARENA_CHECK(ar);
+  const int t = env_int("O3DX_NESTED_T", (int)std::ceil(4.0 * occ));
+  const int64_t nc = (int64_t)G.view.nx * G.view.ny * G.view.nz;
+  KTimer kt("normals_nested", s);
+  O3DX_HIP(hipMemsetAsync(w.tot, 0, 2 * sizeof(unsigned long long), s));
+  const unsigned gc = grid_for(nc, kBlock, 4096);
+  hipLaunchKernelGGL(k_nested_mark, dim3(gc), dim3(kBlock), 0, s, G.view, t, w.d1);
+  hipLaunchKernelGGL(k_nested_cells, dim3(gc), dim3(kBlock), 0, s, G.view, w.d1, w.sub_cnt, w.tot);
+  unsigned long long tot[2];
+  O3DX_TRY(read_back(tot, w.tot, sizeof(tot), s));
+  const int64_t nsub = (int64_t)tot[0], nq = (int64_t)tot[1];
+  if (nq < kNestedMinQueries || nsub > w.cap) return 0;
+  O3DX_TRY(exclusive_scan_i32(w.sub_cnt, w.sub_off, nc, w.scan_tmp, s));
+  hipLaunchKernelGGL(k_nested_gather, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, G.view, w.d1, w.sub_cnt,
+                     w.sub_off, w.sub_xyz, w.sub_id);
+  GridBuild N;
+  const double occ2 = getenv("O3DX_NESTED_OCC") ? atof(getenv("O3DX_NESTED_OCC")) : occ;
+  O3DX_TRY(grid_build(w.sub_xyz, nsub, occ2, 0.0, w.gws, w.gws_bytes, s, &N, nullptr, nullptr, false, 4, false,
+                      w.sub_id, 0.5 * (double)G.view.h));
+  GridView& v = N.view;
+  v.outer = G.view.pts;
+  v.cox = G.view.ox;
+  v.coy = G.view.oy;
+  v.coz = G.view.oz;
+  v.ch = G.view.h;
+  v.cinv_h = G.view.inv_h;
+  v.cslack = G.view.slack;
+  v.cnx = G.view.nx;
+  v.cny = G.view.ny;
+  v.cnz = G.view.nz;
+  v.nbr = G.view.nbr;
+  v.kd2 = G.view.kd2;
+  O3DX_TRY(chunk_plan(nsub, v, kTileQ, w.chunks, w.pws, w.pws_bytes, s));
+  const int64_t upper = chunk_plan_upper(nsub, v, kTileQ);
+  if (kneed <= 32)
+    hipLaunchKernelGGL(k_normals_knn_tile<32>, dim3((unsigned)upper), dim3(kTileQ), 0, s, v, w.chunks, kneed, prior,
+                       out, fb_list, fb_len, 0);
+  else
+    hipLaunchKernelGGL(k_normals_knn_tile<64>, dim3((unsigned)upper), dim3(kTileQ), 0, s, v, w.chunks, kneed, prior,
+                       out, fb_list, fb_len, 0);
+  O3DX_HIP(hipGetLastError());
+  G.view.skip_cells = w.d1;
+  return 0;
+}
+
 static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, int knn, double radius,
                            const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes, hipStream_t s) {
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
@@ -2157,6 +2332,8 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
     if (tiles) O3DX_TRY(chunk_plan(n, G.view, kTileQ, chunks, pws, pws_bytes, s));
     const int64_t nchunks = upper;
     KTimer kt("normals_knn", s);
+    if (tiles && !getenv("O3DX_NESTED_OFF") && n >= 2 * kNestedMinQueries)
+      O3DX_TRY(nested_tiles(G, n, kneed, occ_for(mode, knn), prior, out, list1, lens, ar, s));
     const int32_t* wl = tiles ? list1 : nullptr;
     const int32_t* wlen = tiles ? lens : nullptr;
     // the wave form grid-strides over its list (at most n queries)
@@ -2178,7 +2355,11 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
       // beyond the shell-1 radius: start those at shell 2
       const int s0 = tiles ? 2 : 1;
       KTimer kt_wave("normals_wave", s);
-      if (kneed <= 32)
+      const int wu = env_int("O3DX_WAVE_U", 4);  // candidate loads in flight per lane (A/B)
+      if (kneed <= 32 && wu == 8)
+        hipLaunchKernelGGL((k_normals_knn_wave<32, 8>), dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed,
+                           prior, out, wl, wlen, list2, lens + 1, s0);
+      else if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
                            out, wl, wlen, list2, lens + 1, s0);
       else
@@ -2275,7 +2456,7 @@ extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
   // grid rows (ny * nz) are bounded by the cell cap
   const int64_t rows = cap_cells(n, 4);
   return grid_ws_bytes(n) + 3 * Arena::align((n + 3) * 4) + Arena::align((n / 64 + rows + 4) * 4) +
-         chunk_plan_ws_bytes(n, rows) + 4096;
+         chunk_plan_ws_bytes(n, rows) + nested_ws_bytes(n) + 4096;
 }
 
 extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,

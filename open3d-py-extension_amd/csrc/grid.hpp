@@ -30,7 +30,22 @@ struct GridView {
                               // coordinates, w = -1) and start is the identity (start may be null)
   int32_t* nbr = nullptr;     // test hook (o3dx_set_debug_neighbors): k selected ids per output row
   float* kd2 = nullptr;       // KNN normals: per output row an upper bound of the k-th neighbour d^2
+  // Nested grid (KNN normals on clouds of mixed density, grid.hip "nested
+  // grids"): a finer grid over the dense cells of an outer grid and their
+  // neighbours.  Its w = the point's outer sorted position when the point is a
+  // query here, -(position + 1) when it is only a candidate.  Searches are
+  // capped at the outer grid's shell-1 reach (every point inside it is here).
+  const float4* __restrict__ outer = nullptr;
+  float cox = 0.f, coy = 0.f, coz = 0.f, ch = 0.f, cinv_h = 0.f, cslack = 0.f;
+  int cnx = 0, cny = 0, cnz = 0;
+  const uint8_t* skip_cells = nullptr;  // outer grid: queries in flagged cells are the nested grid's
 };
+
+// outer sorted position / output row of a nested-grid point
+__device__ __forceinline__ int nested_pos(int w) { return w >= 0 ? w : -w - 1; }
+__device__ __forceinline__ int out_row(const GridView& g, int w) {
+  return g.outer ? __float_as_int(g.outer[nested_pos(w)].w) : w;
+}
 
 // First sorted position of cell c (dense tables: the cell itself).
 __device__ __forceinline__ int cell_start(const GridView& g, int c) { return g.dense ? c : g.start[c]; }
@@ -150,6 +165,23 @@ __device__ __forceinline__ double cube_reach(const GridView& g, double x, double
   if (cz - S > 0) r = fmin(r, z - ((double)g.oz + (double)(cz - S) * g.h));
   if (cz + S < g.nz - 1) r = fmin(r, ((double)g.oz + (double)(cz + S + 1) * g.h) - z);
   return r;
+}
+
+// A nested grid's cap: the outer grid's shell-1 completeness radius around q
+// (minus the outer slack); +inf for an outer grid.
+__device__ __forceinline__ double outer_reach(const GridView& g, double x, double y, double z) {
+  if (!g.outer) return INFINITY;
+  const int cx = clampi((int)floorf(((float)x - g.cox) * g.cinv_h), 0, g.cnx - 1);
+  const int cy = clampi((int)floorf(((float)y - g.coy) * g.cinv_h), 0, g.cny - 1);
+  const int cz = clampi((int)floorf(((float)z - g.coz) * g.cinv_h), 0, g.cnz - 1);
+  double r = INFINITY;
+  if (cx - 1 > 0) r = fmin(r, x - ((double)g.cox + (double)(cx - 1) * g.ch));
+  if (cx + 1 < g.cnx - 1) r = fmin(r, ((double)g.cox + (double)(cx + 2) * g.ch) - x);
+  if (cy - 1 > 0) r = fmin(r, y - ((double)g.coy + (double)(cy - 1) * g.ch));
+  if (cy + 1 < g.cny - 1) r = fmin(r, ((double)g.coy + (double)(cy + 2) * g.ch) - y);
+  if (cz - 1 > 0) r = fmin(r, z - ((double)g.coz + (double)(cz - 1) * g.ch));
+  if (cz + 1 < g.cnz - 1) r = fmin(r, ((double)g.coz + (double)(cz + 2) * g.ch) - z);
+  return r - (double)g.cslack;
 }
 
 __device__ __forceinline__ int shell_rmax(const GridView& g, int cx, int cy, int cz) {
@@ -541,8 +573,11 @@ unsigned long long* search_stats_ptr();  // device counters when stats are enabl
 // chosen on the host).
 // ordered = false: points grouped by cell only (no ascending-index order
 // inside a cell; for consumers that do not depend on it).
+// ids: the w stored per point (default: its index; forces ordered = false).
+// max_h: upper bound on h (0 = none).
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
                hipStream_t s, GridBuild* out, float4* extra_sorted = nullptr, const float* extra_src = nullptr,
-               bool blocked = false, int cap_mult = 4, bool ordered = true);
+               bool blocked = false, int cap_mult = 4, bool ordered = true, const int32_t* ids = nullptr,
+               double max_h = 0.0);
 
 }  // namespace o3dx

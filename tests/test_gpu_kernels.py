@@ -427,6 +427,25 @@ def test_normals_raw_planted_plane_big_cells(dev):
     assert_normals(a, O.estimate_normals(pts, O.KNN, 30), pts, k=30, what="raw_planted_plane_1m")
 
 
+@pytest.mark.parametrize("k", [8, 30, 64])
+@pytest.mark.parametrize("frac,sigma", [(0.2, 0.002), (0.5, 0.0002)])
+def test_normals_nested_grid_planted_plane(dev, k, frac, sigma, monkeypatch):
+    """A dense plane inside a sparse volume (C3's composition at 1M): the
+    dense cells' queries run on the nested grid (grid.hip "nested grids").
+    Every row within 1e-5 of the oracle, neighbour sets bit-exact (debug
+    hook), and the normals bit-identical to the run without the nested grid."""
+    pts = S.planted_plane(1_000_000, 40 + k, frac=frac, sigma=sigma).numpy()
+    x = torch.from_numpy(pts).to(dev)
+    with DebugNeighbors(len(pts), k, dev) as dn:
+        a = ops.estimate_normals(x, knn=k).cpu().numpy()
+    monkeypatch.setenv("O3DX_NESTED_OFF", "1")
+    b = ops.estimate_normals(x, knn=k).cpu().numpy()
+    monkeypatch.delenv("O3DX_NESTED_OFF")
+    assert np.array_equal(a, b)
+    assert_neighbour_sets(dn.ids(), pts, k, f"nested_plane_k{k}_f{frac}")
+    assert_normals(a, O.estimate_normals(pts, O.KNN, k), pts, k=k, what=f"nested_plane_k{k}_f{frac}")
+
+
 @pytest.mark.parametrize("k", [5, 30, 64])
 @pytest.mark.parametrize("shape", ["cube", "surface", "dups"])
 def test_normals_knn_paths_agree(dev, k, shape):

@@ -26,7 +26,7 @@ N.reset_kernel_timing()
 ops.estimate_normals(pts, knn=30)
 torch.cuda.synchronize()
 out = {"env": {k: v for k, v in os.environ.items() if k.startswith("O3DX_")}, "ms": round(el, 3)}
-for name in ("grid_count", "grid_sort", "normals_tile", "normals_wave", "normals_knn"):
+for name in ("grid_count", "grid_sort", "normals_nested", "normals_tile", "normals_wave", "normals_knn"):
     ms, c = N.kernel_timing(name)
     if c:
         out[name] = round(ms, 3)
