@@ -1608,12 +1608,36 @@ __device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int 
     O3DX_WAVE_SCAN(S, BODY)        \
   }
 
+// Moments of the wave form's settled queries, finished lane-parallel by
+// k_finish_deferred instead of by lane 0 of each query's wave (FastEigen3x3 in
+// float64 is a few hundred serial instructions per query): list slots below
+// cap; row -1 = handed on.  cap 0: finish in place.
+struct Deferred {
+  double* mom = nullptr;  // [9][cap]
+  int32_t* row = nullptr;
+  int64_t cap = 0;
+};
+
+__global__ void __launch_bounds__(kBlock) k_finish_deferred(Deferred df, const int32_t* __restrict__ len, int kneed,
+                                                            const float* __restrict__ prior, float* __restrict__ out) {
+  const int64_t m = min((int64_t)*len, df.cap);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
+    const int row = df.row[t];
+    if (row < 0) continue;
+    MomAcc acc;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc.m[j] = df.mom[j * df.cap + t];
+    finish_normal(kneed, acc, prior, row, out);
+  }
+}
+
 template <int KMAX, int WU>
 __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const float* __restrict__ prior,
                                            float* __restrict__ out, int64_t s, int lane, int32_t* sel, int32_t* bnd,
                                            int32_t* __restrict__ ra, int32_t* __restrict__ rp,
                                            float* __restrict__ cd2, int32_t* __restrict__ cpos,
-                                           int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int s0) {
+                                           int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int s0,
+                                           const Deferred& df, int64_t t) {
   const float4 q = g.pts[s];
   int cx, cy, cz;
   grid_cell(g, q.x, q.y, q.z, cx, cy, cz);
@@ -1792,11 +1816,20 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
       const double t9[9] = {x, y, z, x * x, x * y, x * z, y * y, y * z, z * z};
 #pragma unroll
       for (int j = 0; j < 9; ++j) acc.m[j] = wave_sum_exact(t9[j]);
-      if (lane == 0) finish_normal(kneed, acc, prior, __float_as_int(q.w), out);
+      if (lane == 0) {
+        if (t < df.cap) {  // the eigen solve runs lane-parallel afterwards (k_finish_deferred)
+#pragma unroll
+          for (int j = 0; j < 9; ++j) df.mom[j * df.cap + t] = acc.m[j];
+          df.row[t] = __float_as_int(q.w);
+        } else {
+          finish_normal(kneed, acc, prior, __float_as_int(q.w), out);
+        }
+      }
     }
   }
   wave_sync();  // the lists are reused by the wave's next query
   if (fb && lane == 0) {
+    if (t < df.cap) df.row[t] = -1;
     if (g.stats) atomicAdd(&g.stats[5], 1ull);
     const int at = atomicAdd(fb_len, 1);
     fb_list[at] = (int32_t)s;
@@ -1810,7 +1843,7 @@ template <int KMAX, int WU = 4>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4))) k_normals_knn_wave(
     GridView g, int kneed, const float* __restrict__ prior, float* __restrict__ out,
     const int32_t* __restrict__ in_list, const int32_t* __restrict__ in_len, int32_t* __restrict__ fb_list,
-    int32_t* __restrict__ fb_len, int s0) {
+    int32_t* __restrict__ fb_len, int s0, Deferred df) {
   __shared__ int32_t sel[kWavesPerBlock][KMAX];
   __shared__ int32_t bnd[kWavesPerBlock][kWaveBnd];
   __shared__ int32_t ra[kWavesPerBlock][kWaveRows];
@@ -1822,7 +1855,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_wav
   for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wv; t < lim; t += (int64_t)gridDim.x * kWavesPerBlock) {
     const int64_t s = in_list ? (int64_t)__builtin_amdgcn_readfirstlane(in_list[t]) : t;
     wave_query<KMAX, WU>(g, kneed, prior, out, s, lane, sel[wv], bnd[wv], ra[wv], rp[wv], cd2[wv], cpos[wv], fb_list,
-                     fb_len, s0);
+                         fb_len, s0, df, t);
   }
 }
 
@@ -2133,7 +2166,7 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
     g.kd2 = d.kd2;
     KTimer kt_wave("normals_wave", s);
     hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(2048), dim3(64 * kWavesPerBlock), 0, s, g, kneed, prior, out,
-                       list, lens, list2, lens + 1, 3);
+                       list, lens, list2, lens + 1, 3, Deferred{});
     kt_wave.stop();
     hipLaunchKernelGGL(k_normals_knn<32>, dim3(64), dim3(kBlock), 0, s, g, xyz, kneed, 0, 0.0, prior, out, list2,
                        lens + 1);
@@ -2309,6 +2342,8 @@ static int nested_tiles(GridBuild& G, int64_t n, int kneed, double occ, const fl
   return 0;
 }
 
+static int64_t defer_cap(int64_t n) { return n / 4 + 64; }
+
 static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, int knn, double radius,
                            const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes, hipStream_t s) {
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
@@ -2322,6 +2357,8 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
     int32_t* lens = ar.take<int32_t>(4);
     int32_t* list1 = ar.take<int32_t>(n);
     int32_t* list2 = ar.take<int32_t>(n);
+    double* dmom = ar.take<double>(9 * defer_cap(n));
+    int32_t* drow = ar.take<int32_t>(defer_cap(n));
     const int64_t upper = chunk_plan_upper(n, G.view, kTileQ);
     int32_t* chunks = ar.take<int32_t>(upper + 2);
     const size_t pws_bytes = chunk_plan_ws_bytes(n, (int64_t)G.view.ny * G.view.nz);
@@ -2355,16 +2392,21 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
       // beyond the shell-1 radius: start those at shell 2
       const int s0 = tiles ? 2 : 1;
       KTimer kt_wave("normals_wave", s);
-      const int wu = env_int("O3DX_WAVE_U", 4);  // candidate loads in flight per lane (A/B)
-      if (kneed <= 32 && wu == 8)
-        hipLaunchKernelGGL((k_normals_knn_wave<32, 8>), dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed,
-                           prior, out, wl, wlen, list2, lens + 1, s0);
-      else if (kneed <= 32)
+      Deferred df;
+      if (wl && env_int("O3DX_WAVE_DEFER", 1)) {
+        df.cap = defer_cap(n);
+        df.mom = dmom;
+        df.row = drow;
+      }
+      if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
-                           out, wl, wlen, list2, lens + 1, s0);
+                           out, wl, wlen, list2, lens + 1, s0, df);
       else
         hipLaunchKernelGGL(k_normals_knn_wave<64>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
-                           out, wl, wlen, list2, lens + 1, s0);
+                           out, wl, wlen, list2, lens + 1, s0, df);
+      if (df.cap)
+        hipLaunchKernelGGL(k_finish_deferred, dim3(grid_for(std::min<int64_t>(n, df.cap), kBlock, 4096)), dim3(kBlock),
+                           0, s, df, wlen, kneed, prior, out);
     }
     O3DX_DISPATCH_K(kneed, k_normals_knn, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed, 0,
                     radius, prior, out, list2, lens + 1);
@@ -2456,7 +2498,8 @@ extern "C" size_t o3dx_normals_workspace_bytes(int64_t n) {
   // grid rows (ny * nz) are bounded by the cell cap
   const int64_t rows = cap_cells(n, 4);
   return grid_ws_bytes(n) + 3 * Arena::align((n + 3) * 4) + Arena::align((n / 64 + rows + 4) * 4) +
-         chunk_plan_ws_bytes(n, rows) + nested_ws_bytes(n) + 4096;
+         chunk_plan_ws_bytes(n, rows) + nested_ws_bytes(n) + Arena::align(9 * 8 * defer_cap(n) + 1) +
+         Arena::align(4 * defer_cap(n) + 1) + 4096;
 }
 
 extern "C" int o3dx_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,

@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 
   -k "nested or raw_planted or paths_agree" > gpurun_out/nested_tests.log 2>&1 || { tail -40 gpurun_out/nested_tests.log; exit 1; }
 tail -3 gpurun_out/nested_tests.log
 : > gpurun_out/nested_time.jsonl
-for cfg in "" "O3DX_WAVE_U=8" "O3DX_GRID_OCC=12" "O3DX_GRID_OCC=14" "O3DX_GRID_OCC=12 O3DX_NESTED_OCC=10" "O3DX_NESTED_T=30"; do
+for cfg in "" "O3DX_WAVE_DEFER=0"; do
   env $cfg timeout -k 10 120 python tools/raw_normals_time.py >> gpurun_out/nested_time.jsonl 2>> gpurun_out/nested_time.err || exit 1
 done
 cat gpurun_out/nested_time.jsonl
