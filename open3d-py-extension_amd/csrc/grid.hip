@@ -184,6 +184,12 @@ static int32_t* debug_nbr(int kneed, int64_t rows) {
   return (g_dbg_nbr && kneed == g_dbg_k && rows <= g_dbg_rows) ? g_dbg_nbr : nullptr;
 }
 
+// integer tuning / A-B switch from the environment
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 static void dims_for(const double mn[3], const double mx[3], double h, int64_t d[3]) {
   for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor(std::max(0.0, mx[a] - mn[a]) / h) + 1;
 }
@@ -1286,13 +1292,21 @@ __device__ __forceinline__ float4 dvox_load(const DenseVox& d, int x, int y, int
 // pair instead of three, the same 12 bytes per slot.
 // The row's loads are all issued before its first f (whose LDS atomics /
 // stores the compiler cannot move reads across).
-template <int L, class F>
+// VX: each slot's (x, y) by its own ds_read_b64 (2 LDS cycles, 64 banks per
+// 32-lane half) instead of the pairs the compiler merges into ds_read2_b64 (8
+// cycles, 32 banks; MI355X_MICROARCH.md §LDS): a volatile load is never merged.
+template <int L, bool VX, class F>
 __device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int st, const float4 q, F& f) {
   float2 a[L];
   float c[L];
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    a[i] = txy[st + i];
+    if constexpr (VX) {
+      typedef __attribute__((address_space(3))) const volatile f32x2 lds_vf2;
+      const f32x2 v = *(lds_vf2*)(&txy[st + i]);
+      a[i] = make_float2(v.x, v.y);
+    } else
+      a[i] = txy[st + i];
     c[i] = tz[st + i];
   }
 #pragma unroll
@@ -1306,26 +1320,26 @@ __device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int
 
 // a scheduling fence per row keeps the unrolled stencil from hoisting every
 // row's loads (register pressure; the other waves hide the LDS latency)
-template <class St, int I, class F>
+template <class St, int I, bool VX, class F>
 __device__ __forceinline__ void mir_rows(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
                                          const float4 q, F& f) {
   if constexpr (I < St::N) {
     constexpr SRow r = St::rows[I];
-    scan_run<r.len>(txy, tz, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)), q, f);
+    scan_run<r.len, VX>(txy, tz, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)), q, f);
     __builtin_amdgcn_sched_barrier(0);
-    mir_rows<St, I + 1>(txy, tz, qs, SY, SZ, xpos, q, f);
+    mir_rows<St, I + 1, VX>(txy, tz, qs, SY, SZ, xpos, q, f);
   }
 }
 
 // The lane's stencil: qs = its own slot, SY / SZ = the y / z slot strides
 // signed by the orientation, xpos = x orientation.
-template <class St, class F>
+template <class St, bool VX, class F>
 __device__ __forceinline__ void stencil_scan(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
                                              const float4 q, F&& f) {
   // the row bases are recomputed per scan (laundered inputs): hoisted and
   // shared across the kernel's scans they would stay live throughout
   asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
-  mir_rows<St, 0>(txy, tz, qs, SY, SZ, xpos, q, f);
+  mir_rows<St, 0, VX>(txy, tz, qs, SY, SZ, xpos, q, f);
 }
 
 // Block shape: WY x WZ waves, each wave a 4^3 voxel block; the block's box is
@@ -1342,7 +1356,7 @@ struct StileShape {
 };
 
 // WPE: waves per SIMD to register-allocate for (LDS allows 3 for 2x2)
-template <int KMAX, int WY, int WZ, int WPE>
+template <int KMAX, int WY, int WZ, int WPE, bool VX>
 __global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
                 int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
@@ -1422,9 +1436,9 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
         atomicAdd(&hw[ix * 64 + lane], 1u);
       };
       if (wide)
-        stencil_scan<Stencil245>(txy, tz, qs, SY, SZ, xpos, q, body);
+        stencil_scan<Stencil245, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
       else
-        stencil_scan<Stencil220>(txy, tz, qs, SY, SZ, xpos, q, body);
+        stencil_scan<Stencil220, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
 #pragma unroll
       for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
       if (lvl == 0) {
@@ -1464,11 +1478,11 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
       }
     };
     if (lsel == 0)
-      stencil_scan<Stencil210>(txy, tz, qs, SY, SZ, xpos, q, body);
+      stencil_scan<Stencil210, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
     else if (lsel == 1)
-      stencil_scan<Stencil220>(txy, tz, qs, SY, SZ, xpos, q, body);
+      stencil_scan<Stencil220, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
     else
-      stencil_scan<Stencil245>(txy, tz, qs, SY, SZ, xpos, q, body);
+      stencil_scan<Stencil245, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
     if (dbg == 3) {
       if (n == 12345) out[0] = 0.f;
       return;
@@ -2143,8 +2157,12 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
       // O3DX_TILE_DEBUG=1/2/3/4: stop after staging / histogram / list scan / moments (profiling only)
       const char* dbg = getenv("O3DX_TILE_DEBUG");
       const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
-      hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d, kneed,
-                         prior, out, list, lens, ffb, dg);
+      if (env_int("O3DX_STILE_VX", 1))
+        hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3, true>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d,
+                           kneed, prior, out, list, lens, ffb, dg);
+      else
+        hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3, false>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d,
+                           kneed, prior, out, list, lens, ffb, dg);
     }
     // the table as a dense GridView (identity cell starts, <= 1 point per cell)
     GridView g{};
@@ -2283,11 +2301,6 @@ static size_t nested_ws_bytes(int64_t n) {
   NestedWs w;
   nested_carve(ar, n, w);
   return ar.used;
-}
-
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
 }
 
 // Builds the nested grid and runs its tiles (hand-offs appended to fb_list as
