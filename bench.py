@@ -518,8 +518,9 @@ def c5_sharded(dev, args, world, rank):
            "icp_fitness": round(out["fitness"], 6),
            "T_err_vs_gt_inverse": float(np.abs(out["transformation"] - np.linalg.inv(synthetic.rigid_transform())).max()),
            "stages_ms_rank0": stages,
-           "collectives": "all_reduce (bounds, counts, fx digit sums, halo proof), all_to_all (halo reps), "
-                          "all_gather (target reps + normals for the replicated ICP target)"}
+           "collectives": "all_reduce (bounds, counts, fx digit sums, halo proof), all_to_all (halo reps; the "
+                          "ICP target rows within reach of each rank's source: distributed.WindowedTarget), "
+                          "all_gather (source boxes)"}
     del tgt, src, tg, sg, out
     torch.cuda.empty_cache()
     return {"c5_sharded": res}

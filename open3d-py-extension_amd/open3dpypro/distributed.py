@@ -311,15 +311,131 @@ def registration_icp_sharded(src: torch.Tensor, target, init=None, max_iteration
                              backend=None, n_source_total: Optional[int] = None):
     """Point-to-plane ICP of a source spread over the ranks (this rank's (n,3)
     float32 share) onto a replicated target (`backend.icp_target(...)`, e.g.
-    ops.ICPTarget): the fx quanta come from the GLOBAL source bounds, so T,
-    fitness and rmse equal ops.registration_icp on the whole source to the
-    bit.  Returns (T, fitness, inlier_rmse)."""
+    ops.ICPTarget) or a WindowedTarget (the target spread over the ranks too):
+    the fx quanta come from the GLOBAL source bounds, so T, fitness and rmse
+    equal ops.registration_icp on the whole source to the bit.  Returns (T,
+    fitness, inlier_rmse)."""
     be = backend or _HIP
     am = allreduce_max(be.absmax(src) if src.shape[0] else np.zeros(3), group)
     n_total = _allreduce_int(src.shape[0], group) if n_source_total is None else int(n_source_total)
     s = be.icp_source(src)
-    return registration_icp_point_to_plane(lambda T: be.icp_accumulate_fx(target, s, T, am), n_total, init,
-                                           max_iteration, relative_fitness, relative_rmse, group)
+    if isinstance(target, WindowedTarget):
+        target.bind(src)
+
+        def acc(T):
+            t = target.for_transform(T)
+            return _ICP_FX_ZERO.copy() if t is None else be.icp_accumulate_fx(t, s, T, am)
+    else:
+        def acc(T):
+            return be.icp_accumulate_fx(target, s, T, am)
+    return registration_icp_point_to_plane(acc, n_total, init, max_iteration, relative_fitness, relative_rmse, group)
+
+
+_ICP_FX_ZERO = np.zeros((32, 4), np.int64)  # a rank without source rows contributes nothing
+
+
+class WindowedTarget:
+    """The ICP target of a source AND a target spread over the ranks (C5:
+    both clouds' voxel reps live in x-slabs): instead of all-gathering the
+    whole target to every rank, each rank holds only the target rows within
+    max_correspondence_distance (+ a margin) of where its source rows can be
+    under the current transformation — the x-range of T applied to the
+    corners of its source's bounding box.
+
+    Every rank knows every rank's source box (one all-gather in bind()) and
+    the same T (the all-reduced sums), so all ranks decide alike, with no
+    collective, when some rank's window no longer covers its need; then all
+    refetch together (one counts + one payload all-to-all).  The rows of a
+    window are kept in global row order (`pos`), so the 1-NN's (d^2, index)
+    tie-break and hence every correspondence, T, fitness and rmse equal the
+    replicated target's to the bit.  Rows: this rank's target share `xyz`,
+    `normals`, ascending global positions `pos`."""
+
+    def __init__(self, xyz: torch.Tensor, normals: torch.Tensor, pos: torch.Tensor,
+                 max_correspondence_distance: float, margin: Optional[float] = None, group=None, backend=None):
+        self.xyz, self.nrm, self.pos = xyz, normals, pos
+        self.mc = float(max_correspondence_distance)
+        self.margin = 4.0 * self.mc if margin is None else float(margin)
+        self.group, self.be = group, backend or _HIP
+        self.boxes = None
+        self.win = None
+        self.target = None
+        self.fetches = 0
+        self.rows_held = 0
+
+    def bind(self, src: torch.Tensor):
+        """all-gather the ranks' source boxes (min xyz, max xyz; empty = +inf / -inf)"""
+        if src.shape[0]:
+            p = src[:, :3].double()
+            box = torch.cat([p.min(0).values, p.max(0).values]).cpu()
+        else:
+            box = torch.tensor([np.inf] * 3 + [-np.inf] * 3, dtype=torch.float64)
+        world, _ = _world(self.group)
+        if world > 1:
+            b = box.to(_comm_device(self.group))
+            parts = [torch.empty_like(b) for _ in range(world)]
+            dist.all_gather(parts, b, group=self.group)
+            box = torch.stack(parts).cpu()
+        else:
+            box = box[None]
+        self.boxes = box.numpy()
+        self.win = None
+
+    def _need(self, T):
+        """per rank the x-interval its source rows can reach under T (with the
+        correspondence radius), None for a rank without source rows"""
+        out = []
+        for b in self.boxes:
+            if not np.all(np.isfinite(b)):
+                out.append(None)
+                continue
+            cs = np.array([[x, y, z] for x in (b[0], b[3]) for y in (b[1], b[4]) for z in (b[2], b[5])])
+            xs = cs @ T[0, :3] + T[0, 3]
+            eps = 1e-6 * (1.0 + np.abs(xs).max() + self.mc)  # float64 transform / float32 coordinate slack
+            out.append((xs.min() - self.mc - eps, xs.max() + self.mc + eps))
+        return out
+
+    def for_transform(self, T):
+        T = np.asarray(T, np.float64).reshape(4, 4)
+        need = self._need(T)
+        ok = self.win is not None and all(
+            n is None or (w is not None and w[0] <= n[0] and n[1] <= w[1]) for n, w in zip(need, self.win))
+        if not ok:
+            self.win = [None if n is None else (n[0] - self.margin, n[1] + self.margin) for n in need]
+            self._fetch()
+        return self.target
+
+    def _fetch(self):
+        world, rank = _world(self.group)
+        x = self.xyz[:, 0]
+        masks = [torch.zeros_like(x, dtype=torch.bool) if w is None else (x >= w[0]) & (x <= w[1])
+                 for w in self.win]
+        self.fetches += 1
+        if world == 1:
+            m = masks[0]
+            rows = torch.cat([self.xyz[m], self.nrm[m]], 1)
+        else:
+            # the own rows stay put; only the other ranks' shares travel
+            packed = torch.cat([self.xyz, self.nrm, self.pos.to(torch.int32).view(torch.float32)[:, None]], 1)
+            masks_out = [torch.zeros_like(m) if j == rank else m for j, m in enumerate(masks)]
+            idx = torch.cat([torch.nonzero(m).flatten() for m in masks_out])
+            ss = [int(v) for v in torch.stack([m.sum() for m in masks_out]).cpu().tolist()]
+            cd = _comm_device(self.group)
+            sc = torch.tensor(ss, dtype=torch.int64, device=cd)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=self.group)
+            rs = rc.cpu().tolist()
+            recv = torch.empty((sum(rs), 7), dtype=torch.float32, device=cd)
+            dist.all_to_all_single(recv, packed[idx].to(cd), output_split_sizes=rs, input_split_sizes=ss,
+                                   group=self.group)
+            recv = torch.cat([packed[masks[rank]], recv.to(self.xyz.device)])
+            o = torch.argsort(recv[:, 6].contiguous().view(torch.int32))
+            rows = recv[o, :6]
+        self.rows_held = int(rows.shape[0])
+        if self.win[rank] is None or rows.shape[0] == 0:
+            self.target = None
+        else:
+            self.target = self.be.icp_target(rows[:, :3].contiguous(), rows[:, 3:].contiguous(), self.mc)
 
 
 def segment_plane_sharded(x: torch.Tensor, pos: torch.Tensor, n_total: int, distance_threshold: float,
@@ -722,9 +838,10 @@ def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tenso
       3. segment_plane on the target reps (segment_plane_sharded; the
          hypotheses sample the reps' global row order, RandomSampler(seed));
       4. point-to-plane ICP of the source reps onto the target reps
-         (registration_icp_sharded: target reps + normals all-gathered in
-         global order, the source sharded, fx moments all-reduced per
-         iteration), icp_iterations iterations from T = I (relative criteria 0).
+         (registration_icp_sharded: the source sharded, each rank holding the
+         target reps + normals within reach of its source (WindowedTarget),
+         fx moments all-reduced per iteration), icp_iterations iterations
+         from T = I (relative criteria 0).
 
     Every result equals the single-GPU chain (ops.voxel_down_sample ->
     estimate_normals -> segment_plane -> registration_icp) bit for bit.
@@ -755,24 +872,15 @@ def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tenso
     t0 = mark("segment_plane", t0)
     world, _ = _world(group)
     if world > 1:
-        info = torch.full((1,), int(trx.shape[0]), dtype=torch.int64, device=_comm_device(group))
-        parts = [torch.empty_like(info) for _ in range(world)]
-        dist.all_gather(parts, info, group=group)
-        counts = [int(p.item()) for p in parts]
-        rows = torch.cat([trx, tn], 1)
-        allrows = _all_gather_rows(rows, counts, group)
-        allpos = _all_gather_rows(pos, counts, group)
-        full = torch.empty_like(allrows)
-        full[allpos] = allrows
-        t_all, n_all = full[:, :3].contiguous(), full[:, 3:].contiguous()
+        target = WindowedTarget(trx, tn, pos, max_correspondence_distance, group=group)
     else:
-        t_all, n_all = trx, tn
-    t0 = mark("icp_gather_target", t0)
-    target = ops.ICPTarget(t_all, n_all, max_correspondence_distance)
-    t0 = mark("icp_target_build", t0)
+        target = ops.ICPTarget(trx, tn, max_correspondence_distance)
     T, fit, rm = registration_icp_sharded(srx, target, max_iteration=icp_iterations, relative_fitness=0.0,
                                           relative_rmse=0.0, group=group)
-    mark("icp_iterations", t0)
+    mark("icp", t0)
+    if timings is not None and world > 1:
+        timings["icp_target_fetches"] = target.fetches
+        timings["icp_target_rows_held"] = target.rows_held
     return {"target_rep_gidx": trg, "target_rep_xyz": trx, "target_normals": tn, "target_reps": mt,
             "source_reps": _allreduce_int(srx.shape[0], group), "plane": plane, "plane_inlier_rows": pos[inl],
             "transformation": T, "fitness": fit, "inlier_rmse": rm}
@@ -781,4 +889,4 @@ def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tenso
 __all__ = ["global_aabb", "global_bounds_device", "slab_bounds", "slab_of", "allreduce_counts", "allreduce_fx",
            "allreduce_max", "allreduce_icp_sums", "registration_icp_point_to_plane", "registration_icp_sharded",
            "segment_plane_sharded", "global_positions", "voxel_normals_slabs", "voxel_slabs", "pipeline_sharded",
-           "shard_range"]
+           "shard_range", "WindowedTarget"]

@@ -383,3 +383,38 @@ def test_fx_rows_oracle_vs_numpy():
     vals = np.array([NPR.fx_value(r) for r in fx[:30]])
     assert vals[28] == ref[28]
     np.testing.assert_allclose(vals, ref[:30], rtol=1e-11, atol=1e-13)
+
+
+def _icp_window_rank(rank, world, margin):
+    """target AND source in x-slabs (C5's layout): WindowedTarget per rank"""
+    from open3dpypro import distributed as Dm
+    src, tgt, tn = _icp_clouds()
+    be = OracleBackend()
+    cut_t = np.quantile(tgt[:, 0], np.linspace(0, 1, world + 1)[1:-1])
+    cut_s = np.quantile(src[:, 0], np.linspace(0, 1, world + 1)[1:-1])
+    pos = np.nonzero(np.searchsorted(cut_t, tgt[:, 0], side="right") == rank)[0]
+    mine = np.searchsorted(cut_s, src[:, 0], side="right") == rank
+    target = Dm.WindowedTarget(torch.from_numpy(tgt[pos]), torch.from_numpy(tn[pos].astype(np.float32)),
+                               torch.from_numpy(pos), 0.05, margin=margin, backend=be)
+    T, f, r = Dm.registration_icp_sharded(torch.from_numpy(src[mine]), target, max_iteration=12, backend=be,
+                                          n_source_total=len(src))
+    return T, f, r, target.fetches, target.rows_held
+
+
+@pytest.mark.parametrize("world,margin", [(2, 0.0), (3, 0.0), (3, None)])
+def test_icp_windowed_target_bit_identical(world, margin):
+    """ICP with the target spread over x-slabs too (distributed.WindowedTarget:
+    each rank holds only the target rows within reach of its source under the
+    current T, refetched by all ranks together when T moves a need past its
+    window; margin 0 refetches at nearly every step): T, fitness and rmse the
+    same bits as the replicated target on one process, with each rank holding
+    a part of the target."""
+    import functools
+    res = spawn(functools.partial(_icp_window_rank, margin=margin), world=world)
+    T1, f1, r1 = _icp_fx_rank(0, 1)
+    src, tgt, tn = _icp_clouds()
+    for T, f, r, fetches, held in res:
+        assert np.array_equal(T, T1) and f == f1 and r == r1
+        assert fetches >= 1 and held < len(tgt)
+    if margin == 0.0:
+        assert max(r[3] for r in res) > 1
