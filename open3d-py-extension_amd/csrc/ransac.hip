@@ -358,6 +358,157 @@ k_plane_upper_w8(const float* __restrict__ xyz, int64_t n, const float4* __restr
   plane_upper_body<kHC, kPL>(xyz, n, pl32, H, hi, bpw, nwp, ncg, partial);
 }
 
+// Upper bounds on the matrix cores.  The distances of 32 points to 32
+// hypotheses are v_mfma_f32_32x32x16_bf16 products of bf16 parts (round to
+// nearest) of the float32 coordinates and the float64 coefficients; bf16 x
+// bf16 products are exact in float32.
+//  TIGHT = false, one MFMA (K = 16), two parts each (x = xh + xl + xr,
+//    |xr| <= 2^-16 |x|):
+//      xh.ah + yh.bh + zh.ch + dh | xl.ah + yl.bh + zl.ch + dl | xh.al + yh.bl + zh.cl
+//    dropped xl.al, xr.a, x.ar, dr (<= 3.1 2^-16 S) + float32 accumulation of
+//    11 terms (<= 2^-19.5 S): |error| < 2^-14 S_h.
+//  TIGHT = true, two MFMAs (K = 32), three parts each (the float32 coordinate
+//    exactly: 3 x 8 significant bits; |ar| <= 2^-24 |a|):
+//      h.h, h.m, m.h, m.m, h.l, l.h per coordinate + dh + dm + dl
+//    dropped m.l, l.m, l.l, x.ar, dr (<= 3.1 2^-24 S) + float32 accumulation of
+//    21 terms (<= 2^-18.4 S): |error| < 2^-17 S_h.
+// S_h = |a| max|x| + |b| max|y| + |c| max|z| + |d|.  Counting |d| < hi_h, hi_h
+// >= thr + (that bound) counts every float64 inlier: an upper bound, as
+// k_plane_upper's (whose float32 band is 6 2^-24 S_h + 2^-20 thr).  The result
+// tile has the hypothesis on the lane (column lane & 31) and 16 point rows in
+// the registers: one compare + one add-with-carry per element, a count per
+// lane, no ballots or scalar popcounts (k_plane_upper's VALU distances cost
+// 1.5 packed fmas + a compare per pair: twice the issue).  Rows past n are
+// NaN: never counted.
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+template <bool TIGHT>
+struct MfmaShape {
+  static constexpr int kTiles = TIGHT ? 4 : 8;      // 32-point tiles per wave batch (A fragments in registers)
+  static constexpr int kChunks = TIGHT ? 16 : 32;   // hypothesis chunks of 32 per block (LDS ~36 KB)
+  static constexpr int kFrags = TIGHT ? 2 : 1;      // B fragments (uint4) per chunk lane
+  static constexpr int kBoundExp = TIGHT ? -17 : -14;
+};
+
+__device__ __forceinline__ uint32_t bf16_rne_bits(float x) {
+  const uint32_t b = __float_as_uint(x);
+  return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_f(uint32_t u) { return __uint_as_float(u << 16); }
+
+__device__ __forceinline__ bf16x8 frag8(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4, uint32_t a5,
+                                        uint32_t a6, uint32_t a7) {
+  u16x8 u;
+  u[0] = (unsigned short)a0;
+  u[1] = (unsigned short)a1;
+  u[2] = (unsigned short)a2;
+  u[3] = (unsigned short)a3;
+  u[4] = (unsigned short)a4;
+  u[5] = (unsigned short)a5;
+  u[6] = (unsigned short)a6;
+  u[7] = (unsigned short)a7;
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// A fragments of point (x, y, z) for lane half h (k = 8h .. 8h + 7 of each MFMA)
+template <bool TIGHT>
+__device__ __forceinline__ void point_frags(float x, float y, float z, int h, bf16x8* A) {
+  constexpr uint32_t one = 0x3f80;
+  const uint32_t xh = bf16_rne_bits(x), yh = bf16_rne_bits(y), zh = bf16_rne_bits(z);
+  const float rx = x - bf16_f(xh), ry = y - bf16_f(yh), rz = z - bf16_f(zh);  // exact
+  const uint32_t xm = bf16_rne_bits(rx), ym = bf16_rne_bits(ry), zm = bf16_rne_bits(rz);
+  const bool h0 = h == 0;
+  if constexpr (!TIGHT) {
+    // h0: xh yh zh 1 | xm ym zm 1   h1: xh yh zh 0 | 0 0 0 0
+    A[0] = frag8(xh, yh, zh, h0 ? one : 0, h0 ? xm : 0, h0 ? ym : 0, h0 ? zm : 0, h0 ? one : 0);
+  } else {
+    const uint32_t xl = bf16_rne_bits(rx - bf16_f(xm)), yl = bf16_rne_bits(ry - bf16_f(ym)),
+                   zl = bf16_rne_bits(rz - bf16_f(zm));
+    // MFMA 1  h0: xh yh zh 1 | xh yh zh 1     h1: xm ym zm 1 | xm ym zm 0
+    // MFMA 2  h0: xh yh zh 0 | xl yl zl 0     h1: 0
+    A[0] = h0 ? frag8(xh, yh, zh, one, xh, yh, zh, one) : frag8(xm, ym, zm, one, xm, ym, zm, 0);
+    A[1] = h0 ? frag8(xh, yh, zh, 0, xl, yl, zl, 0) : frag8(0, 0, 0, 0, 0, 0, 0, 0);
+  }
+}
+
+// grid: (point blocks, hypothesis groups of kChunks x 32); frag: [chunk][64
+// lanes][kFrags] B fragments, hi: [chunk][32]; partial[block x][H] int32 counts.
+// (a register budget of <= 256 VGPRs lets the compiler put the MFMA results
+// in VGPRs, not AGPRs read back one v_accvgpr_read per element)
+template <bool TIGHT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+k_plane_upper_mfma(const float* __restrict__ xyz, int64_t n, const uint4* __restrict__ frag,
+                   const float* __restrict__ hi, int nch, int H, int64_t batches_per_block,
+                   int32_t* __restrict__ partial) {
+  using Sh = MfmaShape<TIGHT>;
+  constexpr int kT = Sh::kTiles, kC = Sh::kChunks, kF = Sh::kFrags;
+  __shared__ uint4 lfrag[kC * 64 * kF];
+  __shared__ float lhi[kC * 32];
+  __shared__ int32_t lcnt[kC * 32];
+  const int c0 = blockIdx.y * kC, ncl = min(kC, nch - c0);
+  for (int t = threadIdx.x; t < ncl * 64 * kF; t += kBlock) lfrag[t] = frag[(int64_t)c0 * 64 * kF + t];
+  for (int t = threadIdx.x; t < ncl * 32; t += kBlock) {
+    lhi[t] = hi[(int64_t)c0 * 32 + t];
+    lcnt[t] = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  constexpr int kBatch = 32 * kT;
+  const int64_t nbat = (n + kBatch - 1) / kBatch;
+  const int64_t b0 = (int64_t)blockIdx.x * batches_per_block, b1 = min(b0 + batches_per_block, nbat);
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int64_t b = b0 + wv; b < b1; b += kBlock / 64) {
+    bf16x8 A[kT][kF];
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+      const int64_t i = b * kBatch + t * 32 + r;
+      float x = __builtin_nanf(""), y = x, z = x;
+      if (i < n) {
+        const P3 v = p[i];
+        x = v.x;
+        y = v.y;
+        z = v.z;
+      }
+      point_frags<TIGHT>(x, y, z, h, A[t]);
+    }
+    for (int c = 0; c < ncl; ++c) {
+      bf16x8 B[kF];
+#pragma unroll
+      for (int f = 0; f < kF; ++f) B[f] = __builtin_bit_cast(bf16x8, lfrag[(c * 64 + lane) * kF + f]);
+      const float hv = lhi[c * 32 + r];
+      int cnt = 0;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) {
+        f32x16 d = {};
+#pragma unroll
+        for (int f = 0; f < kF; ++f) d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[t][f], B[f], d, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) cnt += fabsf(d[e]) < hv ? 1 : 0;
+      }
+      atomicAdd(&lcnt[c * 32 + r], cnt);  // lanes r and r + 32 hold the two row halves
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < ncl * 32; t += kBlock) {
+    const int hh = c0 * 32 + t;
+    if (hh < H) partial[(int64_t)blockIdx.x * H + hh] = lcnt[t];
+  }
+}
+
+// Host side of the fragments: bf16 (round to nearest even) of a float
+static uint16_t bf16_rne_host(float x) {
+  uint32_t b;
+  std::memcpy(&b, &x, 4);
+  return (uint16_t)((b + 0x7fffu + ((b >> 16) & 1u)) >> 16);
+}
+static float bf16_value(uint16_t u) {
+  const uint32_t b = (uint32_t)u << 16;
+  float f;
+  std::memcpy(&f, &b, 4);
+  return f;
+}
+
 // The window results of the flagged (batch, hypothesis) blocks decided in
 // float64 (Open3D's order).  A wave per bitmap word: its batch's points are
 // loaded once, then every flagged hypothesis is re-evaluated (the same packed
@@ -609,6 +760,8 @@ struct CountWs {
   float4* band;
   double* pl64;
   uint8_t* degen;
+  uint4* mfrag;  // k_plane_upper_mfma: B fragments [chunk][64], then hi [chunk][32] (same upload)
+  float* mhi;
   int32_t* partial;
   size_t partial_ints;
   uint32_t* flags;  // (batch, hypothesis chunk) window bitmap of the brute-force count
@@ -619,11 +772,14 @@ struct CountWs {
 static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   H = std::max(H, 1);
   // the per-hypothesis inputs in one block: one upload (upload_planes)
-  uint8_t* up = ar.take<uint8_t>(65 * (size_t)H);
+  const size_t nch = ((size_t)H + 31) / 32, omf = (65 * (size_t)H + 15) & ~(size_t)15;
+  uint8_t* up = ar.take<uint8_t>(omf + nch * (64 * 32 + 32 * 4));
   w->pl32 = reinterpret_cast<float4*>(up);
   w->band = reinterpret_cast<float4*>(up + 16 * (size_t)H);
   w->pl64 = reinterpret_cast<double*>(up + 32 * (size_t)H);
   w->degen = up + 64 * (size_t)H;
+  w->mfrag = reinterpret_cast<uint4*>(up + omf);
+  w->mhi = reinterpret_cast<float*>(up + omf + nch * 64 * 32);
   w->partial_ints = (size_t)std::max(count_blocks(n), kCountWaves) * H;
   w->partial = ar.take<int32_t>(w->partial_ints);
   w->flags = ar.take<uint32_t>((size_t)count_flag_words(n, H, kMinBatchPts, kMinHC));
@@ -635,7 +791,8 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
 // scale of |a x| + |b y| + |c z| + |d| over the cloud, for the float32 band
 static void upload_planes(const double* planes, int H, const double absmax[3], double thr, CountWs& w,
                           std::vector<float4>& p32, std::vector<float4>& bnd, std::vector<uint8_t>& dg,
-                          std::vector<uint8_t>& st, hipStream_t s, int* rc, double* hi_max = nullptr) {
+                          std::vector<uint8_t>& st, hipStream_t s, int* rc, double* hi_max = nullptr,
+                          int mfma = 0) {  // 1 / 2: k_plane_upper_mfma<false / true>'s operands
   if (hi_max) *hi_max = -1.0;
   p32.resize(H);
   bnd.resize(H);
@@ -672,11 +829,61 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
   uint8_t* base = reinterpret_cast<uint8_t*>(w.pl32);
   const size_t ob = reinterpret_cast<uint8_t*>(w.band) - base, o64 = reinterpret_cast<uint8_t*>(w.pl64) - base,
                odg = w.degen - base;
-  st.resize(odg + H);  // the caller keeps it alive until the stream is synchronised
+  const size_t nch = ((size_t)H + 31) / 32, omf = reinterpret_cast<uint8_t*>(w.mfrag) - base,
+               ohi = reinterpret_cast<uint8_t*>(w.mhi) - base;
+  st.assign(mfma ? ohi + nch * 32 * 4 : odg + H, 0);  // the caller keeps it alive until the stream is synchronised
   std::memcpy(st.data(), p32.data(), H * sizeof(float4));
   std::memcpy(st.data() + ob, bnd.data(), H * sizeof(float4));
   std::memcpy(st.data() + o64, planes, 4 * H * sizeof(double));
   std::memcpy(st.data() + odg, dg.data(), H);
+  if (mfma) {
+    // k_plane_upper_mfma's B operand: hypothesis j is column j % 32 of chunk
+    // j / 32; bf16 parts (round to nearest) of the float64 plane.  One MFMA:
+    // lane r (ah bh ch dh | ah bh ch dl), lane r + 32 (al bl cl 0 | 0 0 0 0).
+    // Two MFMAs (tight): MFMA 1 lane r (ah bh ch dh | am bm cm dm), lane r + 32
+    // (ah bh ch dl | am bm cm 0); MFMA 2 lane r (al bl cl 0 | ah bh ch 0), lane
+    // r + 32 zero.  ("m" is the second part, "l" the third.)
+    const bool tight = mfma == 2;
+    const int nf = tight ? 2 : 1;
+    uint16_t* fr = reinterpret_cast<uint16_t*>(st.data() + omf);
+    float* hv = reinterpret_cast<float*>(st.data() + ohi);
+    for (size_t j = 0; j < nch * 32; ++j) hv[j] = -1.0f;
+    for (int j = 0; j < H; ++j) {
+      if (dg[j]) continue;  // zero fragments, hi -1: never counted
+      const double* pl = planes + 4 * j;
+      uint16_t P[3][4];  // parts: h, m, l
+      for (int a = 0; a < 4; ++a) {
+        double rem = pl[a];
+        for (int k = 0; k < 3; ++k) {
+          P[k][a] = bf16_rne_host((float)rem);
+          rem -= (double)bf16_value(P[k][a]);
+        }
+      }
+      const uint16_t(&h_)[4] = P[0];
+      const uint16_t(&m_)[4] = P[1];
+      const uint16_t(&l_)[4] = P[2];
+      auto put = [&](int lane, int f, const uint16_t (&v)[8]) {
+        std::memcpy(fr + (((size_t)(j / 32) * 64 + lane) * nf + f) * 8, v, 16);
+      };
+      const int r = j % 32;
+      if (!tight) {
+        put(r, 0, {h_[0], h_[1], h_[2], h_[3], h_[0], h_[1], h_[2], m_[3]});
+        put(r + 32, 0, {m_[0], m_[1], m_[2], 0, 0, 0, 0, 0});
+      } else {
+        put(r, 0, {h_[0], h_[1], h_[2], h_[3], m_[0], m_[1], m_[2], m_[3]});
+        put(r + 32, 0, {h_[0], h_[1], h_[2], l_[3], m_[0], m_[1], m_[2], 0});
+        put(r, 1, {l_[0], l_[1], l_[2], 0, h_[0], h_[1], h_[2], 0});
+        put(r + 32, 1, {0, 0, 0, 0, 0, 0, 0, 0});
+      }
+      const double S = std::fabs(pl[0]) * absmax[0] + std::fabs(pl[1]) * absmax[1] + std::fabs(pl[2]) * absmax[2] +
+                       std::fabs(pl[3]);
+      const double lim = thr + std::ldexp(1.0, tight ? MfmaShape<true>::kBoundExp : MfmaShape<false>::kBoundExp) * S +
+                         1e-30;
+      float f = (float)lim;
+      if ((double)f < lim) f = std::nextafter(f, INFINITY);
+      hv[(j / 32) * 32 + r] = f;
+    }
+  }
   if (hipMemcpyAsync(base, st.data(), st.size(), hipMemcpyHostToDevice, s) != hipSuccess)
     *rc = fail(O3DX_EIO, "plane upload failed");
 }
@@ -784,13 +991,53 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
   std::vector<uint8_t> st;
   int rc;
   double hmax;
-  upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, st, s, &rc, &hmax);
+  // The matrix-core sweep (two MFMAs, band thr + 2^-17 S_h) is wider than the
+  // VALU sweep's (thr + 6 2^-24 S_h): it is used while its band adds at most
+  // 2 % to thr, so the bounds stay about as tight and the replay consults
+  // about as many hypotheses.  O3DX_RANSAC_UPPER=HCxPLxW forces the VALU
+  // sweep, =mfma2 the two-MFMA and =mfma the one-MFMA form (band 2^-14 S_h).
+  double smax = 0.0;
+  for (int h = 0; h < H; ++h) {
+    const double* pl = planes + 4 * h;
+    const double S = std::fabs(pl[0]) * absmax[0] + std::fabs(pl[1]) * absmax[1] + std::fabs(pl[2]) * absmax[2] +
+                     std::fabs(pl[3]);
+    if (std::isfinite(S)) smax = std::max(smax, S);
+  }
+  const char* ue = getenv("O3DX_RANSAC_UPPER");
+  int mfma = 0;
+  if (ue) mfma = std::strcmp(ue, "mfma2") == 0 ? 2 : std::strcmp(ue, "mfma") == 0 ? 1 : 0;
+  else if (std::ldexp(1.0, MfmaShape<true>::kBoundExp) * smax <= 0.02 * thr) mfma = 2;
+  upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, st, s, &rc, &hmax, mfma);
   if (rc) return rc;
+  KTimer kt("plane_count_upper", s);
+  if (mfma) {
+    const int nch = (H + 31) / 32;
+    auto launch_mfma = [&](auto kern, int tiles, int chunks) {
+      const int ngy = (nch + chunks - 1) / chunks;
+      const int64_t nbat = std::max<int64_t>(1, (n + 32 * tiles - 1) / (32 * tiles));
+      // ~4 batches per wave, at most 2048 point blocks (the partial rows)
+      const int64_t nbx = std::min<int64_t>(2048, std::max<int64_t>(1, (nbat + 15) / 16));
+      const int64_t bpb = (nbat + nbx - 1) / nbx;
+      const unsigned gx = (unsigned)((nbat + bpb - 1) / bpb);
+      hipLaunchKernelGGL(kern, dim3(gx, ngy), dim3(kBlock), 0, s, xyz, n, w.mfrag, w.mhi, nch, H, bpb, w.partial);
+      return gx;
+    };
+    const unsigned gx = mfma == 2 ? launch_mfma(k_plane_upper_mfma<true>, MfmaShape<true>::kTiles,
+                                                MfmaShape<true>::kChunks)
+                                  : launch_mfma(k_plane_upper_mfma<false>, MfmaShape<false>::kTiles,
+                                                MfmaShape<false>::kChunks);
+    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, gx, H, w.counts, s));
+    hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
+    kt.stop();
+    ub.resize(H);
+    O3DX_TRY(read_back(ub.data(), w.counts, H * sizeof(int64_t), s));
+    O3DX_HIP(hipGetLastError());
+    return 0;
+  }
   // hi >= thr + g of every hypothesis (rounded up; nothing counted without any)
   float hi = (float)hmax;
   if ((double)hi < hmax) hi = std::nextafter(hi, INFINITY);
   if (hmax < 0) hi = -1.0f;
-  KTimer kt("plane_count_upper", s);
   int hc = 32, pl = 16, wv = 6;
   if (const char* e = getenv("O3DX_RANSAC_UPPER")) sscanf(e, "%dx%dx%d", &hc, &pl, &wv);
   int nwp;

@@ -674,10 +674,25 @@ def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatc
     valu = ops.plane_count(x, planes, thr)
     monkeypatch.delenv("O3DX_RANSAC_VALU")
     assert np.array_equal(got, valu)
-    # segment_plane's sweep: upper bounds, -1 exactly where degenerate
-    ub = ops.plane_count_upper(x, planes, thr)
-    assert np.array_equal(ub < 0, got < 0) and (ub >= got).all()
-    assert (ub - got).max() <= max(8, n // 10000)  # only window points add
+    # segment_plane's sweep: upper bounds, -1 exactly where degenerate; the
+    # matrix-core sweep (default) counts only points within its documented
+    # band |d| < thr + 2^-14 S_h (+ its own error, < 2^-14 S_h); the VALU
+    # sweep only the float32 window's
+    p64 = pts.astype(np.float64)
+    S_h = np.abs(planes[:, :3]) @ np.abs(p64).max(0) + np.abs(planes[:, 3])
+    for env in (None, "mfma", "mfma2", "32x16x6"):
+        if env:
+            monkeypatch.setenv("O3DX_RANSAC_UPPER", env)
+        ub = ops.plane_count_upper(x, planes, thr)
+        monkeypatch.delenv("O3DX_RANSAC_UPPER", raising=False)
+        assert np.array_equal(ub < 0, got < 0) and (ub >= got).all()
+        if env == "32x16x6":
+            assert (ub - got).max() <= max(8, n // 10000)  # only window points add
+        elif n <= 100_003 and env:
+            d = np.abs(p64 @ planes[:, :3].T + planes[:, 3])
+            band = (d < thr + 2.0 ** (-13 if env == "mfma" else -16) * S_h).sum(0)
+            ok = got >= 0
+            assert (ub[ok] <= band[ok]).all()
     ref = NPR.segment_plane_counts(pts, thr, samples) if n <= 100_003 else None
     if ref is not None:
         assert np.array_equal(got, ref)

@@ -55,8 +55,8 @@ def main():
                      "pairs_per_s": n * H / (ms / max(cnt, 1) * 1e-3)}
         print(json.dumps({name: out[name]}), flush=True)
     # the upper-bound count (segment_plane's sweep) and the whole segment_plane
-    for name in (os.environ.get("UPPER", "32x16x6,32x16x8,16x16x8,32x8x8")).split(","):
-        os.environ["O3DX_RANSAC_UPPER"] = name
+    for name in (os.environ.get("UPPER", "mfma2,mfma,32x16x6")).split(","):
+        os.environ["O3DX_RANSAC_UPPER"] = name  # mfma: k_plane_upper_mfma
         ub = ops.plane_count_upper(x, planes, 0.01)
         N.set_kernel_timing(True)
         N.reset_kernel_timing()
