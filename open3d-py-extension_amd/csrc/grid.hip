@@ -2221,6 +2221,18 @@ __device__ __forceinline__ bool any_around(const GridView& g, int64_t c, F&& f) 
   return false;
 }
 
+// points in cells of >= t points (one read per cell: the trigger test)
+__global__ void __launch_bounds__(kBlock) k_dense_points(GridView g, int t, unsigned long long* __restrict__ tot) {
+  const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
+  unsigned long long b = 0;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+    const int own = g.start[c + 1] - g.start[c];
+    b += own >= t ? (unsigned long long)own : 0ull;
+  }
+  b = wave_sum(b);
+  if (lane_id() == 0 && b) atomicAdd(tot, b);
+}
+
 __global__ void __launch_bounds__(kBlock) k_nested_mark(GridView g, int t, uint8_t* __restrict__ d1) {
   const int64_t nc = (int64_t)g.nx * g.ny * g.nz;
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x)
@@ -2285,7 +2297,7 @@ static void nested_carve(Arena& ar, int64_t n, NestedWs& w) {
   w.sub_cnt = ar.take<int32_t>(nc + 1);
   w.sub_off = ar.take<int32_t>(nc + 1);
   w.scan_tmp = ar.take<int32_t>(scan_workspace_ints(nc + 1));
-  w.tot = ar.take<unsigned long long>(2);
+  w.tot = ar.take<unsigned long long>(3);
   w.sub_xyz = ar.take<float>(3 * w.cap);
   w.sub_id = ar.take<int32_t>(w.cap);
   w.gws_bytes = grid_ws_bytes(w.cap);
@@ -2314,14 +2326,24 @@ static int nested_tiles(GridBuild& G, int64_t n, int kneed, double occ, const fl
   const int t = env_int("O3DX_NESTED_T", (int)std::ceil(4.0 * occ));
   const int64_t nc = (int64_t)G.view.nx * G.view.ny * G.view.nz;
   KTimer kt("normals_nested", s);
-  O3DX_HIP(hipMemsetAsync(w.tot, 0, 2 * sizeof(unsigned long long), s));
+  O3DX_HIP(hipMemsetAsync(w.tot, 0, 3 * sizeof(unsigned long long), s));
   const unsigned gc = grid_for(nc, kBlock, 4096);
+  // worth a second grid only when the dense cells hold a real share of the
+  // queries (a surface's edges and corners, a few denser cells, are cheaper
+  // left to the outer tiles and the wave form)
+  hipLaunchKernelGGL(k_dense_points, dim3(gc), dim3(kBlock), 0, s, G.view, t, w.tot + 2);
+  unsigned long long dense = 0;
+  O3DX_TRY(read_back(&dense, w.tot + 2, sizeof(dense), s));
+  const int64_t minq = std::max<int64_t>(kNestedMinQueries, n / env_int("O3DX_NESTED_DIV", 32));
+  if (getenv("O3DX_NESTED_VERBOSE"))
+    fprintf(stderr, "nested: n=%lld points in dense cells=%llu (min %lld)\n", (long long)n, dense, (long long)minq);
+  if ((int64_t)dense < minq) return 0;
   hipLaunchKernelGGL(k_nested_mark, dim3(gc), dim3(kBlock), 0, s, G.view, t, w.d1);
   hipLaunchKernelGGL(k_nested_cells, dim3(gc), dim3(kBlock), 0, s, G.view, w.d1, w.sub_cnt, w.tot);
   unsigned long long tot[2];
   O3DX_TRY(read_back(tot, w.tot, sizeof(tot), s));
-  const int64_t nsub = (int64_t)tot[0], nq = (int64_t)tot[1];
-  if (nq < kNestedMinQueries || nsub > w.cap) return 0;
+  const int64_t nsub = (int64_t)tot[0];
+  if (nsub > w.cap) return 0;
   O3DX_TRY(exclusive_scan_i32(w.sub_cnt, w.sub_off, nc, w.scan_tmp, s));
   hipLaunchKernelGGL(k_nested_gather, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, G.view, w.d1, w.sub_cnt,
                      w.sub_off, w.sub_xyz, w.sub_id);
