@@ -1346,13 +1346,19 @@ __device__ __forceinline__ void stencil_scan(const float2* txy, const float* tz,
 // the union (4 x 4WY x 4WZ voxels + the 3-voxel margin), staged once for all
 // its waves — 2x2 waves stage 7.7 slots per query instead of 15.6 and fit
 // 3 workgroups (12 waves) per CU in LDS.
+// The z-plane stride is padded to 16 (mod 32): lanes (x, y, z) and (x, y, z+1)
+// of a 32-lane half then read banks 16 apart, and the 32 lanes of a half
+// (4 x 4 x 2 voxels) hit 2.3 distinct slots per bank on average under the
+// random per-lane mirroring instead of 3.1 (ds_read_b64 / ds_read2_b32: bank =
+// slot mod 32; tools/stile_banks.py).
 template <int WY, int WZ>
 struct StileShape {
   static constexpr int NW = WY * WZ;
   static constexpr int EY = kVB * WY + 2 * kVM, EZ = kVB * WZ + 2 * kVM;
   static constexpr int SY = kVE;
-  static constexpr int SZ = kVE * EY;
-  static constexpr int CELLS = kVE * EY * EZ;  // box cells = LDS slots
+  static constexpr int SZ = kVE * EY + (16 - (kVE * EY) % 32 + 32) % 32;
+  static constexpr int NC = kVE * EY * EZ;  // box cells
+  static constexpr int CELLS = SZ * EZ;     // LDS slots (padded planes)
 };
 
 // WPE: waves per SIMD to register-allocate for (LDS allows 3 for 2x2)
@@ -1380,19 +1386,20 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   const int gx0 = bx * kVB - kVM, gy0 = by * (kVB * WY) - kVM, gz0 = bz * (kVB * WZ) - kVM;  // box origin
   {
     constexpr int kT = 64 * Sh::NW;
-    constexpr int J = (kSlots + kT - 1) / kT;
+    constexpr int J = (Sh::NC + kT - 1) / kT;
     float4 buf[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int t = threadIdx.x + kT * j;
-      if (t < kSlots) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kVE) % Sh::EY, gz0 + t / (kVE * Sh::EY));
+      if (t < Sh::NC) buf[j] = dvox_load(d, gx0 + t % kVE, gy0 + (t / kVE) % Sh::EY, gz0 + t / (kVE * Sh::EY));
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int t = threadIdx.x + kT * j;
-      if (t < kSlots) {
-        txy[t] = make_float2(buf[j].x, buf[j].y);
-        tz[t] = buf[j].z;
+      if (t < Sh::NC) {
+        const int u = t % (kVE * Sh::EY) + kSZ * (t / (kVE * Sh::EY));  // padded slot
+        txy[u] = make_float2(buf[j].x, buf[j].y);
+        tz[u] = buf[j].z;
       }
     }
   }
