@@ -42,11 +42,21 @@ def main():
     acc, na = N.kernel_timing("icp_accumulate")
     m, nm = N.kernel_timing("icp_match")
     N.set_kernel_timing(False)
+    per_iter = []  # match time of each iteration from T = I (the first ones see the displaced source)
+    T3 = np.eye(4)
+    N.set_kernel_timing(True)
+    for _ in range(iters):
+        N.reset_kernel_timing()
+        s3, _ = target.accumulate(src4, T3)
+        torch.cuda.synchronize()
+        per_iter.append(round(N.kernel_timing("icp_match")[0], 3))
+        T3 = ops.icp_solve(s3) @ T3
+    N.set_kernel_timing(False)
     err = float(np.abs(T - np.linalg.inv(S.rigid_transform())).max())
     print(json.dumps({"tag": os.environ.get("TAG", ""), "iters_per_s": round(iters / el, 2),
                       "ms_per_iter": round(el / iters * 1e3, 4), "accumulate_ms": round(acc / max(na, 1), 4),
                       "match_ms": round(m / max(nm, 1), 4), "T_err": err, "T": T.round(12).tolist(),
-                      "fitness": float(sums[28]) / n}), flush=True)
+                      "fitness": float(sums[28]) / n, "match_ms_per_iteration": per_iter}), flush=True)
 
 
 if __name__ == "__main__":

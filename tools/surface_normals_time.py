@@ -14,8 +14,12 @@ from open3dpypro import _native as N, ops, synthetic as S  # noqa: E402
 
 dev = torch.device("cuda:0")
 pts = S.box_surface(10_000_000, seed=1, device=dev)
-for env in ({}, {"O3DX_NESTED_OFF": "1"}):
-    os.environ.pop("O3DX_NESTED_OFF", None)
+# argv: NAME=VAL[,NAME=VAL] configurations (default: nested on / off)
+cfgs = [dict(kv.split("=") for kv in a.split(",") if kv) for a in sys.argv[1:]] or [{}, {"O3DX_NESTED_OFF": "1"}]
+keys = {k for c in cfgs for k in c}
+for env in cfgs:
+    for k in keys:
+        os.environ.pop(k, None)
     os.environ.update(env)
     a = ops.estimate_normals(pts, knn=30)
     torch.cuda.synchronize()
