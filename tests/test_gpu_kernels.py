@@ -697,3 +697,31 @@ def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatc
     if ref is not None:
         assert np.array_equal(got, ref)
     assert got[0] == -1
+
+
+@pytest.mark.parametrize("n", [1_000_000])
+def test_c2_pipeline_full_mantissa_coordinates(dev, n):
+    """The C2 step (one-call voxel_down_sample + KNN30 normals on the voxel
+    table) on coordinates with full float32 mantissas and an offset origin —
+    unlike synthetic.uniform_cube's 2^-24 grid, where the float64 moments are
+    exact in any summation order — so the stencil-order sums meet
+    non-representable partial sums: reps bit-exact, every normal row within
+    1e-5 of the oracle, neighbour sets bit-exact."""
+    u = S.uniform_cube(n, 77).double()
+    pts = (u * 3.7 + torch.tensor([-1.234567, 0.3141593, 2.7182818], dtype=torch.float64)).float()
+    p = pts.numpy()
+    assert np.mean(np.abs(p.view(np.int32)) & 0xFF != 0) > 0.9  # low mantissa bits in use
+    vs = S.voxel_size_for(n) * 3.7
+    x = pts.to(dev)
+    f = ops.voxel_down_sample_normals(x, vs, knn=30)
+    a = ops.voxel_down_sample(x, vs, keep_grid=True)
+    with DebugNeighbors(n, 30, dev) as dn:
+        two = ops.estimate_normals(a["rep_xyz"], knn=30, voxel_grid=a["voxel_grid"])
+    assert torch.equal(f["rep_idx"], a["rep_idx"]) and torch.equal(f["normals"], two)
+    rep = f["rep_idx"].cpu().numpy()
+    assert np.array_equal(rep, O.voxel_down_sample(p, vs))
+    reps = p[rep]
+    m = len(reps)
+    assert_normals(f["normals"].cpu().numpy(), O.estimate_normals(reps, O.KNN, 30), reps, k=30,
+                   what="c2_full_mantissa_1m")
+    assert_neighbour_sets(dn.ids()[:m], reps, 30, "c2_full_mantissa_1m")
