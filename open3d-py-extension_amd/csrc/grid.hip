@@ -580,6 +580,7 @@ struct MomAcc {
 #pragma unroll
     for (int j = 0; j < 9; ++j) m[j] = 0.0;
   }
+  __device__ void init(const float4&, float, int) {}
   // Open3D ComputeCovariance cumulant order
   __device__ void add(double x, double y, double z) {
     m[0] += x;
@@ -629,6 +630,7 @@ struct MomAccDD {
 #pragma unroll
     for (int j = 0; j < 9; ++j) m[j] = l[j] = 0.0;
   }
+  __device__ void init(const float4&, float, int) {}
   __device__ __forceinline__ void put(int j, double t) {
     double s, e;
     two_sum(m[j], t, s, e);
@@ -651,6 +653,56 @@ struct MomAccDD {
 #pragma unroll
     for (int j = 0; j < 9; ++j) a.m[j] = m[j] + l[j];
     a.cov(k, c);
+  }
+};
+
+// The same correctly rounded exact sums as MomAccDD at half its cost, for a
+// selection whose members all lie within sqrt(r2) of the query q: each moment
+// starts at an anchor A (a power of two >= 4 x the bound on the sum of |terms|
+// of up to kmax neighbours, from |q| + sqrt(r2) per axis), so every partial
+// sum stays in [A/2, 2A) and is at least as large as any term — Fast2Sum (3
+// flops) then gives each addition's exact error, where MomAccDD's TwoSum
+// takes 6.  m - A is exact (Sterbenz); (m - A) + l, rounded once, is the
+// correctly rounded exact sum under MomAccDD's condition (non-zero
+// coordinates within a factor 2^22: the errors then fit l exactly), so the
+// bits equal MomAccDD's and every other exact path's.
+struct MomAccA {
+  double m[9], l[9], a[9];
+  __device__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) m[j] = l[j] = a[j] = 0.0;
+  }
+  __device__ void init(const float4& q, float r2, int kmax) {
+    const double r = sqrt((double)r2) * (1.0 + 1e-6) + 1e-30;
+    const double X = fabs((double)q.x) + r, Y = fabs((double)q.y) + r, Z = fabs((double)q.z) + r;
+    const double b[9] = {X, Y, Z, X * X, X * Y, X * Z, Y * Y, Y * Z, Z * Z};
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      a[j] = ldexp(1.0, ilogb((double)kmax * b[j]) + 3);  // >= 4 kmax b (ilogb floors)
+      m[j] = a[j];
+    }
+  }
+  __device__ __forceinline__ void put(int j, double t) {
+    const double s = m[j] + t;
+    l[j] += t - (s - m[j]);
+    m[j] = s;
+  }
+  __device__ void add(double x, double y, double z) {
+    put(0, x);
+    put(1, y);
+    put(2, z);
+    put(3, x * x);
+    put(4, x * y);
+    put(5, x * z);
+    put(6, y * y);
+    put(7, y * z);
+    put(8, z * z);
+  }
+  __device__ void cov(int k, double c[6]) const {
+    MomAcc acc;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc.m[j] = (m[j] - a[j]) + l[j];
+    acc.cov(k, c);
   }
 };
 
@@ -835,6 +887,7 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
                                                  float* __restrict__ kd2, bool skip_eigen = false) {
   Acc acc;
   acc.zero();
+  acc.init(q, U * (1.0f + 2.0f * kRelEps), kneed);  // every member lies below the list bound
   int nsel = 0, nb = 0, nU = 0;
   float cmax = 0.0f;  // largest certain key
   int32_t* const nrow = nbr ? nbr + (int64_t)oi * kneed : nullptr;  // test hook
@@ -1038,7 +1091,7 @@ __device__ __forceinline__ void tile_row(const GridView& g, const TileBox& b, co
     atomicAdd(&hw[(ix_ + 1) * 64 + lane], 1u);                                              \
   })
 
-template <int KMAX>
+template <int KMAX, class TAcc = MomAccA>
 __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
                                                              int kneed, const float* __restrict__ prior,
                                                              float* __restrict__ out, int32_t* __restrict__ fb_list,
@@ -1169,7 +1222,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
             if (n == 12345) out[0] = 0.f;  // keep the scan alive
           } else
           fb = n > kListMax ||
-               !finish_selection<KMAX, MomAccDD>(
+               !finish_selection<KMAX, TAcc>(
                    q, kneed, n, Lm, U, lst, lane, [&](int p) { return make_float4(tx[p], ty[p], tz[p], 0.f); },
                    prior, out_row(g, qw), out, g.nbr,
                    [&](int p) { return out_row(g, __float_as_int(g.pts[tile_global_pos(rows, rst, p)].w)); }, g.kd2,
@@ -2422,7 +2475,10 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
       const char* dbg_env = getenv("O3DX_TILE_DEBUG");
       const int dbg = dbg_env ? atoi(dbg_env) : 0;
       KTimer kt_tile("normals_tile", s);
-      if (kneed <= 32)
+      if (kneed <= 32 && env_int("O3DX_TILE_DD", 0))  // A/B: the TwoSum accumulator (same bits)
+        hipLaunchKernelGGL((k_normals_knn_tile<32, MomAccDD>), dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view,
+                           chunks, kneed, prior, out, list1, lens, dbg);
+      else if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_tile<32>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
                            kneed, prior, out, list1, lens, dbg);
       else

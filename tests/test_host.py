@@ -433,3 +433,37 @@ def test_pcd_binary_compressed_host_reader(tmp_path):
     P, Nn, C = pcd_io.read_pcd(p)
     assert np.array_equal(P, pts.astype(np.float64)) and np.array_equal(Nn, nrm.astype(np.float64))
     assert np.allclose(C * 255.0, np.stack([(rgb >> 16) & 255, (rgb >> 8) & 255, rgb & 255], 1))
+
+
+def test_anchored_moment_sums_are_correctly_rounded():
+    """grid.hip MomAccA (the sorted-grid tile kernel's moments): anchored
+    Fast2Sum per moment, restated in numpy float64 with the kernel's operation
+    order, equals math.fsum (the correctly rounded exact sum) on every moment
+    of random neighbourhoods — offsets, scales and mixed signs included — so
+    its bits equal the double-double (TwoSum) accumulator's."""
+    import math
+    rng = np.random.default_rng(7)
+    for trial in range(400):
+        k = int(rng.integers(1, 65))
+        scale = 10.0 ** rng.uniform(-3, 2)
+        q = (rng.uniform(-1, 1, 3) * scale * rng.choice([1, 10, 100])).astype(np.float32)
+        r = scale * rng.uniform(0.01, 0.5)
+        p = (q.astype(np.float64) + rng.uniform(-1, 1, (k, 3)) * r / np.sqrt(3)).astype(np.float32)
+        d2 = ((p.astype(np.float64) - q) ** 2).sum(1)
+        r2 = np.float32(d2.max() * (1 + 2 * 2.0 ** -20))
+        rr = math.sqrt(float(r2)) * (1.0 + 1e-6) + 1e-30
+        X, Y, Z = (abs(float(c)) + rr for c in q)
+        b = [X, Y, Z, X * X, X * Y, X * Z, Y * Y, Y * Z, Z * Z]
+        a = [math.ldexp(1.0, math.frexp(k * bj)[1] - 1 + 3) for bj in b]  # ilogb(v) = frexp exponent - 1
+        m, l = list(a), [0.0] * 9
+        for x, y, z in p.astype(np.float64):
+            for j, t in enumerate((x, y, z, x * x, x * y, x * z, y * y, y * z, z * z)):
+                s = m[j] + t
+                l[j] += t - (s - m[j])
+                m[j] = s
+        got = [(m[j] - a[j]) + l[j] for j in range(9)]
+        pp = p.astype(np.float64)
+        cols = [pp[:, 0], pp[:, 1], pp[:, 2], pp[:, 0] * pp[:, 0], pp[:, 0] * pp[:, 1], pp[:, 0] * pp[:, 2],
+                pp[:, 1] * pp[:, 1], pp[:, 1] * pp[:, 2], pp[:, 2] * pp[:, 2]]
+        exp = [math.fsum(c.tolist()) for c in cols]
+        assert got == exp, (trial, k, got, exp)
