@@ -378,53 +378,71 @@ def c5_pipeline(dev, args):
     a 200M-point box-surface scene and an independent 200M-point sample of it
     moved by T_gt -> voxel_down_sample both (vs 0.5 mm) -> KNN30 normals on the
     target reps -> segment_plane (1000 hypotheses) on the target reps ->
-    point-to-plane ICP source reps -> target reps, 30 iterations from T = I."""
+    point-to-plane ICP source reps -> target reps, 30 iterations from T = I.
+
+    The chain runs twice on the same clouds: an untimed warm-up (its stages
+    are reported as `first_call_stages_ms`: the workspaces' first allocation
+    and first touch after the C4 leg's empty_cache land there — the 521 ms
+    voxel_target of BENCH_r03), then the timed run, as every other leg."""
     n = args.c5_n
     vs = 0.0005
     res = {"n": n, "voxel_size": vs}
-    stages = {}
-
-    def timed(name, fn):
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        r = fn()
-        torch.cuda.synchronize(dev)
-        stages[name] = round((time.perf_counter() - t0) * 1e3, 3)
-        return r
 
     tgt = synthetic.box_surface(n, seed=1, device=dev)
     src = synthetic.apply_transform(synthetic.box_surface(n, seed=2, device=dev), synthetic.rigid_transform())
-    torch.cuda.synchronize(dev)
-    t_all = time.perf_counter()
-    vt = timed("voxel_target", lambda: ops.voxel_down_sample(tgt, vs, keep_grid=True))
-    vsrc = timed("voxel_source", lambda: ops.voxel_down_sample(src, vs))
-    del tgt, src
-    treps, sreps = vt["rep_xyz"], vsrc["rep_xyz"]
-    tn = timed("normals_target", lambda: ops.estimate_normals(treps, knn=30, voxel_grid=vt.get("voxel_grid")))
-    samples = ops.ransac_samples(treps.shape[0], 3, args.ransac_iters, seed=7)
-    plane, inl = timed("segment_plane", lambda: ops.segment_plane(treps, 0.002, 3, args.ransac_iters,
-                                                                  samples=samples))
+    samples = None
 
-    def icp():
-        target = ops.ICPTarget(treps, tn, 0.02)
-        s4 = ops.spatial_sort(sreps)
-        T = np.eye(4)
-        sums = None
-        for _ in range(args.icp_iters):
-            sums, _ = target.accumulate(s4, T)
-            T = ops.icp_solve(sums) @ T
-        return T, sums
+    def chain(stages):
+        nonlocal samples
 
-    T, sums = timed("icp_30", icp)
-    total = time.perf_counter() - t_all
-    res.update({"target_reps": int(treps.shape[0]), "source_reps": int(sreps.shape[0]), "stages_ms": stages,
-                "total_ms": round(total * 1e3, 3), "Mpoints_per_s_voxel_normals_target":
-                round(n / ((stages["voxel_target"] + stages["normals_target"]) * 1e-3) / 1e6, 2),
-                "icp_iters_per_s": round(args.icp_iters / (stages["icp_30"] * 1e-3), 2),
-                "plane": [round(float(v), 6) for v in plane], "plane_inliers": int(inl.numel()),
+        def timed(name, fn):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            r = fn()
+            torch.cuda.synchronize(dev)
+            stages[name] = round((time.perf_counter() - t0) * 1e3, 3)
+            return r
+
+        torch.cuda.synchronize(dev)
+        t_all = time.perf_counter()
+        vt = timed("voxel_target", lambda: ops.voxel_down_sample(tgt, vs, keep_grid=True))
+        vsrc = timed("voxel_source", lambda: ops.voxel_down_sample(src, vs))
+        treps, sreps = vt["rep_xyz"], vsrc["rep_xyz"]
+        tn = timed("normals_target", lambda: ops.estimate_normals(treps, knn=30, voxel_grid=vt.get("voxel_grid")))
+        if samples is None:
+            samples = ops.ransac_samples(treps.shape[0], 3, args.ransac_iters, seed=7)
+        plane, inl = timed("segment_plane", lambda: ops.segment_plane(treps, 0.002, 3, args.ransac_iters,
+                                                                      samples=samples))
+
+        def icp():
+            target = ops.ICPTarget(treps, tn, 0.02)
+            s4 = ops.spatial_sort(sreps)
+            T = np.eye(4)
+            sums = None
+            for _ in range(args.icp_iters):
+                sums, _ = target.accumulate(s4, T)
+                T = ops.icp_solve(sums) @ T
+            return T, sums
+
+        T, sums = timed("icp_30", icp)
+        total = time.perf_counter() - t_all
+        return {"target_reps": int(treps.shape[0]), "source_reps": int(sreps.shape[0]), "total_ms":
+                round(total * 1e3, 3), "plane": [round(float(v), 6) for v in plane], "plane_inliers": int(inl.numel()),
                 "icp_fitness": round(float(sums[28]) / max(int(sreps.shape[0]), 1), 6),
-                "T_err_vs_gt_inverse": float(np.abs(T - np.linalg.inv(synthetic.rigid_transform())).max())})
-    del vt, vsrc, treps, sreps, tn, inl
+                "T_err_vs_gt_inverse": float(np.abs(T - np.linalg.inv(synthetic.rigid_transform())).max())}
+
+    first = {}
+    r0 = chain(first)
+    stages = {}
+    r1 = chain(stages)
+    if (r0["target_reps"], r0["plane_inliers"], r0["plane"]) != (r1["target_reps"], r1["plane_inliers"], r1["plane"]):
+        raise RuntimeError("C5: the warm-up and the timed run disagree")
+    res.update(r1)
+    res.update({"stages_ms": stages, "first_call_stages_ms": first, "first_call_total_ms": r0["total_ms"],
+                "Mpoints_per_s_voxel_normals_target":
+                round(n / ((stages["voxel_target"] + stages["normals_target"]) * 1e-3) / 1e6, 2),
+                "icp_iters_per_s": round(args.icp_iters / (stages["icp_30"] * 1e-3), 2)})
+    del tgt, src
     torch.cuda.empty_cache()
     return {"c5_single_gpu": res}
 

@@ -639,8 +639,12 @@ def _slab_reps_generic(xyz, gidx, voxel_size, group, voxel_fn, presorted):
         xyz, gidx = _exchange(torch.searchsorted(inner, kx, right=True), world, group, xyz, gidx)
         o = torch.argsort(gidx)
         xyz, gidx = xyz[o].contiguous(), gidx[o].contiguous()
-    elif presorted and xyz.shape[0] and bool(((kx < keys[rank]) | (kx >= keys[rank + 1])).any()):
-        raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside this rank's slab")
+    elif presorted:
+        # every rank learns the verdict before any raises (a lone raise would
+        # leave the peers blocked in the next collective)
+        nbad = int(((kx < keys[rank]) | (kx >= keys[rank + 1])).sum()) if xyz.shape[0] else 0
+        if (_allreduce_int(nbad, group) if world > 1 else nbad):
+            raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside its rank's slab")
     rep = voxel_fn(xyz, voxel_size, mn, mx)
     return gidx[rep].contiguous(), xyz[rep].contiguous(), mn, mx, keys
 
@@ -651,8 +655,10 @@ def _slab_reps_device(xyz, gidx, vs, group, presorted):
     slab's reps with GLOBAL keys (a dense x-key window table when the slab is
     not sparse — the library's dense rule, 2n + 2^20 cells — else the hash
     path).  Returns (rep gidx ascending, rep xyz, mn, mx, keys, dims, bad)
-    where `bad` is a device count of points outside the slab (sparse
-    presorted path; the dense window call fails loudly by itself) or None."""
+    where `bad` is a device count of points outside the slab (presorted
+    inputs on more than one rank) or None.  A presorted rank holding such
+    points returns no reps and its count instead of raising, so every caller
+    turns the all-reduced count into the same RuntimeError on every rank."""
     from . import ops
 
     world, rank = _world(group)
@@ -673,7 +679,14 @@ def _slab_reps_device(xyz, gidx, vs, group, presorted):
     bad = None
     if k_hi > k_lo and n_loc > 0:
         if (k_hi - k_lo + 6) * layer <= 2 * n_loc + (1 << 20):
-            out = ops.voxel_down_sample_window(xyz, vs, mn, mx, k_lo, k_hi)
+            try:
+                out = ops.voxel_down_sample_window(xyz, vs, mn, mx, k_lo, k_hi)
+            except RuntimeError as e:
+                if not (presorted and world > 1 and "outside the x-key window" in str(e)):
+                    raise
+                kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+                bad = ((kx < k_lo) | (kx >= k_hi)).sum()
+                return gidx[:0], xyz[:0], mn, mx, keys, dims, bad
         else:
             out = ops.voxel_down_sample(xyz, vs, mn, mx)
             if presorted and world > 1:

@@ -517,6 +517,9 @@ class ICPTarget:
             s = _xyz(src.to(self.xyz.device), "source points")
         if absmax is None:
             absmax = getattr(src, "absmax", None)
+            of = getattr(src, "absmax_of", None)
+            if absmax is None and of is not None:  # spatial_sort's cloud, measured on first use only
+                absmax = src.absmax = _absmax(of)
         L = N.load()
         ns = s.shape[0]
         TT = _c(T, np.float64).reshape(4, 4)
@@ -537,8 +540,10 @@ class ICPTarget:
 def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
     """(n,4) float32 copy of the cloud in a compact spatial order (8^3 blocks of
     grid cells, Morton order inside a block); column 3 holds the original
-    int32 index bits (o3dx_spatial_sort).  The tensor carries `.absmax`, the
-    cloud's |x|,|y|,|z| bounds (ICPTarget.accumulate's default)."""
+    int32 index bits (o3dx_spatial_sort).  The tensor carries `.absmax_of`,
+    the cloud itself: ICPTarget.accumulate measures its |x|,|y|,|z| bounds
+    (the default fx quanta) on first use, so a caller passing its own bounds
+    (a sharded source: the global ones) never pays that host wait."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
@@ -547,20 +552,24 @@ def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
     N.check(L.o3dx_spatial_sort(N.ptr(x), n, float(target_occ), N.ptr(out), N.ptr(ws), ws.numel(),
                                 N.stream_ptr(x.device)), "spatial_sort")
     res = out[:n]
-    res.absmax = absmax(x)  # the cloud's coordinate bounds, for ICPTarget.accumulate's fx quanta
+    res.absmax_of = x
     return res
 
 
 def icp_update(sums, T: np.ndarray) -> np.ndarray:
     """T <- solve(sums) * T in the library's own float64 order (o3dx_icp_update)."""
     TT = np.array(T, np.float64).reshape(4, 4).copy()
-    N.load().o3dx_icp_update(_np_ptr(_c(sums, np.float64)), _np_ptr(TT))
+    rc = N.load().o3dx_icp_update(_np_ptr(_c(sums, np.float64)), _np_ptr(TT))
+    if rc < 0:  # 1 solved, 0 singular (identity update, as Open3D), < 0 a library error
+        N.check(rc, "icp_update")
     return TT
 
 
 def icp_solve(sums) -> np.ndarray:
     upd = np.zeros((4, 4), np.float64)
-    N.load().o3dx_icp_solve_point_to_plane(_np_ptr(_c(sums, np.float64)), _np_ptr(upd))
+    rc = N.load().o3dx_icp_solve_point_to_plane(_np_ptr(_c(sums, np.float64)), _np_ptr(upd))
+    if rc < 0:
+        N.check(rc, "icp_solve")
     return upd
 
 
@@ -592,3 +601,6 @@ def registration_icp(src: torch.Tensor, tgt: torch.Tensor, tgt_normals: torch.Te
     if return_corr:
         out["correspondence_set"] = corr[: int(nc[0])]
     return out
+
+
+_absmax = absmax  # for ICPTarget.accumulate, whose parameter of that name shadows it

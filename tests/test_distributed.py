@@ -215,6 +215,34 @@ def test_c4_slabs_match_single(world):
     _check_slabs(res, _c4_cloud().numpy(), 0.05)
 
 
+def _c4_misplaced_rank(rank, world):
+    """presorted slabs with ONE point of rank 0's slab handed to the last rank
+    only: every rank must raise, none may block in a later collective"""
+    pts = _c4_cloud()
+    vs = 0.05
+    mn, mx = O.aabb(pts.numpy())
+    keys = D.slab_bounds(mn, mx, vs, world)
+    kx = np.floor((pts[:, 0].double().numpy() - mn[0]) / vs).astype(np.int64)
+    owner = np.searchsorted(np.asarray(keys[1:-1]), kx, side="right")
+    stray = int(np.flatnonzero(owner == 0)[0])
+    owner[stray] = world - 1
+    g = torch.from_numpy(np.flatnonzero(owner == rank).astype(np.int64))
+    try:
+        D.voxel_normals_slabs(pts[g], g, vs, knn=30, voxel_fn=_o3_voxel, normals_fn=_o3_normals, presorted=True)
+    except RuntimeError as e:
+        return "raised: " + str(e)
+    return "returned"
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_presorted_stray_point_raises_on_every_rank(world):
+    """a presorted point outside its slab is reported on EVERY rank
+    (the verdict is all-reduced before anyone raises), not only on the rank
+    holding it while its peers wait in the halo exchange."""
+    res = spawn(_c4_misplaced_rank, world=world)
+    assert all(r.startswith("raised") and "outside" in r for r in res), res
+
+
 # A clustered cloud that defeats a halo check limited to the reps near a face:
 # dense blobs sit on every interior slab face (their reps near the face have
 # tiny k-th-neighbour distances), the sparse background keeps a band of 0.04

@@ -153,6 +153,41 @@ def test_c4_slabs_presorted_on_device(world):
     assert np.array_equal(nn[o], ref)
 
 
+def _c4_stray_rank(rank, world):
+    """presorted slabs on the device (the dense x-window branch) with one point
+    of rank 0's slab handed to the last rank only"""
+    dev = torch.device("cuda:0")
+    n = 1_000_000
+    vs = S.voxel_size_for(n)
+    pts = S.uniform_cube(n, 44).to(dev)
+    mn, mx = ops.aabb(pts)
+    keys = D.slab_bounds(mn, mx, vs, world)
+    kx = torch.floor((pts[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+    owner = torch.searchsorted(torch.tensor(keys[1:-1], dtype=torch.int64, device=dev), kx, right=True)
+    stray = int(torch.nonzero(owner == 0)[0])
+    owner[stray] = world - 1
+    g = torch.nonzero(owner == rank).flatten()
+    out = []
+    for fn in (lambda: D.voxel_normals_slabs(pts[g].contiguous(), g, vs, knn=30, presorted=True),
+               lambda: D.voxel_slabs(pts[g].contiguous(), g, vs, presorted=True)):
+        try:
+            fn()
+            out.append("returned")
+        except RuntimeError as e:
+            out.append("raised: " + str(e))
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_presorted_stray_point_raises_on_every_rank_device(world):
+    """the dense-window branch turns a stray presorted point into
+    the all-reduced verdict (every rank raises, no rank blocks), for the
+    normals step and the voxel-only step alike."""
+    res = spawn(_c4_stray_rank, world=world)
+    for r in res:
+        assert all(v.startswith("raised") and "outside" in v for v in r), res
+
+
 # ------------------------------------------------------ C4 at its own size
 C4_N = 50_000_000
 
