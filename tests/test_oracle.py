@@ -135,3 +135,128 @@ def test_icp_oracle_recovers_transform():
     T, fit, rmse, corr = O.registration_icp(src, tgt, tn, 0.02, max_iteration=30)
     assert np.abs(T - np.linalg.inv(Tgt)).max() < 1e-4
     assert fit > 0.99 and len(corr) == int(round(fit * len(src)))
+
+
+# ---------------------------------------------------------------------------
+# The glue around the hot path, pinned by the reference's OWN outputs
+# (tests/golden/ref_glue.npz, written by `python tests/golden/make_golden.py
+# glue` from /root/reference/open3dpypro/processors.py in this container):
+# the test-side restatements (oracle/np_restate.py) AND the build's processors
+# (open3dpypro.processors, on numpy / torch-CPU data: no GPU involved) must
+# reproduce them bit for bit.
+GLUE = os.path.join(os.path.dirname(__file__), "golden", "ref_glue.npz")
+PN_CASES = ["np_f32", "np_f64", "np_f32_6col", "torch_f32", "torch_f64", "np_f32_antiparallel", "np_f64_parallel",
+            "torch_f32_unnormalised"]
+
+
+@pytest.fixture(scope="module")
+def glue():
+    return np.load(GLUE, allow_pickle=False)
+
+
+def _pn_inputs(glue, case):
+    import torch
+
+    x = glue[f"pn_{case}_x"]
+    return (torch.from_numpy(x.copy()) if case.startswith("torch") else x.copy()), [float(v) for v in
+                                                                                   glue[f"pn_{case}_plane"]]
+
+
+@pytest.mark.parametrize("case", PN_CASES)
+def test_plane_normalize_restatement_vs_reference(glue, case):
+    """np_restate.rotate_to_plane_ref == the reference's PlaneNormalize
+    (processors.py:709-744) on its own recorded outputs: xyz and T bit-equal,
+    in the data's dtype, the anti-parallel normal giving R = I."""
+    data, plane = _pn_inputs(glue, case)
+    xyz, T = NPR.rotate_to_plane_ref(data, plane)
+    xyz = xyz.numpy() if hasattr(xyz, "numpy") else xyz
+    T = T.numpy() if hasattr(T, "numpy") else T
+    assert np.array_equal(xyz, glue[f"pn_{case}_out"][:, :3])
+    assert np.array_equal(T.astype(np.float64), glue[f"pn_{case}_T"])
+    if case.endswith("antiparallel"):
+        assert np.array_equal(T[:3, :3], np.eye(3))
+
+
+@pytest.mark.parametrize("case", PN_CASES)
+def test_plane_normalize_processor_vs_reference(glue, case):
+    """The build's Processors.PlaneNormalize == the reference's on the same
+    inputs: the whole output (extra columns passed through) and forward_T."""
+    from open3dpypro import Processors
+    from open3dpypro.PointCloudMat import PointCloudMat, ShapeType
+
+    data, plane = _pn_inputs(glue, case)
+    st = ShapeType.XYZ if data.shape[1] == 3 else ShapeType.XYZRGB
+    pn = Processors.PlaneNormalize(uuid="PlaneNormalize:glue", detection_uuid="det")
+    out, _ = pn.validate([PointCloudMat(shape_type=st).build(data)], {"det": [plane]})
+    got = out[0].data()
+    got = got.numpy() if hasattr(got, "numpy") else got
+    assert got.dtype == glue[f"pn_{case}_out"].dtype
+    assert np.array_equal(got, glue[f"pn_{case}_out"])
+    assert np.array_equal(np.asarray(pn.forward_T[0], np.float64), glue[f"pn_{case}_T"])
+
+
+def test_plane_detection_flip_ema_restatement_vs_reference(glue):
+    """np_restate.plane_flip_ref + ema_ref == the reference's PlaneDetection
+    CPU branch (processors.py:640-650, 697) given the same segment_plane
+    planes, over 3 frames, at alpha 0.1 and at the default alpha 0 (the
+    published plane then stays [0, 0, 0, 0]); the torch branch's EMA over its
+    own recorded per-frame planes (already d >= 0: the flip leaves them)."""
+    for alpha in (0.1, 0.0):
+        best = [0.0, 0.0, 0.0, 0.0]
+        for i, pl in enumerate(glue["pd_planes"]):
+            best = NPR.ema_ref(best, NPR.plane_flip_ref(pl), alpha)
+            assert np.array_equal(np.asarray(best), glue[f"pd_cpu_meta_alpha{alpha}"][i])
+    best = [0.0, 0.0, 0.0, 0.0]
+    for i, pl in enumerate(glue["pdt_planes"]):
+        pl = pl.astype(np.float32)  # the torch branch's plane is a float32 array: plane * alpha stays float32
+        assert pl[3] >= 0 and np.array_equal(NPR.plane_flip_ref(pl), pl)
+        best = NPR.ema_ref(best, NPR.plane_flip_ref(pl), 0.1)
+        assert np.array_equal(np.asarray(best), glue["pdt_meta_alpha0.1"][i])
+
+
+def test_plane_detection_processor_flip_ema_vs_reference(glue, monkeypatch):
+    """The build's Processors.PlaneDetection flip + EMA == the reference's on
+    the same segment_plane planes (injected on both sides: the RANSAC itself
+    is pinned against the oracle by the GPU suite), 3 frames, alpha 0.1 and
+    0: meta[uuid] bit-equal after every frame."""
+    import torch
+
+    from open3dpypro import Processors, ops, processors
+    from open3dpypro.PointCloudMat import PointCloudMat, ShapeType
+
+    monkeypatch.setattr(processors, "_xyz", lambda a: torch.as_tensor(np.asarray(a))[:, :3].float())
+    for alpha in (0.1, 0.0):
+        it = iter(glue["pd_planes"])
+        monkeypatch.setattr(ops, "segment_plane", lambda *a, **k: (np.asarray(next(it), np.float64), None))
+        pd = Processors.PlaneDetection(uuid="PlaneDetection:glue", distance_threshold=0.01, alpha=alpha, seed=1)
+        frames = glue["pd_frames"]
+        mats = [PointCloudMat(shape_type=ShapeType.XYZ).build(frames[0].copy())]
+        pd.validate(mats, {}, run=False)
+        for i, f in enumerate(frames):
+            meta = {}
+            pd.forward_raw([f.copy()], [], meta)
+            assert np.array_equal(np.asarray(meta[pd.uuid][0]), glue[f"pd_cpu_meta_alpha{alpha}"][i])
+
+
+def test_random_sample_radius_selection_vs_reference(glue):
+    """RandomSample (processors.py:320-365) and RadiusSelection (:367-416):
+    the build's processors on numpy and torch-CPU data, with the reference's
+    seeds, equal the reference's recorded outputs (same RNG draws; the numpy
+    radius branch returns float64 xyz, the torch one every column)."""
+    import torch
+
+    from open3dpypro import Processors
+
+    x = glue["rs_x"]
+    rs = Processors.RandomSample(n_samples=1000)
+    np.random.seed(5)
+    assert np.array_equal(rs.forward_raw([x.copy()])[0], glue["rs_np_out"])
+    torch.manual_seed(5)
+    assert np.array_equal(rs.forward_raw([torch.from_numpy(x.copy())])[0].numpy(), glue["rs_torch_out"])
+    r = float(glue["rsel_radius"])
+    sel = Processors.RadiusSelection(radius=r)
+    got = sel.forward_raw([x.copy()])[0]
+    assert got.dtype == np.float64 and np.array_equal(got, glue["rsel_np_out"])
+    assert np.array_equal(sel.forward_raw([torch.from_numpy(x.copy())])[0].numpy(), glue["rsel_torch_out"])
+    q = x[:, :3].astype(np.float64)  # the restated mask (PointCloud.py:264-265)
+    assert np.array_equal(q[(q[:, 0] ** 2 + q[:, 1] ** 2 + q[:, 2] ** 2) ** 0.5 <= r], glue["rsel_np_out"])

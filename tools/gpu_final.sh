@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-end evidence (r03), in two GPU calls:
-#   bash tools/gpu_final.sh tests   — the full -m gpu suite + smoke()
+# Round-end evidence (ROUND, default r04), in two GPU calls:
+#   bash tools/gpu_final.sh tests   — the full -m gpu suite + smoke(), every normal
+#                                     row's parity logged to profiles-bound gpurun_out/\${R}_parity_report.jsonl
 #   bash tools/gpu_final.sh bench   — PMC passes (profiles/pmc_traffic.json refreshed
 #                                     for bench.py's roofline), the default bench line,
 #                                     and the rocprofv3 kernel trace + stats of the bench
@@ -8,8 +9,10 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-R=${ROUND:-r03}
+R=${ROUND:-r04}
 if [ "$1" = tests ]; then
+  export O3DX_PARITY_LOG=$PWD/gpurun_out/${R}_parity_report.jsonl
+  rm -f "$O3DX_PARITY_LOG"
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > gpurun_out/${R}_gpu_tests.log 2>&1 || { tail -30 gpurun_out/${R}_gpu_tests.log; exit 1; }
   tail -2 gpurun_out/${R}_gpu_tests.log
@@ -26,7 +29,7 @@ import json
 old = json.load(open("profiles/pmc_traffic.json"))
 new = json.load(open("gpurun_out/pmc_summary.json"))
 old["kernels"].update(new["kernels"])
-old["round"] = "r03"
+old["round"] = "r04"
 for p in ("profiles/pmc_traffic.json", "gpurun_out/pmc_traffic.json"):
     with open(p, "w") as f:
         json.dump(old, f, indent=1, sort_keys=True)
