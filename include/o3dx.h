@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define O3DX_ABI_VERSION 3
+#define O3DX_ABI_VERSION 4
 
 #define O3DX_OK 0
 #define O3DX_EIO (-5)
@@ -61,6 +61,8 @@ extern "C" {
  *   [29]     sum d^2         (squared correspondence distances, for inlier_rmse)
  *   [30..31] reserved (0) */
 #define O3DX_ICP_NSUMS 32
+/* length of the ICP target descriptor (doubles) */
+#define O3DX_ICP_DESC_LEN 16
 
 /* ---------------------------------------------------------------- misc */
 int o3dx_abi_version(void);
@@ -411,8 +413,9 @@ int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
  * update = Rz(x2) Ry(x1) Rx(x0) | x[3..5], T <- update * T.
  *
  * o3dx_icp_target_build: builds the persistent target structure (spatial grid
- *   of target points + normals) inside `target_ws`; desc_host (16 doubles)
- *   receives its descriptor, to be passed back to o3dx_icp_accumulate.
+ *   of target points + normals) inside `target_ws`; desc_host
+ *   (O3DX_ICP_DESC_LEN doubles) receives its descriptor, to be passed back to
+ *   o3dx_icp_accumulate / o3dx_icp_register.
  * o3dx_spatial_sort: (n,4) float32 copy of a cloud in a compact spatial order
  *   (grid cells of ~target_occ points, 8x8x8 blocks of cells, Morton order
  *   inside a block), w = bits of the original int32 index.  ICP sources are
@@ -432,6 +435,12 @@ int o3dx_plane_from_moments(const double* sum_xyz_host, int64_t count,
  *   (identity update, as Open3D).
  * o3dx_registration_icp_point_to_plane: the whole Open3D loop on one device
  *   (ws sized by o3dx_registration_icp_workspace_bytes; sorts the source once).
+ * o3dx_icp_register (ABI 4): the same loop on a built target (desc_host) and a
+ *   source as o3dx_icp_accumulate takes it (ws sized by
+ *   o3dx_icp_accumulate_workspace_bytes): every iteration — the fused
+ *   correspondence + moments pass, the solve, T <- update * T and Open3D's
+ *   convergence test — runs on the device, the host waits once.  T is the
+ *   same bits as a host loop of o3dx_icp_accumulate + o3dx_icp_update.
  */
 size_t o3dx_icp_target_workspace_bytes(int64_t nt);
 int o3dx_icp_target_build(const float* tgt_dev, const float* tgt_normals_dev,
@@ -455,6 +464,15 @@ size_t o3dx_spatial_sort_workspace_bytes(int64_t n);
 int o3dx_spatial_sort(const float* xyz_dev, int64_t n, double target_occ,
                       float* sorted4_dev, void* ws, size_t ws_bytes,
                       void* stream);
+int o3dx_icp_register(const float* src_dev, int64_t ns, int src_sorted4,
+                      const void* target_ws, const double* desc_host,
+                      const double* init_host, int max_iteration,
+                      double relative_fitness, double relative_rmse,
+                      double max_correspondence_distance,
+                      const double* src_absmax_host, double* T_out_host,
+                      double* fitness_host, double* inlier_rmse_host,
+                      int32_t* corr_out_dev, int64_t* ncorr_host, void* ws,
+                      size_t ws_bytes, void* stream);
 size_t o3dx_registration_icp_workspace_bytes(int64_t ns);
 int o3dx_registration_icp_point_to_plane(
     const float* src_dev, int64_t ns, const float* tgt_dev,

@@ -6,6 +6,9 @@
 // Per point: neighbour set (grid.hpp), Open3D's raw-moment float64 covariance
 // (ComputeCovariance), FastEigen3x3 smallest eigenvector — both in float64,
 // restated from Open3D geometry/EstimateNormals.cpp, utility/Eigen.cpp.
+#include <type_traits>
+#include <utility>
+
 #include "grid.hpp"
 
 namespace o3dx {
@@ -581,17 +584,20 @@ struct MomAcc {
     for (int j = 0; j < 9; ++j) m[j] = 0.0;
   }
   __device__ void init(const float4&, float, int) {}
-  // Open3D ComputeCovariance cumulant order
+  // Open3D ComputeCovariance cumulant order.  The coordinates are float32
+  // values, so every product is exact in float64 and fma(x, y, m) rounds
+  // exactly as m + x * y: one instruction instead of two (the build keeps
+  // -ffp-contract=off).
   __device__ void add(double x, double y, double z) {
     m[0] += x;
     m[1] += y;
     m[2] += z;
-    m[3] += x * x;
-    m[4] += x * y;
-    m[5] += x * z;
-    m[6] += y * y;
-    m[7] += y * z;
-    m[8] += z * z;
+    m[3] = fma(x, x, m[3]);
+    m[4] = fma(x, y, m[4]);
+    m[5] = fma(x, z, m[5]);
+    m[6] = fma(y, y, m[6]);
+    m[7] = fma(y, z, m[7]);
+    m[8] = fma(z, z, m[8]);
   }
   __device__ void cov(int k, double c[6]) const {
     double u[9];
@@ -841,13 +847,13 @@ struct RegHist {
 // Locate the bin of the k-th distance in a histogram over [lo, hi) with
 // `below` points known below lo.  -> bin edges [*L, *U), *cum = points in the
 // bins before it, *cb = points in it; false when no bin reaches k.
-template <class H>
+template <class H, int NB = kHistBins>
 __device__ __forceinline__ bool hist_locate(const H& hist, int kneed, int below, float lo, float hi,
-                                            float* L, float* U, int* cum, int* cb) {
-  const float bw = (hi - lo) / (float)kHistBins;
+                                            float* L, float* U, int* cum, int* cb, int* bin = nullptr) {
+  const float bw = (hi - lo) / (float)NB;
   int bstar = -1, c0 = 0, cn = 0;
 #pragma unroll
-  for (int b = 0; b < kHistBins; ++b) {
+  for (int b = 0; b < NB; ++b) {
     const int c = hist.count(b);
     if (bstar < 0) {
       if (below + c0 + c >= kneed) {
@@ -860,8 +866,9 @@ __device__ __forceinline__ bool hist_locate(const H& hist, int kneed, int below,
   }
   *cum = c0;
   *cb = cn;
+  if (bin) *bin = bstar;
   *L = lo + (float)bstar * bw;
-  *U = (bstar == kHistBins - 1) ? hi : lo + (float)(bstar + 1) * bw;
+  *U = (bstar == NB - 1) ? hi : lo + (float)(bstar + 1) * bw;
   return bstar >= 0;
 }
 
@@ -956,6 +963,121 @@ __device__ __forceinline__ bool finish_selection(const float4 q, int kneed, int 
         acc.add((double)v.x, (double)v.y, (double)v.z);
       } else {
         umin = fminf(umin, bk[i]);
+      }
+    }
+  }
+  if (need < nb) {
+    const float sep = 1.0f - 4.0f * kRelEps;
+    if (need > 0 && !(kmax < umin * sep)) return false;
+    if (nsel > 0 && !(Lm < umin * sep)) return false;
+  }
+  if (kd2) kd2[oi] = fmaxf(cmax, need > 0 ? kmax : 0.0f) * (1.0f + 4.0f * kRelEps);
+  if (skip_eigen) {  // profiling only (O3DX_TILE_DEBUG=4)
+    out[3 * oi] = (float)(acc.m[3] + acc.m[5] + acc.m[8]);
+    return true;
+  }
+  finish_normal(kneed, acc, prior, oi, out);
+  return true;
+}
+
+// finish_selection for the voxel-table kernel, whose list comes in two parts:
+// rows [0, ns) hold the candidates of the bins at least two below the k-th
+// one (d^2 < L (1 - 2 eps) by construction: certain members, no distance
+// needed), rows [ns, ns + nc) those of the two bins below U (classified by
+// their f32 d^2 as finish_selection does).  The band's (k - #certain) nearest
+// are picked by rank (lower position first among equal keys, as the repeated
+// minimum would), over the wave's longest band only.
+template <int KMAX, class Fetch, class Ident>
+__device__ __forceinline__ bool stile_finish(const float4 q, int kneed, int ns, int nc, float L, float U,
+                                             uint16_t (*lst)[64], int lane, Fetch&& fetch,
+                                             const float* __restrict__ prior, int oi, float* __restrict__ out,
+                                             int32_t* __restrict__ nbr, Ident&& ident, float* __restrict__ kd2,
+                                             bool skip_eigen) {
+  MomAcc acc;
+  acc.zero();
+  int32_t* const nrow = nbr ? nbr + (int64_t)oi * kneed : nullptr;  // test hook
+  for (int j = 0; j < ns; j += 4) {
+    int p[4];
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[u] = (int)lst[min(j + u, ns - 1)][lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = fetch(p[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (j + u < ns) {
+        if (nrow) nrow[j + u] = ident(p[u]);
+        acc.add((double)v[u].x, (double)v[u].y, (double)v[u].z);
+      }
+    }
+  }
+  const int n = ns + nc;
+  int nsel = ns, nb = 0, nU = ns;
+  float cmax = ns > 0 ? L : 0.0f;  // a bound of the certain keys
+  const float Lm = L * (1.0f - 2.0f * kRelEps), Ub = U * (1.0f + 2.0f * kRelEps);
+  for (int j = ns; j < n; j += 4) {
+    int p[4];
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[u] = (int)lst[min(j + u, n - 1)][lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = fetch(p[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (j + u < n) {
+        const float d2f = dist2_f32(q, v[u].x, v[u].y, v[u].z);  // the scan's value, bit for bit
+        nU += d2f < U ? 1 : 0;
+        if (d2f < Lm) {
+          if (nrow && nsel < kneed) nrow[nsel] = ident(p[u]);
+          cmax = fmaxf(cmax, d2f);
+          ++nsel;
+          acc.add((double)v[u].x, (double)v[u].y, (double)v[u].z);
+        } else if (d2f < Ub) {
+          lst[min(nb, kBndCap)][lane] = (uint16_t)p[u];  // rows already read
+          ++nb;
+        }
+      }
+    }
+  }
+  if (nsel > kneed || nb > kBndCap || n < kneed || nU < kneed) return false;
+  const int need = kneed - nsel;
+  // the longest band of the lanes here (ballots see only the active lanes; a
+  // shuffle would read the registers of lanes that left the kernel early):
+  // its bits from the top, nb <= kBndCap < 32
+  int nbm = 0;
+#pragma unroll
+  for (int bit = 4; bit >= 0; --bit)
+    if (__ballot(nb >= (nbm | (1 << bit)))) nbm |= 1 << bit;
+  float bk[kBndCap];
+  int bs[kBndCap];
+#pragma unroll
+  for (int i = 0; i < kBndCap; ++i) {
+    bk[i] = INFINITY;
+    bs[i] = 0;
+    if (i < nbm && i < nb) {
+      bs[i] = (int)lst[i][lane];
+      const float4 v = fetch(bs[i]);
+      bk[i] = dist2_f32(q, v.x, v.y, v.z);
+    }
+  }
+  float kmax = -1.0f, umin = INFINITY;
+  int nput = nsel;
+#pragma unroll
+  for (int i = 0; i < kBndCap; ++i) {
+    if (i < nbm) {
+      int rank = 0;
+#pragma unroll
+      for (int j = 0; j < kBndCap; ++j)
+        if (j != i && j < nbm) rank += (j < i ? bk[j] <= bk[i] : bk[j] < bk[i]) ? 1 : 0;
+      if (i < nb) {
+        if (rank < need) {
+          kmax = fmaxf(kmax, bk[i]);
+          const float4 v = fetch(bs[i]);
+          if (nrow) nrow[nput++] = ident(bs[i]);
+          acc.add((double)v.x, (double)v.y, (double)v.z);
+        } else {
+          umin = fminf(umin, bk[i]);
+        }
       }
     }
   }
@@ -1340,59 +1462,88 @@ __device__ __forceinline__ float4 dvox_load(const DenseVox& d, int x, int y, int
   return v;
 }
 
-// f(slot, d2) over L consecutive slots from st: pairs in packed f32, one single.
-// x, y interleaved (one ds_read2_b64 per pair), z apart: two LDS reads per
-// pair instead of three, the same 12 bytes per slot.
-// The row's loads are all issued before its first f (whose LDS atomics /
-// stores the compiler cannot move reads across).
-// VX: each slot's (x, y) by its own ds_read_b64 (2 LDS cycles, 64 banks per
-// 32-lane half) instead of the pairs the compiler merges into ds_read2_b64 (8
-// cycles, 32 banks; MI355X_MICROARCH.md §LDS): a volatile load is never merged.
-template <int L, bool VX, class F>
+// Candidates are numbered in stencil order (row by row, ascending slot within
+// a row); a scan body receives that number as a compile-time constant.
+template <int C>
+using IC = std::integral_constant<int, C>;
+template <class St>
+constexpr int stencil_prefix(int I) {
+  int s = 0;
+  for (int r = 0; r < I; ++r) s += St::rows[r].len;
+  return s;
+}
+template <class St>
+constexpr int stencil_cands() {
+  return stencil_prefix<St>(St::N);
+}
+
+template <int C0, class F, int... I>
+__device__ __forceinline__ void run_bodies(F& f, int st, const float* d2, std::integer_sequence<int, I...>) {
+  (f(IC<C0 + I>{}, st + I, d2[I]), ...);
+}
+
+// f(IC<candidate>, slot, d2) over the L consecutive slots of a row from st.
+// x, y interleaved (each slot's pair by its own ds_read_b64: a volatile load
+// is never merged into the 8-cycle ds_read2_b64, MI355X_MICROARCH.md §LDS), z
+// apart.  The row's loads are all issued before its first f (whose LDS atomics
+// the compiler cannot move reads across).  Distances in plain f32 (v_fma_f32:
+// 2 cycles per wave64 instruction, where v_pk_fma_f32 takes 4 and the packing
+// costs lane moves; grid.o is built without the SLP vectorizer).
+template <int L, int C0, class F>
 __device__ __forceinline__ void scan_run(const float2* txy, const float* tz, int st, const float4 q, F& f) {
   float2 a[L];
   float c[L];
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    if constexpr (VX) {
-      typedef __attribute__((address_space(3))) const volatile f32x2 lds_vf2;
-      const f32x2 v = *(lds_vf2*)(&txy[st + i]);
-      a[i] = make_float2(v.x, v.y);
-    } else
-      a[i] = txy[st + i];
+    typedef __attribute__((address_space(3))) const volatile f32x2 lds_vf2;
+    const f32x2 v = *(lds_vf2*)(&txy[st + i]);
+    a[i] = make_float2(v.x, v.y);
     c[i] = tz[st + i];
   }
+  float d2[L];
 #pragma unroll
-  for (int i = 0; i + 1 < L; i += 2) {
-    const f32x2 dd = dist2_pair(q, (f32x2){a[i].x, a[i + 1].x}, (f32x2){a[i].y, a[i + 1].y}, (f32x2){c[i], c[i + 1]});
-    f(st + i, dd.x);
-    f(st + i + 1, dd.y);
-  }
-  if (L & 1) f(st + L - 1, dist2_f32(q, a[L - 1].x, a[L - 1].y, c[L - 1]));
+  for (int i = 0; i < L; ++i) d2[i] = dist2_f32(q, a[i].x, a[i].y, c[i]);
+  run_bodies<C0>(f, st, d2, std::make_integer_sequence<int, L>{});
 }
 
 // a scheduling fence per row keeps the unrolled stencil from hoisting every
 // row's loads (register pressure; the other waves hide the LDS latency)
-template <class St, int I, bool VX, class F>
+template <class St, int I, class F>
 __device__ __forceinline__ void mir_rows(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
                                          const float4 q, F& f) {
   if constexpr (I < St::N) {
     constexpr SRow r = St::rows[I];
-    scan_run<r.len, VX>(txy, tz, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)), q, f);
+    scan_run<r.len, stencil_prefix<St>(I)>(txy, tz, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)),
+                                           q, f);
     __builtin_amdgcn_sched_barrier(0);
-    mir_rows<St, I + 1, VX>(txy, tz, qs, SY, SZ, xpos, q, f);
+    mir_rows<St, I + 1>(txy, tz, qs, SY, SZ, xpos, q, f);
   }
 }
 
 // The lane's stencil: qs = its own slot, SY / SZ = the y / z slot strides
 // signed by the orientation, xpos = x orientation.
-template <class St, bool VX, class F>
+template <class St, class F>
 __device__ __forceinline__ void stencil_scan(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
                                              const float4 q, F&& f) {
   // the row bases are recomputed per scan (laundered inputs): hoisted and
   // shared across the kernel's scans they would stay live throughout
   asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
-  mir_rows<St, 0, VX>(txy, tz, qs, SY, SZ, xpos, q, f);
+  mir_rows<St, 0>(txy, tz, qs, SY, SZ, xpos, q, f);
+}
+
+// The same stencil walk without loads: f(IC<candidate>, slot).
+template <int C0, class F, int... I>
+__device__ __forceinline__ void walk_bodies(F& f, int st, std::integer_sequence<int, I...>) {
+  (f(IC<C0 + I>{}, st + I), ...);
+}
+template <class St, int I, class F>
+__device__ __forceinline__ void walk_rows(int qs, int SY, int SZ, bool xpos, F& f) {
+  if constexpr (I < St::N) {
+    constexpr SRow r = St::rows[I];
+    walk_bodies<stencil_prefix<St>(I)>(f, qs + r.dy * SY + r.dz * SZ + (xpos ? r.xa : -(r.xa + r.len - 1)),
+                                       std::make_integer_sequence<int, r.len>{});
+    walk_rows<St, I + 1>(qs, SY, SZ, xpos, f);
+  }
 }
 
 // Block shape: WY x WZ waves, each wave a 4^3 voxel block; the block's box is
@@ -1414,8 +1565,125 @@ struct StileShape {
   static constexpr int CELLS = SZ * EZ;     // LDS slots (padded planes)
 };
 
+// The count scan's histogram: 16 slots per lane — 0 below the range, 1..14
+// the bins, 15 at or above it — so a candidate's slot fits a nibble.
+constexpr int kStileBins = 14;
+constexpr int kStileSlots = kStileBins + 2;
+struct StileHist {
+  uint32_t h[kStileSlots];
+  __device__ __forceinline__ int count(int b) const { return (int)h[b + 1]; }  // b in -1..kStileBins
+};
+
+// Count scan + list of one lane (stencil St):
+//   count   f32 d^2 of the stencil's candidates into the histogram over
+//           [lo, hi) (LDS counters, one bank column per lane), each
+//           candidate's level-0 slot kept as a nibble in registers (nib);
+//   locate  the bin b0 holding the k-th distance -> [L, U) (refined, rarely,
+//           by rescans over [L, U));
+//   list    the candidates whose level-0 slot is <= b0 + 1, appended to the
+//           lane's LDS list without a second distance scan.
+// The slot of d^2 is floor(fma(d^2, sc, off)) with an absolute error below
+// 2^-18.6 bins, and [lo, hi) sits at >= 1.5 voxels, so every candidate below
+// U (1 - 2^-17) has slot <= b0 + 1: the list holds every candidate below the
+// finish's band bound U' (1 + 2 eps) for U' = U (1 - 2^-16), passed out as *U.
+// Returns false when the lane hands its query on.
+template <class St, class LST>
+__device__ __forceinline__ bool stile_count_list(const float2* txy, const float* tz, int qs, int SY, int SZ, bool xpos,
+                                                 const float4 q, int kneed, float lo, float hi, uint32_t* hw, LST lst,
+                                                 int lane, int kListMax, int dbg, const DenseVox& d, int* ns_out,
+                                                 int* nc_out, float* L_out, float* U_out) {
+  constexpr int kC = stencil_cands<St>();
+  uint32_t nib[(kC + 7) / 8];
+  uint32_t* const hl = hw + lane;  // this lane's counter column: slot s at hl[64 s]
+  StileHist th;
+#pragma unroll
+  for (int i = 0; i < kStileSlots; ++i) hl[i * 64] = 0u;
+  {
+    const float sc_ = (float)kStileBins / (hi - lo), off_ = 1.0f - lo * sc_;
+    auto body = [&](auto ci, int, float d2) {
+      constexpr int c = decltype(ci)::value;
+      const int ix = (int)__builtin_amdgcn_fmed3f(fmaf(d2, sc_, off_), 0.0f, (float)(kStileSlots - 1));
+      atomicAdd(&hl[ix * 64], 1u);
+      if constexpr ((c & 7) == 0)
+        nib[c >> 3] = (uint32_t)ix;
+      else
+        nib[c >> 3] |= (uint32_t)ix << (4 * (c & 7));
+      // packed here, not at the list walk (the compiler would keep every
+      // candidate's slot live until then)
+      asm volatile("" : "+v"(nib[c >> 3]));
+    };
+    stencil_scan<St>(txy, tz, qs, SY, SZ, xpos, q, body);
+  }
+#pragma unroll
+  for (int i = 0; i < kStileSlots; ++i) th.h[i] = hl[i * 64];
+  int total = th.count(-1);
+#pragma unroll
+  for (int i = 0; i < kStileBins; ++i) total += th.count(i);
+  // the k-th beyond R (or below the histogram's range): handed on
+  if (total < kneed || th.count(-1) >= kneed) {
+    if (d.stats) atomicAdd(&d.stats[7], 1ull);
+    return false;
+  }
+  float L, U;
+  int cum, cb, b0;
+  if (!hist_locate<StileHist, kStileBins>(th, kneed, th.count(-1), lo, hi, &L, &U, &cum, &cb, &b0)) return false;
+  uint32_t h0[kStileSlots];
+#pragma unroll
+  for (int i = 0; i < kStileSlots; ++i) h0[i] = th.h[i];
+  // refinement (a bin holding more than kRefineAt points): rescans re-bin [L, U)
+  for (int lvl = 1; cb > kRefineAt && lvl <= kMaxRefine && U > L; ++lvl) {
+    lo = L;
+    hi = U;
+#pragma unroll
+    for (int i = 0; i < kStileSlots; ++i) hl[i * 64] = 0u;
+    const float sc_ = (float)kStileBins / (hi - lo), off_ = 1.0f - lo * sc_;
+    auto body = [&](auto, int, float d2) {
+      const int ix = (int)__builtin_amdgcn_fmed3f(fmaf(d2, sc_, off_), 0.0f, (float)(kStileSlots - 1));
+      atomicAdd(&hl[ix * 64], 1u);
+    };
+    stencil_scan<St>(txy, tz, qs, SY, SZ, xpos, q, body);
+#pragma unroll
+    for (int i = 0; i < kStileSlots; ++i) th.h[i] = hl[i * 64];
+    const int below = th.count(-1);
+    if (!hist_locate<StileHist, kStileBins>(th, kneed, below, lo, hi, &L, &U, &cum, &cb)) return false;
+  }
+  *L_out = L;
+  *U_out = U * (1.0f - 1.52587890625e-05f);  // U (1 - 2^-16)
+  if (dbg == 2) return true;
+  // the list: level-0 slots <= b0 + 1 (b0 0-based; slot = bin + 1), as many
+  // as the level-0 counts say, in two parts: slots < b0 (bins at least two
+  // below the k-th: certain members) in rows [0, ns), slots b0 and b0 + 1 in
+  // rows [ns, ns + nc).  The histogram's LDS is free again (its counts are in
+  // h0).
+  const uint32_t lim = (uint32_t)b0 + 1u, sure = (uint32_t)b0;
+  int ns = 0, nc = 0;
+#pragma unroll
+  for (int i = 0; i < kStileSlots; ++i) {
+    ns += (uint32_t)i < sure ? (int)h0[i] : 0;
+    nc += (uint32_t)i >= sure && (uint32_t)i <= lim ? (int)h0[i] : 0;
+  }
+  *ns_out = ns;
+  *nc_out = nc;
+  if (ns + nc > kListMax) return true;  // the caller hands the query on
+  uint16_t* ws = &lst[0][lane];
+  uint16_t* wc = &lst[ns][lane];
+  auto conv = [&](auto ci, int slot) {
+    constexpr int c = decltype(ci)::value;
+    const uint32_t v = (nib[c >> 3] >> (4 * (c & 7))) & 15u;
+    if (v <= lim) {
+      const bool s_ = v < sure;
+      *(s_ ? ws : wc) = (uint16_t)slot;
+      ws += s_ ? 64 : 0;
+      wc += s_ ? 0 : 64;
+    }
+  };
+  asm volatile("" : "+v"(qs), "+v"(SY), "+v"(SZ));
+  walk_rows<St, 0>(qs, SY, SZ, xpos, conv);
+  return true;
+}
+
 // WPE: waves per SIMD to register-allocate for (LDS allows 3 for 2x2)
-template <int KMAX, int WY, int WZ, int WPE, bool VX>
+template <int KMAX, int WY, int WZ, int WPE>
 __global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
                 int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
@@ -1423,11 +1691,11 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::CELLS;
   __shared__ float2 txy[kSlots];
   __shared__ float tz[kSlots];
-  // list capacity: the k - 1 points below the k-th bin + that bin (<= kRefineAt
-  // after refinement) + the rounding band
+  // list capacity: the k - 1 points below the k-th bin + that bin and the next
+  // (<= kRefineAt each after refinement) + the rounding band
   constexpr int kListMax = KMAX + kBndCap;
   constexpr int kListWords = ((kListMax + 1) * 64 * (int)sizeof(uint16_t) + 3) / 4;
-  constexpr int kHistWords = kTileSlots * 64;
+  constexpr int kHistWords = kStileSlots * 64;
   constexpr int kSelWords = kListWords > kHistWords ? kListWords : kHistWords;
   __shared__ uint32_t selbuf[Sh::NW][kSelWords];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1481,76 +1749,25 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   const bool wide = wx0 < kEdge || wy0 < kEdge || wz0 < kEdge || wx0 + kVB > d.nx - kEdge ||
                     wy0 + kVB > d.ny - kEdge || wz0 + kVB > d.nz - kEdge;
   float L = 0.f, U = 0.f;
+  int ns = 0, nc = 0;
   if (!fb) {
-    const float R2 = wide ? d.rw2 : d.rc2;
-    TileHist th;
-    float lo = d.hlo2, hi = R2;
-    for (int lvl = 0;; ++lvl) {
-      // histogram over [lo, hi): slot = bin + 1 (0: below lo, 17: at or above hi);
-      // the +1 rides in the fma
-#pragma unroll
-      for (int i = 0; i < kTileSlots; ++i) hw[i * 64 + lane] = 0u;
-      const float sc_ = (float)kHistBins / (hi - lo), off_ = 1.0f - lo * sc_;
-      auto body = [&](int, float d2) {
-        const int ix = (int)__builtin_amdgcn_fmed3f(fmaf(d2, sc_, off_), 0.0f, 17.0f);
-        atomicAdd(&hw[ix * 64 + lane], 1u);
-      };
-      if (wide)
-        stencil_scan<Stencil245, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
-      else
-        stencil_scan<Stencil220, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
-#pragma unroll
-      for (int i = 0; i < kTileSlots; ++i) th.h[i] = hw[i * 64 + lane];
-      if (lvl == 0) {
-        int total = th.count(-1);
-#pragma unroll
-        for (int i = 0; i < kHistBins; ++i) total += th.count(i);
-        // the k-th beyond R (or below the histogram's range): handed on
-        fb = total < kneed || th.count(-1) >= kneed;
-        if (fb) {
-          if (d.stats) atomicAdd(&d.stats[7], 1ull);
-          break;
-        }
-      }
-      int cum, cb;
-      if (!hist_locate(th, kneed, th.count(-1), lo, hi, &L, &U, &cum, &cb)) {
-        fb = true;
-        break;
-      }
-      if (cb <= kRefineAt || lvl == kMaxRefine || !(U > L)) break;
-      lo = L;
-      hi = U;
-    }
+    if (wide)
+      fb = !stile_count_list<Stencil245>(txy, tz, qs, SY, SZ, xpos, q, kneed, d.hlo2, d.rw2, hw, lst, lane, kListMax,
+                                         dbg, d, &ns, &nc, &L, &U);
+    else
+      fb = !stile_count_list<Stencil220>(txy, tz, qs, SY, SZ, xpos, q, kneed, d.hlo2, d.rc2, hw, lst, lane, kListMax,
+                                         dbg, d, &ns, &nc, &L, &U);
   }
-  if (dbg == 2) {
-    if (L == 12345.f) out[0] = 0.f;
+  if (dbg == 2 || dbg == 3) {
+    if (ns + nc == 12345 || L == 12345.f) out[0] = 0.f;  // profiling only: keep the scans alive
     return;
   }
-  const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
-  // the wave's list stencil: the smallest that covers every lane's Up
-  const int lsel = wide ? 2 : __ballot(!fb && !(Up < d.rl2)) == 0 ? 0 : 1;
   if (!fb) {
-    int n = 0;
-    auto body = [&](int pp, float d2) {
-      if (d2 < Up) {  // masked store: only the accepted lanes take part in the LDS banking
-        lst[min(n, kListMax)][lane] = (uint16_t)pp;
-        ++n;
-      }
-    };
-    if (lsel == 0)
-      stencil_scan<Stencil210, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
-    else if (lsel == 1)
-      stencil_scan<Stencil220, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
-    else
-      stencil_scan<Stencil245, VX>(txy, tz, qs, SY, SZ, xpos, q, body);
-    if (dbg == 3) {
-      if (n == 12345) out[0] = 0.f;
-      return;
-    }
-    if (n > kListMax && d.stats) atomicAdd(&d.stats[5], 1ull);
-    fb = n > kListMax ||
-         !finish_selection<KMAX>(
-             q, kneed, n, Lm, U, lst, lane,
+    const bool over = ns + nc > kListMax;
+    if (over && d.stats) atomicAdd(&d.stats[5], 1ull);
+    fb = over ||
+         !stile_finish<KMAX>(
+             q, kneed, ns, nc, L, U, lst, lane,
              [&](int p) { return make_float4(txy[p].x, txy[p].y, tz[p], 0.f); }, prior, oi, out, d.nbr,
              [&](int p) {
                const int bz_ = p / kSZ, r = p - bz_ * kSZ, by_ = r / kSY, bx_ = r - by_ * kSY;
@@ -2217,12 +2434,8 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
       // O3DX_TILE_DEBUG=1/2/3/4: stop after staging / histogram / list scan / moments (profiling only)
       const char* dbg = getenv("O3DX_TILE_DEBUG");
       const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
-      if (env_int("O3DX_STILE_VX", 1))
-        hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3, true>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d,
-                           kneed, prior, out, list, lens, ffb, dg);
-      else
-        hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3, false>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d,
-                           kneed, prior, out, list, lens, ffb, dg);
+      hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d, kneed,
+                         prior, out, list, lens, ffb, dg);
     }
     // the table as a dense GridView (identity cell starts, <= 1 point per cell)
     GridView g{};

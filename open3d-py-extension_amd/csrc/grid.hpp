@@ -264,7 +264,7 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
 // (y, z) rows (below); else by Chebyshev shells of cells.
 template <bool ROWS = true>
 __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, double qy, double qz, double radius,
-                                             double* best_d2, int* best_pos) {
+                                             double* best_d2, int* best_pos, int prior = -1) {
   double bd = INFINITY;
   int bi = -1, bp = -1;
   if (g.n == 0) {
@@ -319,7 +319,14 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
     }
     for_points4(g, p0, p1, visit_point);
   };
-  visit_cell(cx, cy, cz);
+  // prior: a target position to start from (the previous ICP iteration's
+  // match; any real point gives a valid bound, the result is the same)
+  if (prior >= 0) visit_point(prior, g.pts[prior]);
+  bool own_seen = false;
+  if (bi < 0) {
+    visit_cell(cx, cy, cz);
+    own_seen = true;
+  }
   if (bi >= 0) {
     // A match in the own cell bounds the search: every better point lies in
     // the ball of radius sqrt(thr) (+ the assignment slack), so only the
@@ -334,7 +341,7 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
       for (int z = z0; z <= z1; ++z)
         for (int y = y0; y <= y1; ++y)
           for (int x = x0; x <= x1; ++x)
-            if (x != cx || y != cy || z != cz) visit_cell(x, y, z);
+            if (!own_seen || x != cx || y != cy || z != cz) visit_cell(x, y, z);
       search_stats(g, st_cells, st_cands, 2);
       *best_d2 = bd;
       *best_pos = bp;

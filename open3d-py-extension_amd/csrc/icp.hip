@@ -7,55 +7,276 @@
 // (PointToPlane::ComputeTransformation), utility/Eigen.cpp (ComputeJTJandJTr,
 // SolveJacobianSystemAndObtainExtrinsicMatrix, TransformVector6dToMatrix4d).
 //
-// One fused pass per iteration: transform the float32 source by the float64
-// cumulative T, nearest target within max_corr (target grid), residual
-// r = (vs - vt).nt, J = [vs x nt ; nt], and a fixed-order float64 reduction
-// of the 29 moments (21 JTJ + 6 JTr + r^2 + count, plus sum d^2) — per-lane,
-// wave xor-tree, block, then block partials in block order.  The 6x6 solve
-// and the loop stay on the host (float64 LDLT with diagonal pivoting).
+// One pass per iteration (k_icp_step): transform the float32 source by the
+// float64 cumulative T, nearest target within max_corr (target grid), residual
+// r = (vs - vt).nt, J = [vs x nt ; nt], and the 30 moments (21 JTJ + 6 JTr +
+// r^2 + count + sum d^2) as exact fx integers, reduced across the wave while
+// the matched target point and normal are still in registers: no second pass
+// re-gathers them.  The loop itself runs on the device: k_icp_finish sums the
+// block partials, forms fitness / rmse, tests convergence, solves the 6x6
+// system (LDLT with diagonal pivoting) and updates T, so the host enqueues all
+// iterations and waits once.  The solve is one __host__ __device__ function
+// (the build has -ffp-contract=off; division and sqrt are correctly rounded on
+// both sides; sin / cos are the library's own), so the host loop of a sharded
+// source (distributed.py, o3dx_icp_update) reaches the same T to the bit.
+#include <cfloat>
 #include <vector>
+
+#include <type_traits>
+#include <utility>
 
 #include "grid.hpp"
 
 namespace o3dx {
 
-constexpr int kIcpBlocks = 1024;
-constexpr int kNS = O3DX_ICP_NSUMS;
+constexpr int kNS = O3DX_ICP_NSUMS;  // 32 sums: 30 used
+template <int C>
+using IC = std::integral_constant<int, C>;
+constexpr int kNT = 30;
+constexpr int kIcpCopies = 128;  // copies of the digit accumulator (spread the block atomics)
+
+#define O3DX_HD __host__ __device__
+
+// ----------------------------------------------- float64 math, host = device
+// sin and cos of x: Cody-Waite reduction by pi/2 (three-part constant, exact
+// products for |x| < 2^20 pi/2) and the fdlibm kernels on [-pi/4, pi/4]
+// (within an ulp or so of the correctly rounded value).  The same operations
+// on the host and on the device give the same bits.
+O3DX_HD inline void det_sincos(double x, double* s, double* c) {
+  const double inv_pio2 = 6.36619772367581382433e-01;
+  const double pio2_1 = 1.57079632673412561417e+00, pio2_2 = 6.07710050630396597660e-11,
+               pio2_3 = 2.02226624871116645580e-21;
+  const double fn = rint(x * inv_pio2);
+  const double r = ((x - fn * pio2_1) - fn * pio2_2) - fn * pio2_3;
+  const double z = r * r, w = z * z;
+  // __sin / __cos (fdlibm, musl)
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
+               S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
+               C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double rs = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
+  const double sv = r + (z * r) * (S1 + z * rs);
+  const double rc = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+  const double hz = 0.5 * z, wc = 1.0 - hz;
+  const double cv = wc + (((1.0 - wc) - hz) + z * rc);
+  const int n = (int)(((long long)fn) & 3);
+  switch (n) {
+    case 0: *s = sv; *c = cv; break;
+    case 1: *s = cv; *c = -sv; break;
+    case 2: *s = -sv; *c = -cv; break;
+    default: *s = -cv; *c = sv; break;
+  }
+}
+
+O3DX_HD inline bool finite_d(double v) { return v == v && v <= DBL_MAX && v >= -DBL_MAX; }
+
+// 6x6 LDLT with diagonal pivoting.  Every loop is unrolled with constant
+// indices and the pivot's row / column exchange is a per-entry select, so on
+// the device A stays in registers (a dynamically indexed private array would
+// live in scratch); the exchanges are exact moves, the arithmetic is the same
+// operations in the same order on the host and the device.
+O3DX_HD inline bool ldlt_solve6(const double A_in[36], const double b_in[6], double x[6]) {
+  constexpr int n = 6;
+  double A[36];
+#pragma unroll
+  for (int i = 0; i < 36; ++i) A[i] = A_in[i];
+  int perm[6] = {0, 1, 2, 3, 4, 5};
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    int piv = k;
+    double best = fabs(A[k * n + k]);
+#pragma unroll
+    for (int i = k + 1; i < n; ++i)
+      if (fabs(A[i * n + i]) > best) {
+        best = fabs(A[i * n + i]);
+        piv = i;
+      }
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const bool sw = piv == i;
+#pragma unroll
+      for (int j = 0; j < n; ++j) {  // rows k and i
+        const double a = A[k * n + j], c = A[i * n + j];
+        A[k * n + j] = sw ? c : a;
+        A[i * n + j] = sw ? a : c;
+      }
+#pragma unroll
+      for (int r = 0; r < n; ++r) {  // columns k and i
+        const double a = A[r * n + k], c = A[r * n + i];
+        A[r * n + k] = sw ? c : a;
+        A[r * n + i] = sw ? a : c;
+      }
+      const int pk = perm[k], pi = perm[i];
+      perm[k] = sw ? pi : pk;
+      perm[i] = sw ? pk : pi;
+    }
+    const double dk = A[k * n + k];
+    double col[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) col[i] = A[i * n + k];
+#pragma unroll
+    for (int i = k + 1; i < n; ++i)
+#pragma unroll
+      for (int j = k + 1; j < n; ++j) A[i * n + j] -= dk != 0 ? col[i] * col[j] / dk : 0.0;
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) A[i * n + k] = dk != 0 ? col[i] / dk : 0.0;
+  }
+  double y[6];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    double v = b_in[0];
+#pragma unroll
+    for (int t = 1; t < n; ++t) v = perm[i] == t ? b_in[t] : v;
+    y[i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i)
+#pragma unroll
+    for (int j = 0; j < i; ++j) y[i] -= A[i * n + j] * y[j];
+#pragma unroll
+  for (int i = 0; i < n; ++i) y[i] = fabs(A[i * n + i]) > DBL_MIN ? y[i] / A[i * n + i] : 0.0;
+#pragma unroll
+  for (int i = n - 1; i >= 0; --i)
+#pragma unroll
+    for (int j = i + 1; j < n; ++j) y[i] -= A[j * n + i] * y[j];
+#pragma unroll
+  for (int t = 0; t < n; ++t) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) v = perm[i] == t ? y[i] : v;
+    x[t] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i)
+    if (!finite_d(x[i])) return false;
+  return true;
+}
+
+// TransformVector6dToMatrix4d: R = Rz(x2) Ry(x1) Rx(x0), t = x[3..5]
+O3DX_HD inline void vec6_to_mat4(const double x[6], double T[16]) {
+  double sa, ca, sb, cb, sg, cg;
+  det_sincos(x[0], &sa, &ca);
+  det_sincos(x[1], &sb, &cb);
+  det_sincos(x[2], &sg, &cg);
+  const double Rz[9] = {cg, -sg, 0, sg, cg, 0, 0, 0, 1};
+  const double Ry[9] = {cb, 0, sb, 0, 1, 0, -sb, 0, cb};
+  const double Rx[9] = {1, 0, 0, 0, ca, -sa, 0, sa, ca};
+  double A[9], R[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      A[i * 3 + j] = (Rz[i * 3] * Ry[j] + Rz[i * 3 + 1] * Ry[3 + j]) + Rz[i * 3 + 2] * Ry[6 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[i * 3 + j] = (A[i * 3] * Rx[j] + A[i * 3 + 1] * Rx[3 + j]) + A[i * 3 + 2] * Rx[6 + j];
+  for (int i = 0; i < 16; ++i) T[i] = 0;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) T[i * 4 + j] = R[i * 3 + j];
+    T[i * 4 + 3] = x[3 + i];
+  }
+  T[15] = 1;
+}
+
+O3DX_HD inline void mat4_mul(const double* A, const double* B, double* C) {
+  double t[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      t[i * 4 + j] =
+          ((A[i * 4] * B[j] + A[i * 4 + 1] * B[4 + j]) + A[i * 4 + 2] * B[8 + j]) + A[i * 4 + 3] * B[12 + j];
+  for (int i = 0; i < 16; ++i) C[i] = t[i];
+}
+
+O3DX_HD inline int solve_update(const double* sums, double* upd) {
+  double JTJ[36], mb[6], x[6];
+  int t = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int b = a; b < 6; ++b) {
+      JTJ[a * 6 + b] = sums[t];
+      JTJ[b * 6 + a] = sums[t];
+      ++t;
+    }
+  for (int a = 0; a < 6; ++a) mb[a] = -sums[21 + a];
+  if (sums[28] <= 0.0 || !ldlt_solve6(JTJ, mb, x)) {
+    for (int a = 0; a < 16; ++a) upd[a] = (a % 5 == 0) ? 1.0 : 0.0;
+    return 0;
+  }
+  vec6_to_mat4(x, upd);
+  return 1;
+}
+
+O3DX_HD inline int fx_exp_hd(double B) {
+  int e = 0;
+  const double b = (B > 0.0 && B <= DBL_MAX) ? fmax(B, ldexp(1.0, -900)) : 1.0;
+  frexp(b, &e);
+  return e - kFxBits;
+}
+
+// fx exponents of the sums (common.hpp) from bounds that every rank derives
+// alike — the source's |x|,|y|,|z| bounds (the whole source's, on every rank),
+// T and max_correspondence_distance:
+//   |p|  <= Pn = |(|T| absmax + |t|)| (row bounds of T (x,y,z,1), Euclidean)
+//   |J_a| <= Pn |n| (a < 3), |n_a| (a >= 3), |n| <= 1.01 (float32 unit normal)
+//   |r| = |(p - vt).n| <= d |n| < max_corr |n|,  d^2 < max_corr^2
+// (1.01: margin for float rounding; a looser bound only coarsens the quantum).
+O3DX_HD inline void icp_fx_exps(const double absmax[3], const double* T, double max_corr, int q[kNS]) {
+  double P2 = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    const double Pi =
+        ((fabs(T[4 * i]) * absmax[0] + fabs(T[4 * i + 1]) * absmax[1]) + fabs(T[4 * i + 2]) * absmax[2]) +
+        fabs(T[4 * i + 3]);
+    P2 += Pi * Pi;
+  }
+  const double pn = sqrt(P2) * 1.01;
+  double bJ[6];
+  for (int a = 0; a < 6; ++a) bJ[a] = (a < 3 ? pn : 1.0) * 1.01;
+  const double br = max_corr * 1.01 * 1.01;
+  int k = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int b = a; b < 6; ++b) q[k++] = fx_exp_hd(bJ[a] * bJ[b] * 1.01);
+  for (int a = 0; a < 6; ++a) q[21 + a] = fx_exp_hd(bJ[a] * br * 1.01);
+  q[27] = fx_exp_hd(br * br * 1.01);
+  q[28] = fx_exp_hd(1.0);
+  q[29] = fx_exp_hd(max_corr * max_corr * 1.01);
+  q[30] = q[31] = 0;
+}
+
+// The exact value of a {lo, hi} digit sum (lo >= 0) scaled by 2^q, correctly
+// rounded once: the carry of lo moves into hi (|hi| < 2^53), then
+// hi 2^32 + lo is one rounded addition of two exact doubles — the same value
+// as core.hip's fx_to_double (__int128), on the host and on the device.
+O3DX_HD inline double fx_value(int64_t lo, int64_t hi, int q) {
+  const int64_t h = hi + (lo >> 32);
+  const int64_t l = lo & 0xffffffffll;
+  return ldexp(ldexp((double)h, 32) + (double)l, q);
+}
+
+O3DX_HD inline void icp_metrics(const double* sums, int64_t ns, double* fit, double* rm) {
+  const double c = sums[28];
+  if (c <= 0 || ns == 0) {
+    *fit = 0;
+    *rm = 0;
+  } else {
+    *fit = c / (double)ns;
+    *rm = sqrt(sums[29] / c);
+  }
+}
+
+// The device-resident state of one accumulate / registration.
+struct IcpState {
+  double T[16];
+  double absmax[3];
+  double sums[kNS];   // the last accumulate's
+  double fit, rmse;
+  int32_t q[kNS];
+  int32_t done;   // the loop has converged: later steps and finishes return at once
+  int32_t iters;  // updates applied
+};
+
+O3DX_HD inline void state_set_T(IcpState& st, const double* T, double max_corr) {
+  for (int i = 0; i < 16; ++i) st.T[i] = T[i];
+  icp_fx_exps(st.absmax, st.T, max_corr, st.q);
+}
 
 struct Mat4 {
   double m[16];
-};
-
-// One correspondence -> its 30 float64 moment terms: r = (vs - vt).nt,
-// J = [vs x nt ; nt] (Open3D ComputeJTJandJTr order), plus count and d^2.
-constexpr int kNT = 30;
-
-__device__ __forceinline__ void icp_terms(double t[kNT], double px, double py, double pz, const float4 vt,
-                                          const float4 nt, double d2) {
-  const double nx = nt.x, ny = nt.y, nz = nt.z;
-  const double r = ((px - (double)vt.x) * nx + (py - (double)vt.y) * ny) + (pz - (double)vt.z) * nz;
-  double J[6];
-  J[0] = py * nz - pz * ny;
-  J[1] = pz * nx - px * nz;
-  J[2] = px * ny - py * nx;
-  J[3] = nx;
-  J[4] = ny;
-  J[5] = nz;
-  int k = 0;
-#pragma unroll
-  for (int a = 0; a < 6; ++a)
-#pragma unroll
-    for (int b = a; b < 6; ++b) t[k++] = J[a] * J[b];
-#pragma unroll
-  for (int a = 0; a < 6; ++a) t[21 + a] = J[a] * r;
-  t[27] = r * r;
-  t[28] = 1.0;
-  t[29] = d2;
-}
-
-// fx scales (2^-q) of the 30 sums, from bounds every rank derives alike
-struct FxScales {
-  double s[kNT];
 };
 
 // Source point j -> (original index, float64 position under T).  SORTED: src
@@ -87,56 +308,284 @@ __device__ __forceinline__ int64_t icp_source(const float* __restrict__ src, int
   return i;
 }
 
-// Pass 1 — correspondences: one thread per source point, the 1-NN within
-// max_correspondence_distance (nn_search_dev); writes the target's sorted
-// position (-1: none) and, when asked, the target's original index by source
-// index.  No accumulators live here, so the search runs at full occupancy
-// (the search is latency-bound: many waves hide the dependent cell loads).
-// ROWS: the search beyond the own cell walks (y, z) rows (nn_search_dev).
-template <bool SORTED, bool ROWS>
-__global__ void __launch_bounds__(kBlock) k_icp_match(const float* __restrict__ src, int64_t ns, GridView g, Mat4 T,
-                                                      double radius, int32_t* __restrict__ mpos,
-                                                      int32_t* __restrict__ cj) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= ns) return;
-  double px, py, pz;
-  const int64_t i = icp_source<SORTED>(src, j, T, &px, &py, &pz);
-  double d2;
-  int pos;
-  const int tj = nn_search_dev<ROWS>(g, px, py, pz, radius, &d2, &pos);
-  mpos[j] = pos;
-  if (cj) cj[i] = tj;
+// ------------------------------------------------ wave transpose reduction
+// 16 int64 values per lane -> lane l holds the sum over all 64 lanes of value
+// (l >> 2) & 15.  Each step halves the values a lane keeps and doubles the
+// lanes summed into each: pairs (i, i + 8) across the wave halves
+// (v_permlane32_swap), (i, i + 4) across 16-lane rows (v_permlane16_swap),
+// then DPP exchanges with lane l ^ 8 (row_ror:8), l ^ 7 (row_half_mirror),
+// l ^ 1 and l ^ 2 (quad_perm).  About 80 instructions where 16 separate wave
+// sums would take ~400.  EXEC must be full.
+__device__ __forceinline__ int64_t join64(uint32_t lo, uint32_t hi) {
+  return (int64_t)(((uint64_t)hi << 32) | (uint64_t)lo);
+}
+__device__ __forceinline__ int64_t swap32_add(int64_t a, int64_t b) {
+  const auto r0 = __builtin_amdgcn_permlane32_swap((uint32_t)a, (uint32_t)b, false, false);
+  const auto r1 = __builtin_amdgcn_permlane32_swap((uint32_t)((uint64_t)a >> 32), (uint32_t)((uint64_t)b >> 32),
+                                                   false, false);
+  return join64(r0[0], r1[0]) + join64(r0[1], r1[1]);
+}
+__device__ __forceinline__ int64_t swap16_add(int64_t a, int64_t b) {
+  const auto r0 = __builtin_amdgcn_permlane16_swap((uint32_t)a, (uint32_t)b, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap((uint32_t)((uint64_t)a >> 32), (uint32_t)((uint64_t)b >> 32),
+                                                   false, false);
+  return join64(r0[0], r1[0]) + join64(r0[1], r1[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp64(int64_t v) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), CTRL, 0xf, 0xf, false);
+  return join64((uint32_t)lo, (uint32_t)hi);
+}
+// keep one of (a, b) by the lane bit, add the partner's copy of it
+template <int CTRL>
+__device__ __forceinline__ int64_t pair_add(int64_t a, int64_t b, bool bit) {
+  return (bit ? b : a) + dpp64<CTRL>(bit ? a : b);
 }
 
-// Pass 2 — moments: a streaming pass over the matched pairs (source point,
-// target point + normal gathered by sorted position), the 30 moment terms per
-// pair as exact fx integers (common.hpp), summed per lane in int64, then per
-// block into {lo, hi} digit partials: the sums are the same bits for any
-// split of the source over lanes, blocks or ranks.  d^2 is recomputed exactly
-// as the search computed it.
-template <bool SORTED>
-__global__ void __launch_bounds__(kBlock) k_icp_moments(const float* __restrict__ src, int64_t ns, GridView g,
-                                                        const float4* __restrict__ tnorm, Mat4 T,
-                                                        const int32_t* __restrict__ mpos, FxScales sc,
-                                                        int64_t* __restrict__ partial) {
-  __shared__ int64_t sh[(kBlock / 64) * 2 * kNT];
-  int64_t acc[kNT];
+// value i = v(IC<i>): produced pair by pair as the first step consumes them
+// (eight partial sums live, not sixteen values)
+template <class V>
+__device__ __forceinline__ int64_t wave_transpose_sum16(V&& v, int lane) {
+  int64_t w[8], x[4], y[2];
+  w[0] = swap32_add(v(IC<0>{}), v(IC<8>{}));  // lanes >= 32: value i + 8
+  w[1] = swap32_add(v(IC<1>{}), v(IC<9>{}));
+  w[2] = swap32_add(v(IC<2>{}), v(IC<10>{}));
+  w[3] = swap32_add(v(IC<3>{}), v(IC<11>{}));
+  w[4] = swap32_add(v(IC<4>{}), v(IC<12>{}));
+  w[5] = swap32_add(v(IC<5>{}), v(IC<13>{}));
+  w[6] = swap32_add(v(IC<6>{}), v(IC<14>{}));
+  w[7] = swap32_add(v(IC<7>{}), v(IC<15>{}));
 #pragma unroll
-  for (int k = 0; k < kNT; ++k) acc[k] = 0;
+  for (int i = 0; i < 4; ++i) x[i] = swap16_add(w[i], w[i + 4]);  // odd rows: value i + 4
+#pragma unroll
+  for (int i = 0; i < 2; ++i) y[i] = pair_add<0x128>(x[i], x[i + 2], (lane & 8) != 0);  // row_ror:8 = l ^ 8
+  int64_t z = pair_add<0x141>(y[0], y[1], (lane & 4) != 0);  // row_half_mirror = l ^ 7
+  z += dpp64<0xB1>(z);                                        // quad_perm [1,0,3,2] = l ^ 1
+  z += dpp64<0x4E>(z);                                        // quad_perm [2,3,0,1] = l ^ 2
+  return z;
+}
+
+// term k (Open3D ComputeJTJandJTr order: JTJ upper triangle row by row, JTr,
+// r^2; then count and d^2)
+constexpr int jtj_a(int k) {
+  int a = 0, t = k;
+  while (t >= 6 - a) {
+    t -= 6 - a;
+    ++a;
+  }
+  return a;
+}
+constexpr int jtj_b(int k) {
+  int a = 0, t = k;
+  while (t >= 6 - a) {
+    t -= 6 - a;
+    ++a;
+  }
+  return a + t;
+}
+// (J, r, d2 and one are all zero for a lane without a match: every term 0)
+template <int K>
+__device__ __forceinline__ double icp_term(const double (&J)[6], double r, double d2, double one) {
+  if constexpr (K < 21) {
+    constexpr int a = jtj_a(K), b = jtj_b(K);
+    return J[a] * J[b];
+  } else if constexpr (K < 27)
+    return J[K - 21] * r;
+  else if constexpr (K == 27)
+    return r * r;
+  else if constexpr (K == 28)
+    return one;
+  else
+    return d2;
+}
+// fx_term(t, 2^-q) as ldexp then the magic add: ldexp is exact (a result
+// below 2^-1022 rounds to 0 either way), so the bits equal the fma form's
+__device__ __forceinline__ int64_t fx_term_q(double t, int q) {
+  return (int64_t)__double_as_longlong(ldexp(t, -q) + kFxMagic) - kFxMagicBits;
+}
+template <int K>
+__device__ __forceinline__ int64_t icp_fx(const double (&J)[6], double r, double d2, double one,
+                                          const int32_t* __restrict__ q) {
+  if constexpr (K >= kNT)
+    return 0;
+  else
+    return fx_term_q(icp_term<K>(J, r, d2, one), q[K]);
+}
+
+// block b -> a bijection on [0, nb) giving XCD x = b % 8 the contiguous run
+// [x q + min(x, r), ...) of the nb blocks (q = nb / 8, r = nb % 8)
+__device__ __forceinline__ unsigned icp_xcd_block(unsigned b, unsigned nb) {
+  const unsigned x = b & 7, i = b >> 3, q = nb >> 3, r = nb & 7;
+  return x * q + min(x, r) + i;
+}
+
+// One ICP pass, a thread per source point (a full grid: the hardware balances
+// the uneven searches; a loop over several batches per wave costs 25 VGPRs of
+// scalar spills): the transform, the 1-NN (nn_search_dev) and, when matched,
+// the 30 moment terms as fx integers (common.hpp), reduced across the wave at
+// once (lane l keeps term l >> 2 of each half of 16) and split into
+// {lo = low 32 bits, hi = the rest} digits; the block's digits are added
+// (memory-side atomics, ~0.5 KB per block) into one of kIcpCopies accumulator
+// copies (acc[copy][2 kNS]).  mpos[j]
+// = the match's sorted target position (-1: none).  Integer sums: the same
+// bits for any split of the source over lanes, blocks or ranks.
+template <bool SORTED, bool ROWS>
+__global__ void __launch_bounds__(kBlock) k_icp_step(const float* __restrict__ src, int64_t ns, GridView g,
+                                                     const float4* __restrict__ tnorm,
+                                                     const IcpState* __restrict__ st, double radius,
+                                                     int32_t* __restrict__ mpos, int use_prior,
+                                                     int64_t* __restrict__ acc) {
+  __shared__ int64_t sh[kBlock / 64][2 * kNS];
+  if (st->done) return;  // converged: the loop's remaining steps do nothing
+  Mat4 T;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) T.m[i] = st->T[i];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t alo[2] = {0, 0}, ahi[2] = {0, 0};
+  {
+    // workgroups are dealt round-robin over the 8 XCDs: each XCD takes a
+    // contiguous run of the spatially sorted source instead, so the target
+    // cells its waves probe stay in its own L2
+    const int64_t j = (int64_t)icp_xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    int pos = -1;
+    double px = 0, py = 0, pz = 0, d2 = 0;
+    if (j < ns) {
+      icp_source<SORTED>(src, j, T, &px, &py, &pz);
+      // the previous iteration's match as the starting bound (exact either way)
+      nn_search_dev<ROWS>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
+      mpos[j] = pos;
+    }
+    const bool m = pos >= 0;
+    double J[6] = {0, 0, 0, 0, 0, 0}, r = 0;
+    const double one = m ? 1.0 : 0.0;
+    if (!m) d2 = 0.0;
+    if (m) {
+      const float4 vt = g.pts[pos], nt = tnorm[pos];
+      const double nx = nt.x, ny = nt.y, nz = nt.z;
+      r = ((px - (double)vt.x) * nx + (py - (double)vt.y) * ny) + (pz - (double)vt.z) * nz;
+      J[0] = py * nz - pz * ny;
+      J[1] = pz * nx - px * nz;
+      J[2] = px * ny - py * nx;
+      J[3] = nx;
+      J[4] = ny;
+      J[5] = nz;
+    }
+    const int32_t* q = st->q;
+    {
+      const int64_t z = wave_transpose_sum16(
+          [&](auto ci) { return icp_fx<decltype(ci)::value>(J, r, d2, one, q); }, lane);
+      alo[0] += z & 0xffffffffll;
+      ahi[0] += z >> 32;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const int64_t z = wave_transpose_sum16(
+          [&](auto ci) { return icp_fx<16 + decltype(ci)::value>(J, r, d2, one, q); }, lane);
+      alo[1] += z & 0xffffffffll;
+      ahi[1] += z >> 32;
+    }
+  }
+  if ((lane & 3) == 0) {
+    const int t = lane >> 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      sh[wv][2 * (16 * h + t)] = alo[h];
+      sh[wv][2 * (16 * h + t) + 1] = ahi[h];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kNT) {
+    int64_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) s += sh[w][threadIdx.x];
+    if (s)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[(blockIdx.x % kIcpCopies) * 2 * kNS + threadIdx.x]),
+                (unsigned long long)s);
+  }
+}
+
+// The digit sums of the accumulator copies (one workgroup of 1024), which are
+// zeroed again for the next step; dig (LDS) receives 2 kNS digits.
+__device__ __forceinline__ void collect_digits(int64_t* __restrict__ acc, int64_t (*red)[2 * kNS]) {
+  const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  int64_t a = 0;
+  for (int r = grp; r < kIcpCopies; r += 16) {
+    a += acc[r * 2 * kNS + c];
+    acc[r * 2 * kNS + c] = 0;
+  }
+  red[grp][c] = a;
+  __syncthreads();
+  if (threadIdx.x < 2 * kNS) {
+    int64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+    red[0][threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(1024) k_icp_collect(int64_t* __restrict__ acc, int64_t* __restrict__ digits) {
+  __shared__ int64_t red[16][2 * kNS];
+  collect_digits(acc, red);
+  if (threadIdx.x < 2 * kNS) digits[threadIdx.x] = red[0][threadIdx.x];
+}
+
+// The loop's per-iteration bookkeeping, one workgroup: the digit sums of the
+// step's accumulator copies, then (thread 0) the sums, fitness and rmse, Open3D's
+// convergence test against the previous iteration's, and — while iterations
+// remain — the solve and T <- update * T with the next fx exponents.
+__global__ void __launch_bounds__(1024) k_icp_finish(IcpState* __restrict__ st, int64_t* __restrict__ acc,
+                                                     int64_t ns, double max_corr, double rel_fit, double rel_rmse,
+                                                     int it, int max_it) {
+  __shared__ int64_t red[16][2 * kNS];
+  __shared__ IcpState ls;
+  __shared__ double sums[kNS];
+  if (st->done) return;
+  // the state into LDS by all threads at once (one thread alone would wait on
+  // each global access in turn)
+  constexpr int kWords = (int)(sizeof(IcpState) / sizeof(uint32_t));
+  for (int t = threadIdx.x; t < kWords; t += blockDim.x)
+    reinterpret_cast<uint32_t*>(&ls)[t] = reinterpret_cast<const uint32_t*>(st)[t];
+  collect_digits(acc, red);  // (its barriers also publish ls)
+  if (threadIdx.x < kNS)
+    sums[threadIdx.x] =
+        threadIdx.x < kNT ? fx_value(red[0][2 * threadIdx.x], red[0][2 * threadIdx.x + 1], ls.q[threadIdx.x]) : 0.0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sm[kNS];
+    for (int k = 0; k < kNS; ++k) sm[k] = sums[k];
+    double fit, rm;
+    icp_metrics(sm, ns, &fit, &rm);
+    const double pf = ls.fit, pr = ls.rmse;
+    for (int k = 0; k < kNS; ++k) ls.sums[k] = sm[k];
+    ls.fit = fit;
+    ls.rmse = rm;
+    if (it > 0 && fabs(pf - fit) < rel_fit && fabs(pr - rm) < rel_rmse) {
+      ls.done = 1;
+    } else if (it < max_it) {
+      double upd[16], T[16];
+      solve_update(sm, upd);
+      mat4_mul(upd, ls.T, T);
+      state_set_T(ls, T, max_corr);
+      ls.iters = it + 1;
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kWords; t += blockDim.x)
+    reinterpret_cast<uint32_t*>(st)[t] = reinterpret_cast<const uint32_t*>(&ls)[t];
+}
+
+// correspondences of the last step by original source index: cj[i] = the
+// target's original index, -1 for none
+template <bool SORTED>
+__global__ void __launch_bounds__(kBlock) k_corr_from_mpos(const float* __restrict__ src, int64_t ns, GridView g,
+                                                           const int32_t* __restrict__ mpos, int32_t* __restrict__ cj) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += (int64_t)gridDim.x * blockDim.x) {
     const int pos = mpos[j];
-    if (pos < 0) continue;
-    double px, py, pz;
-    icp_source<SORTED>(src, j, T, &px, &py, &pz);
-    const float4 vt = g.pts[pos];
-    double t[kNT];
-    icp_terms(t, px, py, pz, vt, tnorm[pos], dist2_f64(px, py, pz, vt));
-#pragma unroll
-    for (int k = 0; k < kNT; ++k) acc[k] += fx_term(t[k], sc.s[k]);
+    const int64_t i = SORTED ? (int64_t)__float_as_int(reinterpret_cast<const float4*>(src)[j].w) : j;
+    cj[i] = pos >= 0 ? __float_as_int(g.pts[pos].w) : -1;
   }
-  int64_t* out = partial + (int64_t)blockIdx.x * 2 * kNS;
-  block_fx<kBlock, kNT>(acc, sh, out);
-  if (threadIdx.x < 2 * (kNS - kNT)) out[2 * kNT + threadIdx.x] = 0;
 }
 
 __global__ void __launch_bounds__(kBlock) k_corr_flags(const int32_t* __restrict__ cj, int64_t ns,
@@ -152,95 +601,6 @@ __global__ void __launch_bounds__(kBlock) k_corr_pairs(const int32_t* __restrict
     corr[2 * k] = i;
     corr[2 * k + 1] = cj[i];
   }
-}
-
-// ------------------------------------------------------------ host linear algebra
-static bool ldlt_solve6(const double A_in[36], const double b_in[6], double x[6]) {
-  double A[36];
-  std::memcpy(A, A_in, sizeof(A));
-  int perm[6] = {0, 1, 2, 3, 4, 5};
-  const int n = 6;
-  for (int k = 0; k < n; ++k) {
-    int piv = k;
-    double best = std::fabs(A[k * n + k]);
-    for (int i = k + 1; i < n; ++i)
-      if (std::fabs(A[i * n + i]) > best) {
-        best = std::fabs(A[i * n + i]);
-        piv = i;
-      }
-    if (piv != k) {
-      for (int j = 0; j < n; ++j) std::swap(A[k * n + j], A[piv * n + j]);
-      for (int i = 0; i < n; ++i) std::swap(A[i * n + k], A[i * n + piv]);
-      std::swap(perm[k], perm[piv]);
-    }
-    const double dk = A[k * n + k];
-    double col[6];
-    for (int i = k + 1; i < n; ++i) col[i] = A[i * n + k];
-    for (int i = k + 1; i < n; ++i)
-      for (int j = k + 1; j < n; ++j) A[i * n + j] -= dk != 0 ? col[i] * col[j] / dk : 0.0;
-    for (int i = k + 1; i < n; ++i) A[i * n + k] = dk != 0 ? col[i] / dk : 0.0;
-  }
-  double y[6];
-  for (int i = 0; i < n; ++i) y[i] = b_in[perm[i]];
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < i; ++j) y[i] -= A[i * n + j] * y[j];
-  const double tiny = std::numeric_limits<double>::min();
-  for (int i = 0; i < n; ++i) y[i] = std::fabs(A[i * n + i]) > tiny ? y[i] / A[i * n + i] : 0.0;
-  for (int i = n - 1; i >= 0; --i)
-    for (int j = i + 1; j < n; ++j) y[i] -= A[j * n + i] * y[j];
-  for (int i = 0; i < n; ++i) x[perm[i]] = y[i];
-  for (int i = 0; i < n; ++i)
-    if (!std::isfinite(x[i])) return false;
-  return true;
-}
-
-// TransformVector6dToMatrix4d: R = Rz(x2) Ry(x1) Rx(x0), t = x[3..5]
-static void vec6_to_mat4(const double x[6], double T[16]) {
-  const double ca = std::cos(x[0]), sa = std::sin(x[0]);
-  const double cb = std::cos(x[1]), sb = std::sin(x[1]);
-  const double cg = std::cos(x[2]), sg = std::sin(x[2]);
-  const double Rz[9] = {cg, -sg, 0, sg, cg, 0, 0, 0, 1};
-  const double Ry[9] = {cb, 0, sb, 0, 1, 0, -sb, 0, cb};
-  const double Rx[9] = {1, 0, 0, 0, ca, -sa, 0, sa, ca};
-  double A[9], R[9];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j)
-      A[i * 3 + j] = (Rz[i * 3] * Ry[j] + Rz[i * 3 + 1] * Ry[3 + j]) + Rz[i * 3 + 2] * Ry[6 + j];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) R[i * 3 + j] = (A[i * 3] * Rx[j] + A[i * 3 + 1] * Rx[3 + j]) + A[i * 3 + 2] * Rx[6 + j];
-  for (int i = 0; i < 16; ++i) T[i] = 0;
-  for (int i = 0; i < 3; ++i) {
-    for (int j = 0; j < 3; ++j) T[i * 4 + j] = R[i * 3 + j];
-    T[i * 4 + 3] = x[3 + i];
-  }
-  T[15] = 1;
-}
-
-static void mat4_mul(const double* A, const double* B, double* C) {
-  double t[16];
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < 4; ++j)
-      t[i * 4 + j] =
-          ((A[i * 4] * B[j] + A[i * 4 + 1] * B[4 + j]) + A[i * 4 + 2] * B[8 + j]) + A[i * 4 + 3] * B[12 + j];
-  std::memcpy(C, t, sizeof(t));
-}
-
-static int solve_update(const double* sums, double* upd) {
-  double JTJ[36], mb[6], x[6];
-  int t = 0;
-  for (int a = 0; a < 6; ++a)
-    for (int b = a; b < 6; ++b) {
-      JTJ[a * 6 + b] = sums[t];
-      JTJ[b * 6 + a] = sums[t];
-      ++t;
-    }
-  for (int a = 0; a < 6; ++a) mb[a] = -sums[21 + a];
-  if (sums[28] <= 0.0 || !ldlt_solve6(JTJ, mb, x)) {
-    for (int a = 0; a < 16; ++a) upd[a] = (a % 5 == 0) ? 1.0 : 0.0;
-    return 0;
-  }
-  vec6_to_mat4(x, upd);
-  return 1;
 }
 
 // ------------------------------------------------------------ descriptors
@@ -259,6 +619,7 @@ static void desc_pack(const GridBuild& G, const void* base, const float4* normal
 
 static bool desc_unpack(const double* d, const void* base, GridView* g, const float4** normals) {
   if (!d || d[13] != kDescMagic) return false;
+  *g = GridView{};
   g->ox = (float)d[0]; g->oy = (float)d[1]; g->oz = (float)d[2]; g->h = (float)d[3]; g->inv_h = (float)d[4];
   g->slack = (float)d[5];
   g->nx = (int)d[6]; g->ny = (int)d[7]; g->nz = (int)d[8]; g->n = (int64_t)d[9];
@@ -271,36 +632,9 @@ static bool desc_unpack(const double* d, const void* base, GridView* g, const fl
   return true;
 }
 
-// fx exponents of the 32 sums (common.hpp) from bounds that every rank
-// derives alike — the source's |x|,|y|,|z| bounds (the whole source's, on
-// every rank), T and max_correspondence_distance:
-//   |p|  <= Pn = |(|T| absmax + |t|)| (row bounds of T (x,y,z,1), Euclidean)
-//   |J_a| <= Pn |n| (a < 3), |n_a| (a >= 3), |n| <= 1.01 (float32 unit normal)
-//   |r| = |(p - vt).n| <= d |n| < max_corr |n|,  d^2 < max_corr^2
-// (1.01: margin for float rounding; a looser bound only coarsens the quantum).
-static void icp_fx_exps(const double absmax[3], const double* T, double max_corr, int q[kNS]) {
-  double P2 = 0.0;
-  for (int i = 0; i < 3; ++i) {
-    const double Pi = ((std::fabs(T[4 * i]) * absmax[0] + std::fabs(T[4 * i + 1]) * absmax[1]) +
-                       std::fabs(T[4 * i + 2]) * absmax[2]) + std::fabs(T[4 * i + 3]);
-    P2 += Pi * Pi;
-  }
-  const double pn = std::sqrt(P2) * 1.01;
-  double bJ[6];
-  for (int a = 0; a < 6; ++a) bJ[a] = (a < 3 ? pn : 1.0) * 1.01;
-  const double br = max_corr * 1.01 * 1.01;
-  int k = 0;
-  for (int a = 0; a < 6; ++a)
-    for (int b = a; b < 6; ++b) q[k++] = fx_exp(bJ[a] * bJ[b] * 1.01);
-  for (int a = 0; a < 6; ++a) q[21 + a] = fx_exp(bJ[a] * br * 1.01);
-  q[27] = fx_exp(br * br * 1.01);
-  q[28] = fx_exp(1.0);
-  q[29] = fx_exp(max_corr * max_corr * 1.01);
-  q[30] = q[31] = 0;
-}
-
 struct AccWs {
-  int64_t* partial;
+  IcpState* st;
+  int64_t* acc;  // [kIcpCopies][2 kNS], zero between steps
   int64_t* digits;
   int32_t* cj;
   int32_t* mpos;
@@ -312,14 +646,11 @@ struct AccWs {
   double* mm;
 };
 
-// blocks of the moments pass: <= kFxLaneTerms pairs per lane
-static int icp_blocks(int64_t ns) {
-  const int64_t need = (ns + (int64_t)kBlock * kFxLaneTerms - 1) / ((int64_t)kBlock * kFxLaneTerms);
-  return (int)std::max<int64_t>(1, std::max<int64_t>(need, std::min<int64_t>(kIcpBlocks, (ns + kBlock - 1) / kBlock)));
-}
+static unsigned step_blocks(int64_t ns) { return grid_for(ns, kBlock, 1ll << 31); }
 
 static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
-  w->partial = ar.take<int64_t>((size_t)icp_blocks(ns) * 2 * kNS);
+  w->st = ar.take<IcpState>(1);
+  w->acc = ar.take<int64_t>((size_t)kIcpCopies * 2 * kNS);
   w->digits = ar.take<int64_t>(2 * kNS);
   w->cj = ar.take<int32_t>(ns);
   w->mpos = ar.take<int32_t>(ns);
@@ -372,64 +703,79 @@ static int source_absmax(const float* src, int64_t ns, bool sorted, AccWs& w, hi
   return 0;
 }
 
+// use_prior: mpos holds the previous step's matches on this source (the loop)
+static void launch_step(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn,
+                        double radius, AccWs& w, hipStream_t s, int use_prior = 0) {
+  const unsigned nb = step_blocks(ns);
+  // O3DX_ICP_SHELL=1: the Chebyshev shell walk (round 1-2 form) instead of the row walk
+  const bool shell = getenv("O3DX_ICP_SHELL") != nullptr;
+  KTimer km("icp_match", s);
+  if (sorted && !shell)
+    hipLaunchKernelGGL((k_icp_step<true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
+                       use_prior, w.acc);
+  else if (sorted)
+    hipLaunchKernelGGL((k_icp_step<true, false>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
+                       use_prior, w.acc);
+  else if (!shell)
+    hipLaunchKernelGGL((k_icp_step<false, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
+                       use_prior, w.acc);
+  else
+    hipLaunchKernelGGL((k_icp_step<false, false>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius,
+                       w.mpos, use_prior, w.acc);
+}
+
+// correspondences of the last step into corr_out (pairs by original index)
+static int corr_of_last_step(const float* src, int64_t ns, bool sorted, const GridView& g, AccWs& w, hipStream_t s,
+                             int32_t* corr_out, int64_t* ncorr) {
+  if (ns == 0) {
+    if (ncorr) *ncorr = 0;
+    return 0;
+  }
+  if (sorted)
+    hipLaunchKernelGGL(k_corr_from_mpos<true>, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, src, ns, g,
+                       w.mpos, w.cj);
+  else
+    hipLaunchKernelGGL(k_corr_from_mpos<false>, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, src, ns, g,
+                       w.mpos, w.cj);
+  hipLaunchKernelGGL(k_corr_flags, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, ns, w.flags);
+  O3DX_TRY(compact_flags(w.flags, ns, w.src_idx, nullptr, w.cnt, w.scan_tmp, s));
+  int64_t m = 0;
+  O3DX_TRY(read_back(&m, w.cnt, sizeof(int64_t), s));
+  if (m > 0)
+    hipLaunchKernelGGL(k_corr_pairs, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, w.src_idx, m,
+                       corr_out);
+  if (ncorr) *ncorr = m;
+  return 0;
+}
+
+// One accumulate with T on the host (the sharded loop of distributed.py):
 // absmax: the source's coordinate bounds (host, 3) — the same on every rank
 // of a sharded source; fx_out (nullable, host 4 x kNS): the exact sums.
 static int accumulate(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, const double* T,
                       double radius, const double* absmax, AccWs& w, hipStream_t s, double* sums_host,
                       int64_t* fx_out, int32_t* corr_out, int64_t* ncorr) {
-  Mat4 M;
-  std::memcpy(M.m, T, sizeof(M.m));
-  const int nb = icp_blocks(ns);
-  const bool want_corr = corr_out != nullptr;
-  int q[kNS];
-  icp_fx_exps(absmax, T, radius, q);
-  FxScales sc;
-  for (int k = 0; k < kNT; ++k) sc.s[k] = fx_scale(q[k]);
+  IcpState hs{};
+  for (int a = 0; a < 3; ++a) hs.absmax[a] = absmax[a];
+  state_set_T(hs, T, radius);
   KTimer kt("icp_accumulate", s);
   if (ns > 0) {
-    int32_t* cj = want_corr ? w.cj : (int32_t*)nullptr;
-    const unsigned nm = grid_for(ns, kBlock, 1 << 30);
-    KTimer km("icp_match", s);
-    // O3DX_ICP_SHELL=1: the Chebyshev shell walk (round 1-2 form) instead of the row walk
-    const bool shell = getenv("O3DX_ICP_SHELL") != nullptr;
-    if (sorted && !shell)
-      hipLaunchKernelGGL((k_icp_match<true, true>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
-    else if (sorted)
-      hipLaunchKernelGGL((k_icp_match<true, false>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
-    else if (!shell)
-      hipLaunchKernelGGL((k_icp_match<false, true>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos, cj);
-    else
-      hipLaunchKernelGGL((k_icp_match<false, false>), dim3(nm), dim3(kBlock), 0, s, src, ns, g, M, radius, w.mpos,
-                         cj);
-    km.stop();
-    if (sorted)
-      hipLaunchKernelGGL(k_icp_moments<true>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, sc, w.partial);
-    else
-      hipLaunchKernelGGL(k_icp_moments<false>, dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, M, w.mpos, sc, w.partial);
-    O3DX_TRY(reduce_columns_i64(w.partial, nb, 2 * kNS, w.digits, s));
+    O3DX_HIP(hipMemcpyAsync(w.st, &hs, sizeof(IcpState), hipMemcpyHostToDevice, s));
+    O3DX_HIP(hipMemsetAsync(w.acc, 0, (size_t)kIcpCopies * 2 * kNS * sizeof(int64_t), s));
+    launch_step(src, ns, sorted, g, tn, radius, w, s);
+    hipLaunchKernelGGL(k_icp_collect, dim3(1), dim3(1024), 0, s, w.acc, w.digits);
   } else {
     O3DX_HIP(hipMemsetAsync(w.digits, 0, 2 * kNS * sizeof(int64_t), s));
   }
   kt.stop();
-  if (want_corr && ns > 0) {
-    hipLaunchKernelGGL(k_corr_flags, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, ns, w.flags);
-    O3DX_TRY(compact_flags(w.flags, ns, w.src_idx, nullptr, w.cnt, w.scan_tmp, s));
-    int64_t m = 0;
-    O3DX_TRY(read_back(&m, w.cnt, sizeof(int64_t), s));
-    if (m > 0)
-      hipLaunchKernelGGL(k_corr_pairs, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, w.cj, w.src_idx, m,
-                         corr_out);
-    if (ncorr) *ncorr = m;
-  } else if (ncorr) {
-    *ncorr = -1;
-  }
+  if (corr_out) O3DX_TRY(corr_of_last_step(src, ns, sorted, g, w, s, corr_out, ncorr));
+  else if (ncorr) *ncorr = -1;
   int64_t digits[2 * kNS], fx[4 * kNS];
   O3DX_TRY(read_back(digits, w.digits, sizeof(digits), s));
   O3DX_HIP(hipGetLastError());
-  fx_pack(digits, q, kNS, fx);
-  fx_to_double(fx, kNS, sums_host);
+  fx_pack(digits, hs.q, kNS, fx);
+  for (int k = 0; k < kNS; ++k) sums_host[k] = k < kNT ? fx_value(digits[2 * k], digits[2 * k + 1], hs.q[k]) : 0.0;
   if (fx_out) std::memcpy(fx_out, fx, sizeof(fx));
-  if (ncorr && !want_corr) *ncorr = (int64_t)sums_host[28];
+  if (ncorr && !corr_out) *ncorr = (int64_t)sums_host[28];
   return 0;
 }
 
@@ -528,6 +874,68 @@ extern "C" size_t o3dx_registration_icp_workspace_bytes(int64_t ns) {
          std::max(o3dx_icp_accumulate_workspace_bytes(ns), o3dx_spatial_sort_workspace_bytes(ns)) + 1024;
 }
 
+// The whole loop on the device: every iteration's step and finish are queued
+// at once (a converged loop's remaining launches return at their first
+// instruction); the host waits once for the final state.
+static int run_loop(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, double max_corr, const double* init, int max_iteration, double rel_fit,
+                    double rel_rmse, const double* absmax, AccWs& w, hipStream_t s, double* T_out, double* fitness,
+                    double* rmse, int32_t* corr_out, int64_t* ncorr) {
+  IcpState hs{};
+  double T0[16];
+  if (init) std::memcpy(T0, init, sizeof(T0));
+  else
+    for (int a = 0; a < 16; ++a) T0[a] = (a % 5 == 0) ? 1.0 : 0.0;
+  if (ns == 0) {  // no correspondences: T unchanged, fitness and rmse 0
+    std::memcpy(T_out, T0, sizeof(T0));
+    *fitness = 0;
+    *rmse = 0;
+    if (ncorr) *ncorr = 0;
+    return 0;
+  }
+  if (absmax) std::memcpy(hs.absmax, absmax, sizeof(hs.absmax));
+  else O3DX_TRY(source_absmax(src, ns, sorted, w, s, hs.absmax));
+  state_set_T(hs, T0, max_corr);
+  O3DX_HIP(hipMemcpyAsync(w.st, &hs, sizeof(IcpState), hipMemcpyHostToDevice, s));
+  O3DX_HIP(hipMemsetAsync(w.acc, 0, (size_t)kIcpCopies * 2 * kNS * sizeof(int64_t), s));
+  const int iters = std::max(max_iteration, 0);
+  {
+    KTimer kt("icp_loop", s);
+    for (int it = 0; it <= iters; ++it) {
+      // from the second step on, the previous step's matches seed the search
+      launch_step(src, ns, sorted, g, tn, max_corr, w, s, it > 0);
+      hipLaunchKernelGGL(k_icp_finish, dim3(1), dim3(1024), 0, s, w.st, w.acc, ns, max_corr, rel_fit, rel_rmse, it,
+                         iters);
+    }
+  }
+  O3DX_HIP(hipGetLastError());
+  if (corr_out) O3DX_TRY(corr_of_last_step(src, ns, sorted, g, w, s, corr_out, ncorr));
+  O3DX_TRY(read_back(&hs, w.st, sizeof(IcpState), s));
+  std::memcpy(T_out, hs.T, sizeof(hs.T));
+  *fitness = hs.fit;
+  *rmse = hs.rmse;
+  if (!corr_out && ncorr) *ncorr = (int64_t)hs.sums[28];
+  return 0;
+}
+
+extern "C" int o3dx_icp_register(const float* src, int64_t ns, int src_sorted4, const void* target_ws,
+                                 const double* desc, const double* init, int max_iteration, double rel_fit,
+                                 double rel_rmse, double max_corr, const double* src_absmax, double* T_out,
+                                 double* fitness, double* rmse, int32_t* corr_out, int64_t* ncorr, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  if (ns < 0 || (ns > 0 && !src) || !target_ws || !T_out || !fitness || !rmse)
+    return fail(O3DX_EINVAL, "o3dx_icp_register: bad args");
+  if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  GridView g;
+  const float4* tn;
+  if (!desc_unpack(desc, target_ws, &g, &tn)) return fail(O3DX_EINVAL, "invalid ICP target descriptor");
+  if (!ws || ws_bytes < o3dx_icp_accumulate_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
+  Arena ar(ws, ws_bytes);
+  AccWs w;
+  acc_carve(ar, std::max<int64_t>(ns, 1), &w);
+  return run_loop(src, ns, src_sorted4 != 0, g, tn, max_corr, init, max_iteration, rel_fit, rel_rmse, src_absmax,
+                  w, as_stream(stream), T_out, fitness, rmse, corr_out, ncorr);
+}
+
 extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns, const float* tgt,
                                                     const float* tgt_normals, int64_t nt, double max_corr,
                                                     const double* init, int max_iteration, double rel_fit,
@@ -536,8 +944,9 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
                                                     size_t target_ws_bytes, void* ws, size_t ws_bytes, void* stream) {
   if (!T_out || !fitness || !rmse) return fail(O3DX_EINVAL, "registration_icp: bad args");
   if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  if (ns < 0 || (ns > 0 && !src)) return fail(O3DX_EINVAL, "registration_icp: bad args");
   hipStream_t s = as_stream(stream);
-  double desc[16];
+  double desc[O3DX_ICP_DESC_LEN];
   O3DX_TRY(o3dx_icp_target_build(tgt, tgt_normals, nt, max_corr, target_ws, target_ws_bytes, desc, stream));
   GridView g;
   const float4* tn;
@@ -551,43 +960,6 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
   Arena ar(rest, rest_bytes);
   AccWs w;
   acc_carve(ar, std::max<int64_t>(ns, 1), &w);
-  double T[16];
-  if (init) std::memcpy(T, init, sizeof(T));
-  else
-    for (int a = 0; a < 16; ++a) T[a] = (a % 5 == 0) ? 1.0 : 0.0;
-  double sums[kNS];
-  double am[3] = {0, 0, 0};
-  if (ns > 0) O3DX_TRY(source_absmax(src4, ns, true, w, s, am));
-  auto metrics = [&](const double* sm, double& fit, double& rm) {
-    double c = sm[28];
-    if (c <= 0 || ns == 0) {
-      fit = 0;
-      rm = 0;
-    } else {
-      fit = c / (double)ns;
-      rm = std::sqrt(sm[29] / c);
-    }
-  };
-  O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, nullptr, nullptr));
-  double fit, rm;
-  metrics(sums, fit, rm);
-  for (int it = 0; it < max_iteration; ++it) {
-    double upd[16];
-    solve_update(sums, upd);
-    mat4_mul(upd, T, T);
-    const double pf = fit, pr = rm;
-    const bool last = (it + 1 == max_iteration);
-    O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, last ? corr_out : nullptr, last ? ncorr : nullptr));
-    metrics(sums, fit, rm);
-    if (std::fabs(pf - fit) < rel_fit && std::fabs(pr - rm) < rel_rmse) {
-      if (!last && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, corr_out, ncorr));
-      break;
-    }
-  }
-  if (max_iteration <= 0 && corr_out) O3DX_TRY(accumulate(src4, ns, true, g, tn, T, max_corr, am, w, s, sums, nullptr, corr_out, ncorr));
-  std::memcpy(T_out, T, sizeof(T));
-  *fitness = fit;
-  *rmse = rm;
-  if (!corr_out && ncorr) *ncorr = (int64_t)sums[28];
-  return 0;
+  return run_loop(src4, ns, true, g, tn, max_corr, init, max_iteration, rel_fit, rel_rmse, nullptr, w, s, T_out,
+                  fitness, rmse, corr_out, ncorr);
 }

@@ -497,7 +497,7 @@ class ICPTarget:
         nt = self.xyz.shape[0]
         self.max_corr = float(max_correspondence_distance)
         self.ws = torch.empty(L.o3dx_icp_target_workspace_bytes(nt), dtype=torch.uint8, device=self.xyz.device)
-        self.desc = np.zeros(16, np.float64)
+        self.desc = np.zeros(N.ICP_DESC_LEN, np.float64)
         N.check(L.o3dx_icp_target_build(N.ptr(self.xyz), N.ptr(self.normals), nt, self.max_corr, N.ptr(self.ws),
                                         self.ws.numel(), _np_ptr(self.desc), N.stream_ptr(self.xyz.device)),
                 "icp_target_build")
@@ -535,6 +535,40 @@ class ICPTarget:
                                       N.stream_ptr(s.device)), "icp_accumulate")
         out = (sums, (corr[: int(nc[0])] if want_corr else None))
         return out + (fx,) if return_fx else out
+
+    def register(self, src: torch.Tensor, init=None, max_iteration: int = 30, relative_fitness: float = 1e-6,
+                 relative_rmse: float = 1e-6, absmax=None, want_corr: bool = False):
+        """Open3D registration_icp (point-to-plane) onto this target with the
+        whole loop on the device (o3dx_icp_register): each iteration's fused
+        correspondence + moments pass, the solve and the convergence test are
+        queued at once and the host waits once.  `src` as in accumulate (the
+        (n,4) spatial_sort output is faster).  -> dict(transformation,
+        fitness, inlier_rmse[, correspondence_set])."""
+        sorted4 = src.ndim == 2 and src.shape[1] == 4
+        if sorted4:
+            N.require_device(src, "source points")
+            s = src.float().contiguous()
+        else:
+            s = _xyz(src.to(self.xyz.device), "source points")
+        if absmax is None:
+            absmax = getattr(src, "absmax", None)
+        L = N.load()
+        ns = s.shape[0]
+        T0 = _c(np.eye(4) if init is None else init, np.float64).reshape(4, 4)
+        am = None if absmax is None else _c(absmax, np.float64).reshape(3)
+        T = np.zeros((4, 4), np.float64)
+        fit, rm = np.zeros(1), np.zeros(1)
+        corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if want_corr else None
+        nc = np.zeros(1, np.int64)
+        ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp_acc")
+        N.check(L.o3dx_icp_register(N.ptr(s), ns, 1 if sorted4 else 0, N.ptr(self.ws), _np_ptr(self.desc),
+                                    _np_ptr(T0), int(max_iteration), float(relative_fitness), float(relative_rmse),
+                                    self.max_corr, _np_ptr(am), _np_ptr(T), _np_ptr(fit), _np_ptr(rm), N.ptr(corr),
+                                    _np_ptr(nc), N.ptr(ws), ws.numel(), N.stream_ptr(s.device)), "icp_register")
+        out = {"transformation": T, "fitness": float(fit[0]), "inlier_rmse": float(rm[0])}
+        if want_corr:
+            out["correspondence_set"] = corr[: int(nc[0])]
+        return out
 
 
 def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:

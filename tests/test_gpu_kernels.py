@@ -353,6 +353,40 @@ def test_registration_icp_parity(dev):
     assert np.abs(res["transformation"] - Tgt_inv).max() < 2e-3
 
 
+@pytest.mark.parametrize("rel", [0.0, 1e-6])
+def test_icp_device_loop_equals_host_loop(dev, rel):
+    """The loop on the device (ICPTarget.register / o3dx_icp_register: solve,
+    update and convergence test in k_icp_finish) gives the same T, fitness,
+    rmse and correspondences to the bit as the host loop over accumulate +
+    icp_update (the multi-GPU loop's arithmetic), with and without an early
+    convergence stop; registration_icp (the same loop after its own target
+    build and sort) agrees too."""
+    src, tgt = _icp_case(30000, seed=11)
+    tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)
+    t, n = torch.from_numpy(tgt).to(dev), torch.from_numpy(tn).to(dev)
+    target = ops.ICPTarget(t, n, 0.02)
+    s4 = ops.spatial_sort(torch.from_numpy(src).to(dev))
+    am = np.abs(src.astype(np.float64)).max(0)
+    res = target.register(s4, max_iteration=25, relative_fitness=rel, relative_rmse=rel, absmax=am, want_corr=True)
+    T = np.eye(4)
+    sums, _ = target.accumulate(s4, T, absmax=am)
+    fit, rm = sums[28] / len(src), np.sqrt(sums[29] / sums[28])
+    for _ in range(25):
+        T = ops.icp_update(sums, T)
+        pf, pr = fit, rm
+        sums, corr = target.accumulate(s4, T, absmax=am, want_corr=True)
+        fit, rm = sums[28] / len(src), np.sqrt(sums[29] / sums[28])
+        if abs(pf - fit) < rel and abs(pr - rm) < rel:
+            break
+    assert np.array_equal(res["transformation"], T)
+    assert res["fitness"] == fit and res["inlier_rmse"] == rm
+    assert torch.equal(res["correspondence_set"], corr)
+    one = ops.registration_icp(torch.from_numpy(src).to(dev), t, n, 0.02, max_iteration=25, relative_fitness=rel,
+                               relative_rmse=rel)
+    assert np.array_equal(one["transformation"], T) and one["fitness"] == fit
+    assert torch.equal(one["correspondence_set"], corr)
+
+
 def test_icp_accumulate_sorted_source_layout(dev):
     src, tgt = _icp_case(30000, seed=4)
     tn = O.estimate_normals(tgt, O.KNN, 30).astype(np.float32)

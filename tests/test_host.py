@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     for name in decl:
         assert hasattr(lib, name), name
     assert sorted(N.declared_symbols()) == decl
-    assert lib.o3dx_abi_version() == 3
+    assert lib.o3dx_abi_version() == 4
 
 
 def test_library_host_only_entry_points():
@@ -65,6 +65,31 @@ def test_icp_solve_host():
     c, s = np.cos(0.01), np.sin(0.01)
     assert np.allclose(upd[:3, :3], [[c, -s, 0], [s, c, 0], [0, 0, 1]])
     assert np.allclose(upd[:3, 3], x[3:])
+
+
+def test_icp_solve_rotation_angles_host():
+    """The update's rotation uses the library's own sin / cos (the same bits
+    on the host and in the device loop, icp.hip det_sincos): within 2 ulp of
+    numpy's Rz(c) Ry(b) Rx(a) for angles across several quadrants."""
+    rng = np.random.default_rng(5)
+    angles = np.concatenate([rng.uniform(-0.05, 0.05, (300, 3)), rng.uniform(-4, 4, (300, 3)),
+                             np.array([[np.pi / 2, -np.pi, 3 * np.pi / 4], [1e-9, -1e-12, 0.0], [20.0, -33.0, 7.5]])])
+    for x0, x1, x2 in angles:
+        sums = np.zeros(32)
+        t = 0
+        for a in range(6):
+            for b in range(a, 6):
+                sums[t] = 1.0 if a == b else 0.0
+                t += 1
+        sums[21:27] = -np.array([x0, x1, x2, 0.5, -1.0, 2.0])
+        sums[28] = 1
+        upd = o3p.ops.icp_solve(sums)
+        ca, sa, cb, sb, cg, sg = np.cos(x0), np.sin(x0), np.cos(x1), np.sin(x1), np.cos(x2), np.sin(x2)
+        Rz = np.array([[cg, -sg, 0], [sg, cg, 0], [0, 0, 1]])
+        Ry = np.array([[cb, 0, sb], [0, 1, 0], [-sb, 0, cb]])
+        Rx = np.array([[1, 0, 0], [0, ca, -sa], [0, sa, ca]])
+        assert np.abs(upd[:3, :3] - Rz @ Ry @ Rx).max() < 2e-15, (x0, x1, x2)
+        assert np.array_equal(upd[:3, 3], [0.5, -1.0, 2.0]) and np.array_equal(upd[3], [0, 0, 0, 1])
 
 
 def test_fx_to_double_correctly_rounded():

@@ -15,7 +15,7 @@ import sys
 
 SHORT = {"k_normals_stile": "normals_stile", "k_normals_vlist": "normals_stile", "k_normals_knn_tile": "normals_tile", "k_normals_knn_wave": "normals_wave",
          "k_voxel_assign_dense": "voxel_assign", "k_icp_accumulate": "icp_accumulate",
-         "k_icp_match": "icp_match", "k_icp_moments": "icp_moments", "k_vbin_scatter": "vbin_scatter",
+         "k_icp_match": "icp_match", "k_icp_step": "icp_step", "k_icp_moments": "icp_moments", "k_vbin_scatter": "vbin_scatter",
          "k_plane_count": "plane_count", "k_plane_fixup": "plane_fixup", "k_grid_count": "grid_count", "k_grid_cell_sort": "grid_sort",
          "k_vbin_count": "vbin_count", "k_vbin_reduce": "vbin_reduce", "k_gather_vox": "gather_vox",
          "k_aabb_partial": "aabb_partial", "k_tile_compact_u8": "compact_u8",

@@ -1,7 +1,7 @@
 """Focused driver for rocprofv3 (kernel trace / PMC): normals on the C2 reps,
 converged ICP accumulate, RANSAC, the RANSAC count alone, ICP's first
 iteration; a few launches each.  GPU box only.
-Usage: python tools/prof_kernels.py [all|normals|icp|ransac|ransac_count|icp_first]"""
+Usage: python tools/prof_kernels.py [all|normals|icp|icp_loop|ransac|ransac_count|icp_first]"""
 import os
 import sys
 
@@ -33,6 +33,14 @@ if what in ("all", "icp"):
     T = np.linalg.inv(S.rigid_transform())
     for _ in range(3):
         sums, _ = target.accumulate(src4, T)
+    torch.cuda.synchronize()
+if what == "icp_loop":  # the device loop (o3dx_icp_register) from T = I: 30 steps, prior matches from step 2
+    tgt = S.box_surface(N, 1, device=dev)
+    src = S.apply_transform(S.box_surface(N, 2, device=dev), S.rigid_transform())
+    tn = ops.estimate_normals(tgt, knn=30)
+    target = ops.ICPTarget(tgt, tn, 0.02)
+    src4 = ops.spatial_sort(src)
+    target.register(src4, max_iteration=30, relative_fitness=0.0, relative_rmse=0.0)
     torch.cuda.synchronize()
 if what in ("all", "ransac"):
     pts = S.planted_plane(N, 3, device=dev)
