@@ -262,7 +262,9 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
 // Nearest neighbour with d^2 < radius^2 (SearchHybrid(p, r, 1)); returns its
 // original index, -1 if none.  ROWS: the walk beyond the own cell goes by
 // (y, z) rows (below); else by Chebyshev shells of cells.
-template <bool ROWS = true>
+// SHARE: the lanes calling together share first bounds (below); every lane
+// of the wave that runs the search must call it at once.
+template <bool ROWS = true, bool SHARE = false>
 __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, double qy, double qz, double radius,
                                              double* best_d2, int* best_pos, int prior = -1) {
   double bd = INFINITY;
@@ -326,6 +328,26 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   if (bi < 0) {
     visit_cell(cx, cy, cz);
     own_seen = true;
+  }
+  if (SHARE) {
+    // A lane without a match yet borrows the match of the nearest lane (by
+    // lane index) that has one as its starting bound: the queries of a wave
+    // are neighbours in a spatially sorted source, and any real target point
+    // bounds the search (the result is the same) — it spares the clipped
+    // ring walk that would only look for a first bound.  Ballot and shuffle
+    // see the lanes calling here.
+    const uint64_t have = __ballot(bi >= 0);
+    const bool borrow = have && bi < 0;
+    const int lane = (int)(threadIdx.x & 63);
+    int src_lane = lane;
+    if (borrow) {
+      const uint64_t up = lane < 63 ? have >> (lane + 1) : 0ull, down = have & ((1ull << lane) - 1ull);
+      const int du = up ? __ffsll((unsigned long long)up) : 64;         // distance to the next lane above
+      const int dd = down ? lane - (63 - __clzll((long long)down)) : 64;  // ... below
+      src_lane = du <= dd ? lane + du : lane - dd;
+    }
+    const int p = __shfl(bp, src_lane, 64);  // converged: the source lanes take part
+    if (borrow && p >= 0) visit_point(p, g.pts[p]);
   }
   if (bi >= 0) {
     // A match in the own cell bounds the search: every better point lies in

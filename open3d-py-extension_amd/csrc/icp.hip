@@ -431,7 +431,7 @@ __device__ __forceinline__ unsigned icp_xcd_block(unsigned b, unsigned nb) {
 // = the match's sorted target position (-1: none).  Integer sums: the same
 // bits for any split of the source over lanes, blocks or ranks.
 template <bool SORTED, bool ROWS>
-__global__ void __launch_bounds__(kBlock) k_icp_step(const float* __restrict__ src, int64_t ns, GridView g,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_icp_step(const float* __restrict__ src, int64_t ns, GridView g,
                                                      const float4* __restrict__ tnorm,
                                                      const IcpState* __restrict__ st, double radius,
                                                      int32_t* __restrict__ mpos, int use_prior,
@@ -453,7 +453,7 @@ __global__ void __launch_bounds__(kBlock) k_icp_step(const float* __restrict__ s
     if (j < ns) {
       icp_source<SORTED>(src, j, T, &px, &py, &pz);
       // the previous iteration's match as the starting bound (exact either way)
-      nn_search_dev<ROWS>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
+      nn_search_dev<ROWS, true>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
       mpos[j] = pos;
     }
     const bool m = pos >= 0;
