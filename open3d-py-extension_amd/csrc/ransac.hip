@@ -794,6 +794,7 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
                           std::vector<uint8_t>& st, hipStream_t s, int* rc, double* hi_max = nullptr,
                           int mfma = 0) {  // 1 / 2: k_plane_upper_mfma<false / true>'s operands
   if (hi_max) *hi_max = -1.0;
+  const bool band_off = getenv("O3DX_RANSAC_BAND_OFF") != nullptr;
   p32.resize(H);
   bnd.resize(H);
   dg.resize(H);
@@ -877,8 +878,10 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
       }
       const double S = std::fabs(pl[0]) * absmax[0] + std::fabs(pl[1]) * absmax[1] + std::fabs(pl[2]) * absmax[2] +
                        std::fabs(pl[3]);
-      const double lim = thr + std::ldexp(1.0, tight ? MfmaShape<true>::kBoundExp : MfmaShape<false>::kBoundExp) * S +
-                         1e-30;
+      // O3DX_RANSAC_BAND_OFF (test hook, tests/test_gpu_kernels.py): count
+      // |d_mfma| < thr itself, so a test can bound the sweep's own error
+      const double band = band_off ? 0.0 : std::ldexp(1.0, tight ? MfmaShape<true>::kBoundExp : MfmaShape<false>::kBoundExp) * S;
+      const double lim = thr + band + 1e-30;
       float f = (float)lim;
       if ((double)f < lim) f = std::nextafter(f, INFINITY);
       hv[(j / 32) * 32 + r] = f;

@@ -694,6 +694,96 @@ int oref_voxel_down_sample(const float* xyz, int64_t n, const double* minb, cons
   return 0;
 }
 
+// The representatives of oref_voxel_down_sample (max index per voxel key,
+// ascending) computed in parallel for clouds too large for the single pass
+// (200M points: minutes).  Same key formula; points are split into buckets by
+// a hash of their key (per-thread chunks keep each bucket's indices
+// ascending), each bucket keeps the last = max index per key.  The function
+// of the input is the same as the single pass's rep_idx; the CPU suite holds
+// the two equal.
+int oref_voxel_reps_parallel(const float* xyz, int64_t n, const double* minb, const double* maxb, double vs,
+                             int32_t* rep_idx, int64_t* m_out) {
+  if (vs <= 0.0) return -22;
+  double ext = std::max(maxb[0] - minb[0], std::max(maxb[1] - minb[1], maxb[2] - minb[2]));
+  if (vs * (double)std::numeric_limits<int>::max() < ext) return -22;
+  constexpr int kB = 4096;
+  auto key_of = [&](int64_t i, int64_t* k3) {
+    for (int a = 0; a < 3; ++a) k3[a] = (int64_t)std::floor(((double)xyz[3 * i + a] - minb[a]) / vs);
+  };
+  auto bucket_of = [](const int64_t* k3) {
+    uint64_t h = (uint64_t)k3[0] * 0x9E3779B97F4A7C15ull ^ (uint64_t)k3[1] * 0xC2B2AE3D27D4EB4Full ^
+                 (uint64_t)k3[2] * 0x165667B19E3779F9ull;
+    h ^= h >> 29;
+    return (int)(h % kB);
+  };
+  const int T = omp_get_max_threads();
+  std::vector<uint16_t> bk((size_t)n);
+  std::vector<int64_t> cnt((size_t)T * kB, 0);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t a = n * t / T, b = n * (t + 1) / T;
+    int64_t* c = &cnt[(size_t)t * kB];
+    for (int64_t i = a; i < b; ++i) {
+      int64_t k3[3];
+      key_of(i, k3);
+      const int h = bucket_of(k3);
+      bk[i] = (uint16_t)h;
+      ++c[h];
+    }
+  }
+  // offsets: bucket-major, thread-minor (so a bucket's indices stay ascending)
+  std::vector<int64_t> start((size_t)kB + 1, 0);
+  int64_t run = 0;
+  for (int h = 0; h < kB; ++h) {
+    start[h] = run;
+    for (int t = 0; t < T; ++t) {
+      const int64_t v = cnt[(size_t)t * kB + h];
+      cnt[(size_t)t * kB + h] = run;
+      run += v;
+    }
+  }
+  start[kB] = run;
+  std::vector<int32_t> order((size_t)n);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t a = n * t / T, b = n * (t + 1) / T;
+    int64_t* c = &cnt[(size_t)t * kB];
+    for (int64_t i = a; i < b; ++i) order[c[bk[i]]++] = (int32_t)i;
+  }
+  std::vector<std::vector<int32_t>> out(kB);
+#pragma omp parallel for schedule(dynamic, 8) num_threads(T)
+  for (int h = 0; h < kB; ++h) {
+    struct K3 {
+      int64_t x, y, z;
+      bool operator==(const K3& o) const { return x == o.x && y == o.y && z == o.z; }
+    };
+    struct KH3 {
+      size_t operator()(const K3& k) const {
+        return (size_t)(k.x * 73856093 ^ k.y * 19349663 ^ k.z * 83492791);
+      }
+    };
+    std::unordered_map<K3, int32_t, KH3> last;
+    last.reserve((size_t)(start[h + 1] - start[h]));
+    for (int64_t j = start[h]; j < start[h + 1]; ++j) {
+      int64_t k3[3];
+      key_of(order[j], k3);
+      last[K3{k3[0], k3[1], k3[2]}] = order[j];  // ascending: the last is the max
+    }
+    out[h].reserve(last.size());
+    for (auto& kv : last) out[h].push_back(kv.second);
+  }
+  int64_t m = 0;
+  for (int h = 0; h < kB; ++h) {
+    std::copy(out[h].begin(), out[h].end(), rep_idx + m);
+    m += (int64_t)out[h].size();
+  }
+  std::sort(rep_idx, rep_idx + m);
+  *m_out = m;
+  return 0;
+}
+
 // Reference: estimate_normals (PointCloud.py:68-73), CPUNormals
 // (processors.py:243-249).  [upstream] PointCloud::EstimateNormals +
 // EstimatePerPointCovariances (Search >= 3 -> ComputeCovariance else

@@ -44,6 +44,8 @@ def lib():
         L.oref_aabb.argtypes = [_P, _I64, _P]
         L.oref_voxel_down_sample.argtypes = [_P, _I64, _P, _P, _D, _P, _P, _P, _P]
         L.oref_voxel_down_sample.restype = _I32
+        L.oref_voxel_reps_parallel.argtypes = [_P, _I64, _P, _P, _D, _P, _P]
+        L.oref_voxel_reps_parallel.restype = _I32
         L.oref_estimate_normals.argtypes = [_P, _I64, _I32, _I32, _D, _P, _P]
         L.oref_knn_search.argtypes = [_P, _I64, _P, _I64, _I32, _I32, _D, _I32, _P, _P, _P]
         L.oref_fast_eigen3x3.argtypes = [_P, _I64, _P]
@@ -86,9 +88,14 @@ def aabb(xyz):
     return mm[:3].copy(), mm[3:].copy()
 
 
-def voxel_down_sample(xyz, voxel_size, min_bound=None, max_bound=None, trace=False):
+PARALLEL_REPS_AT = 20_000_000
+
+
+def voxel_down_sample(xyz, voxel_size, min_bound=None, max_bound=None, trace=False, parallel=None):
     """Returns (rep_idx ascending int32, voxel_of_point, cubic_id (M,8)) — the
-    latter two only when trace=True."""
+    latter two only when trace=True.  Without trace, clouds of
+    PARALLEL_REPS_AT points or more (or parallel=True) take
+    oref_voxel_reps_parallel, the same function computed over hashed buckets."""
     x = _f32(xyz)
     n = len(x)
     if min_bound is None or max_bound is None:
@@ -99,6 +106,14 @@ def voxel_down_sample(xyz, voxel_size, min_bound=None, max_bound=None, trace=Fal
     mxb = np.ascontiguousarray(max_bound, np.float64)
     rep = np.empty(max(n, 1), np.int32)
     m = np.zeros(1, np.int64)
+    if parallel is None:
+        parallel = n >= PARALLEL_REPS_AT
+    if parallel and not trace:
+        rc = lib().oref_voxel_reps_parallel(_ptr(x), n, _ptr(mnb), _ptr(mxb), float(voxel_size),
+                                            _ptr(rep), _ptr(m))
+        if rc != 0:
+            raise RuntimeError("voxel_size is invalid or too small")
+        return rep[: int(m[0])].copy()
     vop = np.empty(max(n, 1), np.int32) if trace else None
     cub = np.empty(max(8 * n, 8), np.int32) if trace else None
     rc = lib().oref_voxel_down_sample(_ptr(x), n, _ptr(mnb), _ptr(mxb), float(voxel_size),

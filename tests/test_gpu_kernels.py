@@ -733,6 +733,46 @@ def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatc
     assert got[0] == -1
 
 
+def test_mfma2_sweep_error_within_documented_bound(dev, monkeypatch):
+    """The two-MFMA sweep's own error, |d_mfma - d| < 2^-17 S_h,
+    checked directly: with the band switched off (O3DX_RANSAC_BAND_OFF, a test
+    hook) the sweep counts |d_mfma| < thr, so for every hypothesis each point
+    with |d| < thr - 2^-17 S_h must be counted and none with |d| >= thr +
+    2^-17 S_h.  The cloud puts 2048 points per hypothesis at |d| = thr + u
+    2^-16 S_h, u uniform in [-1, 1] (float64 distances of the float32 points),
+    so about half of them lie outside that band on either side; with the band
+    on, every float64 inlier is counted (ub >= exact)."""
+    rng = np.random.default_rng(21)
+    H, per, thr = 32, 2048, 0.01
+    nrm = rng.normal(size=(H, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    off = rng.uniform(-0.3, 0.3, H)
+    planes = np.concatenate([nrm, off[:, None]], 1)
+    base = rng.uniform(-1, 1, (H, per, 3))
+    S_est = np.abs(nrm).sum(1) + np.abs(off)  # |x| <= ~1.2 below: S_h from the cloud itself after
+    pts = []
+    for h in range(H):
+        b = base[h] - ((base[h] @ nrm[h]) + off[h])[:, None] * nrm[h]  # on the plane
+        u = rng.uniform(-1, 1, per)
+        sgn = rng.choice([-1.0, 1.0], per)
+        pts.append(b + (sgn * (thr + u * 2.0 ** -16 * S_est[h]))[:, None] * nrm[h])
+    p32 = np.concatenate(pts).astype(np.float32)
+    p64 = p32.astype(np.float64)
+    S_h = np.abs(planes[:, :3]) @ np.abs(p64).max(0) + np.abs(planes[:, 3])
+    d = np.abs(p64 @ planes[:, :3].T + planes[:, 3])  # (n, H)
+    x = torch.from_numpy(p32).to(dev)
+    monkeypatch.setenv("O3DX_RANSAC_UPPER", "mfma2")
+    monkeypatch.setenv("O3DX_RANSAC_BAND_OFF", "1")
+    got = ops.plane_count_upper(x, planes, thr)
+    monkeypatch.delenv("O3DX_RANSAC_BAND_OFF")
+    lo = (d < thr - 2.0 ** -17 * S_h).sum(0)
+    hi = (d < thr + 2.0 ** -17 * S_h).sum(0)
+    assert ((hi - lo) > per // 3).all()  # the test points straddle the bound
+    assert (lo <= got).all() and (got <= hi).all(), (lo, got, hi)
+    ub = ops.plane_count_upper(x, planes, thr)
+    assert (ub >= (d < thr).sum(0)).all()
+
+
 @pytest.mark.parametrize("n", [1_000_000])
 def test_c2_pipeline_full_mantissa_coordinates(dev, n):
     """The C2 step (one-call voxel_down_sample + KNN30 normals on the voxel

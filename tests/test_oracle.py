@@ -41,6 +41,28 @@ def test_voxel_errors():
         O.voxel_down_sample(x, 0.0)
     with pytest.raises(RuntimeError):
         O.voxel_down_sample(x * 1e6, 1e-10)
+    for par in (False, True):
+        with pytest.raises(RuntimeError):
+            O.voxel_down_sample(x, -1.0, parallel=par)
+
+
+@pytest.mark.parametrize("vs", [0.003, 0.005, 0.02])
+def test_voxel_parallel_reps_equal_single_pass(bunny, vs):
+    # oref_voxel_reps_parallel (used at >= 20M points) == the single pass
+    assert np.array_equal(O.voxel_down_sample(bunny, vs, parallel=True), O.voxel_down_sample(bunny, vs, parallel=False))
+
+
+def test_voxel_parallel_reps_equal_single_pass_large():
+    # 3M points with duplicates and negative coordinates, ~1 point per voxel
+    # down to many: every voxel's max index, in ascending order
+    rng = np.random.default_rng(11)
+    x = (rng.random((3_000_000, 3)) * 2 - 1).astype(np.float32)
+    x[1::7] = x[::7][: len(x[1::7])]
+    for vs in (0.01, 0.05, 0.4):
+        a = O.voxel_down_sample(x, vs, parallel=True)
+        b = O.voxel_down_sample(x, vs, parallel=False)
+        assert len(a) > 1 and np.array_equal(a, b)
+    assert len(O.voxel_down_sample(x[:0], 0.1, parallel=True)) == 0
 
 
 def test_knn_sets_vs_scipy(bunny):
