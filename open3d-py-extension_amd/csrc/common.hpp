@@ -196,6 +196,16 @@ __device__ __forceinline__ void block_fx(const int64_t (&acc)[K], int64_t* sh, i
   __syncthreads();
 }
 
+// The exact value of a {lo, hi} digit sum (lo >= 0) scaled by 2^q, correctly
+// rounded once: the carry of lo moves into hi (|hi| < 2^53), then
+// hi 2^32 + lo is one rounded addition of two exact doubles — the same value
+// as core.hip's fx_to_double (__int128), on the host and on the device.
+__host__ __device__ inline double fx_value(int64_t lo, int64_t hi, int q) {
+  const int64_t h = hi + (lo >> 32);
+  const int64_t l = lo & 0xffffffffll;
+  return ldexp(ldexp((double)h, 32) + (double)l, q);
+}
+
 // {lo, hi} digit sums + exponent of k sums (row j: {lo, hi, q, 0}) -> float64,
 // correctly rounded (one rounding of the exact integer, then the exact scale)
 void fx_to_double(const int64_t* fx4, int64_t k, double* out);

@@ -238,15 +238,7 @@ O3DX_HD inline void icp_fx_exps(const double absmax[3], const double* T, double 
   q[30] = q[31] = 0;
 }
 
-// The exact value of a {lo, hi} digit sum (lo >= 0) scaled by 2^q, correctly
-// rounded once: the carry of lo moves into hi (|hi| < 2^53), then
-// hi 2^32 + lo is one rounded addition of two exact doubles — the same value
-// as core.hip's fx_to_double (__int128), on the host and on the device.
-O3DX_HD inline double fx_value(int64_t lo, int64_t hi, int q) {
-  const int64_t h = hi + (lo >> 32);
-  const int64_t l = lo & 0xffffffffll;
-  return ldexp(ldexp((double)h, 32) + (double)l, q);
-}
+// fx_value: common.hpp
 
 O3DX_HD inline void icp_metrics(const double* sums, int64_t ns, double* fit, double* rm) {
   const double c = sums[28];

@@ -496,6 +496,349 @@ k_plane_upper_mfma(const float* __restrict__ xyz, int64_t n, const uint4* __rest
   }
 }
 
+// ---------------------------------------------------- culled upper sweep
+// Most (point, hypothesis) pairs of a RANSAC sweep are far from the plane.
+// The culled sweep first puts the points in Morton order of a 2^b-per-axis
+// grid over the cloud's box (two-level counting sort, below), so 64
+// consecutive points — a chunk — form a compact patch.  Per chunk the wave takes the box of its
+// finite points (centre c, half extents e) and tests 64 hypotheses at a time
+// (lane = hypothesis):
+//   |n.c + d| - (|a| ex + |b| ey + |c| ez) < limc_h
+// in float32; the survivors are listed in LDS and counted 64 at a time with
+// lane = hypothesis and the chunk's points broadcast (v_readlane): three fmas
+// and a compare per (point, hypothesis), the float32 count |d32| < lim_h of
+// k_plane_upper (lim_h >= thr + 6 2^-24 S_h + 2^-20 thr, so every float64
+// inlier is counted).  Culling is conservative: for p in the box, |d_exact(p)|
+// >= |dc_exact| - r_exact, the float32 dc and r are within 12.2 2^-24 S_h of
+// those, and |d32(p)| < lim_h implies |d_exact(p)| < lim_h + 4 2^-24 S_h; so
+// limc_h = lim_h + 20 2^-24 S_h (rounded up) never drops a pair the float32
+// count would take.  The counts are the same upper bounds as k_plane_upper's
+// (a pair counted here is counted there); the work is the surviving pairs.
+constexpr int kCullBlock = 512;    // 8 waves
+constexpr int kCullHG = 1024;      // hypotheses per block row (LDS ~29 KB)
+constexpr int kCullMinN = 4096;    // smaller clouds keep the dense sweeps
+constexpr int kCullCS = 128;       // points per chunk (one wave)
+constexpr int kCullResident = 256 * 5;  // blocks resident at once (256 CUs x 5 by LDS)
+constexpr int kCullPB = 16;        // points per batch of scalar loads
+
+__device__ __forceinline__ uint32_t spread_bits3(uint32_t v) {  // <= 10 bits -> every third bit
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+// Morton cell of a point on the 2^bits grid over mm = {min xyz, max xyz}
+// (float64 on the device); clamped, non-finite coordinates land in cell 0.
+struct BinGeom {
+  float mn[3], sc[3], top;
+};
+__device__ __forceinline__ BinGeom bin_geom(const double* __restrict__ mm, int bits) {
+  BinGeom g;
+  const double cells = (double)(1 << bits);
+  for (int a = 0; a < 3; ++a) {
+    const double ext = mm[3 + a] - mm[a];
+    g.mn[a] = (float)mm[a];
+    g.sc[a] = ext > 0 ? (float)(cells / ext) : 0.0f;
+  }
+  g.top = (float)((1 << bits) - 1);
+  return g;
+}
+__device__ __forceinline__ uint32_t bin_key(const BinGeom& g, float x, float y, float z) {
+  const float v[3] = {x, y, z};
+  uint32_t k = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float c = fminf(fmaxf((v[a] - g.mn[a]) * g.sc[a], 0.0f), g.top);  // NaN -> 0
+    k |= spread_bits3((uint32_t)c) << a;
+  }
+  return k;
+}
+
+// Two-level Morton order without global atomics: the top kb bits per axis
+// pick a brick (<= 512), the low lb bits a local cell (<= 512); brick-major
+// then cell order is the Morton order of the full grid.  Pass 1: per-block
+// brick histograms (LDS), brick-major, scanned on the device; pass 2: the
+// block's points sorted by brick in an LDS stage, then written as runs (one
+// run per brick and block: coalesced), the local cell in .w; pass 3: one
+// workgroup per brick sorts its range by local cell (LDS counts).
+// The order inside a cell is the LDS atomics' (the sweep does not care).
+constexpr int kCBinBlock = 1024;
+constexpr int kCBinPer = 8;
+constexpr int kCBinChunk = kCBinBlock * kCBinPer;  // points per block, passes 1-2 (13-bit local index)
+constexpr int kCBinMaxBricks = 512;
+constexpr int kCBinMaxLocal = 512;
+constexpr int kCBinLocalBlock = 1024;  // pass 3: a workgroup per brick
+
+__global__ void __launch_bounds__(kCBinBlock) k_cbin_hist(const float* __restrict__ xyz, int64_t n,
+                                                          const double* __restrict__ mm, int bits, int lb, int nb,
+                                                          int32_t* __restrict__ bh) {
+  __shared__ int32_t hist[kCBinMaxBricks];
+  const BinGeom g = bin_geom(mm, bits);
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int k = threadIdx.x; k < nb; k += kCBinBlock) hist[k] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kCBinChunk;
+#pragma unroll 4
+  for (int j = 0; j < kCBinPer; ++j) {
+    const int64_t i = base + threadIdx.x + (int64_t)j * kCBinBlock;
+    if (i < n) {
+      const P3 v = p[i];
+      atomicAdd(&hist[bin_key(g, v.x, v.y, v.z) >> (3 * lb)], 1);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nb; k += kCBinBlock) bh[(int64_t)k * gridDim.x + blockIdx.x] = hist[k];
+}
+
+__global__ void __launch_bounds__(kCBinBlock) k_cbin_scatter(const float* __restrict__ xyz, int64_t n,
+                                                             const double* __restrict__ mm, int bits, int lb, int nb,
+                                                             const int32_t* __restrict__ bstart,
+                                                             float4* __restrict__ tmp) {
+  static_assert(kCBinChunk <= 8192 && kCBinMaxBricks <= 512 && kCBinMaxLocal <= 512, "stage entry: 13 + 9 + 9 bits");
+  __shared__ uint32_t stage[kCBinChunk];  // (local index << 18) | (brick << 9) | cell, sorted by brick
+  __shared__ int32_t lstart[kCBinMaxBricks], cur[kCBinMaxBricks];
+  __shared__ int32_t wsum[kCBinBlock / 64 + 1];
+  const BinGeom g = bin_geom(mm, bits);
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  for (int k = threadIdx.x; k < nb; k += kCBinBlock) cur[k] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kCBinChunk;
+  const uint32_t lmask = (1u << (3 * lb)) - 1u;
+  uint32_t code[kCBinPer];
+#pragma unroll
+  for (int j = 0; j < kCBinPer; ++j) {
+    const int64_t i = base + threadIdx.x + (int64_t)j * kCBinBlock;
+    code[j] = ~0u;
+    if (i < n) {
+      const P3 v = p[i];
+      const uint32_t key = bin_key(g, v.x, v.y, v.z);
+      const uint32_t k = key >> (3 * lb);
+      code[j] = ((uint32_t)(threadIdx.x + j * kCBinBlock) << 18) | (k << 9) | (key & lmask);
+      atomicAdd(&cur[k], 1);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the block's brick counts (one brick per thread: nb <= 512 < kCBinBlock)
+  const int c = threadIdx.x < nb ? cur[threadIdx.x] : 0;
+  int tot;
+  const int ex = block_excl_scan<kCBinBlock>(c, wsum, &tot);
+  if (threadIdx.x < nb) {
+    lstart[threadIdx.x] = ex;
+    cur[threadIdx.x] = ex;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kCBinPer; ++j)
+    if (code[j] != ~0u) stage[atomicAdd(&cur[(code[j] >> 9) & 511u], 1)] = code[j];
+  __syncthreads();
+  // stage slot t of brick k -> the block's run of brick k, consecutive
+  for (int t = threadIdx.x; t < tot; t += kCBinBlock) {
+    const uint32_t e = stage[t];
+    const int k = (int)((e >> 9) & 511u);
+    const P3 v = p[base + (e >> 18)];
+    tmp[bstart[(int64_t)k * gridDim.x + blockIdx.x] + (t - lstart[k])] =
+        make_float4(v.x, v.y, v.z, __int_as_float((int)(e & 511u)));
+  }
+}
+
+__global__ void __launch_bounds__(kCBinLocalBlock) k_cbin_local(const float4* __restrict__ tmp,
+                                                                const int32_t* __restrict__ bstart, int nblk,
+                                                                int nb, int nl, int64_t n, float4* __restrict__ out) {
+  constexpr int B = kCBinLocalBlock, U = 4;  // points per thread per step (loads first)
+  __shared__ int32_t cnt[kCBinMaxLocal];
+  __shared__ int32_t wsum[B / 64 + 1];
+  const int k = blockIdx.x;
+  const int64_t s0 = bstart[(int64_t)k * nblk], s1 = k + 1 < nb ? bstart[(int64_t)(k + 1) * nblk] : n;
+  for (int c = threadIdx.x; c < nl; c += B) cnt[c] = 0;
+  __syncthreads();
+  for (int64_t q0 = s0; q0 < s1; q0 += B * U) {
+    int cl[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = q0 + threadIdx.x + u * B;
+      cl[u] = q < s1 ? __float_as_int(tmp[q].w) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (cl[u] >= 0) atomicAdd(&cnt[cl[u]], 1);
+  }
+  __syncthreads();
+  const int span = (nl + B - 1) / B;
+  const int c0 = threadIdx.x * span, c1 = min(c0 + span, nl);
+  int run = 0;
+  for (int c = c0; c < c1; ++c) run += cnt[c];
+  int tot;
+  int ex = block_excl_scan<B>(run, wsum, &tot);
+  for (int c = c0; c < c1; ++c) {
+    const int v = cnt[c];
+    cnt[c] = ex;
+    ex += v;
+  }
+  __syncthreads();
+  for (int64_t q0 = s0; q0 < s1; q0 += B * U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = q0 + threadIdx.x + u * B;
+      v[u] = q < s1 ? tmp[q] : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cl = __float_as_int(v[u].w);
+      if (cl >= 0) out[s0 + atomicAdd(&cnt[cl], 1)] = make_float4(v[u].x, v[u].y, v[u].z, 0.0f);
+    }
+  }
+}
+
+// v_writelane_b32 (lane `lane` of `old` set to val; val and lane uniform)
+__device__ int o3dx_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+// all-lanes reduction of a float (EXEC full): DPP within 16-lane rows
+// (l ^ 1, l ^ 2, half-row mirror, row_ror:8), then row and half swaps
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+template <class F>
+__device__ __forceinline__ float wave_all_f(float v, F op) {
+  v = op(v, dpp_f<0xB1>(v));
+  v = op(v, dpp_f<0x4E>(v));
+  v = op(v, dpp_f<0x141>(v));
+  v = op(v, dpp_f<0x128>(v));
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+__device__ __forceinline__ float wave_min_f(float v) {
+  return wave_all_f(v, [](float a, float b) { return fminf(a, b); });
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+  return wave_all_f(v, [](float a, float b) { return fmaxf(a, b); });
+}
+
+// grid: (blocks over chunks of kCullCS points, hypothesis rows of kCullHG);
+// pts: the Morton-ordered points, padded with NaN rows to a whole chunk;
+// pl32 [H] float32 planes, lims [H] = (lim, limc, -, -) (degenerate: -1,
+// -inf); partial [block x][H] int32 counts.  Per chunk a wave takes the box
+// of its finite points, tests the hypotheses 64 at a time (lane = hypothesis,
+// coefficients from LDS) and lists the survivors in LDS; every 64 listed
+// survivors (and the rest at the end) are counted with lane = hypothesis and
+// the chunk's points read by scalar loads (wave-uniform addresses): three
+// fmas, a compare and an add per (point, hypothesis).
+__global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* __restrict__ pts, int64_t n,
+                                                                 const float4* __restrict__ pl32,
+                                                                 const float4* __restrict__ lims, int H,
+                                                                 int32_t* __restrict__ partial) {
+  constexpr int kW = kCullBlock / 64, CS = kCullCS;
+  __shared__ float4 lpl[kCullHG];
+  __shared__ float2 llim[kCullHG];
+  __shared__ int32_t lcnt[kCullHG];
+  __shared__ uint16_t lst[kW][128];
+  const int h0 = blockIdx.y * kCullHG, hn = min(kCullHG, H - h0);
+  for (int t = threadIdx.x; t < hn; t += kCullBlock) {
+    lpl[t] = pl32[h0 + t];
+    const float4 l = lims[h0 + t];
+    llim[t] = make_float2(l.x, l.y);
+    lcnt[t] = 0;
+  }
+  __syncthreads();
+  // the wave index as a scalar: chunk addresses are wave-uniform (scalar loads)
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int64_t nchunk = (n + CS - 1) / CS;
+  const int64_t cstep = (int64_t)gridDim.x * kW;
+  float4 nxt[CS / 64];  // the next chunk's points, loaded while this one is swept
+  {
+    const int64_t c0 = min<int64_t>((int64_t)blockIdx.x * kW + wv, nchunk - 1);
+#pragma unroll
+    for (int j = 0; j < CS / 64; ++j) nxt[j] = pts[c0 * CS + j * 64 + lane];
+  }
+  for (int64_t c = (int64_t)blockIdx.x * kW + wv; c < nchunk; c += cstep) {
+    const float4* cp = pts + c * CS;  // wave-uniform
+    float4 cur[CS / 64];
+#pragma unroll
+    for (int j = 0; j < CS / 64; ++j) cur[j] = nxt[j];
+    {
+      const int64_t cn = min(c + cstep, nchunk - 1);
+#pragma unroll
+      for (int j = 0; j < CS / 64; ++j) nxt[j] = pts[cn * CS + j * 64 + lane];
+    }
+    float mnx = INFINITY, mny = INFINITY, mnz = INFINITY, mxx = -INFINITY, mxy = -INFINITY, mxz = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < CS / 64; ++j) {
+      const float4 v = cur[j];
+      const bool fin = __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
+      mnx = fminf(mnx, fin ? v.x : INFINITY);
+      mny = fminf(mny, fin ? v.y : INFINITY);
+      mnz = fminf(mnz, fin ? v.z : INFINITY);
+      mxx = fmaxf(mxx, fin ? v.x : -INFINITY);
+      mxy = fmaxf(mxy, fin ? v.y : -INFINITY);
+      mxz = fmaxf(mxz, fin ? v.z : -INFINITY);
+    }
+    auto u = [](float f) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(f))); };
+    mnx = u(wave_min_f(mnx));
+    mny = u(wave_min_f(mny));
+    mnz = u(wave_min_f(mnz));
+    mxx = u(wave_max_f(mxx));
+    mxy = u(wave_max_f(mxy));
+    mxz = u(wave_max_f(mxz));
+    if (!(mnx <= mxx)) continue;  // no finite point: nothing to count
+    const float cx = 0.5f * mnx + 0.5f * mxx, cy = 0.5f * mny + 0.5f * mxy, cz = 0.5f * mnz + 0.5f * mxz;
+    const float ex = 0.5f * mxx - 0.5f * mnx, ey = 0.5f * mxy - 0.5f * mny, ez = 0.5f * mxz - 0.5f * mnz;
+    // count the listed hypotheses [0, g) against the chunk's points
+    auto eval = [&](int g) {
+      const bool act = lane < g;
+      const int h = act ? (int)lst[wv][lane] : 0;
+      const float4 p = lpl[h];
+      const float lim = act ? llim[h].x : -1.0f;
+      int cnt = 0;
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+      for (int k0 = 0; k0 < CS; k0 += kCullPB) {
+        float4 q[kCullPB];
+#pragma unroll
+        for (int j = 0; j < kCullPB; ++j) q[j] = cp[k0 + j];  // scalar loads
+#pragma unroll
+        for (int j = 0; j < kCullPB; ++j) {
+          const float d = fmaf(p.x, q[j].x, fmaf(p.y, q[j].y, fmaf(p.z, q[j].z, p.w)));
+          cnt += fabsf(d) < lim ? 1 : 0;
+        }
+      }
+      if (act && cnt) atomicAdd(&lcnt[h], cnt);
+    };
+    int nl = 0;  // wave-uniform list length (< 64 between groups)
+    for (int g0 = 0; g0 < hn; g0 += 64) {
+      const int h = g0 + lane;
+      bool surv = false;
+      if (h < hn) {
+        const float4 p = lpl[h];
+        const float dc = fmaf(p.x, cx, fmaf(p.y, cy, fmaf(p.z, cz, p.w)));
+        const float r = fmaf(fabsf(p.x), ex, fmaf(fabsf(p.y), ey, fabsf(p.z) * ez));
+        surv = fabsf(dc) - r < llim[h].y;
+      }
+      const uint64_t m = __ballot(surv);
+      if (surv) lst[wv][nl + __popcll(m & below)] = (uint16_t)h;
+      nl += __popcll(m);
+      __builtin_amdgcn_wave_barrier();
+      if (nl >= 64) {
+        eval(64);
+        const int rest = nl - 64;
+        const uint16_t mv = lane < rest ? lst[wv][64 + lane] : 0;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < rest) lst[wv][lane] = mv;
+        __builtin_amdgcn_wave_barrier();
+        nl = rest;
+      }
+    }
+    if (nl > 0) eval(nl);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < hn; t += kCullBlock) partial[(int64_t)blockIdx.x * H + h0 + t] = lcnt[t];
+}
+
 // Host side of the fragments: bf16 (round to nearest even) of a float
 static uint16_t bf16_rne_host(float x) {
   uint32_t b;
@@ -646,6 +989,57 @@ __global__ void __launch_bounds__(kBlock) k_plane_moments(const float* __restric
   block_fx<kBlock, 6>(acc, sh, partial + (int64_t)blockIdx.x * 12);
 }
 
+// segment_plane's last step in one read of the cloud: the inlier flags of the
+// best plane and the first moments pass (fx sums of x, y, z over the inliers)
+__global__ void __launch_bounds__(kBlock) k_plane_flags_sum(const float* __restrict__ xyz, int64_t n, double a,
+                                                            double b, double c, double d, double thr, MomScales sc,
+                                                            uint8_t* __restrict__ flags,
+                                                            int64_t* __restrict__ partial) {
+  __shared__ int64_t sh[(kBlock / 64) * 6];
+  const double pl[4] = {a, b, c, d};
+  const P3* p = reinterpret_cast<const P3*>(xyz);
+  int64_t acc[3] = {0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const P3 q = p[i];
+    const bool in = plane_dist64(pl, q.x, q.y, q.z) < thr;
+    flags[i] = in ? 1 : 0;
+    if (in) {
+      acc[0] += fx_term((double)q.x, sc.s[0]);
+      acc[1] += fx_term((double)q.y, sc.s[1]);
+      acc[2] += fx_term((double)q.z, sc.s[2]);
+    }
+  }
+  block_fx<kBlock, 3>(acc, sh, partial + (int64_t)blockIdx.x * 6);
+}
+
+// Second moments pass with the centroid formed on the device: c = (fx sum of
+// the first pass) / k, the value the host forms (fx_value = fx_to_double);
+// k = *count (the compaction's), the first pass's digit sums in s1 (3 rows).
+__global__ void __launch_bounds__(kBlock) k_plane_moments_c(const float* __restrict__ xyz,
+                                                            const int32_t* __restrict__ idx,
+                                                            const int64_t* __restrict__ count,
+                                                            const int64_t* __restrict__ s1, int q0, int q1, int q2,
+                                                            MomScales sc, int64_t* __restrict__ partial) {
+  __shared__ int64_t sh[(kBlock / 64) * 12];
+  const int64_t m = *count;
+  const double k = (double)m;
+  const double cx = fx_value(s1[0], s1[1], q0) / k, cy = fx_value(s1[2], s1[3], q1) / k,
+               cz = fx_value(s1[4], s1[5], q2) / k;
+  int64_t acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = idx[j];
+    const double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    const double r0 = x - cx, r1 = y - cy, r2 = z - cz;
+    acc[0] += fx_term(r0 * r0, sc.s[0]);
+    acc[1] += fx_term(r0 * r1, sc.s[1]);
+    acc[2] += fx_term(r0 * r2, sc.s[2]);
+    acc[3] += fx_term(r1 * r1, sc.s[3]);
+    acc[4] += fx_term(r1 * r2, sc.s[4]);
+    acc[5] += fx_term(r2 * r2, sc.s[5]);
+  }
+  block_fx<kBlock, 6>(acc, sh, partial + (int64_t)blockIdx.x * 12);
+}
+
 static int mom_blocks(int64_t m) {
   const int64_t need = (m + (int64_t)kBlock * kFxLaneTerms - 1) / ((int64_t)kBlock * kFxLaneTerms);
   return (int)std::max<int64_t>(1, std::max<int64_t>(need, std::min<int64_t>(kMomBlocks, (m + kBlock - 1) / kBlock)));
@@ -767,7 +1161,21 @@ struct CountWs {
   uint32_t* flags;  // (batch, hypothesis chunk) window bitmap of the brute-force count
   int64_t* counts;
   int64_t* sum_partial;
+  // culled sweep: Morton-ordered copy of the points and its counting sort
+  float4* sorted;
+  float4* tmp;
+  int32_t* bh;
+  int32_t* bstart;
+  int32_t* bscan;
+  int bits;
+  bool binned;  // sorted holds this call's points
 };
+
+// grid bits per axis of the culled sweep's Morton order: ~8 points per cell
+static int cull_bits(int64_t n) {
+  const double b = std::log2(std::max<double>((double)n, 8.0) / 8.0) / 3.0;
+  return std::max(1, std::min(6, (int)std::lround(b)));  // <= 3 + 3: the stage entry's fields
+}
 
 static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   H = std::max(H, 1);
@@ -785,6 +1193,14 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   w->flags = ar.take<uint32_t>((size_t)count_flag_words(n, H, kMinBatchPts, kMinHC));
   w->counts = ar.take<int64_t>(H);
   w->sum_partial = ar.take<int64_t>((size_t)2 * abs_sum_blocks(n) * H);
+  w->bits = cull_bits(n);
+  const int64_t nbh = (int64_t)kCBinMaxBricks * ((n + kCBinChunk - 1) / kCBinChunk);
+  w->sorted = ar.take<float4>((size_t)n + kCullCS);  // + NaN rows to a whole chunk
+  w->tmp = ar.take<float4>((size_t)n);
+  w->bh = ar.take<int32_t>((size_t)nbh + 1);
+  w->bstart = ar.take<int32_t>((size_t)nbh + 1);
+  w->bscan = ar.take<int32_t>(scan_workspace_ints(nbh + 1));
+  w->binned = false;
   return ar.used;
 }
 
@@ -824,6 +1240,12 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
     float half = (float)(std::max((double)mid - (double)lo, (double)hi - (double)mid) * (1.0 + std::ldexp(1.0, -18)));
     if (dg[h]) half = -1.0f;
     bnd[h] = make_float4(lo, hi, mid, half);
+    if (mfma == 3) {  // k_plane_upper_cull: (lim, limc) rounded up; degenerate never counted
+      auto up = [](double v) { float f = (float)v; return (double)f < v ? std::nextafter(f, INFINITY) : f; };
+      const float lim = up(thr + g);
+      bnd[h] = dg[h] ? make_float4(-1.0f, -INFINITY, 0.f, 0.f)
+                     : make_float4(lim, up((double)lim + 20.0 * std::ldexp(1.0, -24) * S), 0.f, 0.f);
+    }
   }
   *rc = 0;
   // one copy of the block laid out as count_carve placed it
@@ -832,12 +1254,13 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
                odg = w.degen - base;
   const size_t nch = ((size_t)H + 31) / 32, omf = reinterpret_cast<uint8_t*>(w.mfrag) - base,
                ohi = reinterpret_cast<uint8_t*>(w.mhi) - base;
-  st.assign(mfma ? ohi + nch * 32 * 4 : odg + H, 0);  // the caller keeps it alive until the stream is synchronised
+  const bool frags = mfma == 1 || mfma == 2;
+  st.assign(frags ? ohi + nch * 32 * 4 : odg + H, 0);  // the caller keeps it alive until the stream is synchronised
   std::memcpy(st.data(), p32.data(), H * sizeof(float4));
   std::memcpy(st.data() + ob, bnd.data(), H * sizeof(float4));
   std::memcpy(st.data() + o64, planes, 4 * H * sizeof(double));
   std::memcpy(st.data() + odg, dg.data(), H);
-  if (mfma) {
+  if (frags) {
     // k_plane_upper_mfma's B operand: hypothesis j is column j % 32 of chunk
     // j / 32; bf16 parts (round to nearest) of the float64 plane.  One MFMA:
     // lane r (ah bh ch dh | ah bh ch dl), lane r + 32 (al bl cl 0 | 0 0 0 0).
@@ -981,13 +1404,45 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   return 0;
 }
 
+// Morton order of the points for the culled sweep; mm_dev: the cloud's
+// min / max on the device (no host wait)
+static int bin_points(const float* xyz, int64_t n, const double* mm_dev, CountWs& w, hipStream_t s) {
+  const int kb = std::min(3, w.bits), lb = w.bits - kb, nb = 1 << (3 * kb), nl = 1 << (3 * lb);
+  const int nblk = (int)((n + kCBinChunk - 1) / kCBinChunk);
+  KTimer kt("plane_bin", s);
+  hipLaunchKernelGGL(k_cbin_hist, dim3(nblk), dim3(kCBinBlock), 0, s, xyz, n, mm_dev, w.bits, lb, nb, w.bh);
+  O3DX_TRY(exclusive_scan_i32(w.bh, w.bstart, (int64_t)nb * nblk, w.bscan, s));
+  hipLaunchKernelGGL(k_cbin_scatter, dim3(nblk), dim3(kCBinBlock), 0, s, xyz, n, mm_dev, w.bits, lb, nb, w.bstart,
+                     w.tmp);
+  hipLaunchKernelGGL(k_cbin_local, dim3(nb), dim3(kCBinLocalBlock), 0, s, w.tmp, w.bstart, nblk, nb, nl, n, w.sorted);
+  O3DX_HIP(hipMemsetAsync(w.sorted + n, 0xff, kCullCS * sizeof(float4), s));  // NaN rows
+  O3DX_HIP(hipGetLastError());
+  w.binned = true;
+  return 0;
+}
+
+// the upper sweep a call takes: 3 culled, 2 / 1 matrix cores, 0 VALU
+static int upper_mode(int64_t n, double smax, double thr) {
+  if (const char* ue = getenv("O3DX_RANSAC_UPPER")) {
+    if (std::strcmp(ue, "cull") == 0) return 3;
+    if (std::strcmp(ue, "mfma2") == 0) return 2;
+    if (std::strcmp(ue, "mfma") == 0) return 1;
+    return 0;
+  }
+  if (n >= kCullMinN) return 3;
+  return std::ldexp(1.0, MfmaShape<true>::kBoundExp) * smax <= 0.02 * thr ? 2 : 0;
+}
+
 // Upper bounds of the counts (k_plane_upper); degenerate hypotheses -1.
 static int run_count_upper(const float* xyz, int64_t n, const double* planes, int H, double thr, CountWs& w,
                            void* aabb_ws, double* mm_dev, hipStream_t s, std::vector<int64_t>& ub,
-                           const double* absmax_in = nullptr) {
+                           const double* absmax_in = nullptr, bool mm_ready = false) {
   double absmax[3];
   if (absmax_in) std::memcpy(absmax, absmax_in, sizeof(absmax));
-  else O3DX_TRY(absmax_of(xyz, n, aabb_ws, mm_dev, s, absmax));
+  else {
+    O3DX_TRY(absmax_of(xyz, n, aabb_ws, mm_dev, s, absmax));
+    mm_ready = true;
+  }
   std::vector<float4> p32;
   std::vector<float4> bnd;
   std::vector<uint8_t> dg;
@@ -1006,13 +1461,32 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
                      std::fabs(pl[3]);
     if (std::isfinite(S)) smax = std::max(smax, S);
   }
-  const char* ue = getenv("O3DX_RANSAC_UPPER");
-  int mfma = 0;
-  if (ue) mfma = std::strcmp(ue, "mfma2") == 0 ? 2 : std::strcmp(ue, "mfma") == 0 ? 1 : 0;
-  else if (std::ldexp(1.0, MfmaShape<true>::kBoundExp) * smax <= 0.02 * thr) mfma = 2;
+  const int mfma = upper_mode(n, smax, thr);
+  if (mfma == 3 && !w.binned) {
+    if (!mm_ready) O3DX_TRY(aabb_device(xyz, n, mm_dev, aabb_ws, s));
+    O3DX_TRY(bin_points(xyz, n, mm_dev, w, s));
+  }
   upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, st, s, &rc, &hmax, mfma);
   if (rc) return rc;
   KTimer kt("plane_count_upper", s);
+  if (mfma == 3) {
+    const int64_t nchunk = (n + kCullCS - 1) / kCullCS;
+    const int64_t rows = std::max<int64_t>(1, std::min<int64_t>((int64_t)(w.partial_ints / std::max(H, 1)), 2048));
+    // one resident wave per chunk stream: 5 blocks per CU (LDS ~30 KB each)
+    const int64_t per_block = kCullBlock / 64;
+    const unsigned gx = (unsigned)std::min<int64_t>(std::min<int64_t>(rows, kCullResident),
+                                                    (nchunk + per_block - 1) / per_block);
+    const unsigned gy = (unsigned)((H + kCullHG - 1) / kCullHG);
+    hipLaunchKernelGGL(k_plane_upper_cull, dim3(gx, gy), dim3(kCullBlock), 0, s, w.sorted, n, w.pl32, w.band, H,
+                       w.partial);
+    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, gx, H, w.counts, s));
+    hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
+    kt.stop();
+    ub.resize(H);
+    O3DX_TRY(read_back(ub.data(), w.counts, H * sizeof(int64_t), s));
+    O3DX_HIP(hipGetLastError());
+    return 0;
+  }
   if (mfma) {
     const int nch = (H + 31) / 32;
     auto launch_mfma = [&](auto kern, int tiles, int chunks) {
@@ -1239,7 +1713,9 @@ struct SegWs {
   double* mm;
   int64_t* cnt;
   int64_t* mom_part;
+  int64_t* mom_part2;
   int64_t* mom_out;
+  int64_t* fin;  // {inlier count, pad, first sums (6), second sums (12)}
 };
 
 static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
@@ -1253,8 +1729,10 @@ static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
   w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(n));
   w->aabb = ar.take<char>(aabb_ws_bytes(n));
   w->cnt = ar.take<int64_t>(4);
-  w->mom_part = ar.take<int64_t>((size_t)mom_blocks(n) * 12);
+  w->mom_part = ar.take<int64_t>((size_t)std::max<int64_t>(mom_blocks(n) * 12, (int64_t)grid_for(n, kBlock, 8192) * 6));
+  w->mom_part2 = ar.take<int64_t>((size_t)mom_blocks(n) * 12);
   w->mom_out = ar.take<int64_t>(16);
+  w->fin = ar.take<int64_t>(24);
   return ar.used;
 }
 
@@ -1573,6 +2051,9 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     std::memcpy(mmh, rb.data() + off_mm, sizeof(mmh));
     for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(mmh[a]), std::fabs(mmh[3 + a]));
   }
+  // the culled sweep's Morton order: queued now, it runs while the host
+  // computes the hypotheses
+  if (H > 0 && upper_mode(n, 0.0, thr) == 3) O3DX_TRY(bin_points(xyz, n, w.mm, w.cw, s));
   if (H > 0) {
     const float* sc = reinterpret_cast<const float*>(rb.data());
     std::vector<double> P((size_t)ransac_n * 3);
@@ -1586,7 +2067,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
   if (H > 0) {
     // upper bounds for all, exact counts for the hypotheses the replay consults
     std::vector<int64_t> counts;
-    O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax));
+    O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax, true));
     std::vector<uint8_t> known(H, 0);
     std::vector<double> sub;
     std::vector<int64_t> ec;
@@ -1614,23 +2095,45 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
   }
   double bp[4] = {0, 0, 0, 0};
   if (best >= 0) std::memcpy(bp, &planes[(size_t)4 * best], sizeof(bp));
-  int64_t k = 0;
+  // the inliers and GetPlaneFromPoints over them with one host wait: flags +
+  // first moments (one read of the cloud), compaction, the centroid and the
+  // second moments on the device; then {k, first sums, second sums} back
+  int64_t fin[20] = {0};
+  int q1[6], q2[6];
+  mom_fx_exps(A, false, q1);
+  mom_fx_exps(A, true, q2);
   if (!plane_is_zero(bp)) {
-    hipLaunchKernelGGL(k_plane_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, bp[0], bp[1], bp[2],
-                       bp[3], thr, w.flags);
-    O3DX_TRY(compact_flags(w.flags, n, inliers_out, nullptr, w.cnt, w.scan_tmp, s));
-    O3DX_TRY(read_back(&k, w.cnt, sizeof(int64_t), s));
+    MomScales sc1, sc2;
+    for (int a = 0; a < 6; ++a) {
+      sc1.s[a] = fx_scale(q1[a]);
+      sc2.s[a] = fx_scale(q2[a]);
+    }
+    const unsigned gf = grid_for(n, kBlock, 8192);
+    hipLaunchKernelGGL(k_plane_flags_sum, dim3(gf), dim3(kBlock), 0, s, xyz, n, bp[0], bp[1], bp[2], bp[3], thr, sc1,
+                       w.flags, w.mom_part);
+    O3DX_TRY(compact_flags(w.flags, n, inliers_out, nullptr, w.fin, w.scan_tmp, s));
+    O3DX_TRY(reduce_columns_i64(w.mom_part, gf, 6, w.fin + 2, s));
+    const int nb2 = mom_blocks(n);
+    hipLaunchKernelGGL(k_plane_moments_c, dim3(nb2), dim3(kBlock), 0, s, xyz, inliers_out, w.fin, w.fin + 2, q1[0],
+                       q1[1], q1[2], sc2, w.mom_part2);
+    O3DX_TRY(reduce_columns_i64(w.mom_part2, nb2, 12, w.fin + 8, s));
+    O3DX_HIP(hipGetLastError());
+    O3DX_TRY(read_back(fin, w.fin, sizeof(fin), s));
   }
+  const int64_t k = fin[0];
   *n_inliers_host = k;
   // GetPlaneFromPoints over the final inliers (zero plane when there are none)
   if (k == 0) {
     for (int a = 0; a < 4; ++a) plane_host[a] = 0;
     return 0;
   }
+  int64_t fx[24];
   double s1[6], s2[6], c[3];
-  O3DX_TRY(run_moments(xyz, inliers_out, k, nullptr, A, w.mom_part, w.mom_out, s, s1));
+  fx_pack(fin + 2, q1, 3, fx);
+  fx_to_double(fx, 3, s1);
   for (int a = 0; a < 3; ++a) c[a] = s1[a] / (double)k;
-  O3DX_TRY(run_moments(xyz, inliers_out, k, c, A, w.mom_part, w.mom_out, s, s2));
+  fx_pack(fin + 8, q2, 6, fx);
+  fx_to_double(fx, 6, s2);
   plane_from_centred(c, s2, plane_host);
   return 0;
 }

@@ -714,13 +714,13 @@ def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatc
     # sweep only the float32 window's
     p64 = pts.astype(np.float64)
     S_h = np.abs(planes[:, :3]) @ np.abs(p64).max(0) + np.abs(planes[:, 3])
-    for env in (None, "mfma", "mfma2", "32x16x6"):
+    for env in (None, "cull", "mfma", "mfma2", "32x16x6"):
         if env:
             monkeypatch.setenv("O3DX_RANSAC_UPPER", env)
         ub = ops.plane_count_upper(x, planes, thr)
         monkeypatch.delenv("O3DX_RANSAC_UPPER", raising=False)
         assert np.array_equal(ub < 0, got < 0) and (ub >= got).all()
-        if env == "32x16x6":
+        if env in ("32x16x6", "cull"):
             assert (ub - got).max() <= max(8, n // 10000)  # only window points add
         elif n <= 100_003 and env:
             d = np.abs(p64 @ planes[:, :3].T + planes[:, 3])
@@ -771,6 +771,66 @@ def test_mfma2_sweep_error_within_documented_bound(dev, monkeypatch):
     assert (lo <= got).all() and (got <= hi).all(), (lo, got, hi)
     ub = ops.plane_count_upper(x, planes, thr)
     assert (ub >= (d < thr).sum(0)).all()
+
+
+@pytest.mark.parametrize("layout", ["straddle", "cube_plane"])
+def test_culled_sweep_within_float32_band(dev, monkeypatch, layout):
+    """The culled sweep (k_plane_upper_cull) counts |d32| < lim_h
+    over the pairs its box test keeps, lim_h = thr + 6 2^-24 S_h + 2^-20 thr
+    rounded up, and the box test drops no pair that count would take: every
+    float64 inlier is counted (|d| < thr) and nothing at |d| >= lim_h + 4
+    2^-24 S_h.  'straddle': 2048 points per hypothesis at |d| = thr + u
+    2^-22 S_h (inside the band, scattered over the cloud's box); 'cube_plane':
+    a uniform cube with a planted plane and 300 random hypotheses, with the
+    chunks' boxes both inside and outside the slabs."""
+    rng = np.random.default_rng(23)
+    thr = 0.01
+    if layout == "straddle":
+        H, per = 32, 2048
+        nrm = rng.normal(size=(H, 3))
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        off = rng.uniform(-0.3, 0.3, H)
+        planes = np.concatenate([nrm, off[:, None]], 1)
+        S_est = np.abs(nrm).sum(1) + np.abs(off)
+        pts = []
+        for h in range(H):
+            b = rng.uniform(-1, 1, (per, 3))
+            b = b - ((b @ nrm[h]) + off[h])[:, None] * nrm[h]
+            u = rng.uniform(-1, 1, per)
+            sgn = rng.choice([-1.0, 1.0], per)
+            pts.append(b + (sgn * (thr + u * 2.0 ** -22 * S_est[h]))[:, None] * nrm[h])
+        p32 = np.concatenate(pts).astype(np.float32)
+    else:
+        n = 200_000
+        p32 = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+        on = rng.uniform(size=n) < 0.2
+        p32[on, 2] = (0.5 + 0.002 * rng.normal(size=on.sum())).astype(np.float32)
+        idx = rng.integers(0, n, (300, 3))
+        a, b, c = (p32[idx[:, k]].astype(np.float64) for k in range(3))
+        nrm = np.cross(b - a, c - a)
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        planes = np.concatenate([nrm, -np.sum(nrm * a, 1, keepdims=True)], 1)
+    p64 = p32.astype(np.float64)
+    S_h = np.abs(planes[:, :3]) @ np.abs(p64).max(0) + np.abs(planes[:, 3])
+    d = np.abs(p64 @ planes[:, :3].T + planes[:, 3])
+    g = 6 * 2.0 ** -24 * S_h + 2.0 ** -20 * thr
+    lim = (thr + g).astype(np.float32).astype(np.float64)
+    lim = np.where(lim < thr + g, np.nextafter(lim.astype(np.float32), np.float32(np.inf)).astype(np.float64), lim)
+    x = torch.from_numpy(p32).to(dev)
+    monkeypatch.setenv("O3DX_RANSAC_UPPER", "cull")
+    got = ops.plane_count_upper(x, planes, thr)
+    lo = (d < thr).sum(0)
+    hi = (d < lim + 4 * 2.0 ** -24 * S_h).sum(0)
+    assert (lo <= got).all() and (got <= hi).all(), (lo, got, hi)
+    # no pair the float32 count takes is culled: |d| < lim_h - 4 2^-24 S_h is counted
+    lo2 = (d < lim - 4.5 * 2.0 ** -24 * S_h).sum(0)
+    assert (lo2 <= got).all(), (lo2, got)
+    if layout == "straddle":
+        assert (lo2 > lo + per // 4).all()  # the band points are inside lim_h: counted
+    monkeypatch.setenv("O3DX_RANSAC_UPPER", "32x16x6")  # the dense VALU sweep: same semantics, no culling
+    dense = ops.plane_count_upper(x, planes, thr)
+    assert (lo <= dense).all()
+    assert np.abs(dense - got).max() <= max(2, 0.001 * lo.max()), (dense, got)
 
 
 @pytest.mark.parametrize("n", [1_000_000])

@@ -1,7 +1,7 @@
 """Focused driver for rocprofv3 (kernel trace / PMC): normals on the C2 reps,
 converged ICP accumulate, RANSAC, the RANSAC count alone, ICP's first
 iteration; a few launches each.  GPU box only.
-Usage: python tools/prof_kernels.py [all|normals|icp|icp_loop|ransac|ransac_count|icp_first]"""
+Usage: python tools/prof_kernels.py [all|normals|icp|icp_loop|ransac|ransac_upper|ransac_count|icp_first]"""
 import os
 import sys
 
@@ -47,6 +47,17 @@ if what in ("all", "ransac"):
     samples = ops.ransac_samples(N, 3, 1000, seed=7)
     for _ in range(2):
         ops.segment_plane(pts, 0.01, 3, 1000, samples=samples)
+    torch.cuda.synchronize()
+if what == "ransac_upper":  # the upper-bound sweep alone (O3DX_RANSAC_UPPER picks it), three calls
+    pts = S.planted_plane(N, 3, device=dev)
+    idx = np.random.default_rng(0).integers(0, N, (1000, 3))
+    p64 = pts.cpu().numpy().astype(np.float64)
+    a, b, c = p64[idx[:, 0]], p64[idx[:, 1]], p64[idx[:, 2]]
+    nrm = np.cross(b - a, c - a)
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-300)
+    planes = np.concatenate([nrm, -np.sum(nrm * a, 1, keepdims=True)], 1)
+    for _ in range(3):
+        ops.plane_count_upper(pts, planes, 0.01)
     torch.cuda.synchronize()
 if what == "ransac_count":
     pts = S.planted_plane(N, 3, device=dev)
