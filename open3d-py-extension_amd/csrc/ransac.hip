@@ -514,7 +514,7 @@ k_plane_upper_mfma(const float* __restrict__ xyz, int64_t n, const uint4* __rest
 // limc_h = lim_h + 20 2^-24 S_h (rounded up) never drops a pair the float32
 // count would take.  The counts are the same upper bounds as k_plane_upper's
 // (a pair counted here is counted there); the work is the surviving pairs.
-constexpr int kCullBlock = 512;    // 8 waves
+constexpr int kCullBlock = 512;    // 8 waves (LDS ~30 KB per block, 34 KB for the exact form)
 constexpr int kCullHG = 1024;      // hypotheses per block row (LDS ~29 KB)
 constexpr int kCullMinN = 4096;    // smaller clouds keep the dense sweeps
 constexpr int kCullCS = 128;       // points per chunk (one wave)
@@ -561,15 +561,15 @@ __device__ __forceinline__ uint32_t bin_key(const BinGeom& g, float x, float y, 
 // then cell order is the Morton order of the full grid.  Pass 1: per-block
 // brick histograms (LDS), brick-major, scanned on the device; pass 2: the
 // block's points sorted by brick in an LDS stage, then written as runs (one
-// run per brick and block: coalesced), the local cell in .w; pass 3: one
-// workgroup per brick sorts its range by local cell (LDS counts).
+// run per brick and block: coalesced), the local cell in .w; pass 3: tiles
+// of each brick sorted by local cell (below).  Both sorts stage the points
+// themselves in LDS, so global reads and writes stay in address order.
 // The order inside a cell is the LDS atomics' (the sweep does not care).
 constexpr int kCBinBlock = 1024;
-constexpr int kCBinPer = 8;
-constexpr int kCBinChunk = kCBinBlock * kCBinPer;  // points per block, passes 1-2 (13-bit local index)
+constexpr int kCBinPer = 4;
+constexpr int kCBinChunk = kCBinBlock * kCBinPer;  // points per block and per tile (LDS stage 64 KB)
 constexpr int kCBinMaxBricks = 512;
 constexpr int kCBinMaxLocal = 512;
-constexpr int kCBinLocalBlock = 1024;  // pass 3: a workgroup per brick
 
 __global__ void __launch_bounds__(kCBinBlock) k_cbin_hist(const float* __restrict__ xyz, int64_t n,
                                                           const double* __restrict__ mm, int bits, int lb, int nb,
@@ -596,8 +596,7 @@ __global__ void __launch_bounds__(kCBinBlock) k_cbin_scatter(const float* __rest
                                                              const double* __restrict__ mm, int bits, int lb, int nb,
                                                              const int32_t* __restrict__ bstart,
                                                              float4* __restrict__ tmp) {
-  static_assert(kCBinChunk <= 8192 && kCBinMaxBricks <= 512 && kCBinMaxLocal <= 512, "stage entry: 13 + 9 + 9 bits");
-  __shared__ uint32_t stage[kCBinChunk];  // (local index << 18) | (brick << 9) | cell, sorted by brick
+  __shared__ float4 stage[kCBinChunk];  // the block's points sorted by brick, .w = (brick << 9) | cell
   __shared__ int32_t lstart[kCBinMaxBricks], cur[kCBinMaxBricks];
   __shared__ int32_t wsum[kCBinBlock / 64 + 1];
   const BinGeom g = bin_geom(mm, bits);
@@ -606,16 +605,17 @@ __global__ void __launch_bounds__(kCBinBlock) k_cbin_scatter(const float* __rest
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kCBinChunk;
   const uint32_t lmask = (1u << (3 * lb)) - 1u;
+  P3 v[kCBinPer];
   uint32_t code[kCBinPer];
 #pragma unroll
   for (int j = 0; j < kCBinPer; ++j) {
     const int64_t i = base + threadIdx.x + (int64_t)j * kCBinBlock;
     code[j] = ~0u;
     if (i < n) {
-      const P3 v = p[i];
-      const uint32_t key = bin_key(g, v.x, v.y, v.z);
+      v[j] = p[i];
+      const uint32_t key = bin_key(g, v[j].x, v[j].y, v[j].z);
       const uint32_t k = key >> (3 * lb);
-      code[j] = ((uint32_t)(threadIdx.x + j * kCBinBlock) << 18) | (k << 9) | (key & lmask);
+      code[j] = (k << 9) | (key & lmask);
       atomicAdd(&cur[k], 1);
     }
   }
@@ -625,70 +625,90 @@ __global__ void __launch_bounds__(kCBinBlock) k_cbin_scatter(const float* __rest
   int tot;
   const int ex = block_excl_scan<kCBinBlock>(c, wsum, &tot);
   if (threadIdx.x < nb) {
-    lstart[threadIdx.x] = ex;
+    // lstart: global address of stage slot 0 for brick k (the block's run start - its stage start)
+    lstart[threadIdx.x] = bstart[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] - ex;
     cur[threadIdx.x] = ex;
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kCBinPer; ++j)
-    if (code[j] != ~0u) stage[atomicAdd(&cur[(code[j] >> 9) & 511u], 1)] = code[j];
+    if (code[j] != ~0u)
+      stage[atomicAdd(&cur[code[j] >> 9], 1)] = make_float4(v[j].x, v[j].y, v[j].z, __int_as_float((int)code[j]));
   __syncthreads();
   // stage slot t of brick k -> the block's run of brick k, consecutive
   for (int t = threadIdx.x; t < tot; t += kCBinBlock) {
-    const uint32_t e = stage[t];
-    const int k = (int)((e >> 9) & 511u);
-    const P3 v = p[base + (e >> 18)];
-    tmp[bstart[(int64_t)k * gridDim.x + blockIdx.x] + (t - lstart[k])] =
-        make_float4(v.x, v.y, v.z, __int_as_float((int)(e & 511u)));
+    const float4 e = stage[t];
+    const uint32_t cd = (uint32_t)__float_as_int(e.w);
+    tmp[(int64_t)lstart[cd >> 9] + t] = make_float4(e.x, e.y, e.z, __int_as_float((int)(cd & 511u)));
   }
 }
 
-__global__ void __launch_bounds__(kCBinLocalBlock) k_cbin_local(const float4* __restrict__ tmp,
-                                                                const int32_t* __restrict__ bstart, int nblk,
-                                                                int nb, int nl, int64_t n, float4* __restrict__ out) {
-  constexpr int B = kCBinLocalBlock, U = 4;  // points per thread per step (loads first)
+// Pass 3 works on tiles: every brick's range cut into pieces of at most
+// kCBinChunk points (so a tile never holds two bricks), listed by one
+// workgroup; each tile is sorted by local cell in LDS on its own and written
+// back in place order (coalesced).  A tile covers its whole brick, so a chunk
+// of the sweep is 1 / (tile / chunk) of the brick along each axis at worst.
+__global__ void __launch_bounds__(kCBinBlock) k_cbin_tiles(const int32_t* __restrict__ bstart, int nblk, int nb,
+                                                           int64_t n, int2* __restrict__ tiles,
+                                                           int32_t* __restrict__ ntiles) {
+  __shared__ int32_t wsum[kCBinBlock / 64 + 1];
+  const int k = threadIdx.x;
+  int64_t s0 = 0, s1 = 0;
+  if (k < nb) {
+    s0 = bstart[(int64_t)k * nblk];
+    s1 = k + 1 < nb ? bstart[(int64_t)(k + 1) * nblk] : n;
+  }
+  const int cnt = (int)((s1 - s0 + kCBinChunk - 1) / kCBinChunk);
+  int tot;
+  const int at = block_excl_scan<kCBinBlock>(cnt, wsum, &tot);
+  for (int t = 0; t < cnt; ++t)
+    tiles[at + t] = make_int2((int)(s0 + (int64_t)t * kCBinChunk), (int)min<int64_t>(s0 + (int64_t)(t + 1) * kCBinChunk, s1));
+  if (threadIdx.x == 0) *ntiles = tot;
+}
+
+__global__ void __launch_bounds__(kCBinBlock) k_cbin_local(const float4* __restrict__ tmp,
+                                                           const int2* __restrict__ tiles,
+                                                           const int32_t* __restrict__ ntiles, int nl,
+                                                           float4* __restrict__ out) {
+  __shared__ float4 stage[kCBinChunk];  // the tile sorted by local cell
   __shared__ int32_t cnt[kCBinMaxLocal];
-  __shared__ int32_t wsum[B / 64 + 1];
-  const int k = blockIdx.x;
-  const int64_t s0 = bstart[(int64_t)k * nblk], s1 = k + 1 < nb ? bstart[(int64_t)(k + 1) * nblk] : n;
-  for (int c = threadIdx.x; c < nl; c += B) cnt[c] = 0;
+  __shared__ int32_t wsum[kCBinBlock / 64 + 1];
+  if ((int)blockIdx.x >= *ntiles) return;  // block-uniform: before any barrier
+  const int2 tl = tiles[blockIdx.x];
+  const int s0 = tl.x, m = tl.y - tl.x;
+  for (int c = threadIdx.x; c < nl; c += kCBinBlock) cnt[c] = 0;
   __syncthreads();
-  for (int64_t q0 = s0; q0 < s1; q0 += B * U) {
-    int cl[U];
+  float4 v[kCBinPer];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t q = q0 + threadIdx.x + u * B;
-      cl[u] = q < s1 ? __float_as_int(tmp[q].w) : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (cl[u] >= 0) atomicAdd(&cnt[cl[u]], 1);
+  for (int j = 0; j < kCBinPer; ++j) {
+    const int t = threadIdx.x + j * kCBinBlock;
+    v[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    if (t < m) v[j] = tmp[s0 + t];
+    if (t < m) atomicAdd(&cnt[__float_as_int(v[j].w)], 1);
   }
   __syncthreads();
-  const int span = (nl + B - 1) / B;
+  const int span = (nl + kCBinBlock - 1) / kCBinBlock;
   const int c0 = threadIdx.x * span, c1 = min(c0 + span, nl);
   int run = 0;
   for (int c = c0; c < c1; ++c) run += cnt[c];
   int tot;
-  int ex = block_excl_scan<B>(run, wsum, &tot);
+  int ex = block_excl_scan<kCBinBlock>(run, wsum, &tot);
   for (int c = c0; c < c1; ++c) {
-    const int v = cnt[c];
+    const int u = cnt[c];
     cnt[c] = ex;
-    ex += v;
+    ex += u;
   }
   __syncthreads();
-  for (int64_t q0 = s0; q0 < s1; q0 += B * U) {
-    float4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t q = q0 + threadIdx.x + u * B;
-      v[u] = q < s1 ? tmp[q] : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-    }
+  for (int j = 0; j < kCBinPer; ++j) {
+    const int cl = __float_as_int(v[j].w);
+    if (cl >= 0) stage[atomicAdd(&cnt[cl], 1)] = make_float4(v[j].x, v[j].y, v[j].z, 0.0f);
+  }
+  __syncthreads();
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int cl = __float_as_int(v[u].w);
-      if (cl >= 0) out[s0 + atomicAdd(&cnt[cl], 1)] = make_float4(v[u].x, v[u].y, v[u].z, 0.0f);
-    }
+  for (int j = 0; j < kCBinPer; ++j) {
+    const int t = threadIdx.x + j * kCBinBlock;
+    if (t < m) out[s0 + t] = stage[t];
   }
 }
 
@@ -721,20 +741,27 @@ __device__ __forceinline__ float wave_max_f(float v) {
 
 // grid: (blocks over chunks of kCullCS points, hypothesis rows of kCullHG);
 // pts: the Morton-ordered points, padded with NaN rows to a whole chunk;
-// pl32 [H] float32 planes, lims [H] = (lim, limc, -, -) (degenerate: -1,
-// -inf); partial [block x][H] int32 counts.  Per chunk a wave takes the box
-// of its finite points, tests the hypotheses 64 at a time (lane = hypothesis,
+// pl32 [H] float32 planes, pl64 [H] the float64 planes, lims [H] = (hi, limc,
+// lo, -) (degenerate: -1, -inf, -1); partial [block x][H] int32 counts —
+// EXACT counts of Open3D's predicate.  Per chunk a wave takes the box of its
+// finite points, tests the hypotheses 64 at a time (lane = hypothesis,
 // coefficients from LDS) and lists the survivors in LDS; every 64 listed
 // survivors (and the rest at the end) are counted with lane = hypothesis and
 // the chunk's points read by scalar loads (wave-uniform addresses): three
-// fmas, a compare and an add per (point, hypothesis).
+// fmas, two compares and an add per (point, hypothesis).  |d32| < lo is an
+// inlier and |d32| >= hi is not (k_plane_count's band, lo / hi = thr -/+ g_h
+// rounded outwards); a hypothesis with a point in between re-counts the chunk
+// in float64 as Open3D evaluates it (rare: the band is ~1e-7 relative).
+template <bool EXACT>
 __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* __restrict__ pts, int64_t n,
                                                                  const float4* __restrict__ pl32,
-                                                                 const float4* __restrict__ lims, int H,
+                                                                 const double* __restrict__ pl64,
+                                                                 const float4* __restrict__ lims, int H, double thr,
                                                                  int32_t* __restrict__ partial) {
   constexpr int kW = kCullBlock / 64, CS = kCullCS;
   __shared__ float4 lpl[kCullHG];
-  __shared__ float2 llim[kCullHG];
+  __shared__ float2 llim[kCullHG];               // (hi, limc)
+  __shared__ float llo[EXACT ? kCullHG : 1];     // lo (the exact form)
   __shared__ int32_t lcnt[kCullHG];
   __shared__ uint16_t lst[kW][128];
   const int h0 = blockIdx.y * kCullHG, hn = min(kCullHG, H - h0);
@@ -742,6 +769,7 @@ __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* _
     lpl[t] = pl32[h0 + t];
     const float4 l = lims[h0 + t];
     llim[t] = make_float2(l.x, l.y);
+    if constexpr (EXACT) llo[t] = l.z;
     lcnt[t] = 0;
   }
   __syncthreads();
@@ -793,8 +821,10 @@ __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* _
       const bool act = lane < g;
       const int h = act ? (int)lst[wv][lane] : 0;
       const float4 p = lpl[h];
-      const float lim = act ? llim[h].x : -1.0f;
-      int cnt = 0;
+      const float hi = act ? llim[h].x : -1.0f;
+      float lo = -1.0f;
+      if constexpr (EXACT) lo = act ? llo[h] : -1.0f;
+      int cnt = 0, chi = 0;  // |d32| < lo and |d32| < hi: they differ when a point is in the band
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
       for (int k0 = 0; k0 < CS; k0 += kCullPB) {
         float4 q[kCullPB];
@@ -802,9 +832,29 @@ __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* _
         for (int j = 0; j < kCullPB; ++j) q[j] = cp[k0 + j];  // scalar loads
 #pragma unroll
         for (int j = 0; j < kCullPB; ++j) {
-          const float d = fmaf(p.x, q[j].x, fmaf(p.y, q[j].y, fmaf(p.z, q[j].z, p.w)));
-          cnt += fabsf(d) < lim ? 1 : 0;
+          const float ad = fabsf(fmaf(p.x, q[j].x, fmaf(p.y, q[j].y, fmaf(p.z, q[j].z, p.w))));
+          if constexpr (EXACT) cnt += ad < lo ? 1 : 0;
+          chi += ad < hi ? 1 : 0;
         }
+      }
+      if constexpr (!EXACT) {  // the upper bound: |d32| < hi
+        if (act && chi) atomicAdd(&lcnt[h], chi);
+        return;
+      }
+      const bool band = chi != cnt;
+      // rare: a hypothesis with a point in the band re-counts the chunk with
+      // the float64 predicate, lane = point (the chunk is in registers)
+      uint64_t bm = __ballot(band);
+      while (bm) {
+        const int b = __builtin_ctzll(bm);
+        bm &= bm - 1;
+        const int hb = __builtin_amdgcn_readlane(h, b);
+        const double* q64 = pl64 + 4 * (int64_t)(h0 + hb);  // wave-uniform: scalar loads
+        const double pd[4] = {q64[0], q64[1], q64[2], q64[3]};
+        int ex = 0;
+#pragma unroll
+        for (int j = 0; j < CS / 64; ++j) ex += __popcll(__ballot(plane_dist64(pd, cur[j].x, cur[j].y, cur[j].z) < thr));
+        cnt = o3dx_writelane(ex, b, cnt);
       }
       if (act && cnt) atomicAdd(&lcnt[h], cnt);
     };
@@ -1164,11 +1214,14 @@ struct CountWs {
   // culled sweep: Morton-ordered copy of the points and its counting sort
   float4* sorted;
   float4* tmp;
+  int2* tiles;
+  int32_t* ntiles;
   int32_t* bh;
   int32_t* bstart;
   int32_t* bscan;
   int bits;
-  bool binned;  // sorted holds this call's points
+  bool binned;        // sorted holds this call's points
+  bool exact_counts;  // the last run_count_upper counted exactly (the culled sweep)
 };
 
 // grid bits per axis of the culled sweep's Morton order: ~8 points per cell
@@ -1197,10 +1250,13 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   const int64_t nbh = (int64_t)kCBinMaxBricks * ((n + kCBinChunk - 1) / kCBinChunk);
   w->sorted = ar.take<float4>((size_t)n + kCullCS);  // + NaN rows to a whole chunk
   w->tmp = ar.take<float4>((size_t)n);
+  w->tiles = ar.take<int2>((size_t)(n + kCBinChunk - 1) / kCBinChunk + kCBinMaxBricks);
+  w->ntiles = ar.take<int32_t>(4);
   w->bh = ar.take<int32_t>((size_t)nbh + 1);
   w->bstart = ar.take<int32_t>((size_t)nbh + 1);
   w->bscan = ar.take<int32_t>(scan_workspace_ints(nbh + 1));
   w->binned = false;
+  w->exact_counts = false;
   return ar.used;
 }
 
@@ -1240,11 +1296,13 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
     float half = (float)(std::max((double)mid - (double)lo, (double)hi - (double)mid) * (1.0 + std::ldexp(1.0, -18)));
     if (dg[h]) half = -1.0f;
     bnd[h] = make_float4(lo, hi, mid, half);
-    if (mfma == 3) {  // k_plane_upper_cull: (lim, limc) rounded up; degenerate never counted
+    if (mfma == 3) {  // k_plane_upper_cull: (hi, limc) rounded up, lo down; degenerate never counted
       auto up = [](double v) { float f = (float)v; return (double)f < v ? std::nextafter(f, INFINITY) : f; };
+      auto down = [](double v) { float f = (float)v; return (double)f > v ? std::nextafter(f, -INFINITY) : f; };
       const float lim = up(thr + g);
-      bnd[h] = dg[h] ? make_float4(-1.0f, -INFINITY, 0.f, 0.f)
-                     : make_float4(lim, up((double)lim + 20.0 * std::ldexp(1.0, -24) * S), 0.f, 0.f);
+      const float lo_c = thr - g > 0 ? down(thr - g) : 0.0f;
+      bnd[h] = dg[h] ? make_float4(-1.0f, -INFINITY, -1.0f, 0.f)
+                     : make_float4(lim, up((double)lim + 20.0 * std::ldexp(1.0, -24) * S), lo_c, 0.f);
     }
   }
   *rc = 0;
@@ -1414,7 +1472,8 @@ static int bin_points(const float* xyz, int64_t n, const double* mm_dev, CountWs
   O3DX_TRY(exclusive_scan_i32(w.bh, w.bstart, (int64_t)nb * nblk, w.bscan, s));
   hipLaunchKernelGGL(k_cbin_scatter, dim3(nblk), dim3(kCBinBlock), 0, s, xyz, n, mm_dev, w.bits, lb, nb, w.bstart,
                      w.tmp);
-  hipLaunchKernelGGL(k_cbin_local, dim3(nb), dim3(kCBinLocalBlock), 0, s, w.tmp, w.bstart, nblk, nb, nl, n, w.sorted);
+  hipLaunchKernelGGL(k_cbin_tiles, dim3(1), dim3(kCBinBlock), 0, s, w.bstart, nblk, nb, n, w.tiles, w.ntiles);
+  hipLaunchKernelGGL(k_cbin_local, dim3(nblk + nb), dim3(kCBinBlock), 0, s, w.tmp, w.tiles, w.ntiles, nl, w.sorted);
   O3DX_HIP(hipMemsetAsync(w.sorted + n, 0xff, kCullCS * sizeof(float4), s));  // NaN rows
   O3DX_HIP(hipGetLastError());
   w.binned = true;
@@ -1461,7 +1520,12 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
                      std::fabs(pl[3]);
     if (std::isfinite(S)) smax = std::max(smax, S);
   }
-  const int mfma = upper_mode(n, smax, thr);
+  int mfma = upper_mode(n, smax, thr);
+  // the culled sweep's sure band needs thr - g_h > 0; tiny thresholds (or
+  // non-finite bounds) take the dense sweeps
+  if (mfma == 3 && !(6.0 * std::ldexp(1.0, -24) * smax + std::ldexp(1.0, -20) * thr < 0.5 * thr))
+    mfma = std::ldexp(1.0, MfmaShape<true>::kBoundExp) * smax <= 0.02 * thr ? 2 : 0;
+  w.exact_counts = false;
   if (mfma == 3 && !w.binned) {
     if (!mm_ready) O3DX_TRY(aabb_device(xyz, n, mm_dev, aabb_ws, s));
     O3DX_TRY(bin_points(xyz, n, mm_dev, w, s));
@@ -1477,8 +1541,11 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
     const unsigned gx = (unsigned)std::min<int64_t>(std::min<int64_t>(rows, kCullResident),
                                                     (nchunk + per_block - 1) / per_block);
     const unsigned gy = (unsigned)((H + kCullHG - 1) / kCullHG);
-    hipLaunchKernelGGL(k_plane_upper_cull, dim3(gx, gy), dim3(kCullBlock), 0, s, w.sorted, n, w.pl32, w.band, H,
-                       w.partial);
+    // O3DX_RANSAC_CULL_EXACT (tests, A/B): the exact form over every hypothesis
+    const bool exact = getenv("O3DX_RANSAC_CULL_EXACT") != nullptr;
+    w.exact_counts = exact;
+    hipLaunchKernelGGL(exact ? k_plane_upper_cull<true> : k_plane_upper_cull<false>, dim3(gx, gy), dim3(kCullBlock), 0,
+                       s, w.sorted, n, w.pl32, w.pl64, w.band, H, thr, w.partial);
     O3DX_TRY(reduce_columns_i32_to_i64(w.partial, gx, H, w.counts, s));
     hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
     kt.stop();
@@ -2068,7 +2135,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     // upper bounds for all, exact counts for the hypotheses the replay consults
     std::vector<int64_t> counts;
     O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax, true));
-    std::vector<uint8_t> known(H, 0);
+    std::vector<uint8_t> known(H, w.cw.exact_counts ? 1 : 0);  // the culled sweep's counts are exact
     std::vector<double> sub;
     std::vector<int64_t> ec;
     for (;;) {

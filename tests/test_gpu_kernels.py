@@ -720,7 +720,7 @@ def test_plane_count_counters_equal_ballot_and_oracle(dev, n, H, thr, monkeypatc
         ub = ops.plane_count_upper(x, planes, thr)
         monkeypatch.delenv("O3DX_RANSAC_UPPER", raising=False)
         assert np.array_equal(ub < 0, got < 0) and (ub >= got).all()
-        if env in ("32x16x6", "cull"):
+        if env in ("32x16x6", "cull") or (env is None and n >= 4096):
             assert (ub - got).max() <= max(8, n // 10000)  # only window points add
         elif n <= 100_003 and env:
             d = np.abs(p64 @ planes[:, :3].T + planes[:, 3])
@@ -773,16 +773,25 @@ def test_mfma2_sweep_error_within_documented_bound(dev, monkeypatch):
     assert (ub >= (d < thr).sum(0)).all()
 
 
+def _open3d_counts(p64, planes, thr):
+    # Open3D's EvaluateRANSACBasedOnDistance predicate in its own order,
+    # |(a x + c z) + (b y + d)| < thr, elementwise float64 (no fma)
+    a, b, c, d = (planes[:, k][None, :] for k in range(4))
+    x, y, z = (p64[:, k][:, None] for k in range(3))
+    return (np.abs((a * x + c * z) + (b * y + d)) < thr).sum(0)
+
+
 @pytest.mark.parametrize("layout", ["straddle", "cube_plane"])
-def test_culled_sweep_within_float32_band(dev, monkeypatch, layout):
-    """The culled sweep (k_plane_upper_cull) counts |d32| < lim_h
-    over the pairs its box test keeps, lim_h = thr + 6 2^-24 S_h + 2^-20 thr
-    rounded up, and the box test drops no pair that count would take: every
-    float64 inlier is counted (|d| < thr) and nothing at |d| >= lim_h + 4
-    2^-24 S_h.  'straddle': 2048 points per hypothesis at |d| = thr + u
-    2^-22 S_h (inside the band, scattered over the cloud's box); 'cube_plane':
-    a uniform cube with a planted plane and 300 random hypotheses, with the
-    chunks' boxes both inside and outside the slabs."""
+def test_culled_sweep_counts_exactly(dev, monkeypatch, layout):
+    """The culled sweep (k_plane_upper_cull): its exact form
+    counts EXACTLY (|d32| < lo_h sure, |d32| >= hi_h out, the band between
+    re-decided in float64 in Open3D's order; the box test drops no pair that
+    could count); its upper form counts |d32| < hi_h, an upper bound.
+    'straddle': 2048 points per hypothesis at |d| = thr + u 2^-22 S_h (inside
+    the float32 band, scattered over the cloud's box: the float64 path runs
+    for most chunks); 'cube_plane': a uniform cube with a planted plane and 300
+    random hypotheses, the chunks' boxes both inside and outside the slabs.
+    The counts equal Open3D's predicate and the dense exact count."""
     rng = np.random.default_rng(23)
     thr = 0.01
     if layout == "straddle":
@@ -818,19 +827,20 @@ def test_culled_sweep_within_float32_band(dev, monkeypatch, layout):
     lim = np.where(lim < thr + g, np.nextafter(lim.astype(np.float32), np.float32(np.inf)).astype(np.float64), lim)
     x = torch.from_numpy(p32).to(dev)
     monkeypatch.setenv("O3DX_RANSAC_UPPER", "cull")
-    got = ops.plane_count_upper(x, planes, thr)
-    lo = (d < thr).sum(0)
-    hi = (d < lim + 4 * 2.0 ** -24 * S_h).sum(0)
-    assert (lo <= got).all() and (got <= hi).all(), (lo, got, hi)
-    # no pair the float32 count takes is culled: |d| < lim_h - 4 2^-24 S_h is counted
-    lo2 = (d < lim - 4.5 * 2.0 ** -24 * S_h).sum(0)
-    assert (lo2 <= got).all(), (lo2, got)
-    if layout == "straddle":
-        assert (lo2 > lo + per // 4).all()  # the band points are inside lim_h: counted
-    monkeypatch.setenv("O3DX_RANSAC_UPPER", "32x16x6")  # the dense VALU sweep: same semantics, no culling
-    dense = ops.plane_count_upper(x, planes, thr)
-    assert (lo <= dense).all()
-    assert np.abs(dense - got).max() <= max(2, 0.001 * lo.max()), (dense, got)
+    ub = ops.plane_count_upper(x, planes, thr)  # the upper-bound form (segment_plane's sweep)
+    monkeypatch.setenv("O3DX_RANSAC_CULL_EXACT", "1")
+    got = ops.plane_count_upper(x, planes, thr)  # the exact form (segment_plane's exact rounds)
+    monkeypatch.delenv("O3DX_RANSAC_CULL_EXACT")
+    ref = _open3d_counts(p64, planes, thr)
+    assert (ub >= ref).all()
+    if layout != "straddle":  # (straddle puts its points in the band on purpose)
+        assert (ub - ref).max() <= max(8, len(p32) // 10000)
+    assert np.array_equal(got, ref), np.nonzero(got != ref)
+    if layout == "straddle":  # each hypothesis' own points straddle thr: about half are inliers
+        own = np.array([_open3d_counts(p64[h * per:(h + 1) * per], planes[h:h + 1], thr)[0] for h in range(H)])
+        assert ((own > per // 4) & (own < 3 * per // 4)).all()
+    monkeypatch.delenv("O3DX_RANSAC_UPPER")
+    assert np.array_equal(ops.plane_count(x, planes, thr), ref)  # the dense exact count agrees
 
 
 @pytest.mark.parametrize("n", [1_000_000])
