@@ -475,6 +475,16 @@ def c4_headline(dev, args, world, rank):
     elapsed = max_over_ranks(t1 - t0, world, dev)
     m = torch.tensor([rg.numel()], dtype=torch.int64, device=comm_dev(dev))
     dist.all_reduce(m)
+    # one more (untimed) step with host timestamps at each phase end: where
+    # the host waits (bounds, halo counts, verdict) and what they cost
+    barrier(world, dev)
+    tl = {}
+    t2 = time.perf_counter()
+    D.voxel_normals_slabs(pts, gidx, vs, knn=args.knn, presorted=True, timings=tl)
+    tl["returned"] = round((time.perf_counter() - t2) * 1e3, 4)
+    torch.cuda.synchronize()
+    tl["synchronized"] = round((time.perf_counter() - t2) * 1e3, 4)
+    c4_headline.host_timeline = tl
     return elapsed, int(m.item()), int(pts.shape[0])
 
 
@@ -756,6 +766,7 @@ def main_multi(args, world, rank, dev):
                                      "kernel_ms_all_ranks": round(k_all, 4), "gpu_shared_by_ranks": shared,
                                      "host_frac": round(max(0.0, 1.0 - busy / wall), 4) if wall > 0 else None},
                   "collectives": "all_reduce (AABB, halo proof), all_to_all (halo representatives)",
+                  "host_timeline_rank0_ms": getattr(c4_headline, "host_timeline", None),
                   "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps / elapsed / 1e9, 2)},
     }
     torch.cuda.empty_cache()

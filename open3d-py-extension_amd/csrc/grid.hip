@@ -1942,7 +1942,10 @@ __device__ __forceinline__ void wave_query(const GridView& g, int kneed, const f
   // A query the tile handed on (s0 = 2) rarely needs more than the shell-1
   // reach + h/2: that ball first (fewer rows and x-cells of the 5^3 cube),
   // then the whole shell.
-  bool trial = s0 >= 2;
+  // (The stile's hand-offs, s0 = 3, are queries whose k-th neighbour lies
+  // beyond its 2.45-voxel stencil — mostly the cube's edges and corners: no
+  // trial ball, the shell itself.)
+  bool trial = s0 == 2;
   // A dense own cell (a thin plane or a cluster far above the grid's mean
   // occupancy) holds the k nearest within a much smaller ball: a first try at
   // the radius its density suggests (2-D estimate, x2 margin; any radius below

@@ -30,6 +30,7 @@ group they degrade to the single-process identity.
 from __future__ import annotations
 
 import math
+import time
 from typing import Callable, Optional, Tuple
 
 import numpy as np
@@ -535,7 +536,8 @@ def _exchange(dest: torch.Tensor, world: int, group, *tensors):
 
 
 def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float, knn: int = 30, group=None,
-                        voxel_fn=None, normals_fn=None, halo: Optional[float] = None, presorted: bool = False):
+                        voxel_fn=None, normals_fn=None, halo: Optional[float] = None, presorted: bool = False,
+                        timings: Optional[dict] = None):
     """C4: voxel_down_sample + estimate_normals(KNN) of one cloud spread over
     the ranks, decomposed into x-slabs aligned to the global voxel grid.
 
@@ -559,6 +561,10 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
     over ranks is the single-GPU result.  Compute defaults to the HIP kernels
     (ops); tests inject the oracle (normals_fn(p, k) -> (normals, kth_d2)).
 
+    timings (device path): a dict that receives host timestamps (ms since the
+    call) at each phase end — no synchronisation is added, so a phase that
+    ends in a host wait shows the wait.
+
     presorted: the caller guarantees every point already lies in this rank's
     slab and the rows are in ascending global index (a spatially tiled
     dataset): the point all-to-all is skipped; a point outside the slab is an
@@ -566,7 +572,7 @@ def voxel_normals_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float
     from . import ops
 
     if voxel_fn is None and normals_fn is None and xyz.is_cuda:
-        return _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted)
+        return _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted, timings)
     world, rank = _world(group)
     if voxel_fn is None:
         def voxel_fn(p, vs, mn, mx):
@@ -649,7 +655,7 @@ def _slab_reps_generic(xyz, gidx, voxel_size, group, voxel_fn, presorted):
     return gidx[rep].contiguous(), xyz[rep].contiguous(), mn, mx, keys
 
 
-def _slab_reps_device(xyz, gidx, vs, group, presorted):
+def _slab_reps_device(xyz, gidx, vs, group, presorted, timings=None, t0=None):
     """HIP form of the slab voxel step: global bounds on the device (one
     all-reduce, one read), points to their slab owner unless presorted, the
     slab's reps with GLOBAL keys (a dense x-key window table when the slab is
@@ -662,7 +668,9 @@ def _slab_reps_device(xyz, gidx, vs, group, presorted):
     from . import ops
 
     world, rank = _world(group)
+    t0 = time.perf_counter() if t0 is None else t0
     mn, mx = global_bounds_device(xyz, group)
+    _stamp(timings, "bounds", t0)
     if not np.all(np.isfinite(mn)):
         raise RuntimeError("voxel_normals_slabs: the cloud is empty on every rank")
     keys = slab_bounds(mn, mx, vs, world)
@@ -693,6 +701,7 @@ def _slab_reps_device(xyz, gidx, vs, group, presorted):
                 kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
                 bad = ((kx < k_lo) | (kx >= k_hi)).sum()
         rxyz, rg = out["rep_xyz"], gidx[out["rep_idx"].long()].contiguous()
+        _stamp(timings, "reps", t0)
     else:
         rxyz, rg = xyz[:0], gidx[:0]
         if n_loc > 0:
@@ -726,7 +735,12 @@ def _two_part_rows(mask_a: torch.Tensor, mask_b: torch.Tensor):
     return buf, torch.stack([na, mask_b.sum()])
 
 
-def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted):
+def _stamp(timings, name, t0):
+    if timings is not None:
+        timings[name] = round((time.perf_counter() - t0) * 1e3, 4)
+
+
+def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted, timings=None):
     """The HIP form of voxel_normals_slabs: every rank keeps a voxel table of
     its slab widened by the halo (global keys, x-key window), so the normals
     run straight off the table (k_normals_stile) on own + halo reps; the halo
@@ -741,7 +755,8 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
 
     world, rank = _world(group)
     vs = float(voxel_size)
-    rg, rxyz, mn, mx, keys, dims, bad = _slab_reps_device(xyz, gidx, vs, group, presorted)
+    t0 = time.perf_counter()
+    rg, rxyz, mn, mx, keys, dims, bad = _slab_reps_device(xyz, gidx, vs, group, presorted, timings, t0)
     k_lo, k_hi, nkeys = keys[rank], keys[rank + 1], keys[-1]
     layer = int(dims[1] * dims[2])
     dev = rxyz.device
@@ -776,6 +791,7 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
             dist.all_to_all_single(rc, sc, group=group)
             counts = torch.cat([sc, rc]).cpu()  # the one host wait of the exchange
             ss, rs = counts[:world].tolist(), counts[world:].tolist()
+            _stamp(timings, f"halo{hk}_counts", t0)
             send = packed[rows[: sum(ss)]].to(cd)
             recv = torch.empty((sum(rs), 4), dtype=torch.float32, device=cd)
             dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=group)
@@ -795,6 +811,7 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
             ux[p_a] = ha[:, :3]
             ux[p_b] = hb[:, :3]
             own = p_own
+            _stamp(timings, f"halo{hk}_merged", t0)
         else:
             ux, own, nu = rxyz, None, n_own
         # the union's voxel table over the slab + halo window, normals off it
@@ -809,6 +826,7 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
             nrm, kd2 = ux.new_zeros((0, 3)), ux.new_zeros((0,))
         if own is not None:
             nrm, kd2 = nrm[own], kd2[own]
+        _stamp(timings, f"normals{hk}_queued", t0)
         if world == 1:
             if int(nbad.item()):
                 raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside this rank's slab")
@@ -826,6 +844,7 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
         parts = [torch.empty_like(info) for _ in range(world)]
         dist.all_gather(parts, info, group=group)
         tab = torch.stack(parts).cpu().numpy()
+        _stamp(timings, f"verdict{hk}", t0)
         if tab[:, 3].sum():
             raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside its rank's slab")
         n_total = int(tab[:, 1].sum())
