@@ -210,6 +210,20 @@ int o3dx_voxel_table_build(const float* xyz_dev, int64_t n,
                            int64_t kx0, int64_t kx1, float* voxel_pts_dev,
                            int64_t voxel_cells, double* geom_host, void* ws,
                            size_t ws_bytes, void* stream);
+/* o3dx_voxel_table_build_deferred: the same table without the host wait.
+ * Rows with a non-finite coordinate are skipped (padding rows of a
+ * fixed-size halo exchange).  The error bits (1: a point outside the window,
+ * 2: two points in one voxel) are OR-ed into status_dev[0] (int64, caller
+ * zeroed) for the caller to check later; the occupancy is not measured
+ * (geom_host[8] = -1), and o3dx_estimate_normals_voxel then runs the
+ * voxel-table kernels without the occupancy test (their results do not
+ * depend on it).  Multi-GPU slab step: replaces Python-side waits. */
+int o3dx_voxel_table_build_deferred(const float* xyz_dev, int64_t n,
+                                    const double* min_bound_host,
+                                    const double* max_bound_host, double voxel_size,
+                                    int64_t kx0, int64_t kx1, float* voxel_pts_dev,
+                                    int64_t voxel_cells, double* geom_host,
+                                    int64_t* status_dev, void* stream);
 
 /* ---------------------------------------------------------------- normals
  * Replaces o3d PointCloud.estimate_normals(search_param,

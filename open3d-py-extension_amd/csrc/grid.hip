@@ -2367,7 +2367,12 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
 static bool dense_vox_applicable(const double* geom, const float4* vox, int64_t n, int mode, int knn, double* kth) {
   if (!vox || geom[7] != 1.0 || mode != O3DX_SEARCH_KNN || getenv("O3DX_NO_STILE")) return false;
   const int kneed = (int)std::min<int64_t>(knn, n);
-  if (kneed < 1 || kneed > 32 || !(geom[8] > 0.0)) return false;
+  if (kneed < 1 || kneed > 32) return false;
+  if (geom[8] == -1.0) {  // o3dx_voxel_table_build_deferred: occupancy not measured
+    *kth = std::cbrt((double)kneed / 4.18879020478639098);
+    return true;
+  }
+  if (!(geom[8] > 0.0)) return false;
   const double dens = (double)n / (8.0 * geom[8]);
   *kth = std::cbrt((double)kneed / (std::min(dens, 1.0) * 4.18879020478639098));
   return dens >= 0.7 && *kth <= 2.0;

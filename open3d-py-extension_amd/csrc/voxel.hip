@@ -273,10 +273,12 @@ constexpr int kFuseChunk = kFuseBlock * kFusePer;
 // dynamic LDS: stage[kFuseChunk] (u64), loc[nb + 1], dst[nb]
 inline size_t fused_lds_bytes(int nb) { return kFuseChunk * sizeof(uint64_t) + (2 * (size_t)nb + 1) * sizeof(int32_t); }
 
+// chunk: points per block (<= kFuseChunk), chosen so the block count is a
+// whole number of CU-waves of blocks (fused_grid)
 __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, int64_t n, const VoxelGeom& g,
                                                 const Bricks& b, int cap, int32_t* __restrict__ btot,
                                                 uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
-                                                int* __restrict__ err) {
+                                                int* __restrict__ err, int chunk) {
   extern __shared__ uint64_t lds_u64[];
   uint64_t* stage = lds_u64;
   int32_t* loc = reinterpret_cast<int32_t*>(lds_u64 + kFuseChunk);  // count -> offset -> cursor
@@ -287,18 +289,19 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   for (int k = threadIdx.x; k < b.nb; k += kFuseBlock) loc[k] = 0;
   if (threadIdx.x == 0) ovf = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kFuseChunk;
+  const int64_t base = (int64_t)blockIdx.x * chunk;
+  const int64_t end = min(base + chunk, n);
   uint32_t code[kFusePer];
   bool bad = false;
   // every load of the chunk first (clamped, unconditional), then the keys
   P3 q[kFusePer];
 #pragma unroll
-  for (int j = 0; j < kFusePer; ++j) q[j] = p[min(base + threadIdx.x + (int64_t)j * kFuseBlock, n - 1)];
+  for (int j = 0; j < kFusePer; ++j) q[j] = p[min(base + threadIdx.x + (int64_t)j * kFuseBlock, end - 1)];
 #pragma unroll
   for (int j = 0; j < kFusePer; ++j) {
     const int64_t i = base + threadIdx.x + (int64_t)j * kFuseBlock;
     code[j] = ~0u;
-    if (i < n) {
+    if (i < end) {
       int v[3];
       if (voxel_of(q[j], g, v)) {
         code[j] = brick_code(v, b);
@@ -349,8 +352,21 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
 __global__ void __launch_bounds__(kFuseBlock) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
                                                        Bricks b, int cap, int32_t* __restrict__ btot,
                                                        uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
-                                                       int* __restrict__ err) {
-  vbin_fused_body(xyz, n, g, b, cap, btot, entries, vid, err);
+                                                       int* __restrict__ err, int chunk) {
+  vbin_fused_body(xyz, n, g, b, cap, btot, entries, vid, err, chunk);
+}
+
+// The one-pass binning's grid: its LDS stage allows one workgroup per CU, so
+// the block count is rounded up to whole rounds of kFuseCUs blocks and the
+// points are spread evenly over them (10M: 768 blocks of 13,021 points instead
+// of 611 of 16,384, whose third round ran on 99 of the 256 CUs).
+constexpr int kFuseCUs = 256;
+static int fused_grid(int64_t n, unsigned* blocks) {
+  const int64_t nb0 = std::max<int64_t>(1, (n + kFuseChunk - 1) / kFuseChunk);
+  const int64_t nb = (nb0 + kFuseCUs - 1) / kFuseCUs * kFuseCUs;
+  const int chunk = (int)std::max<int64_t>(1, (n + nb - 1) / nb);
+  *blocks = (unsigned)std::max<int64_t>(1, (n + chunk - 1) / chunk);
+  return chunk;
 }
 
 // Pass 3: one workgroup per brick: max index per voxel in LDS, then the
@@ -515,11 +531,12 @@ __global__ void k_bin_plan(const double* mm, double vs, int64_t n, int allow, ui
 __global__ void __launch_bounds__(kFuseBlock) k_vbin_fused_pre(const float* __restrict__ xyz, int64_t n,
                                                            const BinPlan* __restrict__ plan,
                                                            int32_t* __restrict__ btot, uint64_t* __restrict__ entries,
-                                                           int32_t* __restrict__ vid, int* __restrict__ err) {
+                                                           int32_t* __restrict__ vid, int* __restrict__ err,
+                                                           int chunk) {
   if (!plan->ok) return;
   const VoxelGeom g = plan->g;
   const Bricks b = plan->b;
-  vbin_fused_body(xyz, n, g, b, plan->cap, btot, entries, vid, err);
+  vbin_fused_body(xyz, n, g, b, plan->cap, btot, entries, vid, err, chunk);
 }
 
 __global__ void __launch_bounds__(kBlock) k_voxel_assign_hash(const float* __restrict__ xyz, int64_t n,
@@ -975,9 +992,11 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       // the bounds (the host replays the same plan below)
       hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, aabb_mailbox_dev(), voxel_size, n, allow_fused,
                          g_fused_overflow_key, w.plan);
-      hipLaunchKernelGGL(k_vbin_fused_pre, dim3((unsigned)((n + kFuseChunk - 1) / kFuseChunk)), dim3(kFuseBlock),
-                         fused_lds_bytes(kFuseMaxBricks), s, xyz, n, w.plan, w.boff, w.entries,
-                         (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
+      unsigned nfb;
+      const int chunk = fused_grid(n, &nfb);
+      hipLaunchKernelGGL(k_vbin_fused_pre, dim3(nfb), dim3(kFuseBlock), fused_lds_bytes(kFuseMaxBricks), s, xyz, n,
+                         w.plan, w.boff, w.entries, (voxel_of_point || cubic_id) ? w.vid : nullptr,
+                         reinterpret_cast<int*>(w.count + 1), chunk);
       pre_launched = true;
     }
     O3DX_TRY(aabb_end(mm, s));
@@ -1055,10 +1074,11 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       if (fused && attempt == 0 && pre_launched) {
         // already running on the device's identical plan
       } else if (fused) {
-        const unsigned nfb = (unsigned)((n + kFuseChunk - 1) / kFuseChunk);
+        unsigned nfb;
+        const int chunk = fused_grid(n, &nfb);
         hipLaunchKernelGGL(k_vbin_fused, dim3(nfb), dim3(kFuseBlock), fused_lds_bytes(bricks.nb), s, xyz, n, g, bricks,
                            cap, btot, w.entries, (voxel_of_point || cubic_id) ? w.vid : nullptr,
-                           reinterpret_cast<int*>(w.count + 1));
+                           reinterpret_cast<int*>(w.count + 1), chunk);
       } else {
         hipLaunchKernelGGL(k_vbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bhist, btot,
                            (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
@@ -1218,20 +1238,27 @@ extern "C" int o3dx_voxel_down_sample_window(const float* xyz, int64_t n, const 
 // ------------------------------------------------------------ table build
 // The voxel table of an arbitrary point set holding at most one point per
 // voxel (a slab's own + halo representatives): vox[v] = (x, y, z, row).
+// skip_nonfinite: rows with a non-finite coordinate are padding (the deferred
+// form); err: int bits (the read-back form) or, with err64, int64 bits.
 __global__ void __launch_bounds__(kBlock) k_table_build(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                        float4* __restrict__ vox, int* __restrict__ err) {
+                                                        float4* __restrict__ vox, int* __restrict__ err,
+                                                        unsigned long long* __restrict__ err64 = nullptr,
+                                                        int skip_nonfinite = 0) {
   const P3* p = reinterpret_cast<const P3*>(xyz);
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const P3 q = p[j];
+    if (skip_nonfinite && !(__builtin_isfinite(q.x) && __builtin_isfinite(q.y) && __builtin_isfinite(q.z))) continue;
     int v[3];
     if (!voxel_of(q, g, v)) {
-      atomicOr(err, 1);
+      if (err64) atomicOr(err64, 1ull);
+      else atomicOr(err, 1);
       continue;
     }
     const int64_t at = v[0] + (int64_t)g.nx * (v[1] + (int64_t)g.ny * v[2]);
     int* w = reinterpret_cast<int*>(&vox[at].w);
     if (atomicCAS(w, -1, (int)j) != -1) {
-      atomicOr(err, 2);
+      if (err64) atomicOr(err64, 2ull);
+      else atomicOr(err, 2);
       continue;
     }
     vox[at].x = q.x;
@@ -1284,6 +1311,44 @@ extern "C" int o3dx_voxel_table_build(const float* xyz, int64_t n, const double*
   if (c[0] & 2) return fail(O3DX_EINVAL, "o3dx_voxel_table_build: two points in one voxel");
   const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny, (double)g.nz,
                          1.0, (double)c[1], (double)g.kx0, 0.0, (double)nvox};
+  for (int k = 0; k < 12; ++k) geom_host[k] = gv[k];
+  return 0;
+}
+
+extern "C" int o3dx_voxel_table_build_deferred(const float* xyz, int64_t n, const double* min_bound_host,
+                                               const double* max_bound_host, double voxel_size, int64_t kx0,
+                                               int64_t kx1, float* voxel_pts, int64_t voxel_cells, double* geom_host,
+                                               int64_t* status_dev, void* stream) {
+  if (geom_host)
+    for (int k = 0; k < 12; ++k) geom_host[k] = 0.0;
+  if (n < 0 || (n > 0 && !xyz) || !voxel_pts || !geom_host || !min_bound_host || !max_bound_host || !status_dev)
+    return fail(O3DX_EINVAL, "o3dx_voxel_table_build_deferred: bad arguments");
+  if (!(voxel_size > 0.0)) return fail(O3DX_EINVAL, "voxel_size <= 0.");
+  double dims[3];
+  voxel_dims(min_bound_host, max_bound_host, voxel_size, dims);
+  if (kx0 < 0 || kx1 <= kx0 || (double)kx1 > dims[0]) return fail(O3DX_EINVAL, "o3dx_voxel_table_build: bad window");
+  VoxelGeom g;
+  g.mnx = min_bound_host[0];
+  g.mny = min_bound_host[1];
+  g.mnz = min_bound_host[2];
+  g.vs = voxel_size;
+  g.ivs = 1.0 / voxel_size;
+  g.kx0 = (int)kx0;
+  g.nx = (int)(kx1 - kx0);
+  g.ny = (int)dims[1];
+  g.nz = (int)dims[2];
+  const int64_t nvox = (int64_t)g.nx * g.ny * g.nz;
+  if (nvox > voxel_cells) return fail(O3DX_ENOMEM, "o3dx_voxel_table_build: table needs %lld voxels", (long long)nvox);
+  hipStream_t s = as_stream(stream);
+  O3DX_HIP(hipMemsetAsync(voxel_pts, 0xFF, (size_t)nvox * 4 * sizeof(float), s));
+  if (n > 0)
+    hipLaunchKernelGGL(k_table_build, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, g,
+                       reinterpret_cast<float4*>(voxel_pts), nullptr, reinterpret_cast<unsigned long long*>(status_dev),
+                       1);
+  O3DX_HIP(hipGetLastError());
+  // occupancy not measured (-1): o3dx_estimate_normals_voxel skips its test
+  const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny, (double)g.nz,
+                         1.0, -1.0, (double)g.kx0, 0.0, (double)nvox};
   for (int k = 0; k < 12; ++k) geom_host[k] = gv[k];
   return 0;
 }

@@ -57,6 +57,7 @@ _SIGS = {
                                               _P]),
     "o3dx_voxel_table_workspace_bytes": (_SZ, []),
     "o3dx_voxel_table_build": (_I32, [_P, _I64, _P, _P, _D, _I64, _I64, _P, _I64, _P, _P, _SZ, _P]),
+    "o3dx_voxel_table_build_deferred": (_I32, [_P, _I64, _P, _P, _D, _I64, _I64, _P, _I64, _P, _P, _P]),
     "o3dx_normals_workspace_bytes": (_SZ, [_I64]),
     "o3dx_estimate_normals_voxel": (_I32, [_P, _P, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_estimate_normals": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),

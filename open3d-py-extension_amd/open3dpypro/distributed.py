@@ -747,10 +747,12 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
     is a whole number of voxel layers.  Same contract and halo proof.
 
     Host waits per step: the bounds (after a device all-reduce), the rep
-    count, per halo round the halo counts (one all-to-all of two counts), the
-    table's occupancy and the verdict (one all-gather of four values).  The
-    halo rows travel as one packed (x, y, z, gidx bits) payload all-to-all,
-    and the union is merged by position (searchsorted) instead of sorted."""
+    count, and per halo round the verdict (one all-gather of five values).
+    The halo rows travel as one packed (x, y, z, gidx bits) all-to-all of
+    fixed size (hk x layer rows per neighbour, padded), so no count exchange
+    waits; the union is merged by position (searchsorted) instead of sorted;
+    the halo table is built without a read-back (its error bits join the
+    verdict)."""
     from . import ops
 
     world, rank = _world(group)
@@ -775,54 +777,79 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
     while True:
         if world > 1 and hk >= min_keys:
             raise RuntimeError("voxel_normals_slabs: the kNN halo is wider than a slab; use fewer ranks")
-        # halo: the own reps of the hk voxel layers next to each interior face
+        # halo: the own reps of the hk voxel layers next to each interior face,
+        # exchanged in fixed-size packets: hk layers hold at most cap = hk x
+        # layer reps (one per voxel), a bound every rank knows without a
+        # count exchange; unused rows are padding (NaN coordinates, gidx bits
+        # INT32_MAX: they sort last and the table build skips them)
         if world > 1:
             zero = torch.zeros(n_own, dtype=torch.bool, device=dev)
             send_lo = (kxr < k_lo + hk) if rank > 0 else zero
             send_hi = (kxr >= k_hi - hk) if rank < world - 1 else zero
-            rows, cnt = _two_part_rows(send_lo, send_hi)
-            sc = torch.zeros(world, dtype=torch.int64, device=dev)
+            cap = hk * layer
+            pad = torch.tensor([np.nan, np.nan, np.nan, 0.0], dtype=torch.float32)
+            pad[3] = torch.tensor([np.iinfo(np.int32).max], dtype=torch.int32).view(torch.float32)[0]
+            send = pad.to(dev).repeat(2 * cap + 1, 1)  # row 2 cap: the dump row of the scatter
+            dump = torch.full((n_own,), 2 * cap, dtype=torch.int64, device=dev)
+            ia = torch.where(send_lo, torch.cumsum(send_lo, 0) - 1, dump)
+            ib = torch.where(send_hi, torch.cumsum(send_hi, 0) - 1 + cap, dump)
+            send.scatter_(0, ia[:, None].expand(-1, 4), packed)
+            send.scatter_(0, ib[:, None].expand(-1, 4), packed)
+            send[2 * cap] = pad.to(dev)
+            ss = [0] * world
+            rs = [0] * world
             if rank > 0:
-                sc[rank - 1] = cnt[0]
+                ss[rank - 1] = rs[rank - 1] = cap
             if rank < world - 1:
-                sc[rank + 1] = cnt[1]
-            sc = sc.to(cd)
-            rc = torch.empty_like(sc)
-            dist.all_to_all_single(rc, sc, group=group)
-            counts = torch.cat([sc, rc]).cpu()  # the one host wait of the exchange
-            ss, rs = counts[:world].tolist(), counts[world:].tolist()
-            _stamp(timings, f"halo{hk}_counts", t0)
-            send = packed[rows[: sum(ss)]].to(cd)
+                ss[rank + 1] = rs[rank + 1] = cap
+            send = torch.cat([send[:cap] if rank > 0 else send[:0], send[cap:2 * cap] if rank < world - 1 else send[:0]])
             recv = torch.empty((sum(rs), 4), dtype=torch.float32, device=cd)
-            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=group)
+            dist.all_to_all_single(recv, send.to(cd), output_split_sizes=rs, input_split_sizes=ss, group=group)
             recv = recv.to(dev)
+            _stamp(timings, f"halo{hk}_exchanged", t0)
             na = rs[rank - 1] if rank > 0 else 0
             ha, hb = recv[:na], recv[na:]
             ga = ha[:, 3].contiguous().view(torch.int32).long()
             gb = hb[:, 3].contiguous().view(torch.int32).long()
             # merge by position: own, lower-neighbour and upper-neighbour rows are
-            # each ascending in global index
+            # each ascending in global index (padding last); padding rows land
+            # at or past the union's end, in NaN-filled rows
             p_own = torch.arange(n_own, device=dev) + torch.searchsorted(ga, rg) + torch.searchsorted(gb, rg)
             p_a = torch.arange(ga.numel(), device=dev) + torch.searchsorted(rg, ga) + torch.searchsorted(gb, ga)
             p_b = torch.arange(gb.numel(), device=dev) + torch.searchsorted(rg, gb) + torch.searchsorted(ga, gb)
-            nu = n_own + ga.numel() + gb.numel()
-            ux = torch.empty((nu, 3), dtype=torch.float32, device=dev)
-            ux[p_own] = rxyz
+            nrows = n_own + ga.numel() + gb.numel()
+            ux = torch.full((nrows, 3), np.nan, dtype=torch.float32, device=dev)
             ux[p_a] = ha[:, :3]
             ux[p_b] = hb[:, :3]
-            own = p_own
+            ux[p_own] = rxyz
+            big = np.iinfo(np.int32).max
+            nu_dev = n_own + (ga < big).sum() + (gb < big).sum()  # the union's size, on the device
+            own, nu = p_own, nrows
             _stamp(timings, f"halo{hk}_merged", t0)
         else:
             ux, own, nu = rxyz, None, n_own
+            nu_dev = None
         # the union's voxel table over the slab + halo window, normals off it
         kx0, kx1 = max(k_lo - hk, 0), min(k_hi + hk, nkeys)
         if nu > 0 and (kx1 - kx0) * layer <= 2 * nu + (1 << 20):
-            grid = ops.voxel_table(ux, vs, mn, mx, kx0, kx1, table)
+            if world > 1:  # deferred table: its error bits join the verdict, no host wait here
+                status = torch.zeros(1, dtype=torch.int64, device=dev)
+                grid = ops.voxel_table(ux, vs, mn, mx, kx0, kx1, table, status=status)
+            else:
+                status = None
+                grid = ops.voxel_table(ux, vs, mn, mx, kx0, kx1, table)
             table = grid.pts
             nrm, kd2 = ops.estimate_normals(ux, knn=knn, voxel_grid=grid, return_kdist=True)
         elif nu > 0:  # sparse slab: the normals sort the union into their own grid
-            nrm, kd2 = ops.estimate_normals(ux, knn=knn, return_kdist=True)
+            status = None
+            if nu_dev is not None:  # (the padding rows out first: this path sorts every row)
+                nv = int(nu_dev)
+                ux_v = ux[:nv]
+                nrm, kd2 = ops.estimate_normals(ux_v, knn=knn, return_kdist=True)
+            else:
+                nrm, kd2 = ops.estimate_normals(ux, knn=knn, return_kdist=True)
         else:
+            status = None
             nrm, kd2 = ux.new_zeros((0, 3)), ux.new_zeros((0,))
         if own is not None:
             nrm, kd2 = nrm[own], kd2[own]
@@ -835,11 +862,16 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
         # union size, points outside the slab
         fail = (torch.sqrt(kd2.double()) >= (t + hk * vs) * (1.0 - 1e-9)).any() if n_own else \
             torch.zeros((), dtype=torch.bool, device=dev)
-        info = torch.zeros(4, dtype=torch.int64, device=dev)  # filled on the device: no host copies
+        info = torch.zeros(5, dtype=torch.int64, device=dev)  # filled on the device: no host copies
         info[0] = fail.to(torch.int64)
         info[1].fill_(n_own)
-        info[2].fill_(nu)
+        if nu_dev is not None:
+            info[2] = nu_dev
+        else:
+            info[2].fill_(nu)
         info[3] = nbad
+        if status is not None:
+            info[4] = status[0]
         info = info.to(cd)
         parts = [torch.empty_like(info) for _ in range(world)]
         dist.all_gather(parts, info, group=group)
@@ -847,6 +879,8 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
         _stamp(timings, f"verdict{hk}", t0)
         if tab[:, 3].sum():
             raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside its rank's slab")
+        if tab[:, 4].any():
+            raise RuntimeError("voxel_normals_slabs: the halo table build failed (bits %d)" % int(np.bitwise_or.reduce(tab[:, 4])))
         n_total = int(tab[:, 1].sum())
         short = any(r[1] > 0 and r[2] < min(knn, n_total) for r in tab)  # fewer than k points: unverifiable
         if not tab[:, 0].any() and not short:

@@ -132,10 +132,14 @@ def voxel_down_sample_window(xyz: torch.Tensor, voxel_size: float, min_bound, ma
 
 
 def voxel_table(xyz: torch.Tensor, voxel_size: float, min_bound, max_bound, kx0: int, kx1: int,
-                table: Optional[torch.Tensor] = None):
+                table: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None):
     """VoxelGrid of points holding at most one point per voxel (a slab's own +
     halo representatives), over the x-key window [kx0, kx1) of the global grid
-    (o3dx_voxel_table_build).  `table`: an optional (cells, 4) float32 buffer."""
+    (o3dx_voxel_table_build).  `table`: an optional (cells, 4) float32 buffer.
+    `status`: a zeroed int64 device tensor — the deferred form
+    (o3dx_voxel_table_build_deferred): no host wait, non-finite rows skipped,
+    error bits OR-ed into status[0] (1: a point outside the window, 2: two
+    points in one voxel) for the caller to check."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
@@ -147,6 +151,11 @@ def voxel_table(xyz: torch.Tensor, voxel_size: float, min_bound, max_bound, kx0:
         table = torch.empty((cells, 4), dtype=torch.float32, device=dev)
     geom = np.zeros(12, np.float64)
     ws = N.workspace(L.o3dx_voxel_table_workspace_bytes(), dev, "table")
+    if status is not None:  # deferred: no host wait, error bits OR-ed into status[0] on the device
+        N.check(L.o3dx_voxel_table_build_deferred(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size),
+                                                  int(kx0), int(kx1), N.ptr(table), table.shape[0], _np_ptr(geom),
+                                                  N.ptr(status), N.stream_ptr(dev)), "voxel_table")
+        return VoxelGrid(geom, table, n)
     N.check(L.o3dx_voxel_table_build(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), int(kx0), int(kx1),
                                      N.ptr(table), table.shape[0], _np_ptr(geom), N.ptr(ws), ws.numel(),
                                      N.stream_ptr(dev)), "voxel_table")
