@@ -277,6 +277,11 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp,
 size_t compact_workspace_ints(int64_t n);
 constexpr int kScanItemsU8 = 16;                      // flags per thread of the u8 compaction
 constexpr int kScanTileBytes = kBlock * kScanItemsU8;  // flags per tile (4096)
+// a device byte range to clear (folded into a kernel that runs anyway)
+struct ZeroSpan {
+  uint8_t* p = nullptr;
+  size_t bytes = 0;
+};
 // Hook of voxel_down_sample_hooked: called with the kept table's geometry
 // (geom[8] = -1: occupancy unknown yet) and the table, after the voxel
 // kernels are queued and before the representative count is read back.
@@ -284,7 +289,7 @@ typedef int (*VoxelHook)(void* ctx, const double* geom12, const void* vox);
 int voxel_down_sample_hooked(const float* xyz, int64_t n, const double* min_bound, const double* max_bound,
                              double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, float* voxel_pts,
                              int64_t voxel_cells, double* geom, void* ws, size_t ws_bytes, void* stream,
-                             VoxelHook hook, void* ctx);
+                             VoxelHook hook, void* ctx, ZeroSpan extra_zero = {});
 int compact_flags_scan(const uint8_t* flags, int64_t n, int64_t* count_dev, int32_t* tmp, hipStream_t s);
 int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* pos_out,
                   int64_t* count_dev, int32_t* tmp, hipStream_t s);
@@ -304,13 +309,10 @@ int aabb_device(const float* xyz, int64_t n, double* mm_dev, void* ws, hipStream
 // pinned memory followed by a sequence number the host polls (no copy kernel,
 // no stream query).  aabb_begin queues the kernels (work queued after it
 // keeps running while the host waits); aabb_end waits and returns {min, max}.
-// z0..z2: device ranges the AABB kernel zeroes on the way (clears folded in)
-struct ZeroSpan {
-  uint8_t* p = nullptr;
-  size_t bytes = 0;
-};
+// z0..z3: device ranges the AABB kernel zeroes on the way (clears folded in;
+// ZeroSpan above)
 int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0 = {}, ZeroSpan z1 = {},
-               ZeroSpan z2 = {});
+               ZeroSpan z2 = {}, ZeroSpan z3 = {});
 int aabb_end(double mm_host[6], hipStream_t s);
 // device view of the bounds aabb_begin's kernels publish ({min, max}, 6
 // doubles): readable by kernels queued after it on the same stream

@@ -425,10 +425,11 @@ __device__ __forceinline__ void grid_zero(uint8_t* p, size_t bytes) {
 
 __global__ void __launch_bounds__(kBlock) k_aabb_partial(const float* __restrict__ xyz, int64_t n,
                                                          float* __restrict__ part, ZeroSpan z0 = {},
-                                                         ZeroSpan z1 = {}, ZeroSpan z2 = {}) {
+                                                         ZeroSpan z1 = {}, ZeroSpan z2 = {}, ZeroSpan z3 = {}) {
   grid_zero(z0.p, z0.bytes);
   grid_zero(z1.p, z1.bytes);
   grid_zero(z2.p, z2.bytes);
+  grid_zero(z3.p, z3.bytes);
   float mn[3] = {INFINITY, INFINITY, INFINITY};
   float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   const P3* p = reinterpret_cast<const P3*>(xyz);
@@ -540,7 +541,8 @@ struct AabbMailbox {
 thread_local AabbMailbox g_ambox;
 }  // namespace
 
-int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0, ZeroSpan z1, ZeroSpan z2) {
+int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0, ZeroSpan z1, ZeroSpan z2,
+               ZeroSpan z3) {
   AabbMailbox& m = g_ambox;
   if (!m.host) {
     void* h = nullptr;
@@ -557,8 +559,8 @@ int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0
   ++m.seq;
   float* part = reinterpret_cast<float*>(ws);
   int nb = (int)std::min<int64_t>(kAabbBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
-  if (z0.bytes || z1.bytes || z2.bytes) nb = kAabbBlocks;  // the clears want the whole grid
-  hipLaunchKernelGGL(k_aabb_partial, dim3(nb), dim3(kBlock), 0, s, xyz, n, part, z0, z1, z2);
+  if (z0.bytes || z1.bytes || z2.bytes || z3.bytes) nb = kAabbBlocks;  // the clears want the whole grid
+  hipLaunchKernelGGL(k_aabb_partial, dim3(nb), dim3(kBlock), 0, s, xyz, n, part, z0, z1, z2, z3);
   hipLaunchKernelGGL(k_aabb_final_host, dim3(1), dim3(1024), 0, s, part, nb, n,
                      reinterpret_cast<double*>(m.dev + 1), m.seq, static_cast<volatile uint64_t*>(m.dev));
   O3DX_HIP(hipGetLastError());

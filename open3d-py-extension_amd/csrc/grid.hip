@@ -2383,7 +2383,7 @@ static bool dense_vox_applicable(const double* geom, const float4* vox, int64_t 
 // dense_vox_applicable once the counts are known.
 static int normals_dense_vox(const double* geom, const float4* vox, const float* xyz, int64_t n, int mode, int knn,
                              const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes, hipStream_t s,
-                             bool spec = false) {
+                             bool spec = false, bool lens_zeroed = false) {
   double kth = 0.0;
   int kneed = knn;
   if (spec) {
@@ -2434,7 +2434,8 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   int32_t* list = ar.take<int32_t>(n);
   int32_t* list2 = ar.take<int32_t>(n);
   O3DX_ARENA_CHECK(ar);
-  O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
+  // (the one-call pipeline clears them in its bounds pass: no fill launch here)
+  if (!lens_zeroed) O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
   {
     KTimer kt("normals_knn", s);
     {
@@ -2903,11 +2904,12 @@ struct SpecNormals {
   size_t ws_bytes;
   hipStream_t s;
   bool launched;
+  bool lens_zeroed;  // the normals' hand-off counters (ws head) cleared by the bounds pass
 };
 static int spec_normals_hook(void* ctx, const double* geom, const void* vox) {
   SpecNormals& c = *static_cast<SpecNormals*>(ctx);
   const int rc = normals_dense_vox(geom, static_cast<const float4*>(vox), c.rep_xyz, c.ncap, O3DX_SEARCH_KNN, c.knn,
-                                   nullptr, c.out, nullptr, c.ws, c.ws_bytes, c.s, true);
+                                   nullptr, c.out, nullptr, c.ws, c.ws_bytes, c.s, true, c.lens_zeroed);
   c.launched = rc == 0;
   return rc == 1 ? 0 : rc;
 }
@@ -2921,9 +2923,11 @@ extern "C" int o3dx_voxel_down_sample_normals(const float* xyz, int64_t n, const
   if (!rep_xyz || !normals || !voxel_pts || !geom || !nws || nws_bytes < o3dx_normals_workspace_bytes(n))
     return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_normals: bad arguments");
   if (knn < 0 || knn > O3DX_MAX_KNN) return fail(O3DX_ENOTSUP, "knn %d outside [0, %d]", knn, O3DX_MAX_KNN);
-  SpecNormals c{rep_xyz, n, knn, normals, nws, nws_bytes, as_stream(stream), false};
+  SpecNormals c{rep_xyz, n, knn, normals, nws, nws_bytes, as_stream(stream), false, true};
+  // normals_dense_vox's hand-off counters: the first 16 B of its workspace
   O3DX_TRY(voxel_down_sample_hooked(xyz, n, min_bound, max_bound, voxel_size, rep_idx, rep_xyz, m_host, voxel_pts,
-                                    voxel_cells, geom, ws, ws_bytes, stream, spec_normals_hook, &c));
+                                    voxel_cells, geom, ws, ws_bytes, stream, spec_normals_hook, &c,
+                                    ZeroSpan{static_cast<uint8_t*>(nws), 4 * sizeof(int32_t)}));
   const int64_t m = *m_host;
   double kth;
   if (c.launched && geom[10] == 0.0 && dense_vox_applicable(geom, reinterpret_cast<const float4*>(voxel_pts), m, O3DX_SEARCH_KNN, knn,

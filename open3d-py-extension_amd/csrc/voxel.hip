@@ -955,7 +955,8 @@ extern "C" int64_t o3dx_voxel_grid_cells(int64_t n, const double* min_bound_host
 static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host, const double* max_bound_host,
                       double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point,
                       int32_t* cubic_id, float* vox, int64_t vox_cap, double* geom, void* ws, size_t ws_bytes,
-                      void* stream, const int64_t* xwin = nullptr, VoxelHook hook = nullptr, void* hook_ctx = nullptr) {
+                      void* stream, const int64_t* xwin = nullptr, VoxelHook hook = nullptr, void* hook_ctx = nullptr,
+                      ZeroSpan extra_zero = {}) {
   if (geom)
     for (int k = 0; k < 12; ++k) geom[k] = 0.0;
   if (n < 0 || (n > 0 && (!xyz || !rep_idx)) || !m_host)
@@ -986,7 +987,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     double mm[6];
     O3DX_TRY(aabb_begin(xyz, n, w.aabb, s, ZeroSpan{reinterpret_cast<uint8_t*>(w.count), 8 * sizeof(int64_t)},
                         ZeroSpan{reinterpret_cast<uint8_t*>(w.boff), (size_t)kMaxBuckets * kTotStride * sizeof(int32_t)},
-                        ZeroSpan{w.flags, (size_t)n}));
+                        ZeroSpan{w.flags, (size_t)n}, extra_zero));
     if (!min_bound_host && !max_bound_host && allow_fused && n > 0 && !getenv("O3DX_VOXEL_NOPRE")) {
       // the binning starts on the device's own plan while the host waits for
       // the bounds (the host replays the same plan below)
@@ -1151,6 +1152,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
                              w.scan_tmp, s));
     }
+    const bool early = hook && grid_kept && attempt == 0;
     // gathers sized by the device-side count (at most n rows), queued ahead
     // of the read-back so they overlap the host round trip
     const unsigned gg = grid_for(n, kBlock, 8192);
@@ -1159,12 +1161,14 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
                          reinterpret_cast<float4*>(vox));
     else if (rep_xyz)
       hipLaunchKernelGGL(k_gather_xyz, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, rep_xyz);
-    if (hook && grid_kept && attempt == 0) {
+    if (early) {
       // the counts' copy is queued first, then the hook's work (the table
       // geometry, occupancy not yet known): the host waits for the copy only
+      // (measured: the copy on a side stream, behind the gather, left a
+      // 6-7 us launch gap before the hook's kernels instead of the 5 us copy)
+      O3DX_TRY(read_back_begin(w.count, 3 * sizeof(int64_t), s));
       const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny,
                              (double)g.nz, 1.0, -1.0, (double)g.kx0, 0.0, nvox};
-      O3DX_TRY(read_back_begin(w.count, 3 * sizeof(int64_t), s));
       O3DX_TRY(hook(hook_ctx, gv, vox));
       O3DX_TRY(read_back_end(counts, 3 * sizeof(int64_t)));
     } else {
@@ -1356,7 +1360,9 @@ extern "C" int o3dx_voxel_table_build_deferred(const float* xyz, int64_t n, cons
 int o3dx::voxel_down_sample_hooked(const float* xyz, int64_t n, const double* min_bound, const double* max_bound,
                              double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, float* voxel_pts,
                              int64_t voxel_cells, double* geom, void* ws, size_t ws_bytes, void* stream,
-                             VoxelHook hook, void* ctx) {
+                             VoxelHook hook, void* ctx, ZeroSpan extra_zero) {
+  if (extra_zero.bytes && min_bound && max_bound)  // no bounds pass to clear it on the way
+    O3DX_HIP(hipMemsetAsync(extra_zero.p, 0, extra_zero.bytes, as_stream(stream)));
   return voxel_impl(xyz, n, min_bound, max_bound, voxel_size, rep_idx, rep_xyz, m_host, nullptr, nullptr, voxel_pts,
-                    voxel_cells, geom, ws, ws_bytes, stream, nullptr, hook, ctx);
+                    voxel_cells, geom, ws, ws_bytes, stream, nullptr, hook, ctx, extra_zero);
 }
