@@ -16,6 +16,7 @@
 // exactly as Open3D evaluates |(a x + c z) + (b y + d)| < thr; inlier counts
 // are ballot-popcounts into LDS.  Sigma|d| (only needed to break fitness ties)
 // is computed exactly in float64 for the tied hypotheses only.
+#include <cfloat>
 #include <cstring>
 #include <random>
 #include <vector>
@@ -1112,15 +1113,20 @@ __global__ void k_gather_samples(const float* __restrict__ xyz, const int32_t* _
   out[3 * j + 2] = xyz[3 * i + 2];
 }
 
-// --------------------------------------------------------------- host math
-static inline void hcross(const double u[3], const double v[3], double o[3]) {
+// ------------------------------------------- plane math (host and device)
+// One definition for both sides: segment_plane's culled path forms the
+// hypotheses on the device (k_ransac_setup), the other paths on the host;
+// compiled with -ffp-contract=off and correctly rounded sqrt / division on
+// both, the planes are the same bits.
+#define O3DX_HD __host__ __device__
+O3DX_HD inline void hcross(const double u[3], const double v[3], double o[3]) {
   o[0] = u[1] * v[2] - u[2] * v[1];
   o[1] = u[2] * v[0] - u[0] * v[2];
   o[2] = u[0] * v[1] - u[1] * v[0];
 }
-static inline double hdot(const double u[3], const double v[3]) { return (u[0] * v[0] + u[1] * v[1]) + u[2] * v[2]; }
+O3DX_HD inline double hdot(const double u[3], const double v[3]) { return (u[0] * v[0] + u[1] * v[1]) + u[2] * v[2]; }
 
-static void plane_from_centred(const double c[3], const double mo[6], double pl[4]) {
+O3DX_HD inline void plane_from_centred(const double c[3], const double mo[6], double pl[4]) {
   const double xx = mo[0], xy = mo[1], xz = mo[2], yy = mo[3], yz = mo[4], zz = mo[5];
   double det_x = yy * zz - yz * yz, det_y = xx * zz - xz * xz, det_z = xx * yy - xy * xy;
   double abc[3];
@@ -1131,7 +1137,7 @@ static void plane_from_centred(const double c[3], const double mo[6], double pl[
   } else {
     abc[0] = xy * yz - xz * yy; abc[1] = xy * xz - yz * xx; abc[2] = det_z;
   }
-  double norm = std::sqrt(hdot(abc, abc));
+  double norm = sqrt(hdot(abc, abc));
   if (norm == 0) {
     pl[0] = pl[1] = pl[2] = pl[3] = 0;
     return;
@@ -1141,14 +1147,14 @@ static void plane_from_centred(const double c[3], const double mo[6], double pl[
   pl[3] = -hdot(abc, c);
 }
 
-// ComputeTrianglePlane (k == 3) / GetPlaneFromPoints (k > 3), host float64
-static void plane_from_pts(const double* P, int k, double pl[4]) {
+// ComputeTrianglePlane (k == 3) / GetPlaneFromPoints (k > 3), float64
+O3DX_HD inline void plane_from_pts(const double* P, int k, double pl[4]) {
   if (k == 3) {
     double e0[3] = {P[3] - P[0], P[4] - P[1], P[5] - P[2]};
     double e1[3] = {P[6] - P[0], P[7] - P[1], P[8] - P[2]};
     double abc[3];
     hcross(e0, e1, abc);
-    double norm = std::sqrt(hdot(abc, abc));
+    double norm = sqrt(hdot(abc, abc));
     if (norm == 0) {
       pl[0] = pl[1] = pl[2] = pl[3] = 0;
       return;
@@ -1169,6 +1175,61 @@ static void plane_from_pts(const double* P, int k, double pl[4]) {
     mo[3] += r1 * r1; mo[4] += r1 * r2; mo[5] += r2 * r2;
   }
   plane_from_centred(c, mo, pl);
+}
+
+// 1: degenerate (count -1); 2: non-finite coefficients (count 0); 0: a plane
+O3DX_HD inline int plane_kind(const double* pl) {
+  if (pl[0] == 0 && pl[1] == 0 && pl[2] == 0 && pl[3] == 0) return 1;
+  for (int a = 0; a < 4; ++a)
+    if (!(pl[a] == pl[a] && pl[a] <= DBL_MAX && pl[a] >= -DBL_MAX)) return 2;
+  return 0;
+}
+
+// The culled sweep's per-hypothesis limits (hi, limc, lo, 0), §4.3:
+// S = |a| max|x| + |b| max|y| + |c| max|z| + |d|, g = 6 2^-24 S + 2^-20 thr,
+// hi = thr + g and limc = hi + 20 2^-24 S rounded up, lo = thr - g rounded
+// down (0 when thr <= g); degenerate: never counted.
+O3DX_HD inline float f32_up(double v) {
+  float f = (float)v;
+  return (double)f < v ? nextafterf(f, INFINITY) : f;
+}
+O3DX_HD inline float f32_down(double v) {
+  float f = (float)v;
+  return (double)f > v ? nextafterf(f, -INFINITY) : f;
+}
+O3DX_HD inline float4 cull_limits(const double* pl, const double absmax[3], double thr, int kind) {
+  if (kind == 1) return make_float4(-1.0f, -INFINITY, -1.0f, 0.f);
+  const double S = fabs(pl[0]) * absmax[0] + fabs(pl[1]) * absmax[1] + fabs(pl[2]) * absmax[2] + fabs(pl[3]);
+  const double g = 6.0 * 5.9604644775390625e-08 * S + 9.5367431640625e-07 * thr;
+  const float lim = f32_up(thr + g);
+  const float lo = thr - g > 0 ? f32_down(thr - g) : 0.0f;
+  return make_float4(lim, f32_up((double)lim + 20.0 * 5.9604644775390625e-08 * S), lo, 0.f);
+}
+
+// segment_plane's culled path forms the hypotheses on the device: per
+// hypothesis plane_from_pts over its gathered sample coordinates, the float32
+// plane, the culled sweep's limits from the device bounds, and the float64
+// plane (+ the bounds, thread 0) into the read-back block.
+__global__ void __launch_bounds__(kBlock) k_ransac_setup(const float* __restrict__ scoord, int H, int rn,
+                                                         const double* __restrict__ mm, double thr,
+                                                         float4* __restrict__ pl32, float4* __restrict__ lims,
+                                                         uint8_t* __restrict__ degen, double* __restrict__ pl64_out,
+                                                         double* __restrict__ mm_out) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h == 0)
+    for (int a = 0; a < 6; ++a) mm_out[a] = mm[a];
+  if (h >= H) return;
+  double absmax[3];
+  for (int a = 0; a < 3; ++a) absmax[a] = fmax(fabs(mm[a]), fabs(mm[3 + a]));
+  double P[48];
+  for (int j = 0; j < rn * 3; ++j) P[j] = (double)scoord[(int64_t)h * rn * 3 + j];
+  double pl[4];
+  plane_from_pts(P, rn, pl);
+  const int kind = plane_kind(pl);
+  for (int a = 0; a < 4; ++a) pl64_out[4 * (int64_t)h + a] = pl[a];
+  pl32[h] = make_float4((float)pl[0], (float)pl[1], (float)pl[2], (float)pl[3]);
+  lims[h] = cull_limits(pl, absmax, thr, kind);
+  degen[h] = (uint8_t)kind;
 }
 
 static bool plane_is_zero(const double* pl) { return pl[0] == 0 && pl[1] == 0 && pl[2] == 0 && pl[3] == 0; }
@@ -1296,14 +1357,7 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
     float half = (float)(std::max((double)mid - (double)lo, (double)hi - (double)mid) * (1.0 + std::ldexp(1.0, -18)));
     if (dg[h]) half = -1.0f;
     bnd[h] = make_float4(lo, hi, mid, half);
-    if (mfma == 3) {  // k_plane_upper_cull: (hi, limc) rounded up, lo down; degenerate never counted
-      auto up = [](double v) { float f = (float)v; return (double)f < v ? std::nextafter(f, INFINITY) : f; };
-      auto down = [](double v) { float f = (float)v; return (double)f > v ? std::nextafter(f, -INFINITY) : f; };
-      const float lim = up(thr + g);
-      const float lo_c = thr - g > 0 ? down(thr - g) : 0.0f;
-      bnd[h] = dg[h] ? make_float4(-1.0f, -INFINITY, -1.0f, 0.f)
-                     : make_float4(lim, up((double)lim + 20.0 * std::ldexp(1.0, -24) * S), lo_c, 0.f);
-    }
+    if (mfma == 3) bnd[h] = cull_limits(pl, absmax, thr, dg[h]);  // k_plane_upper_cull (as k_ransac_setup)
   }
   *rc = 0;
   // one copy of the block laid out as count_carve placed it
@@ -1368,7 +1422,18 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
       hv[(j / 32) * 32 + r] = f;
     }
   }
-  if (hipMemcpyAsync(base, st.data(), st.size(), hipMemcpyHostToDevice, s) != hipSuccess)
+  // through a pinned staging buffer (a direct DMA; a pageable source takes
+  // the runtime's staged, blocking path).  Every caller reads back before it
+  // returns, so the previous upload has landed when the buffer is reused.
+  constexpr size_t kPinCap = 1 << 20;
+  static thread_local void* pin = nullptr;
+  if (st.size() <= kPinCap && !pin && hipHostMalloc(&pin, kPinCap, hipHostMallocDefault) != hipSuccess) pin = nullptr;
+  const void* src = st.data();
+  if (pin && st.size() <= kPinCap) {
+    std::memcpy(pin, st.data(), st.size());
+    src = pin;
+  }
+  if (hipMemcpyAsync(base, src, st.size(), hipMemcpyHostToDevice, s) != hipSuccess)
     *rc = fail(O3DX_EIO, "plane upload failed");
 }
 
@@ -1480,6 +1545,25 @@ static int bin_points(const float* xyz, int64_t n, const double* mm_dev, CountWs
   return 0;
 }
 
+// The culled sweep over w.sorted with the limits already in w.pl32 / w.band /
+// w.degen (host upload or k_ransac_setup): per-hypothesis counts (degenerate
+// -1) into counts_dev, no host wait.
+static int launch_cull(int64_t n, int H, double thr, CountWs& w, bool exact, hipStream_t s, int64_t* counts_dev) {
+  const int64_t nchunk = (n + kCullCS - 1) / kCullCS;
+  const int64_t rows = std::max<int64_t>(1, std::min<int64_t>((int64_t)(w.partial_ints / std::max(H, 1)), 2048));
+  // one resident wave per chunk stream: 5 blocks per CU (LDS ~30 KB each)
+  const int64_t per_block = kCullBlock / 64;
+  const unsigned gx = (unsigned)std::min<int64_t>(std::min<int64_t>(rows, kCullResident),
+                                                  (nchunk + per_block - 1) / per_block);
+  const unsigned gy = (unsigned)((H + kCullHG - 1) / kCullHG);
+  hipLaunchKernelGGL(exact ? k_plane_upper_cull<true> : k_plane_upper_cull<false>, dim3(gx, gy), dim3(kCullBlock), 0,
+                     s, w.sorted, n, w.pl32, w.pl64, w.band, H, thr, w.partial);
+  O3DX_TRY(reduce_columns_i32_to_i64(w.partial, gx, H, counts_dev, s));
+  hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, counts_dev);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
 // the upper sweep a call takes: 3 culled, 2 / 1 matrix cores, 0 VALU
 static int upper_mode(int64_t n, double smax, double thr) {
   if (const char* ue = getenv("O3DX_RANSAC_UPPER")) {
@@ -1534,24 +1618,13 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
   if (rc) return rc;
   KTimer kt("plane_count_upper", s);
   if (mfma == 3) {
-    const int64_t nchunk = (n + kCullCS - 1) / kCullCS;
-    const int64_t rows = std::max<int64_t>(1, std::min<int64_t>((int64_t)(w.partial_ints / std::max(H, 1)), 2048));
-    // one resident wave per chunk stream: 5 blocks per CU (LDS ~30 KB each)
-    const int64_t per_block = kCullBlock / 64;
-    const unsigned gx = (unsigned)std::min<int64_t>(std::min<int64_t>(rows, kCullResident),
-                                                    (nchunk + per_block - 1) / per_block);
-    const unsigned gy = (unsigned)((H + kCullHG - 1) / kCullHG);
     // O3DX_RANSAC_CULL_EXACT (tests, A/B): the exact form over every hypothesis
     const bool exact = getenv("O3DX_RANSAC_CULL_EXACT") != nullptr;
     w.exact_counts = exact;
-    hipLaunchKernelGGL(exact ? k_plane_upper_cull<true> : k_plane_upper_cull<false>, dim3(gx, gy), dim3(kCullBlock), 0,
-                       s, w.sorted, n, w.pl32, w.pl64, w.band, H, thr, w.partial);
-    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, gx, H, w.counts, s));
-    hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
+    O3DX_TRY(launch_cull(n, H, thr, w, exact, s, w.counts));
     kt.stop();
     ub.resize(H);
     O3DX_TRY(read_back(ub.data(), w.counts, H * sizeof(int64_t), s));
-    O3DX_HIP(hipGetLastError());
     return 0;
   }
   if (mfma) {
@@ -1783,6 +1856,7 @@ struct SegWs {
   int64_t* mom_part2;
   int64_t* mom_out;
   int64_t* fin;  // {inlier count, pad, first sums (6), second sums (12)}
+  char* rb;       // the culled path's read-back block: counts (8 H), float64 planes (32 H), bounds (48)
 };
 
 static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
@@ -1800,6 +1874,7 @@ static size_t seg_carve(Arena& ar, int64_t n, int H, int rn, SegWs* w) {
   w->mom_part2 = ar.take<int64_t>((size_t)mom_blocks(n) * 12);
   w->mom_out = ar.take<int64_t>(16);
   w->fin = ar.take<int64_t>(24);
+  w->rb = ar.take<char>(40 * (size_t)H + 64);
   return ar.used;
 }
 
@@ -2106,35 +2181,64 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     hipLaunchKernelGGL(k_gather_samples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, xyz, w.sidx, ns, w.scoord);
   }
   // |x|,|y|,|z| bounds of the cloud: the count's float32 window and the fx
-  // quantum of the refit moments (a sharded driver passes the global ones);
-  // read back together with the sampled coordinates
+  // quantum of the refit moments (a sharded driver passes the global ones)
   O3DX_TRY(aabb_device(xyz, n, w.mm, w.aabb, s));
-  const size_t off_mm = reinterpret_cast<char*>(w.mm) - reinterpret_cast<char*>(w.scoord);
-  std::vector<char> rb(off_mm + 6 * sizeof(double));
-  O3DX_TRY(read_back(rb.data(), w.scoord, rb.size(), s));
   double absmax[3];
-  {
+  std::vector<int64_t> counts;
+  const bool device_setup = H > 0 && upper_mode(n, 0.0, thr) == 3 && !getenv("O3DX_RANSAC_HOST_SETUP");
+  if (device_setup) {
+    // the culled path without a host round trip before the sweep: Morton
+    // order, the hypotheses and their limits on the device (k_ransac_setup,
+    // the host's own plane math), the sweep; then {counts, float64 planes,
+    // bounds} come back in one read
+    O3DX_TRY(bin_points(xyz, n, w.mm, w.cw, s));
+    int64_t* rb_counts = reinterpret_cast<int64_t*>(w.rb);
+    double* rb_pl64 = reinterpret_cast<double*>(w.rb + 8 * (size_t)H);
+    double* rb_mm = reinterpret_cast<double*>(w.rb + 40 * (size_t)H);
+    hipLaunchKernelGGL(k_ransac_setup, dim3((unsigned)((H + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, w.scoord, H,
+                       ransac_n, w.mm, thr, w.cw.pl32, w.cw.band, w.cw.degen, rb_pl64, rb_mm);
+    // the sweep's own tables (pl64 is read only by the exact form): the upload block's
+    {
+      KTimer kt("plane_count_upper", s);
+      O3DX_TRY(launch_cull(n, H, thr, w.cw, false, s, rb_counts));
+    }
+    std::vector<char> rb(40 * (size_t)H + 6 * sizeof(double));
+    O3DX_TRY(read_back(rb.data(), w.rb, rb.size(), s));
+    counts.resize(H);
+    std::memcpy(counts.data(), rb.data(), 8 * (size_t)H);
+    std::memcpy(planes.data(), rb.data() + 8 * (size_t)H, 32 * (size_t)H);
     double mmh[6];
-    std::memcpy(mmh, rb.data() + off_mm, sizeof(mmh));
+    std::memcpy(mmh, rb.data() + 40 * (size_t)H, sizeof(mmh));
     for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(mmh[a]), std::fabs(mmh[3 + a]));
-  }
-  // the culled sweep's Morton order: queued now, it runs while the host
-  // computes the hypotheses
-  if (H > 0 && upper_mode(n, 0.0, thr) == 3) O3DX_TRY(bin_points(xyz, n, w.mm, w.cw, s));
-  if (H > 0) {
-    const float* sc = reinterpret_cast<const float*>(rb.data());
-    std::vector<double> P((size_t)ransac_n * 3);
-    for (int h = 0; h < H; ++h) {
-      for (int j = 0; j < ransac_n * 3; ++j) P[j] = (double)sc[(size_t)h * ransac_n * 3 + j];
-      plane_from_pts(P.data(), ransac_n, &planes[(size_t)4 * h]);
+    w.cw.exact_counts = false;
+  } else {
+    // read back together with the sampled coordinates
+    const size_t off_mm = reinterpret_cast<char*>(w.mm) - reinterpret_cast<char*>(w.scoord);
+    std::vector<char> rb(off_mm + 6 * sizeof(double));
+    O3DX_TRY(read_back(rb.data(), w.scoord, rb.size(), s));
+    {
+      double mmh[6];
+      std::memcpy(mmh, rb.data() + off_mm, sizeof(mmh));
+      for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(mmh[a]), std::fabs(mmh[3 + a]));
+    }
+    // the culled sweep's Morton order: queued now, it runs while the host
+    // computes the hypotheses
+    if (H > 0 && upper_mode(n, 0.0, thr) == 3) O3DX_TRY(bin_points(xyz, n, w.mm, w.cw, s));
+    if (H > 0) {
+      const float* sc = reinterpret_cast<const float*>(rb.data());
+      std::vector<double> P((size_t)ransac_n * 3);
+      for (int h = 0; h < H; ++h) {
+        for (int j = 0; j < ransac_n * 3; ++j) P[j] = (double)sc[(size_t)h * ransac_n * 3 + j];
+        plane_from_pts(P.data(), ransac_n, &planes[(size_t)4 * h]);
+      }
     }
   }
   const double A = std::max(absmax[0], std::max(absmax[1], absmax[2]));
   int best = -1;
   if (H > 0) {
     // upper bounds for all, exact counts for the hypotheses the replay consults
-    std::vector<int64_t> counts;
-    O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax, true));
+    if (!device_setup)
+      O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax, true));
     std::vector<uint8_t> known(H, w.cw.exact_counts ? 1 : 0);  // the culled sweep's counts are exact
     std::vector<double> sub;
     std::vector<int64_t> ec;

@@ -284,6 +284,28 @@ def test_segment_plane_parity(dev, n, iters, ransac_n):
     np.testing.assert_allclose(plane, rplane, rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("ransac_n", [3, 6])
+def test_segment_plane_device_setup_equals_host(dev, monkeypatch, ransac_n):
+    """segment_plane's culled path forms the hypotheses on the device
+    (k_ransac_setup) with the host's own plane math: the same plane and
+    inliers bit for bit as the host-setup path (O3DX_RANSAC_HOST_SETUP), the
+    planes of every hypothesis included (through the chosen plane and its
+    refit), on a planted plane and on degenerate (repeated-point) samples."""
+    n = 100_000
+    pts = S.planted_plane(n, 41).numpy()
+    samples = O.ransac_samples(n, ransac_n, 500, 13).reshape(500, ransac_n)
+    samples[::7, 1] = samples[::7, 0]  # every 7th hypothesis degenerate for ransac_n = 3
+    x = torch.from_numpy(pts).to(dev)
+    p_dev, i_dev = ops.segment_plane(x, 0.01, ransac_n, 500, samples=samples)
+    monkeypatch.setenv("O3DX_RANSAC_HOST_SETUP", "1")
+    p_host, i_host = ops.segment_plane(x, 0.01, ransac_n, 500, samples=samples)
+    assert np.array_equal(np.asarray(p_dev), np.asarray(p_host))
+    assert torch.equal(i_dev, i_host)
+    rplane, rinl, _, _, _ = O.segment_plane(pts, 0.01, ransac_n, 500, samples)
+    assert np.array_equal(i_dev.cpu().numpy().astype(np.int64), rinl)
+    np.testing.assert_allclose(p_dev, rplane, rtol=0, atol=1e-9)
+
+
 def test_segment_plane_ties_small(dev):
     # tiny cloud: many hypotheses tie in count -> rmse tie-break path
     pts = S.planted_plane(60, 3).numpy()
