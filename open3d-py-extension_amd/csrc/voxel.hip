@@ -470,9 +470,12 @@ __host__ __device__ static Bricks plan_bricks(int nx, int ny, int nz, int max_bu
 
 // The one-pass binning's plan from the bounds, the same function on the host
 // and (pre-launched, before the host has the bounds) on the device.
-// the one-pass kernel's LDS (64 KB stage + 8 B per brick + statics) stays
-// under 80 KB for this many bricks: two workgroups per CU
-constexpr int kFuseMaxBricks = 1536;
+// The one-pass kernel's LDS (128 KB stage + 8 B per brick + statics) fits
+// one workgroup per CU up to this many bricks.  2048 admits C4's 50M cloud
+// (232^3 voxels: 1800 bricks of 2^13), which at 1536 fell to count +
+// scatter (1.24 ms against ~0.4 ms); plan_bricks still prefers 2^12-voxel
+// bricks when they fit (C2: 614).
+constexpr int kFuseMaxBricks = 2048;
 static int64_t dense_cap(int64_t n);
 static int64_t entries_cap(int64_t n);
 __host__ __device__ inline int64_t dense_cap_hd(int64_t n) { return 2 * n + (1 << 20); }
