@@ -521,6 +521,24 @@ __host__ __device__ inline void fused_plan(const double mn[3], const double mx[3
   P->ok = 1;
 }
 
+// The same plan on a given geometry (the slab path's x-key window: g.kx0,
+// g.nx = the window's width).
+inline void fused_plan_geom(const VoxelGeom& g, int64_t n, int allow, uint64_t skip_key, BinPlan* P) {
+  P->ok = 0;
+  P->cap = 0;
+  const double nvox = (double)g.nx * (double)g.ny * (double)g.nz;
+  if (!allow || n <= 0 || !(nvox <= (double)dense_cap_hd(n))) return;
+  const Bricks b = plan_bricks(g.nx, g.ny, g.nz, kFuseMaxBricks);
+  if (b.nb <= 0 || b.nb > kFuseMaxBricks) return;
+  const int64_t seg = entries_cap_hd(n) / b.nb;
+  const double full = (double)n * (double)(1ll << (b.sx + b.sy + b.sz)) / nvox;
+  if (seg > INT32_MAX || !((double)seg >= 1.03 * full + 2048.0) || geom_key(g, n) == skip_key) return;
+  P->g = g;
+  P->b = b;
+  P->cap = (int)seg;
+  P->ok = 1;
+}
+
 __global__ void k_bin_plan(const double* mm, double vs, int64_t n, int allow, uint64_t skip_key,
                            BinPlan* __restrict__ plan) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -984,7 +1002,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     return 0;
   };
   // one-pass binning allowed (the plan decides whether it applies)
-  const int allow_fused = !getenv("O3DX_VOXEL_TWOPASS") && !getenv("O3DX_VOXEL_PLAIN") && !xwin ? 1 : 0;
+  const int allow_fused = !getenv("O3DX_VOXEL_TWOPASS") && !getenv("O3DX_VOXEL_PLAIN") ? 1 : 0;
   bool pre_launched = false;
   if (!min_bound_host || !max_bound_host) {
     double mm[6];
@@ -1071,8 +1089,11 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       // brick's share of a uniform cloud with room to spare (and this
       // geometry did not overflow last time)
       BinPlan plan;
-      fused_plan(mn, mx, voxel_size, n, fused_ok && allow_fused, g_fused_overflow_key, &plan);
-      const bool fused = plan.ok && !xwin;
+      if (xwin)  // the slab's window: its own geometry (round 4; count + scatter before)
+        fused_plan_geom(g, n, fused_ok && allow_fused, g_fused_overflow_key, &plan);
+      else
+        fused_plan(mn, mx, voxel_size, n, fused_ok && allow_fused, g_fused_overflow_key, &plan);
+      const bool fused = plan.ok;
       if (fused) bricks = plan.b;  // the one-pass plan's (larger) bricks
       const int cap = fused ? plan.cap : 0;
       if (fused && attempt == 0 && pre_launched) {
