@@ -274,6 +274,50 @@ __global__ void __launch_bounds__(kBlock) k_tile_compact_u8(const uint8_t* __res
   }
 }
 
+// k_tile_compact_u8 with the tile's first output row formed in the block from
+// the raw tile sums (no k_scan_partials launch: the block adds the sums of the
+// tiles before it, at most a few thousand L2-resident words); the last tile
+// writes the total.
+__global__ void __launch_bounds__(kBlock) k_tile_compact_u8_sums(const uint8_t* __restrict__ f, int64_t n,
+                                                                 const int32_t* __restrict__ part,
+                                                                 int32_t* __restrict__ idx_out,
+                                                                 int32_t* __restrict__ pos_out,
+                                                                 int64_t* __restrict__ count_dev) {
+  __shared__ int sh[kBlock / 64 + 1];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  uint8_t v[kScanItems];
+  if (base + kScanItems <= n) {
+    uint4 q = *reinterpret_cast<const uint4*>(f + base);
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(&q);
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) v[j] = b[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      int64_t i = base + j;
+      v[j] = (i < n) ? f[i] : 0;
+    }
+  }
+  int p0 = 0;
+  for (unsigned t = threadIdx.x; t < blockIdx.x; t += kBlock) p0 += part[t];
+  int first;
+  block_excl_scan<kBlock>(p0, sh, &first);
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) s += v[j] != 0;
+  int tot;
+  int ex = block_excl_scan<kBlock>(s, sh, &tot) + first;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *count_dev = (int64_t)first + tot;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = base + j;
+    if (i < n) {
+      if (pos_out) pos_out[i] = ex;
+      if (v[j]) idx_out[ex++] = (int32_t)i;
+    }
+  }
+}
+
 size_t scan_workspace_ints(int64_t n) { return (size_t)((n + kScanTile - 1) / kScanTile) + 64; }
 
 int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp, hipStream_t s) {
@@ -314,9 +358,14 @@ int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* po
     return 0;
   }
   hipLaunchKernelGGL(k_tile_sums_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp);
-  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, tmp, tiles, (int32_t*)nullptr, count_dev);
-  hipLaunchKernelGGL(k_tile_compact_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp, idx_out,
-                     pos_out);
+  if (tiles <= 4096) {  // the blocks read tiles^2 / 2 words in all (C2: 3M, from L2)
+    hipLaunchKernelGGL(k_tile_compact_u8_sums, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp, idx_out,
+                       pos_out, count_dev);
+  } else {
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, tmp, tiles, (int32_t*)nullptr, count_dev);
+    hipLaunchKernelGGL(k_tile_compact_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp, idx_out,
+                       pos_out);
+  }
   O3DX_HIP(hipGetLastError());
   return 0;
 }
