@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define O3DX_ABI_VERSION 4
+#define O3DX_ABI_VERSION 5
 
 #define O3DX_OK 0
 #define O3DX_EIO (-5)
@@ -62,7 +62,7 @@ extern "C" {
  *   [30..31] reserved (0) */
 #define O3DX_ICP_NSUMS 32
 /* length of the ICP target descriptor (doubles) */
-#define O3DX_ICP_DESC_LEN 16
+#define O3DX_ICP_DESC_LEN 24
 
 /* ---------------------------------------------------------------- misc */
 int o3dx_abi_version(void);
@@ -523,6 +523,78 @@ int64_t o3dx_lzf_decompress(const uint8_t* src_host, int64_t n, uint8_t* dst_hos
 int o3dx_pcd_unpack(const uint8_t* data_dev, int64_t n, int nfields, const int32_t* types_host,
                     const int64_t* src_off_host, const int64_t* src_stride_host,
                     float* const* dst_dev_host, const int64_t* dst_stride_host, void* stream);
+
+/* ------------------------------------------------------- float64 boundary
+ * (ABI 5) The hot-path calls on (n,3) float64 clouds, computed on the
+ * caller's float64 values exactly as Open3D computes them on its float64
+ * storage (set_points keeps a float64 Vector3dVector, reference
+ * PointCloud.py:99-102; LAS / E57 scans at georeferenced offsets,
+ * :535-547, :646-687, are not float32-representable).  Same arguments,
+ * errors and workspace rules as the float32 entry points named; the
+ * PointCloud front end takes these only for clouds float32 cannot hold.
+ *
+ * o3dx_aabb_f64: get_min_bound / get_max_bound (PointCloud.py:145-146).
+ * o3dx_voxel_down_sample_f64: voxel_down_sample_and_trace + idxmat.max(1)
+ *   (PointCloud.py:338-341): keys floor((p - min) / vs) in float64;
+ *   rep_xyz_dev (nullable) receives the representatives' float64 coordinates;
+ *   the trace outputs as o3dx_voxel_down_sample.  ENOTSUP beyond 2^22 voxels
+ *   per axis.
+ * o3dx_estimate_normals_f64: estimate_normals (PointCloud.py:68-73): kNN /
+ *   hybrid / radius sets by float64 (d^2, index), Open3D's raw-moment
+ *   covariance summed in that order (float64, unfused) and FastEigen3x3;
+ *   normals out float32.
+ * o3dx_knn_search_f64: KDTreeFlann.search_knn / hybrid (PointCloud.py:148-163)
+ *   for float64 points and queries.
+ * o3dx_plane_count_f64 / o3dx_segment_plane_f64: exact per-hypothesis counts
+ *   |(a x + c z) + (b y + d)| < thr on the float64 coordinates, and
+ *   segment_plane (PointCloud.py:75-77) over them.
+ * o3dx_icp_target_build_f64 / o3dx_spatial_sort_f64 (sorted4: (n,4) float64,
+ *   w = original index) / o3dx_icp_register_f64 /
+ *   o3dx_registration_icp_point_to_plane_f64: point-to-plane ICP with float64
+ *   sources and targets (float32 target normals); a float64 target descriptor
+ *   is refused by the float32 ICP entries and vice versa. */
+size_t o3dx_aabb_f64_workspace_bytes(int64_t n);
+int o3dx_aabb_f64(const double* xyz_dev, int64_t n, double* minmax_host, void* ws, size_t ws_bytes, void* stream);
+size_t o3dx_voxel_f64_workspace_bytes(int64_t n);
+int o3dx_voxel_down_sample_f64(const double* xyz_dev, int64_t n, const double* min_bound_host,
+                               const double* max_bound_host, double voxel_size, int32_t* rep_idx_dev,
+                               double* rep_xyz_dev, int64_t* m_host, int32_t* voxel_of_point_dev,
+                               int32_t* cubic_id_dev, void* ws, size_t ws_bytes, void* stream);
+size_t o3dx_normals_f64_workspace_bytes(int64_t n);
+int o3dx_estimate_normals_f64(const double* xyz_dev, int64_t n, int mode, int knn, double radius,
+                              const float* prior_normals_dev, float* normals_out_dev, float* kd2_out_dev,
+                              void* ws, size_t ws_bytes, void* stream);
+size_t o3dx_knn_f64_workspace_bytes(int64_t n);
+int o3dx_knn_search_f64(const double* xyz_dev, int64_t n, const double* queries_dev, int64_t nq, int mode,
+                        int knn, double radius, int32_t* idx_out_dev, double* d2_out_dev, int32_t* cnt_out_dev,
+                        void* ws, size_t ws_bytes, void* stream);
+int o3dx_plane_count_f64(const double* xyz_dev, int64_t n, const double* planes_host, int H, double thr,
+                         int64_t* counts_host, void* ws, size_t ws_bytes, void* stream);
+size_t o3dx_segment_plane_f64_workspace_bytes(int64_t n, int num_iterations);
+int o3dx_segment_plane_f64(const double* xyz_dev, int64_t n, double distance_threshold, int ransac_n,
+                           int num_iterations, double probability, const int32_t* samples_host,
+                           double* plane_host, int32_t* inliers_out_dev, int64_t* n_inliers_host, void* ws,
+                           size_t ws_bytes, void* stream);
+size_t o3dx_icp_target_f64_workspace_bytes(int64_t nt);
+int o3dx_icp_target_build_f64(const double* tgt_dev, const float* tgt_normals_dev, int64_t nt,
+                              double max_correspondence_distance, void* target_ws, size_t target_ws_bytes,
+                              double* desc_host, void* stream);
+size_t o3dx_spatial_sort_f64_workspace_bytes(int64_t n);
+int o3dx_spatial_sort_f64(const double* xyz_dev, int64_t n, double target_occ, double* sorted4_dev, void* ws,
+                          size_t ws_bytes, void* stream);
+int o3dx_icp_register_f64(const double* src_dev, int64_t ns, int src_sorted4, const void* target_ws,
+                          const double* desc_host, const double* init_host, int max_iteration,
+                          double relative_fitness, double relative_rmse, double max_correspondence_distance,
+                          const double* src_absmax_host, double* T_out_host, double* fitness_host,
+                          double* inlier_rmse_host, int32_t* corr_out_dev, int64_t* ncorr_host, void* ws,
+                          size_t ws_bytes, void* stream);
+size_t o3dx_registration_icp_f64_workspace_bytes(int64_t ns);
+int o3dx_registration_icp_point_to_plane_f64(
+    const double* src_dev, int64_t ns, const double* tgt_dev, const float* tgt_normals_dev, int64_t nt,
+    double max_correspondence_distance, const double* init_host, int max_iteration, double relative_fitness,
+    double relative_rmse, double* T_out_host, double* fitness_host, double* inlier_rmse_host,
+    int32_t* corr_out_dev, int64_t* ncorr_host, void* target_ws, size_t target_ws_bytes, void* ws,
+    size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

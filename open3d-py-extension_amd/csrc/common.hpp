@@ -317,5 +317,8 @@ int aabb_end(double mm_host[6], hipStream_t s);
 // device view of the bounds aabb_begin's kernels publish ({min, max}, 6
 // doubles): readable by kernels queued after it on the same stream
 const double* aabb_mailbox_dev();
+// AABB of float64 points into a device double[6] (no sync); ws: aabb64_ws_bytes
+size_t aabb64_ws_bytes();
+int aabb64_device(const double* xyz, int64_t n, double* mm_dev, void* ws, hipStream_t s);
 
 }  // namespace o3dx

@@ -644,9 +644,91 @@ int aabb_device(const float* xyz, int64_t n, double* mm_dev, void* ws, hipStream
   return 0;
 }
 
+// ---------------------------------------------------------- float64 AABB
+// The float64 boundary (o3dx_*_f64): min / max per axis of an (n,3) float64
+// cloud, Geometry3D::ComputeMinBound/MaxBound on Open3D's float64 storage.
+// Block partials then one final block (min / max are order-independent).
+constexpr int kAabb64Blocks = 1024;
+
+__global__ void __launch_bounds__(kBlock) k_aabb64_partial(const double* __restrict__ xyz, int64_t n,
+                                                           double* __restrict__ part) {
+  double mn[3] = {INFINITY, INFINITY, INFINITY};
+  double mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double v = xyz[3 * i + a];
+      mn[a] = fmin(mn[a], v);
+      mx[a] = fmax(mx[a], v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fmin(mn[a], __shfl_xor(mn[a], o, 64));
+      mx[a] = fmax(mx[a], __shfl_xor(mx[a], o, 64));
+    }
+  __shared__ double sh[kBlock / 64][6];
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0)
+    for (int a = 0; a < 3; ++a) {
+      sh[w][a] = mn[a];
+      sh[w][3 + a] = mx[a];
+    }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double r = sh[0][threadIdx.x];
+    for (int k = 1; k < kBlock / 64; ++k)
+      r = threadIdx.x < 3 ? fmin(r, sh[k][threadIdx.x]) : fmax(r, sh[k][threadIdx.x]);
+    part[blockIdx.x * 6 + threadIdx.x] = r;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_aabb64_final(const double* __restrict__ part, int nb, int64_t n,
+                                                       double* __restrict__ mm) {
+  __shared__ double sh[6][171];
+  const int a = threadIdx.x % 6, g = threadIdx.x / 6;
+  if (g < 170) {
+    double r = a < 3 ? INFINITY : -INFINITY;
+    for (int b = g; b < nb; b += 170) r = a < 3 ? fmin(r, part[b * 6 + a]) : fmax(r, part[b * 6 + a]);
+    sh[a][g] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double r = sh[a][0];
+    for (int k = 1; k < 170; ++k) r = a < 3 ? fmin(r, sh[a][k]) : fmax(r, sh[a][k]);
+    mm[a] = n == 0 ? 0.0 : r;
+  }
+}
+
+size_t aabb64_ws_bytes() { return Arena::align(kAabb64Blocks * 6 * sizeof(double)) + 256; }
+
+int aabb64_device(const double* xyz, int64_t n, double* mm_dev, void* ws, hipStream_t s) {
+  double* part = reinterpret_cast<double*>(ws);
+  const int nb = (int)std::min<int64_t>(kAabb64Blocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL(k_aabb64_partial, dim3(nb), dim3(kBlock), 0, s, xyz, n, part);
+  hipLaunchKernelGGL(k_aabb64_final, dim3(1), dim3(1024), 0, s, part, nb, n, mm_dev);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace o3dx
 
 using namespace o3dx;
+
+extern "C" size_t o3dx_aabb_f64_workspace_bytes(int64_t) { return aabb64_ws_bytes() + 256; }
+
+extern "C" int o3dx_aabb_f64(const double* xyz, int64_t n, double* minmax_host, void* ws, size_t ws_bytes,
+                             void* stream) {
+  if (n < 0 || (n > 0 && !xyz) || !minmax_host) return fail(O3DX_EINVAL, "o3dx_aabb_f64: bad arguments");
+  if (!ws || ws_bytes < o3dx_aabb_f64_workspace_bytes(n)) return fail(O3DX_ENOMEM, "o3dx_aabb_f64: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* mm = reinterpret_cast<double*>((char*)ws + aabb64_ws_bytes());
+  O3DX_TRY(aabb64_device(xyz, n, mm, ws, s));
+  O3DX_TRY(read_back(minmax_host, mm, 6 * sizeof(double), s));
+  return 0;
+}
 
 extern "C" int o3dx_abi_version(void) { return O3DX_ABI_VERSION; }
 

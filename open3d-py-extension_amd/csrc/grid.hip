@@ -2743,6 +2743,172 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
   return 0;
 }
 
+// ------------------------------------------------------ float64 clouds
+// The float64 boundary (include/o3dx.h).  Open3D keeps points as float64
+// (Vector3dVector, reference PointCloud.py:99-102) and computes kNN d^2 and
+// the covariance moments on them; a float64 cloud that float32 cannot hold
+// (LAS / E57 scans at georeferenced offsets, PointCloud.py:535-547, 646-687)
+// must not be rounded.  The search frame is float32 p - o (o = the cloud's
+// minimum bound, so the frame's magnitudes are the cloud's extent, and its
+// rounding stays inside the grid's slack); every deciding d^2 and every
+// moment comes from the exact float64 coordinates sorted alongside
+// (GridView::pts64).
+
+__global__ void __launch_bounds__(kBlock) k_proxy64(const double* __restrict__ xyz, int64_t n, double ox, double oy,
+                                                    double oz, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    out[3 * i] = (float)(xyz[3 * i] - ox);
+    out[3 * i + 1] = (float)(xyz[3 * i + 1] - oy);
+    out[3 * i + 2] = (float)(xyz[3 * i + 2] - oz);
+  }
+}
+
+// pts64[p] = the exact coordinates of sorted point p (w = original index)
+__global__ void __launch_bounds__(kBlock) k_sort64(const float4* __restrict__ pts, int64_t n,
+                                                   const double* __restrict__ xyz, double4* __restrict__ pts64) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int i = __float_as_int(pts[p].w);
+    pts64[p] = make_double4(xyz[3 * (int64_t)i], xyz[3 * (int64_t)i + 1], xyz[3 * (int64_t)i + 2], (double)i);
+  }
+}
+
+size_t grid64_ws_bytes(int64_t n, int cap_mult) {
+  n = std::max<int64_t>(n, 1);
+  return Arena::align(n * 3 * sizeof(float) + 1) + Arena::align(n * sizeof(double4) + 1) +
+         Arena::align(aabb64_ws_bytes() + 64) + grid_ws_bytes(n, cap_mult) + 1024;
+}
+
+int grid64_build(const double* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
+                 hipStream_t s, GridBuild* out, const float* extra_src, int cap_mult, bool blocked,
+                 const double* mm_host) {
+  if (ws_bytes < grid64_ws_bytes(n, cap_mult)) return fail(O3DX_ENOMEM, "float64 grid workspace too small");
+  Arena ar(ws, ws_bytes);
+  float* proxy = ar.take<float>((size_t)std::max<int64_t>(n, 1) * 3);
+  double4* pts64 = ar.take<double4>((size_t)std::max<int64_t>(n, 1));
+  char* aws = ar.take<char>(aabb64_ws_bytes() + 64);
+  const size_t gbytes = grid_ws_bytes(n, cap_mult);
+  char* gws = ar.take<char>(gbytes);
+  O3DX_ARENA_CHECK(ar);
+  double mm[6] = {0, 0, 0, 0, 0, 0};
+  if (mm_host) {
+    std::memcpy(mm, mm_host, sizeof(mm));
+  } else if (n > 0) {
+    double* mmd = reinterpret_cast<double*>(aws + aabb64_ws_bytes());
+    O3DX_TRY(aabb64_device(xyz, n, mmd, aws, s));
+    O3DX_TRY(read_back(mm, mmd, sizeof(mm), s));
+  }
+  if (n > 0)
+    hipLaunchKernelGGL(k_proxy64, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, mm[0], mm[1], mm[2],
+                       proxy);
+  O3DX_TRY(grid_build(proxy, n, target_occ, min_h, gws, gbytes, s, out, nullptr, extra_src, blocked, cap_mult));
+  if (n > 0)
+    hipLaunchKernelGGL(k_sort64, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, out->pts, n, xyz, pts64);
+  O3DX_HIP(hipGetLastError());
+  out->pts64 = pts64;
+  out->view.pts64 = pts64;
+  out->view.o64x = mm[0];
+  out->view.o64y = mm[1];
+  out->view.o64z = mm[2];
+  return 0;
+}
+
+// Open3D ComputeCovariance on float64 storage: the nine cumulants summed in
+// the neighbours' result order (nanoflann's: (d^2, index) ascending), each
+// product rounded then added (the build's -ffp-contract=off) — the float64
+// coordinates' products are not exact, so the order and the roundings are
+// Open3D's own, for the same bits.
+struct MomAccSeq {
+  double m[9];
+  __device__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) m[j] = 0.0;
+  }
+  __device__ void add(double x, double y, double z) {
+    m[0] += x;
+    m[1] += y;
+    m[2] += z;
+    m[3] += x * x;
+    m[4] += x * y;
+    m[5] += x * z;
+    m[6] += y * y;
+    m[7] += y * z;
+    m[8] += z * z;
+  }
+  __device__ void cov(int k, double c[6]) const {
+    MomAcc a;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) a.m[j] = m[j];
+    a.cov(k, c);
+  }
+};
+
+// Normals of a float64 cloud, a lane per point (sorted order): KNN / HYBRID
+// through the register top-K in (d^2, index) order; RADIUS (every neighbour
+// within r, sorted, Open3D's SearchRadius) read off in sorted pages of 32.
+template <int K>
+__global__ void __launch_bounds__(kBlock) k_normals_knn64(GridView g, const double* __restrict__ xyz, int kneed,
+                                                          int mode, double radius, const float* __restrict__ prior,
+                                                          float* __restrict__ out) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.n) return;
+  const double4 q = g.pts64[s];
+  const int oi = (int)q.w;
+  MomAccSeq acc;
+  acc.zero();
+  int cnt = 0;
+  if (mode == O3DX_SEARCH_RADIUS) {
+    double lo_d = -1.0;
+    int lo_i = -1;
+    for (;;) {
+      double bd[32];
+      int bi[32];
+      const int c = knn_search_dev64<32>(g, q.x, q.y, q.z, 32, true, radius, bd, bi, lo_d, lo_i);
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if (j < c) {
+          const int64_t id = bi[j];
+          acc.add(xyz[3 * id], xyz[3 * id + 1], xyz[3 * id + 2]);
+        }
+      cnt += c;
+      if (c < 32) break;
+      lo_d = bd[31];
+      lo_i = bi[31];
+    }
+  } else {
+    double bd[K];
+    int bi[K];
+    cnt = knn_search_dev64<K>(g, q.x, q.y, q.z, kneed, mode == O3DX_SEARCH_HYBRID, radius, bd, bi);
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (j < cnt) {
+        const int id = bi[j];
+        if (g.nbr && j < kneed) g.nbr[(int64_t)oi * kneed + j] = id;
+        if (g.kd2 && j == cnt - 1) g.kd2[oi] = (float)(bd[j] * (1.0 + 1e-6));
+        acc.add(xyz[3 * (int64_t)id], xyz[3 * (int64_t)id + 1], xyz[3 * (int64_t)id + 2]);
+      }
+  }
+  finish_normal(cnt, acc, prior, oi, out);
+}
+
+template <int K>
+__global__ void __launch_bounds__(kBlock) k_knn_query64(GridView g, const double* __restrict__ q, int64_t nq,
+                                                        int kneed, int hybrid, double radius, int kout,
+                                                        int32_t* __restrict__ idx_out, double* __restrict__ d2_out,
+                                                        int32_t* __restrict__ cnt_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  double bd[K];
+  int bi[K];
+  const int cnt = knn_search_dev64<K>(g, q[3 * i], q[3 * i + 1], q[3 * i + 2], kneed, hybrid != 0, radius, bd, bi);
+  cnt_out[i] = cnt;
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if (j < kout) {
+      idx_out[i * kout + j] = j < cnt ? bi[j] : -1;
+      if (d2_out) d2_out[i * kout + j] = j < cnt ? bd[j] : INFINITY;
+    }
+}
+
 }  // namespace o3dx
 
 using namespace o3dx;
@@ -2936,4 +3102,59 @@ extern "C" int o3dx_voxel_down_sample_normals(const float* xyz, int64_t n, const
     return 0;
   return o3dx_estimate_normals_voxel(geom, voxel_pts, rep_xyz, m, O3DX_SEARCH_KNN, knn, 0.0, nullptr, normals, nullptr,
                                      nws, nws_bytes, stream);
+}
+
+// ------------------------------------------------------ float64 boundary
+extern "C" size_t o3dx_normals_f64_workspace_bytes(int64_t n) { return grid64_ws_bytes(n) + 1024; }
+
+extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode, int knn, double radius,
+                                         const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes,
+                                         void* stream) {
+  if (n < 0 || (n > 0 && (!xyz || !out))) return fail(O3DX_EINVAL, "o3dx_estimate_normals_f64: bad arguments");
+  if (mode != O3DX_SEARCH_KNN && mode != O3DX_SEARCH_RADIUS && mode != O3DX_SEARCH_HYBRID)
+    return fail(O3DX_EINVAL, "o3dx_estimate_normals_f64: unknown search mode %d", mode);
+  if (mode != O3DX_SEARCH_RADIUS && (knn < 0 || knn > O3DX_MAX_KNN))
+    return fail(O3DX_ENOTSUP, "knn/max_nn %d outside [0, %d]", knn, O3DX_MAX_KNN);
+  if (mode != O3DX_SEARCH_KNN && !(radius > 0.0)) return fail(O3DX_EINVAL, "radius must be > 0");
+  if (!ws || ws_bytes < o3dx_normals_f64_workspace_bytes(n)) return fail(O3DX_ENOMEM, "normals workspace too small");
+  if (n == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  GridBuild G;
+  O3DX_TRY(grid64_build(xyz, n, occ_for(mode, knn), 0.0, ws, ws_bytes, s, &G));
+  const int kneed = (int)std::min<int64_t>(knn, n);
+  G.view.nbr = mode == O3DX_SEARCH_KNN ? debug_nbr(kneed, n) : nullptr;
+  G.view.kd2 = mode == O3DX_SEARCH_KNN ? kd2 : nullptr;
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  KTimer kt("normals_f64", s);
+  if (mode == O3DX_SEARCH_RADIUS)
+    hipLaunchKernelGGL(k_normals_knn64<4>, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, 0, mode, radius, prior, out);
+  else
+    O3DX_DISPATCH_K(kneed, k_normals_knn64, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius, prior,
+                    out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" size_t o3dx_knn_f64_workspace_bytes(int64_t n) { return grid64_ws_bytes(n) + 1024; }
+
+extern "C" int o3dx_knn_search_f64(const double* xyz, int64_t n, const double* queries, int64_t nq, int mode, int knn,
+                                   double radius, int32_t* idx_out, double* d2_out, int32_t* cnt_out, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  if (n < 0 || nq < 0 || (n > 0 && !xyz) || (nq > 0 && (!queries || !idx_out || !cnt_out)))
+    return fail(O3DX_EINVAL, "o3dx_knn_search_f64: bad arguments");
+  if (mode == O3DX_SEARCH_RADIUS)
+    return fail(O3DX_ENOTSUP, "o3dx_knn_search_f64: radius mode needs a variable-length result (use HYBRID)");
+  if (mode != O3DX_SEARCH_KNN && mode != O3DX_SEARCH_HYBRID) return fail(O3DX_EINVAL, "unknown search mode");
+  if (knn < 1 || knn > O3DX_MAX_KNN) return fail(O3DX_ENOTSUP, "knn %d outside [1, %d]", knn, O3DX_MAX_KNN);
+  if (!ws || ws_bytes < o3dx_knn_f64_workspace_bytes(n)) return fail(O3DX_ENOMEM, "knn workspace too small");
+  if (nq == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  GridBuild G;
+  O3DX_TRY(grid64_build(xyz, n, occ_for(mode, knn), 0.0, ws, ws_bytes, s, &G));
+  const int kneed = (int)std::min<int64_t>(knn, n);
+  const unsigned grid = (unsigned)((nq + kBlock - 1) / kBlock);
+  O3DX_DISPATCH_K(knn, k_knn_query64, dim3(grid), dim3(kBlock), 0, s, G.view, queries, nq, kneed,
+                  mode == O3DX_SEARCH_HYBRID ? 1 : 0, radius, knn, idx_out, d2_out, cnt_out);
+  O3DX_HIP(hipGetLastError());
+  return 0;
 }

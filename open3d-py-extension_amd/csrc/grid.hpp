@@ -39,6 +39,13 @@ struct GridView {
   float cox = 0.f, coy = 0.f, coz = 0.f, ch = 0.f, cinv_h = 0.f, cslack = 0.f;
   int cnx = 0, cny = 0, cnz = 0;
   const uint8_t* skip_cells = nullptr;  // outer grid: queries in flagged cells are the nested grid's
+  // float64 clouds (f64.hip): pts holds float32(p - o64), the search frame
+  // (cells, filters, reach tests; the float32 rounding of the frame is inside
+  // `slack`); pts64 the exact float64 coordinates in the same sorted order, w
+  // = the original index — every distance that decides is computed from them
+  // in nanoflann's order, as Open3D computes it on its float64 storage.
+  const double4* __restrict__ pts64 = nullptr;
+  double o64x = 0.0, o64y = 0.0, o64z = 0.0;
 };
 
 // outer sorted position / output row of a nested-grid point
@@ -192,6 +199,26 @@ __device__ __forceinline__ bool lex_less(double d, int i, double bd, int bi) {
   return d < bd || (d == bd && i < bi);
 }
 
+// nanoflann's d^2 of a float64 grid point (GridView::pts64)
+__device__ __forceinline__ double dist2_d4(double qx, double qy, double qz, const double4& p) {
+  const double dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+  double r = dx * dx;
+  r = r + dy * dy;
+  r = r + dz * dz;
+  return r;
+}
+
+// The deciding float64 d^2 of sorted point p (float32 grid point v): from the
+// exact float64 coordinates on a float64 grid (q in the cloud's own frame),
+// from v itself otherwise
+template <bool F64>
+__device__ __forceinline__ double exact_d2(const GridView& g, double qx, double qy, double qz, int p, const float4& v) {
+  if constexpr (F64)
+    return dist2_d4(qx, qy, qz, g.pts64[p]);
+  else
+    return dist2_f64(qx, qy, qz, v);
+}
+
 // Sorted top-K (by (d2, sorted position)) neighbour search.  kneed <= K.
 // mode: O3DX_SEARCH_KNN or O3DX_SEARCH_HYBRID (r2lim = radius^2, strict <).
 // On return bd/bi[0..cnt) hold the neighbours, nearest first; bi are original
@@ -259,12 +286,83 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
   return cnt;
 }
 
+// knn_search_dev on a float64 grid (GridView::pts64): q in the cloud's own
+// frame, every candidate's d^2 from its exact float64 coordinates.  Paging:
+// only candidates after (lo_d, lo_i) in (d^2, index) order are taken, so a
+// radius search of any size is read off in sorted pages of K (the default
+// (-1, -1) takes all).  Returns the count; bd/bi as knn_search_dev.
+template <int K>
+__device__ __forceinline__ int knn_search_dev64(const GridView& g, double qx, double qy, double qz, int kneed,
+                                                bool hybrid, double radius, double bd[K], int bi[K],
+                                                double lo_d = -1.0, int lo_i = -1) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    bd[j] = INFINITY;
+    bi[j] = 0x7fffffff;
+  }
+  if (g.n == 0 || kneed <= 0) return 0;
+  const double gqx = qx - g.o64x, gqy = qy - g.o64y, gqz = qz - g.o64z;
+  int cx, cy, cz;
+  grid_cell(g, (float)gqx, (float)gqy, (float)gqz, cx, cy, cz);
+  const int rmax = shell_rmax(g, cx, cy, cz);
+  const double r2lim = hybrid ? radius * radius : INFINITY;
+  double wd = INFINITY;
+  int wi = 0x7fffffff;
+  int cnt = 0;
+  int st_cells = 0, st_cands = 0, r = 0;
+  for (r = 0; r <= rmax; ++r) {
+    for_shell(g, cx, cy, cz, r, [&](int c) {
+      const int s1 = g.start[c + 1];
+      if (g.stats) {
+        ++st_cells;
+        st_cands += s1 - g.start[c];
+      }
+      for (int p = g.start[c]; p < s1; ++p) {
+        const double4 v = g.pts64[p];
+        const double d = dist2_d4(qx, qy, qz, v);
+        if (!(d < r2lim)) continue;
+        const int oi = (int)v.w;
+        if (!lex_less(lo_d, lo_i, d, oi)) continue;  // an earlier page's
+        if (lex_less(d, oi, wd, wi)) {
+#pragma unroll
+          for (int j = K - 1; j >= 0; --j) {
+            const bool lt = lex_less(d, oi, bd[j], bi[j]);
+            const bool ltp = (j > 0) ? lex_less(d, oi, bd[j > 0 ? j - 1 : 0], bi[j > 0 ? j - 1 : 0]) : false;
+            if (ltp) {
+              bd[j] = bd[j - 1];
+              bi[j] = bi[j - 1];
+            } else if (lt) {
+              bd[j] = d;
+              bi[j] = oi;
+            }
+          }
+          cnt = cnt < kneed ? cnt + 1 : kneed;
+          if (cnt == kneed) {
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+              if (j == kneed - 1) {
+                wd = bd[j];
+                wi = bi[j];
+              }
+          }
+        }
+      }
+    });
+    const double B = cube_reach(g, gqx, gqy, gqz, cx, cy, cz, r) - g.slack;
+    if (cnt >= kneed && B > 0.0 && wd < B * B) break;
+    if (hybrid && B >= radius) break;
+  }
+  search_stats(g, st_cells, st_cands, r + 1);
+  return cnt;
+}
+
 // Nearest neighbour with d^2 < radius^2 (SearchHybrid(p, r, 1)); returns its
 // original index, -1 if none.  ROWS: the walk beyond the own cell goes by
 // (y, z) rows (below); else by Chebyshev shells of cells.
 // SHARE: the lanes calling together share first bounds (below); every lane
 // of the wave that runs the search must call it at once.
-template <bool ROWS = true, bool SHARE = false>
+// F64: a float64 grid (GridView::pts64), q in the cloud's own frame.
+template <bool ROWS = true, bool SHARE = false, bool F64 = false>
 __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, double qy, double qz, double radius,
                                              double* best_d2, int* best_pos, int prior = -1) {
   double bd = INFINITY;
@@ -274,7 +372,9 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
     *best_pos = -1;
     return -1;
   }
-  const float fx = (float)qx, fy = (float)qy, fz = (float)qz;
+  // q in the grid's frame (float64 grids: relative to o64)
+  const double gqx = F64 ? qx - g.o64x : qx, gqy = F64 ? qy - g.o64y : qy, gqz = F64 ? qz - g.o64z : qz;
+  const float fx = (float)gqx, fy = (float)gqy, fz = (float)gqz;
   int cx, cy, cz;
   // queries may lie outside the grid box: clamped to the nearest cell (cube_reach
   // only counts faces with cells beyond them, so the bound stays valid)
@@ -297,7 +397,7 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   const float sl3 = 3.0f * g.slack;
   auto visit_point = [&](int p, const float4 v) {
     if (dist2_f32(qf, v.x, v.y, v.z) < thr) {
-      const double d = dist2_f64(qx, qy, qz, v);
+      const double d = exact_d2<F64>(g, qx, qy, qz, p, v);
       const int oi = __float_as_int(v.w);
       if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
         bd = d;
@@ -440,7 +540,7 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
   }
   for (;; ++r) {
     // every point within B of q has been visited (or pruned by the bound)
-    const double B = cube_reach(g, qx, qy, qz, cx, cy, cz, r) - g.slack;
+    const double B = cube_reach(g, gqx, gqy, gqz, cx, cy, cz, r) - g.slack;
     if (B >= radius || r >= rmax) break;
     if (bi >= 0 && B > 0.0 && bd < B * B) break;
     const int rr = r + 1;
@@ -592,6 +692,7 @@ struct GridBuild {
   int64_t* scratch;
   int64_t cap_cells;
   GridView view;
+  double4* pts64 = nullptr;  // float64 grids (grid64_build): exact coordinates + index, sorted like pts
 };
 
 size_t grid_ws_bytes(int64_t n, int cap_mult = 4);
@@ -608,5 +709,16 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
                hipStream_t s, GridBuild* out, float4* extra_sorted = nullptr, const float* extra_src = nullptr,
                bool blocked = false, int cap_mult = 4, bool ordered = true, const int32_t* ids = nullptr,
                double max_h = 0.0);
+
+// Float64 clouds (include/o3dx.h "float64 boundary"): a grid over the
+// float32 frame coordinates p - o (o = the cloud's float64 minimum bound),
+// with the exact float64 coordinates sorted alongside (GridView::pts64, w =
+// original index).  Workspace: grid64_ws_bytes.  extra_src: a float32 (n,3)
+// payload sorted alongside (G.extra; ICP target normals).  mm_host
+// (nullable): the cloud's {min, max} when the caller has it.
+size_t grid64_ws_bytes(int64_t n, int cap_mult = 4);
+int grid64_build(const double* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
+                 hipStream_t s, GridBuild* out, const float* extra_src = nullptr, int cap_mult = 4,
+                 bool blocked = false, const double* mm_host = nullptr);
 
 }  // namespace o3dx

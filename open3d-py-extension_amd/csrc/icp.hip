@@ -274,19 +274,36 @@ struct Mat4 {
 // Source point j -> (original index, float64 position under T).  SORTED: src
 // is float4 (x, y, z, bits(original index)) in the compact spatial order of
 // o3dx_spatial_sort, so the 64 queries of a wave probe neighbouring target
-// cells; else plain (n,3) float32 in caller order.
-template <bool SORTED>
-__device__ __forceinline__ int64_t icp_source(const float* __restrict__ src, int64_t j, const Mat4& T, double* px,
+// cells; else plain (n,3) float32 in caller order.  F64 (the float64
+// boundary): double4 (x, y, z, original index) of o3dx_spatial_sort_f64, or
+// plain (n,3) float64.
+template <bool SORTED, bool F64 = false>
+__device__ __forceinline__ int64_t icp_source(const void* __restrict__ src_, int64_t j, const Mat4& T, double* px,
                                               double* py, double* pz) {
   double x, y, z;
   int64_t i;
-  if (SORTED) {
-    const float4 v = reinterpret_cast<const float4*>(src)[j];
+  if constexpr (F64) {
+    if (SORTED) {
+      const double4 v = reinterpret_cast<const double4*>(src_)[j];
+      x = v.x;
+      y = v.y;
+      z = v.z;
+      i = (int64_t)v.w;
+    } else {
+      const double* src = reinterpret_cast<const double*>(src_);
+      i = j;
+      x = src[3 * i];
+      y = src[3 * i + 1];
+      z = src[3 * i + 2];
+    }
+  } else if (SORTED) {
+    const float4 v = reinterpret_cast<const float4*>(src_)[j];
     x = v.x;
     y = v.y;
     z = v.z;
     i = __float_as_int(v.w);
   } else {
+    const float* src = reinterpret_cast<const float*>(src_);
     i = j;
     x = src[3 * i];
     y = src[3 * i + 1];
@@ -422,8 +439,8 @@ __device__ __forceinline__ unsigned icp_xcd_block(unsigned b, unsigned nb) {
 // copies (acc[copy][2 kNS]).  mpos[j]
 // = the match's sorted target position (-1: none).  Integer sums: the same
 // bits for any split of the source over lanes, blocks or ranks.
-template <bool SORTED, bool ROWS>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_icp_step(const float* __restrict__ src, int64_t ns, GridView g,
+template <bool SORTED, bool ROWS, bool F64 = false>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_icp_step(const void* __restrict__ src, int64_t ns, GridView g,
                                                      const float4* __restrict__ tnorm,
                                                      const IcpState* __restrict__ st, double radius,
                                                      int32_t* __restrict__ mpos, int use_prior,
@@ -443,9 +460,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     int pos = -1;
     double px = 0, py = 0, pz = 0, d2 = 0;
     if (j < ns) {
-      icp_source<SORTED>(src, j, T, &px, &py, &pz);
+      icp_source<SORTED, F64>(src, j, T, &px, &py, &pz);
       // the previous iteration's match as the starting bound (exact either way)
-      nn_search_dev<ROWS, true>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
+      nn_search_dev<ROWS, true, F64>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
       mpos[j] = pos;
     }
     const bool m = pos >= 0;
@@ -453,9 +470,21 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     const double one = m ? 1.0 : 0.0;
     if (!m) d2 = 0.0;
     if (m) {
-      const float4 vt = g.pts[pos], nt = tnorm[pos];
+      double vx, vy, vz;
+      if constexpr (F64) {
+        const double4 v = g.pts64[pos];
+        vx = v.x;
+        vy = v.y;
+        vz = v.z;
+      } else {
+        const float4 v = g.pts[pos];
+        vx = v.x;
+        vy = v.y;
+        vz = v.z;
+      }
+      const float4 nt = tnorm[pos];
       const double nx = nt.x, ny = nt.y, nz = nt.z;
-      r = ((px - (double)vt.x) * nx + (py - (double)vt.y) * ny) + (pz - (double)vt.z) * nz;
+      r = ((px - vx) * nx + (py - vy) * ny) + (pz - vz) * nz;
       J[0] = py * nz - pz * ny;
       J[1] = pz * nx - px * nz;
       J[2] = px * ny - py * nx;
@@ -570,12 +599,14 @@ __global__ void __launch_bounds__(1024) k_icp_finish(IcpState* __restrict__ st, 
 
 // correspondences of the last step by original source index: cj[i] = the
 // target's original index, -1 for none
-template <bool SORTED>
-__global__ void __launch_bounds__(kBlock) k_corr_from_mpos(const float* __restrict__ src, int64_t ns, GridView g,
+template <bool SORTED, bool F64 = false>
+__global__ void __launch_bounds__(kBlock) k_corr_from_mpos(const void* __restrict__ src, int64_t ns, GridView g,
                                                            const int32_t* __restrict__ mpos, int32_t* __restrict__ cj) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += (int64_t)gridDim.x * blockDim.x) {
     const int pos = mpos[j];
-    const int64_t i = SORTED ? (int64_t)__float_as_int(reinterpret_cast<const float4*>(src)[j].w) : j;
+    const int64_t i = !SORTED ? j
+                      : F64   ? (int64_t)reinterpret_cast<const double4*>(src)[j].w
+                              : (int64_t)__float_as_int(reinterpret_cast<const float4*>(src)[j].w);
     cj[i] = pos >= 0 ? __float_as_int(g.pts[pos].w) : -1;
   }
 }
@@ -598,16 +629,26 @@ __global__ void __launch_bounds__(kBlock) k_corr_pairs(const int32_t* __restrict
 // ------------------------------------------------------------ descriptors
 constexpr double kDescMagic = 4242.0;
 
+// d[14]: offset of the float64 coordinates (float64 targets, d[15] = 1), d[16..18] their frame origin
 static void desc_pack(const GridBuild& G, const void* base, const float4* normals, double* d) {
   const GridView& g = G.view;
+  for (int k = 0; k < O3DX_ICP_DESC_LEN; ++k) d[k] = 0;
   d[0] = g.ox; d[1] = g.oy; d[2] = g.oz; d[3] = g.h; d[4] = g.inv_h; d[5] = g.slack;
   d[6] = g.nx; d[7] = g.ny; d[8] = g.nz; d[9] = (double)g.n;
   d[10] = (double)((const char*)G.pts - (const char*)base);
   d[11] = (double)((const char*)G.start - (const char*)base);
   d[12] = (double)((const char*)normals - (const char*)base);
   d[13] = kDescMagic;
-  d[14] = d[15] = 0;
+  if (G.pts64) {
+    d[14] = (double)((const char*)G.pts64 - (const char*)base);
+    d[15] = 1;
+    d[16] = g.o64x;
+    d[17] = g.o64y;
+    d[18] = g.o64z;
+  }
 }
+
+static bool desc_is_f64(const double* d) { return d && d[15] == 1; }
 
 static bool desc_unpack(const double* d, const void* base, GridView* g, const float4** normals) {
   if (!d || d[13] != kDescMagic) return false;
@@ -621,6 +662,12 @@ static bool desc_unpack(const double* d, const void* base, GridView* g, const fl
   g->pts = (const float4*)((const char*)base + (int64_t)d[10]);
   g->start = (const int32_t*)((const char*)base + (int64_t)d[11]);
   *normals = (const float4*)((const char*)base + (int64_t)d[12]);
+  if (desc_is_f64(d)) {
+    g->pts64 = (const double4*)((const char*)base + (int64_t)d[14]);
+    g->o64x = d[16];
+    g->o64y = d[17];
+    g->o64z = d[18];
+  }
   return true;
 }
 
@@ -672,8 +719,46 @@ __global__ void __launch_bounds__(kBlock) k_absmax4(const float4* __restrict__ p
     for (int a = 0; a < 3; ++a) atomicMax(&out[a], __float_as_uint(m[a]));
 }
 
-// |x|,|y|,|z| bounds of a source: (n,3) float32 or the (n,4) sorted form
-static int source_absmax(const float* src, int64_t ns, bool sorted, AccWs& w, hipStream_t s, double out[3]) {
+__global__ void __launch_bounds__(kBlock) k_absmax_d4(const double4* __restrict__ p, int64_t n,
+                                                      unsigned long long* __restrict__ out) {
+  double m[3] = {0.0, 0.0, 0.0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double4 v = p[i];
+    m[0] = fmax(m[0], fabs(v.x));
+    m[1] = fmax(m[1], fabs(v.y));
+    m[2] = fmax(m[2], fabs(v.z));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) m[a] = fmax(m[a], __shfl_xor(m[a], o, 64));
+  // non-negative doubles order as their bits
+  if ((threadIdx.x & 63) == 0)
+    for (int a = 0; a < 3; ++a) atomicMax(&out[a], (unsigned long long)__double_as_longlong(m[a]));
+}
+
+// |x|,|y|,|z| bounds of a source: (n,3) float32 or the (n,4) sorted form;
+// f64: (n,3) float64 or the double4 sorted form
+static int source_absmax(const void* src_, int64_t ns, bool sorted, AccWs& w, hipStream_t s, double out[3],
+                         bool f64 = false) {
+  if (f64) {
+    double mm[6];
+    if (sorted) {
+      unsigned long long* u = reinterpret_cast<unsigned long long*>(w.mm);
+      O3DX_HIP(hipMemsetAsync(u, 0, 4 * sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_absmax_d4, dim3(grid_for(ns, kBlock, 1024)), dim3(kBlock), 0, s,
+                         reinterpret_cast<const double4*>(src_), ns, u);
+      unsigned long long b[4];
+      O3DX_TRY(read_back(b, u, sizeof(b), s));
+      for (int a = 0; a < 3; ++a) out[a] = __builtin_bit_cast(double, b[a]);
+      return 0;
+    }
+    O3DX_TRY(aabb64_device(reinterpret_cast<const double*>(src_), ns, w.mm, w.aabb, s));
+    O3DX_TRY(read_back(mm, w.mm, sizeof(mm), s));
+    for (int a = 0; a < 3; ++a) out[a] = std::max(std::fabs(mm[a]), std::fabs(mm[3 + a]));
+    return 0;
+  }
+  const float* src = reinterpret_cast<const float*>(src_);
   if (sorted) {
     unsigned int* u = reinterpret_cast<unsigned int*>(w.mm);
     O3DX_HIP(hipMemsetAsync(u, 0, 4 * sizeof(unsigned int), s));
@@ -696,13 +781,20 @@ static int source_absmax(const float* src, int64_t ns, bool sorted, AccWs& w, hi
 }
 
 // use_prior: mpos holds the previous step's matches on this source (the loop)
-static void launch_step(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn,
+// a float64 target (g.pts64) takes a float64 source
+static void launch_step(const void* src, int64_t ns, bool sorted, const GridView& g, const float4* tn,
                         double radius, AccWs& w, hipStream_t s, int use_prior = 0) {
   const unsigned nb = step_blocks(ns);
   // O3DX_ICP_SHELL=1: the Chebyshev shell walk (round 1-2 form) instead of the row walk
   const bool shell = getenv("O3DX_ICP_SHELL") != nullptr;
   KTimer km("icp_match", s);
-  if (sorted && !shell)
+  if (g.pts64 && sorted)
+    hipLaunchKernelGGL((k_icp_step<true, true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius,
+                       w.mpos, use_prior, w.acc);
+  else if (g.pts64)
+    hipLaunchKernelGGL((k_icp_step<false, true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius,
+                       w.mpos, use_prior, w.acc);
+  else if (sorted && !shell)
     hipLaunchKernelGGL((k_icp_step<true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
                        use_prior, w.acc);
   else if (sorted)
@@ -717,13 +809,16 @@ static void launch_step(const float* src, int64_t ns, bool sorted, const GridVie
 }
 
 // correspondences of the last step into corr_out (pairs by original index)
-static int corr_of_last_step(const float* src, int64_t ns, bool sorted, const GridView& g, AccWs& w, hipStream_t s,
+static int corr_of_last_step(const void* src, int64_t ns, bool sorted, const GridView& g, AccWs& w, hipStream_t s,
                              int32_t* corr_out, int64_t* ncorr) {
   if (ns == 0) {
     if (ncorr) *ncorr = 0;
     return 0;
   }
-  if (sorted)
+  if (sorted && g.pts64)
+    hipLaunchKernelGGL((k_corr_from_mpos<true, true>), dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, src, ns, g,
+                       w.mpos, w.cj);
+  else if (sorted)
     hipLaunchKernelGGL(k_corr_from_mpos<true>, dim3(grid_for(ns, kBlock, 8192)), dim3(kBlock), 0, s, src, ns, g,
                        w.mpos, w.cj);
   else
@@ -743,7 +838,7 @@ static int corr_of_last_step(const float* src, int64_t ns, bool sorted, const Gr
 // One accumulate with T on the host (the sharded loop of distributed.py):
 // absmax: the source's coordinate bounds (host, 3) — the same on every rank
 // of a sharded source; fx_out (nullable, host 4 x kNS): the exact sums.
-static int accumulate(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, const double* T,
+static int accumulate(const void* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, const double* T,
                       double radius, const double* absmax, AccWs& w, hipStream_t s, double* sums_host,
                       int64_t* fx_out, int32_t* corr_out, int64_t* ncorr) {
   IcpState hs{};
@@ -818,6 +913,7 @@ extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, int src_sorted4
                                    double* sums, int64_t* fx_out, int32_t* corr_out, int64_t* ncorr, void* ws,
                                    size_t ws_bytes, void* stream) {
   if (ns < 0 || (ns > 0 && !src) || !target_ws || !T || !sums) return fail(O3DX_EINVAL, "o3dx_icp_accumulate: bad args");
+  if (desc_is_f64(desc)) return fail(O3DX_EINVAL, "a float64 ICP target takes a float64 source (o3dx_icp_register_f64)");
   GridView g;
   const float4* tn;
   if (!desc_unpack(desc, target_ws, &g, &tn)) return fail(O3DX_EINVAL, "invalid ICP target descriptor");
@@ -869,7 +965,7 @@ extern "C" size_t o3dx_registration_icp_workspace_bytes(int64_t ns) {
 // The whole loop on the device: every iteration's step and finish are queued
 // at once (a converged loop's remaining launches return at their first
 // instruction); the host waits once for the final state.
-static int run_loop(const float* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, double max_corr, const double* init, int max_iteration, double rel_fit,
+static int run_loop(const void* src, int64_t ns, bool sorted, const GridView& g, const float4* tn, double max_corr, const double* init, int max_iteration, double rel_fit,
                     double rel_rmse, const double* absmax, AccWs& w, hipStream_t s, double* T_out, double* fitness,
                     double* rmse, int32_t* corr_out, int64_t* ncorr) {
   IcpState hs{};
@@ -885,7 +981,7 @@ static int run_loop(const float* src, int64_t ns, bool sorted, const GridView& g
     return 0;
   }
   if (absmax) std::memcpy(hs.absmax, absmax, sizeof(hs.absmax));
-  else O3DX_TRY(source_absmax(src, ns, sorted, w, s, hs.absmax));
+  else O3DX_TRY(source_absmax(src, ns, sorted, w, s, hs.absmax, g.pts64 != nullptr));
   state_set_T(hs, T0, max_corr);
   O3DX_HIP(hipMemcpyAsync(w.st, &hs, sizeof(IcpState), hipMemcpyHostToDevice, s));
   O3DX_HIP(hipMemsetAsync(w.acc, 0, (size_t)kIcpCopies * 2 * kNS * sizeof(int64_t), s));
@@ -917,6 +1013,7 @@ extern "C" int o3dx_icp_register(const float* src, int64_t ns, int src_sorted4, 
   if (ns < 0 || (ns > 0 && !src) || !target_ws || !T_out || !fitness || !rmse)
     return fail(O3DX_EINVAL, "o3dx_icp_register: bad args");
   if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  if (desc_is_f64(desc)) return fail(O3DX_EINVAL, "a float64 ICP target takes a float64 source (o3dx_icp_register_f64)");
   GridView g;
   const float4* tn;
   if (!desc_unpack(desc, target_ws, &g, &tn)) return fail(O3DX_EINVAL, "invalid ICP target descriptor");
@@ -949,6 +1046,103 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
   char* rest = (char*)ws + Arena::align((size_t)std::max<int64_t>(ns, 1) * sizeof(float4) + 1);
   size_t rest_bytes = ws_bytes - (size_t)(rest - (char*)ws);
   if (ns > 0) O3DX_TRY(o3dx_spatial_sort(src, ns, 8.0, src4, rest, rest_bytes, stream));
+  Arena ar(rest, rest_bytes);
+  AccWs w;
+  acc_carve(ar, std::max<int64_t>(ns, 1), &w);
+  return run_loop(src4, ns, true, g, tn, max_corr, init, max_iteration, rel_fit, rel_rmse, nullptr, w, s, T_out,
+                  fitness, rmse, corr_out, ncorr);
+}
+
+// ------------------------------------------------------ float64 boundary
+// point-to-plane ICP on float64 clouds (the float64 boundary, include/o3dx.h):
+// the target grid is a float64 grid (grid64_build: float32 frame p - o for the
+// search, exact coordinates alongside), the source is transformed from its
+// float64 coordinates, and every correspondence distance, residual and
+// Jacobian comes from the float64 values — Open3D's arithmetic on its
+// float64 storage.  Normals stay float32 (the library's normals output).
+extern "C" size_t o3dx_icp_target_f64_workspace_bytes(int64_t nt) {
+  return grid64_ws_bytes(nt, icp_cap_mult()) + 1024;
+}
+
+extern "C" int o3dx_icp_target_build_f64(const double* tgt, const float* tgt_normals, int64_t nt, double max_corr,
+                                         void* target_ws, size_t target_ws_bytes, double* desc, void* stream) {
+  if (nt < 0 || (nt > 0 && (!tgt || !tgt_normals)) || !desc)
+    return fail(O3DX_EINVAL, "o3dx_icp_target_build_f64: bad args");
+  if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  if (!target_ws || target_ws_bytes < o3dx_icp_target_f64_workspace_bytes(nt))
+    return fail(O3DX_ENOMEM, "icp target workspace too small");
+  GridBuild G;
+  O3DX_TRY(grid64_build(tgt, nt, icp_occ(), icp_min_h(max_corr), target_ws, target_ws_bytes, as_stream(stream), &G,
+                        tgt_normals, icp_cap_mult()));
+  desc_pack(G, target_ws, G.extra, desc);
+  return 0;
+}
+
+extern "C" size_t o3dx_spatial_sort_f64_workspace_bytes(int64_t n) { return grid64_ws_bytes(n) + 1024; }
+
+// (n, 4) float64 copy of the cloud in o3dx_spatial_sort's order: (x, y, z,
+// original index)
+extern "C" int o3dx_spatial_sort_f64(const double* xyz, int64_t n, double target_occ, double* sorted4, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  if (n < 0 || (n > 0 && (!xyz || !sorted4))) return fail(O3DX_EINVAL, "o3dx_spatial_sort_f64: bad args");
+  if (!ws || ws_bytes < o3dx_spatial_sort_f64_workspace_bytes(n))
+    return fail(O3DX_ENOMEM, "spatial_sort workspace too small");
+  if (n == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  GridBuild G;
+  O3DX_TRY(grid64_build(xyz, n, target_occ > 0 ? target_occ : 8.0, 0.0, ws, ws_bytes, s, &G, nullptr, 4,
+                        /*blocked=*/true));
+  O3DX_HIP(hipMemcpyAsync(sorted4, G.pts64, (size_t)n * sizeof(double4), hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+extern "C" int o3dx_icp_register_f64(const double* src, int64_t ns, int src_sorted4, const void* target_ws,
+                                     const double* desc, const double* init, int max_iteration, double rel_fit,
+                                     double rel_rmse, double max_corr, const double* src_absmax, double* T_out,
+                                     double* fitness, double* rmse, int32_t* corr_out, int64_t* ncorr, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  if (ns < 0 || (ns > 0 && !src) || !target_ws || !T_out || !fitness || !rmse)
+    return fail(O3DX_EINVAL, "o3dx_icp_register_f64: bad args");
+  if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  if (!desc_is_f64(desc)) return fail(O3DX_EINVAL, "o3dx_icp_register_f64 needs a float64 target (o3dx_icp_target_build_f64)");
+  GridView g;
+  const float4* tn;
+  if (!desc_unpack(desc, target_ws, &g, &tn)) return fail(O3DX_EINVAL, "invalid ICP target descriptor");
+  if (!ws || ws_bytes < o3dx_icp_accumulate_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
+  Arena ar(ws, ws_bytes);
+  AccWs w;
+  acc_carve(ar, std::max<int64_t>(ns, 1), &w);
+  return run_loop(src, ns, src_sorted4 != 0, g, tn, max_corr, init, max_iteration, rel_fit, rel_rmse, src_absmax,
+                  w, as_stream(stream), T_out, fitness, rmse, corr_out, ncorr);
+}
+
+extern "C" size_t o3dx_registration_icp_f64_workspace_bytes(int64_t ns) {
+  ns = std::max<int64_t>(ns, 1);
+  return Arena::align((size_t)ns * sizeof(double4) + 1) +
+         std::max(o3dx_icp_accumulate_workspace_bytes(ns), o3dx_spatial_sort_f64_workspace_bytes(ns)) + 1024;
+}
+
+extern "C" int o3dx_registration_icp_point_to_plane_f64(const double* src, int64_t ns, const double* tgt,
+                                                        const float* tgt_normals, int64_t nt, double max_corr,
+                                                        const double* init, int max_iteration, double rel_fit,
+                                                        double rel_rmse, double* T_out, double* fitness, double* rmse,
+                                                        int32_t* corr_out, int64_t* ncorr, void* target_ws,
+                                                        size_t target_ws_bytes, void* ws, size_t ws_bytes,
+                                                        void* stream) {
+  if (!T_out || !fitness || !rmse) return fail(O3DX_EINVAL, "registration_icp_f64: bad args");
+  if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  if (ns < 0 || (ns > 0 && !src)) return fail(O3DX_EINVAL, "registration_icp_f64: bad args");
+  hipStream_t s = as_stream(stream);
+  double desc[O3DX_ICP_DESC_LEN];
+  O3DX_TRY(o3dx_icp_target_build_f64(tgt, tgt_normals, nt, max_corr, target_ws, target_ws_bytes, desc, stream));
+  GridView g;
+  const float4* tn;
+  desc_unpack(desc, target_ws, &g, &tn);
+  if (!ws || ws_bytes < o3dx_registration_icp_f64_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
+  double* src4 = (double*)ws;
+  char* rest = (char*)ws + Arena::align((size_t)std::max<int64_t>(ns, 1) * sizeof(double4) + 1);
+  size_t rest_bytes = ws_bytes - (size_t)(rest - (char*)ws);
+  if (ns > 0) O3DX_TRY(o3dx_spatial_sort_f64(src, ns, 8.0, src4, rest, rest_bytes, stream));
   Arena ar(rest, rest_bytes);
   AccWs w;
   acc_carve(ar, std::max<int64_t>(ns, 1), &w);

@@ -33,6 +33,19 @@ struct P3 {
   float x, y, z;
 };
 
+// a point's coordinates as float64: a float32 cloud's (exact) or a float64 cloud's own
+__device__ __forceinline__ void load3(const float* xyz, int64_t i, double& x, double& y, double& z) {
+  const P3 q = reinterpret_cast<const P3*>(xyz)[i];
+  x = q.x;
+  y = q.y;
+  z = q.z;
+}
+__device__ __forceinline__ void load3(const double* xyz, int64_t i, double& x, double& y, double& z) {
+  x = xyz[3 * i];
+  y = xyz[3 * i + 1];
+  z = xyz[3 * i + 2];
+}
+
 __device__ __forceinline__ double plane_dist64(const double* pl, double x, double y, double z) {
   // Eigen Vector4d dot packet order: (a*x + c*z) + (b*y + d*1)
   double ax = pl[0] * x, by = pl[1] * y, cz = pl[2] * z, dw = pl[3] * 1.0;
@@ -955,16 +968,17 @@ constexpr int kSumBlocksX = 64;
 // Sigma |d| over the points with |d| < thr, one hypothesis per blockIdx.y, as
 // an exact fx sum (common.hpp; |d| < thr bounds every term): the same bits for
 // any split of the cloud over blocks or ranks.  partial: [y][x] {lo, hi}.
-__global__ void __launch_bounds__(kBlock) k_plane_abs_sum(const float* __restrict__ xyz, int64_t n,
+template <class T>
+__global__ void __launch_bounds__(kBlock) k_plane_abs_sum(const T* __restrict__ xyz, int64_t n,
                                                           const double* __restrict__ pl64, double thr, double scale,
                                                           int64_t* __restrict__ partial) {
   __shared__ int64_t sh[(kBlock / 64) * 2];
   const double* pl = pl64 + 4 * blockIdx.y;
-  const P3* p = reinterpret_cast<const P3*>(xyz);
   int64_t acc[1] = {0};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    P3 q = p[i];
-    double d = plane_dist64(pl, q.x, q.y, q.z);
+    double x, y, z;
+    load3(xyz, i, x, y, z);
+    double d = plane_dist64(pl, x, y, z);
     if (d < thr) acc[0] += fx_term(d, scale);
   }
   block_fx<kBlock, 1>(acc, sh, partial + 2 * ((int64_t)blockIdx.y * gridDim.x + blockIdx.x));
@@ -974,13 +988,14 @@ static int abs_sum_blocks(int64_t n) {
   return (int)std::max<int64_t>(kSumBlocksX, (n + (int64_t)kBlock * kFxLaneTerms - 1) / ((int64_t)kBlock * kFxLaneTerms));
 }
 
-__global__ void __launch_bounds__(kBlock) k_plane_flags(const float* __restrict__ xyz, int64_t n, double a, double b,
+template <class T>
+__global__ void __launch_bounds__(kBlock) k_plane_flags(const T* __restrict__ xyz, int64_t n, double a, double b,
                                                         double c, double d, double thr, uint8_t* __restrict__ flags) {
   const double pl[4] = {a, b, c, d};
-  const P3* p = reinterpret_cast<const P3*>(xyz);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    P3 q = p[i];
-    flags[i] = plane_dist64(pl, q.x, q.y, q.z) < thr ? 1 : 0;
+    double x, y, z;
+    load3(xyz, i, x, y, z);
+    flags[i] = plane_dist64(pl, x, y, z) < thr ? 1 : 0;
   }
 }
 
@@ -1015,7 +1030,8 @@ struct MomScales {
   double s[6];
 };
 
-__global__ void __launch_bounds__(kBlock) k_plane_moments(const float* __restrict__ xyz, const int32_t* __restrict__ idx,
+template <class T>
+__global__ void __launch_bounds__(kBlock) k_plane_moments(const T* __restrict__ xyz, const int32_t* __restrict__ idx,
                                                           int64_t m, double cx, double cy, double cz, int pass2,
                                                           MomScales sc, int64_t* __restrict__ partial) {
   __shared__ int64_t sh[(kBlock / 64) * 12];
@@ -1042,22 +1058,23 @@ __global__ void __launch_bounds__(kBlock) k_plane_moments(const float* __restric
 
 // segment_plane's last step in one read of the cloud: the inlier flags of the
 // best plane and the first moments pass (fx sums of x, y, z over the inliers)
-__global__ void __launch_bounds__(kBlock) k_plane_flags_sum(const float* __restrict__ xyz, int64_t n, double a,
+template <class T>
+__global__ void __launch_bounds__(kBlock) k_plane_flags_sum(const T* __restrict__ xyz, int64_t n, double a,
                                                             double b, double c, double d, double thr, MomScales sc,
                                                             uint8_t* __restrict__ flags,
                                                             int64_t* __restrict__ partial) {
   __shared__ int64_t sh[(kBlock / 64) * 6];
   const double pl[4] = {a, b, c, d};
-  const P3* p = reinterpret_cast<const P3*>(xyz);
   int64_t acc[3] = {0, 0, 0};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const P3 q = p[i];
-    const bool in = plane_dist64(pl, q.x, q.y, q.z) < thr;
+    double x, y, z;
+    load3(xyz, i, x, y, z);
+    const bool in = plane_dist64(pl, x, y, z) < thr;
     flags[i] = in ? 1 : 0;
     if (in) {
-      acc[0] += fx_term((double)q.x, sc.s[0]);
-      acc[1] += fx_term((double)q.y, sc.s[1]);
-      acc[2] += fx_term((double)q.z, sc.s[2]);
+      acc[0] += fx_term(x, sc.s[0]);
+      acc[1] += fx_term(y, sc.s[1]);
+      acc[2] += fx_term(z, sc.s[2]);
     }
   }
   block_fx<kBlock, 3>(acc, sh, partial + (int64_t)blockIdx.x * 6);
@@ -1066,7 +1083,8 @@ __global__ void __launch_bounds__(kBlock) k_plane_flags_sum(const float* __restr
 // Second moments pass with the centroid formed on the device: c = (fx sum of
 // the first pass) / k, the value the host forms (fx_value = fx_to_double);
 // k = *count (the compaction's), the first pass's digit sums in s1 (3 rows).
-__global__ void __launch_bounds__(kBlock) k_plane_moments_c(const float* __restrict__ xyz,
+template <class T>
+__global__ void __launch_bounds__(kBlock) k_plane_moments_c(const T* __restrict__ xyz,
                                                             const int32_t* __restrict__ idx,
                                                             const int64_t* __restrict__ count,
                                                             const int64_t* __restrict__ s1, int q0, int q1, int q2,
@@ -1103,8 +1121,17 @@ static void mom_fx_exps(double A, bool pass2, int q[6]) {
   for (int k = 0; k < 6; ++k) q[k] = pass2 ? fx_exp(4.0 * A * A * 1.01) : (k < 3 ? fx_exp(A) : 0);
 }
 
-__global__ void k_gather_samples(const float* __restrict__ xyz, const int32_t* __restrict__ idx, int64_t m,
-                                 float* __restrict__ out) {
+// The second pass's exponents from the cloud's extent E (largest max - min):
+// the inliers and their centroid lie in the bounding box, so |x - c| <= E
+// (x 1.01 for rounding).  At a georeferenced offset (|x| ~ 5e5, E ~ 50) the
+// |x| bound would coarsen the centred products' quantum by 2^30.
+static void mom_fx_exps_span(double E, int q[6]) {
+  for (int k = 0; k < 6; ++k) q[k] = fx_exp(E * E * 1.03);
+}
+
+template <class T>
+__global__ void k_gather_samples(const T* __restrict__ xyz, const int32_t* __restrict__ idx, int64_t m,
+                                 T* __restrict__ out) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   int64_t i = idx[j];
@@ -1423,18 +1450,28 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
     }
   }
   // through a pinned staging buffer (a direct DMA; a pageable source takes
-  // the runtime's staged, blocking path).  Every caller reads back before it
-  // returns, so the previous upload has landed when the buffer is reused.
+  // the runtime's staged, blocking path).  An event recorded behind each copy
+  // out of it is waited on before the buffer is written again (a caller that
+  // returned early on an error may have left that copy in flight).
   constexpr size_t kPinCap = 1 << 20;
   static thread_local void* pin = nullptr;
+  static thread_local hipEvent_t pin_done = nullptr;
   if (st.size() <= kPinCap && !pin && hipHostMalloc(&pin, kPinCap, hipHostMallocDefault) != hipSuccess) pin = nullptr;
+  if (pin && !pin_done && hipEventCreateWithFlags(&pin_done, hipEventDisableTiming) != hipSuccess) pin_done = nullptr;
   const void* src = st.data();
-  if (pin && st.size() <= kPinCap) {
+  const bool staged = pin && pin_done && st.size() <= kPinCap;
+  if (staged) {
+    if (hipEventSynchronize(pin_done) != hipSuccess) {
+      *rc = fail(O3DX_EIO, "plane upload: staging buffer wait failed");
+      return;
+    }
     std::memcpy(pin, st.data(), st.size());
     src = pin;
   }
   if (hipMemcpyAsync(base, src, st.size(), hipMemcpyHostToDevice, s) != hipSuccess)
     *rc = fail(O3DX_EIO, "plane upload failed");
+  else if (staged && hipEventRecord(pin_done, s) != hipSuccess)
+    *rc = fail(O3DX_EIO, "plane upload: event record failed");
 }
 
 static int absmax_of(const float* xyz, int64_t n, void* aabb_ws, double* mm_dev, hipStream_t s, double out[3]) {
@@ -1682,7 +1719,8 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
 
 // Sigma |d| of the hypotheses `which` (exact fx sums; fx_host: {lo, hi, q, 0}
 // rows, nullable), their float64 values into sums_host.
-static int run_abs_sum(const float* xyz, int64_t n, const double* planes, const int32_t* which, int L, double thr,
+template <class T>
+static int run_abs_sum(const T* xyz, int64_t n, const double* planes, const int32_t* which, int L, double thr,
                        CountWs& w, hipStream_t s, double* sums_host, int64_t* fx_host = nullptr) {
   if (L == 0) return 0;
   std::vector<double> sel((size_t)4 * L);
@@ -1691,7 +1729,7 @@ static int run_abs_sum(const float* xyz, int64_t n, const double* planes, const 
   O3DX_HIP(hipMemcpyAsync(w.pl64, sel.data(), sel.size() * sizeof(double), hipMemcpyHostToDevice, s));
   const int bx = abs_sum_blocks(n);
   const int q = fx_exp(thr);
-  hipLaunchKernelGGL(k_plane_abs_sum, dim3(bx, L), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, fx_scale(q),
+  hipLaunchKernelGGL(k_plane_abs_sum<T>, dim3(bx, L), dim3(kBlock), 0, s, xyz, n, w.pl64, thr, fx_scale(q),
                      w.sum_partial);
   std::vector<int64_t> part((size_t)2 * bx * L);
   O3DX_TRY(read_back(part.data(), w.sum_partial, part.size() * sizeof(int64_t), s));
@@ -1831,7 +1869,7 @@ static int run_moments(const float* xyz, const int32_t* idx, int64_t m, const do
     const int nb = mom_blocks(m);
     MomScales sc;
     for (int k = 0; k < 6; ++k) sc.s[k] = fx_scale(q[k]);
-    hipLaunchKernelGGL(k_plane_moments, dim3(nb), dim3(kBlock), 0, s, xyz, idx, m, centroid ? centroid[0] : 0.0,
+    hipLaunchKernelGGL(k_plane_moments<float>, dim3(nb), dim3(kBlock), 0, s, xyz, idx, m, centroid ? centroid[0] : 0.0,
                        centroid ? centroid[1] : 0.0, centroid ? centroid[2] : 0.0, centroid ? 1 : 0, sc, part);
     O3DX_TRY(reduce_columns_i64(part, nb, 12, out_dev, s));
     O3DX_TRY(read_back(digits, out_dev, sizeof(digits), s));
@@ -1841,6 +1879,49 @@ static int run_moments(const float* xyz, const int32_t* idx, int64_t m, const do
   fx_to_double(fx, K, out);
   if (fx_host) std::memcpy(fx_host, fx, (size_t)4 * K * sizeof(int64_t));
   return 0;
+}
+
+// ------------------------------------------------------ float64 clouds
+// Exact counts on float64 coordinates (the float64 boundary,
+// o3dx_segment_plane_f64): every (point, hypothesis) pair evaluated as
+// Open3D evaluates it on its float64 storage, |(a x + c z) + (b y + d)| < thr
+// (plane_dist64).  A lane holds kC64Pts points; the block's kC64HC planes sit
+// in LDS (broadcast reads); per hypothesis a wave adds the ballot counts of
+// its points into an LDS counter; partial[bx][H] per block, int32.
+constexpr int kC64Pts = 4;
+constexpr int kC64HC = 64;
+constexpr int kC64MaxBlocks = 2048;  // <= CountWs::partial_ints / H rows
+
+__global__ void __launch_bounds__(kBlock) k_plane_count64(const double* __restrict__ xyz, int64_t n,
+                                                          const double* __restrict__ pl64, int H, double thr,
+                                                          int32_t* __restrict__ partial) {
+  __shared__ double pl[kC64HC][4];
+  __shared__ int cnt[kC64HC];
+  const int h0 = blockIdx.y * kC64HC, hc = min(kC64HC, H - h0);
+  for (int t = threadIdx.x; t < kC64HC * 4; t += kBlock) pl[t >> 2][t & 3] = t < hc * 4 ? pl64[4 * (int64_t)h0 + t] : 0.0;
+  for (int t = threadIdx.x; t < kC64HC; t += kBlock) cnt[t] = 0;
+  __syncthreads();
+  const int64_t tile = (int64_t)kBlock * kC64Pts;
+  for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {
+    double X[kC64Pts], Y[kC64Pts], Z[kC64Pts];
+#pragma unroll
+    for (int k = 0; k < kC64Pts; ++k) {
+      const int64_t i = base + threadIdx.x + (int64_t)k * kBlock;
+      if (i < n) {
+        load3(xyz, i, X[k], Y[k], Z[k]);
+      } else {
+        X[k] = Y[k] = Z[k] = __longlong_as_double(0x7ff8000000000000ll);  // NaN: never counted
+      }
+    }
+    for (int h = 0; h < hc; ++h) {
+      int c = 0;
+#pragma unroll
+      for (int k = 0; k < kC64Pts; ++k) c += __popcll(__ballot(plane_dist64(pl[h], X[k], Y[k], Z[k]) < thr));
+      if ((threadIdx.x & 63) == 0 && c) atomicAdd(&cnt[h], c);
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < hc; t += kBlock) partial[(int64_t)blockIdx.x * H + h0 + t] = cnt[t];
 }
 
 struct SegWs {
@@ -2034,7 +2115,7 @@ extern "C" int o3dx_plane_inliers(const float* xyz, int64_t n, const double* pla
   uint8_t* flags = ar.take<uint8_t>(n + 16);
   int32_t* tmp = ar.take<int32_t>(compact_workspace_ints(n));
   int64_t* cnt = ar.take<int64_t>(2);
-  hipLaunchKernelGGL(k_plane_flags, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1],
+  hipLaunchKernelGGL(k_plane_flags<float>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, plane[0], plane[1],
                      plane[2], plane[3], thr, flags);
   O3DX_TRY(compact_flags(flags, n, idx_out, nullptr, cnt, tmp, s));
   O3DX_TRY(read_back(count_host, cnt, sizeof(int64_t), s));
@@ -2178,7 +2259,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     for (int64_t j = 0; j < ns; ++j)
       if (samples_host[j] < 0 || samples_host[j] >= n) return fail(O3DX_EINVAL, "sample index out of range");
     O3DX_HIP(hipMemcpyAsync(w.sidx, samples_host, ns * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_gather_samples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, xyz, w.sidx, ns, w.scoord);
+    hipLaunchKernelGGL(k_gather_samples<float>, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, xyz, w.sidx, ns, w.scoord);
   }
   // |x|,|y|,|z| bounds of the cloud: the count's float32 window and the fx
   // quantum of the refit moments (a sharded driver passes the global ones)
@@ -2211,6 +2292,19 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     std::memcpy(mmh, rb.data() + 40 * (size_t)H, sizeof(mmh));
     for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(mmh[a]), std::fabs(mmh[3 + a]));
     w.cw.exact_counts = false;
+    // run_count_upper's guard on the culled sweep, replayed on the returned
+    // bounds: a threshold tiny against the coordinates leaves the culled
+    // bounds loose (valid, but the replay would then count many hypotheses
+    // exactly); such inputs take the dense sweep instead
+    double smax = 0.0;
+    for (int h = 0; h < H; ++h) {
+      const double* pl = &planes[(size_t)4 * h];
+      const double S = std::fabs(pl[0]) * absmax[0] + std::fabs(pl[1]) * absmax[1] + std::fabs(pl[2]) * absmax[2] +
+                       std::fabs(pl[3]);
+      if (std::isfinite(S)) smax = std::max(smax, S);
+    }
+    if (!(6.0 * std::ldexp(1.0, -24) * smax + std::ldexp(1.0, -20) * thr < 0.5 * thr))
+      O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax, true));
   } else {
     // read back together with the sampled coordinates
     const size_t off_mm = reinterpret_cast<char*>(w.mm) - reinterpret_cast<char*>(w.scoord);
@@ -2280,12 +2374,12 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
       sc2.s[a] = fx_scale(q2[a]);
     }
     const unsigned gf = grid_for(n, kBlock, 8192);
-    hipLaunchKernelGGL(k_plane_flags_sum, dim3(gf), dim3(kBlock), 0, s, xyz, n, bp[0], bp[1], bp[2], bp[3], thr, sc1,
+    hipLaunchKernelGGL(k_plane_flags_sum<float>, dim3(gf), dim3(kBlock), 0, s, xyz, n, bp[0], bp[1], bp[2], bp[3], thr, sc1,
                        w.flags, w.mom_part);
     O3DX_TRY(compact_flags(w.flags, n, inliers_out, nullptr, w.fin, w.scan_tmp, s));
     O3DX_TRY(reduce_columns_i64(w.mom_part, gf, 6, w.fin + 2, s));
     const int nb2 = mom_blocks(n);
-    hipLaunchKernelGGL(k_plane_moments_c, dim3(nb2), dim3(kBlock), 0, s, xyz, inliers_out, w.fin, w.fin + 2, q1[0],
+    hipLaunchKernelGGL(k_plane_moments_c<float>, dim3(nb2), dim3(kBlock), 0, s, xyz, inliers_out, w.fin, w.fin + 2, q1[0],
                        q1[1], q1[2], sc2, w.mom_part2);
     O3DX_TRY(reduce_columns_i64(w.mom_part2, nb2, 12, w.fin + 8, s));
     O3DX_HIP(hipGetLastError());
@@ -2294,6 +2388,149 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
   const int64_t k = fin[0];
   *n_inliers_host = k;
   // GetPlaneFromPoints over the final inliers (zero plane when there are none)
+  if (k == 0) {
+    for (int a = 0; a < 4; ++a) plane_host[a] = 0;
+    return 0;
+  }
+  int64_t fx[24];
+  double s1[6], s2[6], c[3];
+  fx_pack(fin + 2, q1, 3, fx);
+  fx_to_double(fx, 3, s1);
+  for (int a = 0; a < 3; ++a) c[a] = s1[a] / (double)k;
+  fx_pack(fin + 8, q2, 6, fx);
+  fx_to_double(fx, 6, s2);
+  plane_from_centred(c, s2, plane_host);
+  return 0;
+}
+
+// ------------------------------------------------------ float64 boundary
+// segment_plane on float64 coordinates (LAS / E57-style clouds the float32
+// path would round, reference PointCloud.py:75-77 on the float64 storage of
+// :99-102): the hypotheses from the float64 samples (the host's plane math),
+// exact counts of every hypothesis (k_plane_count64; no upper-bound sweep),
+// Open3D's replay (select_best, Sigma|d| for the ties), then the inliers and
+// the GetPlaneFromPoints refit over them as on the float32 path.
+extern "C" size_t o3dx_segment_plane_f64_workspace_bytes(int64_t n, int iters) {
+  return o3dx_segment_plane_workspace_bytes(n, iters) + Arena::align((size_t)std::max(iters, 1) * 16 * 3 * 8 + 64) +
+         Arena::align(aabb64_ws_bytes() + 64) + 1024;
+}
+
+static int count64(const double* xyz, int64_t n, const double* planes, int H, double thr, CountWs& w, hipStream_t s,
+                   std::vector<int64_t>& counts) {
+  counts.assign(H, 0);
+  if (H == 0) return 0;
+  O3DX_HIP(hipMemcpyAsync(w.pl64, planes, (size_t)4 * H * sizeof(double), hipMemcpyHostToDevice, s));
+  const int64_t tiles = (n + (int64_t)kBlock * kC64Pts - 1) / ((int64_t)kBlock * kC64Pts);
+  const int rows = (int)std::max<int64_t>(1, std::min<int64_t>({tiles, (int64_t)kC64MaxBlocks,
+                                                                 (int64_t)(w.partial_ints / (size_t)H)}));
+  KTimer kt("plane_count", s);
+  if (n > 0) {
+    hipLaunchKernelGGL(k_plane_count64, dim3((unsigned)rows, (unsigned)((H + kC64HC - 1) / kC64HC)), dim3(kBlock), 0,
+                       s, xyz, n, w.pl64, H, thr, w.partial);
+    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, rows, H, w.counts, s));
+    O3DX_TRY(read_back(counts.data(), w.counts, (size_t)H * sizeof(int64_t), s));
+  }
+  O3DX_HIP(hipGetLastError());
+  for (int h = 0; h < H; ++h)
+    if (plane_is_zero(planes + 4 * (size_t)h)) counts[h] = -1;
+  return 0;
+}
+
+extern "C" int o3dx_plane_count_f64(const double* xyz, int64_t n, const double* planes, int H, double thr,
+                                    int64_t* counts, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || H < 0 || (n > 0 && !xyz) || (H > 0 && (!planes || !counts)))
+    return fail(O3DX_EINVAL, "o3dx_plane_count_f64: bad arguments");
+  if (!ws || ws_bytes < o3dx_plane_count_workspace_bytes(n, H)) return fail(O3DX_ENOMEM, "plane_count workspace too small");
+  if (H == 0) return 0;
+  Arena ar(ws, ws_bytes);
+  CountWs w;
+  count_carve(ar, n, H, &w);
+  O3DX_ARENA_CHECK(ar);
+  std::vector<int64_t> c;
+  O3DX_TRY(count64(xyz, n, planes, H, thr, w, as_stream(stream), c));
+  std::memcpy(counts, c.data(), (size_t)H * sizeof(int64_t));
+  return 0;
+}
+
+extern "C" int o3dx_segment_plane_f64(const double* xyz, int64_t n, double thr, int ransac_n, int iters,
+                                      double probability, const int32_t* samples_host, double* plane_host,
+                                      int32_t* inliers_out, int64_t* n_inliers_host, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  if (!(probability > 0.0 && probability <= 1.0)) return fail(O3DX_EINVAL, "Probability must be > 0 or <= 1.0");
+  if (ransac_n < 3) return fail(O3DX_EINVAL, "ransac_n should be set to higher than or equal to 3.");
+  if (n < ransac_n) return fail(O3DX_EINVAL, "There must be at least 'ransac_n' points.");
+  if (ransac_n > 16) return fail(O3DX_ENOTSUP, "ransac_n > 16 not supported");
+  if (iters < 0 || !plane_host || !n_inliers_host || !inliers_out || !xyz || (iters > 0 && !samples_host))
+    return fail(O3DX_EINVAL, "o3dx_segment_plane_f64: bad arguments");
+  if (!ws || ws_bytes < o3dx_segment_plane_f64_workspace_bytes(n, iters))
+    return fail(O3DX_ENOMEM, "segment_plane workspace too small");
+  hipStream_t s = as_stream(stream);
+  const int H = iters;
+  Arena ar(ws, ws_bytes);
+  SegWs w;
+  seg_carve(ar, n, std::max(H, 1), 16, &w);
+  const size_t ncoord = (size_t)std::max(H, 1) * ransac_n * 3;
+  double* sc64 = ar.take<double>(ncoord + 8);  // sampled coordinates, then the cloud's {min, max}
+  double* mmd = sc64 + ncoord;
+  char* aws = ar.take<char>(aabb64_ws_bytes() + 64);
+  O3DX_ARENA_CHECK(ar);
+  if (H > 0) {
+    const int64_t ns = (int64_t)H * ransac_n;
+    for (int64_t j = 0; j < ns; ++j)
+      if (samples_host[j] < 0 || samples_host[j] >= n) return fail(O3DX_EINVAL, "sample index out of range");
+    O3DX_HIP(hipMemcpyAsync(w.sidx, samples_host, ns * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_gather_samples<double>, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, xyz, w.sidx, ns,
+                       sc64);
+  }
+  O3DX_TRY(aabb64_device(xyz, n, mmd, aws, s));
+  std::vector<double> rb(ncoord + 6);
+  O3DX_TRY(read_back(rb.data(), sc64, rb.size() * sizeof(double), s));
+  double absmax[3];
+  for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(rb[ncoord + a]), std::fabs(rb[ncoord + 3 + a]));
+  const double A = std::max(absmax[0], std::max(absmax[1], absmax[2]));
+  std::vector<double> planes((size_t)4 * std::max(H, 1), 0.0);
+  for (int h = 0; h < H; ++h) plane_from_pts(&rb[(size_t)h * ransac_n * 3], ransac_n, &planes[(size_t)4 * h]);
+  int best = -1;
+  if (H > 0) {
+    std::vector<int64_t> counts;
+    O3DX_TRY(count64(xyz, n, planes.data(), H, thr, w.cw, s, counts));
+    std::vector<int32_t> tied = tied_hypotheses(counts, planes.data(), n, ransac_n, probability);
+    std::vector<double> sums(H, std::numeric_limits<double>::quiet_NaN());
+    if (!tied.empty()) {
+      std::vector<double> ts(tied.size());
+      O3DX_TRY(run_abs_sum(xyz, n, planes.data(), tied.data(), (int)tied.size(), thr, w.cw, s, ts.data()));
+      for (size_t j = 0; j < tied.size(); ++j) sums[tied[j]] = ts[j];
+    }
+    best = select_best(counts.data(), sums.data(), planes.data(), H, n, ransac_n, probability);
+  }
+  double bp[4] = {0, 0, 0, 0};
+  if (best >= 0) std::memcpy(bp, &planes[(size_t)4 * best], sizeof(bp));
+  int64_t fin[20] = {0};
+  int q1[6], q2[6];
+  mom_fx_exps(A, false, q1);
+  double E = 0.0;
+  for (int a = 0; a < 3; ++a) E = std::max(E, rb[ncoord + 3 + a] - rb[ncoord + a]);
+  mom_fx_exps_span(E, q2);
+  if (!plane_is_zero(bp)) {
+    MomScales sc1, sc2;
+    for (int a = 0; a < 6; ++a) {
+      sc1.s[a] = fx_scale(q1[a]);
+      sc2.s[a] = fx_scale(q2[a]);
+    }
+    const unsigned gf = grid_for(n, kBlock, 8192);
+    hipLaunchKernelGGL(k_plane_flags_sum<double>, dim3(gf), dim3(kBlock), 0, s, xyz, n, bp[0], bp[1], bp[2], bp[3],
+                       thr, sc1, w.flags, w.mom_part);
+    O3DX_TRY(compact_flags(w.flags, n, inliers_out, nullptr, w.fin, w.scan_tmp, s));
+    O3DX_TRY(reduce_columns_i64(w.mom_part, gf, 6, w.fin + 2, s));
+    const int nb2 = mom_blocks(n);
+    hipLaunchKernelGGL(k_plane_moments_c<double>, dim3(nb2), dim3(kBlock), 0, s, xyz, inliers_out, w.fin, w.fin + 2,
+                       q1[0], q1[1], q1[2], sc2, w.mom_part2);
+    O3DX_TRY(reduce_columns_i64(w.mom_part2, nb2, 12, w.fin + 8, s));
+    O3DX_HIP(hipGetLastError());
+    O3DX_TRY(read_back(fin, w.fin, sizeof(fin), s));
+  }
+  const int64_t k = fin[0];
+  *n_inliers_host = k;
   if (k == 0) {
     for (int a = 0; a < 4; ++a) plane_host[a] = 0;
     return 0;

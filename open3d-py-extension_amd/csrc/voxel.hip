@@ -1273,6 +1273,112 @@ extern "C" int o3dx_voxel_down_sample_window(const float* xyz, int64_t n, const 
                     voxel_pts, voxel_pts ? voxel_cells : 0, geom_host, ws, ws_bytes, stream, win);
 }
 
+// ------------------------------------------------------ float64 clouds
+// The float64 boundary (include/o3dx.h): Open3D computes the voxel key of
+// its float64 points, ref = (p - min_bound) / voxel_size, key = int(floor(ref)),
+// octant bit (ref - key) >= 0.5 (PointCloud::VoxelDownSampleAndTrace;
+// reference PointCloud.py:338-341 on float64 storage, :99-102).  The keys
+// kernel evaluates exactly that in float64 and encodes key + 0.25 (octant bit
+// clear) or key + 0.75 (set) as a float32 coordinate — exact for |key| <
+// 2^22 — so the integer pipeline above runs unchanged on (min 0, voxel size
+// 1): floor(key + 0.25 / 0.75) is the key, the fraction the octant bit, and
+// every representative (max index per voxel), trace row and octant id is the
+// float64 computation's.
+constexpr double kKey64Lim = 4194304.0;  // 2^22
+
+__global__ void __launch_bounds__(kBlock) k_voxel_keys64(const double* __restrict__ xyz, int64_t n, double mnx,
+                                                         double mny, double mnz, double vs, float* __restrict__ out,
+                                                         int* __restrict__ err) {
+  const double mn[3] = {mnx, mny, mnz};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double r = (xyz[3 * i + a] - mn[a]) / vs;
+      const double k = floor(r);
+      if (!(fabs(k) < kKey64Lim)) *err = 1;  // NaN too
+      out[3 * i + a] = (float)(k + ((r - k) >= 0.5 ? 0.75 : 0.25));
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_gather_xyz64(const double* __restrict__ xyz, const int32_t* __restrict__ idx,
+                                                         int64_t m, double* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = idx[j];
+    out[3 * j] = xyz[3 * i];
+    out[3 * j + 1] = xyz[3 * i + 1];
+    out[3 * j + 2] = xyz[3 * i + 2];
+  }
+}
+
+extern "C" size_t o3dx_voxel_f64_workspace_bytes(int64_t n) {
+  n = std::max<int64_t>(n, 1);
+  return o3dx_voxel_workspace_bytes(n) + Arena::align((size_t)n * 3 * sizeof(float) + 1) +
+         Arena::align(aabb64_ws_bytes() + 64) + 1024;
+}
+
+extern "C" int o3dx_voxel_down_sample_f64(const double* xyz, int64_t n, const double* min_bound_host,
+                                          const double* max_bound_host, double voxel_size, int32_t* rep_idx,
+                                          double* rep_xyz, int64_t* m_host, int32_t* voxel_of_point,
+                                          int32_t* cubic_id, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || (n > 0 && (!xyz || !rep_idx)) || !m_host)
+    return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_f64: bad arguments");
+  if (!(voxel_size > 0.0)) return fail(O3DX_EINVAL, "voxel_size <= 0.");
+  if (!ws || ws_bytes < o3dx_voxel_f64_workspace_bytes(n))
+    return fail(O3DX_ENOMEM, "o3dx_voxel_down_sample_f64: workspace too small (need %zu)",
+                o3dx_voxel_f64_workspace_bytes(n));
+  hipStream_t s = as_stream(stream);
+  Arena ar(ws, ws_bytes);
+  float* keys = ar.take<float>((size_t)std::max<int64_t>(n, 1) * 3);
+  char* aws = ar.take<char>(aabb64_ws_bytes() + 64);
+  const size_t vbytes = o3dx_voxel_workspace_bytes(n);
+  char* vws = ar.take<char>(vbytes);
+  O3DX_ARENA_CHECK(ar);
+  double mn[3], mx[3];
+  double* mmd = reinterpret_cast<double*>(aws + aabb64_ws_bytes());
+  if (!min_bound_host || !max_bound_host) {
+    double mm[6];
+    O3DX_TRY(aabb64_device(xyz, n, mmd, aws, s));
+    O3DX_TRY(read_back(mm, mmd, sizeof(mm), s));
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = min_bound_host ? min_bound_host[a] : mm[a];
+      mx[a] = max_bound_host ? max_bound_host[a] : mm[3 + a];
+    }
+  } else {
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = min_bound_host[a];
+      mx[a] = max_bound_host[a];
+    }
+  }
+  const double ext = std::max(mx[0] - mn[0], std::max(mx[1] - mn[1], mx[2] - mn[2]));
+  if (voxel_size * (double)INT32_MAX < ext) return fail(O3DX_EINVAL, "voxel_size is too small.");
+  if (n == 0) {
+    *m_host = 0;
+    return 0;
+  }
+  double dims[3];
+  voxel_dims(mn, mx, voxel_size, dims);
+  for (int a = 0; a < 3; ++a)
+    if (!(dims[a] <= kKey64Lim)) return fail(O3DX_ENOTSUP, "voxel grid spans more than 2^22 cells per axis");
+  int* err = reinterpret_cast<int*>(mmd + 6);
+  O3DX_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k_voxel_keys64, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, mn[0], mn[1], mn[2],
+                     voxel_size, keys, err);
+  if (min_bound_host && max_bound_host) {  // points outside caller bounds may leave the exact key range
+    int e = 0;
+    O3DX_TRY(read_back(&e, err, sizeof(int), s));
+    if (e) return fail(O3DX_ENOTSUP, "voxel keys beyond 2^22 cells (points far outside the bounds?)");
+  }
+  const double kmn[3] = {0.0, 0.0, 0.0}, kmx[3] = {dims[0] - 0.5, dims[1] - 0.5, dims[2] - 0.5};
+  O3DX_TRY(voxel_impl(keys, n, kmn, kmx, 1.0, rep_idx, nullptr, m_host, voxel_of_point, cubic_id, nullptr, 0,
+                      nullptr, vws, vbytes, stream));
+  const int64_t m = *m_host;
+  if (rep_xyz && m > 0)
+    hipLaunchKernelGGL(k_gather_xyz64, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, xyz, rep_idx, m, rep_xyz);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
 // ------------------------------------------------------------ table build
 // The voxel table of an arbitrary point set holding at most one point per
 // voxel (a slab's own + halo representatives): vox[v] = (x, y, z, row).

@@ -4,8 +4,14 @@
 Storage: points / normals / colors live on the GPU as float32 (N,3) torch
 tensors (the kernels' input layout); a float64 host copy of the points is kept
 when the caller supplied host data, so get_points() round-trips the caller's
-values exactly, as Open3D's float64 storage does.  intensity / labels /
-row / column indices are plain numpy attributes, as in the reference.
+values exactly, as Open3D's float64 storage does.  A float64 cloud that
+float32 cannot hold (a LAS / E57 scan at a georeferenced offset; the check
+runs once per set_points) also keeps a float64 device copy, and the hot-path
+methods run the float64 kernels on it (ops / include/o3dx.h "float64
+boundary"): voxel keys, kNN distances, normals' moments, RANSAC distances and
+ICP are then computed from the float64 values, as Open3D computes them.
+intensity / labels / row / column indices are plain numpy attributes, as in
+the reference.
 
 The hot-path methods call libo3dx.so (ops.py); there is no CPU fallback —
 without an MI355X they raise RuntimeError.  Host-only helpers (selections by
@@ -67,6 +73,16 @@ def _as_np(a) -> np.ndarray:
     return np.asarray(a)
 
 
+def _f32_exact(a) -> bool:
+    """Every value of the float64 array / tensor is a float32 value (NaN
+    included): the float32 kernels then see exactly Open3D's float64 inputs."""
+    if isinstance(a, torch.Tensor):
+        t = a.detach()
+        return bool(((t.float().double() == t) | torch.isnan(t)).all().item())
+    with np.errstate(over="ignore", invalid="ignore"):
+        return bool(np.array_equal(a.astype(np.float32).astype(np.float64), a, equal_nan=True))
+
+
 def _check3(a, what):
     if a.ndim != 2 or a.shape[1] != 3:
         raise AssertionError(f"{what} shape must be (n,3)")
@@ -91,10 +107,10 @@ class KDTreeGrid:
     the same search_* methods and return shapes, backed by the GPU grid search."""
 
     def __init__(self, cloud: "PointCloudBase"):
-        self._x = cloud._dev_points()
+        self._x = cloud._hot_points()
 
     def _one(self, query, mode, knn, radius):
-        q = torch.as_tensor(np.asarray(query, np.float32).reshape(1, 3), device=self._x.device)
+        q = torch.as_tensor(np.asarray(query, np.float64).reshape(1, 3), dtype=self._x.dtype, device=self._x.device)
         idx, d2, cnt = ops.knn_search(self._x, q, mode=mode, knn=knn, radius=radius)
         k = int(cnt[0].item())
         return k, idx[0, :k].cpu().numpy().astype(np.int64), d2[0, :k].cpu().numpy()
@@ -117,7 +133,7 @@ class KDTreeGrid:
         # O3DX_MAX_KNN; answer with the exact kNN of the whole cloud instead
         x = self._x
         k = x.shape[0] if knn is None else min(int(knn), x.shape[0])
-        q = torch.as_tensor(np.asarray(query, np.float32).reshape(1, 3), device=x.device)
+        q = torch.as_tensor(np.asarray(query, np.float64).reshape(1, 3), dtype=x.dtype, device=x.device)
         d = x.double() - q.double()
         d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
         order = torch.argsort(d2, stable=True)[:k]
@@ -142,6 +158,7 @@ class PointCloudBase:
         self._pts = None        # (N,3) float32 tensor on the device
         self._pts_host = None   # (N,3) float64 exact host copy (when supplied from host)
         self._pts64 = None      # device float64 copy of _pts_host (plane selections), made on demand
+        self._wide = False      # the float64 values are not float32-representable: hot path in float64
         self._normals = None    # (N,3) float32 tensor
         self._colors = None     # (N,3) float32 tensor in [0,1]
         self.pcd_tree = None
@@ -185,6 +202,7 @@ class PointCloudBase:
         self._pts = other._pts
         self._pts_host = other._pts_host
         self._pts64 = other._pts64
+        self._wide = other._wide
         self._normals = other._normals
         self._colors = other._colors
         self.intensity = other.intensity
@@ -202,14 +220,22 @@ class PointCloudBase:
 
     def _plane_points(self) -> torch.Tensor:
         """The coordinates the plane selections evaluate: the caller's exact
-        float64 values when the cloud came from float64 host data (the
-        reference computes distance2plane on get_points(), float64:
-        PointCloud.py:400-404), else the float32 device points."""
-        if self._pts_host is None:
+        float64 values when the cloud came from float64 data (the reference
+        computes distance2plane on get_points(), float64: PointCloud.py:
+        400-404), else the float32 device points."""
+        if self._pts_host is None and self._pts64 is None:
             return self._dev_points()
         if self._pts64 is None or self._pts64.device.type != "cuda":
-            self._pts64 = torch.as_tensor(self._pts_host, dtype=torch.float64, device=N.default_device())
+            src = self._pts_host if self._pts_host is not None else self._pts64
+            self._pts64 = torch.as_tensor(src, dtype=torch.float64, device=N.default_device())
         return self._pts64
+
+    def _hot_points(self) -> torch.Tensor:
+        """The hot-path kernels' input: the float64 device copy when float32
+        cannot hold the cloud's values (the o3dx_*_f64 entry points, Open3D's
+        float64 arithmetic), else the float32 device points (identical
+        inputs: every float64 value is a float32 value)."""
+        return self._plane_points() if self._wide else self._dev_points()
 
     @staticmethod
     def _to_dev(a, dtype=torch.float32) -> torch.Tensor:
@@ -247,6 +273,11 @@ class PointCloudBase:
                 h = self._pts_host @ T[:3, :3].T + T[:3, 3]  # set_points drops _pts64
                 w = self._pts_host @ T[3, :3] + T[3, 3]
                 self.set_points(h / w[:, None])
+            elif self._pts64 is not None:
+                Tt = torch.as_tensor(T, dtype=torch.float64, device=self._pts64.device)
+                h = self._pts64 @ Tt[:3, :3].T + Tt[:3, 3]
+                w = self._pts64 @ Tt[3, :3] + Tt[3, 3]
+                self.set_points(h / w[:, None])
             else:
                 Tt = torch.as_tensor(T, dtype=torch.float64, device=self._pts.device)
                 p = self._pts.double()
@@ -282,10 +313,10 @@ class PointCloudBase:
         if method == "poisson":
             raise NotImplementedError("orient_normals_consistent_tangent_plane is outside the GPU hot path")
         mode, knn, radius = resolve(param)
-        x = self._dev_points()
+        x = self._hot_points()
         prior = self._normals if self.has_normals() else None
         self._normals = ops.estimate_normals(x, mode=mode, knn=knn, radius=radius, prior=prior,
-                                             voxel_grid=self._kept_voxel_grid(x))
+                                             voxel_grid=None if self._wide else self._kept_voxel_grid(x))
         return self
 
     def _kept_voxel_grid(self, x):
@@ -309,7 +340,7 @@ class PointCloudBase:
     def _segment_plane_dev(self, thickness=0.01, ransac_n=3, num_iterations=450, probability=0.99999999, seed=None,
                            samples=None):
         """segment_plane with the inlier indices left on the device (int32)."""
-        x = self._dev_points()
+        x = self._hot_points()
         n = x.shape[0]
         if samples is None and n >= ransac_n >= 3 and 0 < probability <= 1:
             samples = ops.ransac_samples(n, ransac_n, num_iterations, _next_seed() if seed is None else seed)
@@ -321,7 +352,7 @@ class PointCloudBase:
             return np.zeros(3), np.zeros(3)
         if self._pts_host is not None and not torch.cuda.is_available():
             raise RuntimeError("get_aabb needs the ROCm GPU (no CPU path)")
-        return ops.aabb(self._dev_points())
+        return ops.aabb(self._hot_points())
 
     # ---------------------------------------------------------------- has
     def has_rgb(self) -> bool:
@@ -349,14 +380,18 @@ class PointCloudBase:
     def set_points(self, points):
         if isinstance(points, torch.Tensor):
             _check3(points, "points")
-            self._pts = self._to_dev(points)
             self._pts_host = None
             self._pts64 = None
+            self._wide = points.dtype == torch.float64 and not _f32_exact(points)
+            if self._wide:  # kept in float64 on the device (get_points returns it)
+                self._pts64 = self._to_dev(points, torch.float64)
+            self._pts = self._to_dev(points)
         else:
             p = np.asarray(points)
             _check3(p, "points")
             self._pts_host = np.ascontiguousarray(p, dtype=np.float64)
             self._pts64 = None
+            self._wide = not _f32_exact(self._pts_host)
             self._pts = self._to_dev(self._pts_host.astype(np.float32))
         self.pcd_tree = None
         return self
@@ -380,6 +415,8 @@ class PointCloudBase:
     def get_points(self) -> np.ndarray:
         if self._pts_host is not None:
             return self._pts_host.copy()
+        if self._pts64 is not None:
+            return self._pts64.detach().cpu().numpy().copy()
         if self._pts is None:
             return np.zeros((0, 3))
         return self._pts.detach().cpu().numpy().astype(np.float64)
@@ -491,8 +528,11 @@ class PointCloudSelections(PointCloudBase):
         sel = torch.nonzero(mask).reshape(-1)
         if self.has_points():
             res._pts = self._pts.index_select(0, sel).contiguous()
+            res._wide = self._wide
             if self._pts_host is not None:
                 res._pts_host = self._pts_host[sel.cpu().numpy()]
+            elif self._pts64 is not None:
+                res._pts64 = self._pts64.index_select(0, sel.to(self._pts64.device)).contiguous()
         if self.has_rgb():
             res._colors = self._colors.index_select(0, sel.to(self._colors.device)).contiguous()
         if self.has_normals():
@@ -615,7 +655,7 @@ class PointCloudUtility(PointCloudSelections):
         idxmat (M,8) int32 cubic-id matrix, vec: list of M int arrays).  Row r
         of idxmat / vec is the voxel of representative r; Open3D emits rows in
         its hash-map order instead, which no implementation can reproduce."""
-        x = self._dev_points()
+        x = self._hot_points()
         mn, mx = self.get_aabb()
         out = ops.voxel_down_sample(x, voxel_size, mn, mx, with_xyz=False, trace=True)
         rep = out["rep_idx"]
@@ -629,7 +669,7 @@ class PointCloudUtility(PointCloudSelections):
 
     def voxel_down_sample(self, voxel_size: float):
         """Representatives only (no trace) — the fast path."""
-        x = self._dev_points()
+        x = self._hot_points()
         mn, mx = self.get_aabb()
         out = ops.voxel_down_sample(x, voxel_size, mn, mx, with_xyz=False, keep_grid=True)
         res = self._select_by_idx(out["rep_idx"])
@@ -674,7 +714,7 @@ class PointCloudUtility(PointCloudSelections):
                                "ratio must be positive.")
         if not self.has_points():
             return self.__class__(), []
-        x = self._dev_points()
+        x = self._hot_points()
         idx, d2, cnt = ops.knn_search(x, x, mode=N.SEARCH_KNN, knn=nb_neighbors)
         n = x.shape[0]
         col = torch.arange(d2.shape[1], device=d2.device)
@@ -853,7 +893,10 @@ class PointCloud(PointCloudUtility):
                                "require pre-computed normal vectors for target PointCloud.")
         if max_correspondence_distance <= 0.0:
             raise RuntimeError("Invalid max_correspondence_distance.")
-        r = ops.registration_icp(self._dev_points(), target._dev_points(), target._normals,
+        wide = self._wide or target._wide
+        src = self._plane_points() if wide else self._dev_points()
+        tgt = target._plane_points() if wide else target._dev_points()
+        r = ops.registration_icp(src, tgt, target._normals,
                                  max_correspondence_distance, init, max_iteration, relative_fitness, relative_rmse)
         return RegistrationResult(r["transformation"], r["fitness"], r["inlier_rmse"],
                                   r["correspondence_set"].cpu().numpy().astype(np.int64))

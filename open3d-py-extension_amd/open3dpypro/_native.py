@@ -20,7 +20,7 @@ HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "
 SEARCH_KNN, SEARCH_RADIUS, SEARCH_HYBRID = 0, 1, 2
 MAX_KNN = 64
 ICP_NSUMS = 32
-ICP_DESC_LEN = 16  # include/o3dx.h O3DX_ICP_DESC_LEN
+ICP_DESC_LEN = 24  # include/o3dx.h O3DX_ICP_DESC_LEN
 PCD_TYPES = {("F", 4): 1, ("F", 8): 2, ("U", 1): 3, ("U", 2): 4, ("U", 4): 5, ("I", 1): 6, ("I", 2): 7,
              ("I", 4): 8}
 PCD_RGB = 9
@@ -99,6 +99,27 @@ _SIGS = {
                                  _P]),
     "o3dx_registration_icp_point_to_plane": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,
                                                      _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    # the float64 boundary (ABI 5)
+    "o3dx_aabb_f64_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_aabb_f64": (_I32, [_P, _I64, _P, _P, _SZ, _P]),
+    "o3dx_voxel_f64_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_voxel_down_sample_f64": (_I32, [_P, _I64, _P, _P, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_normals_f64_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_estimate_normals_f64": (_I32, [_P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_knn_f64_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_knn_search_f64": (_I32, [_P, _I64, _P, _I64, _I32, _I32, _D, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_plane_count_f64": (_I32, [_P, _I64, _P, _I32, _D, _P, _P, _SZ, _P]),
+    "o3dx_segment_plane_f64_workspace_bytes": (_SZ, [_I64, _I32]),
+    "o3dx_segment_plane_f64": (_I32, [_P, _I64, _D, _I32, _I32, _D, _P, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_icp_target_f64_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_icp_target_build_f64": (_I32, [_P, _P, _I64, _D, _P, _SZ, _P, _P]),
+    "o3dx_spatial_sort_f64_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_spatial_sort_f64": (_I32, [_P, _I64, _D, _P, _P, _SZ, _P]),
+    "o3dx_icp_register_f64": (_I32, [_P, _I64, _I32, _P, _P, _P, _I32, _D, _D, _D, _P, _P, _P, _P, _P, _P, _P,
+                                     _SZ, _P]),
+    "o3dx_registration_icp_f64_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_registration_icp_point_to_plane_f64": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,
+                                                         _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
 }
 
 _lib = None

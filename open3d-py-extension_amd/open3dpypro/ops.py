@@ -1,7 +1,10 @@
 """Tensor-level hot-path ops: torch-ROCm tensors in, torch tensors out.
 
 Each op is a thin call into libo3dx.so (include/o3dx.h); the tensor is only
-the device array container.  Inputs: (N,3) float32 contiguous on a ROCm GPU.
+the device array container.  Inputs: (N,3) contiguous on a ROCm GPU — float32,
+or float64 for the float64 boundary (o3dx_*_f64: the hot-path ops computed on
+the caller's float64 values, as Open3D computes them on its float64 storage).
+PointCloud passes float64 only for clouds float32 cannot hold.
 """
 from __future__ import annotations
 
@@ -23,6 +26,17 @@ def _xyz(t: torch.Tensor, what="points") -> torch.Tensor:
     return t.contiguous()
 
 
+def _is64(t) -> bool:
+    return isinstance(t, torch.Tensor) and t.dtype == torch.float64
+
+
+def _xyz64(t: torch.Tensor, what="points") -> torch.Tensor:
+    N.require_device(t, what)
+    if t.ndim != 2 or t.shape[1] != 3:
+        raise RuntimeError(f"{what} must have shape (n, 3), got {tuple(t.shape)}")
+    return t.to(torch.float64).contiguous()
+
+
 def _c(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)
 
@@ -33,8 +47,15 @@ def _np_ptr(a):
 
 def aabb(xyz: torch.Tensor):
     """(min_bound, max_bound) as float64 numpy — get_min_bound/get_max_bound."""
-    x = _xyz(xyz)
     L = N.load()
+    if _is64(xyz):
+        x = _xyz64(xyz)
+        n = x.shape[0]
+        ws = N.workspace(L.o3dx_aabb_f64_workspace_bytes(n), x.device, "aabb")
+        out = np.zeros(6, np.float64)
+        N.check(L.o3dx_aabb_f64(N.ptr(x), n, _np_ptr(out), N.ptr(ws), ws.numel(), N.stream_ptr(x.device)), "aabb")
+        return out[:3].copy(), out[3:].copy()
+    x = _xyz(xyz)
     n = x.shape[0]
     ws = N.workspace(L.o3dx_aabb_workspace_bytes(n), x.device)
     out = np.zeros(6, np.float64)
@@ -62,7 +83,10 @@ def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_
     voxel_of_point (N,) int32 and cubic_id (M,8) int32 (if trace);
     voxel_grid (if keep_grid): the voxel table for estimate_normals(...,
     voxel_grid=) on the representatives' points (rep_xyz), or None when the
-    grid was too sparse to keep."""
+    grid was too sparse to keep.  float64 points: o3dx_voxel_down_sample_f64
+    (keys from the float64 coordinates; rep_xyz float64; no voxel table)."""
+    if _is64(xyz):
+        return _voxel_down_sample_f64(xyz, voxel_size, min_bound, max_bound, with_xyz, trace, keep_grid)
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
@@ -101,6 +125,34 @@ def voxel_down_sample(xyz: torch.Tensor, voxel_size: float, min_bound=None, max_
         out["cubic_id"] = cub[: 8 * M].view(M, 8)
     if keep_grid:
         out["voxel_grid"] = VoxelGrid(geom, vox, M) if geom[7] == 1.0 else None
+    return out
+
+
+def _voxel_down_sample_f64(xyz, voxel_size, min_bound, max_bound, with_xyz, trace, keep_grid):
+    x = _xyz64(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    ws = N.workspace(L.o3dx_voxel_f64_workspace_bytes(n), dev)
+    rep = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    rxyz = torch.empty((max(n, 1), 3), dtype=torch.float64, device=dev) if with_xyz else None
+    vop = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if trace else None
+    cub = torch.empty(max(8 * n, 8), dtype=torch.int32, device=dev) if trace else None
+    mnb = None if min_bound is None else _c(min_bound, np.float64)
+    mxb = None if max_bound is None else _c(max_bound, np.float64)
+    m = np.zeros(1, np.int64)
+    N.check(L.o3dx_voxel_down_sample_f64(N.ptr(x), n, _np_ptr(mnb), _np_ptr(mxb), float(voxel_size), N.ptr(rep),
+                                         N.ptr(rxyz), _np_ptr(m), N.ptr(vop), N.ptr(cub), N.ptr(ws), ws.numel(),
+                                         N.stream_ptr(dev)), "voxel_down_sample")
+    M = int(m[0])
+    out = {"rep_idx": rep[:M]}
+    if with_xyz:
+        out["rep_xyz"] = rxyz[:M]
+    if trace:
+        out["voxel_of_point"] = vop[:n]
+        out["cubic_id"] = cub[: 8 * M].view(M, 8)
+    if keep_grid:
+        out["voxel_grid"] = None
     return out
 
 
@@ -215,7 +267,11 @@ def estimate_normals(xyz: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30,
     voxel_grid: the VoxelGrid of the voxel_down_sample that produced `xyz`
     (its rep_xyz); the search grid is then read off the voxel table.
     return_kdist (KNN only): also return (N,) float32 upper bounds of each
-    point's squared k-th-neighbour distance (for halo checks of sharded runs)."""
+    point's squared k-th-neighbour distance (for halo checks of sharded runs).
+    float64 points: o3dx_estimate_normals_f64 (sets and moments from the
+    float64 coordinates; voxel_grid is not used)."""
+    if _is64(xyz):
+        return _estimate_normals_f64(xyz, mode, knn, radius, prior, return_kdist)
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
@@ -241,9 +297,42 @@ def estimate_normals(xyz: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30,
     return out[:n]
 
 
+def _estimate_normals_f64(xyz, mode, knn, radius, prior, return_kdist):
+    x = _xyz64(xyz)
+    L = N.load()
+    n = x.shape[0]
+    dev = x.device
+    if return_kdist and mode != N.SEARCH_KNN:
+        raise ValueError("return_kdist needs KNN search")
+    out = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev)
+    kd2 = torch.empty(max(n, 1), dtype=torch.float32, device=dev) if return_kdist else None
+    pr = None if prior is None else _xyz(prior.to(dev), "prior normals")
+    ws = N.workspace(L.o3dx_normals_f64_workspace_bytes(n), dev)
+    N.check(L.o3dx_estimate_normals_f64(N.ptr(x), n, int(mode), int(knn), float(radius), N.ptr(pr), N.ptr(out),
+                                        N.ptr(kd2), N.ptr(ws), ws.numel(), N.stream_ptr(dev)), "estimate_normals")
+    if return_kdist:
+        return out[:n], kd2[:n]
+    return out[:n]
+
+
 def knn_search(xyz: torch.Tensor, queries: torch.Tensor, mode: int = N.SEARCH_KNN, knn: int = 30,
                radius: float = 0.0):
-    """Batched KDTreeFlann search: (idx (nq,K) int32, d2 (nq,K) float64, count (nq,) int32)."""
+    """Batched KDTreeFlann search: (idx (nq,K) int32, d2 (nq,K) float64, count (nq,) int32).
+    float64 points: o3dx_knn_search_f64 (queries taken as float64)."""
+    if _is64(xyz):
+        x = _xyz64(xyz)
+        q = _xyz64(queries.to(x.device), "queries")
+        L = N.load()
+        n, nq = x.shape[0], q.shape[0]
+        dev = x.device
+        K = int(knn)
+        idx = torch.empty((max(nq, 1), K), dtype=torch.int32, device=dev)
+        d2 = torch.empty((max(nq, 1), K), dtype=torch.float64, device=dev)
+        cnt = torch.empty(max(nq, 1), dtype=torch.int32, device=dev)
+        ws = N.workspace(L.o3dx_knn_f64_workspace_bytes(n), dev)
+        N.check(L.o3dx_knn_search_f64(N.ptr(x), n, N.ptr(q), nq, int(mode), K, float(radius), N.ptr(idx), N.ptr(d2),
+                                      N.ptr(cnt), N.ptr(ws), ws.numel(), N.stream_ptr(dev)), "knn_search")
+        return idx[:nq], d2[:nq], cnt[:nq]
     x = _xyz(xyz)
     q = _xyz(queries.to(x.device), "queries")
     L = N.load()
@@ -270,8 +359,10 @@ def ransac_samples(n: int, ransac_n: int, num_iterations: int, seed: int) -> np.
 
 def segment_plane(xyz: torch.Tensor, distance_threshold: float, ransac_n: int, num_iterations: int,
                   probability: float = 0.99999999, samples: Optional[np.ndarray] = None, seed: int = 0):
-    """Open3D SegmentPlane -> (plane float64[4], inliers (k,) int32 ascending on device)."""
-    x = _xyz(xyz)
+    """Open3D SegmentPlane -> (plane float64[4], inliers (k,) int32 ascending on device).
+    float64 points: o3dx_segment_plane_f64 (exact counts on the float64 coordinates)."""
+    f64 = _is64(xyz)
+    x = _xyz64(xyz) if f64 else _xyz(xyz)
     L = N.load()
     n = x.shape[0]
     dev = x.device
@@ -287,24 +378,28 @@ def segment_plane(xyz: torch.Tensor, distance_threshold: float, ransac_n: int, n
     plane = np.zeros(4, np.float64)
     inl = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     k = np.zeros(1, np.int64)
-    ws = N.workspace(L.o3dx_segment_plane_workspace_bytes(n, num_iterations), dev)
-    rc = L.o3dx_segment_plane(N.ptr(x), n, float(distance_threshold), int(ransac_n), int(num_iterations),
-                              float(probability), _np_ptr(s), _np_ptr(plane), N.ptr(inl), _np_ptr(k), N.ptr(ws),
-                              ws.numel(), N.stream_ptr(dev))
+    wsb = (L.o3dx_segment_plane_f64_workspace_bytes if f64 else L.o3dx_segment_plane_workspace_bytes)
+    ws = N.workspace(wsb(n, num_iterations), dev)
+    fn = L.o3dx_segment_plane_f64 if f64 else L.o3dx_segment_plane
+    rc = fn(N.ptr(x), n, float(distance_threshold), int(ransac_n), int(num_iterations), float(probability),
+            _np_ptr(s), _np_ptr(plane), N.ptr(inl), _np_ptr(k), N.ptr(ws), ws.numel(), N.stream_ptr(dev))
     N.check(rc, "segment_plane")
     return plane, inl[: int(k[0])]
 
 
 def plane_count(xyz: torch.Tensor, planes: np.ndarray, distance_threshold: float) -> np.ndarray:
-    """Exact per-hypothesis inlier counts (-1 for degenerate planes)."""
-    x = _xyz(xyz)
+    """Exact per-hypothesis inlier counts (-1 for degenerate planes); float64
+    points: o3dx_plane_count_f64."""
+    f64 = _is64(xyz)
+    x = _xyz64(xyz) if f64 else _xyz(xyz)
     L = N.load()
     n = x.shape[0]
     P = _c(planes, np.float64).reshape(-1, 4)
     H = P.shape[0]
     counts = np.zeros(max(H, 1), np.int64)
     ws = N.workspace(L.o3dx_plane_count_workspace_bytes(n, H), x.device)
-    N.check(L.o3dx_plane_count(N.ptr(x), n, _np_ptr(P), H, float(distance_threshold), _np_ptr(counts), N.ptr(ws),
+    fn = L.o3dx_plane_count_f64 if f64 else L.o3dx_plane_count
+    N.check(fn(N.ptr(x), n, _np_ptr(P), H, float(distance_threshold), _np_ptr(counts), N.ptr(ws),
                                ws.numel(), N.stream_ptr(x.device)), "plane_count")
     return counts[:H]
 
@@ -498,18 +593,21 @@ class ICPTarget:
     """Persistent target structure (grid of target points + normals) for ICP."""
 
     def __init__(self, tgt: torch.Tensor, tgt_normals: torch.Tensor, max_correspondence_distance: float):
-        self.xyz = _xyz(tgt, "target points")
+        # float64 targets: a float64 grid (o3dx_icp_target_build_f64), float64 sources
+        self.f64 = _is64(tgt)
+        self.xyz = _xyz64(tgt, "target points") if self.f64 else _xyz(tgt, "target points")
         self.normals = _xyz(tgt_normals.to(self.xyz.device), "target normals")
         if self.normals.shape[0] != self.xyz.shape[0]:
             raise RuntimeError("target normals must match target points")
         L = N.load()
         nt = self.xyz.shape[0]
         self.max_corr = float(max_correspondence_distance)
-        self.ws = torch.empty(L.o3dx_icp_target_workspace_bytes(nt), dtype=torch.uint8, device=self.xyz.device)
+        wsb = L.o3dx_icp_target_f64_workspace_bytes if self.f64 else L.o3dx_icp_target_workspace_bytes
+        build = L.o3dx_icp_target_build_f64 if self.f64 else L.o3dx_icp_target_build
+        self.ws = torch.empty(wsb(nt), dtype=torch.uint8, device=self.xyz.device)
         self.desc = np.zeros(N.ICP_DESC_LEN, np.float64)
-        N.check(L.o3dx_icp_target_build(N.ptr(self.xyz), N.ptr(self.normals), nt, self.max_corr, N.ptr(self.ws),
-                                        self.ws.numel(), _np_ptr(self.desc), N.stream_ptr(self.xyz.device)),
-                "icp_target_build")
+        N.check(build(N.ptr(self.xyz), N.ptr(self.normals), nt, self.max_corr, N.ptr(self.ws), self.ws.numel(),
+                      _np_ptr(self.desc), N.stream_ptr(self.xyz.device)), "icp_target_build")
 
     def accumulate(self, src: torch.Tensor, T: np.ndarray, want_corr: bool = False, absmax=None,
                    return_fx: bool = False):
@@ -518,6 +616,8 @@ class ICPTarget:
         or the (n,4) output of spatial_sort (faster).  absmax: |x|,|y|,|z|
         bounds of the WHOLE source (a sharded source passes the global ones);
         default: spatial_sort's record of them, else the library measures src."""
+        if self.f64:
+            raise RuntimeError("ICPTarget.accumulate: float64 targets run the device loop (register)")
         sorted4 = src.ndim == 2 and src.shape[1] == 4
         if sorted4:
             N.require_device(src, "source points")
@@ -556,7 +656,9 @@ class ICPTarget:
         sorted4 = src.ndim == 2 and src.shape[1] == 4
         if sorted4:
             N.require_device(src, "source points")
-            s = src.float().contiguous()
+            s = (src.double() if self.f64 else src.float()).contiguous()
+        elif self.f64:
+            s = _xyz64(src.to(self.xyz.device), "source points")
         else:
             s = _xyz(src.to(self.xyz.device), "source points")
         if absmax is None:
@@ -570,14 +672,29 @@ class ICPTarget:
         corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if want_corr else None
         nc = np.zeros(1, np.int64)
         ws = N.workspace(L.o3dx_icp_accumulate_workspace_bytes(ns), s.device, "icp_acc")
-        N.check(L.o3dx_icp_register(N.ptr(s), ns, 1 if sorted4 else 0, N.ptr(self.ws), _np_ptr(self.desc),
-                                    _np_ptr(T0), int(max_iteration), float(relative_fitness), float(relative_rmse),
-                                    self.max_corr, _np_ptr(am), _np_ptr(T), _np_ptr(fit), _np_ptr(rm), N.ptr(corr),
-                                    _np_ptr(nc), N.ptr(ws), ws.numel(), N.stream_ptr(s.device)), "icp_register")
+        reg = L.o3dx_icp_register_f64 if self.f64 else L.o3dx_icp_register
+        N.check(reg(N.ptr(s), ns, 1 if sorted4 else 0, N.ptr(self.ws), _np_ptr(self.desc), _np_ptr(T0),
+                    int(max_iteration), float(relative_fitness), float(relative_rmse), self.max_corr, _np_ptr(am),
+                    _np_ptr(T), _np_ptr(fit), _np_ptr(rm), N.ptr(corr), _np_ptr(nc), N.ptr(ws), ws.numel(),
+                    N.stream_ptr(s.device)), "icp_register")
         out = {"transformation": T, "fitness": float(fit[0]), "inlier_rmse": float(rm[0])}
         if want_corr:
             out["correspondence_set"] = corr[: int(nc[0])]
         return out
+
+
+def spatial_sort_f64(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
+    """(n,4) float64 form of spatial_sort for float64 sources (x, y, z,
+    original index), o3dx_spatial_sort_f64: ICPTarget.register's fast input
+    on a float64 target."""
+    x = _xyz64(xyz)
+    L = N.load()
+    n = x.shape[0]
+    out = torch.empty((max(n, 1), 4), dtype=torch.float64, device=x.device)
+    ws = N.workspace(L.o3dx_spatial_sort_f64_workspace_bytes(n), x.device, "sort")
+    N.check(L.o3dx_spatial_sort_f64(N.ptr(x), n, float(target_occ), N.ptr(out), N.ptr(ws), ws.numel(),
+                                    N.stream_ptr(x.device)), "spatial_sort_f64")
+    return out[:n]
 
 
 def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
@@ -619,9 +736,12 @@ def icp_solve(sums) -> np.ndarray:
 def registration_icp(src: torch.Tensor, tgt: torch.Tensor, tgt_normals: torch.Tensor,
                      max_correspondence_distance: float, init=None, max_iteration: int = 30,
                      relative_fitness: float = 1e-6, relative_rmse: float = 1e-6, return_corr: bool = True):
-    """Open3D registration_icp + TransformationEstimationPointToPlane on one device."""
-    s = _xyz(src, "source points")
-    t = _xyz(tgt.to(s.device), "target points")
+    """Open3D registration_icp + TransformationEstimationPointToPlane on one device.
+    A float64 source or target: both in float64 (o3dx_registration_icp_point_to_plane_f64)."""
+    f64 = _is64(src) or _is64(tgt)
+    cv = _xyz64 if f64 else _xyz
+    s = cv(src, "source points")
+    t = cv(tgt.to(s.device), "target points")
     tn = _xyz(tgt_normals.to(s.device), "target normals")
     L = N.load()
     ns, nt = s.shape[0], t.shape[0]
@@ -632,13 +752,15 @@ def registration_icp(src: torch.Tensor, tgt: torch.Tensor, tgt_normals: torch.Te
     rm = np.zeros(1)
     corr = torch.empty((max(ns, 1), 2), dtype=torch.int32, device=s.device) if return_corr else None
     nc = np.zeros(1, np.int64)
-    tws = N.workspace(L.o3dx_icp_target_workspace_bytes(nt), s.device, "icp_target")
-    ws = N.workspace(L.o3dx_registration_icp_workspace_bytes(ns), s.device, "icp")
-    rc = L.o3dx_registration_icp_point_to_plane(N.ptr(s), ns, N.ptr(t), N.ptr(tn), nt,
-                                                float(max_correspondence_distance), _np_ptr(T0), int(max_iteration),
-                                                float(relative_fitness), float(relative_rmse), _np_ptr(T),
-                                                _np_ptr(fit), _np_ptr(rm), N.ptr(corr), _np_ptr(nc), N.ptr(tws),
-                                                tws.numel(), N.ptr(ws), ws.numel(), N.stream_ptr(s.device))
+    tws = N.workspace((L.o3dx_icp_target_f64_workspace_bytes if f64 else L.o3dx_icp_target_workspace_bytes)(nt),
+                      s.device, "icp_target")
+    ws = N.workspace((L.o3dx_registration_icp_f64_workspace_bytes if f64 else
+                      L.o3dx_registration_icp_workspace_bytes)(ns), s.device, "icp")
+    fn = L.o3dx_registration_icp_point_to_plane_f64 if f64 else L.o3dx_registration_icp_point_to_plane
+    rc = fn(N.ptr(s), ns, N.ptr(t), N.ptr(tn), nt, float(max_correspondence_distance), _np_ptr(T0),
+            int(max_iteration), float(relative_fitness), float(relative_rmse), _np_ptr(T), _np_ptr(fit),
+            _np_ptr(rm), N.ptr(corr), _np_ptr(nc), N.ptr(tws), tws.numel(), N.ptr(ws), ws.numel(),
+            N.stream_ptr(s.device))
     N.check(rc, "registration_icp")
     out = {"transformation": T, "fitness": float(fit[0]), "inlier_rmse": float(rm[0])}
     if return_corr:

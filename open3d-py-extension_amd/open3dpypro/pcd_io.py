@@ -202,14 +202,18 @@ def read_pcd_device(filename: str, device, remove_nan_points: bool = False, remo
     with open(filename, "rb") as f:
         h = _parse_header(f)
         mode = h["DATA"][0].lower()
-        if mode == "ascii":
-            f.close()
-            pts, nrm, col = read_pcd(filename, remove_nan_points, remove_infinite_points)
-            tt = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
-            return tt(pts), tt(nrm), tt(col)
         fields = h["FIELDS"]
         sizes = [int(v) for v in h.get("SIZE", ["4"] * len(fields))]
         types = [t.upper() for t in h.get("TYPE", ["F"] * len(fields))]
+        wide = any(k in fields and sizes[fields.index(k)] == 8 for k in ("x", "y", "z"))
+        if mode == "ascii" or wide:
+            # ASCII values and F8 coordinates are float64 data (Open3D reads
+            # them into its float64 storage): host decode, float64 points —
+            # PointCloud keeps them in float64 when float32 cannot hold them
+            f.close()
+            pts, nrm, col = read_pcd(filename, remove_nan_points, remove_infinite_points)
+            tt = lambda a, dt=np.float32: None if a is None else torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)  # noqa: E731
+            return tt(pts, np.float64), tt(nrm), tt(col)
         counts = [int(v) for v in h.get("COUNT", ["1"] * len(fields))]
         npts = int(h["POINTS"][0]) if "POINTS" in h else int(h["WIDTH"][0]) * int(h.get("HEIGHT", ["1"])[0])
         rec = sum(sz * c for sz, c in zip(sizes, counts))

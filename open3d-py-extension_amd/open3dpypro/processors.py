@@ -19,7 +19,7 @@ import torch
 
 from . import ops
 from . import _native as N
-from .PointCloud import PointCloud, PointCloudBase, _next_seed
+from .PointCloud import PointCloud, PointCloudBase, _f32_exact, _next_seed
 from .PointCloudMat import PointCloudMat, PointCloudMatInfo, PointCloudMatProcessor, ShapeType
 
 logger = print
@@ -36,7 +36,13 @@ def _to_gpu(a) -> torch.Tensor:
 
 
 def _xyz(a) -> torch.Tensor:
-    return _to_gpu(a)[:, :3].float().contiguous()
+    """The mat's coordinates for the kernels: float32, or float64 when the
+    mat holds float64 values float32 cannot represent (the float64 boundary:
+    the reference's CPU models hand those to Open3D's float64 storage)."""
+    t = _to_gpu(a)[:, :3]
+    if t.dtype == torch.float64 and not _f32_exact(t):
+        return t.contiguous()
+    return t.float().contiguous()
 
 
 class Processors:

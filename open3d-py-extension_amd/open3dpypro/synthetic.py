@@ -98,6 +98,56 @@ def apply_transform(p: torch.Tensor, T: np.ndarray) -> torch.Tensor:
     return (p.double() @ Tt[:3, :3].T + Tt[:3, 3]).to(torch.float32)
 
 
+LAS_OFFSET = (512345.6789, 431234.5678, 118.765)
+
+
+def uniform01_f64(counter: torch.Tensor, seed: int) -> torch.Tensor:
+    """float64 in [0,1) with a full 53-bit mantissa."""
+    return (_srl(splitmix64(counter, seed), 11).to(torch.float64)) * (1.0 / 9007199254740992.0)
+
+
+def las_scene(n: int, seed: int = 0, dims=(40.0, 32.0, 24.0), offset=LAS_OFFSET, T=None,
+              device="cpu") -> torch.Tensor:
+    """(n,3) float64 LAS-like scan: uniform samples on the surface of the box
+    [0,a]x[0,b]x[0,c] metres with full-mantissa float64 coordinates, moved by
+    the rigid motion T (about the box centre; None: identity) and placed at a
+    georeferenced offset (~5e5 m).  Not float32-representable: the float64
+    boundary's test cloud."""
+    a, b, c = dims
+    areas = np.array([b * c, b * c, a * c, a * c, a * b, a * b], np.float64)
+    cum = torch.tensor(np.cumsum(areas) / areas.sum(), dtype=torch.float64, device=device)
+    i = torch.arange(n, dtype=torch.int64, device=device)
+    f = torch.searchsorted(cum, uniform01_f64(i, seed + 13), right=True).clamp_max(5)
+    u = uniform01_f64(3 * i, seed + 17)
+    v = uniform01_f64(3 * i + 1, seed + 17)
+    p = torch.empty((n, 3), dtype=torch.float64, device=device)
+    axis = f // 2
+    side = (f % 2).to(torch.float64)
+    D = torch.tensor([a, b, c], dtype=torch.float64, device=device)
+    for ax in range(3):
+        m = axis == ax
+        o1, o2 = [k for k in range(3) if k != ax]
+        p[m, ax] = side[m] * D[ax]
+        p[m, o1] = u[m] * D[o1]
+        p[m, o2] = v[m] * D[o2]
+    if T is not None:
+        ctr = D * 0.5
+        Tt = torch.tensor(np.asarray(T, np.float64), dtype=torch.float64, device=device)
+        p = (p - ctr) @ Tt[:3, :3].T + Tt[:3, 3] + ctr
+    return p + torch.tensor(offset, dtype=torch.float64, device=device)
+
+
+def las_motion_world(T: np.ndarray, dims=(40.0, 32.0, 24.0), offset=LAS_OFFSET) -> np.ndarray:
+    """The world-frame 4x4 of las_scene's motion T (applied about the box
+    centre): the transformation registration_icp recovers, source -> target,
+    when the source is las_scene(T=T) and the target las_scene()."""
+    c = np.asarray(dims, np.float64) * 0.5 + np.asarray(offset, np.float64)
+    A, B = np.eye(4), np.eye(4)
+    A[:3, 3] = c
+    B[:3, 3] = -c
+    return A @ np.asarray(T, np.float64) @ B
+
+
 def voxel_size_for(n: int) -> float:
     """C2/C4 voxel size (4/N)^(1/3): ~4 points per voxel on the unit cube."""
     return (4.0 / n) ** (1.0 / 3.0)

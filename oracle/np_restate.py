@@ -16,7 +16,7 @@ def voxel_down_sample(xyz, voxel_size, min_bound=None):
     (reference PointCloud.py:338-341, :185-204): representative = largest
     index per voxel, keys floor((p - min_bound)/vs) in float64; returns the
     ascending representative indices."""
-    p = np.asarray(xyz, np.float32).astype(np.float64).reshape(-1, 3)
+    p = np.asarray(xyz, np.float64).reshape(-1, 3)
     if len(p) == 0:
         return np.zeros(0, np.int64)
     mn = p.min(0) if min_bound is None else np.asarray(min_bound, np.float64)
@@ -95,7 +95,7 @@ def triangle_plane(p0, p1, p2):
 
 def segment_plane_counts(xyz, thr, samples):
     """Per-hypothesis exact inlier counts (ransac_n == 3) — EvaluateRANSACBasedOnDistance."""
-    p = np.asarray(xyz, np.float32).astype(np.float64).reshape(-1, 3)
+    p = np.asarray(xyz, np.float64).reshape(-1, 3)
     out = []
     for s in np.asarray(samples).reshape(-1, 3):
         pl = triangle_plane(p[s[0]], p[s[1]], p[s[2]])
@@ -215,7 +215,7 @@ def fx_value(row):
 
 def plane_abs_sum_fx(pts, plane, thr):
     """Sigma |d| over |d| < thr (EvaluateRANSACBasedOnDistance's error sum) as an fx row."""
-    d = plane_dist(plane, np.asarray(pts, np.float32).astype(np.float64).reshape(-1, 3))
+    d = plane_dist(plane, np.asarray(pts, np.float64).reshape(-1, 3))
     return fx_row(d[d < thr], fx_exp(thr))
 
 
@@ -223,7 +223,7 @@ def plane_moments_fx(pts, A, centroid=None):
     """GetPlaneFromPoints' sums over pts as fx rows: {x, y, z} (q from A, the
     cloud's largest |coordinate|) or, with the centroid, centred {xx, xy, xz,
     yy, yz, zz} (q from 4 A^2 * 1.01)."""
-    p = np.asarray(pts, np.float32).astype(np.float64).reshape(-1, 3)
+    p = np.asarray(pts, np.float64).reshape(-1, 3)
     if centroid is None:
         q = fx_exp(A)
         return np.stack([fx_row(p[:, a], q) for a in range(3)])

@@ -15,6 +15,10 @@
 // note names the Open3D source it restates.  The reference call sites each
 // function serves are cited per function.
 //
+// Inputs are float64 coordinates, as Open3D stores them (Vector3dVector):
+// a float32 cloud is passed upcast (exact), a float64 cloud as is (the
+// float64 boundary of libo3dx, include/o3dx.h o3dx_*_f64).
+//
 // Floating-point order choices (documented so the GPU path can match them):
 //   * voxel key  : ((double)p - min_bound) / voxel_size, floor, per axis.
 //   * plane dist : (a*x + c*z) + (b*y + d)  — Eigen's packet reduction of a
@@ -217,7 +221,7 @@ struct KDTree {
   }
 };
 
-std::vector<V3> to_v3(const float* xyz, int64_t n) {
+std::vector<V3> to_v3(const double* xyz, int64_t n) {
   std::vector<V3> v((size_t)n);
   for (int64_t i = 0; i < n; ++i) v[i] = {(double)xyz[3 * i], (double)xyz[3 * i + 1], (double)xyz[3 * i + 2]};
   return v;
@@ -598,7 +602,7 @@ void oref_set_num_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
 // Reference: PointCloud.get_aabb (PointCloud.py:145-146).  [upstream]
 // Geometry3D::ComputeMinBound/MaxBound (zero vector for an empty cloud).
-void oref_aabb(const float* xyz, int64_t n, double* mm) {
+void oref_aabb(const double* xyz, int64_t n, double* mm) {
   if (n == 0) {
     for (int i = 0; i < 6; ++i) mm[i] = 0;
     return;
@@ -623,7 +627,7 @@ void oref_aabb(const float* xyz, int64_t n, double* mm) {
 // that octant.  Output rows here are ordered by ascending representative
 // (= max) index, the order _select_by_idx produces.
 // Returns 0, or -22 on Open3D's LogError conditions.
-int oref_voxel_down_sample(const float* xyz, int64_t n, const double* minb, const double* maxb,
+int oref_voxel_down_sample(const double* xyz, int64_t n, const double* minb, const double* maxb,
                            double vs, int32_t* rep_idx, int64_t* m_out, int32_t* voxel_of_point,
                            int32_t* cubic) {
   if (vs <= 0.0) return -22;
@@ -701,7 +705,7 @@ int oref_voxel_down_sample(const float* xyz, int64_t n, const double* minb, cons
 // ascending), each bucket keeps the last = max index per key.  The function
 // of the input is the same as the single pass's rep_idx; the CPU suite holds
 // the two equal.
-int oref_voxel_reps_parallel(const float* xyz, int64_t n, const double* minb, const double* maxb, double vs,
+int oref_voxel_reps_parallel(const double* xyz, int64_t n, const double* minb, const double* maxb, double vs,
                              int32_t* rep_idx, int64_t* m_out) {
   if (vs <= 0.0) return -22;
   double ext = std::max(maxb[0] - minb[0], std::max(maxb[1] - minb[1], maxb[2] - minb[2]));
@@ -789,7 +793,7 @@ int oref_voxel_reps_parallel(const float* xyz, int64_t n, const double* minb, co
 // EstimatePerPointCovariances (Search >= 3 -> ComputeCovariance else
 // Identity) + FastEigen3x3; zero -> (0,0,1); prior normals flip the sign.
 // normals_out: (n,3) float64.
-void oref_estimate_normals(const float* xyz, int64_t n, int mode, int knn, double radius,
+void oref_estimate_normals(const double* xyz, int64_t n, int mode, int knn, double radius,
                            const double* prior, double* normals_out) {
   std::vector<V3> pts = to_v3(xyz, n);
   KDTree tree;
@@ -827,7 +831,7 @@ void oref_estimate_normals(const float* xyz, int64_t n, int mode, int knn, doubl
 }
 
 // Batched KDTreeFlann search (PointCloud.py:148-163).  Outputs (nq,K) rows.
-void oref_knn_search(const float* xyz, int64_t n, const float* q, int64_t nq, int mode, int knn,
+void oref_knn_search(const double* xyz, int64_t n, const double* q, int64_t nq, int mode, int knn,
                      double radius, int K, int32_t* idx_out, double* d2_out, int32_t* cnt_out) {
   std::vector<V3> pts = to_v3(xyz, n);
   KDTree tree;
@@ -885,7 +889,7 @@ void oref_ransac_samples(int64_t n, int ransac_n, int iters, uint64_t seed, int3
 // hypotheses are scored in parallel, which cannot change a hypothesis' score.
 // counts/sums (nullable): per-hypothesis inlier count and Sigma|d| (0 for
 // degenerate hypotheses, count -1 marks them).  inliers: ascending indices.
-int oref_segment_plane(const float* xyz, int64_t n, double thr, int ransac_n, int iters,
+int oref_segment_plane(const double* xyz, int64_t n, double thr, int ransac_n, int iters,
                        double prob, const int32_t* samples, double* plane_out, int64_t* inliers,
                        int64_t* n_inliers, int64_t* counts, double* sums, int32_t* best_hyp) {
   if (prob <= 0 || prob > 1) return -22;
@@ -970,7 +974,7 @@ int oref_segment_plane(const float* xyz, int64_t n, double thr, int ransac_n, in
   return 0;
 }
 
-void oref_plane_from_points(const float* xyz, const int64_t* idx, int64_t k, double* plane_out) {
+void oref_plane_from_points(const double* xyz, const int64_t* idx, int64_t k, double* plane_out) {
   // gather the k points as doubles
   std::vector<V3> pts((size_t)k);
   std::vector<int64_t> id((size_t)k);
@@ -989,7 +993,7 @@ void oref_plane_from_points(const float* xyz, const int64_t* idx, int64_t k, dou
 // utility/Eigen.cpp ComputeJTJandJTr / SolveJacobianSystemAndObtainExtrinsicMatrix.
 // The source copy is transformed incrementally in float64, as Open3D does.
 // corr (nullable, 2*ns int32) / ncorr: final correspondence set.
-int oref_registration_icp(const float* src, int64_t ns, const float* tgt, const float* tgt_n,
+int oref_registration_icp(const double* src, int64_t ns, const double* tgt, const double* tgt_n,
                           int64_t nt, double max_dist, const double* init, int max_iter,
                           double rel_fit, double rel_rmse, double* T_out, double* fitness,
                           double* rmse, int32_t* corr, int64_t* ncorr) {
@@ -1088,7 +1092,7 @@ int oref_registration_icp(const float* src, int64_t ns, const float* tgt, const 
 
 // Open3D-style single ICP accumulation at transformation T (for sharded tests):
 // sums layout = O3DX_ICP_NSUMS (see include/o3dx.h).
-void oref_icp_accumulate(const float* src, int64_t ns, const float* tgt, const float* tgt_n,
+void oref_icp_accumulate(const double* src, int64_t ns, const double* tgt, const double* tgt_n,
                          int64_t nt, double max_dist, const double* T, double* sums) {
   std::vector<V3> tp = to_v3(tgt, nt);
   std::vector<V3> tn = to_v3(tgt_n, nt);
@@ -1150,7 +1154,7 @@ static void fx_rows(const __int128* acc, const int* q, int k, int64_t* out) {
 
 static __int128 fx_int(double t, int q) { return (__int128)std::nearbyint(std::ldexp(t, -q)); }
 
-void oref_icp_accumulate_fx(const float* src, int64_t ns, const float* tgt, const float* tgt_n, int64_t nt,
+void oref_icp_accumulate_fx(const double* src, int64_t ns, const double* tgt, const double* tgt_n, int64_t nt,
                             double max_dist, const double* T, const double* absmax, int64_t* fx_out) {
   std::vector<V3> tp = to_v3(tgt, nt);
   std::vector<V3> tn = to_v3(tgt_n, nt);

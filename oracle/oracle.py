@@ -65,8 +65,10 @@ def lib():
     return _lib
 
 
-def _f32(a):
-    return np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1, 3))
+def _f64(a):
+    """(n,3) float64 coordinates as Open3D stores them (Vector3dVector): a
+    float32 cloud is upcast exactly, a float64 cloud is taken as is."""
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1, 3))
 
 
 def _ptr(a):
@@ -82,7 +84,7 @@ def set_num_threads(n: int) -> None:
 
 
 def aabb(xyz):
-    x = _f32(xyz)
+    x = _f64(xyz)
     mm = np.zeros(6, np.float64)
     lib().oref_aabb(_ptr(x), len(x), _ptr(mm))
     return mm[:3].copy(), mm[3:].copy()
@@ -96,7 +98,7 @@ def voxel_down_sample(xyz, voxel_size, min_bound=None, max_bound=None, trace=Fal
     latter two only when trace=True.  Without trace, clouds of
     PARALLEL_REPS_AT points or more (or parallel=True) take
     oref_voxel_reps_parallel, the same function computed over hashed buckets."""
-    x = _f32(xyz)
+    x = _f64(xyz)
     n = len(x)
     if min_bound is None or max_bound is None:
         mn, mx = aabb(x)
@@ -127,7 +129,7 @@ def voxel_down_sample(xyz, voxel_size, min_bound=None, max_bound=None, trace=Fal
 
 
 def estimate_normals(xyz, mode=KNN, knn=30, radius=0.0, prior=None):
-    x = _f32(xyz)
+    x = _f64(xyz)
     out = np.zeros((len(x), 3), np.float64)
     pr = None if prior is None else np.ascontiguousarray(prior, np.float64).reshape(-1, 3)
     lib().oref_estimate_normals(_ptr(x), len(x), mode, knn, float(radius), _ptr(pr), _ptr(out))
@@ -135,8 +137,8 @@ def estimate_normals(xyz, mode=KNN, knn=30, radius=0.0, prior=None):
 
 
 def knn_search(xyz, queries, mode=KNN, knn=30, radius=0.0, K=None):
-    x = _f32(xyz)
-    q = _f32(queries)
+    x = _f64(xyz)
+    q = _f64(queries)
     if K is None:
         K = knn
     idx = np.empty((len(q), K), np.int32)
@@ -167,7 +169,7 @@ def covariance(xyz, idx, cnt=None):
     """Open3D ComputeCovariance over neighbour rows idx (m,K) (first cnt[i]
     entries, in the given order — the kNN result order): sequential float64
     raw moments, {xx,xy,xz,yy,yz,zz}.  <3 neighbours -> identity."""
-    p = np.asarray(xyz, np.float32).reshape(-1, 3).astype(np.float64)
+    p = np.asarray(xyz, np.float64).reshape(-1, 3)
     idx = np.asarray(idx).reshape(len(idx), -1)
     cnt = np.full(len(idx), idx.shape[1]) if cnt is None else np.asarray(cnt)
     out = np.zeros((len(idx), 6))
@@ -196,7 +198,7 @@ def segment_plane(xyz, distance_threshold, ransac_n, num_iterations, samples,
                   probability=0.99999999):
     """Returns (plane[4], inliers int64 ascending, counts per hypothesis (-1 =
     degenerate), abs sums per hypothesis, best hypothesis index)."""
-    x = _f32(xyz)
+    x = _f64(xyz)
     n = len(x)
     s = np.ascontiguousarray(samples, np.int32).reshape(num_iterations, ransac_n)
     plane = np.zeros(4, np.float64)
@@ -214,7 +216,7 @@ def segment_plane(xyz, distance_threshold, ransac_n, num_iterations, samples,
 
 
 def plane_from_points(xyz, idx):
-    x = _f32(xyz)
+    x = _f64(xyz)
     i = np.ascontiguousarray(idx, np.int64)
     out = np.zeros(4, np.float64)
     lib().oref_plane_from_points(_ptr(x), _ptr(i), len(i), _ptr(out))
@@ -223,9 +225,9 @@ def plane_from_points(xyz, idx):
 
 def registration_icp(src, tgt, tgt_normals, max_dist, init=None, max_iteration=30,
                      relative_fitness=1e-6, relative_rmse=1e-6):
-    s = _f32(src)
-    t = _f32(tgt)
-    tn = _f32(tgt_normals)
+    s = _f64(src)
+    t = _f64(tgt)
+    tn = _f64(tgt_normals)
     T0 = np.eye(4) if init is None else np.asarray(init, np.float64)
     T0 = np.ascontiguousarray(T0, np.float64)
     T = np.zeros((4, 4), np.float64)
@@ -243,9 +245,9 @@ def registration_icp(src, tgt, tgt_normals, max_dist, init=None, max_iteration=3
 
 
 def icp_accumulate(src, tgt, tgt_normals, max_dist, T):
-    s = _f32(src)
-    t = _f32(tgt)
-    tn = _f32(tgt_normals)
+    s = _f64(src)
+    t = _f64(tgt)
+    tn = _f64(tgt_normals)
     TT = np.ascontiguousarray(T, np.float64)
     sums = np.zeros(32, np.float64)
     lib().oref_icp_accumulate(_ptr(s), len(s), _ptr(t), _ptr(tn), len(t), float(max_dist),
@@ -256,9 +258,9 @@ def icp_accumulate(src, tgt, tgt_normals, max_dist, T):
 def icp_accumulate_fx(src, tgt, tgt_normals, max_dist, T, absmax):
     """The same sums as exact fx rows (32, 4) int64 {lo, hi, q, 0} (the
     order-free form libo3dx uses; restated with 128-bit integers)."""
-    s = _f32(src)
-    t = _f32(tgt)
-    tn = _f32(tgt_normals)
+    s = _f64(src)
+    t = _f64(tgt)
+    tn = _f64(tgt_normals)
     TT = np.ascontiguousarray(T, np.float64)
     am = np.ascontiguousarray(absmax, np.float64).reshape(3)
     fx = np.zeros((32, 4), np.int64)

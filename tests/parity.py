@@ -40,9 +40,13 @@ def assert_normals(got, ref, xyz=None, mode=O.KNN, k=30, radius=0.0, prior=None,
     info = {"rows": int(len(got)), "max_err": float(e.max()) if len(e) else 0.0, "beyond_tol": int(len(bad)),
             "certified": 0}
     if len(bad):
-        assert xyz is not None and mode != O.RADIUS, (what, info)
-        x = np.asarray(xyz, np.float32).reshape(-1, 3)
-        idx, _, cnt = O.knn_search(x, x[bad], mode, k, radius)
+        assert xyz is not None, (what, info)
+        x = np.asarray(xyz).reshape(-1, 3)  # float32 clouds, or float64 ones kept as such
+        if mode == O.RADIUS:  # every neighbour within the radius, sorted (capped rows would not certify)
+            idx, _, cnt = O.knn_search(x, x[bad], mode, k, radius, K=1024)
+            assert (cnt < 1024).all(), (what, "radius neighbourhoods beyond the certificate's cap")
+        else:
+            idx, _, cnt = O.knn_search(x, x[bad], mode, k, radius)
         cov = O.covariance(x, idx, cnt)
         ok = np.zeros(len(bad), bool)
         for nudge in range(1, 27):
@@ -63,7 +67,7 @@ def assert_normals(got, ref, xyz=None, mode=O.KNN, k=30, radius=0.0, prior=None,
 def assert_neighbour_sets(nbr, xyz, k, what=""):
     """Sorted neighbour ids of every row == the oracle's kNN set (bit-exact)."""
     g = np.sort(np.asarray(nbr), 1)
-    x = np.asarray(xyz, np.float32).reshape(-1, 3)
+    x = np.asarray(xyz).reshape(-1, 3)
     idx, _, _ = O.knn_search(x, x, O.KNN, k)
     o = np.sort(idx, 1)
     diff = np.any(g != o, 1)

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     for name in decl:
         assert hasattr(lib, name), name
     assert sorted(N.declared_symbols()) == decl
-    assert lib.o3dx_abi_version() == 4
+    assert lib.o3dx_abi_version() == 5
 
 
 def test_library_host_only_entry_points():
@@ -492,3 +492,19 @@ def test_anchored_moment_sums_are_correctly_rounded():
                 pp[:, 1] * pp[:, 1], pp[:, 1] * pp[:, 2], pp[:, 2] * pp[:, 2]]
         exp = [math.fsum(c.tolist()) for c in cols]
         assert got == exp, (trial, k, got, exp)
+
+
+def test_f32_exact_check():
+    """PointCloud's float64 boundary test: float32-representable float64
+    values (NaN included) take the float32 kernels, anything else float64."""
+    from open3dpypro.PointCloud import _f32_exact
+
+    a = np.array([[0.5, 1.25, np.nan], [3.0, -2.0, 1e30]])
+    assert not _f32_exact(a)  # 1e30 is not a float32 value
+    a[1, 2] = np.float32(1e30)
+    assert _f32_exact(a) and _f32_exact(torch.from_numpy(a))
+    b = a.copy()
+    b[0, 0] = 0.1
+    assert not _f32_exact(b) and not _f32_exact(torch.from_numpy(b))
+    las = S.las_scene(1000).numpy()
+    assert not _f32_exact(las) and _f32_exact(las.astype(np.float32).astype(np.float64))

@@ -160,6 +160,56 @@ def test_icp_oracle_recovers_transform():
 
 
 # ---------------------------------------------------------------------------
+# The float64 boundary: the oracle takes float64 coordinates as Open3D does
+# (oracle.py _f64); a float32 cloud is upcast exactly, so its results are the
+# ones the float32 oracle gave (bunny: voxel counts, normals, RANSAC).
+def test_oracle_float64_input_equals_float32_upcast(bunny):
+    b64 = bunny.astype(np.float64)
+    assert np.array_equal(O.voxel_down_sample(bunny, 0.005), O.voxel_down_sample(b64, 0.005))
+    assert np.array_equal(O.estimate_normals(bunny, O.KNN, 30), O.estimate_normals(b64, O.KNN, 30))
+    s = O.ransac_samples(len(bunny), 3, 100, 5)
+    p32, i32 = O.segment_plane(bunny, 0.01, 3, 100, s)[:2]
+    p64, i64 = O.segment_plane(b64, 0.01, 3, 100, s)[:2]
+    assert np.array_equal(p32, p64) and np.array_equal(i32, i64)
+
+
+def test_oracle_float64_keys_not_rounded():
+    """A float64 cloud keeps its values: voxel keys of points straddling a
+    voxel face that float32 rounding moves across it differ."""
+    x = np.array([[500000.0, 0, 0], [500000.0 + 0.2 - 1e-9, 0, 0], [500000.0 + 0.2 + 1e-9, 0, 0]])
+    rep = O.voxel_down_sample(x, 0.2, min_bound=x.min(0), max_bound=x.max(0))
+    assert len(rep) == 2  # the float32 values are all 500000.0 or 500000.1875: one voxel
+    assert len(O.voxel_down_sample(x.astype(np.float32), 0.2)) == 1
+
+
+def test_icp_offset_conditioning():
+    """Open3D's point-to-plane system on raw coordinates at a LAS-like offset:
+    J = [p x n; n] with |p| ~ 5e5 makes the 6x6 normal matrix singular in
+    float64, and the oracle's T becomes rounding noise (a permuted source
+    moves it, it misses the motion by metres).  At a 1e4 m offset the same
+    registration is well-posed (T stable to ~1e-9).  The float64 GPU parity
+    tests (tests/test_gpu_f64.py test_f64_icp) therefore check the ~5e5 scan
+    in its recentred frame and full-mantissa clouds at 1e4 m."""
+    import torch  # noqa: F401
+    from open3dpypro import synthetic as S
+
+    n = 60_000
+    M = S.rigid_transform(1.0, t=(0.2, -0.12, 0.08))
+    perm = np.random.default_rng(0).permutation(n)
+    spread = {}
+    for name, off in (("1e4", (12345.678, 23456.789, 98.765)), ("las", S.LAS_OFFSET)):
+        tgt = S.las_scene(n, seed=0, offset=off).numpy()
+        src = S.las_scene(n, seed=1, T=M, offset=off).numpy()
+        tn = O.estimate_normals(tgt, O.KNN, 30)
+        kw = dict(max_iteration=30, relative_fitness=0, relative_rmse=0)
+        T1 = O.registration_icp(src, tgt, tn, 0.8, **kw)[0]
+        T2 = O.registration_icp(src[perm], tgt, tn, 0.8, **kw)[0]
+        spread[name] = np.abs(T1 - T2).max()
+    assert spread["1e4"] < 1e-7, spread
+    assert spread["las"] > 1e-4, spread
+
+
+# ---------------------------------------------------------------------------
 # The glue around the hot path, pinned by the reference's OWN outputs
 # (tests/golden/ref_glue.npz, written by `python tests/golden/make_golden.py
 # glue` from /root/reference/open3dpypro/processors.py in this container):
