@@ -524,6 +524,20 @@ int o3dx_pcd_unpack(const uint8_t* data_dev, int64_t n, int nfields, const int32
                     const int64_t* src_off_host, const int64_t* src_stride_host,
                     float* const* dst_dev_host, const int64_t* dst_stride_host, void* stream);
 
+/* ------------------------------------------------------- one-query search
+ * (ABI 5) One KDTreeFlann query of any size (reference PointCloud.py:148-163:
+ * get_points_by_knn asks for up to 10^6 neighbours, get_points_radius for
+ * every point within a radius): mode O3DX_SEARCH_KNN (the knn nearest),
+ * RADIUS (every point with d^2 < radius^2) or HYBRID (the knn nearest of
+ * those).  d^2 in float64 in nanoflann's order on the cloud's coordinates
+ * (xyz_f64: (n,3) float64, else float32); results sorted by (d^2, index).
+ * idx_out_dev / d2_out_dev (nullable) receive the first min(count, cap);
+ * count_host the full count.  Synchronises the stream. */
+size_t o3dx_search_one_workspace_bytes(int64_t n);
+int o3dx_search_one(const void* xyz_dev, int xyz_f64, int64_t n, const double* query_host, int mode, int64_t knn,
+                    double radius, int32_t* idx_out_dev, double* d2_out_dev, int64_t cap, int64_t* count_host,
+                    void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------- float64 boundary
  * (ABI 5) The hot-path calls on (n,3) float64 clouds, computed on the
  * caller's float64 values exactly as Open3D computes them on its float64

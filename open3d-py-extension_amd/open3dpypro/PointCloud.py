@@ -104,44 +104,28 @@ class RegistrationResult:
 
 class KDTreeGrid:
     """Stand-in for o3d.geometry.KDTreeFlann (reference PointCloud.py:148-163):
-    the same search_* methods and return shapes, backed by the GPU grid search."""
+    the same search_* methods and return shapes (k, IntVector-like int64
+    indices, DoubleVector-like float64 d^2).  Each call is one device query of
+    any size (o3dx_search_one: a float64 d^2 pass over the cloud, the
+    candidates compacted and radix-sorted by (d^2, index)) — the reference's
+    get_points_by_knn asks for up to 10^6 neighbours."""
 
     def __init__(self, cloud: "PointCloudBase"):
         self._x = cloud._hot_points()
 
     def _one(self, query, mode, knn, radius):
-        q = torch.as_tensor(np.asarray(query, np.float64).reshape(1, 3), dtype=self._x.dtype, device=self._x.device)
-        idx, d2, cnt = ops.knn_search(self._x, q, mode=mode, knn=knn, radius=radius)
-        k = int(cnt[0].item())
-        return k, idx[0, :k].cpu().numpy().astype(np.int64), d2[0, :k].cpu().numpy()
+        k, idx, d2 = ops.search_one(self._x, np.asarray(query, np.float64).reshape(3), mode=mode, knn=knn,
+                                    radius=radius)
+        return k, idx.cpu().numpy().astype(np.int64), d2.cpu().numpy()
 
     def search_knn_vector_3d(self, query, knn: int):
-        if knn <= N.MAX_KNN:
-            return self._one(query, N.SEARCH_KNN, knn, 0.0)
-        return self._brute(query, knn, None)
+        return self._one(query, N.SEARCH_KNN, knn, 0.0)
 
     def search_hybrid_vector_3d(self, query, radius: float, max_nn: int):
-        if max_nn <= N.MAX_KNN:
-            return self._one(query, N.SEARCH_HYBRID, max_nn, radius)
-        return self._brute(query, max_nn, radius)
+        return self._one(query, N.SEARCH_HYBRID, max_nn, radius)
 
     def search_radius_vector_3d(self, query, radius: float):
-        return self._brute(query, None, radius)
-
-    def _brute(self, query, knn, radius):
-        # large-k / radius queries: the grid search is register-bounded to
-        # O3DX_MAX_KNN; answer with the exact kNN of the whole cloud instead
-        x = self._x
-        k = x.shape[0] if knn is None else min(int(knn), x.shape[0])
-        q = torch.as_tensor(np.asarray(query, np.float64).reshape(1, 3), dtype=x.dtype, device=x.device)
-        d = x.double() - q.double()
-        d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
-        order = torch.argsort(d2, stable=True)[:k]
-        dd = d2[order]
-        if radius is not None:
-            keep = dd < radius * radius
-            order, dd = order[keep], dd[keep]
-        return int(order.numel()), order.cpu().numpy(), dd.cpu().numpy()
+        return self._one(query, N.SEARCH_RADIUS, 0, radius)
 
 
 class PointCloudBase:

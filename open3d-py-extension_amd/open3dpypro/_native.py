@@ -99,6 +99,8 @@ _SIGS = {
                                  _P]),
     "o3dx_registration_icp_point_to_plane": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,
                                                      _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    "o3dx_search_one_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_search_one": (_I32, [_P, _I32, _I64, _P, _I32, _I64, _D, _P, _P, _I64, _P, _P, _SZ, _P]),
     # the float64 boundary (ABI 5)
     "o3dx_aabb_f64_workspace_bytes": (_SZ, [_I64]),
     "o3dx_aabb_f64": (_I32, [_P, _I64, _P, _P, _SZ, _P]),

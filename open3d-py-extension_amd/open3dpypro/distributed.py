@@ -68,10 +68,12 @@ def global_aabb(local_min, local_max, group=None) -> Tuple[np.ndarray, np.ndarra
     return v[:3].copy(), -v[3:].copy()
 
 
-def global_bounds_device(xyz: torch.Tensor, group=None) -> Tuple[np.ndarray, np.ndarray]:
+def global_bounds_device(xyz: torch.Tensor, group=None, with_count: bool = False):
     """Global (min_bound, max_bound) of a cloud spread over the ranks: the
     device AABB of this rank's points (o3dx_aabb_device, no host wait), one
-    all-reduce, one host read.  +inf / -inf when every rank is empty."""
+    all-reduce, one host read.  +inf / -inf when every rank is empty.
+    with_count: also the largest point count of any rank (folded into the
+    same all-reduce as -count), returned third."""
     from . import ops
 
     world, _ = _world(group)
@@ -80,10 +82,14 @@ def global_bounds_device(xyz: torch.Tensor, group=None) -> Tuple[np.ndarray, np.
         v = torch.cat([mm[:3], -mm[3:]])
     else:
         v = torch.full((6,), math.inf, dtype=torch.float64, device=xyz.device)
+    if with_count:
+        v = torch.cat([v, torch.full((1,), -float(xyz.shape[0]), dtype=torch.float64, device=v.device)])
     if world > 1:
         v = v.to(_comm_device(group))
         dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
     h = v.cpu().numpy()
+    if with_count:
+        return h[:3].copy(), -h[3:6].copy(), int(-h[6])
     return h[:3].copy(), -h[3:].copy()
 
 
@@ -655,7 +661,7 @@ def _slab_reps_generic(xyz, gidx, voxel_size, group, voxel_fn, presorted):
     return gidx[rep].contiguous(), xyz[rep].contiguous(), mn, mx, keys
 
 
-def _slab_reps_device(xyz, gidx, vs, group, presorted, timings=None, t0=None):
+def _slab_reps_device(xyz, gidx, vs, group, presorted, timings=None, t0=None, want_nmax=False):
     """HIP form of the slab voxel step: global bounds on the device (one
     all-reduce, one read), points to their slab owner unless presorted, the
     slab's reps with GLOBAL keys (a dense x-key window table when the slab is
@@ -664,12 +670,15 @@ def _slab_reps_device(xyz, gidx, vs, group, presorted, timings=None, t0=None):
     where `bad` is a device count of points outside the slab (presorted
     inputs on more than one rank) or None.  A presorted rank holding such
     points returns no reps and its count instead of raising, so every caller
-    turns the all-reduced count into the same RuntimeError on every rank."""
+    turns the all-reduced count into the same RuntimeError on every rank.
+    With want_nmax, an eighth value: the largest point count any rank held
+    before the slab exchange (from the bounds all-reduce; world x it bounds
+    every rank's reps)."""
     from . import ops
 
     world, rank = _world(group)
     t0 = time.perf_counter() if t0 is None else t0
-    mn, mx = global_bounds_device(xyz, group)
+    mn, mx, nmax = global_bounds_device(xyz, group, with_count=True)
     _stamp(timings, "bounds", t0)
     if not np.all(np.isfinite(mn)):
         raise RuntimeError("voxel_normals_slabs: the cloud is empty on every rank")
@@ -694,7 +703,7 @@ def _slab_reps_device(xyz, gidx, vs, group, presorted, timings=None, t0=None):
                     raise
                 kx = torch.floor((xyz[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
                 bad = ((kx < k_lo) | (kx >= k_hi)).sum()
-                return gidx[:0], xyz[:0], mn, mx, keys, dims, bad
+                return (gidx[:0], xyz[:0], mn, mx, keys, dims, bad) + ((nmax,) if want_nmax else ())
         else:
             out = ops.voxel_down_sample(xyz, vs, mn, mx)
             if presorted and world > 1:
@@ -706,7 +715,7 @@ def _slab_reps_device(xyz, gidx, vs, group, presorted, timings=None, t0=None):
         rxyz, rg = xyz[:0], gidx[:0]
         if n_loc > 0:
             bad = torch.full((), n_loc, dtype=torch.int64, device=xyz.device)
-    return rg, rxyz, mn, mx, keys, dims, bad
+    return (rg, rxyz, mn, mx, keys, dims, bad) + ((nmax,) if want_nmax else ())
 
 
 def voxel_slabs(xyz: torch.Tensor, gidx: torch.Tensor, voxel_size: float, group=None, presorted: bool = False):
@@ -758,7 +767,8 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
     world, rank = _world(group)
     vs = float(voxel_size)
     t0 = time.perf_counter()
-    rg, rxyz, mn, mx, keys, dims, bad = _slab_reps_device(xyz, gidx, vs, group, presorted, timings, t0)
+    rg, rxyz, mn, mx, keys, dims, bad, nmax = _slab_reps_device(xyz, gidx, vs, group, presorted, timings, t0,
+                                                                want_nmax=True)
     k_lo, k_hi, nkeys = keys[rank], keys[rank + 1], keys[-1]
     layer = int(dims[1] * dims[2])
     dev = rxyz.device
@@ -781,8 +791,36 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
         # exchanged in fixed-size packets: hk layers hold at most cap = hk x
         # layer reps (one per voxel), a bound every rank knows without a
         # count exchange; unused rows are padding (NaN coordinates, gidx bits
-        # INT32_MAX: they sort last and the table build skips them)
-        if world > 1:
+        # INT32_MAX: they sort last and the table build skips them).  The
+        # packets are used only while that bound stays within the data (hk x
+        # layer <= the largest rank's point count, or 2^20 rows — every rank
+        # decides alike from global values); a wide, sparse cloud whose voxel
+        # cross-section dwarfs its points (a km-scale scan at cm voxels)
+        # exchanges counted rows instead (one more host wait per round)
+        fixed = hk * layer <= max(nmax, 1 << 20)
+        if world > 1 and not fixed:
+            zero = torch.zeros(n_own, dtype=torch.bool, device=dev)
+            send_lo = (kxr < k_lo + hk) if rank > 0 else zero
+            send_hi = (kxr >= k_hi - hk) if rank < world - 1 else zero
+            cnt = torch.zeros(world, dtype=torch.int64, device=dev)
+            if rank > 0:
+                cnt[rank - 1] = send_lo.sum()
+            if rank < world - 1:
+                cnt[rank + 1] = send_hi.sum()
+            cnt = cnt.to(cd)
+            rcnt = torch.empty_like(cnt)
+            dist.all_to_all_single(rcnt, cnt, group=group)
+            ss, rs = cnt.tolist(), rcnt.tolist()
+            send = torch.cat([packed[send_lo], packed[send_hi]]).to(cd)  # each part ascending in global index
+            recv = torch.empty((sum(rs), 4), dtype=torch.float32, device=cd)
+            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=group)
+            recv = recv.to(dev)
+            _stamp(timings, f"halo{hk}_exchanged", t0)
+            na = rs[rank - 1] if rank > 0 else 0  # the lower neighbour's rows come first
+            ha, hb = recv[:na], recv[na:]
+            ga = ha[:, 3].contiguous().view(torch.int32).long()
+            gb = hb[:, 3].contiguous().view(torch.int32).long()
+        if world > 1 and fixed:
             zero = torch.zeros(n_own, dtype=torch.bool, device=dev)
             send_lo = (kxr < k_lo + hk) if rank > 0 else zero
             send_hi = (kxr >= k_hi - hk) if rank < world - 1 else zero
@@ -811,6 +849,7 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
             ha, hb = recv[:na], recv[na:]
             ga = ha[:, 3].contiguous().view(torch.int32).long()
             gb = hb[:, 3].contiguous().view(torch.int32).long()
+        if world > 1:
             # merge by position: own, lower-neighbour and upper-neighbour rows are
             # each ascending in global index (padding last); padding rows land
             # at or past the union's end, in NaN-filled rows

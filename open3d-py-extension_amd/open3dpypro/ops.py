@@ -349,6 +349,28 @@ def knn_search(xyz: torch.Tensor, queries: torch.Tensor, mode: int = N.SEARCH_KN
     return idx[:nq], d2[:nq], cnt[:nq]
 
 
+def search_one(xyz: torch.Tensor, query, mode: int = N.SEARCH_KNN, knn: int = 30, radius: float = 0.0):
+    """One KDTreeFlann query of any size (o3dx_search_one): (k, idx (k,) int32,
+    d2 (k,) float64) on the device, sorted by (d^2, index).  mode KNN: the knn
+    nearest; RADIUS: every point with d^2 < radius^2; HYBRID: the knn nearest
+    of those.  float32 or float64 points (the cloud's own coordinates)."""
+    f64 = _is64(xyz)
+    x = _xyz64(xyz) if f64 else _xyz(xyz)
+    L = N.load()
+    n = x.shape[0]
+    q = _c(np.asarray(query, np.float64).reshape(3), np.float64)
+    cap = n if mode == N.SEARCH_RADIUS else min(int(knn), n)
+    idx = torch.empty(max(cap, 1), dtype=torch.int32, device=x.device)
+    d2 = torch.empty(max(cap, 1), dtype=torch.float64, device=x.device)
+    cnt = np.zeros(1, np.int64)
+    ws = N.workspace(L.o3dx_search_one_workspace_bytes(n), x.device, "search")
+    N.check(L.o3dx_search_one(N.ptr(x), 1 if f64 else 0, n, _np_ptr(q), int(mode), int(knn), float(radius),
+                              N.ptr(idx), N.ptr(d2), cap, _np_ptr(cnt), N.ptr(ws), ws.numel(),
+                              N.stream_ptr(x.device)), "search_one")
+    k = int(cnt[0])
+    return k, idx[:k], d2[:k]
+
+
 def ransac_samples(n: int, ransac_n: int, num_iterations: int, seed: int) -> np.ndarray:
     """Open3D RandomSampler over mt19937(seed): (iters, ransac_n) int32."""
     out = np.empty((max(num_iterations, 1), ransac_n), np.int32)

@@ -185,15 +185,44 @@ def test_seg_planes_rounds_vs_oracle():
 
 
 def test_kdtree_helpers(bunny):
+    """get_points_by_knn / get_points_radius / search_hybrid (reference
+    PointCloud.py:148-163) through the device one-query search: the full
+    index and d^2 lists equal the oracle's KDTreeFlann results, in (d^2,
+    index) order, for small and large k and for radius queries."""
     pc = o3p.PointCloud(bunny.astype(np.float64))
-    k, idx, d2 = pc.get_points_by_knn(100, 20)
-    ridx, rd2, _ = O.knn_search(bunny, bunny[100:101], O.KNN, 20)
-    assert k == 20 and np.array_equal(idx, ridx[0])
-    k, idx, d2 = pc.get_points_radius(100, 0.005)
-    ridx, _, rc = O.knn_search(bunny, bunny[100:101], O.RADIUS, 0, 0.005, K=4096)
-    assert k == rc[0] and set(idx.tolist()) == set(ridx[0, :k].tolist())
-    k, idx, _ = pc.get_points_by_knn(100, 1000)   # beyond the register path: exact brute force
-    assert k == 1000 and idx[0] == 100
+    for qi in (100, 20000):
+        for k_ in (20, 1000, len(bunny)):
+            k, idx, d2 = pc.get_points_by_knn(qi, k_)
+            ridx, rd2, rc = O.knn_search(bunny, bunny[qi:qi + 1], O.KNN, k_)
+            assert k == rc[0] == min(k_, len(bunny))
+            assert np.array_equal(idx, ridx[0, :k]) and np.array_equal(d2, rd2[0, :k])
+        for r in (0.005, 0.03):
+            k, idx, d2 = pc.get_points_radius(qi, r)
+            ridx, rd2, rc = O.knn_search(bunny, bunny[qi:qi + 1], O.RADIUS, 0, r, K=len(bunny))
+            assert k == rc[0] and np.array_equal(idx, ridx[0, :k]) and np.array_equal(d2, rd2[0, :k])
+        k, idx, d2 = pc.get_KDtree().search_hybrid_vector_3d(bunny[qi], 0.03, 500)
+        ridx, rd2, rc = O.knn_search(bunny, bunny[qi:qi + 1], O.HYBRID, 500, 0.03)
+        assert k == rc[0] and np.array_equal(idx, ridx[0, :k]) and np.array_equal(d2, rd2[0, :k])
+    k, idx, d2 = pc.get_points_by_knn(100)  # the reference's default max_nn = 10^6: the whole cloud, sorted
+    assert k == len(bunny) and idx[0] == 100 and np.all(np.diff(d2) >= 0)
+
+
+def test_search_one_large_k_2m(dev):
+    """One query for 10^6 neighbours on a 2M-point cloud (the default of
+    get_points_by_knn): equal to numpy's lexicographic (d^2, index) order of
+    the same float64 distances (nanoflann's expression)."""
+    n = 2_000_000
+    x = S.uniform_cube(n, 21, device=dev)
+    q = np.array([0.31, 0.62, 0.47])
+    k, idx, d2 = o3p.ops.search_one(x, q, knn=1_000_000)
+    p = x.cpu().numpy().astype(np.float64)
+    dd = ((q[0] - p[:, 0]) ** 2 + (q[1] - p[:, 1]) ** 2) + (q[2] - p[:, 2]) ** 2
+    o = np.lexsort((np.arange(n), dd))[:1_000_000]
+    assert k == 1_000_000 and np.array_equal(idx.cpu().numpy(), o) and np.array_equal(d2.cpu().numpy(), dd[o])
+    k, idx, d2 = o3p.ops.search_one(x, q, mode=2, knn=50_000, radius=0.1)
+    inr = np.nonzero(dd < 0.01)[0]
+    o = inr[np.lexsort((inr, dd[inr]))][:50_000]
+    assert k == len(o) and np.array_equal(idx.cpu().numpy(), o)
 
 
 @pytest.mark.parametrize("force_exact", [False, True])

@@ -106,6 +106,42 @@ def test_c4_slabs_clustered_on_device():
     assert np.array_equal(nn[o], ref)
 
 
+def _wide_cloud():
+    """1000 blobs of 300 points (sigma 0.3 m) scattered over a 1 km cube, 5 cm
+    voxels: the slab grid's cross-section (20000^2 voxels) dwarfs the points,
+    so the fixed-size halo packets (hk x layer rows) are out of the question
+    (they allocated by the grid, not by the data)."""
+    rng = np.random.default_rng(5)
+    c = rng.random((1000, 3)) * 1000.0
+    p = (c[:, None, :] + rng.normal(0.0, 0.3, (1000, 300, 3))).reshape(-1, 3)
+    return p.astype(np.float32), 0.05
+
+
+def _wide_rank(rank, world):
+    dev = torch.device("cuda:0")
+    pts, vs = _wide_cloud()
+    g = torch.arange(rank, len(pts), world, dtype=torch.int64)
+    rg, rx, nrm = D.voxel_normals_slabs(torch.from_numpy(pts)[g].to(dev), g.to(dev), vs, knn=30)
+    return rg, nrm
+
+
+def test_c4_slabs_sparse_wide_cloud_on_device():
+    """A wide, sparse cloud over 2 ranks: the halo goes by counted rows, and
+    the slab result equals the single-GPU one bit for bit."""
+    res = spawn(_wide_rank)
+    dev = torch.device("cuda:0")
+    pts, vs = _wide_cloud()
+    x = torch.from_numpy(pts).to(dev)
+    mn, mx = ops.aabb(x)
+    out = ops.voxel_down_sample(x, vs, mn, mx)
+    ref = ops.estimate_normals(out["rep_xyz"], knn=30).cpu().numpy()
+    g = np.concatenate([r[0] for r in res])
+    nn = np.concatenate([r[1] for r in res])
+    o = np.argsort(g)
+    assert np.array_equal(g[o], out["rep_idx"].cpu().numpy().astype(np.int64))
+    assert np.array_equal(nn[o], ref)
+
+
 def test_kdist_bound_is_an_upper_bound(dev):
     """estimate_normals(return_kdist=True): every row's bound >= the exact
     squared k-th-neighbour distance, and tight (within 1 %), on all paths."""
