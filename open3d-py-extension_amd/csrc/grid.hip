@@ -187,11 +187,6 @@ static int32_t* debug_nbr(int kneed, int64_t rows) {
   return (g_dbg_nbr && kneed == g_dbg_k && rows <= g_dbg_rows) ? g_dbg_nbr : nullptr;
 }
 
-// integer tuning / A-B switch from the environment
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 
 static void dims_for(const double mn[3], const double mx[3], double h, int64_t d[3]) {
   for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor(std::max(0.0, mx[a] - mn[a]) / h) + 1;
@@ -1890,6 +1885,7 @@ __device__ __forceinline__ int wave_rows(const GridView& g, const float4 q, int 
     const bool valid = f_ < ncand;                                               \
     const float d2 = valid ? cd2[f_] : 0.0f;                                     \
     const int pp = valid ? cpos[f_] : -1;                                        \
+    (void)pp;                                                                    \
     BODY                                                                         \
   }
 #define O3DX_WAVE_ANY(BODY)        \
@@ -2221,7 +2217,6 @@ static int pick_k(int k) {
 // grid occupancy target per search mode: ~k/4 points per cell keeps the
 // 27-cell first shell close to 2-3 k candidates
 static double occ_for(int mode, int k) {
-  if (const char* e = getenv("O3DX_GRID_OCC")) return atof(e);  // tuning override
   if (mode == O3DX_SEARCH_RADIUS) return 4.0;
   if (mode == O3DX_SEARCH_KNN) return std::max(4.0, k / 3.0);  // histogram path: shells 0..1 hold k
   return std::max(2.0, k / 4.0);
@@ -2275,7 +2270,7 @@ __global__ void __launch_bounds__(kBlock) k_vgrid_emit(const float4* __restrict_
 // 0: built; 1: no usable voxel grid (caller sorts the points instead).
 static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, double target_occ, void* ws,
                             size_t ws_bytes, hipStream_t s, GridBuild* out) {
-  if (!vox || geom[7] != 1.0 || getenv("O3DX_NO_VOXEL_GRID")) return 1;
+  if (!vox || geom[7] != 1.0) return 1;
   const int vn[3] = {(int)geom[4], (int)geom[5], (int)geom[6]};
   const double vs = geom[3];
   GridLayout L = grid_layout(n, 4);
@@ -2298,7 +2293,6 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
       best = err;
     }
   }
-  if (const char* e = getenv("O3DX_VOXEL_GRID_B")) b = std::max(1, std::min(4, atoi(e)));  // tuning override
   if (b == 0) return 1;
   char* w = (char*)ws;
   GridBuild& G = *out;
@@ -2605,7 +2599,7 @@ static int nested_tiles(GridBuild& G, int64_t n, int kneed, double occ, const fl
   NestedWs w;
   nested_carve(ar, n, w);
   O3DX_ARENA_CHECK(ar);
-  const int t = env_int("O3DX_NESTED_T", (int)std::ceil(4.0 * occ));
+  const int t = (int)std::ceil(4.0 * occ);
   const int64_t nc = (int64_t)G.view.nx * G.view.ny * G.view.nz;
   KTimer kt("normals_nested", s);
   O3DX_HIP(hipMemsetAsync(w.tot, 0, 3 * sizeof(unsigned long long), s));
@@ -2616,9 +2610,7 @@ static int nested_tiles(GridBuild& G, int64_t n, int kneed, double occ, const fl
   hipLaunchKernelGGL(k_dense_points, dim3(gc), dim3(kBlock), 0, s, G.view, t, w.tot + 2);
   unsigned long long dense = 0;
   O3DX_TRY(read_back(&dense, w.tot + 2, sizeof(dense), s));
-  const int64_t minq = std::max<int64_t>(kNestedMinQueries, n / env_int("O3DX_NESTED_DIV", 32));
-  if (getenv("O3DX_NESTED_VERBOSE"))
-    fprintf(stderr, "nested: n=%lld points in dense cells=%llu (min %lld)\n", (long long)n, dense, (long long)minq);
+  const int64_t minq = std::max<int64_t>(kNestedMinQueries, n / 32);
   if ((int64_t)dense < minq) return 0;
   hipLaunchKernelGGL(k_nested_mark, dim3(gc), dim3(kBlock), 0, s, G.view, t, w.d1);
   hipLaunchKernelGGL(k_nested_cells, dim3(gc), dim3(kBlock), 0, s, G.view, w.d1, w.sub_cnt, w.tot);
@@ -2630,8 +2622,7 @@ static int nested_tiles(GridBuild& G, int64_t n, int kneed, double occ, const fl
   hipLaunchKernelGGL(k_nested_gather, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, G.view, w.d1, w.sub_cnt,
                      w.sub_off, w.sub_xyz, w.sub_id);
   GridBuild N;
-  const double occ2 = getenv("O3DX_NESTED_OCC") ? atof(getenv("O3DX_NESTED_OCC")) : occ;
-  O3DX_TRY(grid_build(w.sub_xyz, nsub, occ2, 0.0, w.gws, w.gws_bytes, s, &N, nullptr, nullptr, false, 4, false,
+  O3DX_TRY(grid_build(w.sub_xyz, nsub, occ, 0.0, w.gws, w.gws_bytes, s, &N, nullptr, nullptr, false, 4, false,
                       w.sub_id, 0.5 * (double)G.view.h));
   GridView& v = N.view;
   v.outer = G.view.pts;
@@ -2697,10 +2688,7 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
       const char* dbg_env = getenv("O3DX_TILE_DEBUG");
       const int dbg = dbg_env ? atoi(dbg_env) : 0;
       KTimer kt_tile("normals_tile", s);
-      if (kneed <= 32 && env_int("O3DX_TILE_DD", 0))  // A/B: the TwoSum accumulator (same bits)
-        hipLaunchKernelGGL((k_normals_knn_tile<32, MomAccDD>), dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view,
-                           chunks, kneed, prior, out, list1, lens, dbg);
-      else if (kneed <= 32)
+      if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_tile<32>, dim3((unsigned)nchunks), dim3(kTileQ), 0, s, G.view, chunks,
                            kneed, prior, out, list1, lens, dbg);
       else
@@ -2713,7 +2701,7 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
       const int s0 = tiles ? 2 : 1;
       KTimer kt_wave("normals_wave", s);
       Deferred df;
-      if (wl && env_int("O3DX_WAVE_DEFER", 1)) {
+      if (wl) {
         df.cap = defer_cap(n);
         df.mom = dmom;
         df.row = drow;

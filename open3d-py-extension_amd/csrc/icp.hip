@@ -439,7 +439,7 @@ __device__ __forceinline__ unsigned icp_xcd_block(unsigned b, unsigned nb) {
 // copies (acc[copy][2 kNS]).  mpos[j]
 // = the match's sorted target position (-1: none).  Integer sums: the same
 // bits for any split of the source over lanes, blocks or ranks.
-template <bool SORTED, bool ROWS, bool F64 = false>
+template <bool SORTED, bool F64 = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_icp_step(const void* __restrict__ src, int64_t ns, GridView g,
                                                      const float4* __restrict__ tnorm,
                                                      const IcpState* __restrict__ st, double radius,
@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     if (j < ns) {
       icp_source<SORTED, F64>(src, j, T, &px, &py, &pz);
       // the previous iteration's match as the starting bound (exact either way)
-      nn_search_dev<ROWS, true, F64>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
+      nn_search_dev<true, F64>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
       mpos[j] = pos;
     }
     const bool m = pos >= 0;
@@ -785,29 +785,20 @@ static int source_absmax(const void* src_, int64_t ns, bool sorted, AccWs& w, hi
 static void launch_step(const void* src, int64_t ns, bool sorted, const GridView& g, const float4* tn,
                         double radius, AccWs& w, hipStream_t s, int use_prior = 0) {
   const unsigned nb = step_blocks(ns);
-  // O3DX_ICP_SHELL=1: the Chebyshev shell walk (round 1-2 form) instead of the row walk
-  const bool shell = getenv("O3DX_ICP_SHELL") != nullptr;
   KTimer km("icp_match", s);
   if (g.pts64 && sorted)
-    hipLaunchKernelGGL((k_icp_step<true, true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius,
-                       w.mpos, use_prior, w.acc);
-  else if (g.pts64)
-    hipLaunchKernelGGL((k_icp_step<false, true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius,
-                       w.mpos, use_prior, w.acc);
-  else if (sorted && !shell)
     hipLaunchKernelGGL((k_icp_step<true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
+                       use_prior, w.acc);
+  else if (g.pts64)
+    hipLaunchKernelGGL((k_icp_step<false, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
                        use_prior, w.acc);
   else if (sorted)
     hipLaunchKernelGGL((k_icp_step<true, false>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
                        use_prior, w.acc);
-  else if (!shell)
-    hipLaunchKernelGGL((k_icp_step<false, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
-                       use_prior, w.acc);
   else
-    hipLaunchKernelGGL((k_icp_step<false, false>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius,
-                       w.mpos, use_prior, w.acc);
+    hipLaunchKernelGGL((k_icp_step<false, false>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
+                       use_prior, w.acc);
 }
-
 // correspondences of the last step into corr_out (pairs by original index)
 static int corr_of_last_step(const void* src, int64_t ns, bool sorted, const GridView& g, AccWs& w, hipStream_t s,
                              int32_t* corr_out, int64_t* ncorr) {
@@ -866,22 +857,14 @@ static int accumulate(const void* src, int64_t ns, bool sorted, const GridView& 
   return 0;
 }
 
-// grid occupancy / minimum cell for the 1-NN-within-radius search
-static double icp_min_h(double max_corr) {
-  if (const char* e = getenv("O3DX_ICP_MINH_DIV")) return max_corr / atof(e);  // tuning override
-  return max_corr / 16.0;
-}
+// grid occupancy / minimum cell for the 1-NN-within-radius search (round 2
+// sweeps: max_corr / 20, / 24, / 32 within +-3 % of / 16)
+static double icp_min_h(double max_corr) { return max_corr / 16.0; }
 // target grid cell capacity per point: a surface occupies few of the box's
 // cells, so a finer grid than the volume default keeps the candidates per
 // query low (the dense start table costs 8 B per cell)
-static int icp_cap_mult() {
-  if (const char* e = getenv("O3DX_ICP_CAP")) return std::max(1, atoi(e));
-  return 12;
-}
-static double icp_occ() {
-  if (const char* e = getenv("O3DX_ICP_OCC")) return atof(e);
-  return 2.0;
-}
+static int icp_cap_mult() { return 12; }
+static double icp_occ() { return 2.0; }
 
 }  // namespace o3dx
 

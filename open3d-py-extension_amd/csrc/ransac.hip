@@ -26,7 +26,6 @@
 namespace o3dx {
 
 constexpr int kPts = 16;
-constexpr int kHChunk = 1024;
 constexpr int kCountBlocksMax = 4096;
 
 struct P3 {
@@ -54,84 +53,6 @@ __device__ __forceinline__ double plane_dist64(const double* pl, double x, doubl
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// One block sweeps tiles of kBlock * kPts points against hypotheses
-// [h0, h0 + hc).  Points past n are NaN (every comparison false, no masks).
-// The next hypothesis' coefficients are loaded while the current one is
-// evaluated; distances of two points per packed FMA.
-__global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict__ xyz, int64_t n,
-                                                        const float4* __restrict__ pl32,
-                                                        const float4* __restrict__ band,
-                                                        const double* __restrict__ pl64, int H, int h0, int hc,
-                                                        double thr, int32_t* __restrict__ partial) {
-  static_assert(kPts % 2 == 0, "points are processed in pairs");
-  constexpr int kPairs = kPts / 2;
-  __shared__ int cnt[kHChunk];
-  for (int h = threadIdx.x; h < hc; h += kBlock) cnt[h] = 0;
-  __syncthreads();
-  const P3* p = reinterpret_cast<const P3*>(xyz);
-  const int64_t tile = (int64_t)kBlock * kPts;
-  const float qnan = __int_as_float(0x7fc00000);
-  for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {
-    f32x2 X[kPairs], Y[kPairs], Z[kPairs];
-#pragma unroll
-    for (int k = 0; k < kPairs; ++k) {
-      const int64_t i0 = base + (int64_t)(2 * k) * kBlock + threadIdx.x, i1 = i0 + kBlock;
-      const P3 a = i0 < n ? p[i0] : P3{qnan, qnan, qnan};
-      const P3 b = i1 < n ? p[i1] : P3{qnan, qnan, qnan};
-      X[k] = (f32x2){a.x, b.x};
-      Y[k] = (f32x2){a.y, b.y};
-      Z[k] = (f32x2){a.z, b.z};
-    }
-    float4 P = pl32[h0];
-    float4 B = band[h0];
-    for (int h = 0; h < hc; ++h) {
-      const int hn = (h + 1 < hc) ? h + 1 : h;
-      const float4 Pn = pl32[h0 + hn];
-      const float4 Bn = band[h0 + hn];
-      int wc = 0;
-      // ambiguity band [B.x, B.y) = mid B.z +- B.w (conservative): each lane
-      // keeps its closest |e - mid| (VALU), one ballot per hypothesis
-      float amb = INFINITY;
-      // all distances first (independent chains), then the tests
-      f32x2 D[kPairs];
-#pragma unroll
-      for (int k = 0; k < kPairs; ++k)
-        D[k] = __builtin_elementwise_fma(
-            (f32x2){P.x, P.x}, X[k],
-            __builtin_elementwise_fma((f32x2){P.y, P.y}, Y[k],
-                                      __builtin_elementwise_fma((f32x2){P.z, P.z}, Z[k], (f32x2){P.w, P.w})));
-      __builtin_amdgcn_sched_barrier(0);
-      float am[kPairs];
-#pragma unroll
-      for (int k = 0; k < kPairs; ++k) am[k] = fminf(fabsf(fabsf(D[k].x) - B.z), fabsf(fabsf(D[k].y) - B.z));
-#pragma unroll
-      for (int k = 0; k < kPairs; ++k)
-        wc += __popcll(__ballot(fabsf(D[k].x) < B.x)) + __popcll(__ballot(fabsf(D[k].y) < B.x));
-#pragma unroll
-      for (int k = 0; k < kPairs; ++k) amb = fminf(amb, am[k]);
-      if (__ballot(amb <= B.w)) {  // rare: re-decide band points in float64, Open3D's order
-        const double* pl = pl64 + 4 * (h0 + h);
-#pragma unroll
-        for (int k = 0; k < kPairs; ++k) {
-          const f32x2 d = __builtin_elementwise_fma(
-              (f32x2){P.x, P.x}, X[k],
-              __builtin_elementwise_fma((f32x2){P.y, P.y}, Y[k],
-                                        __builtin_elementwise_fma((f32x2){P.z, P.z}, Z[k], (f32x2){P.w, P.w})));
-          const float e0 = fabsf(d.x), e1 = fabsf(d.y);
-          const bool x0 = !(e0 < B.x) && e0 < B.y && plane_dist64(pl, X[k].x, Y[k].x, Z[k].x) < thr;
-          const bool x1 = !(e1 < B.x) && e1 < B.y && plane_dist64(pl, X[k].y, Y[k].y, Z[k].y) < thr;
-          wc += __popcll(__ballot(x0)) + __popcll(__ballot(x1));
-        }
-      }
-      if (lane_id() == 0 && wc) atomicAdd(&cnt[h], wc);
-      P = Pn;
-      B = Bn;
-    }
-  }
-  __syncthreads();
-  for (int h = threadIdx.x; h < hc; h += kBlock) partial[(int64_t)blockIdx.x * H + h0 + h] = cnt[h];
-}
-
 // ---------------------------------------------------------------------------
 // The counts, one sweep over all hypotheses.  A wave holds a batch of 64 PL
 // points (PL per lane, packed pairs) and HC hypotheses (planes read out of
@@ -150,8 +71,8 @@ __global__ void __launch_bounds__(kBlock) k_plane_count(const float* __restrict_
 // the waves sharing a batch range (all hypothesis chunks) run on one XCD
 // (its L2 serves the re-reads of the points).
 // Shapes: HC hypotheses per wave x PL points per lane per batch (batch =
-// 64 PL points).  Default 32 x 16; O3DX_RANSAC_SHAPE=HCxPL picks another
-// instantiated shape (tuning).
+// 64 PL points): 32 x 16 at 6 waves per SIMD, and for the exact rounds'
+// few hypotheses 16 x 16 / 8 x 16 at 8 waves.
 constexpr int kCountWaves = 2048;      // batch ranges (waves per hypothesis chunk)
 constexpr int kMinBatchPts = 64 * 8;   // smallest instantiated batch (bitmap sizing)
 constexpr int kMinHC = 8;              // smallest instantiated chunk (bitmap sizing)
@@ -281,15 +202,8 @@ __device__ __forceinline__ void plane_count_body(const float* __restrict__ xyz, 
   if (lane < kHC && h0 + lane < H) partial[(int64_t)wp * H + h0 + lane] = mine;
 }
 
-// W > 0: the register budget of W waves per SIMD (occupancy for the
-// dependent fma -> compare -> popcount chains)
-template <int kHC, int kPL, int kPF>
-__global__ void __launch_bounds__(kBlock) k_plane_count_v(const float* __restrict__ xyz, int64_t n,
-                                                          const float4* __restrict__ pl32, int H, float Llo,
-                                                          uint32_t wbits, int64_t bpw, int nwp, int ncg,
-                                                          int32_t* __restrict__ partial, uint32_t* __restrict__ flags) {
-  plane_count_body<kHC, kPL, kPF>(xyz, n, pl32, H, Llo, wbits, bpw, nwp, ncg, partial, flags);
-}
+// the register budget of 8 / 6 waves per SIMD (occupancy for the dependent
+// fma -> compare -> popcount chains; measured r03: 2.4 ms at 4 waves, 1.5 at 6)
 template <int kHC, int kPL, int kPF>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_plane_count_w8(const float* __restrict__ xyz, int64_t n, const float4* __restrict__ pl32, int H, float Llo,
@@ -365,12 +279,6 @@ k_plane_upper(const float* __restrict__ xyz, int64_t n, const float4* __restrict
               int64_t bpw, int nwp, int ncg, int32_t* __restrict__ partial) {
   plane_upper_body<kHC, kPL>(xyz, n, pl32, H, hi, bpw, nwp, ncg, partial);
 }
-template <int kHC, int kPL>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8)))
-k_plane_upper_w8(const float* __restrict__ xyz, int64_t n, const float4* __restrict__ pl32, int H, float hi,
-                 int64_t bpw, int nwp, int ncg, int32_t* __restrict__ partial) {
-  plane_upper_body<kHC, kPL>(xyz, n, pl32, H, hi, bpw, nwp, ncg, partial);
-}
 
 // Upper bounds on the matrix cores.  The distances of 32 points to 32
 // hypotheses are v_mfma_f32_32x32x16_bf16 products of bf16 parts (round to
@@ -433,10 +341,8 @@ __device__ __forceinline__ void point_frags(float x, float y, float z, int h, bf
   const float rx = x - bf16_f(xh), ry = y - bf16_f(yh), rz = z - bf16_f(zh);  // exact
   const uint32_t xm = bf16_rne_bits(rx), ym = bf16_rne_bits(ry), zm = bf16_rne_bits(rz);
   const bool h0 = h == 0;
-  if constexpr (!TIGHT) {
-    // h0: xh yh zh 1 | xm ym zm 1   h1: xh yh zh 0 | 0 0 0 0
-    A[0] = frag8(xh, yh, zh, h0 ? one : 0, h0 ? xm : 0, h0 ? ym : 0, h0 ? zm : 0, h0 ? one : 0);
-  } else {
+  static_assert(TIGHT, "the one-MFMA form was removed in round 5");
+  {
     const uint32_t xl = bf16_rne_bits(rx - bf16_f(xm)), yl = bf16_rne_bits(ry - bf16_f(ym)),
                    zl = bf16_rne_bits(rz - bf16_f(zm));
     // MFMA 1  h0: xh yh zh 1 | xh yh zh 1     h1: xm ym zm 1 | xm ym zm 0
@@ -726,9 +632,6 @@ __global__ void __launch_bounds__(kCBinBlock) k_cbin_local(const float4* __restr
   }
 }
 
-// v_writelane_b32 (lane `lane` of `old` set to val; val and lane uniform)
-__device__ int o3dx_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
-
 // all-lanes reduction of a float (EXEC full): DPP within 16-lane rows
 // (l ^ 1, l ^ 2, half-row mirror, row_ror:8), then row and half swaps
 template <int CTRL>
@@ -756,26 +659,22 @@ __device__ __forceinline__ float wave_max_f(float v) {
 // grid: (blocks over chunks of kCullCS points, hypothesis rows of kCullHG);
 // pts: the Morton-ordered points, padded with NaN rows to a whole chunk;
 // pl32 [H] float32 planes, pl64 [H] the float64 planes, lims [H] = (hi, limc,
-// lo, -) (degenerate: -1, -inf, -1); partial [block x][H] int32 counts —
-// EXACT counts of Open3D's predicate.  Per chunk a wave takes the box of its
-// finite points, tests the hypotheses 64 at a time (lane = hypothesis,
-// coefficients from LDS) and lists the survivors in LDS; every 64 listed
-// survivors (and the rest at the end) are counted with lane = hypothesis and
-// the chunk's points read by scalar loads (wave-uniform addresses): three
-// fmas, two compares and an add per (point, hypothesis).  |d32| < lo is an
-// inlier and |d32| >= hi is not (k_plane_count's band, lo / hi = thr -/+ g_h
-// rounded outwards); a hypothesis with a point in between re-counts the chunk
-// in float64 as Open3D evaluates it (rare: the band is ~1e-7 relative).
-template <bool EXACT>
+// lo, -) (degenerate: -1, -inf, -1); partial [block x][H] int32 upper
+// bounds of the counts.  Per chunk a wave takes the box of its finite points,
+// tests the hypotheses 64 at a time (lane = hypothesis, coefficients from
+// LDS) and lists the survivors in LDS; every 64 listed survivors (and the
+// rest at the end) are counted with lane = hypothesis and the chunk's points
+// read by scalar loads (wave-uniform addresses): three fmas, a compare and an
+// add per (point, hypothesis), |d32| < hi.  (Round 4 measured an exact form —
+// a second compare against lo and a float64 re-count of band chunks — 0.13
+// ms slower than the exact round it would replace; removed in round 5.)
 __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* __restrict__ pts, int64_t n,
                                                                  const float4* __restrict__ pl32,
-                                                                 const double* __restrict__ pl64,
-                                                                 const float4* __restrict__ lims, int H, double thr,
+                                                                 const float4* __restrict__ lims, int H,
                                                                  int32_t* __restrict__ partial) {
   constexpr int kW = kCullBlock / 64, CS = kCullCS;
   __shared__ float4 lpl[kCullHG];
   __shared__ float2 llim[kCullHG];               // (hi, limc)
-  __shared__ float llo[EXACT ? kCullHG : 1];     // lo (the exact form)
   __shared__ int32_t lcnt[kCullHG];
   __shared__ uint16_t lst[kW][128];
   const int h0 = blockIdx.y * kCullHG, hn = min(kCullHG, H - h0);
@@ -783,7 +682,6 @@ __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* _
     lpl[t] = pl32[h0 + t];
     const float4 l = lims[h0 + t];
     llim[t] = make_float2(l.x, l.y);
-    if constexpr (EXACT) llo[t] = l.z;
     lcnt[t] = 0;
   }
   __syncthreads();
@@ -836,9 +734,7 @@ __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* _
       const int h = act ? (int)lst[wv][lane] : 0;
       const float4 p = lpl[h];
       const float hi = act ? llim[h].x : -1.0f;
-      float lo = -1.0f;
-      if constexpr (EXACT) lo = act ? llo[h] : -1.0f;
-      int cnt = 0, chi = 0;  // |d32| < lo and |d32| < hi: they differ when a point is in the band
+      int chi = 0;  // |d32| < hi
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
       for (int k0 = 0; k0 < CS; k0 += kCullPB) {
         float4 q[kCullPB];
@@ -847,30 +743,10 @@ __global__ void __launch_bounds__(kCullBlock) k_plane_upper_cull(const float4* _
 #pragma unroll
         for (int j = 0; j < kCullPB; ++j) {
           const float ad = fabsf(fmaf(p.x, q[j].x, fmaf(p.y, q[j].y, fmaf(p.z, q[j].z, p.w))));
-          if constexpr (EXACT) cnt += ad < lo ? 1 : 0;
           chi += ad < hi ? 1 : 0;
         }
       }
-      if constexpr (!EXACT) {  // the upper bound: |d32| < hi
-        if (act && chi) atomicAdd(&lcnt[h], chi);
-        return;
-      }
-      const bool band = chi != cnt;
-      // rare: a hypothesis with a point in the band re-counts the chunk with
-      // the float64 predicate, lane = point (the chunk is in registers)
-      uint64_t bm = __ballot(band);
-      while (bm) {
-        const int b = __builtin_ctzll(bm);
-        bm &= bm - 1;
-        const int hb = __builtin_amdgcn_readlane(h, b);
-        const double* q64 = pl64 + 4 * (int64_t)(h0 + hb);  // wave-uniform: scalar loads
-        const double pd[4] = {q64[0], q64[1], q64[2], q64[3]};
-        int ex = 0;
-#pragma unroll
-        for (int j = 0; j < CS / 64; ++j) ex += __popcll(__ballot(plane_dist64(pd, cur[j].x, cur[j].y, cur[j].z) < thr));
-        cnt = o3dx_writelane(ex, b, cnt);
-      }
-      if (act && cnt) atomicAdd(&lcnt[h], cnt);
+      if (act && chi) atomicAdd(&lcnt[h], chi);
     };
     int nl = 0;  // wave-uniform list length (< 64 between groups)
     for (int g0 = 0; g0 < hn; g0 += 64) {
@@ -1309,7 +1185,6 @@ struct CountWs {
   int32_t* bscan;
   int bits;
   bool binned;        // sorted holds this call's points
-  bool exact_counts;  // the last run_count_upper counted exactly (the culled sweep)
 };
 
 // grid bits per axis of the culled sweep's Morton order: ~8 points per cell
@@ -1344,7 +1219,6 @@ static size_t count_carve(Arena& ar, int64_t n, int H, CountWs* w) {
   w->bstart = ar.take<int32_t>((size_t)nbh + 1);
   w->bscan = ar.take<int32_t>(scan_workspace_ints(nbh + 1));
   w->binned = false;
-  w->exact_counts = false;
   return ar.used;
 }
 
@@ -1393,7 +1267,7 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
                odg = w.degen - base;
   const size_t nch = ((size_t)H + 31) / 32, omf = reinterpret_cast<uint8_t*>(w.mfrag) - base,
                ohi = reinterpret_cast<uint8_t*>(w.mhi) - base;
-  const bool frags = mfma == 1 || mfma == 2;
+  const bool frags = mfma == 2;
   st.assign(frags ? ohi + nch * 32 * 4 : odg + H, 0);  // the caller keeps it alive until the stream is synchronised
   std::memcpy(st.data(), p32.data(), H * sizeof(float4));
   std::memcpy(st.data() + ob, bnd.data(), H * sizeof(float4));
@@ -1401,13 +1275,11 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
   std::memcpy(st.data() + odg, dg.data(), H);
   if (frags) {
     // k_plane_upper_mfma's B operand: hypothesis j is column j % 32 of chunk
-    // j / 32; bf16 parts (round to nearest) of the float64 plane.  One MFMA:
-    // lane r (ah bh ch dh | ah bh ch dl), lane r + 32 (al bl cl 0 | 0 0 0 0).
-    // Two MFMAs (tight): MFMA 1 lane r (ah bh ch dh | am bm cm dm), lane r + 32
-    // (ah bh ch dl | am bm cm 0); MFMA 2 lane r (al bl cl 0 | ah bh ch 0), lane
-    // r + 32 zero.  ("m" is the second part, "l" the third.)
-    const bool tight = mfma == 2;
-    const int nf = tight ? 2 : 1;
+    // j / 32; bf16 parts (round to nearest) of the float64 plane.  MFMA 1 lane
+    // r (ah bh ch dh | am bm cm dm), lane r + 32 (ah bh ch dl | am bm cm 0);
+    // MFMA 2 lane r (al bl cl 0 | ah bh ch 0), lane r + 32 zero.  ("m" is the
+    // second part, "l" the third.)
+    const int nf = 2;
     uint16_t* fr = reinterpret_cast<uint16_t*>(st.data() + omf);
     float* hv = reinterpret_cast<float*>(st.data() + ohi);
     for (size_t j = 0; j < nch * 32; ++j) hv[j] = -1.0f;
@@ -1429,20 +1301,15 @@ static void upload_planes(const double* planes, int H, const double absmax[3], d
         std::memcpy(fr + (((size_t)(j / 32) * 64 + lane) * nf + f) * 8, v, 16);
       };
       const int r = j % 32;
-      if (!tight) {
-        put(r, 0, {h_[0], h_[1], h_[2], h_[3], h_[0], h_[1], h_[2], m_[3]});
-        put(r + 32, 0, {m_[0], m_[1], m_[2], 0, 0, 0, 0, 0});
-      } else {
-        put(r, 0, {h_[0], h_[1], h_[2], h_[3], m_[0], m_[1], m_[2], m_[3]});
-        put(r + 32, 0, {h_[0], h_[1], h_[2], l_[3], m_[0], m_[1], m_[2], 0});
-        put(r, 1, {l_[0], l_[1], l_[2], 0, h_[0], h_[1], h_[2], 0});
-        put(r + 32, 1, {0, 0, 0, 0, 0, 0, 0, 0});
-      }
+      put(r, 0, {h_[0], h_[1], h_[2], h_[3], m_[0], m_[1], m_[2], m_[3]});
+      put(r + 32, 0, {h_[0], h_[1], h_[2], l_[3], m_[0], m_[1], m_[2], 0});
+      put(r, 1, {l_[0], l_[1], l_[2], 0, h_[0], h_[1], h_[2], 0});
+      put(r + 32, 1, {0, 0, 0, 0, 0, 0, 0, 0});
       const double S = std::fabs(pl[0]) * absmax[0] + std::fabs(pl[1]) * absmax[1] + std::fabs(pl[2]) * absmax[2] +
                        std::fabs(pl[3]);
       // O3DX_RANSAC_BAND_OFF (test hook, tests/test_gpu_kernels.py): count
       // |d_mfma| < thr itself, so a test can bound the sweep's own error
-      const double band = band_off ? 0.0 : std::ldexp(1.0, tight ? MfmaShape<true>::kBoundExp : MfmaShape<false>::kBoundExp) * S;
+      const double band = band_off ? 0.0 : std::ldexp(1.0, MfmaShape<true>::kBoundExp) * S;
       const double lim = thr + band + 1e-30;
       float f = (float)lim;
       if ((double)f < lim) f = std::nextafter(f, INFINITY);
@@ -1494,9 +1361,8 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
   int rc;
   upload_planes(planes, H, absmax, thr, w, p32, bnd, dg, st, s, &rc);
   if (rc) return rc;
-  int nb = count_blocks(n);
   KTimer kt("plane_count", s);
-  if (!getenv("O3DX_RANSAC_VALU")) {
+  {
     // one window for all hypotheses: the union of their float32 windows
     // (degenerate and non-finite planes are never counted: left out)
     float lo = -1.0f, hi = -1.0f;
@@ -1521,8 +1387,7 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
     // the default: every point against every hypothesis on the VALU
     // measured: 6 waves/SIMD fastest (r03); re-counts of a few hypotheses
     // (segment_plane's exact rounds) take a narrower chunk
-    int hc = H <= 8 ? 8 : H <= 16 ? 16 : 32, pl = 16, pf = 0, wv = H <= 16 ? 8 : 6;
-    if (const char* e = getenv("O3DX_RANSAC_SHAPE")) sscanf(e, "%dx%dx%dx%d", &hc, &pl, &pf, &wv);
+    const int hc = H <= 8 ? 8 : H <= 16 ? 16 : 32, pl = 16;
     int nwp;
     int64_t bpw;
     const int nchunks = (H + hc - 1) / hc;
@@ -1534,27 +1399,19 @@ static int run_count(const float* xyz, int64_t n, const double* planes, int H, d
       hipLaunchKernelGGL(kern, dim3((unsigned)(nwp * ncg)), dim3(kBlock), 0, s, xyz, n, w.pl32, H, Llo, wbits, bpw,
                          nwp, ncg, w.partial, w.flags);
     };
-#define O3DX_COUNT(HC, PL, PF)                                                                                     \
-  if (hc == HC && pl == PL && pf == PF) {                                                                          \
-    if (wv == 8) kcount(k_plane_count_w8<HC, PL, PF>);                                                             \
-    else if (wv == 6) kcount(k_plane_count_w6<HC, PL, PF>);                                                        \
-    else kcount(k_plane_count_v<HC, PL, PF>);                                                                      \
-    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));                                          \
-    hipLaunchKernelGGL((k_plane_fixup<HC, PL>), dim3(fgrid), dim3(kBlock), 0, s, xyz, n, w.pl32, w.pl64, H, thr,   \
-                       Llo, wbits, w.flags, nwords, w.counts);                                                      \
-  } else
-    O3DX_COUNT(32, 16, 0) O3DX_COUNT(32, 16, 1) O3DX_COUNT(32, 8, 0) O3DX_COUNT(16, 16, 0) O3DX_COUNT(16, 16, 1)
-    O3DX_COUNT(32, 24, 0) O3DX_COUNT(8, 16, 0)
-    return fail(O3DX_EINVAL,
-                "O3DX_RANSAC_SHAPE: instantiated shapes are 32x16x{0,1}, 32x8x0, 16x16x{0,1}, 32x24x0, 8x16x0");
-#undef O3DX_COUNT
-  } else {  // the ballot/popcount kernel with per-hypothesis windows (A/B reference)
-    for (int h0 = 0; h0 < H; h0 += kHChunk) {
-      int hc = std::min(kHChunk, H - h0);
-      hipLaunchKernelGGL(k_plane_count, dim3(nb), dim3(kBlock), 0, s, xyz, n, w.pl32, w.band, w.pl64, H, h0, hc, thr,
-                         w.partial);
-    }
-    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nb, H, w.counts, s));
+    if (hc == 32) kcount(k_plane_count_w6<32, 16, 0>);
+    else if (hc == 16) kcount(k_plane_count_w8<16, 16, 0>);
+    else kcount(k_plane_count_w8<8, 16, 0>);
+    O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));
+    if (hc == 32)
+      hipLaunchKernelGGL((k_plane_fixup<32, 16>), dim3(fgrid), dim3(kBlock), 0, s, xyz, n, w.pl32, w.pl64, H, thr,
+                         Llo, wbits, w.flags, nwords, w.counts);
+    else if (hc == 16)
+      hipLaunchKernelGGL((k_plane_fixup<16, 16>), dim3(fgrid), dim3(kBlock), 0, s, xyz, n, w.pl32, w.pl64, H, thr,
+                         Llo, wbits, w.flags, nwords, w.counts);
+    else
+      hipLaunchKernelGGL((k_plane_fixup<8, 16>), dim3(fgrid), dim3(kBlock), 0, s, xyz, n, w.pl32, w.pl64, H, thr,
+                         Llo, wbits, w.flags, nwords, w.counts);
   }
   hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
   kt.stop();
@@ -1585,7 +1442,7 @@ static int bin_points(const float* xyz, int64_t n, const double* mm_dev, CountWs
 // The culled sweep over w.sorted with the limits already in w.pl32 / w.band /
 // w.degen (host upload or k_ransac_setup): per-hypothesis counts (degenerate
 // -1) into counts_dev, no host wait.
-static int launch_cull(int64_t n, int H, double thr, CountWs& w, bool exact, hipStream_t s, int64_t* counts_dev) {
+static int launch_cull(int64_t n, int H, CountWs& w, hipStream_t s, int64_t* counts_dev) {
   const int64_t nchunk = (n + kCullCS - 1) / kCullCS;
   const int64_t rows = std::max<int64_t>(1, std::min<int64_t>((int64_t)(w.partial_ints / std::max(H, 1)), 2048));
   // one resident wave per chunk stream: 5 blocks per CU (LDS ~30 KB each)
@@ -1593,20 +1450,20 @@ static int launch_cull(int64_t n, int H, double thr, CountWs& w, bool exact, hip
   const unsigned gx = (unsigned)std::min<int64_t>(std::min<int64_t>(rows, kCullResident),
                                                   (nchunk + per_block - 1) / per_block);
   const unsigned gy = (unsigned)((H + kCullHG - 1) / kCullHG);
-  hipLaunchKernelGGL(exact ? k_plane_upper_cull<true> : k_plane_upper_cull<false>, dim3(gx, gy), dim3(kCullBlock), 0,
-                     s, w.sorted, n, w.pl32, w.pl64, w.band, H, thr, w.partial);
+  hipLaunchKernelGGL(k_plane_upper_cull, dim3(gx, gy), dim3(kCullBlock), 0, s, w.sorted, n, w.pl32, w.band, H,
+                     w.partial);
   O3DX_TRY(reduce_columns_i32_to_i64(w.partial, gx, H, counts_dev, s));
   hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, counts_dev);
   O3DX_HIP(hipGetLastError());
   return 0;
 }
 
-// the upper sweep a call takes: 3 culled, 2 / 1 matrix cores, 0 VALU
+// the upper sweep a call takes: 3 culled, 2 matrix cores, 0 VALU
+// (O3DX_RANSAC_UPPER=cull / mfma2 / valu: test hook forcing one of them)
 static int upper_mode(int64_t n, double smax, double thr) {
   if (const char* ue = getenv("O3DX_RANSAC_UPPER")) {
     if (std::strcmp(ue, "cull") == 0) return 3;
     if (std::strcmp(ue, "mfma2") == 0) return 2;
-    if (std::strcmp(ue, "mfma") == 0) return 1;
     return 0;
   }
   if (n >= kCullMinN) return 3;
@@ -1632,8 +1489,7 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
   // The matrix-core sweep (two MFMAs, band thr + 2^-17 S_h) is wider than the
   // VALU sweep's (thr + 6 2^-24 S_h): it is used while its band adds at most
   // 2 % to thr, so the bounds stay about as tight and the replay consults
-  // about as many hypotheses.  O3DX_RANSAC_UPPER=HCxPLxW forces the VALU
-  // sweep, =mfma2 the two-MFMA and =mfma the one-MFMA form (band 2^-14 S_h).
+  // about as many hypotheses.
   double smax = 0.0;
   for (int h = 0; h < H; ++h) {
     const double* pl = planes + 4 * h;
@@ -1646,7 +1502,6 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
   // non-finite bounds) take the dense sweeps
   if (mfma == 3 && !(6.0 * std::ldexp(1.0, -24) * smax + std::ldexp(1.0, -20) * thr < 0.5 * thr))
     mfma = std::ldexp(1.0, MfmaShape<true>::kBoundExp) * smax <= 0.02 * thr ? 2 : 0;
-  w.exact_counts = false;
   if (mfma == 3 && !w.binned) {
     if (!mm_ready) O3DX_TRY(aabb_device(xyz, n, mm_dev, aabb_ws, s));
     O3DX_TRY(bin_points(xyz, n, mm_dev, w, s));
@@ -1655,10 +1510,7 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
   if (rc) return rc;
   KTimer kt("plane_count_upper", s);
   if (mfma == 3) {
-    // O3DX_RANSAC_CULL_EXACT (tests, A/B): the exact form over every hypothesis
-    const bool exact = getenv("O3DX_RANSAC_CULL_EXACT") != nullptr;
-    w.exact_counts = exact;
-    O3DX_TRY(launch_cull(n, H, thr, w, exact, s, w.counts));
+    O3DX_TRY(launch_cull(n, H, w, s, w.counts));
     kt.stop();
     ub.resize(H);
     O3DX_TRY(read_back(ub.data(), w.counts, H * sizeof(int64_t), s));
@@ -1676,10 +1528,7 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
       hipLaunchKernelGGL(kern, dim3(gx, ngy), dim3(kBlock), 0, s, xyz, n, w.mfrag, w.mhi, nch, H, bpb, w.partial);
       return gx;
     };
-    const unsigned gx = mfma == 2 ? launch_mfma(k_plane_upper_mfma<true>, MfmaShape<true>::kTiles,
-                                                MfmaShape<true>::kChunks)
-                                  : launch_mfma(k_plane_upper_mfma<false>, MfmaShape<false>::kTiles,
-                                                MfmaShape<false>::kChunks);
+    const unsigned gx = launch_mfma(k_plane_upper_mfma<true>, MfmaShape<true>::kTiles, MfmaShape<true>::kChunks);
     O3DX_TRY(reduce_columns_i32_to_i64(w.partial, gx, H, w.counts, s));
     hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
     kt.stop();
@@ -1692,8 +1541,7 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
   float hi = (float)hmax;
   if ((double)hi < hmax) hi = std::nextafter(hi, INFINITY);
   if (hmax < 0) hi = -1.0f;
-  int hc = 32, pl = 16, wv = 6;
-  if (const char* e = getenv("O3DX_RANSAC_UPPER")) sscanf(e, "%dx%dx%d", &hc, &pl, &wv);
+  constexpr int hc = 32, pl = 16;
   int nwp;
   int64_t bpw;
   const int nchunks = (H + hc - 1) / hc;
@@ -1703,11 +1551,7 @@ static int run_count_upper(const float* xyz, int64_t n, const double* planes, in
     hipLaunchKernelGGL(kern, dim3((unsigned)(nwp * ncg)), dim3(kBlock), 0, s, xyz, n, w.pl32, H, hi, bpw, nwp, ncg,
                        w.partial);
   };
-  if (hc == 32 && pl == 16 && wv == 6) launch(k_plane_upper<32, 16>);
-  else if (hc == 32 && pl == 16 && wv == 8) launch(k_plane_upper_w8<32, 16>);
-  else if (hc == 16 && pl == 16 && wv == 8) launch(k_plane_upper_w8<16, 16>);
-  else if (hc == 32 && pl == 8 && wv == 8) launch(k_plane_upper_w8<32, 8>);
-  else return fail(O3DX_EINVAL, "O3DX_RANSAC_UPPER: instantiated shapes are 32x16x6, 32x16x8, 16x16x8, 32x8x8");
+  launch(k_plane_upper<hc, pl>);
   O3DX_TRY(reduce_columns_i32_to_i64(w.partial, nwp, H, w.counts, s));
   hipLaunchKernelGGL(k_mark_degenerate, dim3((H + 255) / 256), dim3(256), 0, s, w.degen, H, w.counts);
   kt.stop();
@@ -2281,7 +2125,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     // the sweep's own tables (pl64 is read only by the exact form): the upload block's
     {
       KTimer kt("plane_count_upper", s);
-      O3DX_TRY(launch_cull(n, H, thr, w.cw, false, s, rb_counts));
+      O3DX_TRY(launch_cull(n, H, w.cw, s, rb_counts));
     }
     std::vector<char> rb(40 * (size_t)H + 6 * sizeof(double));
     O3DX_TRY(read_back(rb.data(), w.rb, rb.size(), s));
@@ -2291,7 +2135,6 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     double mmh[6];
     std::memcpy(mmh, rb.data() + 40 * (size_t)H, sizeof(mmh));
     for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(mmh[a]), std::fabs(mmh[3 + a]));
-    w.cw.exact_counts = false;
     // run_count_upper's guard on the culled sweep, replayed on the returned
     // bounds: a threshold tiny against the coordinates leaves the culled
     // bounds loose (valid, but the replay would then count many hypotheses
@@ -2333,7 +2176,7 @@ extern "C" int o3dx_segment_plane(const float* xyz, int64_t n, double thr, int r
     // upper bounds for all, exact counts for the hypotheses the replay consults
     if (!device_setup)
       O3DX_TRY(run_count_upper(xyz, n, planes.data(), H, thr, w.cw, w.aabb, w.mm, s, counts, absmax, true));
-    std::vector<uint8_t> known(H, w.cw.exact_counts ? 1 : 0);  // the culled sweep's counts are exact
+    std::vector<uint8_t> known(H, 0);
     std::vector<double> sub;
     std::vector<int64_t> ec;
     for (;;) {

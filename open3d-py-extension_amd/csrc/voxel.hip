@@ -1012,14 +1012,15 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     return 0;
   };
   // one-pass binning allowed (the plan decides whether it applies)
-  const int allow_fused = !getenv("O3DX_VOXEL_TWOPASS") && !getenv("O3DX_VOXEL_PLAIN") ? 1 : 0;
+  // O3DX_VOXEL_TWOPASS (tests): the count + scatter path, the one-pass binning's fall-back
+  const int allow_fused = !getenv("O3DX_VOXEL_TWOPASS") ? 1 : 0;
   bool pre_launched = false;
   if (!min_bound_host || !max_bound_host) {
     double mm[6];
     O3DX_TRY(aabb_begin(xyz, n, w.aabb, s, ZeroSpan{reinterpret_cast<uint8_t*>(w.count), 8 * sizeof(int64_t)},
                         ZeroSpan{reinterpret_cast<uint8_t*>(w.boff), (size_t)kMaxBuckets * kTotStride * sizeof(int32_t)},
                         ZeroSpan{w.flags, (size_t)n}, extra_zero));
-    if (!min_bound_host && !max_bound_host && allow_fused && n > 0 && !getenv("O3DX_VOXEL_NOPRE")) {
+    if (!min_bound_host && !max_bound_host && allow_fused && n > 0) {
       // the binning starts on the device's own plan while the host waits for
       // the bounds (the host replays the same plan below)
       hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, aabb_mailbox_dev(), voxel_size, n, allow_fused,
@@ -1088,7 +1089,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     int64_t nslots;
     if (attempt > 0) O3DX_TRY(clears());
     Bricks bricks = dense ? plan_bricks(g.nx, g.ny, g.nz) : Bricks{};
-    if (dense && bricks.nb > 0 && !getenv("O3DX_VOXEL_PLAIN")) {
+    if (dense && bricks.nb > 0) {
       nslots = (int64_t)nvox;
       const unsigned nblk = (unsigned)((n + kBinChunk - 1) / kBinChunk);
       KTimer kt("voxel_assign", s);

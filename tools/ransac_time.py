@@ -1,8 +1,9 @@
 """GPU timing of the RANSAC count kernels at C3 (10M points x 1000 hypotheses).
 
-Each variant (env switches read per call by ransac.hip run_count) is timed
-with the library's own HIP-event timer "plane_count" over a few calls and
-checked equal to the first variant's counts.
+The exact count is timed with the library's own HIP-event timer
+"plane_count" over a few calls; each upper-bound form of segment_plane's
+sweep (O3DX_RANSAC_UPPER, read per call by ransac.hip) is timed and checked
+to bound the exact counts.
 Usage (GPU box): python tools/ransac_time.py [reps]
 """
 import json
@@ -16,11 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "open3d-py-extension_amd"))
 from open3dpypro import _native as N, ops, synthetic as S  # noqa: E402
 
-if os.environ.get("O3DX_LIB_CMP"):  # A/B: a library built from an earlier ransac.hip
-    N.LIB_PATH = os.environ["O3DX_LIB_CMP"]
-
-VARIANTS = [("s32x16x0x6", {}), ("s32x16x0x0", {"O3DX_RANSAC_SHAPE": "32x16x0x0"}),
-            ("s16x16x0x8", {"O3DX_RANSAC_SHAPE": "16x16x0x8"}), ("ballot_legacy", {"O3DX_RANSAC_VALU": "1"})]
+VARIANTS = [("count", {})]
 
 
 def main():
@@ -38,8 +35,6 @@ def main():
     ref = None
     out = {}
     for name, env in variants:
-        for k in ("O3DX_RANSAC_VALU", "O3DX_RANSAC_SHAPE"):
-            os.environ.pop(k, None)
         os.environ.update(env)
         got = ops.plane_count(x, planes, 0.01)  # warm-up
         N.set_kernel_timing(True)
@@ -55,8 +50,8 @@ def main():
                      "pairs_per_s": n * H / (ms / max(cnt, 1) * 1e-3)}
         print(json.dumps({name: out[name]}), flush=True)
     # the upper-bound count (segment_plane's sweep) and the whole segment_plane
-    for name in (os.environ.get("UPPER", "mfma2,mfma,32x16x6")).split(","):
-        os.environ["O3DX_RANSAC_UPPER"] = name  # mfma: k_plane_upper_mfma
+    for name in (os.environ.get("UPPER", "cull,mfma2,valu")).split(","):
+        os.environ["O3DX_RANSAC_UPPER"] = name
         ub = ops.plane_count_upper(x, planes, 0.01)
         N.set_kernel_timing(True)
         N.reset_kernel_timing()
