@@ -231,8 +231,6 @@ void timing_release(hipEvent_t e);   // back to the pool
 int host_wait(hipStream_t s);
 // Device -> host copy of a small result, then host_wait.
 int read_back(void* dst_host, const void* src_dev, size_t bytes, hipStream_t s);
-int read_back_begin(const void* src_dev, size_t bytes, hipStream_t s);  // <= 64 KB, one pending per thread
-int read_back_end(void* dst_host, size_t bytes);
 struct KTimer {
   const char* name;
   hipStream_t s;
@@ -290,9 +288,155 @@ int voxel_down_sample_hooked(const float* xyz, int64_t n, const double* min_boun
                              double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, float* voxel_pts,
                              int64_t voxel_cells, double* geom, void* ws, size_t ws_bytes, void* stream,
                              VoxelHook hook, void* ctx, ZeroSpan extra_zero = {});
+// A few words straight to the host: one kernel thread stores them into mapped
+// pinned memory followed by a sequence number the host polls (no copy kernel
+// in the stream, no event).  post_prepare takes the next sequence number of
+// this host thread's post box; post_wait polls it (falling back to a stream
+// wait) and copies the words out.
+struct HostPost {
+  uint64_t* words = nullptr;  // device view of the mapped words (<= kPostWords)
+  volatile uint64_t* seq_word = nullptr;
+  uint64_t seq = 0;
+};
+constexpr int kPostWords = 8;
+int post_prepare(HostPost* p);
+int post_wait(const HostPost& p, void* dst, size_t bytes, hipStream_t s);
+__device__ __forceinline__ void post_publish(const HostPost& p, const int64_t* src, int nwords) {
+  for (int i = 0; i < nwords; ++i) p.words[i] = (uint64_t)src[i];
+  __threadfence_system();
+  *p.seq_word = p.seq;
+}
+
 int compact_flags_scan(const uint8_t* flags, int64_t n, int64_t* count_dev, int32_t* tmp, hipStream_t s);
+// post (nullable): count_dev[0 .. post_words) is published to the host once
+// the total is known (the earlier words were final before the compaction)
 int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* pos_out,
-                  int64_t* count_dev, int32_t* tmp, hipStream_t s);
+                  int64_t* count_dev, int32_t* tmp, hipStream_t s, const HostPost* post = nullptr,
+                  int post_words = 0);
+
+// --------------------------------------------------------------- bounds
+// zero [p, p + bytes) with the whole grid (16-B stores on the aligned middle)
+__device__ __forceinline__ void grid_zero(uint8_t* p, size_t bytes) {
+  if (!p || !bytes) return;
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
+  const size_t head = std::min(bytes, (size_t)((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15));
+  const size_t nv = (bytes - head) / 16;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  for (size_t k = t0; k < nv; k += st) q[k] = make_uint4(0, 0, 0, 0);
+  for (size_t k = t0; k < head; k += st) p[k] = 0;
+  for (size_t k = head + nv * 16 + t0; k < bytes; k += st) p[k] = 0;
+}
+
+// This thread's share of a grid-strided min / max over an (n,3) float32
+// cloud.  Aligned clouds are read as 16-B vectors, four points per three
+// loads (x y z x | y z x y | z x y z), two chunks in flight per lane; the rows
+// past the last whole chunk (and unaligned clouds) one point at a time.
+__device__ __forceinline__ void aabb_accumulate(const float* __restrict__ xyz, int64_t n, float mn[3], float mx[3]) {
+  for (int a = 0; a < 3; ++a) {
+    mn[a] = INFINITY;
+    mx[a] = -INFINITY;
+  }
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  int64_t i0 = 0;
+  if ((reinterpret_cast<uintptr_t>(xyz) & 15) == 0) {
+    const float4* q = reinterpret_cast<const float4*>(xyz);
+    const int64_t nch = n / 4;
+    i0 = nch * 4;
+    auto take = [&](const float4 a, const float4 b, const float4 d) {
+      mn[0] = fminf(mn[0], fminf(fminf(a.x, a.w), fminf(b.z, d.y)));
+      mn[1] = fminf(mn[1], fminf(fminf(a.y, b.x), fminf(b.w, d.z)));
+      mn[2] = fminf(mn[2], fminf(fminf(a.z, b.y), fminf(d.x, d.w)));
+      mx[0] = fmaxf(mx[0], fmaxf(fmaxf(a.x, a.w), fmaxf(b.z, d.y)));
+      mx[1] = fmaxf(mx[1], fmaxf(fmaxf(a.y, b.x), fmaxf(b.w, d.z)));
+      mx[2] = fmaxf(mx[2], fmaxf(fmaxf(a.z, b.y), fmaxf(d.x, d.w)));
+    };
+    int64_t c = t0;
+    for (; c + st < nch; c += 2 * st) {
+      const float4 a = q[3 * c], b = q[3 * c + 1], d = q[3 * c + 2];
+      const float4 a2 = q[3 * (c + st)], b2 = q[3 * (c + st) + 1], d2 = q[3 * (c + st) + 2];
+      take(a, b, d);
+      take(a2, b2, d2);
+    }
+    if (c < nch) take(q[3 * c], q[3 * c + 1], q[3 * c + 2]);
+  }
+  for (int64_t i = i0 + t0; i < n; i += st) {
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    mn[0] = fminf(mn[0], x);
+    mn[1] = fminf(mn[1], y);
+    mn[2] = fminf(mn[2], z);
+    mx[0] = fmaxf(mx[0], x);
+    mx[1] = fmaxf(mx[1], y);
+    mx[2] = fmaxf(mx[2], z);
+  }
+}
+
+// min / max of the block's threads (6 columns: min x y z, max x y z) into
+// out6 (written by threads 0..5); sh: kBlock / 64 x 6 floats of LDS
+__device__ __forceinline__ void aabb_block_fold(float mn[3], float mx[3], float (*sh)[6], float* out6) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+    }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int a = 0; a < 3; ++a) {
+      sh[w][a] = mn[a];
+      sh[w][3 + a] = mx[a];
+    }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float r = sh[0][threadIdx.x];
+    for (int k = 1; k < kBlock / 64; ++k)
+      r = threadIdx.x < 3 ? fminf(r, sh[k][threadIdx.x]) : fmaxf(r, sh[k][threadIdx.x]);
+    out6[threadIdx.x] = r;
+  }
+}
+
+// Where the bounds' final kernel publishes {min, max}.
+struct AabbOut {
+  double* mm_host;              // mapped pinned memory (device view), then
+  uint64_t seq;                 //   this sequence number into
+  volatile uint64_t* seq_host;  //   the mailbox's word 0
+};
+struct AabbNoTail {
+  __device__ void operator()(const double*) const {}
+};
+
+// The bounds' final fold (one block of kBlock threads) over the nb block
+// partials of k_aabb_partial: publishes {min, max} to the host mailbox, then
+// runs tail(mm) on thread 0 (the voxel path: the one-pass binning's plan, so
+// no separate plan launch).
+template <class Tail>
+__global__ void __launch_bounds__(kBlock) k_aabb_final_tail(const float* __restrict__ part, int nb, int64_t n,
+                                                            AabbOut o, Tail tail) {
+  __shared__ float sh[kBlock / 64][6];
+  __shared__ float fin[6];
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int b = threadIdx.x; b < nb; b += kBlock)
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fminf(mn[a], part[b * 6 + a]);
+      mx[a] = fmaxf(mx[a], part[b * 6 + 3 + a]);
+    }
+  aabb_block_fold(mn, mx, sh, fin);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double mm[6];
+    for (int a = 0; a < 6; ++a) mm[a] = n == 0 ? 0.0 : (double)fin[a];
+    for (int a = 0; a < 6; ++a) o.mm_host[a] = mm[a];
+    __threadfence_system();
+    *o.seq_host = o.seq;
+    tail(mm);
+  }
+}
+
+// Queues the bounds' partial kernel (z0..z3: clears folded in) and returns the
+// mailbox of this host thread for the final kernel (advancing the sequence
+// number aabb_end waits for); *part, *nb: the partials the final kernel folds.
+int aabb_begin_partial(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0, ZeroSpan z1, ZeroSpan z2,
+                       ZeroSpan z3, AabbOut* o, const float** part, int* nb);
 
 // Column reduction of a row-major partials matrix part[rows][width] -> out[width]
 // with a fixed summation order (deterministic).  One block per 64 columns.
@@ -314,9 +458,6 @@ int aabb_device(const float* xyz, int64_t n, double* mm_dev, void* ws, hipStream
 int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0 = {}, ZeroSpan z1 = {},
                ZeroSpan z2 = {}, ZeroSpan z3 = {});
 int aabb_end(double mm_host[6], hipStream_t s);
-// device view of the bounds aabb_begin's kernels publish ({min, max}, 6
-// doubles): readable by kernels queued after it on the same stream
-const double* aabb_mailbox_dev();
 // AABB of float64 points into a device double[6] (no sync); ws: aabb64_ws_bytes
 size_t aabb64_ws_bytes();
 int aabb64_device(const double* xyz, int64_t n, double* mm_dev, void* ws, hipStream_t s);

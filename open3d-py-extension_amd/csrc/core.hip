@@ -75,30 +75,48 @@ int read_back(void* dst_host, const void* src_dev, size_t bytes, hipStream_t s) 
   return host_wait(s);
 }
 
-// Split read-back: the copy into the pinned staging buffer and an event are
-// queued now (read_back_begin), the host waits for that event only
-// (read_back_end) — work queued on the stream in between keeps running.
-static thread_local void* g_rb_pin = nullptr;
-static thread_local hipEvent_t g_rb_ev = nullptr;
+namespace {
+struct PostBox {
+  uint64_t* host = nullptr;  // [0] sequence, [1 ..] words (mapped, coherent)
+  uint64_t* dev = nullptr;
+  uint64_t seq = 0;
+};
+thread_local PostBox g_post;
+}  // namespace
 
-int read_back_begin(const void* src_dev, size_t bytes, hipStream_t s) {
-  if (bytes > (64 << 10)) return fail(O3DX_EINVAL, "read_back_begin: %zu bytes", bytes);
-  if (!g_rb_pin) O3DX_HIP(hipHostMalloc(&g_rb_pin, 64 << 10, hipHostMallocDefault));
-  if (!g_rb_ev) O3DX_HIP(hipEventCreateWithFlags(&g_rb_ev, hipEventDisableTiming));
-  O3DX_HIP(hipMemcpyAsync(g_rb_pin, src_dev, bytes, hipMemcpyDeviceToHost, s));
-  O3DX_HIP(hipEventRecord(g_rb_ev, s));
+int post_prepare(HostPost* p) {
+  PostBox& b = g_post;
+  if (!b.host) {
+    void* h = nullptr;
+    O3DX_HIP(hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocCoherent));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return fail(O3DX_EIO, "post_prepare: no device view of the post box");
+    }
+    b.host = static_cast<uint64_t*>(h);
+    b.dev = static_cast<uint64_t*>(d);
+    b.host[0] = 0;
+  }
+  ++b.seq;
+  p->words = b.dev + 1;
+  p->seq_word = static_cast<volatile uint64_t*>(b.dev);
+  p->seq = b.seq;
   return 0;
 }
 
-int read_back_end(void* dst_host, size_t bytes) {
-  bool done = false;
-  for (int i = 0; i < 1 << 16 && !done; ++i) {
-    const hipError_t e = hipEventQuery(g_rb_ev);
-    if (e == hipSuccess) done = true;
-    else if (e != hipErrorNotReady) break;
+int post_wait(const HostPost& p, void* dst, size_t bytes, hipStream_t s) {
+  if (bytes > kPostWords * sizeof(uint64_t)) return fail(O3DX_EINVAL, "post_wait: %zu bytes", bytes);
+  volatile uint64_t* q = g_post.host;
+  bool seen = false;
+  for (int i = 0; i < (1 << 22) && !seen; ++i) seen = *q == p.seq;  // ~ms of polling
+  if (!seen) {  // slow path: wait for the stream (errors surface here)
+    O3DX_TRY(host_wait(s));
+    seen = *q == p.seq;
+    if (!seen) return fail(O3DX_EIO, "post_wait: the posted words never arrived");
   }
-  if (!done) O3DX_HIP(hipEventSynchronize(g_rb_ev));
-  std::memcpy(dst_host, g_rb_pin, bytes);
+  std::atomic_thread_fence(std::memory_order_acquire);
+  std::memcpy(dst, const_cast<const uint64_t*>(g_post.host) + 1, bytes);
   return 0;
 }
 
@@ -200,7 +218,7 @@ __global__ void __launch_bounds__(kBlock) k_tile_sums_u8(const uint8_t* __restri
 
 // Single-block exclusive scan of the tile partials (in place); total -> *total.
 __global__ void __launch_bounds__(1024) k_scan_partials(int32_t* part, int64_t m, int32_t* total_i32,
-                                                        int64_t* total_i64) {
+                                                        int64_t* total_i64, HostPost post = {}, int post_words = 0) {
   __shared__ int sh[1024 / 64 + 1];
   int carry = 0;
   for (int64_t b = 0; b < m; b += 1024) {
@@ -214,6 +232,7 @@ __global__ void __launch_bounds__(1024) k_scan_partials(int32_t* part, int64_t m
   if (threadIdx.x == 0) {
     if (total_i32) *total_i32 = carry;
     if (total_i64) *total_i64 = carry;
+    if (post.seq && total_i64) post_publish(post, total_i64, post_words);
   }
 }
 
@@ -282,7 +301,8 @@ __global__ void __launch_bounds__(kBlock) k_tile_compact_u8_sums(const uint8_t* 
                                                                  const int32_t* __restrict__ part,
                                                                  int32_t* __restrict__ idx_out,
                                                                  int32_t* __restrict__ pos_out,
-                                                                 int64_t* __restrict__ count_dev) {
+                                                                 int64_t* __restrict__ count_dev, HostPost post,
+                                                                 int post_words) {
   __shared__ int sh[kBlock / 64 + 1];
   int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
   uint8_t v[kScanItems];
@@ -307,7 +327,10 @@ __global__ void __launch_bounds__(kBlock) k_tile_compact_u8_sums(const uint8_t* 
   for (int j = 0; j < kScanItems; ++j) s += v[j] != 0;
   int tot;
   int ex = block_excl_scan<kBlock>(s, sh, &tot) + first;
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *count_dev = (int64_t)first + tot;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    *count_dev = (int64_t)first + tot;
+    if (post.seq) post_publish(post, count_dev, post_words);
+  }
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
     int64_t i = base + j;
@@ -351,18 +374,22 @@ int compact_flags_scan(const uint8_t* flags, int64_t n, int64_t* count_dev, int3
 }
 
 int compact_flags(const uint8_t* flags, int64_t n, int32_t* idx_out, int32_t* pos_out,
-                  int64_t* count_dev, int32_t* tmp, hipStream_t s) {
+                  int64_t* count_dev, int32_t* tmp, hipStream_t s, const HostPost* post, int post_words) {
   int64_t tiles = (n + kScanTile - 1) / kScanTile;
+  const HostPost pp = post ? *post : HostPost{};
+  if (post_words < 0 || post_words > kPostWords) return fail(O3DX_EINVAL, "compact_flags: %d post words", post_words);
   if (tiles == 0) {
     O3DX_HIP(hipMemsetAsync(count_dev, 0, sizeof(int64_t), s));
+    if (post) return fail(O3DX_EINVAL, "compact_flags: nothing to post for an empty input");
     return 0;
   }
   hipLaunchKernelGGL(k_tile_sums_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp);
   if (tiles <= 4096) {  // the blocks read tiles^2 / 2 words in all (C2: 3M, from L2)
     hipLaunchKernelGGL(k_tile_compact_u8_sums, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp, idx_out,
-                       pos_out, count_dev);
+                       pos_out, count_dev, pp, post_words);
   } else {
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, tmp, tiles, (int32_t*)nullptr, count_dev);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, tmp, tiles, (int32_t*)nullptr, count_dev, pp,
+                       post_words);
     hipLaunchKernelGGL(k_tile_compact_u8, dim3((unsigned)tiles), dim3(kBlock), 0, s, flags, n, tmp, idx_out,
                        pos_out);
   }
@@ -453,25 +480,7 @@ void fx_to_double(const int64_t* fx4, int64_t k, double* out) {
 // ------------------------------------------------------------------- AABB
 constexpr int kAabbBlocks = 1024;
 
-struct P3 {
-  float x, y, z;
-};
-
-// Aligned clouds are read as 16-B vectors, four points per three loads
-// (x y z x | y z x y | z x y z), two chunks in flight per lane; the rows
-// past the last whole chunk (and unaligned clouds) one point at a time.
-// zero [p, p + bytes) with the whole grid (16-B stores on the aligned middle)
-__device__ __forceinline__ void grid_zero(uint8_t* p, size_t bytes) {
-  if (!p || !bytes) return;
-  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
-  const size_t head = std::min(bytes, (size_t)((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15));
-  const size_t nv = (bytes - head) / 16;
-  uint4* q = reinterpret_cast<uint4*>(p + head);
-  for (size_t k = t0; k < nv; k += st) q[k] = make_uint4(0, 0, 0, 0);
-  for (size_t k = t0; k < head; k += st) p[k] = 0;
-  for (size_t k = head + nv * 16 + t0; k < bytes; k += st) p[k] = 0;
-}
-
+// per-block partial {min, max} (the two-launch form: aabb_device)
 __global__ void __launch_bounds__(kBlock) k_aabb_partial(const float* __restrict__ xyz, int64_t n,
                                                          float* __restrict__ part, ZeroSpan z0 = {},
                                                          ZeroSpan z1 = {}, ZeroSpan z2 = {}, ZeroSpan z3 = {}) {
@@ -479,62 +488,10 @@ __global__ void __launch_bounds__(kBlock) k_aabb_partial(const float* __restrict
   grid_zero(z1.p, z1.bytes);
   grid_zero(z2.p, z2.bytes);
   grid_zero(z3.p, z3.bytes);
-  float mn[3] = {INFINITY, INFINITY, INFINITY};
-  float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  const P3* p = reinterpret_cast<const P3*>(xyz);
-  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
-  int64_t i0 = 0;
-  if ((reinterpret_cast<uintptr_t>(xyz) & 15) == 0) {
-    const float4* q = reinterpret_cast<const float4*>(xyz);
-    const int64_t nch = n / 4;
-    i0 = nch * 4;
-    auto take = [&](const float4 a, const float4 b, const float4 d) {
-      mn[0] = fminf(mn[0], fminf(fminf(a.x, a.w), fminf(b.z, d.y)));
-      mn[1] = fminf(mn[1], fminf(fminf(a.y, b.x), fminf(b.w, d.z)));
-      mn[2] = fminf(mn[2], fminf(fminf(a.z, b.y), fminf(d.x, d.w)));
-      mx[0] = fmaxf(mx[0], fmaxf(fmaxf(a.x, a.w), fmaxf(b.z, d.y)));
-      mx[1] = fmaxf(mx[1], fmaxf(fmaxf(a.y, b.x), fmaxf(b.w, d.z)));
-      mx[2] = fmaxf(mx[2], fmaxf(fmaxf(a.z, b.y), fmaxf(d.x, d.w)));
-    };
-    int64_t c = t0;
-    for (; c + st < nch; c += 2 * st) {
-      const float4 a = q[3 * c], b = q[3 * c + 1], d = q[3 * c + 2];
-      const float4 a2 = q[3 * (c + st)], b2 = q[3 * (c + st) + 1], d2 = q[3 * (c + st) + 2];
-      take(a, b, d);
-      take(a2, b2, d2);
-    }
-    if (c < nch) take(q[3 * c], q[3 * c + 1], q[3 * c + 2]);
-  }
-  for (int64_t i = i0 + t0; i < n; i += st) {
-    P3 q = p[i];
-    mn[0] = fminf(mn[0], q.x);
-    mn[1] = fminf(mn[1], q.y);
-    mn[2] = fminf(mn[2], q.z);
-    mx[0] = fmaxf(mx[0], q.x);
-    mx[1] = fmaxf(mx[1], q.y);
-    mx[2] = fmaxf(mx[2], q.z);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
-      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
-    }
+  float mn[3], mx[3];
+  aabb_accumulate(xyz, n, mn, mx);
   __shared__ float sh[kBlock / 64][6];
-  const int w = threadIdx.x >> 6;
-  if (lane_id() == 0)
-    for (int a = 0; a < 3; ++a) {
-      sh[w][a] = mn[a];
-      sh[w][3 + a] = mx[a];
-    }
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    float r = sh[0][threadIdx.x];
-    for (int k = 1; k < kBlock / 64; ++k)
-      r = threadIdx.x < 3 ? fminf(r, sh[k][threadIdx.x]) : fmaxf(r, sh[k][threadIdx.x]);
-    part[blockIdx.x * 6 + threadIdx.x] = r;
-  }
+  aabb_block_fold(mn, mx, sh, part + (size_t)blockIdx.x * 6);
 }
 
 __global__ void __launch_bounds__(1024) k_aabb_final(const float* __restrict__ part, int nb, int64_t n,
@@ -555,32 +512,6 @@ __global__ void __launch_bounds__(1024) k_aabb_final(const float* __restrict__ p
   }
 }
 
-// k_aabb_final's host-visible twin: thread a reduces column a, then the
-// values are published to mapped host memory before the sequence number
-__global__ void __launch_bounds__(1024) k_aabb_final_host(const float* __restrict__ part, int nb, int64_t n,
-                                                          double* __restrict__ mm_host, uint64_t seq,
-                                                          volatile uint64_t* seq_host) {
-  __shared__ float sh[6][171];
-  const int a = threadIdx.x % 6, g = threadIdx.x / 6;
-  if (g < 170) {
-    float r = a < 3 ? INFINITY : -INFINITY;
-    for (int b = g; b < nb; b += 170) r = a < 3 ? fminf(r, part[b * 6 + a]) : fmaxf(r, part[b * 6 + a]);
-    sh[a][g] = r;
-  }
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    float r = sh[a][0];
-    for (int k = 1; k < 170; ++k) r = a < 3 ? fminf(r, sh[a][k]) : fmaxf(r, sh[a][k]);
-    mm_host[a] = n == 0 ? 0.0 : (double)r;
-    __threadfence_system();
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    *seq_host = seq;
-  }
-}
-
 namespace {
 struct AabbMailbox {
   uint64_t* host = nullptr;  // [0] sequence, [1..6] bounds (mapped, coherent)
@@ -590,8 +521,8 @@ struct AabbMailbox {
 thread_local AabbMailbox g_ambox;
 }  // namespace
 
-int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0, ZeroSpan z1, ZeroSpan z2,
-               ZeroSpan z3) {
+int aabb_begin_partial(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0, ZeroSpan z1, ZeroSpan z2,
+                       ZeroSpan z3, AabbOut* o, const float** part, int* nb) {
   AabbMailbox& m = g_ambox;
   if (!m.host) {
     void* h = nullptr;
@@ -606,17 +537,28 @@ int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0
     m.host[0] = 0;
   }
   ++m.seq;
-  float* part = reinterpret_cast<float*>(ws);
-  int nb = (int)std::min<int64_t>(kAabbBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
-  if (z0.bytes || z1.bytes || z2.bytes || z3.bytes) nb = kAabbBlocks;  // the clears want the whole grid
-  hipLaunchKernelGGL(k_aabb_partial, dim3(nb), dim3(kBlock), 0, s, xyz, n, part, z0, z1, z2, z3);
-  hipLaunchKernelGGL(k_aabb_final_host, dim3(1), dim3(1024), 0, s, part, nb, n,
-                     reinterpret_cast<double*>(m.dev + 1), m.seq, static_cast<volatile uint64_t*>(m.dev));
-  O3DX_HIP(hipGetLastError());
+  o->mm_host = reinterpret_cast<double*>(m.dev + 1);
+  o->seq = m.seq;
+  o->seq_host = static_cast<volatile uint64_t*>(m.dev);
+  float* pt = reinterpret_cast<float*>(ws);
+  int b = (int)std::min<int64_t>(kAabbBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
+  if (z0.bytes || z1.bytes || z2.bytes || z3.bytes) b = kAabbBlocks;  // the clears want the whole grid
+  hipLaunchKernelGGL(k_aabb_partial, dim3(b), dim3(kBlock), 0, s, xyz, n, pt, z0, z1, z2, z3);
+  *part = pt;
+  *nb = b;
   return 0;
 }
 
-const double* aabb_mailbox_dev() { return reinterpret_cast<const double*>(g_ambox.dev + 1); }
+int aabb_begin(const float* xyz, int64_t n, void* ws, hipStream_t s, ZeroSpan z0, ZeroSpan z1, ZeroSpan z2,
+               ZeroSpan z3) {
+  AabbOut o;
+  const float* part;
+  int nb;
+  O3DX_TRY(aabb_begin_partial(xyz, n, ws, s, z0, z1, z2, z3, &o, &part, &nb));
+  hipLaunchKernelGGL(k_aabb_final_tail<AabbNoTail>, dim3(1), dim3(kBlock), 0, s, part, nb, n, o, AabbNoTail{});
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
 
 int aabb_end(double mm_host[6], hipStream_t s) {
   AabbMailbox& m = g_ambox;

@@ -102,6 +102,7 @@ struct Bricks {
   int sx, sy, sz;     // log2 brick extent per axis
   int nbx, nby, nbz;  // bricks per axis
   int nb;
+  int ncp;            // one-pass binning: segment copies per brick
 };
 
 // floor(d / vs) through a multiply: q = d * (1/vs) is within |q| 2^-51 of the
@@ -141,7 +142,10 @@ constexpr int kTotStride = 16;  // int32 per brick total (one 64-B line each)
 // b % copies (its own slice of the brick's segment).  768 blocks x 614
 // bricks of returning atomics on 614 words were serialised per word (C2:
 // ~20 us of the kernel's 84); 4 copies cut each word's queue to a quarter.
+// (measured round 5 at C2: 1 / 2 / 4 copies within 3 %; 8, one per XCD by
+// block % 8, 55 % slower)
 __host__ __device__ inline int seg_copies(int nb) { return nb <= kMaxBuckets / 4 ? 4 : nb <= kMaxBuckets / 2 ? 2 : 1; }
+constexpr int kMaxCopies = 4;
 
 __global__ void __launch_bounds__(kBinBlock) k_vbin_count(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
                                                        Bricks b, int32_t* __restrict__ roff,
@@ -271,40 +275,46 @@ __global__ void __launch_bounds__(kBinBlock) k_vbin_scatter(const float* __restr
 // run lands at k * cap + offset: no scan over bricks or blocks), and writes
 // the runs from the LDS stage.  A brick whose total passes cap drops the
 // excess and raises err bit 16: the host reruns with count + scatter.
+// FB threads x FP points per thread, one workgroup per CU (measured: two
+// 512 x 14 workgroups per CU, 87 us against 77 at C2 — twice the blocks make
+// twice the reservation atomics, ~18 us of the kernel)
 constexpr int kFusePer = 16;
 constexpr int kFuseBlock = 1024;
 constexpr int kFuseChunk = kFuseBlock * kFusePer;
 
-// dynamic LDS: stage[kFuseChunk] (u64), loc[nb + 1], dst[nb]
-inline size_t fused_lds_bytes(int nb) { return kFuseChunk * sizeof(uint64_t) + (2 * (size_t)nb + 1) * sizeof(int32_t); }
+// dynamic LDS: stage[FB * FP] (u64), loc[nb + 1], dst[nb]
+inline size_t fused_lds_bytes(int nb, int chunk_cap = kFuseChunk) {
+  return (size_t)chunk_cap * sizeof(uint64_t) + (2 * (size_t)nb + 1) * sizeof(int32_t);
+}
 
 // chunk: points per block (<= kFuseChunk), chosen so the block count is a
 // whole number of CU-waves of blocks (fused_grid)
+template <int FB, int FP>
 __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, int64_t n, const VoxelGeom& g,
                                                 const Bricks& b, int cap, int32_t* __restrict__ btot,
                                                 uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
                                                 int* __restrict__ err, int chunk) {
   extern __shared__ uint64_t lds_u64[];
   uint64_t* stage = lds_u64;
-  int32_t* loc = reinterpret_cast<int32_t*>(lds_u64 + kFuseChunk);  // count -> offset -> cursor
+  int32_t* loc = reinterpret_cast<int32_t*>(lds_u64 + FB * FP);      // count -> offset -> cursor
   int32_t* dst = loc + b.nb + 1;                                      // segment index of stage slot 0, per brick
-  __shared__ int32_t wsum[kFuseBlock / 64 + 1];
+  __shared__ int32_t wsum[FB / 64 + 1];
   __shared__ int ovf;
   const P3* p = reinterpret_cast<const P3*>(xyz);
-  for (int k = threadIdx.x; k < b.nb; k += kFuseBlock) loc[k] = 0;
+  for (int k = threadIdx.x; k < b.nb; k += FB) loc[k] = 0;
   if (threadIdx.x == 0) ovf = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * chunk;
   const int64_t end = min(base + chunk, n);
-  uint32_t code[kFusePer];
+  uint32_t code[FP];
   bool bad = false;
   // every load of the chunk first (clamped, unconditional), then the keys
-  P3 q[kFusePer];
+  P3 q[FP];
 #pragma unroll
-  for (int j = 0; j < kFusePer; ++j) q[j] = p[min(base + threadIdx.x + (int64_t)j * kFuseBlock, end - 1)];
+  for (int j = 0; j < FP; ++j) q[j] = p[min(base + threadIdx.x + (int64_t)j * FB, end - 1)];
 #pragma unroll
-  for (int j = 0; j < kFusePer; ++j) {
-    const int64_t i = base + threadIdx.x + (int64_t)j * kFuseBlock;
+  for (int j = 0; j < FP; ++j) {
+    const int64_t i = base + threadIdx.x + (int64_t)j * FB;
     code[j] = ~0u;
     if (i < end) {
       int v[3];
@@ -320,13 +330,13 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   }
   if (bad) *err = 1;
   __syncthreads();
-  const int span = (b.nb + kFuseBlock - 1) / kFuseBlock;
+  const int span = (b.nb + FB - 1) / FB;
   const int k0 = threadIdx.x * span, k1 = min(k0 + span, b.nb);
   int run = 0;
   for (int k = k0; k < k1; ++k) run += loc[k];
   int tot;
-  int ex = block_excl_scan<kFuseBlock>(run, wsum, &tot);
-  const int ncp = seg_copies(b.nb), cq = (int)(blockIdx.x & (unsigned)(ncp - 1)), sub = cap / ncp;
+  int ex = block_excl_scan<FB>(run, wsum, &tot);
+  const int ncp = b.ncp, cq = (int)(blockIdx.x & (unsigned)(ncp - 1)), sub = cap / ncp;
   for (int k = k0; k < k1; ++k) {
     const int c = loc[k];
     loc[k] = ex;
@@ -339,14 +349,14 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kFusePer; ++j) {
+  for (int j = 0; j < FP; ++j) {
     if (code[j] == ~0u) continue;
-    const int64_t i = base + threadIdx.x + (int64_t)j * kFuseBlock;
+    const int64_t i = base + threadIdx.x + (int64_t)j * FB;
     const int at = atomicAdd(&loc[code[j] >> 16], 1);
     stage[at] = ((uint64_t)(code[j] >> 16) << 48) | ((uint64_t)(code[j] & 0xffffu) << 32) | (uint32_t)i;
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < tot; t += kFuseBlock) {
+  for (int t = threadIdx.x; t < tot; t += FB) {
     const uint64_t e = stage[t];
     const int k = (int)(e >> 48);
     const int o = dst[k] + t;
@@ -355,11 +365,11 @@ __device__ __forceinline__ void vbin_fused_body(const float* __restrict__ xyz, i
   if (threadIdx.x == 0 && ovf) atomicOr(err, 16);
 }
 
-__global__ void __launch_bounds__(kFuseBlock) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                       Bricks b, int cap, int32_t* __restrict__ btot,
-                                                       uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
-                                                       int* __restrict__ err, int chunk) {
-  vbin_fused_body(xyz, n, g, b, cap, btot, entries, vid, err, chunk);
+template <int FB, int FP>
+__global__ void __launch_bounds__(FB) k_vbin_fused(const float* __restrict__ xyz, int64_t n, VoxelGeom g, Bricks b,
+                                                   int cap, int32_t* __restrict__ btot, uint64_t* __restrict__ entries,
+                                                   int32_t* __restrict__ vid, int* __restrict__ err, int chunk) {
+  vbin_fused_body<FB, FP>(xyz, n, g, b, cap, btot, entries, vid, err, chunk);
 }
 
 // The one-pass binning's grid: its LDS stage allows one workgroup per CU, so
@@ -367,9 +377,9 @@ __global__ void __launch_bounds__(kFuseBlock) k_vbin_fused(const float* __restri
 // points are spread evenly over them (10M: 768 blocks of 13,021 points instead
 // of 611 of 16,384, whose third round ran on 99 of the 256 CUs).
 constexpr int kFuseCUs = 256;
-static int fused_grid(int64_t n, unsigned* blocks) {
-  const int64_t nb0 = std::max<int64_t>(1, (n + kFuseChunk - 1) / kFuseChunk);
-  const int64_t nb = (nb0 + kFuseCUs - 1) / kFuseCUs * kFuseCUs;
+static int fused_grid(int64_t n, unsigned* blocks, int chunk_cap = kFuseChunk, int per_cu = 1) {
+  const int64_t nb0 = std::max<int64_t>(1, (n + chunk_cap - 1) / chunk_cap);
+  const int64_t nb = (nb0 + kFuseCUs * per_cu - 1) / (kFuseCUs * per_cu) * (kFuseCUs * per_cu);
   const int chunk = (int)std::max<int64_t>(1, (n + nb - 1) / nb);
   *blocks = (unsigned)std::max<int64_t>(1, (n + chunk - 1) / chunk);
   return chunk;
@@ -394,13 +404,18 @@ __global__ void __launch_bounds__(kReduceBlock) k_vbin_reduce(const uint64_t* __
   const int bk = blockIdx.x;
   // the brick's entries: its run of the scanned layout, or the filled part
   // of each copy's slice of its fixed segment
-  const int ncp = cap ? seg_copies(b.nb) : 1, sub = cap / ncp;
+  const int ncp = cap ? b.ncp : 1, sub = cap / ncp;
   for (int cq = 0; cq < ncp; ++cq) {
     const int64_t e0 = cap ? (int64_t)bk * cap + (int64_t)cq * sub : bbase[bk];
     const int64_t e1 = cap ? e0 + min(btot[(bk * ncp + cq) * kTotStride], sub) : bbase[bk + 1];
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += kReduceBlock) {
-      const uint64_t w = entries[e];
-      atomicMax(&tab[(int)(w >> 32)], (int32_t)(uint32_t)w);
+    constexpr int kU = 8;  // entry loads in flight per thread
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += (int64_t)kU * kReduceBlock) {
+      uint64_t wv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) wv[u] = entries[min(e + (int64_t)u * kReduceBlock, e1 - 1)];
+#pragma unroll
+      for (int u = 0; u < kU; ++u)  // (a clamped duplicate is harmless for a max)
+        atomicMax(&tab[(int)(wv[u] >> 32)], (int32_t)(uint32_t)wv[u]);
     }
   }
   __syncthreads();
@@ -471,7 +486,7 @@ __host__ __device__ static Bricks plan_bricks(int nx, int ny, int nz, int max_bu
     for (int a = 0; a < 3; ++a) nb[a] = (d[a] + (1ll << sh[a]) - 1) >> sh[a];
     const int64_t total = nb[0] * nb[1] * nb[2];
     if (total <= max_buckets) {
-      b = Bricks{sh[0], sh[1], sh[2], (int)nb[0], (int)nb[1], (int)nb[2], (int)total};
+      b = Bricks{sh[0], sh[1], sh[2], (int)nb[0], (int)nb[1], (int)nb[2], (int)total, 1};
       return b;
     }
   }
@@ -486,6 +501,10 @@ __host__ __device__ static Bricks plan_bricks(int nx, int ny, int nz, int max_bu
 // scatter (1.24 ms against ~0.4 ms); plan_bricks still prefers 2^12-voxel
 // bricks when they fit (C2: 614).
 constexpr int kFuseMaxBricks = 2048;
+// brick totals: (brick, copy) counters on their own 64-B lines (seg_copies
+// keeps bricks x copies <= kMaxBuckets)
+constexpr int64_t kTotWords = (int64_t)kMaxBuckets * kTotStride;
+static_assert(kFuseMaxBricks * 2 <= kMaxBuckets && kMaxBuckets / 4 * kMaxCopies <= kMaxBuckets, "totals");
 static int64_t dense_cap(int64_t n);
 static int64_t entries_cap(int64_t n);
 __host__ __device__ inline int64_t dense_cap_hd(int64_t n) { return 2 * n + (1 << 20); }
@@ -527,6 +546,7 @@ __host__ __device__ inline void fused_plan(const double mn[3], const double mx[3
   if (seg > INT32_MAX || !((double)seg >= 1.03 * full + 2048.0) || geom_key(g, n) == skip_key) return;
   P->g = g;
   P->b = b;
+  P->b.ncp = seg_copies(b.nb);
   P->cap = (int)seg;
   P->ok = 1;
 }
@@ -545,29 +565,49 @@ inline void fused_plan_geom(const VoxelGeom& g, int64_t n, int allow, uint64_t s
   if (seg > INT32_MAX || !((double)seg >= 1.03 * full + 2048.0) || geom_key(g, n) == skip_key) return;
   P->g = g;
   P->b = b;
+  P->b.ncp = seg_copies(b.nb);
   P->cap = (int)seg;
   P->ok = 1;
 }
 
-__global__ void k_bin_plan(const double* mm, double vs, int64_t n, int allow, uint64_t skip_key,
-                           BinPlan* __restrict__ plan) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+// The one-pass binning's plan, computed by the bounds' final kernel
+// (k_aabb_final_tail) from the bounds it just folded.
+struct PlanTail {
+  double vs;
+  int64_t n;
+  int allow;
+  uint64_t skip_key;
+  BinPlan* plan;
+  __device__ void operator()(const double* mm) const {
     const double mn[3] = {mm[0], mm[1], mm[2]}, mx[3] = {mm[3], mm[4], mm[5]};
     BinPlan P;
     fused_plan(mn, mx, vs, n, allow, skip_key, &P);
     *plan = P;
   }
-}
+};
 
-__global__ void __launch_bounds__(kFuseBlock) k_vbin_fused_pre(const float* __restrict__ xyz, int64_t n,
-                                                           const BinPlan* __restrict__ plan,
-                                                           int32_t* __restrict__ btot, uint64_t* __restrict__ entries,
-                                                           int32_t* __restrict__ vid, int* __restrict__ err,
-                                                           int chunk) {
+template <int FB, int FP>
+__global__ void __launch_bounds__(FB) k_vbin_fused_pre(const float* __restrict__ xyz, int64_t n,
+                                                       const BinPlan* __restrict__ plan, int32_t* __restrict__ btot,
+                                                       uint64_t* __restrict__ entries, int32_t* __restrict__ vid,
+                                                       int* __restrict__ err, int chunk) {
   if (!plan->ok) return;
   const VoxelGeom g = plan->g;
   const Bricks b = plan->b;
-  vbin_fused_body(xyz, n, g, b, plan->cap, btot, entries, vid, err, chunk);
+  vbin_fused_body<FB, FP>(xyz, n, g, b, plan->cap, btot, entries, vid, err, chunk);
+}
+
+// launch of the one-pass binning (nb_lds: the bricks its LDS is sized for)
+template <bool PRE, class... A>
+static void launch_fused(int nb_lds, int64_t n, hipStream_t s, A... args) {
+  unsigned nfb;
+  const int chunk = fused_grid(n, &nfb);
+  if constexpr (PRE)
+    hipLaunchKernelGGL((k_vbin_fused_pre<kFuseBlock, kFusePer>), dim3(nfb), dim3(kFuseBlock), fused_lds_bytes(nb_lds),
+                       s, args..., chunk);
+  else
+    hipLaunchKernelGGL((k_vbin_fused<kFuseBlock, kFusePer>), dim3(nfb), dim3(kFuseBlock), fused_lds_bytes(nb_lds), s,
+                       args..., chunk);
 }
 
 __global__ void __launch_bounds__(kBlock) k_voxel_assign_hash(const float* __restrict__ xyz, int64_t n,
@@ -648,23 +688,45 @@ __device__ __forceinline__ bool voxel_hid(const P3& q, const VoxelGeom& g, const
 
 __device__ __forceinline__ int hbin_of(uint64_t h, const HMix& m) { return (int)(h >> (m.k - kHBinBits)); }
 
+// Blocks of the hash-binned passes: each takes a contiguous chunk of `chunk`
+// points (a multiple of kBinRound).  At most kHBinBlocks blocks: the
+// bin-major histogram (kHBins x blocks ints), its scan and the per-block
+// runs scale with the block count, so few large blocks keep the histogram
+// small and each (bin, block) run long (C5's 200M points: 12.2K blocks of 16K
+// wrote a 200 MB histogram whose scan alone took 1 ms, and runs of ~4
+// entries per bin and block).
+constexpr int kHBinBlocks = 2048;
+static int hbin_grid(int64_t n, int* chunk) {
+  const int64_t nb0 = std::min<int64_t>(std::max<int64_t>(1, (n + kBinChunk - 1) / kBinChunk), kHBinBlocks);
+  int64_t c = (n + nb0 - 1) / nb0;
+  c = (c + kBinRound - 1) / kBinRound * kBinRound;
+  *chunk = (int)c;
+  return (int)std::max<int64_t>(1, (n + c - 1) / c);
+}
+
 __global__ void __launch_bounds__(kBinBlock) k_hbin_count(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                       HMix m, int32_t* __restrict__ bhist, int* __restrict__ err) {
+                                                       HMix m, int chunk, int32_t* __restrict__ bhist,
+                                                       int* __restrict__ err) {
   __shared__ int32_t hist[kHBins];
   const P3* p = reinterpret_cast<const P3*>(xyz);
   for (int k = threadIdx.x; k < kHBins; k += kBinBlock) hist[k] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kBinChunk;
+  const int64_t base = (int64_t)blockIdx.x * chunk, end = min(base + chunk, n);
   bool bad = false;
-#pragma unroll 4
-  for (int j = 0; j < kBinPer; ++j) {
-    const int64_t i = base + threadIdx.x + (int64_t)j * kBinBlock;
-    if (i >= n) break;
-    uint64_t h;
-    if (voxel_hid(p[i], g, m, &h))
-      atomicAdd(&hist[hbin_of(h, m)], 1);
-    else
-      bad = true;
+  constexpr int kU = 8;  // loads in flight per thread
+  for (int64_t i0 = base + threadIdx.x; i0 < end; i0 += (int64_t)kU * kBinBlock) {
+    P3 q[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) q[u] = p[min(i0 + (int64_t)u * kBinBlock, end - 1)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (i0 + (int64_t)u * kBinBlock >= end) break;
+      uint64_t h;
+      if (voxel_hid(q[u], g, m, &h))
+        atomicAdd(&hist[hbin_of(h, m)], 1);
+      else
+        bad = true;
+    }
   }
   if (bad) *err = 8;
   __syncthreads();
@@ -675,7 +737,7 @@ __global__ void __launch_bounds__(kBinBlock) k_hbin_count(const float* __restric
 inline size_t hscatter_lds_bytes() { return kBinRound * sizeof(uint64_t) + 2 * (size_t)kHBins * sizeof(int32_t); }
 
 __global__ void __launch_bounds__(kBinBlock) k_hbin_scatter(const float* __restrict__ xyz, int64_t n, VoxelGeom g,
-                                                         HMix m, const int32_t* __restrict__ boff,
+                                                         HMix m, int chunk, const int32_t* __restrict__ boff,
                                                          uint64_t* __restrict__ entries) {
   extern __shared__ uint64_t lds_u64[];
   uint64_t* stage = lds_u64;
@@ -684,11 +746,11 @@ __global__ void __launch_bounds__(kBinBlock) k_hbin_scatter(const float* __restr
   __shared__ int32_t wsum[kBinBlock / 64 + 1];
   const P3* p = reinterpret_cast<const P3*>(xyz);
   for (int k = threadIdx.x; k < kHBins; k += kBinBlock) cur[k] = boff[(int64_t)k * gridDim.x + blockIdx.x];
-  const int64_t base = (int64_t)blockIdx.x * kBinChunk;
+  const int64_t base = (int64_t)blockIdx.x * chunk;
   constexpr int kPer = kBinRound / kBinBlock;
   constexpr int span = kHBins / kBinBlock;
   const int rbits = m.k - kHBinBits;
-  for (int r0 = 0; r0 < kBinChunk && base + r0 < n; r0 += kBinRound) {
+  for (int r0 = 0; r0 < chunk && base + r0 < n; r0 += kBinRound) {
     for (int k = threadIdx.x; k < kHBins; k += kBinBlock) loc[k] = 0;
     __syncthreads();
     // staged entry per point: rest << 24 | bin << 12 | position in the round
@@ -698,13 +760,17 @@ __global__ void __launch_bounds__(kBinBlock) k_hbin_scatter(const float* __restr
     // way out.
     static_assert(kBinRound == 4096 && kHBinBits == 12, "staged entry layout");
     uint64_t en[kPer];
+    P3 q[kPer];
+    const int64_t lim = min(base + chunk, n);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) q[j] = p[min(base + r0 + threadIdx.x + (int64_t)j * kBinBlock, lim - 1)];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int pos = threadIdx.x + j * kBinBlock;
       const int64_t i = base + r0 + pos;
       uint64_t h;
       en[j] = ~0ull;
-      if (i < n && voxel_hid(p[i], g, m, &h)) {
+      if (i < lim && voxel_hid(q[j], g, m, &h)) {
         const int bin = hbin_of(h, m);
         en[j] = ((h & ((1ull << rbits) - 1)) << 24) | ((uint64_t)bin << 12) | (uint64_t)pos;
         atomicAdd(&loc[bin], 1);
@@ -762,24 +828,32 @@ __global__ void __launch_bounds__(kHReduceBlock) k_hbin_reduce(const uint64_t* _
   const int bk = blockIdx.x;
   const uint32_t mask = (uint32_t)slots - 1u;
   const int32_t e0 = boff[(int64_t)bk * nblk], e1 = boff[(int64_t)(bk + 1) * nblk];
-  for (int32_t e = e0 + threadIdx.x; e < e1; e += kHReduceBlock) {
-    const uint64_t w = entries[e];
-    const uint32_t key = (uint32_t)(w >> 32);
-    const int32_t idx = (int32_t)(uint32_t)w;
-    uint32_t s = key & mask;  // the rest is already mixed
-    int probes = 0;
-    while (true) {
-      const uint32_t prev = atomicCAS(&hk[s], 0xFFFFFFFFu, key);
-      if (prev == 0xFFFFFFFFu || prev == key) break;
-      s = (s + 1) & mask;
-      if (++probes == slots) break;
+  constexpr int kU = 8;  // entry loads in flight per thread
+  for (int32_t e0u = e0 + threadIdx.x; e0u < e1; e0u += kU * kHReduceBlock) {
+    uint64_t wv[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) wv[u] = entries[min(e0u + u * kHReduceBlock, e1 - 1)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (e0u + u * kHReduceBlock >= e1) break;
+      const uint64_t w = wv[u];
+      const uint32_t key = (uint32_t)(w >> 32);
+      const int32_t idx = (int32_t)(uint32_t)w;
+      uint32_t s = key & mask;  // the rest is already mixed
+      int probes = 0;
+      while (true) {
+        const uint32_t prev = atomicCAS(&hk[s], 0xFFFFFFFFu, key);
+        if (prev == 0xFFFFFFFFu || prev == key) break;
+        s = (s + 1) & mask;
+        if (++probes == slots) break;
+      }
+      if (probes == slots) {  // the bin's table is full
+        full = 1;
+        continue;
+      }
+      atomicMax(&hr[s], idx);
+      if (vid) vid[idx] = bk * slots + (int32_t)s;
     }
-    if (probes == slots) {  // the bin's table is full
-      full = 1;
-      continue;
-    }
-    atomicMax(&hr[s], idx);
-    if (vid) vid[idx] = bk * slots + (int32_t)s;
   }
   __syncthreads();
   if (full) {
@@ -943,7 +1017,7 @@ static size_t carve(Arena& ar, int64_t n, VoxelWs* w) {
   w->keys = tb ? reinterpret_cast<unsigned long long*>(tb + Arena::align(hc * sizeof(int32_t))) : nullptr;
   w->entries = ar.take<uint64_t>(entries_cap(n));
   w->bhist = ar.take<int32_t>(bin_hist_ints(n));
-  w->boff = ar.take<int32_t>(std::max<int64_t>(bin_hist_ints(n) + 1, (int64_t)kMaxBuckets * (kTotStride + 1) + 1));
+  w->boff = ar.take<int32_t>(std::max<int64_t>(bin_hist_ints(n) + 1, kTotWords + (int64_t)kMaxBuckets + 1));
   w->vid = ar.take<int32_t>(n);
   w->flags = ar.take<uint8_t>(n + 16);
   w->pos = ar.take<int32_t>(n);
@@ -1007,7 +1081,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   // for the bounds (the first attempt below skips them)
   auto clears = [&]() -> int {
     O3DX_HIP(hipMemsetAsync(w.count, 0, 8 * sizeof(int64_t), s));
-    O3DX_HIP(hipMemsetAsync(w.boff, 0, (size_t)kMaxBuckets * kTotStride * sizeof(int32_t), s));
+    O3DX_HIP(hipMemsetAsync(w.boff, 0, (size_t)kTotWords * sizeof(int32_t), s));
     if (n > 0) O3DX_HIP(hipMemsetAsync(w.flags, 0, n, s));
     return 0;
   };
@@ -1017,20 +1091,24 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   bool pre_launched = false;
   if (!min_bound_host || !max_bound_host) {
     double mm[6];
-    O3DX_TRY(aabb_begin(xyz, n, w.aabb, s, ZeroSpan{reinterpret_cast<uint8_t*>(w.count), 8 * sizeof(int64_t)},
-                        ZeroSpan{reinterpret_cast<uint8_t*>(w.boff), (size_t)kMaxBuckets * kTotStride * sizeof(int32_t)},
-                        ZeroSpan{w.flags, (size_t)n}, extra_zero));
+    const ZeroSpan zc{reinterpret_cast<uint8_t*>(w.count), 8 * sizeof(int64_t)};
+    const ZeroSpan zb{reinterpret_cast<uint8_t*>(w.boff), (size_t)kTotWords * sizeof(int32_t)};
+    const ZeroSpan zf{w.flags, (size_t)n};
     if (!min_bound_host && !max_bound_host && allow_fused && n > 0) {
-      // the binning starts on the device's own plan while the host waits for
-      // the bounds (the host replays the same plan below)
-      hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, aabb_mailbox_dev(), voxel_size, n, allow_fused,
-                         g_fused_overflow_key, w.plan);
-      unsigned nfb;
-      const int chunk = fused_grid(n, &nfb);
-      hipLaunchKernelGGL(k_vbin_fused_pre, dim3(nfb), dim3(kFuseBlock), fused_lds_bytes(kFuseMaxBricks), s, xyz, n,
-                         w.plan, w.boff, w.entries, (voxel_of_point || cubic_id) ? w.vid : nullptr,
-                         reinterpret_cast<int*>(w.count + 1), chunk);
+      // the bounds' final kernel also forms the one-pass binning's plan,
+      // and the binning starts on it while the host waits for the bounds (the
+      // host replays the same plan below)
+      AabbOut o;
+      const float* part;
+      int nb;
+      O3DX_TRY(aabb_begin_partial(xyz, n, w.aabb, s, zc, zb, zf, extra_zero, &o, &part, &nb));
+      const PlanTail tail{voxel_size, n, allow_fused, g_fused_overflow_key, w.plan};
+      hipLaunchKernelGGL(k_aabb_final_tail<PlanTail>, dim3(1), dim3(kBlock), 0, s, part, nb, n, o, tail);
+      launch_fused<true>(kFuseMaxBricks, n, s, xyz, n, (const BinPlan*)w.plan, w.boff, w.entries,
+                         (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
       pre_launched = true;
+    } else {
+      O3DX_TRY(aabb_begin(xyz, n, w.aabb, s, zc, zb, zf, extra_zero));
     }
     O3DX_TRY(aabb_end(mm, s));
     for (int a = 0; a < 3; ++a) {
@@ -1083,8 +1161,10 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   bool hbin_ok = hbin_min >= 0;
   bool fused_ok = true;
   int attempts_made = 0;
+  HostPost counts_post;
   for (int attempt = 0; attempt < 4; ++attempt) {
     attempts_made = attempt;
+    bool posted = false;
     grid_kept = false;
     int64_t nslots;
     if (attempt > 0) O3DX_TRY(clears());
@@ -1095,7 +1175,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       KTimer kt("voxel_assign", s);
       // the brick totals (w.boff, cleared with the counts)
       int32_t* btot = w.boff;
-      int32_t* bbase = w.boff + (size_t)kMaxBuckets * kTotStride;
+      int32_t* bbase = w.boff + (size_t)kTotWords;
       // one pass into fixed per-brick segments when a segment holds a full
       // brick's share of a uniform cloud with room to spare (and this
       // geometry did not overflow last time)
@@ -1110,11 +1190,8 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       if (fused && attempt == 0 && pre_launched) {
         // already running on the device's identical plan
       } else if (fused) {
-        unsigned nfb;
-        const int chunk = fused_grid(n, &nfb);
-        hipLaunchKernelGGL(k_vbin_fused, dim3(nfb), dim3(kFuseBlock), fused_lds_bytes(bricks.nb), s, xyz, n, g, bricks,
-                           cap, btot, w.entries, (voxel_of_point || cubic_id) ? w.vid : nullptr,
-                           reinterpret_cast<int*>(w.count + 1), chunk);
+        launch_fused<false>(bricks.nb, n, s, xyz, n, g, bricks, cap, btot, w.entries,
+                     (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
       } else {
         hipLaunchKernelGGL(k_vbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, bricks, w.bhist, btot,
                            (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
@@ -1144,20 +1221,27 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       // xyz + a thread-per-rep table fill took 54 + 36 us against 14 + 56 us
       // for the compaction + k_gather_vox below at C2 — the sparse in-order
       // read of the cloud costs what the random gather does)
+      // the one-call pipeline (a hook, attempt 0): the counts go to the host
+      // from the compaction's last kernel, not by a copy queued after the gathers
+      if (hook && keep && attempt == 0) {
+        O3DX_TRY(post_prepare(&counts_post));
+        posted = true;
+      }
       O3DX_TRY(compact_flags(w.flags, n, rep_idx, (voxel_of_point || cubic_id) ? w.pos : nullptr, w.count,
-                             w.scan_tmp, s));
+                             w.scan_tmp, s, posted ? &counts_post : nullptr, 3));
     } else if (!dense && hbin_ok && n >= hbin_min && hbin_mix(nvox).k <= kHMaxBits) {
-      const unsigned nblk = (unsigned)((n + kBinChunk - 1) / kBinChunk);
+      int hchunk;
+      const unsigned nblk = (unsigned)hbin_grid(n, &hchunk);
       const HMix hm = hbin_mix(nvox);
       int slots = hbin_slots(n);
       if (const char* e = getenv("O3DX_VOXEL_HBIN_SLOTS"))  // tests: force the overflow fall-back
         slots = std::max(2, std::min(slots, atoi(e)));
       const bool trace = voxel_of_point || cubic_id;
       KTimer kt("voxel_assign", s);
-      hipLaunchKernelGGL(k_hbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, hm, w.bhist,
+      hipLaunchKernelGGL(k_hbin_count, dim3(nblk), dim3(kBinBlock), 0, s, xyz, n, g, hm, hchunk, w.bhist,
                          reinterpret_cast<int*>(w.count + 1));
       O3DX_TRY(exclusive_scan_i32(w.bhist, w.boff, (int64_t)kHBins * nblk, w.scan_tmp, s));
-      hipLaunchKernelGGL(k_hbin_scatter, dim3(nblk), dim3(kBinBlock), hscatter_lds_bytes(), s, xyz, n, g, hm, w.boff,
+      hipLaunchKernelGGL(k_hbin_scatter, dim3(nblk), dim3(kBinBlock), hscatter_lds_bytes(), s, xyz, n, g, hm, hchunk, w.boff,
                          w.entries);
       hipLaunchKernelGGL(k_hbin_reduce, dim3(kHBins), dim3(kHReduceBlock), 0, s, w.entries, w.boff, (int)nblk, slots,
                          w.flags, trace ? w.table : nullptr, trace ? w.vid : nullptr,
@@ -1197,15 +1281,16 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     else if (rep_xyz)
       hipLaunchKernelGGL(k_gather_xyz, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, rep_xyz);
     if (early) {
-      // the counts' copy is queued first, then the hook's work (the table
-      // geometry, occupancy not yet known): the host waits for the copy only
-      // (measured: the copy on a side stream, behind the gather, left a
-      // 6-7 us launch gap before the hook's kernels instead of the 5 us copy)
-      O3DX_TRY(read_back_begin(w.count, 3 * sizeof(int64_t), s));
+      // the hook's work (the table geometry, occupancy not yet known) is
+      // queued right behind the gathers; the host then waits for the counts
+      // the compaction posted (earlier: a 5 us copy kernel queued in between)
       const double gv[12] = {g.mnx + (double)g.kx0 * g.vs, g.mny, g.mnz, g.vs, (double)g.nx, (double)g.ny,
                              (double)g.nz, 1.0, -1.0, (double)g.kx0, 0.0, nvox};
       O3DX_TRY(hook(hook_ctx, gv, vox));
-      O3DX_TRY(read_back_end(counts, 3 * sizeof(int64_t)));
+      if (posted)
+        O3DX_TRY(post_wait(counts_post, counts, 3 * sizeof(int64_t), s));
+      else
+        O3DX_TRY(read_back(counts, w.count, 3 * sizeof(int64_t), s));
     } else {
       O3DX_TRY(read_back(counts, w.count, 3 * sizeof(int64_t), s));
     }

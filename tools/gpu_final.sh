@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-end evidence (ROUND, default r04), in two GPU calls:
+# Round-end evidence (ROUND, default r05), in two GPU calls:
 #   bash tools/gpu_final.sh tests   — the full -m gpu suite + smoke(), every normal
 #                                     row's parity logged to profiles-bound gpurun_out/\${R}_parity_report.jsonl
 #   bash tools/gpu_final.sh bench   — PMC passes (profiles/pmc_traffic.json refreshed
@@ -9,7 +9,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-R=${ROUND:-r04}
+R=${ROUND:-r05}
 if [ "$1" = tests ]; then
   export O3DX_PARITY_LOG=$PWD/gpurun_out/${R}_parity_report.jsonl
   rm -f "$O3DX_PARITY_LOG"
@@ -25,11 +25,11 @@ rm -rf gpurun_out/pmc
 bash tools/pmc.sh gpurun_out/pmc -- python tools/prof_kernels.py ${PMC_WHAT:-all} > gpurun_out/pmc.log 2>&1 || exit $?
 python tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_summary.json || exit $?
 python - <<'PYEOF' || exit $?
-import json
+import json, os
 old = json.load(open("profiles/pmc_traffic.json"))
 new = json.load(open("gpurun_out/pmc_summary.json"))
 old["kernels"].update(new["kernels"])
-old["round"] = "r04"
+old["round"] = os.environ.get("ROUND", "r05")
 for p in ("profiles/pmc_traffic.json", "gpurun_out/pmc_traffic.json"):
     with open(p, "w") as f:
         json.dump(old, f, indent=1, sort_keys=True)
