@@ -364,14 +364,33 @@ __device__ __forceinline__ int knn_search_dev64(const GridView& g, double qx, do
 // SHARE: the lanes calling together share first bounds (below); every lane
 // of the wave that runs the search must call it at once.
 // F64: a float64 grid (GridView::pts64), q in the cloud's own frame.
-template <bool SHARE = false, bool F64 = false>
+// EXT (the ICP loop's skip proof, icp.hip k_icp_step): the search covers the
+// ball of radius sqrt(best) + ext instead of sqrt(best), and *margin receives
+// a lower bound of (distance of any other target point) - (best distance):
+// every other point examined in that ball has its exact distance kept, every
+// point not examined lies beyond it.  Same result (best) either way.
+template <bool SHARE = false, bool F64 = false, bool EXT = false>
 __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, double qy, double qz, double radius,
-                                             double* best_d2, int* best_pos, int prior = -1) {
+                                             double* best_d2, int* best_pos, int prior = -1, double ext = 0.0,
+                                             double* margin = nullptr) {
   double bd = INFINITY;
   int bi = -1, bp = -1;
-  if (g.n == 0) {
+  double sd = INFINITY;  // EXT: smallest exact d^2 of the other examined points
+  auto finish = [&]() {
     *best_d2 = bd;
-    *best_pos = -1;
+    *best_pos = bp;
+    if constexpr (EXT) {
+      if (bi < 0) {
+        *margin = 0.0;
+      } else {
+        const double db = sqrt(bd);
+        *margin = fmin(sqrt(sd), db + ext) - db;
+      }
+    }
+  };
+  if (g.n == 0) {
+    bp = -1;
+    finish();
     return -1;
   }
   // q in the grid's frame (float64 grids: relative to o64)
@@ -401,10 +420,13 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
       const double d = exact_d2<F64>(g, qx, qy, qz, p, v);
       const int oi = __float_as_int(v.w);
       if (d < r2lim && lex_less(d, oi, bd, bi < 0 ? 0x7fffffff : bi)) {
+        if (EXT) sd = fmin(sd, bd);  // the former best is another point now
         bd = d;
         bi = oi;
         bp = p;
-        thr = bound_of(sqrt(d));
+        thr = bound_of(sqrt(d) + ext);
+      } else if (EXT && oi != bi) {  // (the best itself may be visited twice)
+        sd = fmin(sd, d);
       }
     }
   };
@@ -466,8 +488,7 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
           for (int x = x0; x <= x1; ++x)
             if (!own_seen || x != cx || y != cy || z != cz) visit_cell(x, y, z);
       search_stats(g, st_cells, st_cands, 2);
-      *best_d2 = bd;
-      *best_pos = bp;
+      finish();
       return bi;
     }
   }
@@ -535,8 +556,7 @@ __device__ __forceinline__ int nn_search_dev(const GridView& g, double qx, doubl
     if (bi < 0) ring_walk(true);
     ring_walk(false);
     search_stats(g, st_cells + rows, st_cands, r + 1);
-    *best_d2 = bd;
-    *best_pos = bp;
+    finish();
     return bi;
   }
 }

@@ -254,6 +254,7 @@ O3DX_HD inline void icp_metrics(const double* sums, int64_t ns, double* fit, dou
 // The device-resident state of one accumulate / registration.
 struct IcpState {
   double T[16];
+  double Tp[16];  // the previous step's T (the skip proof's motion bound)
   double absmax[3];
   double sums[kNS];   // the last accumulate's
   double fit, rmse;
@@ -263,6 +264,7 @@ struct IcpState {
 };
 
 O3DX_HD inline void state_set_T(IcpState& st, const double* T, double max_corr) {
+  for (int i = 0; i < 16; ++i) st.Tp[i] = st.T[i];
   for (int i = 0; i < 16; ++i) st.T[i] = T[i];
   icp_fx_exps(st.absmax, st.T, max_corr, st.q);
 }
@@ -277,9 +279,17 @@ struct Mat4 {
 // cells; else plain (n,3) float32 in caller order.  F64 (the float64
 // boundary): double4 (x, y, z, original index) of o3dx_spatial_sort_f64, or
 // plain (n,3) float64.
+// Eigen 4x4 * (x,y,z,1): ((T0 x + T1 y) + T2 z) + T3 per row
+__device__ __forceinline__ void apply_T(const double* t, double x, double y, double z, double* px, double* py,
+                                        double* pz) {
+  *px = ((t[0] * x + t[1] * y) + t[2] * z) + t[3];
+  *py = ((t[4] * x + t[5] * y) + t[6] * z) + t[7];
+  *pz = ((t[8] * x + t[9] * y) + t[10] * z) + t[11];
+}
+
 template <bool SORTED, bool F64 = false>
 __device__ __forceinline__ int64_t icp_source(const void* __restrict__ src_, int64_t j, const Mat4& T, double* px,
-                                              double* py, double* pz) {
+                                              double* py, double* pz, double* raw = nullptr) {
   double x, y, z;
   int64_t i;
   if constexpr (F64) {
@@ -309,11 +319,12 @@ __device__ __forceinline__ int64_t icp_source(const void* __restrict__ src_, int
     y = src[3 * i + 1];
     z = src[3 * i + 2];
   }
-  const double* t = T.m;
-  // Eigen 4x4 * (x,y,z,1): ((T0 x + T1 y) + T2 z) + T3 per row
-  *px = ((t[0] * x + t[1] * y) + t[2] * z) + t[3];
-  *py = ((t[4] * x + t[5] * y) + t[6] * z) + t[7];
-  *pz = ((t[8] * x + t[9] * y) + t[10] * z) + t[11];
+  if (raw) {
+    raw[0] = x;
+    raw[1] = y;
+    raw[2] = z;
+  }
+  apply_T(T.m, x, y, z, px, py, pz);
   return i;
 }
 
@@ -439,12 +450,20 @@ __device__ __forceinline__ unsigned icp_xcd_block(unsigned b, unsigned nb) {
 // copies (acc[copy][2 kNS]).  mpos[j]
 // = the match's sorted target position (-1: none).  Integer sums: the same
 // bits for any split of the source over lanes, blocks or ranks.
-template <bool SORTED, bool F64 = false>
+// round a non-negative double down to float
+__device__ __forceinline__ float float_down(double x) {
+  float f = (float)x;
+  if ((double)f > x && f > 0.0f) f = __int_as_float(__float_as_int(f) - 1);
+  return f;
+}
+
+template <bool SORTED, bool F64 = false, bool SKIP = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_icp_step(const void* __restrict__ src, int64_t ns, GridView g,
                                                      const float4* __restrict__ tnorm,
                                                      const IcpState* __restrict__ st, double radius,
                                                      int32_t* __restrict__ mpos, int use_prior,
-                                                     int64_t* __restrict__ acc) {
+                                                     int64_t* __restrict__ acc, float* __restrict__ budget,
+                                                     double ext) {
   __shared__ int64_t sh[kBlock / 64][2 * kNS];
   if (st->done) return;  // converged: the loop's remaining steps do nothing
   Mat4 T;
@@ -460,10 +479,53 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     int pos = -1;
     double px = 0, py = 0, pz = 0, d2 = 0;
     if (j < ns) {
-      icp_source<SORTED, F64>(src, j, T, &px, &py, &pz);
-      // the previous iteration's match as the starting bound (exact either way)
-      nn_search_dev<true, F64>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
-      mpos[j] = pos;
+      double raw[3];
+      icp_source<SORTED, F64>(src, j, T, &px, &py, &pz, raw);
+      bool kept = false;
+      if (SKIP && use_prior) {
+        // Skip proof: the last full search of this point left every other
+        // target point at least budget[j] farther than its match (EXT below),
+        // less twice each later motion.  The point moved by delta since the
+        // previous step (|T p - Tp p|, from the same products the step forms),
+        // so the match stays the unique nearest — the same (d^2, index) minimum
+        // a full search returns — while budget > 2 delta (+ a rounding guard).
+        const float b = budget[j];
+        const int mp = mpos[j];
+        if (mp >= 0 && b > 0.0f) {
+          double qx, qy, qz;
+          apply_T(st->Tp, raw[0], raw[1], raw[2], &qx, &qy, &qz);
+          const double dx = px - qx, dy = py - qy, dz = pz - qz;
+          const double guard = 1e-12 * (fabs(px) + fabs(py) + fabs(pz));
+          const double left = (double)b - 2.0 * (sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 1e-12) + guard);
+          if (left > 0.0) {
+            const int m = mp;
+            double d;
+            if constexpr (F64) {
+              d = dist2_d4(px, py, pz, g.pts64[m]);
+            } else {
+              const float4 v = g.pts[m];
+              d = exact_d2<false>(g, px, py, pz, m, v);
+            }
+            if (d < radius * radius) {
+              kept = true;
+              pos = m;
+              d2 = d;
+              budget[j] = float_down(left);
+            }
+          }
+        }
+      }
+      if (!kept) {
+        // the previous iteration's match as the starting bound (exact either way)
+        if constexpr (SKIP) {
+          double marg;
+          nn_search_dev<true, F64, true>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1, ext, &marg);
+          budget[j] = pos >= 0 ? float_down(marg) : 0.0f;
+        } else {
+          nn_search_dev<true, F64>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
+        }
+        mpos[j] = pos;
+      }
     }
     const bool m = pos >= 0;
     double J[6] = {0, 0, 0, 0, 0, 0}, r = 0;
@@ -677,6 +739,7 @@ struct AccWs {
   int64_t* digits;
   int32_t* cj;
   int32_t* mpos;
+  float* budget;  // the device loop's skip proof: margin left per source point
   uint8_t* flags;
   int32_t* src_idx;
   int32_t* scan_tmp;
@@ -693,6 +756,7 @@ static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
   w->digits = ar.take<int64_t>(2 * kNS);
   w->cj = ar.take<int32_t>(ns);
   w->mpos = ar.take<int32_t>(ns);
+  w->budget = ar.take<float>(ns);
   w->flags = ar.take<uint8_t>(ns + 16);
   w->src_idx = ar.take<int32_t>(ns);
   w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(ns));
@@ -782,22 +846,29 @@ static int source_absmax(const void* src_, int64_t ns, bool sorted, AccWs& w, hi
 
 // use_prior: mpos holds the previous step's matches on this source (the loop)
 // a float64 target (g.pts64) takes a float64 source
+// skip: the device loop's skip proof (w.budget; k_icp_step), whose full
+// searches cover a quarter cell beyond the match for the margin
 static void launch_step(const void* src, int64_t ns, bool sorted, const GridView& g, const float4* tn,
-                        double radius, AccWs& w, hipStream_t s, int use_prior = 0) {
+                        double radius, AccWs& w, hipStream_t s, int use_prior = 0, bool skip = false) {
   const unsigned nb = step_blocks(ns);
+  const double ext = 0.25 * (double)g.h;
   KTimer km("icp_match", s);
-  if (g.pts64 && sorted)
-    hipLaunchKernelGGL((k_icp_step<true, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
-                       use_prior, w.acc);
-  else if (g.pts64)
-    hipLaunchKernelGGL((k_icp_step<false, true>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
-                       use_prior, w.acc);
-  else if (sorted)
-    hipLaunchKernelGGL((k_icp_step<true, false>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
-                       use_prior, w.acc);
-  else
-    hipLaunchKernelGGL((k_icp_step<false, false>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos,
-                       use_prior, w.acc);
+#define O3DX_STEP(SO, F6, SK)                                                                                     \
+  hipLaunchKernelGGL((k_icp_step<SO, F6, SK>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos, \
+                     use_prior, w.acc, w.budget, ext)
+  const bool f64 = g.pts64 != nullptr;
+  if (skip) {
+    if (f64 && sorted) O3DX_STEP(true, true, true);
+    else if (f64) O3DX_STEP(false, true, true);
+    else if (sorted) O3DX_STEP(true, false, true);
+    else O3DX_STEP(false, false, true);
+  } else {
+    if (f64 && sorted) O3DX_STEP(true, true, false);
+    else if (f64) O3DX_STEP(false, true, false);
+    else if (sorted) O3DX_STEP(true, false, false);
+    else O3DX_STEP(false, false, false);
+  }
+#undef O3DX_STEP
 }
 // correspondences of the last step into corr_out (pairs by original index)
 static int corr_of_last_step(const void* src, int64_t ns, bool sorted, const GridView& g, AccWs& w, hipStream_t s,
@@ -969,11 +1040,13 @@ static int run_loop(const void* src, int64_t ns, bool sorted, const GridView& g,
   O3DX_HIP(hipMemcpyAsync(w.st, &hs, sizeof(IcpState), hipMemcpyHostToDevice, s));
   O3DX_HIP(hipMemsetAsync(w.acc, 0, (size_t)kIcpCopies * 2 * kNS * sizeof(int64_t), s));
   const int iters = std::max(max_iteration, 0);
+  // O3DX_ICP_SKIP=0 (tests, A/B): every step searches in full
+  const bool skip = !(getenv("O3DX_ICP_SKIP") && atoi(getenv("O3DX_ICP_SKIP")) == 0);
   {
     KTimer kt("icp_loop", s);
     for (int it = 0; it <= iters; ++it) {
       // from the second step on, the previous step's matches seed the search
-      launch_step(src, ns, sorted, g, tn, max_corr, w, s, it > 0);
+      launch_step(src, ns, sorted, g, tn, max_corr, w, s, it > 0, skip);
       hipLaunchKernelGGL(k_icp_finish, dim3(1), dim3(1024), 0, s, w.st, w.acc, ns, max_corr, rel_fit, rel_rmse, it,
                          iters);
     }
