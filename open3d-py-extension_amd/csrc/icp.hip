@@ -261,6 +261,8 @@ struct IcpState {
   int32_t q[kNS];
   int32_t done;   // the loop has converged: later steps and finishes return at once
   int32_t iters;  // updates applied
+  int32_t ext_on;    // the device loop: this step searches the extended ball (margins for the skip proof)
+  int32_t ext_prev;  // ... and the previous one did (the margins are valid)
 };
 
 O3DX_HD inline void state_set_T(IcpState& st, const double* T, double max_corr) {
@@ -457,15 +459,27 @@ __device__ __forceinline__ float float_down(double x) {
   return f;
 }
 
-template <bool SORTED, bool F64 = false, bool SKIP = false>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_icp_step(const void* __restrict__ src, int64_t ns, GridView g,
+#ifndef ICP_W2
+#define ICP_W2 6
+#endif
+#ifndef ICP_W1
+#define ICP_W1 8
+#endif
+// MODE 0: the plain step (accumulate); the device loop launches MODE 1 and 2
+// each step, and the one the state picks runs: 1 the plain search, 2 the skip
+// proof with extended-ball searches (SKIP)
+template <bool SORTED, bool F64 = false, int MODE = 0>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? ICP_W2 : ICP_W1))) k_icp_step(const void* __restrict__ src, int64_t ns, GridView g,
                                                      const float4* __restrict__ tnorm,
                                                      const IcpState* __restrict__ st, double radius,
                                                      int32_t* __restrict__ mpos, int use_prior,
                                                      int64_t* __restrict__ acc, float* __restrict__ budget,
                                                      double ext) {
+  constexpr bool SKIP = MODE == 2;
   __shared__ int64_t sh[kBlock / 64][2 * kNS];
   if (st->done) return;  // converged: the loop's remaining steps do nothing
+  if (MODE == 1 && st->ext_on) return;
+  if (MODE == 2 && !st->ext_on) return;
   Mat4 T;
 #pragma unroll
   for (int i = 0; i < 16; ++i) T.m[i] = st->T[i];
@@ -477,12 +491,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     // cells its waves probe stay in its own L2
     const int64_t j = (int64_t)icp_xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
     int pos = -1;
-    double px = 0, py = 0, pz = 0, d2 = 0;
+    double px = 0, py = 0, pz = 0, d2 = 0, vx = 0, vy = 0, vz = 0;
+    float4 nt = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j < ns) {
       double raw[3];
       icp_source<SORTED, F64>(src, j, T, &px, &py, &pz, raw);
       bool kept = false;
-      if (SKIP && use_prior) {
+      if (SKIP && use_prior && st->ext_prev) {
         // Skip proof: the last full search of this point left every other
         // target point at least budget[j] farther than its match (EXT below),
         // less twice each later motion.  The point moved by delta since the
@@ -492,26 +507,39 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
         const float b = budget[j];
         const int mp = mpos[j];
         if (mp >= 0 && b > 0.0f) {
+          // the match's point and normal, both gathers in flight at once
+          double cx, cy, cz;
+          if constexpr (F64) {
+            const double4 c = g.pts64[mp];
+            cx = c.x;
+            cy = c.y;
+            cz = c.z;
+          } else {
+            const float4 c = g.pts[mp];
+            cx = c.x;
+            cy = c.y;
+            cz = c.z;
+          }
+          const float4 cn = tnorm[mp];
           double qx, qy, qz;
           apply_T(st->Tp, raw[0], raw[1], raw[2], &qx, &qy, &qz);
           const double dx = px - qx, dy = py - qy, dz = pz - qz;
           const double guard = 1e-12 * (fabs(px) + fabs(py) + fabs(pz));
           const double left = (double)b - 2.0 * (sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 1e-12) + guard);
-          if (left > 0.0) {
-            const int m = mp;
-            double d;
-            if constexpr (F64) {
-              d = dist2_d4(px, py, pz, g.pts64[m]);
-            } else {
-              const float4 v = g.pts[m];
-              d = exact_d2<false>(g, px, py, pz, m, v);
-            }
-            if (d < radius * radius) {
-              kept = true;
-              pos = m;
-              d2 = d;
-              budget[j] = float_down(left);
-            }
+          // the match's exact d^2 at the new position (nanoflann order, as exact_d2)
+          const double ex = px - cx, ey = py - cy, ez = pz - cz;
+          double d = ex * ex;
+          d = d + ey * ey;
+          d = d + ez * ez;
+          if (left > 0.0 && d < radius * radius) {
+            kept = true;
+            pos = mp;
+            d2 = d;
+            vx = cx;
+            vy = cy;
+            vz = cz;
+            nt = cn;
+            budget[j] = float_down(left);
           }
         }
       }
@@ -525,6 +553,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
           nn_search_dev<true, F64>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1);
         }
         mpos[j] = pos;
+        if (pos >= 0) {
+          if constexpr (F64) {
+            const double4 v = g.pts64[pos];
+            vx = v.x;
+            vy = v.y;
+            vz = v.z;
+          } else {
+            const float4 v = g.pts[pos];
+            vx = v.x;
+            vy = v.y;
+            vz = v.z;
+          }
+          nt = tnorm[pos];
+        }
       }
     }
     const bool m = pos >= 0;
@@ -532,20 +574,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     const double one = m ? 1.0 : 0.0;
     if (!m) d2 = 0.0;
     if (m) {
-      double vx, vy, vz;
-      if constexpr (F64) {
-        const double4 v = g.pts64[pos];
-        vx = v.x;
-        vy = v.y;
-        vz = v.z;
-      } else {
-        const float4 v = g.pts[pos];
-        vx = v.x;
-        vy = v.y;
-        vz = v.z;
-      }
-      const float4 nt = tnorm[pos];
-      const double nx = nt.x, ny = nt.y, nz = nt.z;
+    const double nx = nt.x, ny = nt.y, nz = nt.z;
       r = ((px - vx) * nx + (py - vy) * ny) + (pz - vz) * nz;
       J[0] = py * nz - pz * ny;
       J[1] = pz * nx - px * nz;
@@ -620,7 +649,7 @@ __global__ void __launch_bounds__(1024) k_icp_collect(int64_t* __restrict__ acc,
 // remain — the solve and T <- update * T with the next fx exponents.
 __global__ void __launch_bounds__(1024) k_icp_finish(IcpState* __restrict__ st, int64_t* __restrict__ acc,
                                                      int64_t ns, double max_corr, double rel_fit, double rel_rmse,
-                                                     int it, int max_it) {
+                                                     int it, int max_it, double ext) {
   __shared__ int64_t red[16][2 * kNS];
   __shared__ IcpState ls;
   __shared__ double sums[kNS];
@@ -650,8 +679,20 @@ __global__ void __launch_bounds__(1024) k_icp_finish(IcpState* __restrict__ st, 
       double upd[16], T[16];
       solve_update(sm, upd);
       mat4_mul(upd, ls.T, T);
+      // the update's motion bound over the source box: |(T - T_old) p| per row
+      double mv = 0.0;
+      for (int r = 0; r < 3; ++r) {
+        const double e = fabs(T[4 * r] - ls.T[4 * r]) * ls.absmax[0] + fabs(T[4 * r + 1] - ls.T[4 * r + 1]) * ls.absmax[1] +
+                         fabs(T[4 * r + 2] - ls.T[4 * r + 2]) * ls.absmax[2] + fabs(T[4 * r + 3] - ls.T[4 * r + 3]);
+        mv += e * e;
+      }
       state_set_T(ls, T, max_corr);
       ls.iters = it + 1;
+      // the next step searches the extended ball (margins for the skip proof)
+      // once the updates move the source by less than half of the extension:
+      // before that the margins could not survive the next motion anyway
+      ls.ext_prev = ls.ext_on;
+      ls.ext_on = ext > 0.0 && sqrt(mv) < 0.5 * ext ? 1 : 0;
     }
   }
   __syncthreads();
@@ -757,6 +798,7 @@ static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
   w->cj = ar.take<int32_t>(ns);
   w->mpos = ar.take<int32_t>(ns);
   w->budget = ar.take<float>(ns);
+
   w->flags = ar.take<uint8_t>(ns + 16);
   w->src_idx = ar.take<int32_t>(ns);
   w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(ns));
@@ -853,21 +895,24 @@ static void launch_step(const void* src, int64_t ns, bool sorted, const GridView
   const unsigned nb = step_blocks(ns);
   const double ext = 0.25 * (double)g.h;
   KTimer km("icp_match", s);
-#define O3DX_STEP(SO, F6, SK)                                                                                     \
-  hipLaunchKernelGGL((k_icp_step<SO, F6, SK>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos, \
+#define O3DX_STEP(SO, F6, MO)                                                                                     \
+  hipLaunchKernelGGL((k_icp_step<SO, F6, MO>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos, \
                      use_prior, w.acc, w.budget, ext)
+#define O3DX_STEPS(MO)                         \
+  do {                                         \
+    if (f64 && sorted) O3DX_STEP(true, true, MO);   \
+    else if (f64) O3DX_STEP(false, true, MO);       \
+    else if (sorted) O3DX_STEP(true, false, MO);    \
+    else O3DX_STEP(false, false, MO);               \
+  } while (0)
   const bool f64 = g.pts64 != nullptr;
-  if (skip) {
-    if (f64 && sorted) O3DX_STEP(true, true, true);
-    else if (f64) O3DX_STEP(false, true, true);
-    else if (sorted) O3DX_STEP(true, false, true);
-    else O3DX_STEP(false, false, true);
+  if (skip) {  // the state picks one of the two at run time
+    O3DX_STEPS(1);
+    O3DX_STEPS(2);
   } else {
-    if (f64 && sorted) O3DX_STEP(true, true, false);
-    else if (f64) O3DX_STEP(false, true, false);
-    else if (sorted) O3DX_STEP(true, false, false);
-    else O3DX_STEP(false, false, false);
+    O3DX_STEPS(0);
   }
+#undef O3DX_STEPS
 #undef O3DX_STEP
 }
 // correspondences of the last step into corr_out (pairs by original index)
@@ -1048,7 +1093,7 @@ static int run_loop(const void* src, int64_t ns, bool sorted, const GridView& g,
       // from the second step on, the previous step's matches seed the search
       launch_step(src, ns, sorted, g, tn, max_corr, w, s, it > 0, skip);
       hipLaunchKernelGGL(k_icp_finish, dim3(1), dim3(1024), 0, s, w.st, w.acc, ns, max_corr, rel_fit, rel_rmse, it,
-                         iters);
+                         iters, skip ? 0.25 * (double)g.h : 0.0);
     }
   }
   O3DX_HIP(hipGetLastError());

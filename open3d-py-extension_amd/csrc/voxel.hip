@@ -522,7 +522,7 @@ __host__ __device__ inline uint64_t geom_key(const VoxelGeom& g, int64_t n) {
 }
 
 __host__ __device__ inline void fused_plan(const double mn[3], const double mx[3], double vs, int64_t n, int allow,
-                                           uint64_t skip_key, BinPlan* P) {
+                                           uint64_t skip_key, BinPlan* P, uint64_t one_copy_key = ~0ull) {
   P->ok = 0;
   P->cap = 0;
   double dims[3];
@@ -546,14 +546,15 @@ __host__ __device__ inline void fused_plan(const double mn[3], const double mx[3
   if (seg > INT32_MAX || !((double)seg >= 1.03 * full + 2048.0) || geom_key(g, n) == skip_key) return;
   P->g = g;
   P->b = b;
-  P->b.ncp = seg_copies(b.nb);
+  P->b.ncp = geom_key(g, n) == one_copy_key ? 1 : seg_copies(b.nb);
   P->cap = (int)seg;
   P->ok = 1;
 }
 
 // The same plan on a given geometry (the slab path's x-key window: g.kx0,
 // g.nx = the window's width).
-inline void fused_plan_geom(const VoxelGeom& g, int64_t n, int allow, uint64_t skip_key, BinPlan* P) {
+inline void fused_plan_geom(const VoxelGeom& g, int64_t n, int allow, uint64_t skip_key, BinPlan* P,
+                            uint64_t one_copy_key = ~0ull) {
   P->ok = 0;
   P->cap = 0;
   const double nvox = (double)g.nx * (double)g.ny * (double)g.nz;
@@ -565,7 +566,7 @@ inline void fused_plan_geom(const VoxelGeom& g, int64_t n, int allow, uint64_t s
   if (seg > INT32_MAX || !((double)seg >= 1.03 * full + 2048.0) || geom_key(g, n) == skip_key) return;
   P->g = g;
   P->b = b;
-  P->b.ncp = seg_copies(b.nb);
+  P->b.ncp = geom_key(g, n) == one_copy_key ? 1 : seg_copies(b.nb);
   P->cap = (int)seg;
   P->ok = 1;
 }
@@ -576,12 +577,12 @@ struct PlanTail {
   double vs;
   int64_t n;
   int allow;
-  uint64_t skip_key;
+  uint64_t skip_key, one_copy_key;
   BinPlan* plan;
   __device__ void operator()(const double* mm) const {
     const double mn[3] = {mm[0], mm[1], mm[2]}, mx[3] = {mm[3], mm[4], mm[5]};
     BinPlan P;
-    fused_plan(mn, mx, vs, n, allow, skip_key, &P);
+    fused_plan(mn, mx, vs, n, allow, skip_key, &P, one_copy_key);
     *plan = P;
   }
 };
@@ -984,6 +985,10 @@ static int64_t dense_cap(int64_t n) { return dense_cap_hd(n); }
 // binned entries: n for the scanned layout, + 1/2 + 2^20 of segment slack
 static int64_t entries_cap(int64_t n) { return entries_cap_hd(n); }
 static thread_local uint64_t g_fused_overflow_key = ~0ull;  // last geometry whose one-pass binning overflowed
+// ... whose copied segments overflowed: the one-pass binning retries with one
+// copy per brick (a spatially ordered cloud sends each brick's
+// points from a few consecutive blocks, i.e. into one or two copies)
+static thread_local uint64_t g_fused_one_copy_key = ~0ull;
 static int64_t bin_blocks(int64_t n) { return (n + kBinChunk - 1) / kBinChunk; }
 static int64_t bin_hist_ints(int64_t n) { return bin_blocks(n) * kMaxBuckets; }
 static int64_t hash_cap(int64_t n) {
@@ -1102,7 +1107,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       const float* part;
       int nb;
       O3DX_TRY(aabb_begin_partial(xyz, n, w.aabb, s, zc, zb, zf, extra_zero, &o, &part, &nb));
-      const PlanTail tail{voxel_size, n, allow_fused, g_fused_overflow_key, w.plan};
+      const PlanTail tail{voxel_size, n, allow_fused, g_fused_overflow_key, g_fused_one_copy_key, w.plan};
       hipLaunchKernelGGL(k_aabb_final_tail<PlanTail>, dim3(1), dim3(kBlock), 0, s, part, nb, n, o, tail);
       launch_fused<true>(kFuseMaxBricks, n, s, xyz, n, (const BinPlan*)w.plan, w.boff, w.entries,
                          (voxel_of_point || cubic_id) ? w.vid : nullptr, reinterpret_cast<int*>(w.count + 1));
@@ -1162,7 +1167,9 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
   bool fused_ok = true;
   int attempts_made = 0;
   HostPost counts_post;
-  for (int attempt = 0; attempt < 4; ++attempt) {
+  int fused_ncp = 0;  // segment copies of the attempt's one-pass binning (0: not that path)
+  for (int attempt = 0; attempt < 5; ++attempt) {
+    fused_ncp = 0;
     attempts_made = attempt;
     bool posted = false;
     grid_kept = false;
@@ -1181,10 +1188,11 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
       // geometry did not overflow last time)
       BinPlan plan;
       if (xwin)  // the slab's window: its own geometry (round 4; count + scatter before)
-        fused_plan_geom(g, n, fused_ok && allow_fused, g_fused_overflow_key, &plan);
+        fused_plan_geom(g, n, fused_ok && allow_fused, g_fused_overflow_key, &plan, g_fused_one_copy_key);
       else
-        fused_plan(mn, mx, voxel_size, n, fused_ok && allow_fused, g_fused_overflow_key, &plan);
+        fused_plan(mn, mx, voxel_size, n, fused_ok && allow_fused, g_fused_overflow_key, &plan, g_fused_one_copy_key);
       const bool fused = plan.ok;
+      fused_ncp = fused ? plan.b.ncp : 0;
       if (fused) bricks = plan.b;  // the one-pass plan's (larger) bricks
       const int cap = fused ? plan.cap : 0;
       if (fused && attempt == 0 && pre_launched) {
@@ -1296,9 +1304,13 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
     }
     int errflag = (int)(counts[1] & 0xffffffff);
     if (errflag == 0) break;
-    if (errflag & 16) {  // a brick outgrew its one-pass segment: count + scatter (and remember)
-      g_fused_overflow_key = geom_key(g, n);
-      fused_ok = false;
+    if (errflag & 16) {  // a brick outgrew its one-pass segment (remembered per geometry):
+      if (fused_ncp > 1) {  // copied segments: one copy per brick next
+        g_fused_one_copy_key = geom_key(g, n);
+      } else {  // one copy: count + scatter
+        g_fused_overflow_key = geom_key(g, n);
+        fused_ok = false;
+      }
       if (!(errflag & ~16)) continue;
       errflag &= ~16;
     }

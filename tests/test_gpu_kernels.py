@@ -58,18 +58,24 @@ def test_voxel_uniform(dev, n, seed):
         assert np.array_equal(rep, NPR.voxel_down_sample(pts.numpy(), vs))
 
 
-@pytest.mark.parametrize("case", ["uniform", "hot_brick"])
+@pytest.mark.parametrize("case", ["uniform", "hot_brick", "spatially_sorted"])
 def test_voxel_binning_one_pass_and_fallback(dev, monkeypatch, case):
     """The one-pass binning into fixed per-brick segments (uniform cloud) and
     its fall-back to count + scatter when a brick outgrows its segment (75 %
     of the points in one brick): representatives, trace and the one-call
     normals equal the oracle's / the two-pass path's.  The hot-brick one-call
     run fires the normals on attempt 0's table and must redo them on the
-    rebuilt one (geom[10])."""
+    rebuilt one (geom[10]).  A spatially sorted cloud sends each brick's
+    points from one or two blocks, i.e. into one of the brick's segment
+    copies: it overflows the copies and retries with one copy per brick."""
     rng = np.random.default_rng(41)
     if case == "uniform":
         n = 400_001
         pts = rng.random((n, 3)).astype(np.float32)
+    elif case == "spatially_sorted":
+        n = 400_001
+        pts = ops.spatial_sort(torch.from_numpy(rng.random((n, 3)).astype(np.float32)).to(dev))[:, :3]
+        pts = pts.contiguous().cpu().numpy()
     else:
         n = 400_003
         pts = np.concatenate([rng.random((300_003, 3)) * 0.01, rng.random((100_000, 3))]).astype(np.float32)
@@ -407,6 +413,35 @@ def test_icp_device_loop_equals_host_loop(dev, rel):
                                relative_rmse=rel)
     assert np.array_equal(one["transformation"], T) and one["fitness"] == fit
     assert torch.equal(one["correspondence_set"], corr)
+
+
+@pytest.mark.parametrize("n", [300_000, 2_000_000])
+def test_icp_skip_proof_equals_full_search(dev, monkeypatch, n):
+    """The device loop's skip proof (icp.hip k_icp_step MODE 2: a point keeps
+    its match while twice its motion stays below the margin its last
+    extended-ball search left) returns the correspondences of a full search
+    in every iteration: T, fitness, rmse and the final correspondence set
+    equal the loop with every step searching (O3DX_ICP_SKIP=0) to the bit,
+    and most converged steps search far fewer points (the debug search
+    counters count searched queries only)."""
+    from open3dpypro import _native as N
+    src, tgt = _icp_case(n, seed=21)
+    t = torch.from_numpy(tgt).to(dev)
+    n_ = ops.estimate_normals(t, knn=30)
+    target = ops.ICPTarget(t, n_, 0.02)
+    s4 = ops.spatial_sort(torch.from_numpy(src).to(dev))
+    runs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("O3DX_ICP_SKIP", mode)
+        N.search_stats(True)
+        res = target.register(s4, max_iteration=30, relative_fitness=0.0, relative_rmse=0.0, want_corr=True)
+        runs[mode] = (res, N.search_stats()["queries"])
+        N.search_stats(False)
+    (a, qa), (b, qb) = runs["1"], runs["0"]
+    assert np.array_equal(a["transformation"], b["transformation"])
+    assert a["fitness"] == b["fitness"] and a["inlier_rmse"] == b["inlier_rmse"]
+    assert torch.equal(a["correspondence_set"], b["correspondence_set"])
+    assert qb >= 31 * n and qa < 0.5 * qb, (qa, qb)
 
 
 def test_icp_accumulate_sorted_source_layout(dev):
