@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define O3DX_ABI_VERSION 5
+#define O3DX_ABI_VERSION 6
 
 #define O3DX_OK 0
 #define O3DX_EIO (-5)
@@ -224,6 +224,58 @@ int o3dx_voxel_table_build_deferred(const float* xyz_dev, int64_t n,
                                     int64_t kx0, int64_t kx1, float* voxel_pts_dev,
                                     int64_t voxel_cells, double* geom_host,
                                     int64_t* status_dev, void* stream);
+
+/* The slab step without host waits between the voxel window and the verdict
+ * (ABI 6; open3dpypro.distributed.voxel_normals_slabs, the reference's
+ * per-rank placement processors.py:206-207 scaled to one cloud over ranks).
+ * o3dx_voxel_down_sample_window_deferred: o3dx_voxel_down_sample_window
+ * (no table kept) whose counts stay on the device: counts_dev[3] (int64)
+ * = {m, error bits, occupancy}; error bit 16 = the one-pass binning
+ * overflowed (re-run the synchronous form), any other bit = points outside
+ * the window.  rep_idx_dev / rep_xyz_dev hold m rows.
+ * o3dx_slab_halo_pack: over the window's m reps (capacity cap rows): the
+ * reps' global ids rg_out[i] = gidx_dev[rep_idx[i]] (int64), and, when
+ * pcap > 0, send_dev (2 pcap, 4) float32 = the reps whose x key
+ * floor((x - min_x) / voxel_size) is < k_lo_send (has_lo) in rows
+ * [0, pcap), >= k_hi_send (has_hi) in rows [pcap, 2 pcap), each part in rep
+ * order as (x, y, z, int32 bits of the global id), padded with NaN rows of
+ * id INT32_MAX.  Workspace o3dx_slab_pack_workspace_bytes(cap).
+ * o3dx_slab_halo_merge: the own reps and the received rows (na rows from the
+ * lower neighbour then nb from the upper, each ascending in id, padding
+ * last) merged into ascending global id: ux_dev (ux_rows >= cap + na + nb,
+ * 3) float32, NaN past the union; own_pos_dev[i] = the union row of own rep
+ * i; nu_dev[0] = the union size.
+ * o3dx_slab_verdict: after the normals of the union rows (normals_union,
+ * kd2_union from o3dx_estimate_normals_voxel): normals_own[i] = the own
+ * reps' normals; info_dev[5] (int64) = {1 if some own rep's sqrt(kd2) >=
+ * (t + halo)(1 - 1e-9), t its distance to the interior faces x_lo (has_lo)
+ * / x_hi (has_hi); m; union size; the window's error bits; status_dev[0]}.
+ * No host synchronisation in any of them. */
+int o3dx_voxel_down_sample_window_deferred(const float* xyz_dev, int64_t n,
+                                           const double* min_bound_host,
+                                           const double* max_bound_host,
+                                           double voxel_size, int64_t kx0, int64_t kx1,
+                                           int32_t* rep_idx_dev, float* rep_xyz_dev,
+                                           int64_t* counts_dev, void* ws,
+                                           size_t ws_bytes, void* stream);
+size_t o3dx_slab_pack_workspace_bytes(int64_t cap);
+int o3dx_slab_halo_pack(const float* rep_xyz_dev, const int32_t* rep_idx_dev,
+                        const int64_t* gidx_dev, const int64_t* counts_dev,
+                        int64_t cap, double min_x, double voxel_size,
+                        int64_t k_lo_send, int64_t k_hi_send, int has_lo, int has_hi,
+                        int64_t* rg_out_dev, float* send_dev, int64_t pcap,
+                        void* ws, size_t ws_bytes, void* stream);
+int o3dx_slab_halo_merge(const float* rep_xyz_dev, const int64_t* rg_dev,
+                         const int64_t* counts_dev, int64_t cap,
+                         const float* recv_dev, int64_t na, int64_t nb,
+                         float* ux_dev, int64_t ux_rows, int32_t* own_pos_dev,
+                         int64_t* nu_dev, void* stream);
+int o3dx_slab_verdict(const float* rep_xyz_dev, const int32_t* own_pos_dev,
+                      const int64_t* counts_dev, int64_t cap,
+                      const float* kd2_union_dev, const float* normals_union_dev,
+                      double x_lo, double x_hi, int has_lo, int has_hi, double halo,
+                      const int64_t* nu_dev, const int64_t* status_dev,
+                      float* normals_own_dev, int64_t* info_dev, void* stream);
 
 /* ---------------------------------------------------------------- normals
  * Replaces o3d PointCloud.estimate_normals(search_param,

@@ -1066,7 +1066,7 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
                       double voxel_size, int32_t* rep_idx, float* rep_xyz, int64_t* m_host, int32_t* voxel_of_point,
                       int32_t* cubic_id, float* vox, int64_t vox_cap, double* geom, void* ws, size_t ws_bytes,
                       void* stream, const int64_t* xwin = nullptr, VoxelHook hook = nullptr, void* hook_ctx = nullptr,
-                      ZeroSpan extra_zero = {}) {
+                      ZeroSpan extra_zero = {}, int64_t* counts_dev = nullptr) {
   if (geom)
     for (int k = 0; k < 12; ++k) geom[k] = 0.0;
   if (n < 0 || (n > 0 && (!xyz || !rep_idx)) || !m_host)
@@ -1288,6 +1288,16 @@ static int voxel_impl(const float* xyz, int64_t n, const double* min_bound_host,
                          reinterpret_cast<float4*>(vox));
     else if (rep_xyz)
       hipLaunchKernelGGL(k_gather_xyz, dim3(gg), dim3(kBlock), 0, s, xyz, rep_idx, w.count, rep_xyz);
+    if (counts_dev) {
+      // deferred (o3dx_voxel_down_sample_window_deferred): {m, error bits,
+      // occupancy} stay on the device for the caller; no retry (an overflow
+      // of the one-pass binning is error bit 16, the caller re-runs the
+      // synchronous form)
+      O3DX_HIP(hipMemcpyAsync(counts_dev, w.count, 3 * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+      O3DX_HIP(hipGetLastError());
+      *m_host = -1;
+      return 0;
+    }
     if (early) {
       // the hook's work (the table geometry, occupancy not yet known) is
       // queued right behind the gathers; the host then waits for the counts
@@ -1369,6 +1379,21 @@ extern "C" int o3dx_voxel_down_sample_window(const float* xyz, int64_t n, const 
   const int64_t win[2] = {kx0, kx1};
   return voxel_impl(xyz, n, min_bound_host, max_bound_host, voxel_size, rep_idx, rep_xyz, m_host, nullptr, nullptr,
                     voxel_pts, voxel_pts ? voxel_cells : 0, geom_host, ws, ws_bytes, stream, win);
+}
+
+extern "C" int o3dx_voxel_down_sample_window_deferred(const float* xyz, int64_t n, const double* min_bound_host,
+                                                      const double* max_bound_host, double voxel_size, int64_t kx0,
+                                                      int64_t kx1, int32_t* rep_idx, float* rep_xyz,
+                                                      int64_t* counts_dev, void* ws, size_t ws_bytes, void* stream) {
+  if (!min_bound_host || !max_bound_host || !counts_dev)
+    return fail(O3DX_EINVAL, "o3dx_voxel_down_sample_window_deferred: bounds and counts_dev are required");
+  const int64_t win[2] = {kx0, kx1};
+  int64_t m_host = 0;
+  if (n == 0) {  // nothing queued: the counts are zero
+    O3DX_HIP(hipMemsetAsync(counts_dev, 0, 3 * sizeof(int64_t), as_stream(stream)));
+  }
+  return voxel_impl(xyz, n, min_bound_host, max_bound_host, voxel_size, rep_idx, rep_xyz, &m_host, nullptr, nullptr,
+                    nullptr, 0, nullptr, ws, ws_bytes, stream, win, nullptr, nullptr, {}, counts_dev);
 }
 
 // ------------------------------------------------------ float64 clouds

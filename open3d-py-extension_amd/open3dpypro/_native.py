@@ -14,7 +14,9 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libo3dx.so")
+# O3DX_LIB: another in-tree build of the same library (A/B timing of kernel
+# variants in one GPU call; tools/ scripts only)
+LIB_PATH = os.environ.get("O3DX_LIB") or os.path.join(_HERE, "_lib", "libo3dx.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "o3dx.h")
 
 SEARCH_KNN, SEARCH_RADIUS, SEARCH_HYBRID = 0, 1, 2
@@ -122,6 +124,13 @@ _SIGS = {
     "o3dx_registration_icp_f64_workspace_bytes": (_SZ, [_I64]),
     "o3dx_registration_icp_point_to_plane_f64": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,
                                                          _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    # the slab step's device side (ABI 6)
+    "o3dx_voxel_down_sample_window_deferred": (_I32, [_P, _I64, _P, _P, _D, _I64, _I64, _P, _P, _P, _P, _SZ, _P]),
+    "o3dx_slab_pack_workspace_bytes": (_SZ, [_I64]),
+    "o3dx_slab_halo_pack": (_I32, [_P, _P, _P, _P, _I64, _D, _D, _I64, _I64, _I32, _I32, _P, _P, _I64, _P, _SZ,
+                                   _P]),
+    "o3dx_slab_halo_merge": (_I32, [_P, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _P]),
+    "o3dx_slab_verdict": (_I32, [_P, _P, _P, _I64, _P, _P, _D, _D, _I32, _I32, _D, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

@@ -29,6 +29,7 @@ group they degrade to the single-process identity.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import time
 from typing import Callable, Optional, Tuple
@@ -73,7 +74,8 @@ def global_bounds_device(xyz: torch.Tensor, group=None, with_count: bool = False
     device AABB of this rank's points (o3dx_aabb_device, no host wait), one
     all-reduce, one host read.  +inf / -inf when every rank is empty.
     with_count: also the largest point count of any rank (folded into the
-    same all-reduce as -count), returned third."""
+    same all-reduce as -count), returned third; with_count="both": the
+    smallest as well, fourth."""
     from . import ops
 
     world, _ = _world(group)
@@ -82,12 +84,15 @@ def global_bounds_device(xyz: torch.Tensor, group=None, with_count: bool = False
         v = torch.cat([mm[:3], -mm[3:]])
     else:
         v = torch.full((6,), math.inf, dtype=torch.float64, device=xyz.device)
-    if with_count:
-        v = torch.cat([v, torch.full((1,), -float(xyz.shape[0]), dtype=torch.float64, device=v.device)])
+    if with_count:  # -count (the largest) and count (the smallest) in the same MIN all-reduce
+        c = float(xyz.shape[0])
+        v = torch.cat([v, torch.tensor([-c, c], dtype=torch.float64).to(v.device)])
     if world > 1:
         v = v.to(_comm_device(group))
         dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
     h = v.cpu().numpy()
+    if with_count == "both":
+        return h[:3].copy(), -h[3:6].copy(), int(-h[6]), int(h[7])
     if with_count:
         return h[:3].copy(), -h[3:6].copy(), int(-h[6])
     return h[:3].copy(), -h[3:].copy()
@@ -749,7 +754,144 @@ def _stamp(timings, name, t0):
         timings[name] = round((time.perf_counter() - t0) * 1e3, 4)
 
 
+def _deferred_eligible(keys, layer, hk, nmin, nmax):
+    """Whether the deferred slab step applies at halo width hk, from values
+    every rank holds alike (global bounds, slab keys, the smallest / largest
+    point count): each slab's window has a dense voxel table (the library's
+    rule, 2 n + 2^20 cells, with the smallest rank's n), the halo packets have
+    their fixed size (hk x layer rows within the data) and each rank's union
+    table over slab + halo stays within the same rule."""
+    if nmin <= 0:
+        return False
+    widest = max(keys[r + 1] - keys[r] for r in range(len(keys) - 1))
+    lim = 2 * nmin + (1 << 20)
+    return ((widest + 6) * layer <= lim and hk * layer <= max(nmax, 1 << 20)
+            and (widest + 2 * hk) * layer <= lim)
+
+
 def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presorted, timings=None):
+    """The HIP form of voxel_normals_slabs with one host wait per halo round.
+
+    A presorted cloud (each rank's points already in its slab: a spatially
+    tiled dataset, the C4 layout) whose slabs hold dense voxel tables runs the
+    step without reading the representative count back: the voxel window
+    keeps its counts on the device (o3dx_voxel_down_sample_window_deferred),
+    the halo packets are formed, merged into global order and the halo proof
+    checked by library kernels that read that count (o3dx_slab_halo_pack /
+    _merge / _verdict), and the host reads the verdict all-gather once per
+    round — {fail, m, union size, window error bits, table status} of every
+    rank — which also tells it m.  Host waits per step: the bounds (their
+    all-reduce also carries the smallest and largest point count, so every
+    rank takes the same path) and one per halo round.  Any other input, and
+    a window whose one-pass binning overflowed, takes the synchronous form
+    (_voxel_normals_slabs_sync) on every rank alike."""
+    from . import ops
+
+    world, rank = _world(group)
+    if world == 1 or not presorted or xyz.shape[0] > np.iinfo(np.int32).max:
+        return _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted, timings)
+    vs = float(voxel_size)
+    t0 = time.perf_counter()
+    mn, mx, nmax, nmin = global_bounds_device(xyz, group, with_count="both")
+    _stamp(timings, "bounds", t0)
+    if not np.all(np.isfinite(mn)):
+        raise RuntimeError("voxel_normals_slabs: the cloud is empty on every rank")
+    keys = slab_bounds(mn, mx, vs, world)
+    k_lo, k_hi, nkeys = keys[rank], keys[rank + 1], keys[-1]
+    dims = np.floor(np.maximum(np.asarray(mx) - np.asarray(mn), 0.0) / vs) + 1
+    layer = int(dims[1] * dims[2])
+    hk = max(1, int(math.ceil(float(halo) / vs))) if halo else 3
+    min_keys = min(keys[r + 1] - keys[r] for r in range(world))
+    if min_keys < 1 or not _deferred_eligible(keys, layer, hk, nmin, nmax):
+        return _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted, timings)
+    L = N.load()
+    dev = xyz.device
+    st = N.stream_ptr(dev)
+    x = xyz.contiguous()
+    g = gidx.to(torch.int64).contiguous()
+    n = int(x.shape[0])
+    mnb, mxb = np.ascontiguousarray(mn, np.float64), np.ascontiguousarray(mx, np.float64)
+    pmn, pmx = mnb.ctypes.data_as(ctypes.c_void_p), mxb.ctypes.data_as(ctypes.c_void_p)
+    ws = N.workspace(L.o3dx_voxel_workspace_bytes(n), dev)
+    rep = torch.empty(n, dtype=torch.int32, device=dev)
+    rxyz = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    cnt = torch.empty(3, dtype=torch.int64, device=dev)
+    N.check(L.o3dx_voxel_down_sample_window_deferred(N.ptr(x), n, pmn, pmx, vs, int(k_lo), int(k_hi), N.ptr(rep),
+                                                     N.ptr(rxyz), N.ptr(cnt), N.ptr(ws), ws.numel(), st),
+            "voxel_normals_slabs")
+    _stamp(timings, "reps_queued", t0)
+    has_lo, has_hi = int(rank > 0), int(rank < world - 1)
+    x_lo, x_hi = float(mn[0]) + k_lo * vs, float(mn[0]) + k_hi * vs
+    cd = _comm_device(group)
+    rg = torch.empty(n, dtype=torch.int64, device=dev)
+    table = None
+    while True:
+        if hk >= min_keys:
+            raise RuntimeError("voxel_normals_slabs: the kNN halo is wider than a slab; use fewer ranks")
+        if not _deferred_eligible(keys, layer, hk, nmin, nmax):  # every rank alike
+            return _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted, timings)
+        # halo packets: the reps of the hk voxel layers next to each interior
+        # face, fixed size (hk x layer rows: at most one rep per voxel), padded
+        pcap = hk * layer
+        send = torch.empty((2 * pcap, 4), dtype=torch.float32, device=dev)
+        pws = N.workspace(L.o3dx_slab_pack_workspace_bytes(n), dev, "slab")
+        N.check(L.o3dx_slab_halo_pack(N.ptr(rxyz), N.ptr(rep), N.ptr(g), N.ptr(cnt), n, float(mn[0]), vs,
+                                      int(k_lo + hk), int(k_hi - hk), has_lo, has_hi, N.ptr(rg), N.ptr(send), pcap,
+                                      N.ptr(pws), pws.numel(), st), "voxel_normals_slabs")
+        ss = [0] * world
+        if has_lo:
+            ss[rank - 1] = pcap
+        if has_hi:
+            ss[rank + 1] = pcap
+        part = send if (has_lo and has_hi) else (send[:pcap] if has_lo else send[pcap:])
+        recv = torch.empty((sum(ss), 4), dtype=torch.float32, device=cd)
+        dist.all_to_all_single(recv, part.to(cd), output_split_sizes=ss, input_split_sizes=ss, group=group)
+        recv = recv.to(dev)
+        _stamp(timings, f"halo{hk}_exchanged", t0)
+        na = pcap if has_lo else 0  # the lower neighbour's rows come first
+        nb = int(recv.shape[0]) - na
+        ux_rows = n + na + nb
+        ux = torch.empty((ux_rows, 3), dtype=torch.float32, device=dev)
+        own_pos = torch.empty(n, dtype=torch.int32, device=dev)
+        nu = torch.empty(1, dtype=torch.int64, device=dev)
+        N.check(L.o3dx_slab_halo_merge(N.ptr(rxyz), N.ptr(rg), N.ptr(cnt), n, N.ptr(recv), na, nb, N.ptr(ux), ux_rows,
+                                       N.ptr(own_pos), N.ptr(nu), st), "voxel_normals_slabs")
+        _stamp(timings, f"halo{hk}_merged", t0)
+        # the union's voxel table over slab + halo (padding rows skipped; its
+        # error bits join the verdict), the normals straight off it
+        kx0, kx1 = max(k_lo - hk, 0), min(k_hi + hk, nkeys)
+        status = torch.zeros(1, dtype=torch.int64, device=dev)
+        grid = ops.voxel_table(ux, vs, mn, mx, kx0, kx1, table, status=status)
+        table = grid.pts
+        nrm_u, kd2_u = ops.estimate_normals(ux, knn=knn, voxel_grid=grid, return_kdist=True)
+        nrm = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        info = torch.empty(5, dtype=torch.int64, device=dev)
+        N.check(L.o3dx_slab_verdict(N.ptr(rxyz), N.ptr(own_pos), N.ptr(cnt), n, N.ptr(kd2_u), N.ptr(nrm_u), x_lo,
+                                    x_hi, has_lo, has_hi, hk * vs, N.ptr(nu), N.ptr(status), N.ptr(nrm), N.ptr(info),
+                                    st), "voxel_normals_slabs")
+        _stamp(timings, f"normals{hk}_queued", t0)
+        info = info.to(cd)
+        parts = [torch.empty_like(info) for _ in range(world)]
+        dist.all_gather(parts, info, group=group)
+        tab = torch.stack(parts).cpu().numpy()
+        _stamp(timings, f"verdict{hk}", t0)
+        err = tab[:, 3]
+        if (err & ~16).any():
+            raise RuntimeError("voxel_normals_slabs(presorted=True): a point lies outside its rank's slab")
+        if (err & 16).any():  # a one-pass binning overflowed somewhere: the synchronous form re-bins
+            return _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted, timings)
+        if tab[:, 4].any():
+            raise RuntimeError("voxel_normals_slabs: the halo table build failed (bits %d)"
+                               % int(np.bitwise_or.reduce(tab[:, 4])))
+        n_total = int(tab[:, 1].sum())
+        short = any(r[1] > 0 and r[2] < min(knn, n_total) for r in tab)  # fewer than k points: unverifiable
+        if not tab[:, 0].any() and not short:
+            m = int(tab[rank, 1])
+            return rg[:m], rxyz[:m], nrm[:m]
+        hk *= 2
+
+
+def _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted, timings=None):
     """The HIP form of voxel_normals_slabs: every rank keeps a voxel table of
     its slab widened by the halo (global keys, x-key window), so the normals
     run straight off the table (k_normals_stile) on own + halo reps; the halo
