@@ -137,6 +137,55 @@ __global__ void __launch_bounds__(kBigBlock) k_grid_big_cells(const float4* __re
   }
 }
 
+// Radix path of grid_build (large cell arrays: a surface cloud's fine grid
+// holds up to cap_mult x n cells, 240 MB at C5, and the counting sort's
+// returning atomics into it are random read-modify-writes of HBM lines):
+// the cell keys are sorted with their point indices by a stable radix sort
+// (in-cell order = ascending index, as the ordered counting path gives), the
+// cell counts come from the runs of equal keys, and one gather writes the
+// sorted points.  No atomics on the cell array.
+__global__ void __launch_bounds__(kBlock) k_grid_keys(const float* __restrict__ xyz, int64_t n, GridView g,
+                                                      uint32_t* __restrict__ key, int32_t* __restrict__ val) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int cx, cy, cz;
+    grid_cell(g, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], cx, cy, cz);
+    key[i] = (uint32_t)cell_index(g, cx, cy, cz);
+    val[i] = (int32_t)i;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_run_flags(const uint32_t* __restrict__ skey, int64_t n,
+                                                      uint8_t* __restrict__ flags) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x)
+    flags[p] = (p == 0 || skey[p] != skey[p - 1]) ? 1 : 0;
+}
+
+// runs[j] = the first sorted position of the j-th distinct key (nr of them)
+__global__ void __launch_bounds__(kBlock) k_run_counts(const uint32_t* __restrict__ skey, const int32_t* __restrict__ runs,
+                                                       const int64_t* __restrict__ nr, int64_t n,
+                                                       int32_t* __restrict__ count) {
+  const int64_t m = *nr;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = runs[j], b = j + 1 < m ? (int64_t)runs[j + 1] : n;
+    count[skey[a]] = (int32_t)(b - a);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_grid_gather(const float* __restrict__ xyz, int64_t n,
+                                                        const int32_t* __restrict__ sval, float4* __restrict__ pts,
+                                                        const float* __restrict__ extra_src, float4* __restrict__ extra,
+                                                        const int32_t* __restrict__ ids) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = sval[p];
+    pts[p] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __int_as_float(ids ? ids[i] : (int)i));
+    if (extra) extra[p] = make_float4(extra_src[3 * i], extra_src[3 * i + 1], extra_src[3 * i + 2], 0.f);
+  }
+}
+
+// from this many cells (and points) the fine pass takes the radix path
+constexpr int64_t kRadixMinCells = (int64_t)1 << 24;
+constexpr int64_t kRadixMinPoints = (int64_t)1 << 20;
+
 // cell-index capacity: cap_mult cells per point (the dense start table costs
 // 8 B per cell: count + start)
 static int64_t cap_cells(int64_t n, int cap_mult) { return std::max<int64_t>((int64_t)cap_mult * n, 4096); }
@@ -282,6 +331,37 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
     g.bnx = (int)((d[0] + 7) / 8);
     g.bny = (int)((d[1] + 7) / 8);
     const int64_t nc = cell_space(d, blocked);
+    // the fine pass of a surface cloud (pass 1) over a large cell array: the
+    // radix path (O3DX_GRID_ATOMIC: tests, the counting path instead)
+    if (pass == 1 && nc >= kRadixMinCells && n >= kRadixMinPoints && n < INT32_MAX && !getenv("O3DX_GRID_ATOMIC")) {
+      int bits = 1;
+      while (bits < 32 && ((int64_t)1 << bits) < nc) ++bits;
+      const size_t need = cell_sort_temp_bytes(n, bits);
+      const size_t avail = L.count - L.tmp_extra;  // tmp_extra: unused on this path
+      if (need <= avail) {
+        KTimer kt_sort("grid_sort", s);
+        uint32_t* key = reinterpret_cast<uint32_t*>(G.cell);
+        int32_t* val = G.rank;
+        uint32_t* skey = reinterpret_cast<uint32_t*>(w + L.tmp);
+        int32_t* sval = reinterpret_cast<int32_t*>(skey + n);
+        const unsigned gn = grid_for(n, kBlock, 8192);
+        hipLaunchKernelGGL(k_grid_keys, dim3(gn), dim3(kBlock), 0, s, xyz, n, g, key, val);
+        O3DX_TRY(cell_sort(key, skey, val, sval, n, bits, w + L.tmp_extra, avail, s));
+        // the runs of equal keys -> cell counts -> starts
+        uint8_t* flags = reinterpret_cast<uint8_t*>(G.rank);  // val is dead after the sort
+        int32_t* runs = G.cell;                                // so is key
+        int64_t* nr = G.scratch + 2;
+        hipLaunchKernelGGL(k_run_flags, dim3(gn), dim3(kBlock), 0, s, skey, n, flags);
+        O3DX_TRY(compact_flags(flags, n, runs, nullptr, nr, G.scan_tmp, s));
+        O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
+        hipLaunchKernelGGL(k_run_counts, dim3(gn), dim3(kBlock), 0, s, skey, runs, nr, n, G.count);
+        O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));
+        hipLaunchKernelGGL(k_grid_gather, dim3(gn), dim3(kBlock), 0, s, xyz, n, sval, G.pts, extra_src, extra_sorted,
+                           ids);
+        O3DX_HIP(hipGetLastError());
+        break;
+      }
+    }
     KTimer kt_count("grid_count", s);
     O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
     if (n > 0)

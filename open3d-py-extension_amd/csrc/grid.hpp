@@ -700,6 +700,10 @@ unsigned long long* search_stats_ptr();  // device counters when stats are enabl
 // inside a cell; for consumers that do not depend on it).
 // ids: the w stored per point (default: its index; forces ordered = false).
 // max_h: upper bound on h (0 = none).
+// search.hip: stable radix sort of (cell key < 2^bits, point index) pairs
+size_t cell_sort_temp_bytes(int64_t n, int bits);
+int cell_sort(const uint32_t* key, uint32_t* skey, const int32_t* val, int32_t* sval, int64_t n, int bits, void* tmp,
+              size_t tmp_bytes, hipStream_t s);
 int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, void* ws, size_t ws_bytes,
                hipStream_t s, GridBuild* out, float4* extra_sorted = nullptr, const float* extra_src = nullptr,
                bool blocked = false, int cap_mult = 4, bool ordered = true, const int32_t* ids = nullptr,

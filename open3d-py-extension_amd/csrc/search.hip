@@ -90,6 +90,22 @@ struct SearchWs {
   size_t sort_bytes;
 };
 
+// Stable radix sort of (cell key, point index) pairs for grid_build's
+// large cell arrays (grid.hip): keys below 2^bits.
+size_t cell_sort_temp_bytes(int64_t n, int bits) {
+  size_t b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)std::max<int64_t>(n, 1), 0,
+                                           bits);
+  return b;
+}
+
+int cell_sort(const uint32_t* key, uint32_t* skey, const int32_t* val, int32_t* sval, int64_t n, int bits, void* tmp,
+              size_t tmp_bytes, hipStream_t s) {
+  O3DX_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, key, skey, val, sval, (int)n, 0, bits, s));
+  return 0;
+}
+
 static size_t sort_temp_bytes(int64_t n) {
   size_t b = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,

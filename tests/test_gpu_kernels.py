@@ -312,6 +312,27 @@ def test_segment_plane_device_setup_equals_host(dev, monkeypatch, ransac_n):
     np.testing.assert_allclose(p_dev, rplane, rtol=0, atol=1e-9)
 
 
+def test_segment_plane_tiny_threshold_device_setup(dev, monkeypatch):
+    """A threshold tiny against the coordinates (a plane 1e3 units from the
+    origin, thr 2e-6): the culled sweep's guard (6 2^-24 S + 2^-20 thr <
+    thr / 2) fails, and the device-setup path replays it on the bounds it
+    reads back and recounts with the dense sweep — plane and
+    inliers equal the host-setup path's and the oracle's."""
+    n = 20_000
+    pts = S.planted_plane(n, 43, sigma=1e-6).numpy().astype(np.float64)
+    pts = (pts + np.array([1000.0, -700.0, 1000.0])).astype(np.float32)
+    samples = O.ransac_samples(n, 3, 300, 17)
+    x = torch.from_numpy(pts).to(dev)
+    p_dev, i_dev = ops.segment_plane(x, 2e-6, 3, 300, samples=samples)
+    monkeypatch.setenv("O3DX_RANSAC_HOST_SETUP", "1")
+    p_host, i_host = ops.segment_plane(x, 2e-6, 3, 300, samples=samples)
+    assert np.array_equal(np.asarray(p_dev), np.asarray(p_host))
+    assert torch.equal(i_dev, i_host)
+    rplane, rinl, _, _, _ = O.segment_plane(pts, 2e-6, 3, 300, samples)
+    assert np.array_equal(i_dev.cpu().numpy().astype(np.int64), rinl)
+    np.testing.assert_allclose(p_dev, rplane, rtol=0, atol=1e-9)
+
+
 def test_segment_plane_ties_small(dev):
     # tiny cloud: many hypotheses tie in count -> rmse tie-break path
     pts = S.planted_plane(60, 3).numpy()
@@ -917,3 +938,26 @@ def test_c2_pipeline_full_mantissa_coordinates(dev, n):
     assert_normals(f["normals"].cpu().numpy(), O.estimate_normals(reps, O.KNN, 30), reps, k=30,
                    what="c2_full_mantissa_1m")
     assert_neighbour_sets(dn.ids()[:m], reps, 30, "c2_full_mantissa_1m")
+
+
+def test_grid_radix_path_equals_counting_path(dev, monkeypatch):
+    """A surface cloud's fine grid over a large cell array is sorted by a
+    stable radix sort of the cell keys (grid.hip, no atomics on the cell
+    array); the counting path (O3DX_GRID_ATOMIC) gives the same grid: normals
+    and k-th-distance bounds bit for bit, the ICP target's registration the
+    same T, and the blocked spatial sort the same order."""
+    pts = S.box_surface(5_000_000, 61).to(dev)
+    src = S.apply_transform(S.box_surface(2_000_000, 62), S.rigid_transform()).to(dev)
+    runs = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("O3DX_GRID_ATOMIC", env)
+        nrm, kd2 = ops.estimate_normals(pts, knn=30, return_kdist=True)
+        tgt = ops.ICPTarget(pts, nrm, 0.02)
+        s4 = ops.spatial_sort(src)
+        reg = tgt.register(s4, max_iteration=5, relative_fitness=0.0, relative_rmse=0.0)
+        runs.append((nrm.cpu(), kd2.cpu(), reg["transformation"], s4.cpu()))
+    a, b = runs
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert np.array_equal(a[2], b[2])
+    assert torch.equal(a[3], b[3])
