@@ -182,6 +182,20 @@ __global__ void __launch_bounds__(kBlock) k_grid_gather(const float* __restrict_
   }
 }
 
+// the surface test of a large cloud on every `stride`-th point: no returning
+// atomics, no per-point writes (a surface puts hundreds of points in each
+// coarse cell, and the full count's returning atomics queue on those cells)
+__global__ void __launch_bounds__(kBlock) k_grid_count_sample(const float* __restrict__ xyz, int64_t n, GridView g,
+                                                              int stride, int32_t* __restrict__ count) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t * stride < n; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t * stride;
+    int cx, cy, cz;
+    grid_cell(g, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], cx, cy, cz);
+    atomicAdd(&count[cell_index(g, cx, cy, cz)], 1);
+  }
+}
+constexpr int kSampleStride = 8;
+
 // from this many cells (and points) the fine pass takes the radix path
 constexpr int64_t kRadixMinCells = (int64_t)1 << 24;
 constexpr int64_t kRadixMinPoints = (int64_t)1 << 20;
@@ -363,11 +377,37 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
       }
     }
     KTimer kt_count("grid_count", s);
+    bool sampled = false;
+    if (pass == 0 && n >= kRadixMinPoints && !getenv("O3DX_GRID_ATOMIC")) {
+      // large clouds: the surface test on a 1/8 sample (the occupied cells it
+      // sees are a lower bound, so its mean occupancy an upper bound of the
+      // cloud's); a surface goes straight to its fine pass, a volume to the
+      // full count at this h below
+      unsigned long long occ = 0;
+      O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
+      O3DX_HIP(hipMemsetAsync(G.scratch, 0, sizeof(int64_t), s));
+      hipLaunchKernelGGL(k_grid_count_sample, dim3(grid_for((n + kSampleStride - 1) / kSampleStride, kBlock, 8192)),
+                         dim3(kBlock), 0, s, xyz, n, g, kSampleStride, G.count);
+      hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(nc, kBlock, 1024)), dim3(kBlock), 0, s, G.count, nc,
+                         (unsigned long long*)G.scratch);
+      O3DX_TRY(read_back(&occ, G.scratch, sizeof(occ), s));
+      const double mean_occ = occ ? nn / (double)occ : nn;
+      if (mean_occ > 2.5 * target_occ) {
+        double hn = h * std::sqrt(target_occ / mean_occ);
+        if (min_h > 0) hn = std::max(hn, min_h);
+        hn = fit_cap(hn);
+        if (hn < h * 0.9) {
+          h = hn;
+          continue;
+        }
+      }
+      sampled = true;
+    }
     O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
     if (n > 0)
       hipLaunchKernelGGL(k_grid_count, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, xyz, n, g, G.count,
                          G.cell, G.rank);
-    if (pass == 0 && n > 64) {
+    if (pass == 0 && n > 64 && !sampled) {
       // surface-like clouds: occupied cells are far denser than the box average
       unsigned long long occ = 0;
       O3DX_HIP(hipMemsetAsync(G.scratch, 0, sizeof(int64_t), s));
