@@ -106,6 +106,100 @@ def test_c4_slabs_clustered_on_device():
     assert np.array_equal(nn[o], ref)
 
 
+def _presorted_share(pts, vs, rank, world):
+    """the rows of this rank's x-slab (a spatially tiled dataset), ascending"""
+    mn, mx = ops.aabb(pts)
+    keys = D.slab_bounds(mn, mx, vs, world)
+    kx = torch.floor((pts[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
+    return torch.nonzero((kx >= keys[rank]) & (kx < keys[rank + 1])).flatten()
+
+
+def _hollow_cloud():
+    """1.2M uniform points with the band |x - 0.5| < 0.12 thinned to 1 in 200:
+    over 2 slabs (face at x = 0.5) the reps near the face have their k-th
+    neighbour ~7 voxels away, so the first halos (3, 6 voxel layers) fail the
+    proof and the halo widens; the slabs stay dense enough for the deferred
+    step's voxel tables."""
+    n = 1_200_000
+    pts = S.uniform_cube(n, 46)
+    keep = ((pts[:, 0] - 0.5).abs() >= 0.12) | (torch.arange(n) % 200 == 0)
+    return pts[keep].contiguous(), S.voxel_size_for(n)
+
+
+def _hollow_rank(rank, world):
+    dev = torch.device("cuda:0")
+    pts, vs = _hollow_cloud()
+    x = pts.to(dev)
+    g = _presorted_share(x, vs, rank, world)
+    tl = {}
+    rg, rx, nrm = D.voxel_normals_slabs(x[g].contiguous(), g, vs, knn=30, presorted=True, timings=tl)
+    return rg, nrm, sorted(tl)
+
+
+def test_c4_slabs_presorted_deferred_widens_halo():
+    """The deferred slab step (presorted slabs: the window's counts stay on the
+    device, halo packets / merge / proof by library kernels, one verdict read
+    per round) on a cloud whose reps near the face need a wider halo: it takes
+    the deferred path, widens the halo on the verdict, and the result equals
+    the single-GPU one bit for bit."""
+    res = spawn(_hollow_rank)
+    dev = torch.device("cuda:0")
+    pts, vs = _hollow_cloud()
+    x = pts.to(dev)
+    mn, mx = ops.aabb(x)
+    out = ops.voxel_down_sample(x, vs, mn, mx)
+    ref = ops.estimate_normals(out["rep_xyz"], knn=30).cpu().numpy()
+    g = np.concatenate([r[0] for r in res])
+    nn = np.concatenate([r[1] for r in res])
+    o = np.argsort(g)
+    assert np.array_equal(g[o], out["rep_idx"].cpu().numpy().astype(np.int64))
+    assert np.array_equal(nn[o], ref)
+    for _, _, stamps in res:
+        assert "reps_queued" in stamps  # the deferred path ran
+        assert sum(1 for k in stamps if k.startswith("verdict")) >= 2, stamps  # the halo was widened
+
+
+def _gap_rank(rank, world):
+    """presorted over 3 ranks, the middle slab empty (nothing in the middle
+    third of x): every rank takes the synchronous path alike"""
+    dev = torch.device("cuda:0")
+    n = 300_000
+    pts = S.uniform_cube(n, 45)
+    pts[:, 0] = torch.where(pts[:, 0] < 0.5, pts[:, 0] * 0.6, 0.4 + pts[:, 0] * 0.6)
+    x = pts.to(dev)
+    vs = S.voxel_size_for(n)
+    g = _presorted_share(x, vs, rank, world)
+    tl = {}
+    rg, rx, nrm = D.voxel_normals_slabs(x[g].contiguous(), g, vs, knn=30, presorted=True, timings=tl)
+    return rg, nrm, sorted(tl)
+
+
+def test_c4_presorted_empty_slab_takes_sync_path():
+    """A presorted cloud with an empty slab: the bounds all-reduce's smallest
+    count is 0, so every rank takes the synchronous form alike; the result is
+    the single-GPU one."""
+    res = spawn(_gap_rank, world=3)
+    dev = torch.device("cuda:0")
+    n = 300_000
+    pts = S.uniform_cube(n, 45)
+    pts[:, 0] = torch.where(pts[:, 0] < 0.5, pts[:, 0] * 0.6, 0.4 + pts[:, 0] * 0.6)
+    x = pts.to(dev)
+    vs = S.voxel_size_for(n)
+    mn, mx = ops.aabb(x)
+    out = ops.voxel_down_sample(x, vs, mn, mx)
+    ref = ops.estimate_normals(out["rep_xyz"], knn=30).cpu().numpy()
+    g = np.concatenate([r[0] for r in res])
+    nn = np.concatenate([r[1] for r in res])
+    o = np.argsort(g)
+    assert np.array_equal(g[o], out["rep_idx"].cpu().numpy().astype(np.int64))
+    assert res[1][0].size == 0
+    for _, _, stamps in res:
+        assert "reps_queued" not in stamps
+    # the two non-empty slabs' normals: every row within 1e-5 of the oracle
+    reps = out["rep_xyz"].cpu().numpy()
+    assert_normals(nn[o], O.estimate_normals(reps, O.KNN, 30), reps, k=30, what="c4_gap_slabs")
+
+
 def _wide_cloud():
     """1000 blobs of 300 points (sigma 0.3 m) scattered over a 1 km cube, 5 cm
     voxels: the slab grid's cross-section (20000^2 voxels) dwarfs the points,
