@@ -1,13 +1,13 @@
 #!/bin/bash
 # A/B of a library variant (tools/build_variant.sh) on the bench's headline
 # step and kernel timers: the in-tree build, then _lib/var/libo3dx_$1.so.
-# Usage (via gpurun): bash tools/ab_bench.sh NAME [bench args...]
+# Usage (via gpurun): bash tools/ab_bench.sh NAME[,NAME...] [bench args...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 V=$1; shift
 mkdir -p gpurun_out
-for lib in base "$V"; do
+for lib in base ${V//,/ }; do
   if [ "$lib" = base ]; then unset O3DX_LIB; else export O3DX_LIB=$PWD/open3d-py-extension_amd/open3dpypro/_lib/var/libo3dx_$lib.so; fi
   timeout -k 10 300 python bench.py --no-cpu "$@" > gpurun_out/ab_$lib.json 2> gpurun_out/ab_$lib.err || exit 1
   python - "$lib" <<'PY'
