@@ -446,3 +446,20 @@ def test_icp_windowed_target_bit_identical(world, margin):
         assert fetches >= 1 and held < len(tgt)
     if margin == 0.0:
         assert max(r[3] for r in res) > 1
+
+
+def test_deferred_slab_eligibility_is_global():
+    """The deferred slab step's eligibility (distributed._deferred_eligible)
+    depends only on values every rank holds alike — the slab keys, the layer,
+    the halo width and the smallest / largest point count — so all ranks take
+    the same path; an empty rank, a window too sparse for a dense table, a
+    halo packet larger than the data or a union table beyond the dense rule
+    each send every rank to the synchronous form."""
+    keys = D.slab_bounds([0.0, 0.0, 0.0], [1.0, 1.0, 1.0], 0.01, 4)  # 101 keys, widest slab 26
+    layer = 101 * 101
+    assert D._deferred_eligible(keys, layer, 3, 2_000_000, 2_500_000)
+    assert not D._deferred_eligible(keys, layer, 3, 0, 2_500_000)           # an empty rank
+    assert not D._deferred_eligible(keys, 50_000_000, 3, 2_000_000, 2_500_000)  # sparse window
+    assert not D._deferred_eligible(keys, layer, 2000, 2_000_000, 2_500_000)   # halo packets beyond the data
+    big = D.slab_bounds([0.0, 0.0, 0.0], [1.0, 1.0, 1.0], 0.001, 2)        # 1001 keys, layer 1e6
+    assert not D._deferred_eligible(big, 1001 * 1001, 3, 100_000, 100_000)
