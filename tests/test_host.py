@@ -50,6 +50,28 @@ def test_library_host_only_entry_points():
     assert bad == -22 and b"ransac_n" in N.load().o3dx_last_error()
 
 
+def test_slab_entry_points_validate_before_touching_the_device():
+    """ABI 6's slab entry points reject bad arguments with -EINVAL (or
+    -ENOMEM for a short workspace) and a message, before any device call
+    (so this runs without a GPU)."""
+    L = N.load()
+    v = ctypes.c_void_p(8)  # never dereferenced: the checks come first
+    assert L.o3dx_slab_pack_workspace_bytes(1000) > 0
+    rc = L.o3dx_slab_halo_pack(v, v, v, None, 10, 0.0, 0.1, 1, 2, 1, 1, v, v, 4, v, 1 << 30, None)
+    assert rc == -22 and b"slab_halo_pack" in L.o3dx_last_error()
+    rc = L.o3dx_slab_halo_pack(v, v, v, v, 1000, 0.0, 0.1, 1, 2, 1, 1, v, v, 4, v, 16, None)
+    assert rc == -12 and b"workspace" in L.o3dx_last_error()
+    rc = L.o3dx_slab_halo_merge(v, v, v, 10, v, 4, 4, v, 17, v, v, None)  # ux rows < cap + na + nb
+    assert rc == -22 and b"slab_halo_merge" in L.o3dx_last_error()
+    rc = L.o3dx_slab_verdict(v, None, v, 10, v, v, 0.0, 1.0, 1, 1, 0.3, v, v, v, v, None)
+    assert rc == -22 and b"slab_verdict" in L.o3dx_last_error()
+    lo, hi = np.zeros(3), np.ones(3)
+    rc = L.o3dx_voxel_down_sample_window_deferred(v, 10, lo.ctypes.data_as(ctypes.c_void_p),
+                                                  hi.ctypes.data_as(ctypes.c_void_p), 0.1, 0, 5, v, v, None, v,
+                                                  1 << 30, None)
+    assert rc == -22 and b"counts_dev" in L.o3dx_last_error()
+
+
 def test_icp_solve_host():
     # JTJ = I, JTr = -x  ->  x; small rotation about z + translation
     x = np.array([0, 0, 0.01, 0.1, -0.2, 0.3])
