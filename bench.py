@@ -371,6 +371,38 @@ def c4_single_gpu(dev, args):
                               "algorithmic_bytes": "12 N + 28 M (SURVEY.md 8(d))"}}
 
 
+def f64_las(dev, args):
+    """The float64 boundary at C2's size: a 10M-point LAS-like scan (box
+    surface at a ~5e5 m offset, full-mantissa float64 that float32 cannot
+    hold) through voxel_down_sample (5 cm) + KNN30 normals on the
+    representatives, both on the float64 kernels (o3dx_*_f64); beside it the
+    same scan re-centred and rounded to float32 (the float32 kernels).
+    tools/f64_time.py times the whole chain (RANSAC, ICP too)."""
+    n = args.n
+    las = synthetic.las_scene(n, seed=0, device=dev)
+    x0 = torch.tensor(synthetic.LAS_OFFSET, dtype=torch.float64, device=dev)
+    out = {}
+    for tag, pts in (("f64", las), ("f32_recentred", (las - x0).float())):
+        def step():
+            reps = ops.voxel_down_sample(pts, 0.05)["rep_xyz"]
+            return reps, ops.estimate_normals(reps, knn=args.knn)
+
+        step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            reps, _nrm = step()
+        torch.cuda.synchronize(dev)
+        el = (time.perf_counter() - t0) / 3
+        out[tag] = {"ms": round(el * 1e3, 3), "voxels": int(reps.shape[0]),
+                    "Mpoints_per_s": round(n / el / 1e6, 2)}
+        del reps, _nrm, pts
+    del las
+    torch.cuda.empty_cache()
+    out["note"] = "two library calls (voxel_down_sample, estimate_normals) per step, 5 cm voxels, KNN30"
+    return {"f64_las": out}
+
+
 def c5_pipeline(dev, args):
     """C5's full pipeline on one GPU (200M points fit one MI355X's HBM):
     a 200M-point box-surface scene and an independent 200M-point sample of it
@@ -709,7 +741,8 @@ def main():
     if not args.no_secondary:
         for name, fn in (("secondary", lambda: secondary(dev, args)),
                          ("c4", lambda: c4_single_gpu(dev, args) if args.c4_n > 0 else {}),
-                         ("c5", lambda: c5_pipeline(dev, args) if args.c5_n > 0 else {})):
+                         ("c5", lambda: c5_pipeline(dev, args) if args.c5_n > 0 else {}),
+                         ("f64_las", lambda: f64_las(dev, args))):
             try:
                 line["extra"].update(fn())
             except RuntimeError as e:  # report, never hide
