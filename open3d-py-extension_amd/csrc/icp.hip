@@ -803,7 +803,9 @@ static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
   w->src_idx = ar.take<int32_t>(ns);
   w->scan_tmp = ar.take<int32_t>(compact_workspace_ints(ns));
   w->cnt = ar.take<int64_t>(2);
-  w->aabb = ar.take<char>(aabb_ws_bytes(ns));
+  // scratch of the source bounds: the float32 partials (aabb_ws_bytes) or,
+  // for a float64 source, the float64 ones (aabb64_ws_bytes, twice as wide)
+  w->aabb = ar.take<char>(std::max(aabb_ws_bytes(ns), aabb64_ws_bytes()));
   w->mm = ar.take<double>(8);
   return ar.used;
 }

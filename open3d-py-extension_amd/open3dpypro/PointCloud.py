@@ -142,7 +142,16 @@ class PointCloudBase:
         self._pts = None        # (N,3) float32 tensor on the device
         self._pts_host = None   # (N,3) float64 exact host copy (when supplied from host)
         self._pts64 = None      # device float64 copy of _pts_host (plane selections), made on demand
-        self._wide = False      # the float64 values are not float32-representable: hot path in float64
+        # _wide: SOME float64 value is not float32-representable, so every hot
+        # op runs its float64 kernels (o3dx_*_f64) to keep Open3D's float64
+        # arithmetic on the exact values.  This is not limited to georeferenced
+        # scans: np.random float64 arrays and a cloud after transform() with a
+        # general rotation (transform() re-calls set_points) qualify too.  The
+        # float64 path is slower (normals ~2-4x) and keeps no
+        # voxel table for the normals.  Pass float32 values (or
+        # points.astype(np.float32)) to opt into the float32 kernels: Open3D's
+        # result on those values is the same either way.
+        self._wide = False
         self._normals = None    # (N,3) float32 tensor
         self._colors = None     # (N,3) float32 tensor in [0,1]
         self.pcd_tree = None

@@ -788,7 +788,7 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
     from . import ops
 
     world, rank = _world(group)
-    if world == 1 or not presorted or xyz.shape[0] > np.iinfo(np.int32).max:
+    if world == 1 or not presorted:
         return _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted, timings)
     vs = float(voxel_size)
     t0 = time.perf_counter()
@@ -796,6 +796,8 @@ def _voxel_normals_slabs_device(xyz, gidx, voxel_size, knn, group, halo, presort
     _stamp(timings, "bounds", t0)
     if not np.all(np.isfinite(mn)):
         raise RuntimeError("voxel_normals_slabs: the cloud is empty on every rank")
+    if nmax > np.iinfo(np.int32).max:  # decided on the global count: every rank takes the same path
+        return _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted, timings)
     keys = slab_bounds(mn, mx, vs, world)
     k_lo, k_hi, nkeys = keys[rank], keys[rank + 1], keys[-1]
     dims = np.floor(np.maximum(np.asarray(mx) - np.asarray(mn), 0.0) / vs) + 1

@@ -678,7 +678,15 @@ class ICPTarget:
         sorted4 = src.ndim == 2 and src.shape[1] == 4
         if sorted4:
             N.require_device(src, "source points")
-            s = (src.double() if self.f64 else src.float()).contiguous()
+            # the index column's encoding follows the dtype (spatial_sort:
+            # int32 bits in a float32 column; spatial_sort_f64: the index as a
+            # double), so a cast would corrupt it: the sorted form must match
+            want = torch.float64 if self.f64 else torch.float32
+            if src.dtype != want:
+                raise RuntimeError(f"ICPTarget.register: a {'float64' if self.f64 else 'float32'} target takes the "
+                                   f"({'spatial_sort_f64' if self.f64 else 'spatial_sort'}) sorted source, got "
+                                   f"{src.dtype}")
+            s = src.contiguous()
         elif self.f64:
             s = _xyz64(src.to(self.xyz.device), "source points")
         else:

@@ -55,6 +55,26 @@ def test_voxel_grid_kept_until_points_change(bunny):
     assert_normals(down2.estimate_normals().get_normals(), exp, shifted, k=30, what="bunny_shifted")
 
 
+def test_transformed_cloud_path(bunny):
+    """Which kernels a float32-loaded cloud takes after transform(): a general
+    rotation leaves float64 values float32 cannot hold, so the cloud switches
+    to the float64 kernels (PointCloudBase._wide, documented in its
+    constructor); a float32 copy of the same values takes the float32 ones.
+    Both give Open3D's normals on the values they hold."""
+    pc = o3p.PointCloud(bunny.astype(np.float64))
+    assert not pc._wide
+    th = 0.3
+    T = np.eye(4)
+    T[:3, :3] = [[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]]
+    pc.transform(T)
+    assert pc._wide and pc._hot_points().dtype == torch.float64
+    p64 = pc.get_points()
+    assert_normals(pc.estimate_normals().get_normals(), O.estimate_normals(p64, O.KNN, 30), p64, k=30,
+                   what="bunny_rotated_f64")
+    narrow = o3p.PointCloud(p64.astype(np.float32))
+    assert not narrow._wide and narrow._hot_points().dtype == torch.float32
+
+
 def test_voxel_trace_api(bunny):
     pc = o3p.PointCloud(bunny.astype(np.float64))
     down, idxmat, vec = pc.voxel_down_sample_and_trace(0.01)

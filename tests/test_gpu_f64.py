@@ -191,3 +191,45 @@ def test_f64_pcd_f8_roundtrip(tmp_path, las_np):
     path.write_bytes(hdr.encode() + np.ascontiguousarray(pts, "<f8").tobytes())
     pc = PointCloud().read_pcd(str(path))
     assert pc._wide and np.array_equal(pc.get_points(), pts)
+
+
+@pytest.mark.parametrize("form", ["unsorted", "sorted_f64"])
+@pytest.mark.parametrize("skip", ["1", "0"])
+def test_f64_icp_target_register_forms(dev, monkeypatch, form, skip):
+    """ICPTarget(float64).register on an unsorted float64 source of > 200k
+    points with no absmax (the source bounds run through the float64 AABB
+    scratch) and on a spatial_sort_f64 source: the same T, fitness and rmse as
+    registration_icp_f64, with and without the skip proof."""
+    monkeypatch.setenv("O3DX_ICP_SKIP", skip)
+    n = 300_000
+    off = (12345.678, 23456.789, 98.765)
+    M = S.rigid_transform(1.0, t=(0.2, -0.12, 0.08))
+    tgt = S.las_scene(n, seed=0, offset=off, device=dev)
+    src = S.las_scene(n, seed=1, T=M, offset=off, device=dev)
+    tn = ops.estimate_normals(tgt, knn=30)
+    ref = ops.registration_icp(src, tgt, tn, 0.8, max_iteration=20, relative_fitness=0, relative_rmse=0,
+                               return_corr=False)
+    target = ops.ICPTarget(tgt, tn, 0.8)
+    s = src if form == "unsorted" else ops.spatial_sort_f64(src)
+    res = target.register(s, max_iteration=20, relative_fitness=0, relative_rmse=0)
+    np.testing.assert_allclose(res["transformation"], ref["transformation"], atol=1e-9)
+    assert abs(res["fitness"] - ref["fitness"]) < 1e-12
+    assert abs(res["inlier_rmse"] - ref["inlier_rmse"]) < 1e-9
+
+
+def test_f64_icp_target_sorted_dtype_mismatch(dev):
+    """A sorted source whose dtype does not match the target's raises instead
+    of casting (the index column's encoding differs between the two forms)."""
+    n = 5000
+    off = (12345.678, 23456.789, 98.765)
+    tgt64 = S.las_scene(n, seed=0, offset=off, device=dev)
+    tn = ops.estimate_normals(tgt64, knn=30)
+    t64 = ops.ICPTarget(tgt64, tn, 0.8)
+    src32 = (S.las_scene(n, seed=1, offset=off, device=dev) - torch.tensor(off, dtype=torch.float64,
+                                                                          device=dev)).float()
+    with pytest.raises(RuntimeError, match="sorted source"):
+        t64.register(ops.spatial_sort(src32), max_iteration=2)
+    tgt32 = (tgt64 - torch.tensor(off, dtype=torch.float64, device=dev)).float()
+    t32 = ops.ICPTarget(tgt32, ops.estimate_normals(tgt32, knn=30), 0.8)
+    with pytest.raises(RuntimeError, match="sorted source"):
+        t32.register(ops.spatial_sort_f64(src32.double()), max_iteration=2)
