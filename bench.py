@@ -10,16 +10,26 @@ same GPU: C3 (RANSAC 1000 hypotheses + point-to-plane ICP 30 iterations at
 the CPU baselines (the oracle, an Open3D-equivalent C++ restatement) of the
 voxel+normals step, RANSAC and ICP on the same inputs.
 
-N > 1 (torchrun, one process per GPU, RCCL): C4 — ONE 50M-point cloud tiled
-over the ranks as voxel-aligned x-slabs (each rank's points resident in its
-slab), one step = global AABB all-reduce, slab voxel reps, halo exchange of
-boundary representatives (all-to-all), normals off the slab's voxel table,
-halo proof all-reduce (open3dpypro.distributed.voxel_normals_slabs): strong
-scaling; plus the sharded ICP (RCCL moment all-gather per iteration).
-`value` = points of the whole job / max-over-ranks time.
+N > 1 (one process per GPU, RCCL): C2 per GPU, weak scaling — ONE
+uniform-random cloud of N x 10M points over [0,N) x [0,1)^2 (the C2 density,
+C2's voxel size), tiled over the ranks as voxel-aligned x-slabs (each rank's
+~10M points resident in its slab); one step = global AABB all-reduce, slab
+voxel reps, halo exchange of boundary representatives (all-to-all), normals
+off the slab's voxel table, halo-proof verdict all-gather
+(open3dpypro.distributed.voxel_normals_slabs).  `value` = points of the whole
+job / max-over-ranks time.  Beside it: C4 (ONE 50M cloud over the same ranks,
+strong scaling), the sharded ICP and the sharded C5 pipeline.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-   or: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Launch forms:
+  python bench.py --gpus N      (no WORLD_SIZE in the environment, N > 1): the
+      parent never touches a GPU; it starts fresh child processes, one per GPU
+      (RANK / LOCAL_RANK / WORLD_SIZE, RCCL), for 1, 2, 4, ... N ranks in turn
+      and prints ONE line: the N-rank figures, the whole 1 -> N curve
+      (`scaling_curve`, C2-per-GPU weak and C4 strong) and the CPU baseline
+      (timed by the parent after the GPU runs);
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+      (WORLD_SIZE set): this process is one rank of an N-rank run; rank 0
+      prints the N-rank line.
 """
 from __future__ import annotations
 
@@ -76,6 +86,14 @@ def parse():
     ap.add_argument("--c4-n", type=int, default=50_000_000, help="C4 cloud size (0: skip the C4 legs)")
     ap.add_argument("--dist-icp", action="store_true",
                     help="also run the sharded-ICP leg (RCCL) when world == 1 (under torchrun)")
+    ap.add_argument("--scaling-child", action="store_true",
+                    help="(set by the --gpus N launcher) one point of the scaling curve: the headline and C4 "
+                         "only, no CPU legs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU work: each rank joins a gloo rendezvous, all-reduces its rank count and rank 0 "
+                         "prints a placeholder line (checks the --gpus N launcher on a CPU host)")
+    ap.add_argument("--child-timeout", type=int, default=900,
+                    help="seconds one rank count of the --gpus N sweep may take before its processes are killed")
     return ap.parse_args()
 
 
@@ -473,15 +491,19 @@ def c5_pipeline(dev, args):
     return {"c5_single_gpu": res}
 
 
-def c4_headline(dev, args, world, rank):
-    """N > 1 headline (C4): ONE 50M-point cloud, each rank's points resident in
-    its voxel-aligned x-slab (a spatially tiled dataset; placement untimed),
-    one step = open3dpypro.distributed.voxel_normals_slabs(presorted=True)."""
+def slab_headline(dev, args, world, rank, n, stretch, vs, timer_filter=None):
+    """N > 1 step: ONE uniform-random n-point cloud over [0,stretch) x [0,1)^2,
+    each rank's points resident in its voxel-aligned x-slab (a spatially tiled
+    dataset; placement untimed), one step =
+    open3dpypro.distributed.voxel_normals_slabs(presorted=True).
+    stretch = world, vs = C2's: C2 per GPU (weak scaling); stretch = 1: C4
+    (one 50M cloud, strong scaling).  Returns (max-over-ranks seconds, global
+    reps, this rank's points, rank 0's host timeline of one more step)."""
     from open3dpypro import distributed as D
 
-    n = args.c4_n
-    vs = synthetic.voxel_size_for(n)
     full = synthetic.uniform_cube(n, seed=0, device=dev)
+    if stretch != 1:
+        full[:, 0] *= float(stretch)
     mn, mx = ops.aabb(full)
     keys = D.slab_bounds(mn, mx, vs, world)
     kx = torch.floor((full[:, 0].double() - float(mn[0])) / vs).to(torch.int64)
@@ -496,7 +518,8 @@ def c4_headline(dev, args, world, rank):
     for _ in range(args.warmup):
         rg, _, _ = step()
     _native.reset_kernel_timing()
-    _native.set_kernel_timing(True)
+    _native.kernel_timing_filter(timer_filter)
+    _native.set_kernel_timing(not args.no_kernel_events)
     barrier(world, dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -504,11 +527,12 @@ def c4_headline(dev, args, world, rank):
     barrier(world, dev)
     t1 = time.perf_counter()
     _native.set_kernel_timing(False)
+    _native.kernel_timing_filter(None)
     elapsed = max_over_ranks(t1 - t0, world, dev)
     m = torch.tensor([rg.numel()], dtype=torch.int64, device=comm_dev(dev))
     dist.all_reduce(m)
     # one more (untimed) step with host timestamps at each phase end: where
-    # the host waits (bounds, halo counts, verdict) and what they cost
+    # the host waits (bounds, verdict) and what they cost
     barrier(world, dev)
     tl = {}
     t2 = time.perf_counter()
@@ -516,8 +540,10 @@ def c4_headline(dev, args, world, rank):
     tl["returned"] = round((time.perf_counter() - t2) * 1e3, 4)
     torch.cuda.synchronize()
     tl["synchronized"] = round((time.perf_counter() - t2) * 1e3, 4)
-    c4_headline.host_timeline = tl
-    return elapsed, int(m.item()), int(pts.shape[0])
+    n_local = int(pts.shape[0])
+    del pts, gidx
+    torch.cuda.empty_cache()
+    return elapsed, int(m.item()), n_local, tl
 
 
 def c5_sharded(dev, args, world, rank):
@@ -612,17 +638,16 @@ def roofline(kernels, M, N, pmc_json):
             "algorithmic_bytes_per_launch": algo_bytes[dom],
             "note": "exact kNN selection is LDS / VALU-issue work, not HBM streaming: DESIGN.md §4.1"}
     if pmc.get("SQ_INSTS_VALU") and dom.startswith("normals"):
-        # the measured limit (PMC): VALU issue.  achieved = the launch's VALU
-        # wave-instructions / its duration; peak = one wave64 VALU instruction
-        # per 2 cycles per SIMD (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
+        # the headline stays SURVEY 8(d)'s algorithmic bytes / HBM peak; the
+        # measured limit (PMC) is VALU issue, reported beside it: the launch's
+        # VALU wave-instructions / its duration against one wave64 VALU
+        # instruction per 2 cycles per SIMD (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
         valu_peak = 1024 * 2.4e9 / 2.0 / 1e9
         valu_ach = pmc["SQ_INSTS_VALU"] / avg_s / 1e9
-        roof.update({"bound": "valu", "achieved": round(valu_ach, 2), "peak": valu_peak,
-                     "unit": "G wave64-VALU-instr/s", "frac": round(valu_ach / valu_peak, 4),
-                     "hbm_algorithmic": {"achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                         "frac": round(ach / HBM_PEAK_GBS, 5)},
-                     "note": "exact kNN selection is VALU-issue / LDS work, not HBM streaming (PMC in "
-                             "profiles/pmc_traffic.json; DESIGN.md §4.1)"})
+        roof["valu"] = {"achieved": round(valu_ach, 2), "peak": valu_peak, "unit": "G wave64-VALU-instr/s",
+                        "frac": round(valu_ach / valu_peak, 4)}
+        roof["note"] = ("exact kNN selection is VALU-issue / LDS work, not HBM streaming: the kernel's own limit "
+                        "is the `valu` block (PMC in profiles/pmc_traffic.json; DESIGN.md §4.1)")
     if pmc.get("SQ_INSTS_VALU"):
         # VALU-issue floor (MI355X_MICROARCH.md: a wave64 VALU instruction issues in 2 cycles on a SIMD
         # holding >= 2 waves; float64 / transcendental ones take longer, so this is a lower bound)
@@ -649,6 +674,10 @@ def roofline(kernels, M, N, pmc_json):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args)  # before anything touches a GPU
+    if args.dry_run:
+        return dry_run(args)
     world, rank, dev = setup_dist(args.dist_icp)
     if world > 1:
         return main_multi(args, world, rank, dev)
@@ -738,7 +767,12 @@ def main():
             line["extra"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
     del pts
     torch.cuda.empty_cache()
-    if not args.no_secondary:
+    if args.scaling_child and args.c4_n > 0:  # one point of the --gpus N curve: C2 + C4 only
+        try:
+            line["extra"].update(c4_single_gpu(dev, args))
+        except RuntimeError as e:
+            line["extra"]["c4_error"] = str(e)
+    elif not args.no_secondary:
         for name, fn in (("secondary", lambda: secondary(dev, args)),
                          ("c4", lambda: c4_single_gpu(dev, args) if args.c4_n > 0 else {}),
                          ("c5", lambda: c5_pipeline(dev, args) if args.c5_n > 0 else {}),
@@ -767,8 +801,13 @@ def main():
 
 
 def main_multi(args, world, rank, dev):
-    """N > 1: the C4 headline (strong scaling of one 50M cloud over the ranks)."""
-    elapsed, M, n_local = c4_headline(dev, args, world, rank)
+    """N > 1 ranks: the headline is C2 per GPU (weak scaling: one N x 10M
+    cloud over [0,N) x [0,1)^2 in x-slabs, C2's voxel size); beside it C4 (one
+    50M cloud over the same ranks: strong scaling), the sharded ICP and C5."""
+    n_per = args.n
+    N = n_per * world
+    vs = synthetic.voxel_size_for(n_per)
+    elapsed, M, n_local, tl = slab_headline(dev, args, world, rank, N, world, vs)
     kernels = kernel_table()
     # host/kernel split of the step: the library's event-timed kernel spans
     # (voxel, compaction, normals) per step on this rank, summed over the ranks
@@ -781,29 +820,42 @@ def main_multi(args, world, rank, dev):
     wall = elapsed / args.steps * 1e3
     shared = os.environ.get("O3DX_BENCH_SHARED_GPU") == "1"
     busy = k_all if shared else k_ms
-    N = args.c4_n
     value = float(N) * args.steps / elapsed / 1e6
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"C4: one uniform-random {N // 1_000_000}M-pt float32 cloud tiled over {world} GPUs "
-                               "as voxel-aligned x-slabs, voxel_down_sample(vs=(4/N)^(1/3)) + estimate_normals(KNN30) "
-                               "with a verified halo exchange of boundary representatives over RCCL",
-                   "n_points": N, "voxel_size": synthetic.voxel_size_for(N), "voxels": M, "knn": args.knn,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"C2 per GPU: one uniform-random {world} x {n_per // 1_000_000}M-pt float32 cloud over "
+                               f"[0,{world})x[0,1)^2 (C2's density) tiled over {world} GPUs as voxel-aligned x-slabs, "
+                               "voxel_down_sample(vs=C2's (4/10M)^(1/3)) + estimate_normals(KNN30) with a verified "
+                               "halo exchange of boundary representatives over RCCL",
+                   "n_points": N, "points_per_gpu": n_per, "voxel_size": vs, "voxels": M, "knn": args.knn,
                    "parallelism": f"x-slab spatial tiling x{world}", "points_rank0": n_local},
         "roofline": roofline(kernels, M / world, N / world, args.pmc_json),
         "cpu_baseline": None,
         "extra": {"kernels_rank0": kernels,
+                  "world_size_observed": dist.get_world_size(), "backend": dist.get_backend(),
                   "step_breakdown": {"wall_ms": round(wall, 4), "kernel_ms_rank0": round(k_ms, 4),
                                      "kernel_ms_all_ranks": round(k_all, 4), "gpu_shared_by_ranks": shared,
                                      "host_frac": round(max(0.0, 1.0 - busy / wall), 4) if wall > 0 else None},
-                  "collectives": "all_reduce (AABB, halo proof), all_to_all (halo representatives)",
-                  "host_timeline_rank0_ms": getattr(c4_headline, "host_timeline", None),
+                  "collectives": "all_reduce (AABB + counts), all_to_all (halo representatives), all_gather "
+                                 "(halo-proof verdict)",
+                  "host_timeline_rank0_ms": tl,
                   "pipeline_algorithmic_GBs": round((12.0 * N + 28.0 * M) * args.steps / elapsed / 1e9, 2)},
     }
+    if args.c4_n > 0:
+        try:
+            n4 = args.c4_n
+            el4, m4, nl4, tl4 = slab_headline(dev, args, world, rank, n4, 1, synthetic.voxel_size_for(n4),
+                                              timer_filter=["normals_stile"])
+            line["extra"]["c4_strong"] = {"n": n4, "ranks": world, "voxels": m4, "points_rank0": nl4,
+                                          "ms": round(el4 / args.steps * 1e3, 3),
+                                          "value": round(n4 * args.steps / el4 / 1e6, 2), "unit": "Mpoints/s",
+                                          "scaling": "strong", "host_timeline_rank0_ms": tl4}
+        except RuntimeError as e:  # report, never hide
+            line["extra"]["c4_error"] = str(e)
     torch.cuda.empty_cache()
-    if not args.no_secondary:
+    if not args.no_secondary and not args.scaling_child:
         for name, fn in (("icp_sharded", lambda: secondary_sharded_icp(dev, args, world, rank)),
                          ("c5", lambda: c5_sharded(dev, args, world, rank) if args.c5_n > 0 else {})):
             try:
@@ -817,5 +869,164 @@ def main_multi(args, world, rank, dev):
     dist.destroy_process_group()
 
 
+def dry_run(args):
+    """--dry-run: the launch plumbing without a GPU (gloo on the CPU)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    seen = 1
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        t = torch.ones(1, dtype=torch.int64)
+        dist.all_reduce(t)
+        seen = int(t.item())
+    line = {"metric": METRIC, "value": float(seen), "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1.0, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "dry-run", "config": {"workload": "dry-run"},
+            "roofline": None, "cpu_baseline": None,
+            "extra": {"world_size_observed": seen, "scaling_child": args.scaling_child, "no_cpu": args.no_cpu,
+                      "local_rank": os.environ.get("LOCAL_RANK"), "c4_single_gpu": {"Mpoints_per_s": 1.0},
+                      "c4_strong": {"value": float(seen)}}}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _rank_counts(n: int):
+    """1, 2, 4, ... below n, then n itself"""
+    out, c = [1], 2
+    while c < n:
+        out.append(c)
+        c *= 2
+    return out + ([n] if n > 1 else [])
+
+
+def _strip_gpus(argv):
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a == "--gpus":
+            skip = True
+            continue
+        if a.startswith("--gpus="):
+            continue
+        out.append(a)
+    return out
+
+
+def _run_ranks(n, argv, timeout_s):
+    """One point of the curve: n fresh processes (one per GPU, LOCAL_RANK =
+    rank, RCCL rendezvous on 127.0.0.1), rank 0's JSON line back.  A rank
+    that fails or overruns ends the whole group (its PIDs, never a pattern)."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        if n > 1:
+            env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        else:
+            for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+                env.pop(k, None)
+        cmd = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", str(n)] + argv
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = []
+    import threading
+
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    deadline = time.time() + timeout_s
+    err = None
+    while True:
+        codes = [p.poll() for p in procs]
+        if all(c is not None for c in codes):
+            if any(codes):
+                err = f"{n} ranks: exit codes {codes}"
+            break
+        if any(c not in (None, 0) for c in codes):
+            err = f"{n} ranks: exit codes {codes} (the rest stopped)"
+            break
+        if time.time() > deadline:
+            err = f"{n} ranks: over {timeout_s}s (stopped)"
+            break
+        time.sleep(0.5)
+    if err:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            p.wait()
+    reader.join(timeout=30)
+    text = out0[0].decode() if out0 and out0[0] else ""
+    lines = [ln for ln in text.splitlines() if ln.startswith("{")]
+    if err or not lines:
+        return None, err or f"{n} ranks: no result line"
+    return json.loads(lines[-1]), None
+
+
+def launch(args):
+    """python bench.py --gpus N with no WORLD_SIZE: the 1 -> N scaling curve in
+    one run.  This process never initialises a GPU (children only); it starts
+    one fresh process per GPU for each rank count in turn (1, 2, 4, ... N),
+    each rank count a separate rendezvous, and prints one line: the N-rank
+    figures, `scaling_curve` (per count: value, ms, efficiency =
+    value_n / (n x value_1)) and the CPU baseline, timed here after the GPU
+    runs (reference precedent for one process per device:
+    processors.py:204-208, :1088-1098)."""
+    N = args.gpus
+    base = _strip_gpus(sys.argv[1:])
+    runs, errors = {}, []
+    for n in _rank_counts(N):
+        argv = list(base) + ["--no-cpu"] + ([] if n == N else ["--scaling-child"])
+        log(f"bench launcher: {n} rank(s)")
+        line, err = _run_ranks(n, argv, args.child_timeout)
+        if err:
+            errors.append(err)
+            log("bench launcher:", err)
+            break  # nothing more on the GPU after a failed run
+        runs[n] = line
+    if N in runs:
+        line = runs[N]
+    else:
+        line = {"metric": METRIC, "value": None, "unit": "Mpoints/s", "n_gpus": N, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f64", "data": "synthetic", "config": {}, "roofline": None,
+                "cpu_baseline": None, "extra": {}}
+    weak, c4 = {}, {}
+    v1 = runs.get(1, {}).get("value")
+    c41 = runs.get(1, {}).get("extra", {}).get("c4_single_gpu", {}).get("Mpoints_per_s")
+    for n, ln in sorted(runs.items()):
+        v = ln.get("value")
+        weak[str(n)] = {"value": v, "ms_per_step": ln.get("ms_per_step"),
+                        "efficiency": round(v / (n * v1), 4) if (v and v1) else None}
+        cv = (ln.get("extra", {}).get("c4_single_gpu", {}).get("Mpoints_per_s") if n == 1
+              else ln.get("extra", {}).get("c4_strong", {}).get("value"))
+        c4[str(n)] = {"value": cv, "efficiency": round(cv / (n * c41), 4) if (cv and c41) else None}
+    line["scaling_curve"] = {"unit": "Mpoints/s", "weak_c2_per_gpu": weak, "strong_c4_50M": c4,
+                             "note": "1 rank = the single-GPU C2 step (one-call pipeline); n > 1 = the x-slab step "
+                                     "with the halo exchange over RCCL; efficiency = value_n / (n x value_1)"}
+    line["launcher"] = {"form": "bench.py --gpus N: fresh child processes per rank count, one per GPU",
+                        "rank_counts": sorted(runs), "errors": errors}
+    if not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_n)
+        if line.get("value") and line["cpu_baseline"]["value"] > 0:
+            line.setdefault("extra", {})["gpu_over_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
+    print(json.dumps(line), flush=True)
+    return 1 if errors else 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
