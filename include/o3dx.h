@@ -76,7 +76,9 @@ int o3dx_fx_to_double(const int64_t* fx_host, int64_t k, double* out_host);
  * stream; o3dx_kernel_timing() waits for the pending events and returns the
  * accumulated milliseconds and launch count of one kernel by name
  * ("voxel_assign", "normals_knn", "grid_build", "plane_count",
- * "icp_accumulate", ...).  Returns 0 if the name was seen, -1 otherwise. */
+ * "icp_accumulate", ...).  Returns 0 if the name was seen, -1 otherwise.
+ * Process-wide profiling switch (mutex-guarded event lists): the one piece of
+ * state shared across threads; it adds event records, never changes results. */
 void o3dx_set_kernel_timing(int enable);
 /* Restrict timing to the comma-separated timer names ("" or NULL: all). */
 void o3dx_kernel_timing_filter(const char* names_csv);
@@ -90,7 +92,8 @@ int o3dx_kernel_timing(const char* name, double* total_ms, int64_t* launches);
  * gave up {box over LDS capacity, too few points within the shell-1 radius};
  * o3dx_search_stats copies those eight counters out (synchronises the device).
  * Enabling allocates a 64-byte device buffer — the only device allocation the
- * library ever makes; off by default. */
+ * library ever makes; off by default.  Thread-local: the setting and buffer
+ * belong to the calling host thread (one buffer per thread that enables it). */
 int o3dx_set_search_stats(int enable);
 int o3dx_search_stats(int64_t* out8_host);
 
@@ -102,6 +105,7 @@ int o3dx_search_stats(int64_t* out8_host);
  * the order it summed them; ids = the caller's point rows).  Only calls whose
  * k equals `k` and whose rows are < `rows` write.  NULL turns it off.  The
  * buffer is caller-owned; the library keeps the pointer until it is reset.
+ * Thread-local: only launches made by the thread that set it write.
  *
  * o3dx_fast_eigen3x3: the device FastEigen3x3 (the normals kernels' solver)
  * on m covariances {xx,xy,xz,yy,yz,zz} (f64, dev) -> smallest-eigenvalue

@@ -236,16 +236,19 @@ static GridLayout grid_layout(int64_t n, int cap_mult) {
 
 size_t grid_ws_bytes(int64_t n, int cap_mult) { return grid_layout(n, cap_mult).total; }
 
+// Test / profiling hooks.  They are thread-local: a hook set on one host
+// thread affects only the launches that thread makes, so the library stays
+// re-entrant across threads; unset they cost a null test.
 // Debug-only search statistics (o3dx_search_stats): the one place the library
 // allocates device memory, and only after o3dx_set_search_stats(1).
-static unsigned long long* g_stats = nullptr;
-static bool g_stats_on = false;
+static thread_local unsigned long long* g_stats = nullptr;
+static thread_local bool g_stats_on = false;
 unsigned long long* search_stats_ptr() { return g_stats_on ? g_stats : nullptr; }
 
 // Test hook (o3dx_set_debug_neighbors): caller-owned (rows, k) buffer.
-static int32_t* g_dbg_nbr = nullptr;
-static int64_t g_dbg_rows = 0;
-static int g_dbg_k = 0;
+static thread_local int32_t* g_dbg_nbr = nullptr;
+static thread_local int64_t g_dbg_rows = 0;
+static thread_local int g_dbg_k = 0;
 static int32_t* debug_nbr(int kneed, int64_t rows) {
   return (g_dbg_nbr && kneed == g_dbg_k && rows <= g_dbg_rows) ? g_dbg_nbr : nullptr;
 }

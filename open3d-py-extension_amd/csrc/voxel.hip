@@ -984,7 +984,12 @@ __global__ void __launch_bounds__(kBlock) k_voxel_occ2(const T* __restrict__ tab
 static int64_t dense_cap(int64_t n) { return dense_cap_hd(n); }
 // binned entries: n for the scanned layout, + 1/2 + 2^20 of segment slack
 static int64_t entries_cap(int64_t n) { return entries_cap_hd(n); }
-static thread_local uint64_t g_fused_overflow_key = ~0ull;  // last geometry whose one-pass binning overflowed
+// Path-selection memory (per host thread, never shared): the last geometry
+// whose one-pass binning overflowed.  It picks which (equally exact) binning
+// path a later call on the same geometry tries first, so that call skips a
+// doomed attempt; results never depend on it (every path yields the same reps,
+// tests/test_gpu_kernels.py runs each).
+static thread_local uint64_t g_fused_overflow_key = ~0ull;
 // ... whose copied segments overflowed: the one-pass binning retries with one
 // copy per brick (a spatially ordered cloud sends each brick's
 // points from a few consecutive blocks, i.e. into one or two copies)
