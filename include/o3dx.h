@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define O3DX_ABI_VERSION 6
+#define O3DX_ABI_VERSION 7
 
 #define O3DX_OK 0
 #define O3DX_EIO (-5)
@@ -552,6 +552,51 @@ int o3dx_registration_icp_point_to_plane(
     double* T_out_host, double* fitness_host, double* inlier_rmse_host,
     int32_t* corr_out_dev, int64_t* ncorr_host, void* target_ws,
     size_t target_ws_bytes, void* ws, size_t ws_bytes, void* stream);
+
+/* Sharded ICP device loop (ABI 7; distributed.registration_icp_sharded, the
+ * north star's "6x6 JTJ RCCL all-reduce", SURVEY 8(e) ICP row).  Each rank
+ * holds a share of the source (src as o3dx_icp_register takes it) and the
+ * target (replicated, or the window its share can reach) and queues per
+ * iteration it = 0 .. max_iteration, with no host wait:
+ *   o3dx_icp_shard_step    the rank's fused match + fx-moment step (skip proof
+ *                          included; use_prior = 0 on the first step and
+ *                          after a resume) and its digit sums -> digits_dev
+ *                          (2 x 32 int64, device);
+ *   (caller)               SUM all-reduce of digits_dev over the ranks;
+ *   o3dx_icp_shard_finish  sums, fitness / rmse over n_total (the GLOBAL
+ *                          source count), Open3D's convergence test, the 6x6
+ *                          solve and T <- update * T: identical on every rank.
+ * src_absmax_host (begin) must be the GLOBAL source bounds (fx quanta): T is
+ * then o3dx_icp_register's on the whole source to the bit.  win_dev (nullable,
+ * device, world rows {box min xyz, box max xyz, window lo, window hi}): the
+ * finish stops the loop when the new T needs target rows outside some rank's
+ * window (info[2] of o3dx_icp_shard_state); the caller refetches the windows
+ * and calls o3dx_icp_shard_resume, then continues from it = info[1].  widen
+ * (step and finish alike): the window's cover beyond the correspondence
+ * radius; a grid whose skip-proof ball extension (0.1 cell) exceeds it
+ * searches in full (+inf: replicated target, no cap).  ws is
+ * sized by o3dx_icp_accumulate_workspace_bytes(ns) and carries the state
+ * between the calls.  float32 clouds. */
+int o3dx_icp_shard_begin(const double* init_host, const double* src_absmax_host,
+                         double max_correspondence_distance, int64_t ns,
+                         void* ws, size_t ws_bytes, void* stream);
+int o3dx_icp_shard_step(const float* src_dev, int64_t ns, int src_sorted4,
+                        const void* target_ws, const double* desc_host,
+                        double max_correspondence_distance, int use_prior,
+                        double widen, int64_t* digits_dev, void* ws, size_t ws_bytes,
+                        void* stream);
+int o3dx_icp_shard_finish(const int64_t* digits_dev, int64_t n_total, int it,
+                          int max_iteration, double relative_fitness,
+                          double relative_rmse,
+                          double max_correspondence_distance,
+                          const double* desc_host, const double* win_dev,
+                          int world, double widen, int64_t ns, void* ws,
+                          size_t ws_bytes, void* stream);
+int o3dx_icp_shard_state(int64_t ns, void* ws, size_t ws_bytes,
+                         double* T_out_host, double* fitness_host,
+                         double* inlier_rmse_host, int32_t* info3_host,
+                         void* stream);
+int o3dx_icp_shard_resume(int64_t ns, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- PCD IO
  * o3dx_pcd_unpack: decode PCD fields on the device (replaces the host-side

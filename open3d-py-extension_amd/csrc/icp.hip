@@ -263,6 +263,7 @@ struct IcpState {
   int32_t iters;  // updates applied
   int32_t ext_on;    // the device loop: this step searches the extended ball (margins for the skip proof)
   int32_t ext_prev;  // ... and the previous one did (the margins are valid)
+  int32_t wstop;     // the sharded loop: the new T leaves some rank's target window (the host refetches)
 };
 
 O3DX_HD inline void state_set_T(IcpState& st, const double* T, double max_corr) {
@@ -643,13 +644,44 @@ __global__ void __launch_bounds__(1024) k_icp_collect(int64_t* __restrict__ acc,
   if (threadIdx.x < 2 * kNS) digits[threadIdx.x] = red[0][threadIdx.x];
 }
 
+// Sharded loop: whether the x-range every rank's source box can reach under T
+// (+ the correspondence radius, the rounding slack and `widen`, the skip
+// proof's ball extension) still lies inside that rank's target window.  win:
+// world rows {box min xyz, box max xyz, window lo, window hi}; a rank without
+// source rows has a non-finite box and needs nothing.  The arithmetic is
+// distributed.WindowedTarget._need's, so every rank decides alike.
+__device__ inline bool windows_cover(const double* __restrict__ win, int world, const double* T, double mc,
+                                     double widen) {
+  for (int r = 0; r < world; ++r) {
+    const double* b = win + 8 * r;
+    bool fin = true;
+    for (int a = 0; a < 6; ++a) fin = fin && isfinite(b[a]);
+    if (!fin) continue;
+    double lo = INFINITY, hi = -INFINITY, am = 0.0;
+    for (int c = 0; c < 8; ++c) {
+      const double x = (c & 1) ? b[3] : b[0], y = (c & 2) ? b[4] : b[1], z = (c & 4) ? b[5] : b[2];
+      const double xs = ((x * T[0] + y * T[1]) + z * T[2]) + T[3];
+      lo = fmin(lo, xs);
+      hi = fmax(hi, xs);
+      am = fmax(am, fabs(xs));
+    }
+    const double eps = 1e-6 * (1.0 + am + mc);
+    if (!(b[6] <= lo - mc - eps - widen && hi + mc + eps + widen <= b[7])) return false;
+  }
+  return true;
+}
+
 // The loop's per-iteration bookkeeping, one workgroup: the digit sums of the
-// step's accumulator copies, then (thread 0) the sums, fitness and rmse, Open3D's
+// step's accumulator copies (or, in the sharded loop, the digits summed over
+// the ranks), then (thread 0) the sums, fitness and rmse, Open3D's
 // convergence test against the previous iteration's, and — while iterations
 // remain — the solve and T <- update * T with the next fx exponents.
 __global__ void __launch_bounds__(1024) k_icp_finish(IcpState* __restrict__ st, int64_t* __restrict__ acc,
                                                      int64_t ns, double max_corr, double rel_fit, double rel_rmse,
-                                                     int it, int max_it, double ext) {
+                                                     int it, int max_it, double ext,
+                                                     const int64_t* __restrict__ digits = nullptr,
+                                                     const double* __restrict__ win = nullptr, int world = 0,
+                                                     double widen = 0.0) {
   __shared__ int64_t red[16][2 * kNS];
   __shared__ IcpState ls;
   __shared__ double sums[kNS];
@@ -659,7 +691,12 @@ __global__ void __launch_bounds__(1024) k_icp_finish(IcpState* __restrict__ st, 
   constexpr int kWords = (int)(sizeof(IcpState) / sizeof(uint32_t));
   for (int t = threadIdx.x; t < kWords; t += blockDim.x)
     reinterpret_cast<uint32_t*>(&ls)[t] = reinterpret_cast<const uint32_t*>(st)[t];
-  collect_digits(acc, red);  // (its barriers also publish ls)
+  if (digits) {
+    if (threadIdx.x < 2 * kNS) red[0][threadIdx.x] = digits[threadIdx.x];
+    __syncthreads();
+  } else {
+    collect_digits(acc, red);  // (its barriers also publish ls)
+  }
   if (threadIdx.x < kNS)
     sums[threadIdx.x] =
         threadIdx.x < kNT ? fx_value(red[0][2 * threadIdx.x], red[0][2 * threadIdx.x + 1], ls.q[threadIdx.x]) : 0.0;
@@ -693,6 +730,10 @@ __global__ void __launch_bounds__(1024) k_icp_finish(IcpState* __restrict__ st, 
       // before that the margins could not survive the next motion anyway
       ls.ext_prev = ls.ext_on;
       ls.ext_on = ext > 0.0 && sqrt(mv) < 0.5 * ext ? 1 : 0;
+      if (win && !windows_cover(win, world, ls.T, max_corr, widen)) {
+        ls.done = 1;  // the next step needs other target rows: the host refetches and resumes
+        ls.wstop = 1;
+      }
     }
   }
   __syncthreads();
@@ -1127,6 +1168,125 @@ extern "C" int o3dx_icp_register(const float* src, int64_t ns, int src_sorted4, 
   acc_carve(ar, std::max<int64_t>(ns, 1), &w);
   return run_loop(src, ns, src_sorted4 != 0, g, tn, max_corr, init, max_iteration, rel_fit, rel_rmse, src_absmax,
                   w, as_stream(stream), T_out, fitness, rmse, corr_out, ncorr);
+}
+
+// ------------------------------------------------ the sharded device loop
+// distributed.registration_icp_sharded: every rank holds a share of the
+// source (and the target, or the window of it its share can reach) and queues
+// per iteration, with no host wait:
+//   o3dx_icp_shard_step    its rows' fused match + fx-moment step (the device
+//                          loop's, skip proof included) and the digit sums
+//                          into digits_dev (2 x 32 int64);
+//   (the caller)           a SUM all-reduce of digits_dev over the ranks (RCCL);
+//   o3dx_icp_shard_finish  the loop's finish on the summed digits: sums,
+//                          fitness / rmse over the GLOBAL source count, the
+//                          convergence test, solve and update — the same on
+//                          every rank, so every rank holds the same T.
+// The fx quanta come from the global source bounds (begin's absmax), so the
+// digits add exactly and T equals the single-GPU o3dx_icp_register's to the
+// bit.  With windows (win_dev), the finish also stops the loop (state wstop)
+// when the new T needs target rows outside some rank's window; the host reads
+// the state (o3dx_icp_shard_state), refetches and calls o3dx_icp_shard_resume.
+static int shard_ws(void* ws, size_t ws_bytes, int64_t ns, AccWs* w) {
+  if (!ws || ws_bytes < o3dx_icp_accumulate_workspace_bytes(ns)) return fail(O3DX_ENOMEM, "icp workspace too small");
+  Arena ar(ws, ws_bytes);
+  acc_carve(ar, std::max<int64_t>(ns, 1), w);
+  return 0;
+}
+
+extern "C" int o3dx_icp_shard_begin(const double* init, const double* src_absmax, double max_corr, int64_t ns,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  if (ns < 0 || !src_absmax) return fail(O3DX_EINVAL, "o3dx_icp_shard_begin: bad args");
+  if (!(max_corr > 0.0)) return fail(O3DX_EINVAL, "max_correspondence_distance must be > 0");
+  AccWs w;
+  O3DX_TRY(shard_ws(ws, ws_bytes, ns, &w));
+  hipStream_t s = as_stream(stream);
+  IcpState hs{};
+  double T0[16];
+  if (init) std::memcpy(T0, init, sizeof(T0));
+  else
+    for (int a = 0; a < 16; ++a) T0[a] = (a % 5 == 0) ? 1.0 : 0.0;
+  std::memcpy(hs.absmax, src_absmax, sizeof(hs.absmax));
+  state_set_T(hs, T0, max_corr);
+  O3DX_HIP(hipMemcpyAsync(w.st, &hs, sizeof(IcpState), hipMemcpyHostToDevice, s));
+  O3DX_HIP(hipMemsetAsync(w.acc, 0, (size_t)kIcpCopies * 2 * kNS * sizeof(int64_t), s));
+  return 0;
+}
+
+static bool icp_skip_on() { return !(getenv("O3DX_ICP_SKIP") && atoi(getenv("O3DX_ICP_SKIP")) == 0); }
+
+// widen: the largest skip-proof extension a window covers (the ball of a full
+// search reaches 0.1 h beyond the match); a grid whose extension is larger
+// searches without the skip proof.  +inf for a replicated target.
+extern "C" int o3dx_icp_shard_step(const float* src, int64_t ns, int src_sorted4, const void* target_ws,
+                                   const double* desc, double max_corr, int use_prior, double widen,
+                                   int64_t* digits_dev, void* ws, size_t ws_bytes, void* stream) {
+  if (ns < 0 || (ns > 0 && !src) || !digits_dev) return fail(O3DX_EINVAL, "o3dx_icp_shard_step: bad args");
+  AccWs w;
+  O3DX_TRY(shard_ws(ws, ws_bytes, ns, &w));
+  hipStream_t s = as_stream(stream);
+  if (ns == 0 || !target_ws) {  // nothing to match here: this rank adds zeros
+    O3DX_HIP(hipMemsetAsync(digits_dev, 0, 2 * kNS * sizeof(int64_t), s));
+    return 0;
+  }
+  if (desc_is_f64(desc)) return fail(O3DX_EINVAL, "o3dx_icp_shard_step: float32 targets only");
+  GridView g;
+  const float4* tn;
+  if (!desc_unpack(desc, target_ws, &g, &tn)) return fail(O3DX_EINVAL, "invalid ICP target descriptor");
+  launch_step(src, ns, src_sorted4 != 0, g, tn, max_corr, w, s, use_prior ? 1 : 0,
+              icp_skip_on() && 0.1 * (double)g.h <= widen);
+  hipLaunchKernelGGL(k_icp_collect, dim3(1), dim3(1024), 0, s, w.acc, digits_dev);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int o3dx_icp_shard_finish(const int64_t* digits_dev, int64_t n_total, int it, int max_iteration,
+                                     double rel_fit, double rel_rmse, double max_corr, const double* desc,
+                                     const double* win_dev, int world, double widen, int64_t ns, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  if (!digits_dev || n_total < 0 || it < 0 || (win_dev && world < 1)) return fail(O3DX_EINVAL, "o3dx_icp_shard_finish: bad args");
+  AccWs w;
+  O3DX_TRY(shard_ws(ws, ws_bytes, ns, &w));
+  // the skip proof's extension of this rank's target grid (0: no target here)
+  const double ext =
+      (desc && desc[13] == kDescMagic && icp_skip_on() && 0.1 * (double)(float)desc[3] <= widen) ? 0.1 * (double)(float)desc[3] : 0.0;
+  hipLaunchKernelGGL(k_icp_finish, dim3(1), dim3(1024), 0, as_stream(stream), w.st, w.acc, std::max<int64_t>(n_total, 1),
+                     max_corr, rel_fit, rel_rmse, it, std::max(max_iteration, 0), ext, digits_dev, win_dev, world,
+                     widen);
+  O3DX_HIP(hipGetLastError());
+  return 0;
+}
+
+// info: {done, iterations applied, window stop}
+extern "C" int o3dx_icp_shard_state(int64_t ns, void* ws, size_t ws_bytes, double* T_out, double* fitness,
+                                    double* rmse, int32_t* info, void* stream) {
+  if (!T_out || !fitness || !rmse || !info) return fail(O3DX_EINVAL, "o3dx_icp_shard_state: bad args");
+  AccWs w;
+  O3DX_TRY(shard_ws(ws, ws_bytes, ns, &w));
+  IcpState hs;
+  O3DX_TRY(read_back(&hs, w.st, sizeof(IcpState), as_stream(stream)));
+  std::memcpy(T_out, hs.T, sizeof(hs.T));
+  *fitness = hs.fit;
+  *rmse = hs.rmse;
+  info[0] = hs.done;
+  info[1] = hs.iters;
+  info[2] = hs.wstop;
+  return 0;
+}
+
+// after a window stop: the loop continues (the host has refetched the windows;
+// the next step must not reuse the previous matches: pass use_prior = 0)
+extern "C" int o3dx_icp_shard_resume(int64_t ns, void* ws, size_t ws_bytes, void* stream) {
+  AccWs w;
+  O3DX_TRY(shard_ws(ws, ws_bytes, ns, &w));
+  hipStream_t s = as_stream(stream);
+  IcpState hs;
+  O3DX_TRY(read_back(&hs, w.st, sizeof(IcpState), s));
+  hs.done = 0;
+  hs.wstop = 0;
+  hs.ext_prev = 0;  // the margins were measured against the old window
+  O3DX_HIP(hipMemcpyAsync(w.st, &hs, sizeof(IcpState), hipMemcpyHostToDevice, s));
+  return 0;
 }
 
 extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns, const float* tgt,

@@ -97,6 +97,11 @@ _SIGS = {
     "o3dx_registration_icp_workspace_bytes": (_SZ, [_I64]),
     "o3dx_icp_solve_point_to_plane": (_I32, [_P, _P]),
     "o3dx_icp_update": (_I32, [_P, _P]),
+    "o3dx_icp_shard_begin": (_I32, [_P, _P, _D, _I64, _P, _SZ, _P]),
+    "o3dx_icp_shard_step": (_I32, [_P, _I64, _I32, _P, _P, _D, _I32, _D, _P, _P, _SZ, _P]),
+    "o3dx_icp_shard_finish": (_I32, [_P, _I64, _I32, _I32, _D, _D, _D, _P, _P, _I32, _D, _I64, _P, _SZ, _P]),
+    "o3dx_icp_shard_state": (_I32, [_I64, _P, _SZ, _P, _P, _P, _P, _P]),
+    "o3dx_icp_shard_resume": (_I32, [_I64, _P, _SZ, _P]),
     "o3dx_icp_register": (_I32, [_P, _I64, _I32, _P, _P, _P, _I32, _D, _D, _D, _P, _P, _P, _P, _P, _P, _P, _SZ,
                                  _P]),
     "o3dx_registration_icp_point_to_plane": (_I32, [_P, _I64, _P, _P, _I64, _D, _P, _I32, _D, _D, _P, _P,

@@ -327,6 +327,9 @@ def registration_icp_sharded(src: torch.Tensor, target, init=None, max_iteration
     the fx quanta come from the GLOBAL source bounds, so T, fitness and rmse
     equal ops.registration_icp on the whole source to the bit.  Returns (T,
     fitness, inlier_rmse)."""
+    if backend is None and isinstance(src, torch.Tensor) and src.is_cuda and src.dtype == torch.float32:
+        return _registration_icp_sharded_device(src, target, init, max_iteration, relative_fitness, relative_rmse,
+                                                group, n_source_total)
     be = backend or _HIP
     am = allreduce_max(be.absmax(src) if src.shape[0] else np.zeros(3), group)
     n_total = _allreduce_int(src.shape[0], group) if n_source_total is None else int(n_source_total)
@@ -344,6 +347,61 @@ def registration_icp_sharded(src: torch.Tensor, target, init=None, max_iteration
 
 
 _ICP_FX_ZERO = np.zeros((32, 4), np.int64)  # a rank without source rows contributes nothing
+
+
+def _allreduce_digits(digits: torch.Tensor, group=None):
+    """SUM all-reduce of the loop's 64 int64 digits: in place on the device
+    under RCCL (stream-ordered, no host wait); through the host under gloo."""
+    world, _ = _world(group)
+    if world == 1:
+        return
+    if _comm_device(group).type == "cuda":
+        dist.all_reduce(digits, op=dist.ReduceOp.SUM, group=group)
+    else:
+        h = digits.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        digits.copy_(h)
+
+
+def _registration_icp_sharded_device(src, target, init, max_iteration, relative_fitness, relative_rmse, group,
+                                     n_source_total):
+    """The sharded ICP as the device loop (o3dx_icp_shard_*, ops.ICPShardLoop):
+    per iteration each rank queues its step (skip proof included), the digit
+    all-reduce and the shared finish — no host solve, no host wait; the host
+    reads the state once at the end (and at a window stop, when the new T
+    needs target rows outside some rank's window: refetch, resume).  T,
+    fitness and rmse equal the single-GPU o3dx_icp_register's to the bit."""
+    from . import ops
+
+    world, _ = _world(group)
+    am = allreduce_max(ops.absmax(src) if src.shape[0] else np.zeros(3), group)
+    n_total = _allreduce_int(src.shape[0], group) if n_source_total is None else int(n_source_total)
+    s = ops.spatial_sort(src) if src.shape[0] else src
+    T0 = np.eye(4) if init is None else np.array(init, np.float64).reshape(4, 4)
+    windowed = isinstance(target, WindowedTarget)
+    if windowed:
+        target.bind(src)
+        tgt = target.for_transform(T0)
+        mc, widen = target.mc, target.widen
+        win = target.window_table(src.device)
+    else:
+        tgt, mc, widen, win = target, target.max_corr, float("inf"), None
+    loop = ops.ICPShardLoop(s, am, mc, T0)
+    digits = torch.zeros(64, dtype=torch.int64, device=src.device)
+    it0 = 0
+    while True:
+        for it in range(it0, max(int(max_iteration), 0) + 1):
+            loop.step(tgt, digits, use_prior=it > it0, widen=widen)
+            _allreduce_digits(digits, group)
+            loop.finish(digits, n_total, it, max_iteration, relative_fitness, relative_rmse, tgt, win, widen)
+        T, fit, rm, info = loop.state()
+        if not (windowed and info[2]):
+            return T, fit, rm
+        # a window stop (every rank alike): refetch the windows for T, go on
+        tgt = target.for_transform(T)
+        win = target.window_table(src.device)
+        loop.resume()
+        it0 = int(info[1])
 
 
 class WindowedTarget:
@@ -367,6 +425,10 @@ class WindowedTarget:
                  max_correspondence_distance: float, margin: Optional[float] = None, group=None, backend=None):
         self.xyz, self.nrm, self.pos = xyz, normals, pos
         self.mc = float(max_correspondence_distance)
+        # the need also covers `widen` beyond the radius: the skip proof's
+        # full searches reach 0.1 cell past the match (the device loop caps it
+        # at widen, o3dx_icp_shard_step)
+        self.widen = self.mc
         self.margin = 4.0 * self.mc if margin is None else float(margin)
         self.group, self.be = group, backend or _HIP
         self.boxes = None
@@ -401,11 +463,23 @@ class WindowedTarget:
             if not np.all(np.isfinite(b)):
                 out.append(None)
                 continue
-            cs = np.array([[x, y, z] for x in (b[0], b[3]) for y in (b[1], b[4]) for z in (b[2], b[5])])
-            xs = cs @ T[0, :3] + T[0, 3]
-            eps = 1e-6 * (1.0 + np.abs(xs).max() + self.mc)  # float64 transform / float32 coordinate slack
-            out.append((xs.min() - self.mc - eps, xs.max() + self.mc + eps))
+            # the corners' x under T in the device check's order (windows_cover, icp.hip)
+            xs = [((x * T[0, 0] + y * T[0, 1]) + z * T[0, 2]) + T[0, 3]
+                  for z in (b[2], b[5]) for y in (b[1], b[4]) for x in (b[0], b[3])]
+            lo, hi = min(xs), max(xs)
+            eps = 1e-6 * (1.0 + max(abs(v) for v in xs) + self.mc)  # float64 transform / float32 coordinate slack
+            out.append((lo - self.mc - eps - self.widen, hi + self.mc + eps + self.widen))
         return out
+
+    def window_table(self, device) -> torch.Tensor:
+        """(world, 8) float64 rows {source box min xyz, max xyz, window lo, hi}
+        for the device loop's window check (a rank without source rows: an
+        infinite box, no window needed)."""
+        rows = np.zeros((len(self.boxes), 8), np.float64)
+        for r, (b, w) in enumerate(zip(self.boxes, self.win)):
+            rows[r, :6] = b
+            rows[r, 6:] = (np.inf, -np.inf) if w is None else w
+        return torch.from_numpy(rows).to(device)
 
     def for_transform(self, T):
         T = np.asarray(T, np.float64).reshape(4, 4)
@@ -1076,7 +1150,8 @@ def _voxel_normals_slabs_sync(xyz, gidx, voxel_size, knn, group, halo, presorted
 def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tensor, src_gidx: torch.Tensor,
                      voxel_size: float, knn: int = 30, distance_threshold: float = 0.002, ransac_n: int = 3,
                      num_iterations: int = 1000, seed: int = 7, max_correspondence_distance: float = 0.02,
-                     icp_iterations: int = 30, presorted: bool = False, group=None, timings: Optional[dict] = None):
+                     icp_iterations: int = 30, presorted: bool = False, group=None, timings: Optional[dict] = None,
+                     backend=None):
     """C5 over the ranks (BASELINE configs[4]; the reference's chain
     test_pipeline.py:406-434 — VoxelDownsample -> normals -> PlaneDetection —
     plus the north star's ICP, with each cloud's device placement per rank as
@@ -1097,10 +1172,16 @@ def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tenso
     Returns a dict: target_rep_gidx / target_rep_xyz / target_normals (this
     rank's), source_reps (global count), plane, plane_inlier_rows (global row
     positions of this rank's inliers among the target reps), target_reps
-    (global count), transformation, fitness, inlier_rmse."""
+    (global count), transformation, fitness, inlier_rmse.
+
+    backend: the per-rank compute (default: the HIP kernels); the CPU tests
+    pass the oracle restated behind the same interface (voxel, normals,
+    absmax, the RANSAC and ICP hooks of _HipBackend)."""
     import time
 
     from . import ops
+
+    be = backend
 
     def mark(name, t0):
         if timings is not None:
@@ -1109,23 +1190,30 @@ def pipeline_sharded(tgt: torch.Tensor, tgt_gidx: torch.Tensor, src: torch.Tenso
         return time.perf_counter()
 
     t0 = time.perf_counter()
-    trg, trx, tn = voxel_normals_slabs(tgt, tgt_gidx, voxel_size, knn, group, presorted=presorted)
+    if be is None:
+        trg, trx, tn = voxel_normals_slabs(tgt, tgt_gidx, voxel_size, knn, group, presorted=presorted)
+    else:
+        trg, trx, tn = voxel_normals_slabs(tgt, tgt_gidx, voxel_size, knn, group, voxel_fn=be.voxel,
+                                           normals_fn=be.normals, presorted=presorted)
     t0 = mark("voxel_normals_target", t0)
-    srg, srx = voxel_slabs(src, src_gidx, voxel_size, group, presorted=presorted)
+    if be is None:
+        srg, srx = voxel_slabs(src, src_gidx, voxel_size, group, presorted=presorted)
+    else:
+        srg, srx = _slab_reps_generic(src, src_gidx, voxel_size, group, be.voxel, presorted)[:2]
     t0 = mark("voxel_source", t0)
     pos, mt = global_positions(trg, group)
-    am = allreduce_max(ops.absmax(trx) if trx.shape[0] else np.zeros(3), group)
+    am = allreduce_max((be or _HIP).absmax(trx) if trx.shape[0] else np.zeros(3), group)
     samples = ops.ransac_samples(mt, ransac_n, num_iterations, seed)
     plane, inl = segment_plane_sharded(trx, pos, mt, distance_threshold, ransac_n, num_iterations,
-                                       samples=samples, absmax=am, group=group)
+                                       samples=samples, absmax=am, group=group, backend=be)
     t0 = mark("segment_plane", t0)
     world, _ = _world(group)
     if world > 1:
-        target = WindowedTarget(trx, tn, pos, max_correspondence_distance, group=group)
+        target = WindowedTarget(trx, tn, pos, max_correspondence_distance, group=group, backend=be)
     else:
-        target = ops.ICPTarget(trx, tn, max_correspondence_distance)
+        target = (be or _HIP).icp_target(trx, tn, max_correspondence_distance)
     T, fit, rm = registration_icp_sharded(srx, target, max_iteration=icp_iterations, relative_fitness=0.0,
-                                          relative_rmse=0.0, group=group)
+                                          relative_rmse=0.0, group=group, backend=be)
     mark("icp", t0)
     if timings is not None and world > 1:
         timings["icp_target_fetches"] = target.fetches

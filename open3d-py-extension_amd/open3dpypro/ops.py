@@ -713,6 +713,65 @@ class ICPTarget:
         return out
 
 
+class ICPShardLoop:
+    """One rank's side of the sharded device loop (o3dx_icp_shard_*,
+    distributed.registration_icp_sharded): the state lives in the workspace;
+    step() queues the rank's match + moments into a 64-int64 digit tensor,
+    the caller all-reduces it, finish() queues the shared solve / update.
+    Nothing here waits on the device except state() and resume()."""
+
+    def __init__(self, src: torch.Tensor, absmax, max_correspondence_distance: float, init=None):
+        sorted4 = src.ndim == 2 and src.shape[1] == 4
+        if sorted4:
+            N.require_device(src, "source points")
+            if src.dtype != torch.float32:
+                raise RuntimeError("ICPShardLoop: float32 sources (spatial_sort output or (n,3))")
+            self.src = src.contiguous()
+        else:
+            self.src = _xyz(src, "source points")
+        self.sorted4 = 1 if sorted4 else 0
+        self.ns = int(self.src.shape[0])
+        self.mc = float(max_correspondence_distance)
+        self.dev = self.src.device
+        L = N.load()
+        self.L = L
+        self.ws = torch.empty(int(L.o3dx_icp_accumulate_workspace_bytes(self.ns)), dtype=torch.uint8,
+                              device=self.dev)
+        T0 = _c(np.eye(4) if init is None else init, np.float64).reshape(4, 4)
+        am = _c(absmax, np.float64).reshape(3)
+        self.st = N.stream_ptr(self.dev)
+        N.check(L.o3dx_icp_shard_begin(_np_ptr(T0), _np_ptr(am), self.mc, self.ns, N.ptr(self.ws), self.ws.numel(),
+                                       self.st), "icp_shard_begin")
+
+    def step(self, target, digits: torch.Tensor, use_prior: bool, widen: float = float("inf")):
+        tws = None if target is None else N.ptr(target.ws)
+        desc = None if target is None else _np_ptr(target.desc)
+        N.check(self.L.o3dx_icp_shard_step(N.ptr(self.src), self.ns, self.sorted4, tws, desc, self.mc,
+                                           1 if use_prior else 0, float(widen), N.ptr(digits), N.ptr(self.ws),
+                                           self.ws.numel(), self.st), "icp_shard_step")
+
+    def finish(self, digits: torch.Tensor, n_total: int, it: int, max_iteration: int, relative_fitness: float,
+               relative_rmse: float, target=None, win: Optional[torch.Tensor] = None, widen: float = float("inf")):
+        desc = None if target is None else _np_ptr(target.desc)
+        world = 0 if win is None else int(win.shape[0])
+        N.check(self.L.o3dx_icp_shard_finish(N.ptr(digits), int(n_total), int(it), int(max_iteration),
+                                             float(relative_fitness), float(relative_rmse), self.mc, desc,
+                                             None if win is None else N.ptr(win), world, float(widen), self.ns,
+                                             N.ptr(self.ws), self.ws.numel(), self.st), "icp_shard_finish")
+
+    def state(self):
+        """(T, fitness, inlier_rmse, info {done, iterations applied, window stop}) — one host wait"""
+        T = np.zeros((4, 4), np.float64)
+        fit, rm = np.zeros(1), np.zeros(1)
+        info = np.zeros(3, np.int32)
+        N.check(self.L.o3dx_icp_shard_state(self.ns, N.ptr(self.ws), self.ws.numel(), _np_ptr(T), _np_ptr(fit),
+                                            _np_ptr(rm), _np_ptr(info), self.st), "icp_shard_state")
+        return T, float(fit[0]), float(rm[0]), info
+
+    def resume(self):
+        N.check(self.L.o3dx_icp_shard_resume(self.ns, N.ptr(self.ws), self.ws.numel(), self.st), "icp_shard_resume")
+
+
 def spatial_sort_f64(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
     """(n,4) float64 form of spatial_sort for float64 sources (x, y, z,
     original index), o3dx_spatial_sort_f64: ICPTarget.register's fast input

@@ -342,6 +342,14 @@ class OracleBackend:
         tgt, tn, mc = target
         return O.icp_accumulate_fx(src, tgt, tn, mc, T, absmax)
 
+    # the slab steps of distributed.pipeline_sharded
+    def voxel(self, p, vs, mn, mx):
+        return _o3_voxel(p, vs, mn, mx)
+
+    def normals(self, p, k):
+        n, kd = _o3_normals(p, k)
+        return n.float(), kd
+
 
 def _plane_cloud():
     pts = S.planted_plane(30_000, 12, frac=0.3).numpy()
@@ -358,7 +366,7 @@ def _plane_rank(rank, world, thr=0.01):
     return plane, pos[inl]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_segment_plane_sharded_bit_identical(world):
     """RANSAC with the rows spread over the ranks (sampled rows summed as bit
     patterns, integer counts, fx tie sums and refit moments): plane and
@@ -386,7 +394,7 @@ def _icp_fx_rank(rank, world):
     return Dm.registration_icp_sharded(torch.from_numpy(src[a:b]), target, max_iteration=12, backend=be)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_icp_sharded_fx_bit_identical(world):
     """Point-to-plane ICP with the source sharded: the fx moments make T,
     fitness and rmse the same bits for 1, 2 and 3 ranks; the loop is the
@@ -429,7 +437,7 @@ def _icp_window_rank(rank, world, margin):
     return T, f, r, target.fetches, target.rows_held
 
 
-@pytest.mark.parametrize("world,margin", [(2, 0.0), (3, 0.0), (3, None)])
+@pytest.mark.parametrize("world,margin", [(2, 0.0), (3, 0.0), (3, None), (8, 0.0)])
 def test_icp_windowed_target_bit_identical(world, margin):
     """ICP with the target spread over x-slabs too (distributed.WindowedTarget:
     each rank holds only the target rows within reach of its source under the
@@ -463,3 +471,61 @@ def test_deferred_slab_eligibility_is_global():
     assert not D._deferred_eligible(keys, layer, 2000, 2_000_000, 2_500_000)   # halo packets beyond the data
     big = D.slab_bounds([0.0, 0.0, 0.0], [1.0, 1.0, 1.0], 0.001, 2)        # 1001 keys, layer 1e6
     assert not D._deferred_eligible(big, 1001 * 1001, 3, 100_000, 100_000)
+
+
+# ------------------------------------------------------ eight ranks (one node)
+def _weak_cloud(world):
+    """C2-per-GPU layout (bench.py's N-rank headline): world unit cubes of
+    points side by side along x, one uniform cloud over [0,world) x [0,1)^2"""
+    p = S.uniform_cube(20_000 * world, 37)
+    p[:, 0] *= float(world)
+    return p
+
+
+def _weak_rank(rank, world):
+    pts = _weak_cloud(world)
+    g = torch.arange(rank, pts.shape[0], world, dtype=torch.int64)  # interleaved: the point exchange runs
+    return D.voxel_normals_slabs(pts[g], g, 0.05, knn=30, voxel_fn=_o3_voxel, normals_fn=_o3_normals)
+
+
+def test_c4_slabs_eight_ranks():
+    """the slab decomposition on 8 ranks (gloo), each slab one
+    unit cube of the weak-scaling layout: reps and normals equal to one
+    process's, bit for bit."""
+    res = spawn(_weak_rank, world=8)
+    _check_slabs(res, _weak_cloud(8).numpy(), 0.05)
+
+
+def _pipe_clouds():
+    tgt = S.box_surface(100_000, 1)
+    src = S.apply_transform(S.box_surface(100_000, 2), S.rigid_transform())
+    return tgt, src
+
+
+def _pipe_rank(rank, world):
+    tgt, src = _pipe_clouds()
+    gt = torch.arange(rank, tgt.shape[0], world, dtype=torch.int64)
+    gs = torch.arange(rank, src.shape[0], world, dtype=torch.int64)
+    out = D.pipeline_sharded(tgt[gt], gt, src[gs], gs, 0.01, knn=30, distance_threshold=0.002, num_iterations=200,
+                             seed=7, max_correspondence_distance=0.02, icp_iterations=6, backend=OracleBackend())
+    return (out["target_rep_gidx"], out["target_normals"], out["plane"], out["plane_inlier_rows"],
+            out["transformation"], out["fitness"], out["inlier_rmse"], out["target_reps"], out["source_reps"])
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_pipeline_sharded_ranks_match_one(world):
+    """C5's chain (distributed.pipeline_sharded: slab voxel reps + normals of
+    the target, slab reps of the source, sharded RANSAC, sharded ICP with a
+    windowed target) on 2 and 8 gloo ranks with the oracle as each rank's
+    compute: every output the same bits as the chain on one process."""
+    res = spawn(_pipe_rank, world=world)
+    one = _plain(_pipe_rank(0, 1))
+    g = np.concatenate([r[0] for r in res])
+    o = np.argsort(g, kind="stable")
+    assert np.array_equal(g[o], one[0])
+    assert np.array_equal(np.concatenate([r[1] for r in res])[o], one[1])
+    assert np.array_equal(np.sort(np.concatenate([r[3] for r in res])), np.sort(one[3])) and len(one[3]) > 0
+    for r in res:
+        assert np.array_equal(r[2], one[2]) and r[7] == one[7] and r[8] == one[8]
+        assert np.array_equal(r[4], one[4]) and r[5] == one[5] and r[6] == one[6]
+    assert one[5] > 0.9 and np.abs(one[4] - np.linalg.inv(S.rigid_transform())).max() < 2e-3

@@ -450,3 +450,60 @@ def test_c5_pipeline_sharded_matches_single(world, tiled):
         assert np.array_equal(r[4], icp["transformation"])
         assert r[5] == icp["fitness"] and r[6] == icp["inlier_rmse"]
     assert np.abs(icp["transformation"] - np.linalg.inv(S.rigid_transform())).max() < 1e-3
+
+
+# ------------------------------------------ sharded ICP: the device loop
+def _icp_window_dev_rank(rank, world, margin, rel):
+    """target AND source in x-slabs, each rank a WindowedTarget: the device
+    loop (o3dx_icp_shard_*) with window stops when T leaves a window"""
+    dev = torch.device("cuda:0")
+    src, tgt = _clouds()
+    t = torch.from_numpy(tgt).to(dev)
+    tn = ops.estimate_normals(t, knn=30)
+    cut_t = np.quantile(tgt[:, 0], np.linspace(0, 1, world + 1)[1:-1])
+    cut_s = np.quantile(src[:, 0], np.linspace(0, 1, world + 1)[1:-1])
+    pos = np.nonzero(np.searchsorted(cut_t, tgt[:, 0], side="right") == rank)[0]
+    mine = np.searchsorted(cut_s, src[:, 0], side="right") == rank
+    p = torch.from_numpy(pos).to(dev)
+    target = D.WindowedTarget(t[p].contiguous(), tn[p].contiguous(), p, 0.02, margin=margin)
+    T, f, r = D.registration_icp_sharded(torch.from_numpy(src[mine]).to(dev), target, max_iteration=20,
+                                         relative_fitness=rel, relative_rmse=rel, n_source_total=len(src))
+    return T, f, r, target.fetches
+
+
+@pytest.mark.parametrize("world,margin,rel", [(2, 0.0, 0.0), (3, None, 1e-6)])
+def test_sharded_icp_device_loop_windowed(world, margin, rel):
+    """The sharded device loop with the target spread over the ranks too:
+    margin 0 makes nearly every update leave some window, so the loop stops
+    on the device, the windows are refetched and the loop resumes (the
+    matches of the old window are not reused); with Open3D's relative
+    criteria the loop may also converge early on every rank alike.  T,
+    fitness and rmse equal the single-GPU device loop's to the bit."""
+    import functools
+
+    res = spawn(functools.partial(_icp_window_dev_rank, margin=margin, rel=rel), world=world)
+    src, tgt = _clouds()
+    dev = torch.device("cuda:0")
+    t = torch.from_numpy(tgt).to(dev)
+    tn = ops.estimate_normals(t, knn=30)
+    one = ops.registration_icp(torch.from_numpy(src).to(dev), t, tn, 0.02, max_iteration=20, relative_fitness=rel,
+                               relative_rmse=rel, return_corr=False)
+    for T, f, r, fetches in res:
+        assert np.array_equal(T, one["transformation"]) and f == one["fitness"] and r == one["inlier_rmse"]
+    if margin == 0.0:
+        assert max(r[3] for r in res) > 1  # the window-stop path ran
+
+
+def _icp_skip_off_rank(rank, world):
+    import os
+    os.environ["O3DX_ICP_SKIP"] = "0"
+    return _rank(rank, world)
+
+
+def test_sharded_icp_device_loop_full_search():
+    """O3DX_ICP_SKIP=0: every step of the sharded device loop searches in
+    full; the same T as the skip-proof loop's (and the single GPU's)."""
+    res = spawn(_icp_skip_off_rank, world=2)
+    res2 = spawn(_rank, world=2)
+    for (T, f, r), (T2, f2, r2) in zip(res, res2):
+        assert np.array_equal(T, T2) and f == f2 and r == r2

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     for name in decl:
         assert hasattr(lib, name), name
     assert sorted(N.declared_symbols()) == decl
-    assert lib.o3dx_abi_version() == 6
+    assert lib.o3dx_abi_version() == 7
 
 
 def test_library_host_only_entry_points():
