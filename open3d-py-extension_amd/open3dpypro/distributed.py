@@ -380,6 +380,7 @@ def _registration_icp_sharded_device(src, target, init, max_iteration, relative_
     T0 = np.eye(4) if init is None else np.array(init, np.float64).reshape(4, 4)
     windowed = isinstance(target, WindowedTarget)
     if windowed:
+        target.widen = target.mc
         target.bind(src)
         tgt = target.for_transform(T0)
         mc, widen = target.mc, target.widen
@@ -425,10 +426,11 @@ class WindowedTarget:
                  max_correspondence_distance: float, margin: Optional[float] = None, group=None, backend=None):
         self.xyz, self.nrm, self.pos = xyz, normals, pos
         self.mc = float(max_correspondence_distance)
-        # the need also covers `widen` beyond the radius: the skip proof's
-        # full searches reach 0.1 cell past the match (the device loop caps it
-        # at widen, o3dx_icp_shard_step)
-        self.widen = self.mc
+        # the need also covers `widen` beyond the radius: under the device
+        # loop (registration_icp_sharded on the GPU) the skip proof's full
+        # searches reach 0.1 cell past the match, capped at widen = the radius
+        # (o3dx_icp_shard_step); the host loop searches the radius only
+        self.widen = 0.0
         self.margin = 4.0 * self.mc if margin is None else float(margin)
         self.group, self.be = group, backend or _HIP
         self.boxes = None
