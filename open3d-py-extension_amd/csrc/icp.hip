@@ -475,7 +475,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOD
                                                      const IcpState* __restrict__ st, double radius,
                                                      int32_t* __restrict__ mpos, int use_prior,
                                                      int64_t* __restrict__ acc, float* __restrict__ budget,
-                                                     double ext) {
+                                                     double ext, float4* __restrict__ mca,
+                                                     float2* __restrict__ mcb) {
   constexpr bool SKIP = MODE == 2;
   __shared__ int64_t sh[kBlock / 64][2 * kNS];
   if (st->done) return;  // converged: the loop's remaining steps do nothing
@@ -508,20 +509,26 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOD
         const float b = budget[j];
         const int mp = mpos[j];
         if (mp >= 0 && b > 0.0f) {
-          // the match's point and normal, both gathers in flight at once
+          // the match's point and normal: float32 targets read them from the
+          // match cache the last full search wrote (mca / mcb, in source
+          // order: coalesced, where gathers by target position are not),
+          // float64 targets gather them
           double cx, cy, cz;
+          float4 cn;
           if constexpr (F64) {
             const double4 c = g.pts64[mp];
             cx = c.x;
             cy = c.y;
             cz = c.z;
+            cn = tnorm[mp];
           } else {
-            const float4 c = g.pts[mp];
-            cx = c.x;
-            cy = c.y;
-            cz = c.z;
+            const float4 a = mca[j];
+            const float2 bb = mcb[j];
+            cx = a.x;
+            cy = a.y;
+            cz = a.z;
+            cn = make_float4(a.w, bb.x, bb.y, 0.f);
           }
-          const float4 cn = tnorm[mp];
           double qx, qy, qz;
           apply_T(st->Tp, raw[0], raw[1], raw[2], &qx, &qy, &qz);
           const double dx = px - qx, dy = py - qy, dz = pz - qz;
@@ -567,6 +574,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOD
             vz = v.z;
           }
           nt = tnorm[pos];
+          if constexpr (SKIP && !F64) {  // the match cache of the next steps' skip proofs
+            mca[j] = make_float4((float)vx, (float)vy, (float)vz, nt.x);
+            mcb[j] = make_float2(nt.y, nt.z);
+          }
         }
       }
     }
@@ -822,6 +833,8 @@ struct AccWs {
   int32_t* cj;
   int32_t* mpos;
   float* budget;  // the device loop's skip proof: margin left per source point
+  float4* mca;    // ... and its match cache: (target x, y, z, normal x) per source point
+  float2* mcb;    // (normal y, z)
   uint8_t* flags;
   int32_t* src_idx;
   int32_t* scan_tmp;
@@ -839,6 +852,8 @@ static size_t acc_carve(Arena& ar, int64_t ns, AccWs* w) {
   w->cj = ar.take<int32_t>(ns);
   w->mpos = ar.take<int32_t>(ns);
   w->budget = ar.take<float>(ns);
+  w->mca = ar.take<float4>(ns);
+  w->mcb = ar.take<float2>(ns);
 
   w->flags = ar.take<uint8_t>(ns + 16);
   w->src_idx = ar.take<int32_t>(ns);
@@ -941,7 +956,7 @@ static void launch_step(const void* src, int64_t ns, bool sorted, const GridView
   KTimer km("icp_match", s);
 #define O3DX_STEP(SO, F6, MO)                                                                                     \
   hipLaunchKernelGGL((k_icp_step<SO, F6, MO>), dim3(nb), dim3(kBlock), 0, s, src, ns, g, tn, w.st, radius, w.mpos, \
-                     use_prior, w.acc, w.budget, ext)
+                     use_prior, w.acc, w.budget, ext, w.mca, w.mcb)
 #define O3DX_STEPS(MO)                         \
   do {                                         \
     if (f64 && sorted) O3DX_STEP(true, true, MO);   \
