@@ -128,6 +128,28 @@ class KDTreeGrid:
         return self._one(query, N.SEARCH_RADIUS, 0, radius)
 
 
+def _warn_offset_icp(src: "PointCloudBase", tgt: "PointCloudBase"):
+    """Point-to-plane ICP forms J = p x n on the raw coordinates, so its 6x6
+    normal matrix has entries ~|p|^2 against ~1: far from the origin relative
+    to its extent (georeferenced LAS / E57 scans, ~5e5 m) the system is
+    rounding noise in float64 — for Open3D as well (tests/test_oracle.py
+    test_icp_offset_conditioning).  Warn; the remedy is to register in a
+    re-centred frame (subtract a common origin from both clouds)."""
+    import warnings
+
+    mn, mx = src.get_aabb() if hasattr(src, "get_aabb") else (None, None)
+    tmn, tmx = tgt.get_aabb() if hasattr(tgt, "get_aabb") else (None, None)
+    if mn is None or tmn is None:
+        return
+    far = max(np.abs(np.asarray(mn)).max(), np.abs(np.asarray(mx)).max(), np.abs(np.asarray(tmn)).max(),
+              np.abs(np.asarray(tmx)).max())
+    ext = max(float(np.max(np.asarray(mx) - np.asarray(mn))), float(np.max(np.asarray(tmx) - np.asarray(tmn))), 1e-12)
+    if far / ext > 1e3:
+        warnings.warn(f"registration_icp: the clouds lie {far:.3g} from the origin at an extent of {ext:.3g}; "
+                      "point-to-plane ICP on raw coordinates that far out is ill-conditioned in float64 (Open3D's "
+                      "too): register in a re-centred frame", RuntimeWarning, stacklevel=3)
+
+
 class PointCloudBase:
     COLOR_CHART = np.asarray([[230, 0, 18], [243, 152, 0], [252, 200, 0], [143, 195, 31], [0, 153, 68],
                               [0, 160, 233], [29, 32, 136], [146, 7, 131], [228, 0, 127]])
@@ -889,6 +911,8 @@ class PointCloud(PointCloudUtility):
         wide = self._wide or target._wide
         src = self._plane_points() if wide else self._dev_points()
         tgt = target._plane_points() if wide else target._dev_points()
+        if wide:
+            _warn_offset_icp(self, target)
         r = ops.registration_icp(src, tgt, target._normals,
                                  max_correspondence_distance, init, max_iteration, relative_fitness, relative_rmse)
         return RegistrationResult(r["transformation"], r["fitness"], r["inlier_rmse"],

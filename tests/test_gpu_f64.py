@@ -233,3 +233,21 @@ def test_f64_icp_target_sorted_dtype_mismatch(dev):
     t32 = ops.ICPTarget(tgt32, ops.estimate_normals(tgt32, knn=30), 0.8)
     with pytest.raises(RuntimeError, match="sorted source"):
         t32.register(ops.spatial_sort_f64(src32.double()), max_iteration=2)
+
+
+def test_f64_registration_icp_warns_at_georeferenced_offset():
+    """registration_icp on a raw georeferenced scan (the
+    ~5e5 m offset) warns that the point-to-plane system is ill-conditioned
+    there (for Open3D as well) and names the remedy; the 1e4 m case does not."""
+    n = 20_000
+    src = PointCloud(S.las_scene(n, seed=1).numpy())
+    tgt = PointCloud(S.las_scene(n, seed=0).numpy()).estimate_normals()
+    with pytest.warns(RuntimeWarning, match="re-centred frame"):
+        src.registration_icp(tgt, 0.8, max_iteration=2)
+    off = (12345.678, 23456.789, 98.765)
+    s2 = PointCloud(S.las_scene(n, seed=1, offset=off).numpy())
+    t2 = PointCloud(S.las_scene(n, seed=0, offset=off).numpy()).estimate_normals()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        s2.registration_icp(t2, 0.8, max_iteration=2)
