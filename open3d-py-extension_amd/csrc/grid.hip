@@ -830,6 +830,36 @@ struct MomAccA {
   }
 };
 
+// Open3D ComputeCovariance on float64 storage: the nine cumulants summed in
+// the neighbours' result order (nanoflann's: (d^2, index) ascending), each
+// product rounded then added (the build's -ffp-contract=off) — the float64
+// coordinates' products are not exact, so the order and the roundings are
+// Open3D's own, for the same bits.
+struct MomAccSeq {
+  double m[9];
+  __device__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) m[j] = 0.0;
+  }
+  __device__ void add(double x, double y, double z) {
+    m[0] += x;
+    m[1] += y;
+    m[2] += z;
+    m[3] += x * x;
+    m[4] += x * y;
+    m[5] += x * z;
+    m[6] += y * y;
+    m[7] += y * z;
+    m[8] += z * z;
+  }
+  __device__ void cov(int k, double c[6]) const {
+    MomAcc a;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) a.m[j] = m[j];
+    a.cov(k, c);
+  }
+};
+
 // wave-wide exact sum of exact terms (the same condition as MomAccDD): an
 // xor tree of (h, l) pairs joined by TwoSum, h + l rounded once
 __device__ __forceinline__ double wave_sum_exact(double t) {
@@ -1213,6 +1243,136 @@ __device__ __forceinline__ bool stile_finish(const float4 q, int kneed, int ns, 
   return true;
 }
 
+// The float64 tiles' completion (GridView::pts64: a float64 cloud whose tile
+// distances are float32 FRAME distances, within g.d64 of the exact ones).
+// lst[0..n) holds every candidate with frame d^2 < Ub; entries with frame d^2
+// < Lm are certain members, the rest are the band.  The band's (k - #certain)
+// nearest are picked by the EXACT float64 (d^2, original index) order; then
+// all k members are sorted by it (a bitonic network over 32 registers) and
+// summed in that order with separate float64 products and sums — nanoflann's
+// result order and Open3D's ComputeCovariance arithmetic, for the same bits
+// as the float64 lane-per-query form (k_normals_knn64).
+struct Key64 {
+  double d;
+  int i;  // original index (the tie-break)
+  int p;  // LDS tile slot
+};
+__device__ __forceinline__ bool key_less(const Key64& a, const Key64& b) {
+  return a.d < b.d || (a.d == b.d && a.i < b.i);
+}
+template <int I, int J, bool UP>
+__device__ __forceinline__ void key_ce(Key64 (&k)[32]) {
+  const bool sw = UP ? key_less(k[J], k[I]) : key_less(k[I], k[J]);
+  const Key64 a = k[I], b = k[J];
+  k[I].d = sw ? b.d : a.d;
+  k[I].i = sw ? b.i : a.i;
+  k[I].p = sw ? b.p : a.p;
+  k[J].d = sw ? a.d : b.d;
+  k[J].i = sw ? a.i : b.i;
+  k[J].p = sw ? a.p : b.p;
+}
+// bitonic sort of 32 keys, ascending (compile-time indices throughout)
+template <int SZ, int ST, int I>
+__device__ __forceinline__ void key_stage(Key64 (&k)[32]) {
+  if constexpr (I < 32) {
+    constexpr int J = I ^ ST;
+    if constexpr (J > I) key_ce<I, J, (I & SZ) == 0>(k);
+    key_stage<SZ, ST, I + 1>(k);
+  }
+}
+template <int SZ, int ST>
+__device__ __forceinline__ void key_merge(Key64 (&k)[32]) {
+  if constexpr (ST > 0) {
+    key_stage<SZ, ST, 0>(k);
+    key_merge<SZ, ST / 2>(k);
+  }
+}
+template <int SZ>
+__device__ __forceinline__ void key_sort(Key64 (&k)[32]) {
+  if constexpr (SZ <= 32) {
+    key_merge<SZ, SZ / 2>(k);
+    key_sort<SZ * 2>(k);
+  }
+}
+
+__device__ __forceinline__ Key64 key64_of(const double4* __restrict__ pts64, double qx, double qy, double qz,
+                                          const int32_t* tp, int p) {
+  const double4 v = pts64[tp[p]];
+  return Key64{dist2_d4(qx, qy, qz, v), (int)v.w, p};
+}
+
+// (the grid's members by value: a GridView reference would put the kernel
+// argument in scratch)
+__device__ __forceinline__ bool finish_selection64(const double4* __restrict__ pts64, int32_t* __restrict__ nbr,
+                                                   float* __restrict__ kd2, double qx, double qy, double qz,
+                                                   const float4 q, int kneed, int n, float Lm, float U, float Ub,
+                                                   uint16_t (*lst)[64], uint16_t (*band)[64], int lane,
+                                                   const float* tx, const float* ty, const float* tz,
+                                                   const int32_t* tp, const float* __restrict__ prior, int oi,
+                                                   float* __restrict__ out) {
+  // 1. certain members compacted to the front of the list, the band apart
+  int nsel = 0, nb = 0, nU = 0;
+  for (int j = 0; j < n; ++j) {
+    const int p = (int)lst[j][lane];
+    const float d2f = dist2_f32(q, tx[p], ty[p], tz[p]);
+    nU += d2f < U ? 1 : 0;
+    if (d2f < Lm) {
+      lst[nsel][lane] = (uint16_t)p;  // (the write position never passes the read position)
+      ++nsel;
+    } else if (d2f < Ub) {
+      band[min(nb, kBndCap)][lane] = (uint16_t)p;
+      ++nb;
+    }
+  }
+  // nU >= k: the k-th nearest lies within sqrt(U) + d64, so all k nearest are listed
+  if (nsel > kneed || nb > kBndCap || nsel + nb < kneed || nU < kneed) return false;
+  const int need = kneed - nsel;
+  // 2. the band's `need` nearest by the exact order, appended
+  Key64 bk[kBndCap];
+#pragma unroll
+  for (int i = 0; i < kBndCap; ++i) {
+    bk[i] = Key64{INFINITY, 0x7fffffff, 0};
+    if (i < nb) bk[i] = key64_of(pts64, qx, qy, qz, tp, (int)band[i][lane]);
+  }
+  uint32_t picked = 0;
+  for (int t = 0; t < need; ++t) {  // repeated minimum (register indices stay compile-time)
+    Key64 best{INFINITY, 0x7fffffff, 0};
+    int bi = 0;
+#pragma unroll
+    for (int i = 0; i < kBndCap; ++i)
+      if (!((picked >> i) & 1u) && key_less(bk[i], best)) {
+        best = bk[i];
+        bi = i;
+      }
+    picked |= 1u << bi;
+    lst[nsel + t][lane] = (uint16_t)best.p;
+  }
+  // 3. the k members in the exact order, Open3D's sequential moments
+  Key64 kk[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    kk[i] = Key64{INFINITY, 0x7fffffff, 0};
+    if (i < kneed) kk[i] = key64_of(pts64, qx, qy, qz, tp, (int)lst[i][lane]);
+  }
+  key_sort<2>(kk);
+  MomAccSeq acc;
+  acc.zero();
+  int32_t* const nrow = nbr ? nbr + (int64_t)oi * kneed : nullptr;  // test hook
+  double dk = 0.0;  // the k-th key (no dynamic index into the register array)
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    if (i < kneed) {
+      const double4 v = pts64[tp[kk[i].p]];
+      if (nrow) nrow[i] = kk[i].i;
+      acc.add(v.x, v.y, v.z);
+      dk = kk[i].d;
+    }
+  }
+  if (kd2) kd2[oi] = (float)(dk * (1.0 + 1e-6));
+  finish_normal(kneed, acc, prior, oi, out);
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // KNN normals, LDS-tile form (first level of the default KNN path).
 // One block = one wave = one chunk of <= 64 consecutive queries in one grid
@@ -1331,13 +1491,19 @@ __device__ __forceinline__ void tile_row(const GridView& g, const TileBox& b, co
     atomicAdd(&hw[(ix_ + 1) * 64 + lane], 1u);                                              \
   })
 
-template <int KMAX, class TAcc = MomAccA>
+// F64: a float64 cloud's grid (GridView::pts64, frame coordinates in pts):
+// the same scans on the frame, widened by the frame error g.d64, and the
+// exact completion finish_selection64 (KMAX 32).
+template <int KMAX, class TAcc = MomAccA, bool F64 = false>
 __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
                                                              int kneed, const float* __restrict__ prior,
                                                              float* __restrict__ out, int32_t* __restrict__ fb_list,
                                                              int32_t* __restrict__ fb_len, int dbg) {
   static_assert(kTileQ == 64, "one wave per tile");
+  static_assert(!F64 || KMAX == 32, "float64 tiles sort 32 keys");
   __shared__ float tx[kTilePts], ty[kTilePts], tz[kTilePts];
+  __shared__ int32_t tp[F64 ? kTilePts : 1];              // float64: the slots' global positions
+  __shared__ uint16_t band64[F64 ? kBndCap + 1 : 1][64];  // float64: the band apart from the list
   __shared__ int32_t ccs[kTileCs];
   __shared__ int32_t rows[kMaxTileRows + 1];
   __shared__ int32_t rst[kMaxTileRows];
@@ -1394,7 +1560,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
       box.z1 = min(az + 1, g.nz - 1);
       box.nxr = box.x1 - box.x0 + 1;
       box.nyr = box.y1 - box.y0 + 1;
-      staged = stage_tile<kTileQ, kTilePts>(g, box, tx, ty, tz, ccs, kTileCs, rows, rst);
+      staged = stage_tile<kTileQ, kTilePts>(g, box, tx, ty, tz, ccs, kTileCs, rows, rst, F64 ? tp : nullptr);
       if (staged >= 0 || x_hi == x_lo) break;
       __syncthreads();
       x_hi = x_lo + (x_hi - x_lo) / 2;
@@ -1408,7 +1574,10 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
         const double reach = cube_reach(g, q.x, q.y, q.z, cx, cy, cz, 1);
         double R = (reach == INFINITY) ? (double)(g.nx + g.ny + g.nz) * g.h : reach - g.slack;
         R = fmin(R, outer_reach(g, q.x, q.y, q.z));
-        const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - 4.0f * kRelEps) : 0.0f;
+        // float64: the k nearest by exact distance lie within frame distance
+        // sqrt(U) + 2 d64 of the frame query, which must stay inside R
+        if (F64) R -= 2.0 * (double)g.d64;
+        const float R2 = (R > 0.0) ? (float)(R * R) * (1.0f - (F64 ? 16.0f : 4.0f) * kRelEps) : 0.0f;
         uint32_t* hw = selbuf;
         TileHist th;
         O3DX_TILE_HIST(0.0f, (float)kHistBins / fmaxf(R2, 1e-30f), R2)
@@ -1430,7 +1599,13 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
           O3DX_TILE_HIST(lo, (float)kHistBins / (hi - lo), hi)
         }
         if (!fb && dbg != 2) {
-          const float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
+          float Lm = L * (1.0f - 2.0f * kRelEps), Up = U * (1.0f + 2.0f * kRelEps);
+          if constexpr (F64) {  // frame distances: certain below sqrt(L) - 2 d64, listed below sqrt(U) + 2 d64
+            const float e2 = 2.0f * g.d64, sl = sqrtf(L) * (1.0f - 2.0f * kRelEps) - e2;
+            Lm = sl > 0.0f ? sl * sl * (1.0f - 4.0f * kRelEps) : -1.0f;
+            const float su = sqrtf(U) * (1.0f + 2.0f * kRelEps) + e2;
+            Up = su * su * (1.0f + 4.0f * kRelEps);
+          }
           // branch-free append of every candidate below Up: candidate u of a
           // group of four is written to slot n + (#accepted before u), so the
           // accepted ones end up contiguous and a rejected one is overwritten
@@ -1460,6 +1635,11 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
           }
           if (dbg == 3) {
             if (n == 12345) out[0] = 0.f;  // keep the scan alive
+          } else if constexpr (F64) {
+            const double4 q64 = g.pts64[s];
+            fb = n > kListMax || !finish_selection64(g.pts64, g.nbr, g.kd2, q64.x, q64.y, q64.z, q, kneed, n, Lm, U,
+                                                     Up, lst, band64, lane, tx, ty, tz, tp, prior, out_row(g, qw),
+                                                     out);
           } else
           fb = n > kListMax ||
                !finish_selection<KMAX, TAcc>(
@@ -2917,51 +3097,44 @@ int grid64_build(const double* xyz, int64_t n, double target_occ, double min_h, 
   O3DX_HIP(hipGetLastError());
   out->pts64 = pts64;
   out->view.pts64 = pts64;
+  {
+    // frame error: each frame coordinate (float)(p - o) lies in [0, extent],
+    // rounded by at most half an ulp of the largest extent; a distance between
+    // two frame points is then within 2 sqrt(3) of those of the exact one
+    double fm = 0.0;
+    for (int a = 0; a < 3; ++a) fm = std::max(fm, mm[3 + a] - mm[a]);
+    const double half_ulp = fm > 0.0 ? std::ldexp(1.0, std::ilogb(fm) - 24) : 0.0;
+    out->view.d64 = (float)(2.0 * std::sqrt(3.0) * half_ulp * 1.01 + 1e-30);
+  }
   out->view.o64x = mm[0];
   out->view.o64y = mm[1];
   out->view.o64z = mm[2];
   return 0;
 }
 
-// Open3D ComputeCovariance on float64 storage: the nine cumulants summed in
-// the neighbours' result order (nanoflann's: (d^2, index) ascending), each
-// product rounded then added (the build's -ffp-contract=off) — the float64
-// coordinates' products are not exact, so the order and the roundings are
-// Open3D's own, for the same bits.
-struct MomAccSeq {
-  double m[9];
-  __device__ void zero() {
-#pragma unroll
-    for (int j = 0; j < 9; ++j) m[j] = 0.0;
-  }
-  __device__ void add(double x, double y, double z) {
-    m[0] += x;
-    m[1] += y;
-    m[2] += z;
-    m[3] += x * x;
-    m[4] += x * y;
-    m[5] += x * z;
-    m[6] += y * y;
-    m[7] += y * z;
-    m[8] += z * z;
-  }
-  __device__ void cov(int k, double c[6]) const {
-    MomAcc a;
-#pragma unroll
-    for (int j = 0; j < 9; ++j) a.m[j] = m[j];
-    a.cov(k, c);
-  }
-};
-
 // Normals of a float64 cloud, a lane per point (sorted order): KNN / HYBRID
 // through the register top-K in (d^2, index) order; RADIUS (every neighbour
 // within r, sorted, Open3D's SearchRadius) read off in sorted pages of 32.
 template <int K>
+__device__ __forceinline__ void knn64_normal_query(const GridView& g, const double* __restrict__ xyz, int kneed,
+                                                   int mode, double radius, const float* __restrict__ prior,
+                                                   float* __restrict__ out, int64_t s);
+
+// list (nullable): the sorted positions the float64 tiles handed on (*list_len of them)
+template <int K>
 __global__ void __launch_bounds__(kBlock) k_normals_knn64(GridView g, const double* __restrict__ xyz, int kneed,
                                                           int mode, double radius, const float* __restrict__ prior,
-                                                          float* __restrict__ out) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= g.n) return;
+                                                          float* __restrict__ out, const int32_t* __restrict__ list,
+                                                          const int32_t* __restrict__ list_len) {
+  const int64_t lim = list ? (int64_t)*list_len : g.n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < lim; t += (int64_t)gridDim.x * blockDim.x)
+    knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list ? list[t] : t);
+}
+
+template <int K>
+__device__ __forceinline__ void knn64_normal_query(const GridView& g, const double* __restrict__ xyz, int kneed,
+                                                   int mode, double radius, const float* __restrict__ prior,
+                                                   float* __restrict__ out, int64_t s) {
   const double4 q = g.pts64[s];
   const int oi = (int)q.w;
   MomAccSeq acc;
@@ -3216,7 +3389,16 @@ extern "C" int o3dx_voxel_down_sample_normals(const float* xyz, int64_t n, const
 }
 
 // ------------------------------------------------------ float64 boundary
-extern "C" size_t o3dx_normals_f64_workspace_bytes(int64_t n) { return grid64_ws_bytes(n) + 1024; }
+// [float64 grid][tiles: lens, hand-off list, chunk starts, chunk-plan scratch]
+static size_t normals64_tiles_bytes(int64_t n) {
+  n = std::max<int64_t>(n, 1);
+  const int64_t rows = cap_cells(n, 4);  // grid rows (ny * nz) are bounded by the cell cap
+  return Arena::align(4 * 4 + 1) + Arena::align(n * 4 + 1) + Arena::align((n / 64 + rows + 4) * 4 + 1) +
+         chunk_plan_ws_bytes(n, rows) + 1024;
+}
+extern "C" size_t o3dx_normals_f64_workspace_bytes(int64_t n) {
+  return grid64_ws_bytes(n) + normals64_tiles_bytes(n) + 1024;
+}
 
 extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode, int knn, double radius,
                                          const float* prior, float* out, float* kd2, void* ws, size_t ws_bytes,
@@ -3237,11 +3419,36 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
   G.view.kd2 = mode == O3DX_SEARCH_KNN ? kd2 : nullptr;
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
   KTimer kt("normals_f64", s);
-  if (mode == O3DX_SEARCH_RADIUS)
-    hipLaunchKernelGGL(k_normals_knn64<4>, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, 0, mode, radius, prior, out);
-  else
+  const int32_t* none = nullptr;
+  if (mode == O3DX_SEARCH_KNN && kneed >= 1 && kneed <= 32 && !getenv("O3DX_F64_NO_TILES")) {
+    // LDS tiles on the float32 frame, the exact float64 order deciding
+    // (k_normals_knn_tile<32, *, true>), then the lane-per-query form for the
+    // queries they hand on
+    const size_t g64 = grid64_ws_bytes(n);
+    Arena ar((char*)ws + g64, ws_bytes - g64);
+    int32_t* lens = ar.take<int32_t>(4);
+    int32_t* list = ar.take<int32_t>(n);
+    const int64_t upper = chunk_plan_upper(n, G.view, kTileQ);
+    int32_t* chunks = ar.take<int32_t>(upper + 2);
+    const size_t pws_bytes = chunk_plan_ws_bytes(n, (int64_t)G.view.ny * G.view.nz);
+    void* pws = ar.take<char>(pws_bytes);
+    O3DX_ARENA_CHECK(ar);
+    O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
+    O3DX_TRY(chunk_plan(n, G.view, kTileQ, chunks, pws, pws_bytes, s));
+    {
+      KTimer kt_tile("normals_tile64", s);
+      hipLaunchKernelGGL((k_normals_knn_tile<32, MomAccA, true>), dim3((unsigned)upper), dim3(kTileQ), 0, s, G.view,
+                         chunks, kneed, prior, out, list, lens, 0);
+    }
+    O3DX_DISPATCH_K(kneed, k_normals_knn64, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed, mode,
+                    radius, prior, out, (const int32_t*)list, (const int32_t*)lens);
+  } else if (mode == O3DX_SEARCH_RADIUS) {
+    hipLaunchKernelGGL(k_normals_knn64<4>, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, 0, mode, radius, prior, out,
+                       none, none);
+  } else {
     O3DX_DISPATCH_K(kneed, k_normals_knn64, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius, prior,
-                    out);
+                    out, none, none);
+  }
   O3DX_HIP(hipGetLastError());
   return 0;
 }

@@ -46,6 +46,9 @@ struct GridView {
   // in nanoflann's order, as Open3D computes it on its float64 storage.
   const double4* __restrict__ pts64 = nullptr;
   double o64x = 0.0, o64y = 0.0, o64z = 0.0;
+  // |frame distance - exact distance| <= d64 (both points' float32 frame
+  // roundings, 2 sqrt(3) half-ulps of the frame's largest magnitude)
+  float d64 = 0.f;
 };
 
 // outer sorted position / output row of a nested-grid point
@@ -582,10 +585,12 @@ struct TileBox {
 // PTS/BLOCK) global loads before the first LDS store.
 constexpr int kMaxTileRows = 36;
 
+// tp (nullable): also each slot's global sorted position (the float64 tiles
+// fetch the exact coordinates of their members by it).
 template <int BLOCK, int PTS>
-__device__ int stage_tile(const GridView& g, const TileBox& b, float* __restrict__ tx, float* __restrict__ ty,
+__device__ __forceinline__ int stage_tile(const GridView& g, const TileBox& b, float* __restrict__ tx, float* __restrict__ ty,
                           float* __restrict__ tz, int32_t* __restrict__ ccs, int cs_cap, int32_t* __restrict__ rows,
-                          int32_t* __restrict__ rstart) {
+                          int32_t* __restrict__ rstart, int32_t* __restrict__ tp = nullptr) {
   static_assert(BLOCK >= kMaxTileRows, "row scan needs one lane per row");
   const int nrows = b.nyr * (b.z1 - b.z0 + 1);
   const int w = b.nxr + 1;
@@ -616,13 +621,15 @@ __device__ int stage_tile(const GridView& g, const TileBox& b, float* __restrict
   }
   constexpr int J = (PTS + BLOCK - 1) / BLOCK;
   float4 buf[J];
+  int gp[J];
   int k = 0;  // f only grows, so the row index is carried along
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int f = threadIdx.x + j * BLOCK;
     if (f < total) {
       while (rows[k + 1] <= f) ++k;
-      buf[j] = g.pts[rstart[k] + (f - rows[k])];
+      gp[j] = rstart[k] + (f - rows[k]);
+      buf[j] = g.pts[gp[j]];
     }
   }
 #pragma unroll
@@ -632,6 +639,7 @@ __device__ int stage_tile(const GridView& g, const TileBox& b, float* __restrict
       tx[f] = buf[j].x;
       ty[f] = buf[j].y;
       tz[f] = buf[j].z;
+      if (tp) tp[f] = gp[j];
     }
   }
   __syncthreads();

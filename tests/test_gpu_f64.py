@@ -84,6 +84,30 @@ def test_f64_normals_knn30(las, las_np):
     assert_neighbour_sets(dn.ids(), las_np, 30, "f64_las_knn30")
 
 
+@pytest.mark.parametrize("k", [30, 16, 5])
+def test_f64_normals_tiles_equal_lane_form(las, monkeypatch, k):
+    """The float64 LDS tiles (frame-distance selection, exact (d^2, index)
+    order, sequential float64 moments) give the lane-per-query form's normals
+    bit for bit (O3DX_F64_NO_TILES=1), hand-offs included, and the same k-th
+    distance bounds."""
+    a, kd_a = ops.estimate_normals(las, knn=k, return_kdist=True)
+    monkeypatch.setenv("O3DX_F64_NO_TILES", "1")
+    b, kd_b = ops.estimate_normals(las, knn=k, return_kdist=True)
+    assert torch.equal(a, b)
+    assert torch.equal(kd_a, kd_b)
+
+
+def test_f64_normals_tiles_reps_vs_oracle(las_np, dev):
+    """The tiles on the voxel representatives of the scan (5 cm-ish spacing,
+    the f64_las bench leg's shape) against the oracle, sets bit-exact."""
+    reps = las_np[O.voxel_down_sample(las_np, 0.05)]
+    x = torch.as_tensor(reps, device=dev)
+    with DebugNeighbors(len(reps), 30, dev) as dn:
+        got = ops.estimate_normals(x, knn=30).cpu().numpy()
+    assert_normals(got, O.estimate_normals(reps, O.KNN, 30), reps, k=30, what="f64_las_reps_tiles")
+    assert_neighbour_sets(dn.ids(), reps, 30, "f64_las_reps_tiles")
+
+
 def test_f64_normals_pointcloud_reps(las_np):
     """The pipeline of the reference (voxel_down_sample -> estimate_normals)
     through the drop-in API on the float64 scan."""
