@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-end evidence (ROUND, default r05), in two GPU calls:
+# Round-end evidence (ROUND, default r06), in two GPU calls:
 #   bash tools/gpu_final.sh tests   — the full -m gpu suite + smoke(), every normal
 #                                     row's parity logged to profiles-bound gpurun_out/\${R}_parity_report.jsonl
 #   bash tools/gpu_final.sh bench   — PMC passes (profiles/pmc_traffic.json refreshed
@@ -9,7 +9,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-R=${ROUND:-r05}
+R=${ROUND:-r06}
 if [ "$1" = tests ]; then
   export O3DX_PARITY_LOG=$PWD/gpurun_out/${R}_parity_report.jsonl
   rm -f "$O3DX_PARITY_LOG"
@@ -29,13 +29,18 @@ import json, os
 old = json.load(open("profiles/pmc_traffic.json"))
 new = json.load(open("gpurun_out/pmc_summary.json"))
 old["kernels"].update(new["kernels"])
-old["round"] = os.environ.get("ROUND", "r05")
+old["round"] = os.environ.get("ROUND", "r06")
 for p in ("profiles/pmc_traffic.json", "gpurun_out/pmc_traffic.json"):
     with open(p, "w") as f:
         json.dump(old, f, indent=1, sort_keys=True)
 PYEOF
 timeout -k 10 500 python bench.py > gpurun_out/${R}_bench.json 2> gpurun_out/${R}_bench.err || exit $?
 cat gpurun_out/${R}_bench.json
+# C2 only (the headline step, no secondary legs): its own kernel stats, so
+# the roofline recomputes from profiles/ without other configs' launches
+rm -rf gpurun_out/prof_${R}_c2
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R}_c2 -o run --output-format csv -- \
+  python bench.py --no-cpu --no-secondary > gpurun_out/${R}_prof_c2.log 2>&1 || exit $?
 rm -rf gpurun_out/prof_${R}
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R} -o run --output-format csv -- \
   python bench.py --no-cpu > gpurun_out/${R}_prof_bench.log 2>&1 || exit $?
