@@ -1254,8 +1254,7 @@ __device__ __forceinline__ bool stile_finish(const float4 q, int kneed, int ns, 
 // as the float64 lane-per-query form (k_normals_knn64).
 struct Key64 {
   double d;
-  int i;  // original index (the tie-break)
-  int p;  // LDS tile slot
+  int i;  // original index: the tie-break, and the row of the caller's float64 array
 };
 __device__ __forceinline__ bool key_less(const Key64& a, const Key64& b) {
   return a.d < b.d || (a.d == b.d && a.i < b.i);
@@ -1266,10 +1265,8 @@ __device__ __forceinline__ void key_ce(Key64 (&k)[32]) {
   const Key64 a = k[I], b = k[J];
   k[I].d = sw ? b.d : a.d;
   k[I].i = sw ? b.i : a.i;
-  k[I].p = sw ? b.p : a.p;
   k[J].d = sw ? a.d : b.d;
   k[J].i = sw ? a.i : b.i;
-  k[J].p = sw ? a.p : b.p;
 }
 // bitonic sort of 32 keys, ascending (compile-time indices throughout)
 template <int SZ, int ST, int I>
@@ -1298,13 +1295,14 @@ __device__ __forceinline__ void key_sort(Key64 (&k)[32]) {
 __device__ __forceinline__ Key64 key64_of(const double4* __restrict__ pts64, double qx, double qy, double qz,
                                           const int32_t* tp, int p) {
   const double4 v = pts64[tp[p]];
-  return Key64{dist2_d4(qx, qy, qz, v), (int)v.w, p};
+  return Key64{dist2_d4(qx, qy, qz, v), (int)v.w};
 }
 
 // (the grid's members by value: a GridView reference would put the kernel
 // argument in scratch)
-__device__ __forceinline__ bool finish_selection64(const double4* __restrict__ pts64, int32_t* __restrict__ nbr,
-                                                   float* __restrict__ kd2, double qx, double qy, double qz,
+__device__ __forceinline__ bool finish_selection64(const double4* __restrict__ pts64, const double* __restrict__ xyz,
+                                                   int32_t* __restrict__ nbr, float* __restrict__ kd2, double qx,
+                                                   double qy, double qz,
                                                    const float4 q, int kneed, int n, float Lm, float U, float Ub,
                                                    uint16_t (*lst)[64], uint16_t (*band)[64], int lane,
                                                    const float* tx, const float* ty, const float* tz,
@@ -1331,12 +1329,12 @@ __device__ __forceinline__ bool finish_selection64(const double4* __restrict__ p
   Key64 bk[kBndCap];
 #pragma unroll
   for (int i = 0; i < kBndCap; ++i) {
-    bk[i] = Key64{INFINITY, 0x7fffffff, 0};
+    bk[i] = Key64{INFINITY, 0x7fffffff};
     if (i < nb) bk[i] = key64_of(pts64, qx, qy, qz, tp, (int)band[i][lane]);
   }
   uint32_t picked = 0;
   for (int t = 0; t < need; ++t) {  // repeated minimum (register indices stay compile-time)
-    Key64 best{INFINITY, 0x7fffffff, 0};
+    Key64 best{INFINITY, 0x7fffffff};
     int bi = 0;
 #pragma unroll
     for (int i = 0; i < kBndCap; ++i)
@@ -1345,13 +1343,13 @@ __device__ __forceinline__ bool finish_selection64(const double4* __restrict__ p
         bi = i;
       }
     picked |= 1u << bi;
-    lst[nsel + t][lane] = (uint16_t)best.p;
+    lst[nsel + t][lane] = band[bi][lane];
   }
   // 3. the k members in the exact order, Open3D's sequential moments
   Key64 kk[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
-    kk[i] = Key64{INFINITY, 0x7fffffff, 0};
+    kk[i] = Key64{INFINITY, 0x7fffffff};
     if (i < kneed) kk[i] = key64_of(pts64, qx, qy, qz, tp, (int)lst[i][lane]);
   }
   key_sort<2>(kk);
@@ -1362,9 +1360,9 @@ __device__ __forceinline__ bool finish_selection64(const double4* __restrict__ p
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
     if (i < kneed) {
-      const double4 v = pts64[tp[kk[i].p]];
+      const int64_t id = kk[i].i;
       if (nrow) nrow[i] = kk[i].i;
-      acc.add(v.x, v.y, v.z);
+      acc.add(xyz[3 * id], xyz[3 * id + 1], xyz[3 * id + 2]);
       dk = kk[i].d;
     }
   }
@@ -1495,7 +1493,7 @@ __device__ __forceinline__ void tile_row(const GridView& g, const TileBox& b, co
 // the same scans on the frame, widened by the frame error g.d64, and the
 // exact completion finish_selection64 (KMAX 32).
 template <int KMAX, class TAcc = MomAccA, bool F64 = false>
-__global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
+__global__ void __launch_bounds__(kTileQ) __attribute__((amdgpu_waves_per_eu(2))) k_normals_knn_tile(GridView g, const int32_t* __restrict__ chunk_starts,
                                                              int kneed, const float* __restrict__ prior,
                                                              float* __restrict__ out, int32_t* __restrict__ fb_list,
                                                              int32_t* __restrict__ fb_len, int dbg) {
@@ -1637,7 +1635,7 @@ __global__ void __launch_bounds__(kTileQ) k_normals_knn_tile(GridView g, const i
             if (n == 12345) out[0] = 0.f;  // keep the scan alive
           } else if constexpr (F64) {
             const double4 q64 = g.pts64[s];
-            fb = n > kListMax || !finish_selection64(g.pts64, g.nbr, g.kd2, q64.x, q64.y, q64.z, q, kneed, n, Lm, U,
+            fb = n > kListMax || !finish_selection64(g.pts64, g.xyz64, g.nbr, g.kd2, q64.x, q64.y, q64.z, q, kneed, n, Lm, U,
                                                      Up, lst, band64, lane, tx, ty, tz, tp, prior, out_row(g, qw),
                                                      out);
           } else
@@ -3126,9 +3124,14 @@ __global__ void __launch_bounds__(kBlock) k_normals_knn64(GridView g, const doub
                                                           int mode, double radius, const float* __restrict__ prior,
                                                           float* __restrict__ out, const int32_t* __restrict__ list,
                                                           const int32_t* __restrict__ list_len) {
-  const int64_t lim = list ? (int64_t)*list_len : g.n;
+  if (!list) {  // every point, a thread each
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < g.n) knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, s);
+    return;
+  }
+  const int64_t lim = (int64_t)*list_len;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < lim; t += (int64_t)gridDim.x * blockDim.x)
-    knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list ? list[t] : t);
+    knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list[t]);
 }
 
 template <int K>
@@ -3425,6 +3428,7 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
     // (k_normals_knn_tile<32, *, true>), then the lane-per-query form for the
     // queries they hand on
     const size_t g64 = grid64_ws_bytes(n);
+    G.view.xyz64 = xyz;
     Arena ar((char*)ws + g64, ws_bytes - g64);
     int32_t* lens = ar.take<int32_t>(4);
     int32_t* list = ar.take<int32_t>(n);

@@ -49,6 +49,7 @@ struct GridView {
   // |frame distance - exact distance| <= d64 (both points' float32 frame
   // roundings, 2 sqrt(3) half-ulps of the frame's largest magnitude)
   float d64 = 0.f;
+  const double* __restrict__ xyz64 = nullptr;  // the caller's (n,3) float64 points (original order)
 };
 
 // outer sorted position / output row of a nested-grid point
