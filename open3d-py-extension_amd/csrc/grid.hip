@@ -1254,48 +1254,50 @@ __device__ __forceinline__ bool stile_finish(const float4 q, int kneed, int ns, 
 // as the float64 lane-per-query form (k_normals_knn64).
 struct Key64 {
   double d;
-  int i;  // original index: the tie-break, and the row of the caller's float64 array
+  int g;  // sorted grid position: the exact coordinates (pts64[g], w = the original index)
 };
-__device__ __forceinline__ bool key_less(const Key64& a, const Key64& b) {
-  return a.d < b.d || (a.d == b.d && a.i < b.i);
+// (d^2, original index) order; the index is read only on an exact d^2 tie
+__device__ __forceinline__ bool key_less(const Key64& a, const Key64& b, const double4* __restrict__ pts64) {
+  if (a.d != b.d) return a.d < b.d;
+  return a.g != b.g && pts64[a.g].w < pts64[b.g].w;
 }
 template <int I, int J, bool UP>
-__device__ __forceinline__ void key_ce(Key64 (&k)[32]) {
-  const bool sw = UP ? key_less(k[J], k[I]) : key_less(k[I], k[J]);
+__device__ __forceinline__ void key_ce(Key64 (&k)[32], const double4* __restrict__ pts64) {
+  const bool sw = UP ? key_less(k[J], k[I], pts64) : key_less(k[I], k[J], pts64);
   const Key64 a = k[I], b = k[J];
   k[I].d = sw ? b.d : a.d;
-  k[I].i = sw ? b.i : a.i;
+  k[I].g = sw ? b.g : a.g;
   k[J].d = sw ? a.d : b.d;
-  k[J].i = sw ? a.i : b.i;
+  k[J].g = sw ? a.g : b.g;
 }
 // bitonic sort of 32 keys, ascending (compile-time indices throughout)
 template <int SZ, int ST, int I>
-__device__ __forceinline__ void key_stage(Key64 (&k)[32]) {
+__device__ __forceinline__ void key_stage(Key64 (&k)[32], const double4* __restrict__ pts64) {
   if constexpr (I < 32) {
     constexpr int J = I ^ ST;
-    if constexpr (J > I) key_ce<I, J, (I & SZ) == 0>(k);
-    key_stage<SZ, ST, I + 1>(k);
+    if constexpr (J > I) key_ce<I, J, (I & SZ) == 0>(k, pts64);
+    key_stage<SZ, ST, I + 1>(k, pts64);
   }
 }
 template <int SZ, int ST>
-__device__ __forceinline__ void key_merge(Key64 (&k)[32]) {
+__device__ __forceinline__ void key_merge(Key64 (&k)[32], const double4* __restrict__ pts64) {
   if constexpr (ST > 0) {
-    key_stage<SZ, ST, 0>(k);
-    key_merge<SZ, ST / 2>(k);
+    key_stage<SZ, ST, 0>(k, pts64);
+    key_merge<SZ, ST / 2>(k, pts64);
   }
 }
 template <int SZ>
-__device__ __forceinline__ void key_sort(Key64 (&k)[32]) {
+__device__ __forceinline__ void key_sort(Key64 (&k)[32], const double4* __restrict__ pts64) {
   if constexpr (SZ <= 32) {
-    key_merge<SZ, SZ / 2>(k);
-    key_sort<SZ * 2>(k);
+    key_merge<SZ, SZ / 2>(k, pts64);
+    key_sort<SZ * 2>(k, pts64);
   }
 }
 
 __device__ __forceinline__ Key64 key64_of(const double4* __restrict__ pts64, double qx, double qy, double qz,
                                           const int32_t* tp, int p) {
-  const double4 v = pts64[tp[p]];
-  return Key64{dist2_d4(qx, qy, qz, v), (int)v.w};
+  const int g = tp[p];
+  return Key64{dist2_d4(qx, qy, qz, pts64[g]), g};
 }
 
 // (the grid's members by value: a GridView reference would put the kernel
@@ -1329,16 +1331,16 @@ __device__ __forceinline__ bool finish_selection64(const double4* __restrict__ p
   Key64 bk[kBndCap];
 #pragma unroll
   for (int i = 0; i < kBndCap; ++i) {
-    bk[i] = Key64{INFINITY, 0x7fffffff};
+    bk[i] = Key64{INFINITY, -1};
     if (i < nb) bk[i] = key64_of(pts64, qx, qy, qz, tp, (int)band[i][lane]);
   }
   uint32_t picked = 0;
   for (int t = 0; t < need; ++t) {  // repeated minimum (register indices stay compile-time)
-    Key64 best{INFINITY, 0x7fffffff};
+    Key64 best{INFINITY, -1};
     int bi = 0;
 #pragma unroll
     for (int i = 0; i < kBndCap; ++i)
-      if (!((picked >> i) & 1u) && key_less(bk[i], best)) {
+      if (!((picked >> i) & 1u) && (best.g < 0 || key_less(bk[i], best, pts64))) {
         best = bk[i];
         bi = i;
       }
@@ -1349,10 +1351,10 @@ __device__ __forceinline__ bool finish_selection64(const double4* __restrict__ p
   Key64 kk[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
-    kk[i] = Key64{INFINITY, 0x7fffffff};
+    kk[i] = Key64{INFINITY, 0x7fffffff};  // padding: after every member (INFINITY ties only padding)
     if (i < kneed) kk[i] = key64_of(pts64, qx, qy, qz, tp, (int)lst[i][lane]);
   }
-  key_sort<2>(kk);
+  key_sort<2>(kk, pts64);
   MomAccSeq acc;
   acc.zero();
   int32_t* const nrow = nbr ? nbr + (int64_t)oi * kneed : nullptr;  // test hook
@@ -1360,9 +1362,9 @@ __device__ __forceinline__ bool finish_selection64(const double4* __restrict__ p
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
     if (i < kneed) {
-      const int64_t id = kk[i].i;
-      if (nrow) nrow[i] = kk[i].i;
-      acc.add(xyz[3 * id], xyz[3 * id + 1], xyz[3 * id + 2]);
+      const double4 v = pts64[kk[i].g];
+      if (nrow) nrow[i] = (int)v.w;
+      acc.add(v.x, v.y, v.z);
       dk = kk[i].d;
     }
   }

@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for lib in base "$@" base "$@"; do
+for lib in ikey "$@" ikey "$@"; do
   export O3DX_LIB=$PWD/open3d-py-extension_amd/open3dpypro/_lib/var/libo3dx_$lib.so
   echo "== $lib"
   timeout -k 10 200 python tools/surface_normals_time.py "" 2>/dev/null | tee -a gpurun_out/r06_surface_ab.txt || exit 1
