@@ -469,22 +469,23 @@ __device__ __forceinline__ float float_down(double x) {
 // MODE 0: the plain step (accumulate); the device loop launches MODE 1 and 2
 // each step, and the one the state picks runs: 1 the plain search, 2 the skip
 // proof with extended-ball searches (SKIP)
-// MODE 3 (O3DX_ICP_MERGED, A/B): one launch whose waves take the state's
-// branch at run time (no second, empty launch per iteration)
+// (Measured and dropped, round 6: one merged launch whose waves take the
+// state's branch at run time instead of the two launches of which one returns
+// at once — 2700 against 2750 it/s at C3: the merged kernel's register
+// allocation costs the search steps more than the 9 us empty launch.)
 template <bool SORTED, bool F64 = false, int MODE = 0>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE >= 2 ? ICP_W2 : ICP_W1))) k_icp_step(const void* __restrict__ src, int64_t ns, GridView g,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? ICP_W2 : ICP_W1))) k_icp_step(const void* __restrict__ src, int64_t ns, GridView g,
                                                      const float4* __restrict__ tnorm,
                                                      const IcpState* __restrict__ st, double radius,
                                                      int32_t* __restrict__ mpos, int use_prior,
                                                      int64_t* __restrict__ acc, float* __restrict__ budget,
                                                      double ext, float4* __restrict__ mca,
                                                      float2* __restrict__ mcb) {
-  constexpr bool SKIP = MODE >= 2;  // compiled in; MODE 3 takes it while the state's ext_on holds
+  constexpr bool SKIP = MODE == 2;
   __shared__ int64_t sh[kBlock / 64][2 * kNS];
   if (st->done) return;  // converged: the loop's remaining steps do nothing
   if (MODE == 1 && st->ext_on) return;
   if (MODE == 2 && !st->ext_on) return;
-  const bool ext_now = MODE == 2 || (MODE == 3 && st->ext_on);  // wave-uniform
   Mat4 T;
 #pragma unroll
   for (int i = 0; i < 16; ++i) T.m[i] = st->T[i];
@@ -502,7 +503,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOD
       double raw[3];
       icp_source<SORTED, F64>(src, j, T, &px, &py, &pz, raw);
       bool kept = false;
-      if (SKIP && ext_now && use_prior && st->ext_prev) {
+      if (SKIP && use_prior && st->ext_prev) {
         // Skip proof: the last full search of this point left every other
         // target point at least budget[j] farther than its match (EXT below),
         // less twice each later motion.  The point moved by delta since the
@@ -556,7 +557,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOD
       }
       if (!kept) {
         // the previous iteration's match as the starting bound (exact either way)
-        if (SKIP && ext_now) {
+        if constexpr (SKIP) {
           double marg;
           nn_search_dev<true, F64, true>(g, px, py, pz, radius, &d2, &pos, use_prior ? mpos[j] : -1, ext, &marg);
           budget[j] = pos >= 0 ? float_down(marg) : 0.0f;
@@ -577,7 +578,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOD
             vz = v.z;
           }
           nt = tnorm[pos];
-          if (SKIP && !F64 && ext_now) {  // the match cache of the next steps' skip proofs
+          if constexpr (SKIP && !F64) {  // the match cache of the next steps' skip proofs
             mca[j] = make_float4((float)vx, (float)vy, (float)vz, nt.x);
             mcb[j] = make_float2(nt.y, nt.z);
           }
@@ -968,10 +969,7 @@ static void launch_step(const void* src, int64_t ns, bool sorted, const GridView
     else O3DX_STEP(false, false, MO);               \
   } while (0)
   const bool f64 = g.pts64 != nullptr;
-  const bool merged = getenv("O3DX_ICP_MERGED") && atoi(getenv("O3DX_ICP_MERGED")) != 0;
-  if (skip && merged) {
-    O3DX_STEPS(3);
-  } else if (skip) {  // the state picks one of the two at run time
+  if (skip) {  // the state picks one of the two at run time
     O3DX_STEPS(1);
     O3DX_STEPS(2);
   } else {
