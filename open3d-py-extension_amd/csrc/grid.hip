@@ -3118,27 +3118,6 @@ int grid64_build(const double* xyz, int64_t n, double target_occ, double min_h, 
 template <int K>
 __device__ __forceinline__ void knn64_normal_query(const GridView& g, const double* __restrict__ xyz, int kneed,
                                                    int mode, double radius, const float* __restrict__ prior,
-                                                   float* __restrict__ out, int64_t s);
-
-// list (nullable): the sorted positions the float64 tiles handed on (*list_len of them)
-template <int K>
-__global__ void __launch_bounds__(kBlock) k_normals_knn64(GridView g, const double* __restrict__ xyz, int kneed,
-                                                          int mode, double radius, const float* __restrict__ prior,
-                                                          float* __restrict__ out, const int32_t* __restrict__ list,
-                                                          const int32_t* __restrict__ list_len) {
-  if (!list) {  // every point, a thread each
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < g.n) knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, s);
-    return;
-  }
-  const int64_t lim = (int64_t)*list_len;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < lim; t += (int64_t)gridDim.x * blockDim.x)
-    knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list[t]);
-}
-
-template <int K>
-__device__ __forceinline__ void knn64_normal_query(const GridView& g, const double* __restrict__ xyz, int kneed,
-                                                   int mode, double radius, const float* __restrict__ prior,
                                                    float* __restrict__ out, int64_t s) {
   const double4 q = g.pts64[s];
   const int oi = (int)q.w;
@@ -3177,6 +3156,28 @@ __device__ __forceinline__ void knn64_normal_query(const GridView& g, const doub
       }
   }
   finish_normal(cnt, acc, prior, oi, out);
+}
+
+// every point, a thread each (the round-5 launch form)
+template <int K>
+__global__ void __launch_bounds__(kBlock) k_normals_knn64(GridView g, const double* __restrict__ xyz, int kneed,
+                                                          int mode, double radius, const float* __restrict__ prior,
+                                                          float* __restrict__ out) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < g.n) knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, s);
+}
+
+// the sorted positions the float64 tiles handed on (*list_len of them)
+template <int K>
+__global__ void __launch_bounds__(kBlock) k_normals_knn64_list(GridView g, const double* __restrict__ xyz, int kneed,
+                                                               int mode, double radius,
+                                                               const float* __restrict__ prior,
+                                                               float* __restrict__ out,
+                                                               const int32_t* __restrict__ list,
+                                                               const int32_t* __restrict__ list_len) {
+  const int64_t lim = (int64_t)*list_len;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < lim; t += (int64_t)gridDim.x * blockDim.x)
+    knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list[t]);
 }
 
 template <int K>
@@ -3424,7 +3425,6 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
   G.view.kd2 = mode == O3DX_SEARCH_KNN ? kd2 : nullptr;
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
   KTimer kt("normals_f64", s);
-  const int32_t* none = nullptr;
   if (mode == O3DX_SEARCH_KNN && kneed >= 1 && kneed <= 32 && !getenv("O3DX_F64_NO_TILES")) {
     // LDS tiles on the float32 frame, the exact float64 order deciding
     // (k_normals_knn_tile<32, *, true>), then the lane-per-query form for the
@@ -3446,14 +3446,13 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
       hipLaunchKernelGGL((k_normals_knn_tile<32, MomAccA, true>), dim3((unsigned)upper), dim3(kTileQ), 0, s, G.view,
                          chunks, kneed, prior, out, list, lens, 0);
     }
-    O3DX_DISPATCH_K(kneed, k_normals_knn64, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed, mode,
-                    radius, prior, out, (const int32_t*)list, (const int32_t*)lens);
+    O3DX_DISPATCH_K(kneed, k_normals_knn64_list, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed,
+                    mode, radius, prior, out, (const int32_t*)list, (const int32_t*)lens);
   } else if (mode == O3DX_SEARCH_RADIUS) {
-    hipLaunchKernelGGL(k_normals_knn64<4>, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, 0, mode, radius, prior, out,
-                       none, none);
+    hipLaunchKernelGGL(k_normals_knn64<4>, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, 0, mode, radius, prior, out);
   } else {
     O3DX_DISPATCH_K(kneed, k_normals_knn64, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius, prior,
-                    out, none, none);
+                    out);
   }
   O3DX_HIP(hipGetLastError());
   return 0;

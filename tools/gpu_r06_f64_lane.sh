@@ -1,14 +1,11 @@
 #!/bin/bash
-# the float64 lane form (O3DX_F64_NO_TILES=1) in the round-5 build and now, and the tiles
+# the float64 lane form (O3DX_F64_NO_TILES=1) and the tiles, with the tiles' hand-off statistics
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for v in r05 in-tree; do
-  if [ $v = in-tree ]; then unset O3DX_LIB; else export O3DX_LIB=$PWD/open3d-py-extension_amd/open3dpypro/_lib/var/libo3dx_$v.so; fi
-  O3DX_F64_NO_TILES=1 timeout -k 10 200 python tools/f64_normals_ab.py 2>/dev/null | tee -a gpurun_out/r06_f64_lane.txt || exit 1
-done
-unset O3DX_LIB
+O3DX_F64_NO_TILES=1 timeout -k 10 200 python tools/f64_normals_ab.py 2>/dev/null | tee -a gpurun_out/r06_f64_lane.txt || exit 1
+timeout -k 10 200 python tools/f64_normals_ab.py 2>/dev/null | tee -a gpurun_out/r06_f64_lane.txt || exit 1
 timeout -k 10 200 python - <<'PY' 2>/dev/null | tee -a gpurun_out/r06_f64_lane.txt
 import os, sys, json, torch
 sys.path.insert(0, "open3d-py-extension_amd")
