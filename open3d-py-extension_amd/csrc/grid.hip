@@ -3160,7 +3160,7 @@ __device__ __forceinline__ void knn64_normal_query(const GridView& g, const doub
 
 // every point, a thread each (the round-5 launch form)
 template <int K>
-__global__ void __launch_bounds__(kBlock) k_normals_knn64(GridView g, const double* __restrict__ xyz, int kneed,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) k_normals_knn64(GridView g, const double* __restrict__ xyz, int kneed,
                                                           int mode, double radius, const float* __restrict__ prior,
                                                           float* __restrict__ out) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3169,15 +3169,16 @@ __global__ void __launch_bounds__(kBlock) k_normals_knn64(GridView g, const doub
 
 // the sorted positions the float64 tiles handed on (*list_len of them)
 template <int K>
-__global__ void __launch_bounds__(kBlock) k_normals_knn64_list(GridView g, const double* __restrict__ xyz, int kneed,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) k_normals_knn64_list(GridView g, const double* __restrict__ xyz, int kneed,
                                                                int mode, double radius,
                                                                const float* __restrict__ prior,
                                                                float* __restrict__ out,
                                                                const int32_t* __restrict__ list,
                                                                const int32_t* __restrict__ list_len) {
-  const int64_t lim = (int64_t)*list_len;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < lim; t += (int64_t)gridDim.x * blockDim.x)
-    knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list[t]);
+  // a thread per listed query over a grid sized for the worst case (a
+  // grid-stride loop here costs the query 36 more VGPRs: 1 wave per SIMD)
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < (int64_t)*list_len) knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list[t]);
 }
 
 template <int K>
@@ -3446,8 +3447,8 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
       hipLaunchKernelGGL((k_normals_knn_tile<32, MomAccA, true>), dim3((unsigned)upper), dim3(kTileQ), 0, s, G.view,
                          chunks, kneed, prior, out, list, lens, 0);
     }
-    O3DX_DISPATCH_K(kneed, k_normals_knn64_list, dim3(std::min(grid, 1024u)), dim3(kBlock), 0, s, G.view, xyz, kneed,
-                    mode, radius, prior, out, (const int32_t*)list, (const int32_t*)lens);
+    O3DX_DISPATCH_K(kneed, k_normals_knn64_list, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius,
+                    prior, out, (const int32_t*)list, (const int32_t*)lens);
   } else if (mode == O3DX_SEARCH_RADIUS) {
     hipLaunchKernelGGL(k_normals_knn64<4>, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, 0, mode, radius, prior, out);
   } else {

@@ -295,6 +295,9 @@ __device__ __forceinline__ int knn_search_dev(const GridView& g, float qx, float
 // only candidates after (lo_d, lo_i) in (d^2, index) order are taken, so a
 // radius search of any size is read off in sorted pages of K (the default
 // (-1, -1) takes all).  Returns the count; bd/bi as knn_search_dev.
+#ifndef O3DX_F64_BATCH
+#define O3DX_F64_BATCH 2
+#endif
 template <int K>
 __device__ __forceinline__ int knn_search_dev64(const GridView& g, double qx, double qy, double qz, int kneed,
                                                 bool hybrid, double radius, double bd[K], int bi[K],
@@ -321,8 +324,15 @@ __device__ __forceinline__ int knn_search_dev64(const GridView& g, double qx, do
         ++st_cells;
         st_cands += s1 - g.start[c];
       }
-      for (int p = g.start[c]; p < s1; ++p) {
-        const double4 v = g.pts64[p];
+      // O3DX_F64_BATCH candidates' loads in flight at once (the same visiting order)
+      for (int p0 = g.start[c]; p0 < s1; p0 += O3DX_F64_BATCH) {
+        double4 vv[O3DX_F64_BATCH];
+#pragma unroll
+        for (int u = 0; u < O3DX_F64_BATCH; ++u) vv[u] = g.pts64[min(p0 + u, s1 - 1)];
+#pragma unroll
+        for (int u = 0; u < O3DX_F64_BATCH; ++u) {
+        if (p0 + u >= s1) break;
+        const double4 v = vv[u];
         const double d = dist2_d4(qx, qy, qz, v);
         if (!(d < r2lim)) continue;
         const int oi = (int)v.w;
@@ -349,6 +359,7 @@ __device__ __forceinline__ int knn_search_dev64(const GridView& g, double qx, do
                 wi = bi[j];
               }
           }
+        }
         }
       }
     });
