@@ -349,6 +349,9 @@ def registration_icp_sharded(src: torch.Tensor, target, init=None, max_iteration
 _ICP_FX_ZERO = np.zeros((32, 4), np.int64)  # a rank without source rows contributes nothing
 
 
+_ICP_CHUNK = 8  # sharded device loop: iterations queued between two state reads
+
+
 def _allreduce_digits(digits: torch.Tensor, group=None):
     """SUM all-reduce of the loop's 64 int64 digits: in place on the device
     under RCCL (stream-ordered, no host wait); through the host under gloo."""
@@ -389,12 +392,23 @@ def _registration_icp_sharded_device(src, target, init, max_iteration, relative_
         tgt, mc, widen, win = target, target.max_corr, float("inf"), None
     loop = ops.ICPShardLoop(s, am, mc, T0)
     digits = torch.zeros(64, dtype=torch.int64, device=src.device)
+    last = max(int(max_iteration), 0)
     it0 = 0
     while True:
-        for it in range(it0, max(int(max_iteration), 0) + 1):
-            loop.step(tgt, digits, use_prior=it > it0, widen=widen)
-            _allreduce_digits(digits, group)
-            loop.finish(digits, n_total, it, max_iteration, relative_fitness, relative_rmse, tgt, win, widen)
+        # iterations are queued in chunks; between chunks one state read tells
+        # every rank alike whether the loop converged (or stopped on a window),
+        # so a converged loop does not keep queuing empty steps and all-reduces
+        it = it0
+        while it <= last:
+            for _ in range(_ICP_CHUNK):
+                if it > last:
+                    break
+                loop.step(tgt, digits, use_prior=it > it0, widen=widen)
+                _allreduce_digits(digits, group)
+                loop.finish(digits, n_total, it, max_iteration, relative_fitness, relative_rmse, tgt, win, widen)
+                it += 1
+            if it <= last and loop.state()[3][0]:
+                break
         T, fit, rm, info = loop.state()
         if not (windowed and info[2]):
             return T, fit, rm
