@@ -831,7 +831,8 @@ def main_multi(args, world, rank, dev):
                                "halo exchange of boundary representatives over RCCL",
                    "n_points": N, "points_per_gpu": n_per, "voxel_size": vs, "voxels": M, "knn": args.knn,
                    "parallelism": f"x-slab spatial tiling x{world}", "points_rank0": n_local},
-        "roofline": roofline(kernels, M / world, N / world, args.pmc_json),
+        "roofline": (None if os.environ.get("O3DX_BENCH_SHARED_GPU") == "1"  # ranks sharing one GPU: no roofline
+                     else roofline(kernels, M / world, N / world, args.pmc_json)),
         "cpu_baseline": None,
         "extra": {"kernels_rank0": kernels,
                   "world_size_observed": dist.get_world_size(), "backend": dist.get_backend(),
