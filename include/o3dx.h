@@ -534,6 +534,14 @@ size_t o3dx_spatial_sort_workspace_bytes(int64_t n);
 int o3dx_spatial_sort(const float* xyz_dev, int64_t n, double target_occ,
                       float* sorted4_dev, void* ws, size_t ws_bytes,
                       void* stream);
+/* o3dx_spatial_sort_bounds (ABI 7, added): o3dx_spatial_sort that also
+ * returns absmax_host[3] = the cloud's |x|,|y|,|z| bounds (from the bounds
+ * the sort's grid already measures; the same values o3dx_icp_accumulate /
+ * o3dx_icp_register would measure on the sorted copy), so the ICP call that
+ * follows takes them as src_absmax_host and skips its own pass + host wait. */
+int o3dx_spatial_sort_bounds(const float* xyz_dev, int64_t n, double target_occ,
+                             float* sorted4_dev, double* absmax_host, void* ws,
+                             size_t ws_bytes, void* stream);
 int o3dx_icp_register(const float* src_dev, int64_t ns, int src_sorted4,
                       const void* target_ws, const double* desc_host,
                       const double* init_host, int max_iteration,

@@ -171,6 +171,75 @@ __global__ void __launch_bounds__(kBlock) k_run_counts(const uint32_t* __restric
   }
 }
 
+// The dense start table straight from the runs (no per-cell count array and
+// no scan over the cells): start[c] = the sorted position of the first run
+// whose key is >= c (n past the last run), for every cell c in [0, nc].  Two
+// passes: k_run_chunks (a thread per run) keys the runs (rkey[j]) and marks,
+// for each chunk of kStartChunk cells, the first run at or after the chunk's
+// first cell (cf[chunk]); k_start_fill (a block per chunk) stages the chunk's
+// runs in LDS and writes its cells' starts, 16 consecutive cells per thread.
+// Traffic: the runs once, the table once (written) — against a memset, a
+// scattered count write and three passes of the scan over the cells before.
+constexpr int kStartPer = 16;
+constexpr int kStartChunk = kBlock * kStartPer;  // 4096 cells
+__global__ void __launch_bounds__(kBlock) k_run_chunks(const uint32_t* __restrict__ skey, const int32_t* __restrict__ runs,
+                                                       const int64_t* __restrict__ nr, int64_t nchunks,
+                                                       uint32_t* __restrict__ rkey, int32_t* __restrict__ cf) {
+  const int64_t m = *nr;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = skey[runs[j]];
+    rkey[j] = k;
+    // chunks c with key[j - 1] < c * kStartChunk <= key[j] start at run j
+    const int64_t c0 = j == 0 ? 0 : (int64_t)(skey[runs[j - 1]] / kStartChunk) + 1;
+    const int64_t c1 = k / kStartChunk;
+    for (int64_t c = c0; c <= c1; ++c) cf[c] = (int32_t)j;
+    if (j == m - 1)  // the chunks after the last run's: every cell there starts at n
+      for (int64_t c = c1 + 1; c <= nchunks; ++c) cf[c] = (int32_t)m;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_start_fill(const uint32_t* __restrict__ rkey,
+                                                       const int32_t* __restrict__ runs,
+                                                       const int64_t* __restrict__ nr, const int32_t* __restrict__ cf,
+                                                       int64_t nc, int64_t n, int32_t* __restrict__ start) {
+  __shared__ uint32_t key[kStartChunk];
+  __shared__ int32_t pos[kStartChunk + 1];
+  const int64_t m = *nr;
+  const int64_t base = (int64_t)blockIdx.x * kStartChunk;
+  const int j0 = cf[blockIdx.x], j1 = cf[blockIdx.x + 1];
+  const int cnt = j1 - j0;  // runs keyed inside this chunk (<= kStartChunk: distinct keys)
+  for (int t = threadIdx.x; t < cnt; t += kBlock) {
+    key[t] = rkey[j0 + t];
+    pos[t] = runs[j0 + t];
+  }
+  if (threadIdx.x == 0) pos[cnt] = j1 < m ? runs[j1] : (int32_t)n;
+  __syncthreads();
+  const int64_t c0 = base + (int64_t)threadIdx.x * kStartPer;
+  if (c0 > nc) return;
+  // first staged run with key >= c0, then forward over the thread's cells
+  int lo = 0, hi = cnt;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)key[mid] < c0) lo = mid + 1;
+    else hi = mid;
+  }
+  int32_t v[kStartPer];
+#pragma unroll
+  for (int i = 0; i < kStartPer; ++i) {
+    while (lo < cnt && (int64_t)key[lo] < c0 + i) ++lo;
+    v[i] = pos[lo];
+  }
+  if (c0 + kStartPer <= nc + 1) {
+    int4* o = reinterpret_cast<int4*>(start + c0);  // c0 is a multiple of 16: 64-B aligned
+#pragma unroll
+    for (int i = 0; i < kStartPer / 4; ++i) o[i] = make_int4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < kStartPer; ++i)
+      if (c0 + i <= nc) start[c0 + i] = v[i];
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_grid_gather(const float* __restrict__ xyz, int64_t n,
                                                         const int32_t* __restrict__ sval, float4* __restrict__ pts,
                                                         const float* __restrict__ extra_src, float4* __restrict__ extra,
@@ -288,6 +357,7 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
   double mm[6];
   O3DX_TRY(aabb_device(xyz, n, G.mm, G.aabb_ws, s));
   O3DX_TRY(read_back(mm, G.mm, 6 * sizeof(double), s));
+  std::memcpy(G.mm_host, mm, sizeof(mm));
   const double mn[3] = {mm[0], mm[1], mm[2]}, mx[3] = {mm[3], mm[4], mm[5]};
   double ext[3], maxabs = 0, maxext = 0;
   for (int a = 0; a < 3; ++a) {
@@ -370,9 +440,20 @@ int grid_build(const float* xyz, int64_t n, double target_occ, double min_h, voi
         int64_t* nr = G.scratch + 2;
         hipLaunchKernelGGL(k_run_flags, dim3(gn), dim3(kBlock), 0, s, skey, n, flags);
         O3DX_TRY(compact_flags(flags, n, runs, nullptr, nr, G.scan_tmp, s));
-        O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
-        hipLaunchKernelGGL(k_run_counts, dim3(gn), dim3(kBlock), 0, s, skey, runs, nr, n, G.count);
-        O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));
+        if (getenv("O3DX_GRID_SCAN_STARTS")) {  // the count + scan form (A/B, tests)
+          O3DX_HIP(hipMemsetAsync(G.count, 0, (nc + 1) * sizeof(int32_t), s));
+          hipLaunchKernelGGL(k_run_counts, dim3(gn), dim3(kBlock), 0, s, skey, runs, nr, n, G.count);
+          O3DX_TRY(exclusive_scan_i32(G.count, G.start, nc, G.scan_tmp, s));
+        } else {
+          // run keys in the count array (m <= n <= its cells), chunk heads in
+          // the scan scratch (>= one int per 4096 cells + 64)
+          const int64_t nchunks = (nc + 1 + kStartChunk - 1) / kStartChunk;
+          uint32_t* rkey = reinterpret_cast<uint32_t*>(G.count);
+          int32_t* cf = G.scan_tmp;
+          hipLaunchKernelGGL(k_run_chunks, dim3(gn), dim3(kBlock), 0, s, skey, runs, nr, nchunks, rkey, cf);
+          hipLaunchKernelGGL(k_start_fill, dim3((unsigned)nchunks), dim3(kBlock), 0, s, rkey, runs, nr, cf, nc, n,
+                             G.start);
+        }
         hipLaunchKernelGGL(k_grid_gather, dim3(gn), dim3(kBlock), 0, s, xyz, n, sval, G.pts, extra_src, extra_sorted,
                            ids);
         O3DX_HIP(hipGetLastError());
@@ -1980,11 +2061,56 @@ __device__ __forceinline__ bool stile_count_list(const float2* txy, const float*
   return true;
 }
 
+// Block coordinates of a stile launch.  part 0: every block of the block box;
+// 1: its shell (the blocks on a face of the box: the z end planes, then the
+// ring of every plane between); 2: the interior (needs nbx, nby, nbz >= 3).
+// The shell holds the table's faces, where the stencil ball is cut and the
+// hand-offs arise: launched apart, its hand-off tail runs while the interior
+// blocks still stream (normals_dense_vox).
+__device__ __forceinline__ void stile_block(const DenseVox& d, int part, int& bx, int& by, int& bz) {
+  const int nbx = d.nbx, nby = d.nby, nbz = d.nbz;
+  if (part == 0) {
+    const int b = xcd_block(blockIdx.x, nbx * nby * nbz);
+    bx = b % nbx;
+    by = (b / nbx) % nby;
+    bz = b / (nbx * nby);
+    return;
+  }
+  const int ix = nbx - 2, iy = nby - 2, iz = nbz - 2;
+  if (part == 2) {
+    const int t = xcd_block(blockIdx.x, ix * iy * iz);
+    bx = 1 + t % ix;
+    by = 1 + (t / ix) % iy;
+    bz = 1 + t / (ix * iy);
+    return;
+  }
+  const int plane = nbx * nby, ring = plane - ix * iy;
+  int t = xcd_block(blockIdx.x, 2 * plane + iz * ring);
+  if (t < 2 * plane) {
+    bz = t < plane ? 0 : nbz - 1;
+    const int r = t % plane;
+    bx = r % nbx;
+    by = r / nbx;
+    return;
+  }
+  t -= 2 * plane;
+  bz = 1 + t / ring;
+  int r = t % ring;
+  if (r < 2 * nbx) {
+    by = r < nbx ? 0 : nby - 1;
+    bx = r % nbx;
+  } else {
+    r -= 2 * nbx;
+    by = 1 + (r >> 1);
+    bx = (r & 1) ? nbx - 1 : 0;
+  }
+}
+
 // WPE: waves per SIMD to register-allocate for (LDS allows 3 for 2x2)
 template <int KMAX, int WY, int WZ, int WPE>
 __global__ void __launch_bounds__(64 * WY * WZ) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* __restrict__ out,
-                int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg) {
+                int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_len, int force_fb, int dbg, int part) {
   using Sh = StileShape<WY, WZ>;
   constexpr int kSY = Sh::SY, kSZ = Sh::SZ, kSlots = Sh::CELLS;
   __shared__ float2 txy[kSlots];
@@ -1999,9 +2125,8 @@ k_normals_stile(DenseVox d, int kneed, const float* __restrict__ prior, float* _
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint16_t(*lst)[64] = reinterpret_cast<uint16_t(*)[64]>(selbuf[wv]);
   uint32_t* hw = selbuf[wv];
-  const int nb = d.nbx * d.nby * d.nbz;
-  const int b = xcd_block(blockIdx.x, nb);
-  const int bx = b % d.nbx, by = (b / d.nbx) % d.nby, bz = b / (d.nbx * d.nby);
+  int bx, by, bz;
+  stile_block(d, part, bx, by, bz);
   const int gx0 = bx * kVB - kVM, gy0 = by * (kVB * WY) - kVM, gz0 = bz * (kVB * WZ) - kVM;  // box origin
   {
     constexpr int kT = 64 * Sh::NW;
@@ -2654,6 +2779,39 @@ static int grid_from_voxels(const double* geom, const float4* vox, int64_t n, do
   return 0;
 }
 
+// A second stream per host thread and device (created on first use, kept for
+// the thread's life): the stile's shell blocks and their hand-off tail run
+// there beside the interior blocks.  nullptr (no split) when `s` is not on
+// the current device or creation fails.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, a_done = nullptr, join = nullptr;
+};
+static SideStream* side_stream(hipStream_t s) {
+  constexpr int kMaxDev = 64;
+  static thread_local SideStream tab[kMaxDev];
+  int cur = -1;
+  hipDevice_t sd = -1;
+  if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(s, &sd) != hipSuccess || sd != cur || cur < 0 ||
+      cur >= kMaxDev)
+    return nullptr;
+  SideStream& x = tab[cur];
+  if (!x.s) {
+    SideStream y;
+    if (hipStreamCreateWithFlags(&y.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&y.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&y.a_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&y.join, hipEventDisableTiming) != hipSuccess) {
+      for (hipEvent_t e : {y.fork, y.a_done, y.join})
+        if (e) (void)hipEventDestroy(e);
+      (void)hipStreamDestroy(y.s);
+      return nullptr;
+    }
+    x = y;
+  }
+  return &x;
+}
+
 // KNN normals straight off the dense voxel table (k_normals_stile; hand-offs
 // to the wave form and the register top-k over the table).  1: not applicable
 // (the caller builds a search grid instead).
@@ -2733,16 +2891,43 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   O3DX_ARENA_CHECK(ar);
   // (the one-call pipeline clears them in its bounds pass: no fill launch here)
   if (!lens_zeroed) O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
+  // Split launch (a block box of >= 3 blocks per axis): the shell blocks on a
+  // side stream, launched first, then their hand-off tail there, while the
+  // interior blocks run on s; the interior's own (rare) hand-offs follow on s.
+  // The interior's hand-offs go to lists of their own (list3 / list4,
+  // counters lens[2] / lens[3]).
+  const int64_t nint = (int64_t)std::max(d.nbx - 2, 0) * std::max(d.nby - 2, 0) * std::max(d.nbz - 2, 0);
+  SideStream* side = nullptr;
+  int32_t *list3 = nullptr, *list4 = nullptr;
+  // (O3DX_STILE_SPLIT=1: split any box of >= 3 blocks per axis — tests;
+  // O3DX_STILE_NO_SPLIT: one launch — A/B)
+  const char* force_split = getenv("O3DX_STILE_SPLIT");
+  const bool want_split = 2 * nint >= nb || (force_split && force_split[0] == '1');
+  if (d.nbx >= 3 && d.nby >= 3 && d.nbz >= 3 && want_split && !getenv("O3DX_STILE_NO_SPLIT")) {
+    list3 = ar.take<int32_t>(n);  // the interior's hand-off lists
+    list4 = ar.take<int32_t>(n);
+    if (ar.ok()) side = side_stream(s);
+  }
   {
     KTimer kt("normals_knn", s);
-    {
-      KTimer kt_tile("normals_stile", s);
-      // O3DX_TILE_DEBUG=1/2/3/4: stop after staging / histogram / list scan / moments (profiling only)
-      const char* dbg = getenv("O3DX_TILE_DEBUG");
-      const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
+    // O3DX_TILE_DEBUG=1/2/3/4: stop after staging / histogram / list scan / moments (profiling only)
+    const char* dbg = getenv("O3DX_TILE_DEBUG");
+    const int ffb = getenv("O3DX_STILE_FORCE_FB") ? 1 : 0, dg = dbg ? atoi(dbg) : 0;
+    KTimer kt_tile("normals_stile", s);
+    if (side) {
+      O3DX_HIP(hipEventRecord(side->fork, s));
+      O3DX_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
+      hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3>), dim3((unsigned)(nb - nint)), dim3(64 * wy * wz), 0,
+                         side->s, d, kneed, prior, out, list, lens, ffb, dg, 1);
+      O3DX_HIP(hipEventRecord(side->a_done, side->s));
+      hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3>), dim3((unsigned)nint), dim3(64 * wy * wz), 0, s, d, kneed,
+                         prior, out, list3, lens + 2, ffb, dg, 2);
+      O3DX_HIP(hipStreamWaitEvent(s, side->a_done, 0));
+    } else {
       hipLaunchKernelGGL((k_normals_stile<32, wy, wz, 3>), dim3((unsigned)nb), dim3(64 * wy * wz), 0, s, d, kneed,
-                         prior, out, list, lens, ffb, dg);
+                         prior, out, list, lens, ffb, dg, 0);
     }
+    kt_tile.stop();
     // the table as a dense GridView (identity cell starts, <= 1 point per cell)
     GridView g{};
     g.pts = vox;
@@ -2761,12 +2946,23 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
     g.stats = d.stats;
     g.nbr = d.nbr;
     g.kd2 = d.kd2;
-    KTimer kt_wave("normals_wave", s);
-    hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(2048), dim3(64 * kWavesPerBlock), 0, s, g, kneed, prior, out,
-                       list, lens, list2, lens + 1, 3, Deferred{});
-    kt_wave.stop();
-    hipLaunchKernelGGL(k_normals_knn<32>, dim3(64), dim3(kBlock), 0, s, g, xyz, kneed, 0, 0.0, prior, out, list2,
-                       lens + 1);
+    auto tail = [&](hipStream_t st, int32_t* l1, int32_t* n1, int32_t* l2, int32_t* n2) {
+      hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(2048), dim3(64 * kWavesPerBlock), 0, st, g, kneed, prior, out,
+                         l1, n1, l2, n2, 3, Deferred{});
+      hipLaunchKernelGGL(k_normals_knn<32>, dim3(64), dim3(kBlock), 0, st, g, xyz, kneed, 0, 0.0, prior, out, l2,
+                         n2);
+    };
+    if (side) {
+      tail(side->s, list, lens, list2, lens + 1);
+      O3DX_HIP(hipEventRecord(side->join, side->s));
+      KTimer kt_wave("normals_wave", s);
+      tail(s, list3, lens + 2, list4, lens + 3);
+      kt_wave.stop();
+      O3DX_HIP(hipStreamWaitEvent(s, side->join, 0));
+    } else {
+      KTimer kt_wave("normals_wave", s);
+      tail(s, list, lens, list2, lens + 1);
+    }
   }
   O3DX_HIP(hipGetLastError());
   return 0;
@@ -3181,6 +3377,169 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))
   if (t < (int64_t)*list_len) knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list[t]);
 }
 
+// The float64 tiles' hand-offs (KNN, kneed <= 32), a wave per query instead
+// of a lane: each Chebyshev shell's rows (a face row = one point range, an
+// inner row = its two end cells) become one flat candidate range spread over
+// the 64 lanes, every lane keeping its own kW64Keep nearest in exact
+// (d^2, index) order; the shell loop stops as knn_search_dev64's does (the
+// k-th inside the shell's reach, counted conservatively over the lanes'
+// lists).  The k nearest are then drawn from the lanes' heads in order — the
+// same members in the same order as the lane form, accumulated in the same
+// sequence (MomAccSeq).  A lane whose list runs dry while it saw more than it
+// kept could hide a nearer one: such a query goes on to the lane form
+// (fb list).  One lane form query walks its shells' candidates alone, one
+// load batch at a time; here 64 lanes share them.
+constexpr int kW64Keep = 8;
+constexpr int kW64Waves = 4;
+__global__ void __launch_bounds__(64 * kW64Waves) k_normals_knn64_wave(GridView g, const double* __restrict__ xyz,
+                                                                        int kneed, const float* __restrict__ prior,
+                                                                        float* __restrict__ out,
+                                                                        const int32_t* __restrict__ list,
+                                                                        const int32_t* __restrict__ list_len,
+                                                                        int32_t* __restrict__ fb,
+                                                                        int32_t* __restrict__ fb_len, int keep_lim) {
+  __shared__ int32_t s_a0[kW64Waves][64], s_l0[kW64Waves][64], s_a1[kW64Waves][64], s_rp[kW64Waves][65];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t *ta0 = s_a0[wv], *tl0 = s_l0[wv], *ta1 = s_a1[wv], *trp = s_rp[wv];
+  const int64_t m = *list_len;
+  for (int64_t t = (int64_t)blockIdx.x * kW64Waves + wv; t < m; t += (int64_t)gridDim.x * kW64Waves) {
+    const int64_t s = list[t];
+    const double4 q = g.pts64[s];
+    const int oi = (int)q.w;
+    const double gqx = q.x - g.o64x, gqy = q.y - g.o64y, gqz = q.z - g.o64z;
+    int cx, cy, cz;
+    grid_cell(g, (float)gqx, (float)gqy, (float)gqz, cx, cy, cz);
+    const int rmax = shell_rmax(g, cx, cy, cz);
+    double bd[kW64Keep];
+    int bi[kW64Keep];
+#pragma unroll
+    for (int j = 0; j < kW64Keep; ++j) {
+      bd[j] = INFINITY;
+      bi[j] = 0x7fffffff;
+    }
+    int seen = 0;
+    for (int r = 0; r <= rmax; ++r) {
+      const int side = 2 * r + 1, nrows = side * side;
+      for (int r0 = 0; r0 < nrows; r0 += 64) {
+        const int row = r0 + lane;
+        int a0 = 0, l0 = 0, a1 = 0, l1 = 0;
+        if (row < nrows) {
+          const int dz = row / side - r, dy = row % side - r;
+          const int z = cz + dz, y = cy + dy;
+          if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
+            const int rb = g.nx * (y + g.ny * z);
+            if (dz == -r || dz == r || dy == -r || dy == r) {  // a face row: the cells cx - r .. cx + r
+              const int x0 = max(cx - r, 0), x1 = min(cx + r, g.nx - 1);
+              if (x0 <= x1) {
+                a0 = g.start[rb + x0];
+                l0 = g.start[rb + x1 + 1] - a0;
+              }
+            } else {  // an inner row (r >= 1): its two end cells
+              if (cx - r >= 0) {
+                a0 = g.start[rb + cx - r];
+                l0 = g.start[rb + cx - r + 1] - a0;
+              }
+              if (cx + r < g.nx) {
+                a1 = g.start[rb + cx + r];
+                l1 = g.start[rb + cx + r + 1] - a1;
+              }
+            }
+          }
+        }
+        const int inc = wave_incl_scan(l0 + l1);
+        const int tot = __shfl(inc, 63, 64);
+        ta0[lane] = a0;
+        tl0[lane] = l0;
+        ta1[lane] = a1;
+        trp[lane + 1] = inc;
+        if (lane == 0) trp[0] = 0;
+        wave_sync();
+        int rw = 0;
+        for (int b = 0; b < tot; b += 64) {
+          const int f = b + lane;
+          if (f < tot) {
+            while (trp[rw + 1] <= f) ++rw;
+            const int o = f - trp[rw];
+            const int p = o < tl0[rw] ? ta0[rw] + o : ta1[rw] + (o - tl0[rw]);
+            const double4 v = g.pts64[p];
+            const double d = dist2_d4(q.x, q.y, q.z, v);
+            const int id = (int)v.w;
+            ++seen;
+            if (lex_less(d, id, bd[kW64Keep - 1], bi[kW64Keep - 1])) {
+#pragma unroll
+              for (int j = kW64Keep - 1; j >= 0; --j) {
+                const bool lt = lex_less(d, id, bd[j], bi[j]);
+                const bool ltp = j > 0 ? lex_less(d, id, bd[j > 0 ? j - 1 : 0], bi[j > 0 ? j - 1 : 0]) : false;
+                if (ltp) {
+                  bd[j] = bd[j - 1];
+                  bi[j] = bi[j - 1];
+                } else if (lt) {
+                  bd[j] = d;
+                  bi[j] = id;
+                }
+              }
+            }
+          }
+        }
+        wave_sync();  // the row table is rewritten by the next 64 rows
+      }
+      const double B = cube_reach(g, gqx, gqy, gqz, cx, cy, cz, r) - g.slack;
+      if (B > 0.0) {
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < kW64Keep; ++j) c += bd[j] < B * B ? 1 : 0;
+        if (wave_sum(c) >= kneed) break;  // the k-th lies inside the reach
+      }
+    }
+    const int total = wave_sum(seen);
+    const int want = min(kneed, total);
+    const int kept = min(seen, keep_lim);  // keep_lim < kW64Keep: tests of the hand-on
+    MomAccSeq acc;
+    acc.zero();
+    int h = 0;
+    bool bad = false;
+    double kd = 0.0;
+    for (int j = 0; j < want; ++j) {
+      if (__any(h == kept && seen > kept)) {  // a dry lane that saw more than it kept
+        bad = true;
+        break;
+      }
+      double md = bd[0];
+      int mi = bi[0];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(md, o, 64);
+        const int oo = __shfl_xor(mi, o, 64);
+        if (lex_less(od, oo, md, mi)) {
+          md = od;
+          mi = oo;
+        }
+      }
+      if (bd[0] == md && bi[0] == mi) {  // the owner pops its head
+#pragma unroll
+        for (int u = 0; u + 1 < kW64Keep; ++u) {
+          bd[u] = bd[u + 1];
+          bi[u] = bi[u + 1];
+        }
+        bd[kW64Keep - 1] = INFINITY;
+        bi[kW64Keep - 1] = 0x7fffffff;
+        ++h;
+      }
+      if (lane == 0 && g.nbr) g.nbr[(int64_t)oi * kneed + j] = mi;
+      acc.add(xyz[3 * (int64_t)mi], xyz[3 * (int64_t)mi + 1], xyz[3 * (int64_t)mi + 2]);
+      kd = md;
+    }
+    if (lane == 0) {
+      if (bad) {
+        fb[atomicAdd(fb_len, 1)] = (int32_t)s;
+      } else {
+        if (g.kd2 && want > 0) g.kd2[oi] = (float)(kd * (1.0 + 1e-6));
+        finish_normal(want, acc, prior, oi, out);
+      }
+    }
+  }
+}
+
 template <int K>
 __global__ void __launch_bounds__(kBlock) k_knn_query64(GridView g, const double* __restrict__ q, int64_t nq,
                                                         int kneed, int hybrid, double radius, int kout,
@@ -3396,11 +3755,12 @@ extern "C" int o3dx_voxel_down_sample_normals(const float* xyz, int64_t n, const
 }
 
 // ------------------------------------------------------ float64 boundary
-// [float64 grid][tiles: lens, hand-off list, chunk starts, chunk-plan scratch]
+// [float64 grid][tiles: lens, hand-off list, chunk starts, chunk-plan scratch,
+// the wave form's hand-off list]
 static size_t normals64_tiles_bytes(int64_t n) {
   n = std::max<int64_t>(n, 1);
   const int64_t rows = cap_cells(n, 4);  // grid rows (ny * nz) are bounded by the cell cap
-  return Arena::align(4 * 4 + 1) + Arena::align(n * 4 + 1) + Arena::align((n / 64 + rows + 4) * 4 + 1) +
+  return Arena::align(4 * 4 + 1) + 2 * Arena::align(n * 4 + 1) + Arena::align((n / 64 + rows + 4) * 4 + 1) +
          chunk_plan_ws_bytes(n, rows) + 1024;
 }
 extern "C" size_t o3dx_normals_f64_workspace_bytes(int64_t n) {
@@ -3439,6 +3799,7 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
     int32_t* chunks = ar.take<int32_t>(upper + 2);
     const size_t pws_bytes = chunk_plan_ws_bytes(n, (int64_t)G.view.ny * G.view.nz);
     void* pws = ar.take<char>(pws_bytes);
+    int32_t* list2 = ar.take<int32_t>(n);
     O3DX_ARENA_CHECK(ar);
     O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
     O3DX_TRY(chunk_plan(n, G.view, kTileQ, chunks, pws, pws_bytes, s));
@@ -3447,8 +3808,21 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
       hipLaunchKernelGGL((k_normals_knn_tile<32, MomAccA, true>), dim3((unsigned)upper), dim3(kTileQ), 0, s, G.view,
                          chunks, kneed, prior, out, list, lens, 0);
     }
-    O3DX_DISPATCH_K(kneed, k_normals_knn64_list, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius,
-                    prior, out, (const int32_t*)list, (const int32_t*)lens);
+    if (getenv("O3DX_F64_NO_WAVE")) {  // every hand-off to the lane form (A/B, tests)
+      O3DX_DISPATCH_K(kneed, k_normals_knn64_list, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius,
+                      prior, out, (const int32_t*)list, (const int32_t*)lens);
+    } else {
+      // the hand-offs a wave each; the few it cannot settle (lens[2]) to the lane form
+      KTimer kt_wave("normals_wave64", s);
+      const unsigned wblocks = (unsigned)std::min<int64_t>((n + kW64Waves - 1) / kW64Waves, 2048);
+      const char* kl = getenv("O3DX_F64_WAVE_KEEP");  // tests: a shorter list hands more queries on
+      const int keep = kl ? std::max(1, std::min(kW64Keep, atoi(kl))) : kW64Keep;
+      hipLaunchKernelGGL(k_normals_knn64_wave, dim3(wblocks), dim3(64 * kW64Waves), 0, s, G.view, xyz, kneed, prior,
+                         out, (const int32_t*)list, (const int32_t*)lens, list2, lens + 2, keep);
+      kt_wave.stop();
+      O3DX_DISPATCH_K(kneed, k_normals_knn64_list, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius,
+                      prior, out, (const int32_t*)list2, (const int32_t*)(lens + 2));
+    }
   } else if (mode == O3DX_SEARCH_RADIUS) {
     hipLaunchKernelGGL(k_normals_knn64<4>, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, 0, mode, radius, prior, out);
   } else {

@@ -708,6 +708,7 @@ struct GridBuild {
   int64_t cap_cells;
   GridView view;
   double4* pts64 = nullptr;  // float64 grids (grid64_build): exact coordinates + index, sorted like pts
+  double mm_host[6] = {0, 0, 0, 0, 0, 0};  // the cloud's bounds (min xyz, max xyz), read back by grid_build
 };
 
 size_t grid_ws_bytes(int64_t n, int cap_mult = 4);

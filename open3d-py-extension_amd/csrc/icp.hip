@@ -1092,17 +1092,29 @@ extern "C" int o3dx_icp_accumulate(const float* src, int64_t ns, int src_sorted4
 
 extern "C" size_t o3dx_spatial_sort_workspace_bytes(int64_t n) { return grid_ws_bytes(n) + 1024; }
 
-extern "C" int o3dx_spatial_sort(const float* xyz, int64_t n, double target_occ, float* sorted4, void* ws,
-                                 size_t ws_bytes, void* stream) {
+extern "C" int o3dx_spatial_sort_bounds(const float* xyz, int64_t n, double target_occ, float* sorted4,
+                                        double* absmax, void* ws, size_t ws_bytes, void* stream) {
   if (n < 0 || (n > 0 && (!xyz || !sorted4))) return fail(O3DX_EINVAL, "o3dx_spatial_sort: bad args");
   if (!ws || ws_bytes < o3dx_spatial_sort_workspace_bytes(n)) return fail(O3DX_ENOMEM, "spatial_sort workspace too small");
-  if (n == 0) return 0;
+  if (n == 0) {
+    if (absmax) absmax[0] = absmax[1] = absmax[2] = 0.0;
+    return 0;
+  }
   hipStream_t s = as_stream(stream);
   GridBuild G;
   O3DX_TRY(grid_build(xyz, n, target_occ > 0 ? target_occ : 8.0, 0.0, ws, ws_bytes, s, &G, nullptr, nullptr,
                       /*blocked=*/true));
   O3DX_HIP(hipMemcpyAsync(sorted4, G.pts, (size_t)n * sizeof(float4), hipMemcpyDeviceToDevice, s));
+  // the exact float32 min / max, widened to double: max(|min|, |max|) per
+  // axis is the largest |coordinate|, bit for bit what k_absmax4 finds
+  if (absmax)
+    for (int a = 0; a < 3; ++a) absmax[a] = std::max(std::fabs(G.mm_host[a]), std::fabs(G.mm_host[3 + a]));
   return 0;
+}
+
+extern "C" int o3dx_spatial_sort(const float* xyz, int64_t n, double target_occ, float* sorted4, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  return o3dx_spatial_sort_bounds(xyz, n, target_occ, sorted4, nullptr, ws, ws_bytes, stream);
 }
 
 extern "C" int o3dx_icp_solve_point_to_plane(const double* sums, double* upd) {
@@ -1328,11 +1340,12 @@ extern "C" int o3dx_registration_icp_point_to_plane(const float* src, int64_t ns
   float* src4 = (float*)ws;
   char* rest = (char*)ws + Arena::align((size_t)std::max<int64_t>(ns, 1) * sizeof(float4) + 1);
   size_t rest_bytes = ws_bytes - (size_t)(rest - (char*)ws);
-  if (ns > 0) O3DX_TRY(o3dx_spatial_sort(src, ns, 8.0, src4, rest, rest_bytes, stream));
+  double am[3] = {0, 0, 0};
+  if (ns > 0) O3DX_TRY(o3dx_spatial_sort_bounds(src, ns, 8.0, src4, am, rest, rest_bytes, stream));
   Arena ar(rest, rest_bytes);
   AccWs w;
   acc_carve(ar, std::max<int64_t>(ns, 1), &w);
-  return run_loop(src4, ns, true, g, tn, max_corr, init, max_iteration, rel_fit, rel_rmse, nullptr, w, s, T_out,
+  return run_loop(src4, ns, true, g, tn, max_corr, init, max_iteration, rel_fit, rel_rmse, am, w, s, T_out,
                   fitness, rmse, corr_out, ncorr);
 }
 

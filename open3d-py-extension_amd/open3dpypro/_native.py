@@ -92,6 +92,7 @@ _SIGS = {
     "o3dx_icp_accumulate": (_I32, [_P, _I64, _I32, _P, _P, _P, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "o3dx_spatial_sort_workspace_bytes": (_SZ, [_I64]),
     "o3dx_spatial_sort": (_I32, [_P, _I64, _D, _P, _P, _SZ, _P]),
+    "o3dx_spatial_sort_bounds": (_I32, [_P, _I64, _D, _P, _P, _P, _SZ, _P]),
     "o3dx_pcd_unpack": (_I32, [_P, _I64, _I32, _P, _P, _P, _P, _P, _P]),
     "o3dx_lzf_decompress": (_I64, [_P, _I64, _P, _I64]),
     "o3dx_registration_icp_workspace_bytes": (_SZ, [_I64]),

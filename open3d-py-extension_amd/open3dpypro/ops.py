@@ -789,18 +789,21 @@ def spatial_sort_f64(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor
 def spatial_sort(xyz: torch.Tensor, target_occ: float = 8.0) -> torch.Tensor:
     """(n,4) float32 copy of the cloud in a compact spatial order (8^3 blocks of
     grid cells, Morton order inside a block); column 3 holds the original
-    int32 index bits (o3dx_spatial_sort).  The tensor carries `.absmax_of`,
-    the cloud itself: ICPTarget.accumulate measures its |x|,|y|,|z| bounds
-    (the default fx quanta) on first use, so a caller passing its own bounds
-    (a sharded source: the global ones) never pays that host wait."""
+    int32 index bits (o3dx_spatial_sort_bounds).  The tensor carries
+    `.absmax`, the cloud's |x|,|y|,|z| bounds from the sort's own bounds pass
+    (the default fx quanta of ICPTarget.accumulate / register, which then
+    skip their own measuring pass and host wait; a sharded source passes the
+    global bounds instead), and `.absmax_of`, the cloud itself."""
     x = _xyz(xyz)
     L = N.load()
     n = x.shape[0]
     out = torch.empty((max(n, 1), 4), dtype=torch.float32, device=x.device)
     ws = N.workspace(L.o3dx_spatial_sort_workspace_bytes(n), x.device, "sort")
-    N.check(L.o3dx_spatial_sort(N.ptr(x), n, float(target_occ), N.ptr(out), N.ptr(ws), ws.numel(),
-                                N.stream_ptr(x.device)), "spatial_sort")
+    am = np.zeros(3, np.float64)
+    N.check(L.o3dx_spatial_sort_bounds(N.ptr(x), n, float(target_occ), N.ptr(out), _np_ptr(am), N.ptr(ws),
+                                       ws.numel(), N.stream_ptr(x.device)), "spatial_sort")
     res = out[:n]
+    res.absmax = am  # the sort's own bounds: ICP on it skips its absmax pass
     res.absmax_of = x
     return res
 

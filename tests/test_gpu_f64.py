@@ -84,13 +84,21 @@ def test_f64_normals_knn30(las, las_np):
     assert_neighbour_sets(dn.ids(), las_np, 30, "f64_las_knn30")
 
 
+@pytest.mark.parametrize("handoff", ["wave", "wave_keep1", "lane"])
 @pytest.mark.parametrize("k", [30, 16, 5])
-def test_f64_normals_tiles_equal_lane_form(las, monkeypatch, k):
+def test_f64_normals_tiles_equal_lane_form(las, monkeypatch, k, handoff):
     """The float64 LDS tiles (frame-distance selection, exact (d^2, index)
     order, sequential float64 moments) give the lane-per-query form's normals
-    bit for bit (O3DX_F64_NO_TILES=1), hand-offs included, and the same k-th
-    distance bounds."""
+    bit for bit (O3DX_F64_NO_TILES=1), hand-offs included — the tiles'
+    hand-offs served a wave per query (k_normals_knn64_wave, default) or a lane
+    each (O3DX_F64_NO_WAVE) — and the same k-th distance bounds."""
+    if handoff == "lane":
+        monkeypatch.setenv("O3DX_F64_NO_WAVE", "1")
+    if handoff == "wave_keep1":  # the wave form hands nearly every query on
+        monkeypatch.setenv("O3DX_F64_WAVE_KEEP", "1")
     a, kd_a = ops.estimate_normals(las, knn=k, return_kdist=True)
+    monkeypatch.delenv("O3DX_F64_NO_WAVE", raising=False)
+    monkeypatch.delenv("O3DX_F64_WAVE_KEEP", raising=False)
     monkeypatch.setenv("O3DX_F64_NO_TILES", "1")
     b, kd_b = ops.estimate_normals(las, knn=k, return_kdist=True)
     assert torch.equal(a, b)

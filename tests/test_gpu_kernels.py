@@ -672,6 +672,8 @@ STILE_ENVS = [
     {},
     {"O3DX_STILE_FORCE_FB": "1"},
     {"O3DX_NO_STILE": "1"},
+    {"O3DX_STILE_SPLIT": "1"},  # shell blocks + their hand-offs on the side stream
+    {"O3DX_STILE_SPLIT": "1", "O3DX_STILE_FORCE_FB": "1"},
 ]
 
 

@@ -29,8 +29,8 @@ N.set_kernel_timing(True)
 N.reset_kernel_timing()
 ops.estimate_normals(reps, knn=30)
 torch.cuda.synchronize()
-kt = {k: round(N.kernel_timing(k)[0], 3) for k in ("normals_f64", "normals_tile64", "grid_count", "grid_sort")}
+kt = {k: round(N.kernel_timing(k)[0], 3) for k in ("normals_f64", "normals_tile64", "normals_wave64", "grid_count", "grid_sort")}
 N.set_kernel_timing(False)
 print(json.dumps({"lib": os.path.basename(os.environ.get("O3DX_LIB", "in-tree")),
-                  "no_tiles": os.environ.get("O3DX_F64_NO_TILES"), "reps": int(reps.shape[0]),
+                  "no_tiles": os.environ.get("O3DX_F64_NO_TILES"), "no_wave": os.environ.get("O3DX_F64_NO_WAVE"), "reps": int(reps.shape[0]),
                   "ms_min": round(min(ts), 3), "timers": kt, "same": bool(torch.equal(a, b))}), flush=True)
