@@ -2891,19 +2891,20 @@ static int normals_dense_vox(const double* geom, const float4* vox, const float*
   O3DX_ARENA_CHECK(ar);
   // (the one-call pipeline clears them in its bounds pass: no fill launch here)
   if (!lens_zeroed) O3DX_HIP(hipMemsetAsync(lens, 0, 4 * sizeof(int32_t), s));
-  // Split launch (a block box of >= 3 blocks per axis): the shell blocks on a
-  // side stream, launched first, then their hand-off tail there, while the
-  // interior blocks run on s; the interior's own (rare) hand-offs follow on s.
+  // Split launch (opt-in, O3DX_STILE_SPLIT=1; a block box of >= 3 blocks per
+  // axis): the shell blocks on a side stream, launched first, then their
+  // hand-off tail there, while the interior blocks run on s; the interior's
+  // own hand-offs follow on s.  Measured at C2 (profiles/r06_stile_split_ab.txt):
+  // 0.776 ms per step against 0.755 in one launch — the two concurrent
+  // launches stretched the stile 0.470 -> 0.511 ms, and the interior still
+  // hands on a few queries, so a 27 us tail stays on the critical path.
   // The interior's hand-offs go to lists of their own (list3 / list4,
   // counters lens[2] / lens[3]).
   const int64_t nint = (int64_t)std::max(d.nbx - 2, 0) * std::max(d.nby - 2, 0) * std::max(d.nbz - 2, 0);
   SideStream* side = nullptr;
   int32_t *list3 = nullptr, *list4 = nullptr;
-  // (O3DX_STILE_SPLIT=1: split any box of >= 3 blocks per axis — tests;
-  // O3DX_STILE_NO_SPLIT: one launch — A/B)
-  const char* force_split = getenv("O3DX_STILE_SPLIT");
-  const bool want_split = 2 * nint >= nb || (force_split && force_split[0] == '1');
-  if (d.nbx >= 3 && d.nby >= 3 && d.nbz >= 3 && want_split && !getenv("O3DX_STILE_NO_SPLIT")) {
+  const char* want = getenv("O3DX_STILE_SPLIT");
+  if (d.nbx >= 3 && d.nby >= 3 && d.nbz >= 3 && want && want[0] == '1') {
     list3 = ar.take<int32_t>(n);  // the interior's hand-off lists
     list4 = ar.take<int32_t>(n);
     if (ar.ok()) side = side_stream(s);
@@ -3391,7 +3392,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))
 // load batch at a time; here 64 lanes share them.
 constexpr int kW64Keep = 8;
 constexpr int kW64Waves = 4;
-__global__ void __launch_bounds__(64 * kW64Waves) k_normals_knn64_wave(GridView g, const double* __restrict__ xyz,
+constexpr int kW64Cube = 2;
+#ifdef O3DX_W64_WPE
+#define O3DX_W64_ATTR __attribute__((amdgpu_waves_per_eu(O3DX_W64_WPE)))
+#else
+#define O3DX_W64_ATTR
+#endif
+__global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_wave(GridView g, const double* __restrict__ xyz,
                                                                         int kneed, const float* __restrict__ prior,
                                                                         float* __restrict__ out,
                                                                         const int32_t* __restrict__ list,
@@ -3418,8 +3425,13 @@ __global__ void __launch_bounds__(64 * kW64Waves) k_normals_knn64_wave(GridView 
       bi[j] = 0x7fffffff;
     }
     int seen = 0;
-    for (int r = 0; r <= rmax; ++r) {
+    // the first pass covers the whole cube of radius r0 (a hand-off's k-th
+    // neighbour lies beyond the tile's reach: shells 0 .. 2 one by one would
+    // cost three dependent rounds of loads), then shell by shell
+    const int r0 = min(kW64Cube, rmax);
+    for (int r = r0; r <= rmax; ++r) {
       const int side = 2 * r + 1, nrows = side * side;
+      const bool cube = r == r0;
       for (int r0 = 0; r0 < nrows; r0 += 64) {
         const int row = r0 + lane;
         int a0 = 0, l0 = 0, a1 = 0, l1 = 0;
@@ -3428,7 +3440,7 @@ __global__ void __launch_bounds__(64 * kW64Waves) k_normals_knn64_wave(GridView 
           const int z = cz + dz, y = cy + dy;
           if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
             const int rb = g.nx * (y + g.ny * z);
-            if (dz == -r || dz == r || dy == -r || dy == r) {  // a face row: the cells cx - r .. cx + r
+            if (cube || dz == -r || dz == r || dy == -r || dy == r) {  // a full row: the cells cx - r .. cx + r
               const int x0 = max(cx - r, 0), x1 = min(cx + r, g.nx - 1);
               if (x0 <= x1) {
                 a0 = g.start[rb + x0];
