@@ -3390,14 +3390,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))
 // kept could hide a nearer one: such a query goes on to the lane form
 // (fb list).  One lane form query walks its shells' candidates alone, one
 // load batch at a time; here 64 lanes share them.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
 constexpr int kW64Keep = 8;
 constexpr int kW64Waves = 4;
-constexpr int kW64Cube = 2;
-#ifdef O3DX_W64_WPE
-#define O3DX_W64_ATTR __attribute__((amdgpu_waves_per_eu(O3DX_W64_WPE)))
-#else
-#define O3DX_W64_ATTR
+constexpr int kW64Cube = 0;  // (2: the radius-2 cube first — measured slower, 0.66 -> 0.74 ms)
+// 4 waves per SIMD (128 VGPRs, a few spills): 0.74 -> 0.46 ms over 3 waves
+// for the scan's 38K hand-offs (profiles/r06_f64_wave_ab.txt)
+#ifndef O3DX_W64_WPE
+#define O3DX_W64_WPE 4
 #endif
+#define O3DX_W64_ATTR __attribute__((amdgpu_waves_per_eu(O3DX_W64_WPE)))
 __global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_wave(GridView g, const double* __restrict__ xyz,
                                                                         int kneed, const float* __restrict__ prior,
                                                                         float* __restrict__ out,
@@ -3406,6 +3412,8 @@ __global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_
                                                                         int32_t* __restrict__ fb,
                                                                         int32_t* __restrict__ fb_len, int keep_lim) {
   __shared__ int32_t s_a0[kW64Waves][64], s_l0[kW64Waves][64], s_a1[kW64Waves][64], s_rp[kW64Waves][65];
+  __shared__ double s_md[kW64Waves][32];  // the members (want = min(kneed, seen) <= 32)
+  __shared__ int32_t s_mi[kW64Waves][32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int32_t *ta0 = s_a0[wv], *tl0 = s_l0[wv], *ta1 = s_a1[wv], *trp = s_rp[wv];
   const int64_t m = *list_len;
@@ -3425,9 +3433,8 @@ __global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_
       bi[j] = 0x7fffffff;
     }
     int seen = 0;
-    // the first pass covers the whole cube of radius r0 (a hand-off's k-th
-    // neighbour lies beyond the tile's reach: shells 0 .. 2 one by one would
-    // cost three dependent rounds of loads), then shell by shell
+    // the first pass covers the whole cube of radius r0 (kW64Cube), then
+    // shell by shell
     const int r0 = min(kW64Cube, rmax);
     for (int r = r0; r <= rmax; ++r) {
       const int side = 2 * r + 1, nrows = side * side;
@@ -3505,41 +3512,101 @@ __global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_
     }
     const int total = wave_sum(seen);
     const int want = min(kneed, total);
-    const int kept = min(seen, keep_lim);  // keep_lim < kW64Keep: tests of the hand-on
+    // keep_lim < kW64Keep (tests of the hand-on): the lists as if shorter
+#pragma unroll
+    for (int e = 0; e < kW64Keep; ++e)
+      if (e >= keep_lim) {
+        bd[e] = INFINITY;
+        bi[e] = 0x7fffffff;
+      }
+    const int kept = min(seen, keep_lim);
+    // the want-th smallest d^2 over the lanes' lists: a bitwise search on the
+    // (order-preserving) bits of the non-negative doubles, counted by ballots
+    uint64_t kb = 0;
+    for (int b = 62; b >= 0; --b) {
+      const uint64_t t = kb | (1ull << b);
+      int c = 0;
+#pragma unroll
+      for (int e = 0; e < kW64Keep; ++e) c += __popcll(__ballot((uint64_t)__double_as_longlong(bd[e]) < t));
+      if (c < want) kb = t;
+    }
+    const double kd = __longlong_as_double((long long)kb);
+    // members: d^2 < kd, then the smallest indices among d^2 == kd
+    int lt = 0, eq = 0;
+#pragma unroll
+    for (int e = 0; e < kW64Keep; ++e) {
+      lt += __popcll(__ballot(bd[e] < kd));
+      eq += __popcll(__ballot(bd[e] == kd));
+    }
+    int ki = 0x7fffffff;  // the largest member index at d^2 == kd
+    if (want > 0 && eq > want - lt) {  // an exact tie at the want-th distance
+      int r = 0;
+      for (int b = 30; b >= 0; --b) {
+        const int t = r | (1 << b);
+        int c = 0;
+#pragma unroll
+        for (int e = 0; e < kW64Keep; ++e) c += __popcll(__ballot(bd[e] == kd && bi[e] < t));
+        if (c < want - lt) r = t;
+      }
+      ki = r;
+    }
+    // a lane that saw more than it kept hides candidates after its last kept
+    // one: a nearer one than the want-th could hide there when that last kept
+    // one is itself a member (keyed at or below (kd, ki))
+    bool bad;
+    {
+      double ld = INFINITY;
+      int li = 0x7fffffff;
+#pragma unroll
+      for (int e = 0; e < kW64Keep; ++e)
+        if (e == kept - 1) {  // (no dynamic register index)
+          ld = bd[e];
+          li = bi[e];
+        }
+      bad = want > 0 && __any(seen > kept && kept > 0 && !lex_less(kd, ki, ld, li));
+    }
     MomAccSeq acc;
     acc.zero();
-    int h = 0;
-    bool bad = false;
-    double kd = 0.0;
-    for (int j = 0; j < want; ++j) {
-      if (__any(h == kept && seen > kept)) {  // a dry lane that saw more than it kept
-        bad = true;
-        break;
-      }
-      double md = bd[0];
-      int mi = bi[0];
+    if (!bad && want > 0) {
+      // compact the members into the wave's LDS rows, then rank them by
+      // (d^2, index): member l lands in slot rank(l)
+      double* md = s_md[wv];
+      int32_t* mi = s_mi[wv];
+      int base = 0;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double od = __shfl_xor(md, o, 64);
-        const int oo = __shfl_xor(mi, o, 64);
-        if (lex_less(od, oo, md, mi)) {
-          md = od;
-          mi = oo;
+      for (int e = 0; e < kW64Keep; ++e) {
+        const bool mem = bd[e] < kd || (bd[e] == kd && bi[e] <= ki);
+        const uint64_t mask = __ballot(mem);
+        if (mem) {
+          const int at = base + lanes_below(mask);
+          md[at] = bd[e];
+          mi[at] = bi[e];
         }
+        base += __popcll(mask);
       }
-      if (bd[0] == md && bi[0] == mi) {  // the owner pops its head
-#pragma unroll
-        for (int u = 0; u + 1 < kW64Keep; ++u) {
-          bd[u] = bd[u + 1];
-          bi[u] = bi[u + 1];
-        }
-        bd[kW64Keep - 1] = INFINITY;
-        bi[kW64Keep - 1] = 0x7fffffff;
-        ++h;
+      wave_sync();
+      double myd = 0.0;
+      int myi = 0, rank = 0;
+      if (lane < want) {
+        myd = md[lane];
+        myi = mi[lane];
+        for (int u = 0; u < want; ++u) rank += lex_less(md[u], mi[u], myd, myi) ? 1 : 0;
       }
-      if (lane == 0 && g.nbr) g.nbr[(int64_t)oi * kneed + j] = mi;
-      acc.add(xyz[3 * (int64_t)mi], xyz[3 * (int64_t)mi + 1], xyz[3 * (int64_t)mi + 2]);
-      kd = md;
+      wave_sync();
+      if (lane < want) mi[rank] = myi;
+      wave_sync();
+      // member l's coordinates, all loads at once; then Open3D's sequence
+      double px = 0.0, py = 0.0, pz = 0.0;
+      int id = 0;
+      if (lane < want) {
+        id = mi[lane];
+        px = xyz[3 * (int64_t)id];
+        py = xyz[3 * (int64_t)id + 1];
+        pz = xyz[3 * (int64_t)id + 2];
+        if (g.nbr) g.nbr[(int64_t)oi * kneed + lane] = id;
+      }
+      for (int u = 0; u < want; ++u) acc.add(readlane_f64(px, u), readlane_f64(py, u), readlane_f64(pz, u));
+      wave_sync();
     }
     if (lane == 0) {
       if (bad) {

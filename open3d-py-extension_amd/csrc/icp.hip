@@ -511,7 +511,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOD
         // so the match stays the unique nearest — the same (d^2, index) minimum
         // a full search returns — while budget > 2 delta (+ a rounding guard).
         const float b = budget[j];
-        const int mp = mpos[j];
+        // b > 0 only after a full search matched (budget 0 otherwise), so a
+        // float32 target's cached match needs no mpos read (4 B per point of
+        // a skip step's 48); a float64 target gathers by position
+        const int mp = F64 ? mpos[j] : 0;
         if (mp >= 0 && b > 0.0f) {
           // the match's point and normal: float32 targets read them from the
           // match cache the last full search wrote (mca / mcb, in source
