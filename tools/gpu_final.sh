@@ -41,6 +41,7 @@ cat gpurun_out/${R}_bench.json
 rm -rf gpurun_out/prof_${R}_c2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R}_c2 -o run --output-format csv -- \
   python bench.py --no-cpu --no-secondary > gpurun_out/${R}_prof_c2.log 2>&1 || exit $?
+[ -n "$NO_FULL_PROF" ] && { echo FINAL_DONE; exit 0; }
 rm -rf gpurun_out/prof_${R}
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${R} -o run --output-format csv -- \
   python bench.py --no-cpu > gpurun_out/${R}_prof_bench.log 2>&1 || exit $?
