@@ -377,9 +377,10 @@ def _registration_icp_sharded_device(src, target, init, max_iteration, relative_
     from . import ops
 
     world, _ = _world(group)
-    am = allreduce_max(ops.absmax(src) if src.shape[0] else np.zeros(3), group)
-    n_total = _allreduce_int(src.shape[0], group) if n_source_total is None else int(n_source_total)
     s = ops.spatial_sort(src) if src.shape[0] else src
+    # the global bounds from each rank's sort (its own bounds pass): no extra pass
+    am = allreduce_max(np.asarray(s.absmax, np.float64) if src.shape[0] else np.zeros(3), group)
+    n_total = _allreduce_int(src.shape[0], group) if n_source_total is None else int(n_source_total)
     T0 = np.eye(4) if init is None else np.array(init, np.float64).reshape(4, 4)
     windowed = isinstance(target, WindowedTarget)
     if windowed:
