@@ -3364,13 +3364,8 @@ __global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_
         }
       bad = want > 0 && __any(seen > kept && kept > 0 && !lex_less(kd, ki, ld, li));
     }
-    // float64 clouds: Open3D's sequential float64 sums in member order; float32
-    // clouds: the tiles' exact anchored sums (MomAccA, order-free: a query's
-    // normal is the same bits whichever kernel settles it, on any rank split)
-    std::conditional_t<F64, MomAccSeq, MomAccA> acc;
+    MomAccSeq acc;
     acc.zero();
-    if constexpr (!F64)
-      if (want > 0) acc.init(make_float4((float)q.x, (float)q.y, (float)q.z, 0.f), (float)kd, kneed);
     if (!bad && want > 0) {
       // compact the members into the wave's LDS rows, then rank them by
       // (d^2, index): member l lands in slot rank(l)
