@@ -3150,274 +3150,6 @@ static int nested_tiles(GridBuild& G, int64_t n, int kneed, double occ, const fl
   return 0;
 }
 
-// The float64 tiles' hand-offs (KNN, kneed <= 32), a wave per query instead
-// of a lane: each Chebyshev shell's rows (a face row = one point range, an
-// inner row = its two end cells) become one flat candidate range spread over
-// the 64 lanes, every lane keeping its own kW64Keep nearest in exact
-// (d^2, index) order; the shell loop stops as knn_search_dev64's does (the
-// k-th inside the shell's reach, counted conservatively over the lanes'
-// lists).  The k nearest are then drawn from the lanes' heads in order — the
-// same members in the same order as the lane form, accumulated in the same
-// sequence (MomAccSeq).  A lane whose list runs dry while it saw more than it
-// kept could hide a nearer one: such a query goes on to the lane form
-// (fb list).  One lane form query walks its shells' candidates alone, one
-// load batch at a time; here 64 lanes share them.
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
-}
-constexpr int kW64Keep = 8;
-constexpr int kW64Waves = 4;
-constexpr int kW64Cube = 0;  // (2: the radius-2 cube first — measured slower, 0.66 -> 0.74 ms)
-// 4 waves per SIMD (128 VGPRs, a few spills): 0.74 -> 0.46 ms over 3 waves
-// for the scan's 38K hand-offs (profiles/r06_f64_wave_ab.txt)
-#ifndef O3DX_W64_WPE
-#define O3DX_W64_WPE 4
-#endif
-#define O3DX_W64_ATTR __attribute__((amdgpu_waves_per_eu(O3DX_W64_WPE)))
-// F64 = false: the same form on a float32 sorted grid (the tiles' hand-offs
-// of o3dx_estimate_normals): d^2 in float64 from the float32 coordinates
-// (nanoflann's key), the moments from the float32 cloud widened to double.
-template <class T>
-__device__ __forceinline__ void w64_point(const GridView& g, int64_t p, double& x, double& y, double& z, int& id) {
-  if constexpr (sizeof(T) == sizeof(double)) {
-    const double4 v = g.pts64[p];
-    x = v.x;
-    y = v.y;
-    z = v.z;
-    id = (int)v.w;
-  } else {
-    const float4 v = g.pts[p];
-    x = v.x;
-    y = v.y;
-    z = v.z;
-    id = __float_as_int(v.w);
-  }
-}
-template <class T = double>
-__global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_wave(GridView g, const T* __restrict__ xyz,
-                                                                        int kneed, const float* __restrict__ prior,
-                                                                        float* __restrict__ out,
-                                                                        const int32_t* __restrict__ list,
-                                                                        const int32_t* __restrict__ list_len,
-                                                                        int32_t* __restrict__ fb,
-                                                                        int32_t* __restrict__ fb_len, int keep_lim) {
-  __shared__ int32_t s_a0[kW64Waves][64], s_l0[kW64Waves][64], s_a1[kW64Waves][64], s_rp[kW64Waves][65];
-  __shared__ double s_md[kW64Waves][32];  // the members (want = min(kneed, seen) <= 32)
-  __shared__ int32_t s_mi[kW64Waves][32];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int32_t *ta0 = s_a0[wv], *tl0 = s_l0[wv], *ta1 = s_a1[wv], *trp = s_rp[wv];
-  const int64_t m = *list_len;
-  for (int64_t t = (int64_t)blockIdx.x * kW64Waves + wv; t < m; t += (int64_t)gridDim.x * kW64Waves) {
-    constexpr bool F64 = sizeof(T) == sizeof(double);
-    const int64_t s = list[t];
-    double4 q;
-    int oi;
-    w64_point<T>(g, s, q.x, q.y, q.z, oi);
-    // the grid's frame: a float64 grid's float32 frame sits at its origin
-    const double gqx = F64 ? q.x - g.o64x : q.x, gqy = F64 ? q.y - g.o64y : q.y, gqz = F64 ? q.z - g.o64z : q.z;
-    int cx, cy, cz;
-    grid_cell(g, (float)gqx, (float)gqy, (float)gqz, cx, cy, cz);
-    const int rmax = shell_rmax(g, cx, cy, cz);
-    double bd[kW64Keep];
-    int bi[kW64Keep];
-#pragma unroll
-    for (int j = 0; j < kW64Keep; ++j) {
-      bd[j] = INFINITY;
-      bi[j] = 0x7fffffff;
-    }
-    int seen = 0;
-    // the first pass covers the whole cube of radius r0 (kW64Cube), then
-    // shell by shell
-    const int r0 = min(kW64Cube, rmax);
-    for (int r = r0; r <= rmax; ++r) {
-      const int side = 2 * r + 1, nrows = side * side;
-      const bool cube = r == r0;
-      for (int r0 = 0; r0 < nrows; r0 += 64) {
-        const int row = r0 + lane;
-        int a0 = 0, l0 = 0, a1 = 0, l1 = 0;
-        if (row < nrows) {
-          const int dz = row / side - r, dy = row % side - r;
-          const int z = cz + dz, y = cy + dy;
-          if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
-            const int rb = g.nx * (y + g.ny * z);
-            if (cube || dz == -r || dz == r || dy == -r || dy == r) {  // a full row: the cells cx - r .. cx + r
-              const int x0 = max(cx - r, 0), x1 = min(cx + r, g.nx - 1);
-              if (x0 <= x1) {
-                a0 = g.start[rb + x0];
-                l0 = g.start[rb + x1 + 1] - a0;
-              }
-            } else {  // an inner row (r >= 1): its two end cells
-              if (cx - r >= 0) {
-                a0 = g.start[rb + cx - r];
-                l0 = g.start[rb + cx - r + 1] - a0;
-              }
-              if (cx + r < g.nx) {
-                a1 = g.start[rb + cx + r];
-                l1 = g.start[rb + cx + r + 1] - a1;
-              }
-            }
-          }
-        }
-        const int inc = wave_incl_scan(l0 + l1);
-        const int tot = __shfl(inc, 63, 64);
-        ta0[lane] = a0;
-        tl0[lane] = l0;
-        ta1[lane] = a1;
-        trp[lane + 1] = inc;
-        if (lane == 0) trp[0] = 0;
-        wave_sync();
-        int rw = 0;
-        for (int b = 0; b < tot; b += 64) {
-          const int f = b + lane;
-          if (f < tot) {
-            while (trp[rw + 1] <= f) ++rw;
-            const int o = f - trp[rw];
-            const int p = o < tl0[rw] ? ta0[rw] + o : ta1[rw] + (o - tl0[rw]);
-            double vx, vy, vz;
-            int id;
-            w64_point<T>(g, p, vx, vy, vz, id);
-            const double dx = q.x - vx, dy = q.y - vy, dz = q.z - vz;
-            double d = dx * dx;  // dist2_d4 / dist2_f64's order
-            d = d + dy * dy;
-            d = d + dz * dz;
-            seen += d < INFINITY ? 1 : 0;  // (an empty slot of a dense grid is not a candidate)
-            if (lex_less(d, id, bd[kW64Keep - 1], bi[kW64Keep - 1])) {
-#pragma unroll
-              for (int j = kW64Keep - 1; j >= 0; --j) {
-                const bool lt = lex_less(d, id, bd[j], bi[j]);
-                const bool ltp = j > 0 ? lex_less(d, id, bd[j > 0 ? j - 1 : 0], bi[j > 0 ? j - 1 : 0]) : false;
-                if (ltp) {
-                  bd[j] = bd[j - 1];
-                  bi[j] = bi[j - 1];
-                } else if (lt) {
-                  bd[j] = d;
-                  bi[j] = id;
-                }
-              }
-            }
-          }
-        }
-        wave_sync();  // the row table is rewritten by the next 64 rows
-      }
-      const double B = cube_reach(g, gqx, gqy, gqz, cx, cy, cz, r) - g.slack;
-      if (B > 0.0) {
-        int c = 0;
-#pragma unroll
-        for (int j = 0; j < kW64Keep; ++j) c += bd[j] < B * B ? 1 : 0;
-        if (wave_sum(c) >= kneed) break;  // the k-th lies inside the reach
-      }
-    }
-    const int total = wave_sum(seen);
-    const int want = min(kneed, total);
-    // keep_lim < kW64Keep (tests of the hand-on): the lists as if shorter
-#pragma unroll
-    for (int e = 0; e < kW64Keep; ++e)
-      if (e >= keep_lim) {
-        bd[e] = INFINITY;
-        bi[e] = 0x7fffffff;
-      }
-    const int kept = min(seen, keep_lim);
-    // the want-th smallest d^2 over the lanes' lists: a bitwise search on the
-    // (order-preserving) bits of the non-negative doubles, counted by ballots
-    uint64_t kb = 0;
-    for (int b = 62; b >= 0; --b) {
-      const uint64_t t = kb | (1ull << b);
-      int c = 0;
-#pragma unroll
-      for (int e = 0; e < kW64Keep; ++e) c += __popcll(__ballot((uint64_t)__double_as_longlong(bd[e]) < t));
-      if (c < want) kb = t;
-    }
-    const double kd = __longlong_as_double((long long)kb);
-    // members: d^2 < kd, then the smallest indices among d^2 == kd
-    int lt = 0, eq = 0;
-#pragma unroll
-    for (int e = 0; e < kW64Keep; ++e) {
-      lt += __popcll(__ballot(bd[e] < kd));
-      eq += __popcll(__ballot(bd[e] == kd));
-    }
-    int ki = 0x7fffffff;  // the largest member index at d^2 == kd
-    if (want > 0 && eq > want - lt) {  // an exact tie at the want-th distance
-      int r = 0;
-      for (int b = 30; b >= 0; --b) {
-        const int t = r | (1 << b);
-        int c = 0;
-#pragma unroll
-        for (int e = 0; e < kW64Keep; ++e) c += __popcll(__ballot(bd[e] == kd && bi[e] < t));
-        if (c < want - lt) r = t;
-      }
-      ki = r;
-    }
-    // a lane that saw more than it kept hides candidates after its last kept
-    // one: a nearer one than the want-th could hide there when that last kept
-    // one is itself a member (keyed at or below (kd, ki))
-    bool bad;
-    {
-      double ld = INFINITY;
-      int li = 0x7fffffff;
-#pragma unroll
-      for (int e = 0; e < kW64Keep; ++e)
-        if (e == kept - 1) {  // (no dynamic register index)
-          ld = bd[e];
-          li = bi[e];
-        }
-      bad = want > 0 && __any(seen > kept && kept > 0 && !lex_less(kd, ki, ld, li));
-    }
-    MomAccSeq acc;
-    acc.zero();
-    if (!bad && want > 0) {
-      // compact the members into the wave's LDS rows, then rank them by
-      // (d^2, index): member l lands in slot rank(l)
-      double* md = s_md[wv];
-      int32_t* mi = s_mi[wv];
-      int base = 0;
-#pragma unroll
-      for (int e = 0; e < kW64Keep; ++e) {
-        const bool mem = bd[e] < kd || (bd[e] == kd && bi[e] <= ki);
-        const uint64_t mask = __ballot(mem);
-        if (mem) {
-          const int at = base + lanes_below(mask);
-          md[at] = bd[e];
-          mi[at] = bi[e];
-        }
-        base += __popcll(mask);
-      }
-      wave_sync();
-      double myd = 0.0;
-      int myi = 0, rank = 0;
-      if (lane < want) {
-        myd = md[lane];
-        myi = mi[lane];
-        for (int u = 0; u < want; ++u) rank += lex_less(md[u], mi[u], myd, myi) ? 1 : 0;
-      }
-      wave_sync();
-      if (lane < want) mi[rank] = myi;
-      wave_sync();
-      // member l's coordinates, all loads at once; then Open3D's sequence
-      double px = 0.0, py = 0.0, pz = 0.0;
-      int id = 0;
-      if (lane < want) {
-        id = mi[lane];
-        px = xyz[3 * (int64_t)id];
-        py = xyz[3 * (int64_t)id + 1];
-        pz = xyz[3 * (int64_t)id + 2];
-        if (g.nbr) g.nbr[(int64_t)oi * kneed + lane] = id;
-      }
-      for (int u = 0; u < want; ++u) acc.add(readlane_f64(px, u), readlane_f64(py, u), readlane_f64(pz, u));
-      wave_sync();
-    }
-    if (lane == 0) {
-      if (bad) {
-        fb[atomicAdd(fb_len, 1)] = (int32_t)s;
-      } else {
-        if (g.kd2 && want > 0) g.kd2[oi] = (float)(kd * (1.0 + 1e-6));
-        finish_normal(want, acc, prior, oi, out);
-      }
-    }
-  }
-}
-
 static int64_t defer_cap(int64_t n) { return n / 4 + 64; }
 
 static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, int knn, double radius,
@@ -3474,16 +3206,7 @@ static int normals_on_grid(GridBuild& G, const float* xyz, int64_t n, int mode, 
         df.mom = dmom;
         df.row = drow;
       }
-      if (wl && kneed <= 32 && !getenv("O3DX_WAVE32_OLD")) {
-        // the tiles' hand-offs a wave each in the exact-key form of the
-        // float64 path (k_normals_knn64_wave<float>: ballot-counted k-th
-        // distance, members ranked in LDS, one load round, Open3D's
-        // sequential moments); what it cannot settle to the lane form below
-        const unsigned wb = (unsigned)std::min<int64_t>((n + kW64Waves - 1) / kW64Waves, 2048);
-        hipLaunchKernelGGL(k_normals_knn64_wave<float>, dim3(wb), dim3(64 * kW64Waves), 0, s, G.view, xyz, kneed,
-                           prior, out, wl, wlen, list2, lens + 1, kW64Keep);
-        df.cap = 0;
-      } else if (kneed <= 32)
+      if (kneed <= 32)
         hipLaunchKernelGGL(k_normals_knn_wave<32>, dim3(gw), dim3(64 * kWavesPerBlock), 0, s, G.view, kneed, prior,
                            out, wl, wlen, list2, lens + 1, s0, df);
       else
@@ -3653,6 +3376,247 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))
   // grid-stride loop here costs the query 36 more VGPRs: 1 wave per SIMD)
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < (int64_t)*list_len) knn64_normal_query<K>(g, xyz, kneed, mode, radius, prior, out, list[t]);
+}
+
+// The float64 tiles' hand-offs (KNN, kneed <= 32), a wave per query instead
+// of a lane: each Chebyshev shell's rows (a face row = one point range, an
+// inner row = its two end cells) become one flat candidate range spread over
+// the 64 lanes, every lane keeping its own kW64Keep nearest in exact
+// (d^2, index) order; the shell loop stops as knn_search_dev64's does (the
+// k-th inside the shell's reach, counted conservatively over the lanes'
+// lists).  The k nearest are then drawn from the lanes' heads in order — the
+// same members in the same order as the lane form, accumulated in the same
+// sequence (MomAccSeq).  A lane whose list runs dry while it saw more than it
+// kept could hide a nearer one: such a query goes on to the lane form
+// (fb list).  One lane form query walks its shells' candidates alone, one
+// load batch at a time; here 64 lanes share them.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+constexpr int kW64Keep = 8;
+constexpr int kW64Waves = 4;
+constexpr int kW64Cube = 0;  // (2: the radius-2 cube first — measured slower, 0.66 -> 0.74 ms)
+// 4 waves per SIMD (128 VGPRs, a few spills): 0.74 -> 0.46 ms over 3 waves
+// for the scan's 38K hand-offs (profiles/r06_f64_wave_ab.txt)
+#ifndef O3DX_W64_WPE
+#define O3DX_W64_WPE 4
+#endif
+#define O3DX_W64_ATTR __attribute__((amdgpu_waves_per_eu(O3DX_W64_WPE)))
+__global__ void __launch_bounds__(64 * kW64Waves) O3DX_W64_ATTR k_normals_knn64_wave(GridView g, const double* __restrict__ xyz,
+                                                                        int kneed, const float* __restrict__ prior,
+                                                                        float* __restrict__ out,
+                                                                        const int32_t* __restrict__ list,
+                                                                        const int32_t* __restrict__ list_len,
+                                                                        int32_t* __restrict__ fb,
+                                                                        int32_t* __restrict__ fb_len, int keep_lim) {
+  __shared__ int32_t s_a0[kW64Waves][64], s_l0[kW64Waves][64], s_a1[kW64Waves][64], s_rp[kW64Waves][65];
+  __shared__ double s_md[kW64Waves][32];  // the members (want = min(kneed, seen) <= 32)
+  __shared__ int32_t s_mi[kW64Waves][32];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t *ta0 = s_a0[wv], *tl0 = s_l0[wv], *ta1 = s_a1[wv], *trp = s_rp[wv];
+  const int64_t m = *list_len;
+  for (int64_t t = (int64_t)blockIdx.x * kW64Waves + wv; t < m; t += (int64_t)gridDim.x * kW64Waves) {
+    const int64_t s = list[t];
+    const double4 q = g.pts64[s];
+    const int oi = (int)q.w;
+    const double gqx = q.x - g.o64x, gqy = q.y - g.o64y, gqz = q.z - g.o64z;
+    int cx, cy, cz;
+    grid_cell(g, (float)gqx, (float)gqy, (float)gqz, cx, cy, cz);
+    const int rmax = shell_rmax(g, cx, cy, cz);
+    double bd[kW64Keep];
+    int bi[kW64Keep];
+#pragma unroll
+    for (int j = 0; j < kW64Keep; ++j) {
+      bd[j] = INFINITY;
+      bi[j] = 0x7fffffff;
+    }
+    int seen = 0;
+    // the first pass covers the whole cube of radius r0 (kW64Cube), then
+    // shell by shell
+    const int r0 = min(kW64Cube, rmax);
+    for (int r = r0; r <= rmax; ++r) {
+      const int side = 2 * r + 1, nrows = side * side;
+      const bool cube = r == r0;
+      for (int r0 = 0; r0 < nrows; r0 += 64) {
+        const int row = r0 + lane;
+        int a0 = 0, l0 = 0, a1 = 0, l1 = 0;
+        if (row < nrows) {
+          const int dz = row / side - r, dy = row % side - r;
+          const int z = cz + dz, y = cy + dy;
+          if (z >= 0 && z < g.nz && y >= 0 && y < g.ny) {
+            const int rb = g.nx * (y + g.ny * z);
+            if (cube || dz == -r || dz == r || dy == -r || dy == r) {  // a full row: the cells cx - r .. cx + r
+              const int x0 = max(cx - r, 0), x1 = min(cx + r, g.nx - 1);
+              if (x0 <= x1) {
+                a0 = g.start[rb + x0];
+                l0 = g.start[rb + x1 + 1] - a0;
+              }
+            } else {  // an inner row (r >= 1): its two end cells
+              if (cx - r >= 0) {
+                a0 = g.start[rb + cx - r];
+                l0 = g.start[rb + cx - r + 1] - a0;
+              }
+              if (cx + r < g.nx) {
+                a1 = g.start[rb + cx + r];
+                l1 = g.start[rb + cx + r + 1] - a1;
+              }
+            }
+          }
+        }
+        const int inc = wave_incl_scan(l0 + l1);
+        const int tot = __shfl(inc, 63, 64);
+        ta0[lane] = a0;
+        tl0[lane] = l0;
+        ta1[lane] = a1;
+        trp[lane + 1] = inc;
+        if (lane == 0) trp[0] = 0;
+        wave_sync();
+        int rw = 0;
+        for (int b = 0; b < tot; b += 64) {
+          const int f = b + lane;
+          if (f < tot) {
+            while (trp[rw + 1] <= f) ++rw;
+            const int o = f - trp[rw];
+            const int p = o < tl0[rw] ? ta0[rw] + o : ta1[rw] + (o - tl0[rw]);
+            const double4 v = g.pts64[p];
+            const double d = dist2_d4(q.x, q.y, q.z, v);
+            const int id = (int)v.w;
+            ++seen;
+            if (lex_less(d, id, bd[kW64Keep - 1], bi[kW64Keep - 1])) {
+#pragma unroll
+              for (int j = kW64Keep - 1; j >= 0; --j) {
+                const bool lt = lex_less(d, id, bd[j], bi[j]);
+                const bool ltp = j > 0 ? lex_less(d, id, bd[j > 0 ? j - 1 : 0], bi[j > 0 ? j - 1 : 0]) : false;
+                if (ltp) {
+                  bd[j] = bd[j - 1];
+                  bi[j] = bi[j - 1];
+                } else if (lt) {
+                  bd[j] = d;
+                  bi[j] = id;
+                }
+              }
+            }
+          }
+        }
+        wave_sync();  // the row table is rewritten by the next 64 rows
+      }
+      const double B = cube_reach(g, gqx, gqy, gqz, cx, cy, cz, r) - g.slack;
+      if (B > 0.0) {
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < kW64Keep; ++j) c += bd[j] < B * B ? 1 : 0;
+        if (wave_sum(c) >= kneed) break;  // the k-th lies inside the reach
+      }
+    }
+    const int total = wave_sum(seen);
+    const int want = min(kneed, total);
+    // keep_lim < kW64Keep (tests of the hand-on): the lists as if shorter
+#pragma unroll
+    for (int e = 0; e < kW64Keep; ++e)
+      if (e >= keep_lim) {
+        bd[e] = INFINITY;
+        bi[e] = 0x7fffffff;
+      }
+    const int kept = min(seen, keep_lim);
+    // the want-th smallest d^2 over the lanes' lists: a bitwise search on the
+    // (order-preserving) bits of the non-negative doubles, counted by ballots
+    uint64_t kb = 0;
+    for (int b = 62; b >= 0; --b) {
+      const uint64_t t = kb | (1ull << b);
+      int c = 0;
+#pragma unroll
+      for (int e = 0; e < kW64Keep; ++e) c += __popcll(__ballot((uint64_t)__double_as_longlong(bd[e]) < t));
+      if (c < want) kb = t;
+    }
+    const double kd = __longlong_as_double((long long)kb);
+    // members: d^2 < kd, then the smallest indices among d^2 == kd
+    int lt = 0, eq = 0;
+#pragma unroll
+    for (int e = 0; e < kW64Keep; ++e) {
+      lt += __popcll(__ballot(bd[e] < kd));
+      eq += __popcll(__ballot(bd[e] == kd));
+    }
+    int ki = 0x7fffffff;  // the largest member index at d^2 == kd
+    if (want > 0 && eq > want - lt) {  // an exact tie at the want-th distance
+      int r = 0;
+      for (int b = 30; b >= 0; --b) {
+        const int t = r | (1 << b);
+        int c = 0;
+#pragma unroll
+        for (int e = 0; e < kW64Keep; ++e) c += __popcll(__ballot(bd[e] == kd && bi[e] < t));
+        if (c < want - lt) r = t;
+      }
+      ki = r;
+    }
+    // a lane that saw more than it kept hides candidates after its last kept
+    // one: a nearer one than the want-th could hide there when that last kept
+    // one is itself a member (keyed at or below (kd, ki))
+    bool bad;
+    {
+      double ld = INFINITY;
+      int li = 0x7fffffff;
+#pragma unroll
+      for (int e = 0; e < kW64Keep; ++e)
+        if (e == kept - 1) {  // (no dynamic register index)
+          ld = bd[e];
+          li = bi[e];
+        }
+      bad = want > 0 && __any(seen > kept && kept > 0 && !lex_less(kd, ki, ld, li));
+    }
+    MomAccSeq acc;
+    acc.zero();
+    if (!bad && want > 0) {
+      // compact the members into the wave's LDS rows, then rank them by
+      // (d^2, index): member l lands in slot rank(l)
+      double* md = s_md[wv];
+      int32_t* mi = s_mi[wv];
+      int base = 0;
+#pragma unroll
+      for (int e = 0; e < kW64Keep; ++e) {
+        const bool mem = bd[e] < kd || (bd[e] == kd && bi[e] <= ki);
+        const uint64_t mask = __ballot(mem);
+        if (mem) {
+          const int at = base + lanes_below(mask);
+          md[at] = bd[e];
+          mi[at] = bi[e];
+        }
+        base += __popcll(mask);
+      }
+      wave_sync();
+      double myd = 0.0;
+      int myi = 0, rank = 0;
+      if (lane < want) {
+        myd = md[lane];
+        myi = mi[lane];
+        for (int u = 0; u < want; ++u) rank += lex_less(md[u], mi[u], myd, myi) ? 1 : 0;
+      }
+      wave_sync();
+      if (lane < want) mi[rank] = myi;
+      wave_sync();
+      // member l's coordinates, all loads at once; then Open3D's sequence
+      double px = 0.0, py = 0.0, pz = 0.0;
+      int id = 0;
+      if (lane < want) {
+        id = mi[lane];
+        px = xyz[3 * (int64_t)id];
+        py = xyz[3 * (int64_t)id + 1];
+        pz = xyz[3 * (int64_t)id + 2];
+        if (g.nbr) g.nbr[(int64_t)oi * kneed + lane] = id;
+      }
+      for (int u = 0; u < want; ++u) acc.add(readlane_f64(px, u), readlane_f64(py, u), readlane_f64(pz, u));
+      wave_sync();
+    }
+    if (lane == 0) {
+      if (bad) {
+        fb[atomicAdd(fb_len, 1)] = (int32_t)s;
+      } else {
+        if (g.kd2 && want > 0) g.kd2[oi] = (float)(kd * (1.0 + 1e-6));
+        finish_normal(want, acc, prior, oi, out);
+      }
+    }
+  }
 }
 
 template <int K>
@@ -3932,7 +3896,7 @@ extern "C" int o3dx_estimate_normals_f64(const double* xyz, int64_t n, int mode,
       const unsigned wblocks = (unsigned)std::min<int64_t>((n + kW64Waves - 1) / kW64Waves, 2048);
       const char* kl = getenv("O3DX_F64_WAVE_KEEP");  // tests: a shorter list hands more queries on
       const int keep = kl ? std::max(1, std::min(kW64Keep, atoi(kl))) : kW64Keep;
-      hipLaunchKernelGGL(k_normals_knn64_wave<double>, dim3(wblocks), dim3(64 * kW64Waves), 0, s, G.view, xyz, kneed, prior,
+      hipLaunchKernelGGL(k_normals_knn64_wave, dim3(wblocks), dim3(64 * kW64Waves), 0, s, G.view, xyz, kneed, prior,
                          out, (const int32_t*)list, (const int32_t*)lens, list2, lens + 2, keep);
       kt_wave.stop();
       O3DX_DISPATCH_K(kneed, k_normals_knn64_list, dim3(grid), dim3(kBlock), 0, s, G.view, xyz, kneed, mode, radius,
