@@ -748,7 +748,8 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": None, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "scaling": "weak",  # the first point of the --gpus N weak curve (C2 per GPU)
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": "C2: uniform-random 10M pts float32, voxel_down_sample(vs=(4/N)^(1/3)) "
                                "+ estimate_normals(KNN30) on the representatives",
                    "n_points": N, "voxel_size": vs, "voxels": int(M), "knn": args.knn, "parallelism": "single"},
